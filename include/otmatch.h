@@ -1,0 +1,295 @@
+/*
+ * otmatch.h -- C ABI of libotmatch.so, the MI355X-native map matcher that
+ * replaces the /report path of Open Traffic Reporter.
+ *
+ * What it replaces (reference = burritojustice/reporter):
+ *   - the HTTP hop the Java batcher makes for every match request:
+ *       String response = HttpClient.POST(url, post_body);
+ *         src/main/java/org/opentraffic/reporter/Batch.java:63
+ *         src/main/java/org/opentraffic/reporter/HttpClient.java:18-45
+ *   - the Python service that answers it:
+ *       SegmentMatcherHandler.handle_request / report
+ *         py/reporter_service.py:218-240, :110-215
+ *   - the Valhalla/meili matcher that service calls:
+ *       valhalla.Configure(conf)          py/reporter_service.py:279
+ *       valhalla.SegmentMatcher()          py/reporter_service.py:52
+ *       SegmentMatcher.Match(json) -> json py/reporter_service.py:112
+ *
+ * Conventions: plain C types only; no exceptions cross this boundary; every
+ * buffer the library returns is released with otm_free().  Status codes of
+ * the request-level calls are the HTTP codes reporter_service.py would send
+ * (200 / 400 / 500) and the body is byte-identical to what it would write.
+ * Engine-level calls return 0 on success and a negative OTM_E* code on
+ * failure, with a message available from otm_last_error().
+ *
+ * Thread safety: an engine handle may be used from many threads at once.
+ */
+#ifndef OTMATCH_H
+#define OTMATCH_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OTM_OK 0
+#define OTM_EINVAL (-1)   /* bad argument / config                          */
+#define OTM_EIO (-2)      /* graph file unreadable / malformed              */
+#define OTM_EDEVICE (-3)  /* HIP runtime error (no device, OOM, fault)      */
+#define OTM_ECONFIG (-4)  /* env config rejected (reporter_service.py:55-62) */
+#define OTM_EAGAIN (-5)   /* async queue full                               */
+
+typedef struct otm_engine otm_engine;
+
+/* ------------------------------------------------------------------ engine */
+
+/* Create an engine: load the flattened graph named by the config file into
+ * the HBM of devices[0] and read the matcher parameters.
+ *   cfg_path: JSON file; {"otm":{"graph":"<.otmg path>"}, "meili":{"default":
+ *             {sigma_z, beta, max_route_distance_factor, breakage_distance,
+ *              interpolation_distance, search_radius, max_search_radius,
+ *              max_candidates}}}.  Unknown keys are ignored.
+ *   Env (read once, here): REPORT_LEVELS, TRANSITION_LEVELS, THRESHOLD_SEC
+ *   with reporter_service.py's parsing (make_thread_locals, :51-62),
+ *   including its quirk that THRESHOLD_SEC goes through strtobool: a value
+ *   such as "15" is rejected with OTM_ECONFIG ("invalid truth value '15'"),
+ *   where the reference's worker threads would die.
+ * Replaces valhalla.Configure (py/reporter_service.py:279) + per-thread
+ * SegmentMatcher() construction (:52).  ndev must be 1 in this release;
+ * multi-GPU runs one engine per process/GPU. */
+int otm_engine_create(const char* cfg_path, const int* devices, int ndev,
+                      otm_engine** out);
+void otm_engine_destroy(otm_engine* eng);
+
+/* Last error message for this thread (eng may be NULL). */
+const char* otm_last_error(const otm_engine* eng);
+
+/* Release any buffer returned by this library. */
+void otm_free(void* p);
+
+/* ---------------------------------------------------------- request level */
+
+/* The /report endpoint, in process.  req = the POST body the Java batcher
+ * builds (Batch.java:52-61).  Returns the HTTP status (200/400/500) and sets
+ * *resp to the exact body reporter_service.py would send
+ * (handle_request, py/reporter_service.py:218-240; do(), :259-264).
+ * Replaces HttpClient.POST(url, body) at Batch.java:63. */
+int otm_report(otm_engine* eng, const char* req, size_t len, char** resp,
+               size_t* resp_len);
+
+/* Many /report requests at once: one GPU batch.  codes[i], resps[i],
+ * resp_lens[i] as for otm_report.  Returns 0 or a negative engine error. */
+int otm_report_batch(otm_engine* eng, int n, const char* const* reqs,
+                     const size_t* lens, char** resps, size_t* resp_lens,
+                     int* codes);
+
+/* valhalla.SegmentMatcher().Match(json) (py/reporter_service.py:112):
+ * request JSON (uuid + trace) in, {"segments":[...]} JSON out.  Returns 200
+ * on success, 500 with {"error":...} otherwise. */
+int otm_match_json(otm_engine* eng, const char* req, size_t len, char** resp,
+                   size_t* resp_len);
+
+/* report() with a caller-supplied matcher output: runs
+ * reporter_service.py:110-215 over `match_json` (what SegmentMatcher.Match
+ * returned) for the request `req`.  Lets a host keep any matcher and use the
+ * native post-processing.  eng may be NULL (then the env is read now). */
+int otm_report_segments(otm_engine* eng, const char* req, size_t len,
+                        const char* match_json, size_t match_len, char** resp,
+                        size_t* resp_len);
+
+/* Async form of otm_report for hosts that cannot block per key (the Kafka
+ * Streams processor issues one blocking POST per record today,
+ * BatchingProcessor.java:69).  Requests submitted before a poll are matched
+ * together in one GPU batch; results for one tag come back once, results of
+ * one uuid in submit order. */
+typedef struct otm_result {
+  uint64_t tag;
+  int code;
+  char* body; /* release with otm_free */
+  size_t body_len;
+} otm_result;
+int otm_submit(otm_engine* eng, const char* req, size_t len, uint64_t tag);
+/* Fills up to max results; waits at most timeout_us for the first one.
+ * Returns the number filled (>=0) or a negative engine error. */
+int otm_poll(otm_engine* eng, otm_result* out, int max, int timeout_us);
+
+/* Java request encoder (Batch.report + Point.Serder.put_json,
+ * Batch.java:52-61, Point.java:39-45): float32 lat/lon through
+ * DecimalFormat("###.######") HALF_EVEN, long time, int accuracy.
+ * *out is allocated by the library. */
+int otm_encode_request(const char* uuid, int n, const float* lat,
+                       const float* lon, const int64_t* time,
+                       const int32_t* accuracy, char** out, size_t* out_len);
+
+/* ----------------------------------------------------------- binary level */
+
+/* A batch of traces, structure of arrays.  Points of trace t are
+ * [trace_off[t], trace_off[t+1]).  The same struct describes host buffers
+ * (otm_match_soa) or device buffers (otm_match_device). */
+typedef struct otm_batch {
+  int32_t n_traces;
+  int64_t n_points;
+  const int64_t* trace_off; /* n_traces + 1 */
+  const float* lat;
+  const float* lon;
+  const double* time;    /* epoch seconds */
+  const float* accuracy; /* metres; <= 0 means "not given" (gps_accuracy) */
+} otm_batch;
+
+/* One matched OSMLR segment (the elements of "segments", README.md:152-165). */
+typedef struct otm_segment {
+  int64_t segment_id;   /* -1: no OSMLR association (key omitted in JSON) */
+  double start_time;    /* valid only if (flags & OTM_SEG_START_VALID)     */
+  double end_time;      /* valid only if (flags & OTM_SEG_END_VALID)       */
+  int32_t length;       /* metres, -1 if partially traversed               */
+  int32_t queue_length; /* always 0 in this era                           */
+  int32_t begin_shape_index;
+  int32_t end_shape_index;
+  int32_t way_off; /* into otm_results.way_ids */
+  int32_t way_cnt;
+  uint32_t flags;
+  uint32_t pad;
+} otm_segment;
+#define OTM_SEG_START_VALID 1u
+#define OTM_SEG_END_VALID 2u
+#define OTM_SEG_INTERNAL 4u
+
+/* One datastore report (reporter_service.py:160-166). */
+typedef struct otm_report_rec {
+  int64_t id;
+  int64_t next_id; /* -1: key absent */
+  double t0;
+  double t1; /* if (flags & OTM_REP_T1_INT_MINUS1) the JSON value is -1 */
+  int32_t length;
+  int32_t queue_length;
+  uint32_t flags;
+  uint32_t pad;
+} otm_report_rec;
+#define OTM_REP_T1_INT_MINUS1 1u
+
+/* Per-trace outcome: the stats block (reporter_service.py:201-213),
+ * shape_used (:125-127) and where the trace's segments/reports live. */
+typedef struct otm_trace_result {
+  int32_t code; /* 200, or 500 (error_kind says why) */
+  int32_t error_kind;
+  int32_t seg_off, seg_cnt;
+  int32_t rep_off, rep_cnt;
+  int32_t shape_used; /* -1 == None */
+  int32_t successful_count;
+  int32_t unreported_count;
+  int32_t discontinuities;
+  int32_t invalid_speeds;
+  int32_t unassociated;
+  int32_t successful_length; /* metres of the LAST counted segment, -1 none */
+  int32_t unreported_length; /* ditto */
+} otm_trace_result;
+#define OTM_TERR_NONE 0
+#define OTM_TERR_ZERODIV 1         /* "float division by zero" */
+#define OTM_TERR_CAND_OVERFLOW 2   /* > OTM_MAX_HITS edges within radius */
+#define OTM_TERR_SEARCH_OVERFLOW 3 /* bounded search settled too many nodes */
+
+/* Host-side result arrays of one batch (owned by the engine until the next
+ * call on the same thread's engine, or copy them). */
+typedef struct otm_results {
+  int32_t n_traces;
+  int32_t n_segments;
+  int32_t n_reports;
+  int32_t n_way_ids;
+  const otm_trace_result* traces;
+  const otm_segment* segments;
+  const otm_report_rec* reports;
+  const int64_t* way_ids;
+} otm_results;
+
+/* Match a host-resident batch; results copied back to host. */
+int otm_match_soa(otm_engine* eng, const otm_batch* in, otm_results* out);
+
+/* Match a batch whose arrays are already in this engine's device memory.
+ * Results stay on the device (fetch with otm_fetch_results).  `stream` is a
+ * hipStream_t (NULL = the engine's own stream); the call returns after the
+ * work is enqueued and the variable-size outputs are sized. */
+int otm_match_device(otm_engine* eng, const otm_batch* in_dev, void* stream);
+int otm_fetch_results(otm_engine* eng, otm_results* out);
+
+/* Per-segment speed histogram, accumulated on the device by every match
+ * call: counts u32[n_segments * nbins], bin = floor(kph / bin_kph) clamped to
+ * nbins-1, one count per datastore report.  The buffer is CALLER-owned device
+ * memory (e.g. a torch tensor) so the host can reduce it across GPUs with
+ * RCCL.  Pass NULL to stop accumulating. */
+int otm_hist_bind(otm_engine* eng, void* dev_counts, int nbins, float bin_kph);
+int otm_graph_info(const otm_engine* eng, int64_t* n_nodes, int64_t* n_edges,
+                   int64_t* n_segments);
+
+/* Work counters of the last batch (for the roofline's algorithmic bytes). */
+typedef struct otm_work_counters {
+  int64_t points, columns, cells_visited, cell_entries_scanned;
+  int64_t edges_projected_unique, shape_points_projected, candidates;
+  int64_t searches, nodes_settled, edges_relaxed, transitions;
+  int64_t route_searches, route_edges, segments_out, reports_out;
+} otm_work_counters;
+/* Enable (1) or disable (0) counting; counting runs extra atomics, so timed
+ * runs keep it off. */
+int otm_set_counting(otm_engine* eng, int on);
+int otm_get_counters(otm_engine* eng, otm_work_counters* out);
+
+/* Per-stage timings (ms) of the last otm_match_device call, from HIP events
+ * on the engine stream: [columns, candidates, trans_size, transitions,
+ * viterbi, route, segments, report].  Enabled with otm_set_timing. */
+int otm_set_timing(otm_engine* eng, int on);
+int otm_get_stage_ms(otm_engine* eng, float* ms, int n);
+
+/* Stage outputs of the last batch, for parity tests (device -> host copy).
+ * what: 0 ncand i32[P], 1 cand_edge i32[P*KMAX], 2 cand_off f32[P*KMAX],
+ * 3 cand_emis f32[P*KMAX], 4 trans_off i64[P+1], 5 trans f32[total],
+ * 6 state i32[P], 7 col_prev i32[P], 8 route_dist f32[P], 9 gc f32[P]. */
+int otm_debug_fetch(otm_engine* eng, int what, void* dst, size_t bytes,
+                    size_t* needed);
+int otm_kmax(void);
+
+/* --------------------------------------------------- synthetic inputs ---- */
+/* Harness tooling, not the hot path: the seeded synthetic road network and
+ * probe traces of SURVEY.md §8(d) (no real Valhalla tiles exist here). */
+typedef struct otm_synth_graph_params {
+  double center_lat, center_lon;
+  double width_m, height_m;
+  double block_m;  /* grid spacing (150 m city) */
+  double jitter_m; /* node position jitter (+-) */
+  int arterial_every;
+  int highway_every;
+  double unassoc_frac; /* local street blocks without OSMLR coverage */
+  int complex_every;   /* >0: crossings of lines that are multiples of this
+                          become 4-node squares of internal edges */
+  double seg_max_m;    /* OSMLR segment max length */
+  double cell_deg;     /* grid index cell (meili grid.size 500 / 0.25 deg) */
+  uint64_t seed;
+} otm_synth_graph_params;
+void otm_synth_graph_defaults(otm_synth_graph_params* p);
+int otm_synth_graph(const otm_synth_graph_params* p, const char* out_path);
+
+typedef struct otm_synth_trace_params {
+  int32_t n_vehicles;
+  int32_t points_per_vehicle;
+  double interval_s;
+  double noise_sigma_m;
+  float accuracy;
+  double t0;
+  uint64_t seed;
+  int32_t vehicle_offset; /* global index of vehicle 0 (for sharding) */
+} otm_synth_trace_params;
+/* Fills caller-allocated arrays sized n_vehicles*points_per_vehicle (lat,
+ * lon, time, accuracy, true_edge, true_off) and n_vehicles+1 (trace_off).
+ * Graph is read from graph_path. */
+int otm_synth_traces(const char* graph_path, const otm_synth_trace_params* p,
+                     int64_t* trace_off, float* lat, float* lon, double* time,
+                     float* accuracy, int32_t* true_edge, float* true_off);
+
+/* Kafka's default key partitioner (murmur2, seed 0x9747b28c) -- the shard of
+ * a uuid: (murmur2(key) & 0x7fffffff) % n. */
+int32_t otm_murmur2(const char* key, size_t len);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* OTMATCH_H */

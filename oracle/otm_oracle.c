@@ -1,0 +1,1235 @@
+/*
+ * otm_oracle.c -- CPU oracle of the map-matching hot path.
+ * TEST INFRASTRUCTURE: only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg use it, as the checker or the timed CPU baseline.
+ *
+ * This file IS the written spec of SegmentMatcher.Match
+ * (py/reporter_service.py:112 -> Valhalla 2.2.7 meili, not present here;
+ * DESIGN.md §3 restates the same rules in prose).  Every float operation is
+ * spelled out in evaluation order and the library is built with
+ * -ffp-contract=off so that the GPU kernels, which follow the same order,
+ * agree bit for bit.  Parity against meili itself is UNPINNED.
+ *
+ *   S1 columns      interpolation_distance filter, chain links (gc, breakage)
+ *   S2 candidates   grid cells in the radius box -> per-edge best projection
+ *                   -> sort (sqdist, edge) -> first max_candidates
+ *   S3 emission     sqdist / (2 sigma_z^2)
+ *   S4 transitions  bounded Dijkstra per distinct source node, route distance
+ *                   r, cost |r - gc| / beta when r <= factor * gc
+ *   S5 viterbi      min-sum, ties -> lowest index, dead column -> chain break
+ *   S6 route        re-run the winning searches, predecessor edges
+ *   S7 segments     traversals -> OSMLR groups, times linear in distance
+ *   S8 report       py/reporter_service.py:110-215 on typed records
+ */
+#define _GNU_SOURCE
+#include <fcntl.h>
+#include <math.h>
+#include <pthread.h>
+#include <stdatomic.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include "../include/otm_graph_format.h"
+#include "orc_internal.h"
+#include "otm_oracle.h"
+
+#define MPD_F 111319.4954833f /* (float)(20037581.187 / 180), Batch.java:33 */
+#define INF_F INFINITY
+
+#define TERR_NONE 0
+#define TERR_ZERODIV 1
+#define TERR_CAND_OVERFLOW 2
+#define TERR_SEARCH_OVERFLOW 3
+
+static const char* terr_msg(int k) {
+  switch (k) {
+    case TERR_ZERODIV: return "float division by zero";
+    case TERR_CAND_OVERFLOW: return "too many candidate edges within search radius";
+    case TERR_SEARCH_OVERFLOW: return "route search exceeded node limit";
+  }
+  return "";
+}
+
+/* ================================================================== graph */
+struct orc_graph {
+  otmg_header h;
+  void* map;
+  size_t bytes;
+  const float *nlat, *nlon;
+  const int32_t* out_off;
+  const int32_t *efrom, *eto;
+  const float* elen;
+  const int32_t* eshape;
+  const int64_t* eway;
+  const int32_t *eseg, *eseg_pos;
+  const uint8_t* eflags;
+  const float *slat, *slon, *scum;
+  const uint64_t* gid;
+  const float* glen;
+  const int64_t* cell_off;
+  const uint32_t* cell_ent;
+};
+
+orc_graph* orc_graph_load(const char* path) {
+  int fd = open(path, O_RDONLY);
+  if (fd < 0) return NULL;
+  struct stat st;
+  if (fstat(fd, &st) != 0 || (size_t)st.st_size < sizeof(otmg_header)) {
+    close(fd);
+    return NULL;
+  }
+  void* m = mmap(NULL, (size_t)st.st_size, PROT_READ, MAP_PRIVATE, fd, 0);
+  close(fd);
+  if (m == MAP_FAILED) return NULL;
+  orc_graph* g = (orc_graph*)calloc(1, sizeof(orc_graph));
+  g->map = m;
+  g->bytes = (size_t)st.st_size;
+  memcpy(&g->h, m, sizeof(otmg_header));
+  if (memcmp(g->h.magic, OTMG_MAGIC, 8) != 0 || g->h.version != OTMG_VERSION) {
+    orc_graph_free(g);
+    return NULL;
+  }
+#define SEC(s) ((const void*)((const char*)m + g->h.sec[s].offset))
+  g->nlat = SEC(OTMG_NODE_LAT);
+  g->nlon = SEC(OTMG_NODE_LON);
+  g->out_off = SEC(OTMG_NODE_OUT_OFF);
+  g->efrom = SEC(OTMG_EDGE_FROM);
+  g->eto = SEC(OTMG_EDGE_TO);
+  g->elen = SEC(OTMG_EDGE_LEN);
+  g->eshape = SEC(OTMG_EDGE_SHAPE_OFF);
+  g->eway = SEC(OTMG_EDGE_WAY);
+  g->eseg = SEC(OTMG_EDGE_SEG);
+  g->eseg_pos = SEC(OTMG_EDGE_SEG_POS);
+  g->eflags = SEC(OTMG_EDGE_FLAGS);
+  g->slat = SEC(OTMG_SHAPE_LAT);
+  g->slon = SEC(OTMG_SHAPE_LON);
+  g->scum = SEC(OTMG_SHAPE_CUM);
+  g->gid = SEC(OTMG_SEG_ID);
+  g->glen = SEC(OTMG_SEG_LEN);
+  g->cell_off = SEC(OTMG_CELL_OFF);
+  g->cell_ent = SEC(OTMG_CELL_ENT);
+#undef SEC
+  return g;
+}
+void orc_graph_free(orc_graph* g) {
+  if (!g) return;
+  if (g->map) munmap(g->map, g->bytes);
+  free(g);
+}
+int64_t orc_graph_count(const orc_graph* g, int what) {
+  return what == 0 ? g->h.n_nodes : (what == 1 ? g->h.n_edges : g->h.n_segments);
+}
+void orc_params_default(orc_params* p) {
+  p->sigma_z = 4.07f;
+  p->beta = 3.0f;
+  p->max_route_distance_factor = 5.0f;
+  p->breakage_distance = 2000.0f;
+  p->interpolation_distance = 10.0f;
+  p->search_radius = 50.0f;
+  p->max_search_radius = 100.0f;
+  p->gps_accuracy = 5.0f;
+  p->max_candidates = ORC_KMAX;
+}
+void orc_report_cfg_default(orc_report_cfg* c) {
+  memset(c, 0, sizeof *c);
+  c->n_report = 2;
+  c->report_levels[0] = 0;
+  c->report_levels[1] = 1;
+  c->n_transition = 2;
+  c->transition_levels[0] = 0;
+  c->transition_levels[1] = 1;
+  c->threshold_sec = 15.0;
+}
+void orc_free(void* p) { free(p); }
+
+/* ================================================================== math */
+/* cos of an angle in degrees: degree-14 Taylor polynomial in x^2, Horner
+ * order, float.  |lat| <= 90 keeps |x| <= pi/2 (truncation < 1e-10). */
+float orc_cos_deg(float deg) {
+  const float x = deg * 0.017453292519943295f;
+  const float x2 = x * x;
+  float c = -1.1470745597729725e-11f;
+  c = c * x2 + 2.08767569878681e-09f;
+  c = c * x2 - 2.755731922398589e-07f;
+  c = c * x2 + 2.48015873015873e-05f;
+  c = c * x2 - 0.001388888888888889f;
+  c = c * x2 + 0.041666666666666664f;
+  c = c * x2 - 0.5f;
+  c = c * x2 + 1.0f;
+  return c;
+}
+/* equirectangular distance at the mean latitude (meters) */
+static float orc_gc(float la, float lo, float lb, float lob) {
+  const float ls = MPD_F * orc_cos_deg((la + lb) * 0.5f);
+  const float dx = (lob - lo) * ls;
+  const float dy = (lb - la) * MPD_F;
+  return sqrtf(dx * dx + dy * dy);
+}
+
+/* ================================================================== S2 candidates */
+typedef struct {
+  int32_t edge;
+  float sqd, off;
+  int32_t k;
+} hit;
+
+static int hit_cmp(const void* a, const void* b) {
+  const hit* x = (const hit*)a;
+  const hit* y = (const hit*)b;
+  if (x->sqd < y->sqd) return -1;
+  if (x->sqd > y->sqd) return 1;
+  return (x->edge > y->edge) - (x->edge < y->edge);
+}
+
+/* projection of the probe (lat,lon) onto shape segment k of edge e */
+static void project(const orc_graph* g, int32_t e, int32_t k, float lat, float lon, float ls, float* sqd_out,
+                    float* off_out) {
+  const int32_t a = g->eshape[e] + k, b = a + 1;
+  const float ax = (g->slon[a] - lon) * ls;
+  const float ay = (g->slat[a] - lat) * MPD_F;
+  const float bx = (g->slon[b] - lon) * ls;
+  const float by = (g->slat[b] - lat) * MPD_F;
+  const float vx = bx - ax;
+  const float vy = by - ay;
+  const float l2 = vx * vx + vy * vy;
+  float t = 0.0f;
+  if (l2 > 0.0f) {
+    const float dot = ax * vx + ay * vy;
+    t = -dot / l2;
+    t = t < 0.0f ? 0.0f : (t > 1.0f ? 1.0f : t);
+  }
+  const float px = ax + t * vx;
+  const float py = ay + t * vy;
+  *sqd_out = px * px + py * py;
+  float off = g->scum[a] + t * (g->scum[b] - g->scum[a]);
+  const float len = g->elen[e];
+  off = off > len ? len : off;
+  *off_out = off;
+}
+
+/* radius rule: max(search_radius, accuracy or gps_accuracy), capped */
+static float probe_radius(const orc_params* P, float acc) {
+  const float a = acc > 0.0f ? acc : P->gps_accuracy;
+  float r = a > P->search_radius ? a : P->search_radius;
+  return r < P->max_search_radius ? r : P->max_search_radius;
+}
+
+/* returns number of candidates, or -1 on overflow */
+static int candidates(const orc_graph* g, const orc_params* P, float lat, float lon, float acc, int32_t* c_edge,
+                      float* c_off, float* c_emis, hit* hits, orc_counters* C) {
+  const float r = probe_radius(P, acc);
+  const float r2 = r * r;
+  const float ls = MPD_F * orc_cos_deg(lat);
+  const float dlat = r / MPD_F;
+  const float dlon = r / ls;
+  const double cell = g->h.grid_cell_deg;
+  const double la_lo = ((double)lat - (double)dlat - g->h.grid_lat0) / cell;
+  const double la_hi = ((double)lat + (double)dlat - g->h.grid_lat0) / cell;
+  const double lo_lo = ((double)lon - (double)dlon - g->h.grid_lon0) / cell;
+  const double lo_hi = ((double)lon + (double)dlon - g->h.grid_lon0) / cell;
+  const double R = g->h.grid_rows, Cn = g->h.grid_cols;
+  int nh = 0;
+  if (!(la_hi < 0.0 || lo_hi < 0.0 || la_lo >= R || lo_lo >= Cn)) {
+    const int r0 = la_lo < 0.0 ? 0 : (int)floor(la_lo);
+    const int r1 = la_hi >= R ? (int)R - 1 : (int)floor(la_hi);
+    const int c0 = lo_lo < 0.0 ? 0 : (int)floor(lo_lo);
+    const int c1 = lo_hi >= Cn ? (int)Cn - 1 : (int)floor(lo_hi);
+    for (int rr = r0; rr <= r1; ++rr) {
+      for (int cc = c0; cc <= c1; ++cc) {
+        const size_t cidx = (size_t)rr * (size_t)g->h.grid_cols + (size_t)cc;
+        C->cells_visited++;
+        for (int64_t q = g->cell_off[cidx]; q < g->cell_off[cidx + 1]; ++q) {
+          const uint32_t ent = g->cell_ent[q];
+          const int32_t e = (int32_t)(ent >> 4), k = (int32_t)(ent & 15u);
+          float sqd, off;
+          project(g, e, k, lat, lon, ls, &sqd, &off);
+          C->cell_entries_scanned++;
+          if (!(sqd <= r2)) continue;
+          int f = -1;
+          for (int h = 0; h < nh; ++h)
+            if (hits[h].edge == e) {
+              f = h;
+              break;
+            }
+          if (f < 0) {
+            if (nh == ORC_MAX_HITS) return -1;
+            hits[nh].edge = e;
+            hits[nh].sqd = sqd;
+            hits[nh].off = off;
+            hits[nh].k = k;
+            ++nh;
+          } else if (sqd < hits[f].sqd || (sqd == hits[f].sqd && k < hits[f].k)) {
+            hits[f].sqd = sqd;
+            hits[f].off = off;
+            hits[f].k = k;
+          }
+        }
+      }
+    }
+  }
+  qsort(hits, (size_t)nh, sizeof(hit), hit_cmp);
+  const int K = nh < P->max_candidates ? nh : P->max_candidates;
+  const float ds = (2.0f * P->sigma_z) * P->sigma_z;
+  for (int j = 0; j < K; ++j) {
+    c_edge[j] = hits[j].edge;
+    c_off[j] = hits[j].off;
+    c_emis[j] = hits[j].sqd / ds;
+  }
+  C->candidates += K;
+  return K;
+}
+
+/* ================================================================== S4/S6 bounded Dijkstra */
+typedef struct {
+  float d;
+  int32_t n;
+} hnode;
+
+typedef struct ws {
+  float* dist;
+  int32_t* pred;
+  uint32_t* lab;
+  uint32_t* done;
+  uint32_t stamp;
+  hnode* heap;
+  size_t hn, hcap;
+  int32_t nlab;
+  hit hits[ORC_MAX_HITS + 1];
+} ws;
+
+static void hpush(ws* w, float d, int32_t n) {
+  if (w->hn == w->hcap) {
+    w->hcap = w->hcap ? w->hcap * 2 : 1024;
+    w->heap = (hnode*)realloc(w->heap, w->hcap * sizeof(hnode));
+  }
+  size_t i = w->hn++;
+  while (i > 0) {
+    size_t p = (i - 1) / 2;
+    if (w->heap[p].d <= d) break;
+    w->heap[i] = w->heap[p];
+    i = p;
+  }
+  w->heap[i].d = d;
+  w->heap[i].n = n;
+}
+static hnode hpop(ws* w) {
+  hnode top = w->heap[0];
+  hnode last = w->heap[--w->hn];
+  size_t i = 0;
+  while (1) {
+    size_t c = 2 * i + 1;
+    if (c >= w->hn) break;
+    if (c + 1 < w->hn && w->heap[c + 1].d < w->heap[c].d) ++c;
+    if (w->heap[c].d >= last.d) break;
+    w->heap[i] = w->heap[c];
+    i = c;
+  }
+  if (w->hn) w->heap[i] = last;
+  return top;
+}
+
+/* Labels D(v) for every v with D(v) <= B from source node u (D(u) = 0).
+ * pred(v) = the lexicographically smallest (D(w) + len(e), e) over in-edges.
+ * Returns 0, or -1 when more than ORC_SEARCH_LIMIT nodes are labelled. */
+static int dijkstra(const orc_graph* g, ws* w, int32_t u, float B, orc_counters* C) {
+  if (++w->stamp == 0) {
+    memset(w->lab, 0, sizeof(uint32_t) * (size_t)g->h.n_nodes);
+    memset(w->done, 0, sizeof(uint32_t) * (size_t)g->h.n_nodes);
+    w->stamp = 1;
+  }
+  const uint32_t s = w->stamp;
+  w->hn = 0;
+  w->lab[u] = s;
+  w->dist[u] = 0.0f;
+  w->pred[u] = -1;
+  w->nlab = 1;
+  hpush(w, 0.0f, u);
+  int64_t relaxed = 0;
+  while (w->hn) {
+    hnode h = hpop(w);
+    if (w->done[h.n] == s || h.d != w->dist[h.n]) continue;
+    w->done[h.n] = s;
+    const float d = h.d;
+    for (int32_t e = g->out_off[h.n]; e < g->out_off[h.n + 1]; ++e) {
+      ++relaxed;
+      const float nd = d + g->elen[e];
+      if (!(nd <= B)) continue;
+      const int32_t v = g->eto[e];
+      if (w->lab[v] != s) {
+        if (w->nlab == ORC_SEARCH_LIMIT) return -1;
+        w->lab[v] = s;
+        w->dist[v] = nd;
+        w->pred[v] = e;
+        w->nlab++;
+        hpush(w, nd, v);
+      } else if (nd < w->dist[v]) {
+        w->dist[v] = nd;
+        w->pred[v] = e;
+        hpush(w, nd, v);
+      } else if (nd == w->dist[v] && e < w->pred[v]) {
+        w->pred[v] = e;
+      }
+    }
+  }
+  C->searches++;
+  C->nodes_settled += w->nlab;
+  C->edges_relaxed += relaxed;
+  return 0;
+}
+
+/* ================================================================== per-batch state */
+typedef struct tres {
+  orc_segment* segs;
+  int nseg, cseg;
+  int64_t* ways;
+  int nway, cway;
+  orc_report_rec* reps;
+  int nrep, crep;
+  orc_trace_result tr;
+} tres;
+
+typedef struct batch {
+  const orc_graph* g;
+  const orc_params* P;
+  const orc_report_cfg* rc;
+  int32_t n_traces;
+  const int64_t* toff_pts;
+  const float *lat, *lon, *acc;
+  const double* time;
+  /* point-indexed stage arrays */
+  uint8_t* is_col;
+  uint8_t* chain_start;
+  int32_t *ncand, *cand_edge, *state, *col_prev;
+  float *cand_off, *cand_emis, *route_dist, *gc;
+  int32_t* terr; /* per trace error kind */
+  int64_t* trans_off;
+  float* trans;
+  tres* res;
+  atomic_int next;
+  int phase;
+  orc_counters* ctr; /* per thread */
+} batch;
+
+#define GROW(arr, n, cap, T)                                   \
+  do {                                                         \
+    if ((n) == (cap)) {                                        \
+      (cap) = (cap) ? 2 * (cap) : 8;                           \
+      (arr) = (T*)realloc((arr), sizeof(T) * (size_t)(cap));   \
+    }                                                          \
+  } while (0)
+
+/* ------------------------------------------------------------ S1 + S2 */
+static void phase_a(batch* B, ws* w, int32_t t, orc_counters* C) {
+  const orc_graph* g = B->g;
+  const orc_params* P = B->P;
+  const int64_t a = B->toff_pts[t], b = B->toff_pts[t + 1];
+  int64_t last = -1;
+  for (int64_t p = a; p < b; ++p) {
+    B->ncand[p] = 0;
+    B->col_prev[p] = -1;
+    B->gc[p] = 0.0f;
+    B->is_col[p] = 0;
+    C->points++;
+    float gcv = 0.0f;
+    if (last >= 0) {
+      gcv = orc_gc(B->lat[last], B->lon[last], B->lat[p], B->lon[p]);
+      if (!(gcv >= P->interpolation_distance)) continue;
+    }
+    B->is_col[p] = 1;
+    C->columns++;
+    B->gc[p] = gcv;
+    int K = candidates(g, P, B->lat[p], B->lon[p], B->acc[p], B->cand_edge + p * ORC_KMAX,
+                       B->cand_off + p * ORC_KMAX, B->cand_emis + p * ORC_KMAX, w->hits, C);
+    if (K < 0) {
+      if (!B->terr[t]) B->terr[t] = TERR_CAND_OVERFLOW;
+      K = 0;
+    }
+    B->ncand[p] = K;
+    if (last >= 0 && K > 0 && B->ncand[last] > 0 && gcv <= P->breakage_distance) B->col_prev[p] = (int32_t)last;
+    last = p;
+  }
+}
+
+/* ------------------------------------------------------------ S4 */
+static int transitions(batch* B, ws* w, int64_t p, orc_counters* C) {
+  const orc_graph* g = B->g;
+  const int64_t q = B->col_prev[p];
+  const int Kq = B->ncand[q], Kp = B->ncand[p];
+  const float gcv = B->gc[p];
+  const float bound = B->P->max_route_distance_factor * gcv;
+  float* T = B->trans + B->trans_off[p];
+  for (int k = 0; k < Kq * Kp; ++k) T[k] = INF_F;
+  const int32_t* eq = B->cand_edge + q * ORC_KMAX;
+  const float* oq = B->cand_off + q * ORC_KMAX;
+  const int32_t* ep = B->cand_edge + p * ORC_KMAX;
+  const float* op = B->cand_off + p * ORC_KMAX;
+  int32_t srcs[ORC_KMAX];
+  int ns = 0;
+  for (int i = 0; i < Kq; ++i) {
+    int32_t u = g->eto[eq[i]];
+    int seen = 0;
+    for (int s = 0; s < ns; ++s) seen |= srcs[s] == u;
+    if (!seen) srcs[ns++] = u;
+  }
+  for (int s = 0; s < ns; ++s) {
+    const int32_t u = srcs[s];
+    if (dijkstra(g, w, u, bound, C) < 0) return -1;
+    for (int i = 0; i < Kq; ++i) {
+      if (g->eto[eq[i]] != u) continue;
+      const float start = g->elen[eq[i]] - oq[i];
+      for (int j = 0; j < Kp; ++j) {
+        float r;
+        if (ep[j] == eq[i] && op[j] >= oq[i]) {
+          r = op[j] - oq[i];
+        } else {
+          const int32_t v = g->efrom[ep[j]];
+          if (w->lab[v] != w->stamp) continue;
+          const float sd = start + w->dist[v];
+          r = sd + op[j];
+        }
+        if (r <= bound) {
+          const float diff = fabsf(r - gcv);
+          T[i * Kp + j] = diff / B->P->beta;
+          C->transitions++;
+        }
+      }
+    }
+  }
+  return 0;
+}
+
+/* ------------------------------------------------------------ S5 */
+static void viterbi(batch* B, int32_t t, uint8_t* bp /* [npts*KMAX] */) {
+  const int64_t a = B->toff_pts[t], b = B->toff_pts[t + 1];
+  float prev[ORC_KMAX], cur[ORC_KMAX];
+  int open = 0;
+  int64_t last = -1;
+#define BACKTRACK(endp)                                                                \
+  do {                                                                                 \
+    int64_t pp = (endp);                                                               \
+    int bj = -1;                                                                       \
+    float bv = INF_F;                                                                  \
+    for (int j = 0; j < B->ncand[pp]; ++j)                                             \
+      if (prev[j] < bv) {                                                              \
+        bv = prev[j];                                                                  \
+        bj = j;                                                                        \
+      }                                                                                \
+    int jj = bj;                                                                       \
+    while (1) {                                                                        \
+      B->state[pp] = jj;                                                               \
+      if (B->chain_start[pp]) break;                                                   \
+      jj = bp[(pp - a) * ORC_KMAX + jj];                                               \
+      pp = B->col_prev[pp];                                                            \
+    }                                                                                  \
+  } while (0)
+  for (int64_t p = a; p < b; ++p) {
+    B->state[p] = -1;
+    B->chain_start[p] = 0;
+  }
+  for (int64_t p = a; p < b; ++p) {
+    if (!B->is_col[p]) continue;
+    const int Kp = B->ncand[p];
+    if (Kp == 0) {
+      if (open) BACKTRACK(last);
+      open = 0;
+      continue;
+    }
+    const float* em = B->cand_emis + p * ORC_KMAX;
+    int started = 0;
+    if (open && B->col_prev[p] == last) {
+      const int Kq = B->ncand[last];
+      const float* T = B->trans + B->trans_off[p];
+      int any = 0;
+      for (int j = 0; j < Kp; ++j) {
+        float best = INF_F;
+        int bi = -1;
+        for (int i = 0; i < Kq; ++i) {
+          const float v = prev[i] + T[i * Kp + j];
+          if (v < best) {
+            best = v;
+            bi = i;
+          }
+        }
+        if (bi >= 0) {
+          cur[j] = best + em[j];
+          bp[(p - a) * ORC_KMAX + j] = (uint8_t)bi;
+          any = 1;
+        } else {
+          cur[j] = INF_F;
+          bp[(p - a) * ORC_KMAX + j] = 0xFF;
+        }
+      }
+      if (!any) {
+        BACKTRACK(last);
+      } else {
+        started = 1;
+      }
+    } else if (open) {
+      BACKTRACK(last);
+    }
+    if (!started) {
+      for (int j = 0; j < Kp; ++j) cur[j] = em[j];
+      B->chain_start[p] = 1;
+    }
+    memcpy(prev, cur, sizeof(float) * (size_t)Kp);
+    open = 1;
+    last = p;
+  }
+  if (open) BACKTRACK(last);
+#undef BACKTRACK
+}
+
+/* ------------------------------------------------------------ S6 + S7 */
+typedef struct {
+  int32_t edge;
+  float off0, off1;
+  double t0, t1;
+  int32_t sh0, sh1;
+} trav;
+
+typedef struct {
+  trav* v;
+  int n, cap;
+} travs;
+
+static void tpush(travs* T, trav x) {
+  GROW(T->v, T->n, T->cap, trav);
+  T->v[T->n++] = x;
+}
+
+static void emit_group(batch* B, tres* R, const trav* f, const trav* l, const trav* all, int gi0, int gi1) {
+  const orc_graph* g = B->g;
+  GROW(R->segs, R->nseg, R->cseg, orc_segment);
+  orc_segment* s = &R->segs[R->nseg++];
+  memset(s, 0, sizeof *s);
+  const int32_t sg = g->eseg[f->edge];
+  int sv, ev;
+  if (sg >= 0) {
+    sv = f->off0 == 0.0f && (g->eflags[f->edge] & OTM_EDGE_SEG_BEGIN);
+    ev = l->off1 == g->elen[l->edge] && (g->eflags[l->edge] & OTM_EDGE_SEG_END);
+    s->segment_id = (int64_t)g->gid[sg];
+    s->length = (sv && ev) ? (int32_t)floor((double)g->glen[sg] + 0.5) : -1;
+  } else {
+    sv = f->off0 == 0.0f;
+    ev = l->off1 == g->elen[l->edge];
+    s->segment_id = -1;
+    s->length = -1;
+    if (g->eflags[f->edge] & OTM_EDGE_INTERNAL) s->flags |= 4u;
+  }
+  if (sv) {
+    s->flags |= 1u;
+    s->start_time = f->t0;
+  }
+  if (ev) {
+    s->flags |= 2u;
+    s->end_time = l->t1;
+  }
+  s->queue_length = 0;
+  s->begin_shape_index = f->sh0;
+  s->end_shape_index = l->sh1;
+  s->way_off = R->nway;
+  for (int k = gi0; k <= gi1; ++k) {
+    const int64_t way = g->eway[all[k].edge];
+    if (R->nway > s->way_off && R->ways[R->nway - 1] == way) continue;
+    GROW(R->ways, R->nway, R->cway, int64_t);
+    R->ways[R->nway++] = way;
+  }
+  s->way_cnt = R->nway - s->way_off;
+}
+
+static void group_chain(batch* B, tres* R, const travs* T) {
+  const orc_graph* g = B->g;
+  int gs = -1; /* group start index */
+  for (int k = 0; k < T->n; ++k) {
+    const int32_t e = T->v[k].edge;
+    int join = 0;
+    if (gs >= 0) {
+      const int32_t pe = T->v[k - 1].edge;
+      const int32_t s = g->eseg[e], ps = g->eseg[pe];
+      if (s >= 0) join = ps == s && g->eseg_pos[e] == g->eseg_pos[pe] + 1;
+      else join = ps < 0 && ((g->eflags[e] ^ g->eflags[pe]) & OTM_EDGE_INTERNAL) == 0;
+    }
+    if (!join) {
+      if (gs >= 0) emit_group(B, R, &T->v[gs], &T->v[k - 1], T->v, gs, k - 1);
+      gs = k;
+    }
+  }
+  if (gs >= 0) emit_group(B, R, &T->v[gs], &T->v[T->n - 1], T->v, gs, T->n - 1);
+}
+
+/* route of step p (from state at q = col_prev[p] to state at p) */
+static int route_step(batch* B, ws* w, int64_t p, int32_t* path, int* plen, int* same, float* R,
+                      orc_counters* C) {
+  const orc_graph* g = B->g;
+  const int64_t q = B->col_prev[p];
+  const int i = B->state[q], j = B->state[p];
+  const int32_t ei = B->cand_edge[q * ORC_KMAX + i], ej = B->cand_edge[p * ORC_KMAX + j];
+  const float oi = B->cand_off[q * ORC_KMAX + i], oj = B->cand_off[p * ORC_KMAX + j];
+  *plen = 0;
+  if (ei == ej && oj >= oi) {
+    *same = 1;
+    *R = oj - oi;
+    return 0;
+  }
+  *same = 0;
+  const float bound = B->P->max_route_distance_factor * B->gc[p];
+  const int32_t u = g->eto[ei], v = g->efrom[ej];
+  if (dijkstra(g, w, u, bound, C) < 0) return -1;
+  C->route_searches++;
+  int n = 0;
+  for (int32_t x = v; x != u;) {
+    const int32_t e = w->pred[x];
+    path[n++] = e;
+    x = g->efrom[e];
+  }
+  for (int k = 0; k < n / 2; ++k) {
+    int32_t tmp = path[k];
+    path[k] = path[n - 1 - k];
+    path[n - 1 - k] = tmp;
+  }
+  *plen = n;
+  C->route_edges += n;
+  const float start = g->elen[ei] - oi;
+  const float sd = start + w->dist[v];
+  *R = sd + oj;
+  return 0;
+}
+
+static double time_at(double ta, double tb, float x, float R) {
+  if (R > 0.0f) return ta + (tb - ta) * ((double)x / (double)R);
+  return ta;
+}
+
+static int segments_of_trace(batch* B, ws* w, int32_t t, tres* R, orc_counters* C) {
+  const orc_graph* g = B->g;
+  const int64_t a = B->toff_pts[t], b = B->toff_pts[t + 1];
+  travs T = {0};
+  int32_t* path = NULL;
+  int pcap = 0;
+  int open = 0;   /* a chain is open */
+  int nstate = 0; /* states in the open chain */
+  trav cur = {0};
+  int64_t lastp = -1;
+  int rc = 0;
+  for (int64_t p = a; p <= b; ++p) {
+    const int is_state = p < b && B->is_col[p] && B->state[p] >= 0;
+    if (p < b && !is_state) continue;
+    const int new_chain = p == b || B->chain_start[p];
+    if (open && new_chain) {
+      /* close the open chain */
+      const int32_t sl = B->state[lastp];
+      cur.off1 = B->cand_off[lastp * ORC_KMAX + sl];
+      cur.t1 = B->time[lastp];
+      cur.sh1 = (int32_t)(lastp - a);
+      tpush(&T, cur);
+      if (nstate >= 2) group_chain(B, R, &T);
+      T.n = 0;
+      open = 0;
+    }
+    if (p == b) break;
+    const int j = B->state[p];
+    const int32_t ej = B->cand_edge[p * ORC_KMAX + j];
+    const float oj = B->cand_off[p * ORC_KMAX + j];
+    if (new_chain) {
+      cur.edge = ej;
+      cur.off0 = oj;
+      cur.t0 = B->time[p];
+      cur.sh0 = (int32_t)(p - a);
+      open = 1;
+      nstate = 1;
+      lastp = p;
+      continue;
+    }
+    /* step lastp -> p */
+    if (pcap < 4096) {
+      pcap = 4096;
+      path = (int32_t*)realloc(path, sizeof(int32_t) * (size_t)pcap);
+    }
+    int plen, same;
+    float Rd;
+    if (route_step(B, w, p, path, &plen, &same, &Rd, C) < 0) {
+      rc = -1;
+      break;
+    }
+    B->route_dist[p] = Rd;
+    const double ta = B->time[lastp], tb = B->time[p];
+    const int32_t ca = (int32_t)(lastp - a), cb = (int32_t)(p - a);
+    if (!same) {
+      const int32_t ei = cur.edge;
+      const float start = g->elen[ei] - B->cand_off[lastp * ORC_KMAX + B->state[lastp]];
+      float x = start;
+      cur.off1 = g->elen[ei];
+      cur.t1 = time_at(ta, tb, x, Rd);
+      cur.sh1 = x >= Rd ? cb : ca;
+      tpush(&T, cur);
+      float dd = 0.0f;
+      for (int k = 0; k < plen; ++k) {
+        const int32_t pe = path[k];
+        trav m;
+        m.edge = pe;
+        m.off0 = 0.0f;
+        m.off1 = g->elen[pe];
+        const float xb = start + dd;
+        dd = dd + g->elen[pe];
+        const float xe = start + dd;
+        m.t0 = time_at(ta, tb, xb, Rd);
+        m.t1 = time_at(ta, tb, xe, Rd);
+        m.sh0 = xb >= Rd ? cb : ca;
+        m.sh1 = xe >= Rd ? cb : ca;
+        tpush(&T, m);
+      }
+      x = start + dd;
+      cur.edge = ej;
+      cur.off0 = 0.0f;
+      cur.t0 = time_at(ta, tb, x, Rd);
+      cur.sh0 = x >= Rd ? cb : ca;
+    }
+    nstate++;
+    lastp = p;
+  }
+  free(T.v);
+  free(path);
+  return rc;
+}
+
+/* ------------------------------------------------------------ S8 typed report */
+static int in_lv(const int64_t* lv, int n, int64_t x) {
+  for (int k = 0; k < n; ++k)
+    if (lv[k] == x) return 1;
+  return 0;
+}
+static int typed_report(batch* B, int32_t t, tres* R) {
+  const orc_report_cfg* rc = B->rc;
+  const double end_time = B->time[B->toff_pts[t + 1] - 1];
+  orc_trace_result* o = &R->tr;
+  int last_idx = R->nseg - 1;
+#define ST(s) (((s).flags & 1u) ? (s).start_time : -1.0)
+#define ET(s) (((s).flags & 2u) ? (s).end_time : -1.0)
+  while (last_idx >= 0 && end_time - ST(R->segs[last_idx]) < rc->threshold_sec) --last_idx;
+  o->shape_used = last_idx >= 0 ? R->segs[last_idx].begin_shape_index : -1;
+  int have = 0, first = 1;
+  const orc_segment* prior = NULL;
+  int64_t prior_level = -1;
+  o->successful_length = o->unreported_length = -1;
+  for (int idx = 0; idx <= last_idx; ++idx) {
+    const orc_segment* s = &R->segs[idx];
+    const int internal = (s->flags & 4u) != 0;
+    if (idx != 0 && ST(*s) == -1.0 && ET(R->segs[idx - 1]) == -1.0) o->discontinuities++;
+    const int64_t level = s->segment_id >= 0 ? (s->segment_id & 7) : -1;
+    if (have && prior->segment_id >= 0 && prior->length > 0 && !internal) {
+      if (in_lv(rc->report_levels, rc->n_report, prior_level)) {
+        const int trans = in_lv(rc->transition_levels, rc->n_transition, level);
+        const double t0 = ST(*prior);
+        const double t1 = trans ? ST(*s) : ET(*prior);
+        const double den = t1 - t0;
+        if (den == 0.0) return TERR_ZERODIV;
+        const double speed = ((double)prior->length / den) * 3.6;
+        if (speed < 200.0) {
+          GROW(R->reps, R->nrep, R->crep, orc_report_rec);
+          orc_report_rec* r = &R->reps[R->nrep++];
+          memset(r, 0, sizeof *r);
+          r->id = prior->segment_id;
+          r->next_id = (trans && s->segment_id >= 0) ? s->segment_id : -1;
+          r->t0 = t0;
+          r->t1 = t1;
+          if (trans && !(s->flags & 1u)) r->flags |= 1u;
+          r->length = prior->length;
+          r->queue_length = prior->queue_length;
+          o->successful_count++;
+          o->successful_length = prior->length;
+        } else {
+          o->invalid_speeds++;
+        }
+      } else {
+        o->unreported_count++;
+        o->unreported_length = prior->length;
+      }
+    }
+    if (!(internal && !first)) {
+      prior = s;
+      prior_level = level;
+      have = 1;
+    }
+    first = 0;
+    if (s->segment_id < 0 && !internal) o->unassociated++;
+  }
+#undef ST
+#undef ET
+  return 0;
+}
+
+static void phase_b(batch* B, ws* w, int32_t t, orc_counters* C) {
+  const int64_t a = B->toff_pts[t], b = B->toff_pts[t + 1];
+  tres* R = &B->res[t];
+  memset(R, 0, sizeof *R);
+  R->tr.shape_used = -1;
+  R->tr.successful_length = R->tr.unreported_length = -1;
+  int err = B->terr[t];
+  for (int64_t p = a; p < b; ++p) B->route_dist[p] = 0.0f;
+  if (!err) {
+    for (int64_t p = a; p < b && !err; ++p)
+      if (B->is_col[p] && B->col_prev[p] >= 0)
+        if (transitions(B, w, p, C) < 0) err = TERR_SEARCH_OVERFLOW;
+  }
+  uint8_t* bp = (uint8_t*)malloc((size_t)(b - a) * ORC_KMAX + 1);
+  if (!err) viterbi(B, t, bp);
+  else
+    for (int64_t p = a; p < b; ++p) B->state[p] = -1;
+  free(bp);
+  if (!err && segments_of_trace(B, w, t, R, C) < 0) err = TERR_SEARCH_OVERFLOW;
+  if (!err) err = typed_report(B, t, R);
+  if (err) {
+    /* a report()-stage error (ZeroDivisionError) keeps the matched segments:
+       Match succeeded, only the response is the error body */
+    if (err != TERR_ZERODIV) R->nseg = R->nway = 0;
+    R->nrep = 0;
+    memset(&R->tr, 0, sizeof R->tr);
+    R->tr.code = 500;
+    R->tr.error_kind = err;
+    R->tr.shape_used = -1;
+    R->tr.successful_length = R->tr.unreported_length = -1;
+  } else {
+    R->tr.code = 200;
+    C->segments_out += R->nseg;
+    C->reports_out += R->nrep;
+  }
+}
+
+/* ================================================================== threads */
+typedef struct {
+  batch* B;
+  int tid;
+} targ;
+
+static void* worker(void* arg) {
+  targ* A = (targ*)arg;
+  batch* B = A->B;
+  ws w;
+  memset(&w, 0, sizeof w);
+  const size_t nn = (size_t)B->g->h.n_nodes;
+  w.dist = (float*)malloc(sizeof(float) * nn);
+  w.pred = (int32_t*)malloc(sizeof(int32_t) * nn);
+  w.lab = (uint32_t*)calloc(nn, sizeof(uint32_t));
+  w.done = (uint32_t*)calloc(nn, sizeof(uint32_t));
+  orc_counters* C = &B->ctr[A->tid];
+  while (1) {
+    int t = atomic_fetch_add(&B->next, 1);
+    if (t >= B->n_traces) break;
+    if (B->phase == 0) phase_a(B, &w, t, C);
+    else phase_b(B, &w, t, C);
+  }
+  free(w.dist);
+  free(w.pred);
+  free(w.lab);
+  free(w.done);
+  free(w.heap);
+  return NULL;
+}
+
+static void run_phase(batch* B, int phase, int nthreads) {
+  B->phase = phase;
+  atomic_store(&B->next, 0);
+  if (nthreads <= 1) {
+    targ a = {B, 0};
+    worker(&a);
+    return;
+  }
+  pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * (size_t)nthreads);
+  targ* args = (targ*)malloc(sizeof(targ) * (size_t)nthreads);
+  for (int i = 0; i < nthreads; ++i) {
+    args[i].B = B;
+    args[i].tid = i;
+    pthread_create(&th[i], NULL, worker, &args[i]);
+  }
+  for (int i = 0; i < nthreads; ++i) pthread_join(th[i], NULL);
+  free(th);
+  free(args);
+}
+
+int orc_match_batch(const orc_graph* g, const orc_params* p, const orc_report_cfg* rc, int32_t n_traces,
+                    const int64_t* trace_off, const float* lat, const float* lon, const double* time,
+                    const float* accuracy, int nthreads, int keep_stages, orc_results* out) {
+  memset(out, 0, sizeof *out);
+  if (p->max_candidates < 1 || p->max_candidates > ORC_KMAX) return -1;
+  if (nthreads < 1) nthreads = 1;
+  const int64_t P = trace_off[n_traces];
+  batch B;
+  memset(&B, 0, sizeof B);
+  B.g = g;
+  B.P = p;
+  B.rc = rc;
+  B.n_traces = n_traces;
+  B.toff_pts = trace_off;
+  B.lat = lat;
+  B.lon = lon;
+  B.time = time;
+  B.acc = accuracy;
+  const size_t PP = (size_t)P + 1;
+  B.is_col = (uint8_t*)calloc(PP, 1);
+  B.chain_start = (uint8_t*)calloc(PP, 1);
+  B.ncand = (int32_t*)calloc(PP, 4);
+  B.cand_edge = (int32_t*)calloc(PP * ORC_KMAX, 4);
+  B.cand_off = (float*)calloc(PP * ORC_KMAX, 4);
+  B.cand_emis = (float*)calloc(PP * ORC_KMAX, 4);
+  B.state = (int32_t*)calloc(PP, 4);
+  B.col_prev = (int32_t*)calloc(PP, 4);
+  B.route_dist = (float*)calloc(PP, 4);
+  B.gc = (float*)calloc(PP, 4);
+  B.terr = (int32_t*)calloc((size_t)n_traces + 1, 4);
+  B.trans_off = (int64_t*)calloc(PP, 8);
+  B.res = (tres*)calloc((size_t)n_traces + 1, sizeof(tres));
+  B.ctr = (orc_counters*)calloc((size_t)nthreads, sizeof(orc_counters));
+  run_phase(&B, 0, nthreads);
+  /* transition matrix offsets, point order */
+  int64_t acc = 0;
+  for (int64_t q = 0; q < P; ++q) {
+    B.trans_off[q] = acc;
+    if (B.is_col[q] && B.col_prev[q] >= 0) acc += (int64_t)B.ncand[B.col_prev[q]] * B.ncand[q];
+  }
+  B.trans_off[P] = acc;
+  B.trans = (float*)malloc(sizeof(float) * (size_t)(acc + 1));
+  run_phase(&B, 1, nthreads);
+  /* gather */
+  out->n_traces = n_traces;
+  out->traces = (orc_trace_result*)calloc((size_t)n_traces + 1, sizeof(orc_trace_result));
+  int64_t ns = 0, nw = 0, nr = 0;
+  for (int32_t t = 0; t < n_traces; ++t) {
+    ns += B.res[t].nseg;
+    nw += B.res[t].nway;
+    nr += B.res[t].nrep;
+  }
+  out->segments = (orc_segment*)calloc((size_t)ns + 1, sizeof(orc_segment));
+  out->way_ids = (int64_t*)calloc((size_t)nw + 1, 8);
+  out->reports = (orc_report_rec*)calloc((size_t)nr + 1, sizeof(orc_report_rec));
+  ns = nw = nr = 0;
+  for (int32_t t = 0; t < n_traces; ++t) {
+    tres* R = &B.res[t];
+    out->traces[t] = R->tr;
+    out->traces[t].seg_off = (int32_t)ns;
+    out->traces[t].seg_cnt = R->nseg;
+    out->traces[t].rep_off = (int32_t)nr;
+    out->traces[t].rep_cnt = R->nrep;
+    for (int k = 0; k < R->nseg; ++k) {
+      out->segments[ns + k] = R->segs[k];
+      out->segments[ns + k].way_off += (int32_t)nw;
+    }
+    memcpy(out->way_ids + nw, R->ways, sizeof(int64_t) * (size_t)R->nway);
+    memcpy(out->reports + nr, R->reps, sizeof(orc_report_rec) * (size_t)R->nrep);
+    ns += R->nseg;
+    nw += R->nway;
+    nr += R->nrep;
+    free(R->segs);
+    free(R->ways);
+    free(R->reps);
+  }
+  out->n_segments = (int32_t)ns;
+  out->n_way_ids = (int32_t)nw;
+  out->n_reports = (int32_t)nr;
+  for (int i = 0; i < nthreads; ++i) {
+    const int64_t* s = (const int64_t*)&B.ctr[i];
+    int64_t* d = (int64_t*)&out->counters;
+    for (size_t k = 0; k < sizeof(orc_counters) / 8; ++k) d[k] += s[k];
+  }
+  out->n_points = P;
+  if (keep_stages) {
+    out->ncand = B.ncand;
+    out->cand_edge = B.cand_edge;
+    out->cand_off = B.cand_off;
+    out->cand_emis = B.cand_emis;
+    out->trans_off = B.trans_off;
+    out->trans = B.trans;
+    out->state = B.state;
+    out->col_prev = B.col_prev;
+    out->route_dist = B.route_dist;
+    out->gc = B.gc;
+  } else {
+    free(B.ncand);
+    free(B.cand_edge);
+    free(B.cand_off);
+    free(B.cand_emis);
+    free(B.trans_off);
+    free(B.trans);
+    free(B.state);
+    free(B.col_prev);
+    free(B.route_dist);
+    free(B.gc);
+  }
+  free(B.is_col);
+  free(B.chain_start);
+  free(B.terr);
+  free(B.res);
+  free(B.ctr);
+  return 0;
+}
+
+void orc_results_free(orc_results* r) {
+  free(r->traces);
+  free(r->segments);
+  free(r->reports);
+  free(r->way_ids);
+  free(r->ncand);
+  free(r->cand_edge);
+  free(r->cand_off);
+  free(r->cand_emis);
+  free(r->trans_off);
+  free(r->trans);
+  free(r->state);
+  free(r->col_prev);
+  free(r->route_dist);
+  free(r->gc);
+  memset(r, 0, sizeof *r);
+}
+
+/* ================================================================== JSON Match */
+static int num_of(const jv* v, double* d) {
+  if (!v || (v->t != JV_INT && v->t != JV_FLOAT)) return 0;
+  *d = v->t == JV_INT ? (double)v->i : v->d;
+  return 1;
+}
+
+/* segments JSON of one trace (key order of README.md:136) */
+static void write_segments(sbuf* out, const orc_results* r, int32_t t) {
+  const orc_trace_result* tr = &r->traces[t];
+  sb_puts(out, "{\"segments\":[");
+  for (int k = 0; k < tr->seg_cnt; ++k) {
+    const orc_segment* s = &r->segments[tr->seg_off + k];
+    if (k) sb_puts(out, ",");
+    sb_puts(out, "{");
+    if (s->segment_id >= 0) sb_printf(out, "\"segment_id\":%lld,", (long long)s->segment_id);
+    sb_puts(out, "\"way_ids\":[");
+    for (int w = 0; w < s->way_cnt; ++w) sb_printf(out, w ? ",%lld" : "%lld", (long long)r->way_ids[s->way_off + w]);
+    sb_puts(out, "],\"start_time\":");
+    if (s->flags & 1u) py_float_repr(out, s->start_time);
+    else sb_puts(out, "-1");
+    sb_puts(out, ",\"end_time\":");
+    if (s->flags & 2u) py_float_repr(out, s->end_time);
+    else sb_puts(out, "-1");
+    sb_printf(out, ",\"queue_length\":%d,\"length\":%d,\"internal\":%s,\"begin_shape_index\":%d,\"end_shape_index\":%d}",
+              s->queue_length, s->length, (s->flags & 4u) ? "true" : "false", s->begin_shape_index,
+              s->end_shape_index);
+  }
+  sb_puts(out, "]}");
+}
+
+int orc_match_dom(const orc_graph* g, const orc_params* p, const jv* req, sbuf* out, char** err) {
+  const jv* tr = jv_get(req, "trace");
+  if (!tr || tr->t != JV_ARR) {
+    *err = strdup("trace must be an array of points");
+    return 0;
+  }
+  const int64_t n = (int64_t)tr->n;
+  float* lat = (float*)malloc(sizeof(float) * (size_t)(n + 1));
+  float* lon = (float*)malloc(sizeof(float) * (size_t)(n + 1));
+  float* acc = (float*)malloc(sizeof(float) * (size_t)(n + 1));
+  double* tm = (double*)malloc(sizeof(double) * (size_t)(n + 1));
+  for (int64_t k = 0; k < n; ++k) {
+    const jv* pt = tr->items[k];
+    double la, lo, ti, ac;
+    if (!pt || pt->t != JV_OBJ || !num_of(jv_get(pt, "lat"), &la) || !num_of(jv_get(pt, "lon"), &lo) ||
+        !num_of(jv_get(pt, "time"), &ti)) {
+      char buf[128];
+      snprintf(buf, sizeof buf, "trace point %lld must have numeric lat, lon and time", (long long)k);
+      *err = strdup(buf);
+      free(lat);
+      free(lon);
+      free(acc);
+      free(tm);
+      return 0;
+    }
+    lat[k] = (float)la;
+    lon[k] = (float)lo;
+    tm[k] = ti;
+    acc[k] = num_of(jv_get(pt, "accuracy"), &ac) ? (float)ac : 0.0f;
+  }
+  int64_t off[2] = {0, n};
+  orc_report_cfg rc;
+  orc_report_cfg_default(&rc);
+  orc_results r;
+  orc_match_batch(g, p, &rc, 1, off, lat, lon, tm, acc, 1, 0, &r);
+  free(lat);
+  free(lon);
+  free(acc);
+  free(tm);
+  int ok = 1;
+  if (r.traces[0].code == 500 && r.traces[0].error_kind != TERR_ZERODIV) {
+    *err = strdup(terr_msg(r.traces[0].error_kind));
+    ok = 0;
+  } else {
+    write_segments(out, &r, 0);
+  }
+  orc_results_free(&r);
+  return ok;
+}
+
+/* ================================================================== JSON batch (CPU baseline) */
+typedef struct {
+  const orc_graph* g;
+  const orc_params* p;
+  const orc_report_cfg* rc;
+  int n;
+  const char* const* bodies;
+  const size_t* lens;
+  int* codes;
+  char** outs;
+  size_t* out_lens;
+  atomic_int next;
+} jbatch;
+
+static void* jworker(void* arg) {
+  jbatch* J = (jbatch*)arg;
+  while (1) {
+    int i = atomic_fetch_add(&J->next, 1);
+    if (i >= J->n) break;
+    J->codes[i] = orc_handle_request(J->g, J->p, J->rc, "/report", J->bodies[i], J->lens[i], &J->outs[i],
+                                     &J->out_lens[i]);
+  }
+  return NULL;
+}
+
+int orc_handle_batch(const orc_graph* g, const orc_params* p, const orc_report_cfg* rc, int n,
+                     const char* const* bodies, const size_t* lens, int nthreads, int* codes, char** outs,
+                     size_t* out_lens) {
+  jbatch J = {g, p, rc, n, bodies, lens, codes, outs, out_lens, 0};
+  if (nthreads < 1) nthreads = 1;
+  pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * (size_t)nthreads);
+  for (int i = 0; i < nthreads; ++i) pthread_create(&th[i], NULL, jworker, &J);
+  for (int i = 0; i < nthreads; ++i) pthread_join(th[i], NULL);
+  free(th);
+  return 0;
+}
+
+/* ================================================================== polyline6 */
+/* py/generate_test_trace.py:9-29 */
+int64_t orc_decode_polyline6(const char* enc, size_t len, double* out, int64_t max_pairs) {
+  int64_t prev[2] = {0, 0}, n = 0;
+  size_t i = 0;
+  while (i < len) {
+    int64_t ll[2] = {0, 0};
+    for (int j = 0; j < 2; ++j) {
+      int shift = 0;
+      int64_t byte = 0x20;
+      while (byte >= 0x20) {
+        if (i >= len) return -1;
+        byte = (int64_t)(unsigned char)enc[i++] - 63;
+        ll[j] |= (byte & 0x1f) << shift;
+        shift += 5;
+      }
+      ll[j] = prev[j] + ((ll[j] & 1) ? ~(ll[j] >> 1) : (ll[j] >> 1));
+      prev[j] = ll[j];
+    }
+    if (n < max_pairs) {
+      char buf[64];
+      const double inv = 1.0 / 1e6;
+      snprintf(buf, sizeof buf, "%.6f", (double)ll[1] * inv);
+      out[2 * n] = strtod(buf, NULL);
+      snprintf(buf, sizeof buf, "%.6f", (double)ll[0] * inv);
+      out[2 * n + 1] = strtod(buf, NULL);
+    }
+    ++n;
+  }
+  return n;
+}

@@ -247,6 +247,9 @@ int otm_get_stage_ms(otm_engine* eng, float* ms, int n);
 int otm_debug_fetch(otm_engine* eng, int what, void* dst, size_t bytes,
                     size_t* needed);
 int otm_kmax(void);
+/* Which HIP runtime this library is bound to ("<path> hip_runtime_version=N"):
+ * a host that also runs torch must load torch first so both share one. */
+const char* otm_runtime_info(void);
 
 /* --------------------------------------------------- synthetic inputs ---- */
 /* Harness tooling, not the hot path: the seeded synthetic road network and

@@ -1,0 +1,504 @@
+// abi.cpp -- the extern "C" surface of libotmatch.so (include/otmatch.h).
+#include <dlfcn.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <sstream>
+
+#include "engine.h"
+#include "json.h"
+#include "report.h"
+
+using otm::json::Kind;
+using otm::json::Value;
+
+namespace {
+
+thread_local std::string t_err;
+
+int fail(int code, const std::string& msg) {
+  t_err = msg;
+  otm::set_thread_error(msg);
+  return code;
+}
+
+char* dup_out(const std::string& s, size_t* n) {
+  char* p = (char*)std::malloc(s.size() + 1);
+  std::memcpy(p, s.data(), s.size());
+  p[s.size()] = 0;
+  if (n) *n = s.size();
+  return p;
+}
+
+bool read_file(const char* path, std::string* out) {
+  std::ifstream f(path, std::ios::binary);
+  if (!f) return false;
+  std::stringstream ss;
+  ss << f.rdbuf();
+  *out = ss.str();
+  return true;
+}
+
+void fill_device_params(otm_engine* E) {
+  const otm::MatchConfig& m = E->mc;
+  E->dp.sigma_z = m.sigma_z;
+  E->dp.beta = m.beta;
+  E->dp.factor = m.max_route_distance_factor;
+  E->dp.breakage = m.breakage_distance;
+  E->dp.interp = m.interpolation_distance;
+  E->dp.search_radius = m.search_radius;
+  E->dp.max_search_radius = m.max_search_radius;
+  E->dp.gps_accuracy = m.gps_accuracy;
+  E->dp.max_candidates = m.max_candidates;
+  const otm::ReportConfig& r = E->rc;
+  std::memset(&E->drc, 0, sizeof E->drc);
+  E->drc.n_report = (int)std::min<size_t>(r.report_levels.size(), 16);
+  E->drc.n_transition = (int)std::min<size_t>(r.transition_levels.size(), 16);
+  for (int k = 0; k < E->drc.n_report; ++k) E->drc.report_levels[k] = r.report_levels[(size_t)k];
+  for (int k = 0; k < E->drc.n_transition; ++k) E->drc.transition_levels[k] = r.transition_levels[(size_t)k];
+  E->drc.threshold_sec = r.threshold_sec;
+}
+
+// One GPU batch over parsed requests: results[k] -> (code, body)
+void run_requests(otm_engine* E, std::vector<Value>& traces, std::vector<int>& codes, std::vector<std::string>& bodies,
+                  const std::vector<int>& todo, bool match_only) {
+  // points of every request that passed validation
+  std::vector<int64_t> off(1, 0);
+  std::vector<float> lat, lon, acc;
+  std::vector<double> tm;
+  std::vector<int> which;  // request index of each batch trace
+  for (int k : todo) {
+    otm::TracePoints tp;
+    std::string perr;
+    if (!otm::extract_points(traces[(size_t)k], &tp, &perr)) {
+      codes[(size_t)k] = 500;
+      bodies[(size_t)k] = otm::error_body(perr);
+      continue;
+    }
+    lat.insert(lat.end(), tp.lat.begin(), tp.lat.end());
+    lon.insert(lon.end(), tp.lon.begin(), tp.lon.end());
+    acc.insert(acc.end(), tp.acc.begin(), tp.acc.end());
+    tm.insert(tm.end(), tp.time.begin(), tp.time.end());
+    off.push_back((int64_t)lat.size());
+    which.push_back(k);
+  }
+  if (which.empty()) return;
+  otm_batch b;
+  b.n_traces = (int32_t)which.size();
+  b.n_points = off.back();
+  b.trace_off = off.data();
+  b.lat = lat.data();
+  b.lon = lon.data();
+  b.time = tm.data();
+  b.accuracy = acc.data();
+  std::string err;
+  otm_results r;
+  int rc;
+  {
+    std::lock_guard<std::mutex> lk(E->mu);
+    (void)hipSetDevice(E->device);
+    rc = otm::engine_match_host(E, &b, &err);
+    if (!rc) rc = otm::engine_fetch(E, &r, &err);
+    if (!rc) {
+      for (size_t n = 0; n < which.size(); ++n) {
+        const int k = which[n];
+        std::string out;
+        if (match_only) {
+          const otm_trace_result& tr = r.traces[n];
+          if (tr.code != 200 && tr.error_kind != OTM_TERR_ZERODIV) {
+            codes[(size_t)k] = 500;
+            bodies[(size_t)k] = otm::error_body(otm::trace_error_text(tr.error_kind));
+          } else {
+            otm::write_match_json(r, (int32_t)n, &out);
+            codes[(size_t)k] = 200;
+            bodies[(size_t)k] = std::move(out);
+          }
+        } else {
+          codes[(size_t)k] = otm::write_report_response(r, (int32_t)n, &out);
+          bodies[(size_t)k] = std::move(out);
+          const int inv = r.traces[n].code == 200 ? r.traces[n].invalid_speeds : 0;
+          for (int q = 0; q < inv; ++q) std::fputs("Speed exceeds 200kph\n", stderr);
+        }
+      }
+    }
+  }
+  if (rc) {
+    // a device failure fails the batch, not the process (500 like :239-240)
+    for (int k : which) {
+      codes[(size_t)k] = 500;
+      bodies[(size_t)k] = otm::error_body(err);
+    }
+  }
+}
+
+void report_many(otm_engine* E, int n, const char* const* reqs, const size_t* lens, int* codes, char** resps,
+                 size_t* resp_lens) {
+  std::vector<Value> traces((size_t)n);
+  std::vector<int> c((size_t)n, 0);
+  std::vector<std::string> bodies((size_t)n);
+  std::vector<int> todo;
+  for (int k = 0; k < n; ++k) {
+    int code = otm::parse_request("/report", std::string_view(reqs[k], lens[k]), &traces[(size_t)k],
+                                  &bodies[(size_t)k]);
+    if (code) c[(size_t)k] = code;
+    else todo.push_back(k);
+  }
+  run_requests(E, traces, c, bodies, todo, false);
+  for (int k = 0; k < n; ++k) {
+    codes[k] = c[(size_t)k];
+    resps[k] = dup_out(bodies[(size_t)k], &resp_lens[k]);
+  }
+}
+
+void worker_loop(otm_engine* E) {
+  while (true) {
+    std::vector<otm_engine::Pending> batch;
+    {
+      std::unique_lock<std::mutex> lk(E->qmu);
+      E->qcv.wait(lk, [&] { return E->stop || !E->queue.empty(); });
+      if (E->stop && E->queue.empty()) return;
+      while (!E->queue.empty() && batch.size() < 65536) {
+        batch.push_back(std::move(E->queue.front()));
+        E->queue.pop_front();
+      }
+    }
+    const int n = (int)batch.size();
+    std::vector<const char*> reqs((size_t)n);
+    std::vector<size_t> lens((size_t)n), rl((size_t)n);
+    std::vector<int> codes((size_t)n);
+    std::vector<char*> resps((size_t)n);
+    for (int k = 0; k < n; ++k) {
+      reqs[(size_t)k] = batch[(size_t)k].body.data();
+      lens[(size_t)k] = batch[(size_t)k].body.size();
+    }
+    report_many(E, n, reqs.data(), lens.data(), codes.data(), resps.data(), rl.data());
+    {
+      std::lock_guard<std::mutex> lk(E->qmu);
+      for (int k = 0; k < n; ++k)
+        E->done.push_back(otm_result{batch[(size_t)k].tag, codes[(size_t)k], resps[(size_t)k], rl[(size_t)k]});
+    }
+    E->qcv.notify_all();
+  }
+}
+
+// Java DecimalFormat("###.######", HALF_EVEN) of a float widened to double
+// (Point.java:29,41-42).  "###" sets no minimum integer digit, so |x| < 1
+// prints without its leading zero (".5", "-.5"); a value that rounds to zero
+// prints "0" (with the sign of a negative input).  No JVM exists here to pin
+// this against: the rules are DecimalFormat's documented behaviour.
+void java_decimal6(float f, std::string* o) {
+  char buf[64];
+  std::snprintf(buf, sizeof buf, "%.6f", (double)f);  // exact binary value, half-even
+  std::string s(buf);
+  const bool neg = s[0] == '-';
+  std::string mag = neg ? s.substr(1) : s;
+  size_t end = mag.size();
+  while (end > 0 && mag[end - 1] == '0') --end;
+  if (end > 0 && mag[end - 1] == '.') --end;
+  mag.resize(end);
+  if (mag.size() > 1 && mag[0] == '0' && mag[1] == '.') mag = mag.substr(1);
+  if (neg) o->push_back('-');
+  o->append(mag);
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* otm_last_error(const otm_engine*) { return t_err.empty() ? otm::thread_error() : t_err.c_str(); }
+
+void otm_free(void* p) { std::free(p); }
+
+int otm_kmax(void) { return otm::KMAX; }
+
+const char* otm_runtime_info(void) {
+  static thread_local std::string info;
+  Dl_info di;
+  int ver = 0;
+  (void)hipRuntimeGetVersion(&ver);
+  const char* path = dladdr((void*)&hipRuntimeGetVersion, &di) && di.dli_fname ? di.dli_fname : "?";
+  info = std::string(path) + " hip_runtime_version=" + std::to_string(ver);
+  return info.c_str();
+}
+
+int otm_engine_create(const char* cfg_path, const int* devices, int ndev, otm_engine** out) {
+  if (!out) return fail(OTM_EINVAL, "out is NULL");
+  *out = nullptr;
+  if (ndev != 1 || !devices) return fail(OTM_EINVAL, "exactly one device per engine (one engine per GPU process)");
+  std::string text;
+  if (!cfg_path || !read_file(cfg_path, &text)) return fail(OTM_EINVAL, std::string("cannot read config ") + (cfg_path ? cfg_path : "(null)"));
+  Value cfg;
+  std::string perr;
+  if (!otm::json::parse(text, &cfg, &perr)) return fail(OTM_EINVAL, "config: " + perr);
+  const Value* o = cfg.get("otm");
+  const Value* gp = o ? o->get("graph") : nullptr;
+  if (!gp || gp->kind != Kind::Str) return fail(OTM_EINVAL, "config: otm.graph (path) is required");
+  std::string graph = gp->s;
+  if (!graph.empty() && graph[0] != '/') {
+    std::string c(cfg_path);
+    const size_t sl = c.rfind('/');
+    if (sl != std::string::npos) graph = c.substr(0, sl + 1) + graph;
+  }
+  auto* E = new otm_engine();
+  const Value* meili = cfg.get("meili");
+  const Value* dflt = meili ? meili->get("default") : nullptr;
+  if (dflt && dflt->kind == Kind::Obj) {
+    auto getf = [&](const char* k, float* dst) {
+      const Value* v = dflt->get(k);
+      if (v && v->is_num()) *dst = (float)v->num();
+    };
+    getf("sigma_z", &E->mc.sigma_z);
+    getf("beta", &E->mc.beta);
+    getf("max_route_distance_factor", &E->mc.max_route_distance_factor);
+    getf("breakage_distance", &E->mc.breakage_distance);
+    getf("interpolation_distance", &E->mc.interpolation_distance);
+    getf("search_radius", &E->mc.search_radius);
+    getf("max_search_radius", &E->mc.max_search_radius);
+    getf("gps_accuracy", &E->mc.gps_accuracy);
+    const Value* mk = dflt->get("max_candidates");
+    if (mk && mk->kind == Kind::Int) E->mc.max_candidates = (int)mk->i;
+  }
+  if (E->mc.max_candidates < 1 || E->mc.max_candidates > otm::KMAX) {
+    delete E;
+    return fail(OTM_EINVAL, "max_candidates must be in [1, 32]");
+  }
+  std::string err;
+  if (!otm::read_report_env(&E->rc, &err)) {
+    delete E;
+    return fail(OTM_ECONFIG, err);
+  }
+  fill_device_params(E);
+  int rc = otm::engine_init(E, graph.c_str(), devices[0], &err);
+  if (rc) {
+    otm::engine_free(E);
+    delete E;
+    return fail(rc, err);
+  }
+  *out = E;
+  return OTM_OK;
+}
+
+void otm_engine_destroy(otm_engine* E) {
+  if (!E) return;
+  if (E->worker_started) {
+    {
+      std::lock_guard<std::mutex> lk(E->qmu);
+      E->stop = true;
+    }
+    E->qcv.notify_all();
+    E->worker.join();
+    for (auto& r : E->done) std::free(r.body);
+  }
+  otm::engine_free(E);
+  delete E;
+}
+
+int otm_report(otm_engine* E, const char* req, size_t len, char** resp, size_t* resp_len) {
+  int code = 0;
+  const char* reqs[1] = {req};
+  report_many(E, 1, reqs, &len, &code, resp, resp_len);
+  return code;
+}
+
+int otm_report_batch(otm_engine* E, int n, const char* const* reqs, const size_t* lens, char** resps,
+                     size_t* resp_lens, int* codes) {
+  if (!E || n < 0) return fail(OTM_EINVAL, "bad arguments");
+  report_many(E, n, reqs, lens, codes, resps, resp_lens);
+  return OTM_OK;
+}
+
+int otm_match_json(otm_engine* E, const char* req, size_t len, char** resp, size_t* resp_len) {
+  std::vector<Value> traces(1);
+  std::vector<int> codes(1, 0);
+  std::vector<std::string> bodies(1);
+  std::string perr;
+  if (!otm::json::parse(std::string_view(req, len), &traces[0], &perr)) {
+    *resp = dup_out(otm::error_body(perr), resp_len);
+    return 500;
+  }
+  if (traces[0].kind != Kind::Obj) {
+    *resp = dup_out(otm::error_body("request must be a JSON object"), resp_len);
+    return 500;
+  }
+  run_requests(E, traces, codes, bodies, {0}, true);
+  *resp = dup_out(bodies[0], resp_len);
+  return codes[0];
+}
+
+int otm_report_segments(otm_engine* E, const char* req, size_t len, const char* match_json, size_t match_len,
+                        char** resp, size_t* resp_len) {
+  otm::ReportConfig rc;
+  if (E) {
+    rc = E->rc;
+  } else {
+    std::string err;
+    if (!otm::read_report_env(&rc, &err)) {
+      *resp = dup_out(otm::error_body(err), resp_len);
+      return 500;
+    }
+  }
+  Value trace;
+  std::string body;
+  int code = otm::parse_request("/report", std::string_view(req, len), &trace, &body);
+  if (code) {
+    *resp = dup_out(body, resp_len);
+    return code;
+  }
+  Value segs;
+  std::string perr;
+  if (!otm::json::parse(std::string_view(match_json, match_len), &segs, &perr)) {
+    *resp = dup_out(otm::error_body(perr), resp_len);
+    return 500;
+  }
+  std::string out, errtext, exc;
+  if (!otm::report_dom(rc, trace, &segs, &out, &errtext, &exc)) {
+    *resp = dup_out(otm::error_body(exc), resp_len);
+    return 500;
+  }
+  if (!errtext.empty()) std::fputs(errtext.c_str(), stderr);
+  *resp = dup_out(out, resp_len);
+  return 200;
+}
+
+int otm_submit(otm_engine* E, const char* req, size_t len, uint64_t tag) {
+  if (!E) return fail(OTM_EINVAL, "engine is NULL");
+  std::lock_guard<std::mutex> lk(E->qmu);
+  if (!E->worker_started) {
+    E->worker = std::thread(worker_loop, E);
+    E->worker_started = true;
+  }
+  if (E->queue.size() >= (1u << 22)) return fail(OTM_EAGAIN, "submit queue full");
+  E->queue.push_back(otm_engine::Pending{tag, std::string(req, len)});
+  E->qcv.notify_all();
+  return OTM_OK;
+}
+
+int otm_poll(otm_engine* E, otm_result* out, int max, int timeout_us) {
+  if (!E || max < 0) return fail(OTM_EINVAL, "bad arguments");
+  std::unique_lock<std::mutex> lk(E->qmu);
+  if (E->done.empty() && timeout_us > 0)
+    E->qcv.wait_for(lk, std::chrono::microseconds(timeout_us), [&] { return !E->done.empty(); });
+  int n = 0;
+  while (n < max && !E->done.empty()) {
+    out[n++] = E->done.front();
+    E->done.pop_front();
+  }
+  return n;
+}
+
+int otm_encode_request(const char* uuid, int n, const float* lat, const float* lon, const int64_t* time,
+                       const int32_t* accuracy, char** out, size_t* out_len) {
+  // Batch.java:52-61 + Point.java:39-45
+  std::string s;
+  s.reserve(9 + std::strlen(uuid) + 11 + (size_t)n * 72 + 2);
+  s.append("{\"uuid\":\"");
+  s.append(uuid);
+  s.append("\",\"trace\":[");
+  for (int k = 0; k < n; ++k) {
+    s.append("{\"lat\":");
+    java_decimal6(lat[k], &s);
+    s.append(",\"lon\":");
+    java_decimal6(lon[k], &s);
+    s.append(",\"time\":");
+    otm::json::put_int(time[k], &s);
+    s.append(",\"accuracy\":");
+    otm::json::put_int(accuracy[k], &s);
+    s.append("},");
+  }
+  // sb.replace(len-1, len+1, "]}"): the trailing ',' becomes "]}"; with no
+  // points the '[' itself is replaced (Batch.java:60)
+  s.pop_back();
+  s.append("]}");
+  *out = dup_out(s, out_len);
+  return OTM_OK;
+}
+
+int otm_match_soa(otm_engine* E, const otm_batch* in, otm_results* out) {
+  if (!E || !in || !out) return fail(OTM_EINVAL, "bad arguments");
+  std::lock_guard<std::mutex> lk(E->mu);
+  (void)hipSetDevice(E->device);
+  std::string err;
+  int rc = otm::engine_match_host(E, in, &err);
+  if (!rc) rc = otm::engine_fetch(E, out, &err);
+  return rc ? fail(rc, err) : OTM_OK;
+}
+
+int otm_match_device(otm_engine* E, const otm_batch* in, void* stream) {
+  if (!E || !in) return fail(OTM_EINVAL, "bad arguments");
+  std::lock_guard<std::mutex> lk(E->mu);
+  (void)hipSetDevice(E->device);
+  otm::DevBatch b;
+  b.n_traces = in->n_traces;
+  b.n_points = in->n_points;
+  b.trace_off = in->trace_off;
+  b.lat = in->lat;
+  b.lon = in->lon;
+  b.time = in->time;
+  b.acc = in->accuracy;
+  std::string err;
+  int rc = otm::engine_match(E, b, (hipStream_t)stream, &err);
+  return rc ? fail(rc, err) : OTM_OK;
+}
+
+int otm_fetch_results(otm_engine* E, otm_results* out) {
+  if (!E || !out) return fail(OTM_EINVAL, "bad arguments");
+  std::lock_guard<std::mutex> lk(E->mu);
+  std::string err;
+  int rc = otm::engine_fetch(E, out, &err);
+  return rc ? fail(rc, err) : OTM_OK;
+}
+
+int otm_hist_bind(otm_engine* E, void* dev_counts, int nbins, float bin_kph) {
+  if (!E) return fail(OTM_EINVAL, "engine is NULL");
+  if (dev_counts && (nbins < 1 || !(bin_kph > 0.0f))) return fail(OTM_EINVAL, "nbins >= 1 and bin_kph > 0");
+  std::lock_guard<std::mutex> lk(E->mu);
+  E->hist = (uint32_t*)dev_counts;
+  E->nbins = dev_counts ? nbins : 0;
+  E->bin_kph = bin_kph;
+  return OTM_OK;
+}
+
+int otm_graph_info(const otm_engine* E, int64_t* n_nodes, int64_t* n_edges, int64_t* n_segments) {
+  if (!E) return fail(OTM_EINVAL, "engine is NULL");
+  if (n_nodes) *n_nodes = E->host.h.n_nodes;
+  if (n_edges) *n_edges = E->host.h.n_edges;
+  if (n_segments) *n_segments = E->host.h.n_segments;
+  return OTM_OK;
+}
+
+int otm_set_counting(otm_engine* E, int on) {
+  if (!E) return fail(OTM_EINVAL, "engine is NULL");
+  E->counting = on != 0;
+  return OTM_OK;
+}
+
+int otm_get_counters(otm_engine* E, otm_work_counters* out) {
+  if (!E || !out) return fail(OTM_EINVAL, "bad arguments");
+  std::lock_guard<std::mutex> lk(E->mu);
+  return otm::engine_counters(E, out) ? fail(OTM_EDEVICE, "counter copy failed") : OTM_OK;
+}
+
+int otm_set_timing(otm_engine* E, int on) {
+  if (!E) return fail(OTM_EINVAL, "engine is NULL");
+  E->timing = on != 0;
+  return OTM_OK;
+}
+
+int otm_get_stage_ms(otm_engine* E, float* ms, int n) {
+  if (!E || !ms) return fail(OTM_EINVAL, "bad arguments");
+  for (int k = 0; k < n && k < 8; ++k) ms[k] = E->stage_ms[k];
+  return OTM_OK;
+}
+
+int otm_debug_fetch(otm_engine* E, int what, void* dst, size_t bytes, size_t* needed) {
+  if (!E) return fail(OTM_EINVAL, "engine is NULL");
+  std::lock_guard<std::mutex> lk(E->mu);
+  std::string err;
+  int rc = otm::engine_debug_fetch(E, what, dst, bytes, needed, &err);
+  return rc ? fail(rc, err) : OTM_OK;
+}
+
+}  // extern "C"

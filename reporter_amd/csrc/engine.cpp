@@ -1,0 +1,408 @@
+// engine.cpp -- graph upload and per-batch orchestration of the kernels.
+//
+// Stands in for valhalla.Configure (py/reporter_service.py:279: load tiles
+// once) and for one SegmentMatcher per worker (:52): here one engine per GPU
+// holds the flattened graph in HBM and matches whole batches of traces.
+#include "engine.h"
+
+#include <cstring>
+
+namespace otm {
+
+#define HIPCHK(x)                                                              \
+  do {                                                                         \
+    hipError_t e_ = (x);                                                       \
+    if (e_ != hipSuccess) {                                                    \
+      *err = std::string(#x) + ": " + hipGetErrorString(e_);                   \
+      return OTM_EDEVICE;                                                      \
+    }                                                                          \
+  } while (0)
+
+static int ensure(otm_engine::Buf& b, size_t bytes, std::string* err) {
+  if (bytes == 0) bytes = 16;
+  if (b.cap >= bytes) return OTM_OK;
+  if (b.p) (void)hipFree(b.p);
+  b.p = nullptr;
+  b.cap = 0;
+  size_t want = bytes + bytes / 4;  // headroom against regrowth
+  HIPCHK(hipMalloc(&b.p, want));
+  b.cap = want;
+  return OTM_OK;
+}
+
+template <class T>
+static T* P(otm_engine::Buf& b) {
+  return (T*)b.p;
+}
+
+int engine_init(otm_engine* E, const char* graph_path, int device, std::string* err) {
+  int rc = load_graph(graph_path, &E->host, err);
+  if (rc) return rc;
+  E->device = device;
+  HIPCHK(hipSetDevice(device));
+  HIPCHK(hipStreamCreateWithFlags(&E->stream, hipStreamNonBlocking));
+  const otmg_header& h = E->host.h;
+  auto up = [&](int sec, const void** dst) -> int {
+    void* d = nullptr;
+    size_t n = h.sec[sec].bytes ? h.sec[sec].bytes : 16;
+    HIPCHK(hipMalloc(&d, n));
+    if (h.sec[sec].bytes) HIPCHK(hipMemcpy(d, E->host.section(sec), h.sec[sec].bytes, hipMemcpyHostToDevice));
+    E->graph_allocs.push_back(d);
+    *dst = d;
+    return OTM_OK;
+  };
+  DevGraph& g = E->g;
+  const void* tmp;
+#define UP(sec, field, T)                 \
+  if ((rc = up(sec, &tmp))) return rc;    \
+  g.field = (const T*)tmp;
+  UP(OTMG_NODE_LAT, node_lat, float);
+  UP(OTMG_NODE_LON, node_lon, float);
+  UP(OTMG_NODE_OUT_OFF, out_off, int32_t);
+  UP(OTMG_EDGE_FROM, e_from, int32_t);
+  UP(OTMG_EDGE_TO, e_to, int32_t);
+  UP(OTMG_EDGE_LEN, e_len, float);
+  UP(OTMG_EDGE_SHAPE_OFF, e_shape_off, int32_t);
+  UP(OTMG_EDGE_WAY, e_way, int64_t);
+  UP(OTMG_EDGE_SEG, e_seg, int32_t);
+  UP(OTMG_EDGE_SEG_POS, e_seg_pos, int32_t);
+  UP(OTMG_EDGE_FLAGS, e_flags, uint8_t);
+  UP(OTMG_SHAPE_LAT, s_lat, float);
+  UP(OTMG_SHAPE_LON, s_lon, float);
+  UP(OTMG_SHAPE_CUM, s_cum, float);
+  UP(OTMG_SEG_ID, g_id, uint64_t);
+  UP(OTMG_SEG_LEN, g_len, float);
+  UP(OTMG_CELL_OFF, cell_off, int64_t);
+  UP(OTMG_CELL_ENT, cell_ent, uint32_t);
+#undef UP
+  g.n_nodes = h.n_nodes;
+  g.n_edges = h.n_edges;
+  g.n_segments = h.n_segments;
+  g.grid_rows = h.grid_rows;
+  g.grid_cols = h.grid_cols;
+  g.lat0 = h.grid_lat0;
+  g.lon0 = h.grid_lon0;
+  g.cell = h.grid_cell_deg;
+  HIPCHK(hipMalloc((void**)&E->ctr, sizeof(DevCounters)));
+  HIPCHK(hipMalloc((void**)&E->ctr_save, sizeof(DevCounters)));
+  HIPCHK(hipMemset(E->ctr, 0, sizeof(DevCounters)));
+  for (auto& e : E->ev) HIPCHK(hipEventCreate(&e));
+  return OTM_OK;
+}
+
+void engine_free(otm_engine* E) {
+  if (E->device >= 0) (void)hipSetDevice(E->device);
+  for (void* p : E->graph_allocs) (void)hipFree(p);
+  E->graph_allocs.clear();
+  otm_engine::Buf* bufs[] = {&E->in_off,      &E->in_lat,      &E->in_lon,     &E->in_time,       &E->in_acc,
+                             &E->pt_trace,    &E->is_col,      &E->prevc,      &E->gc,            &E->ncand,
+                             &E->cand_edge,   &E->cand_off,    &E->cand_emis,  &E->col_prev,      &E->trans_off,
+                             &E->trans,       &E->bp,          &E->state,      &E->chain_start,   &E->route_dist,
+                             &E->path_off,    &E->path_len,    &E->path_pool,  &E->trace_err,     &E->overflow_list,
+                             &E->counters_i32, &E->scan_tmp,   &E->big_key,    &E->big_lab,       &E->big_inq,
+                             &E->big_fr,      &E->o_traces,    &E->o_seg_cnt,  &E->o_way_cnt,     &E->o_segments,
+                             &E->o_seg_gidx,  &E->o_way_ids,   &E->o_reports};
+  for (auto* b : bufs) {
+    if (b->p) (void)hipFree(b->p);
+    b->p = nullptr;
+    b->cap = 0;
+  }
+  if (E->ctr) (void)hipFree(E->ctr);
+  if (E->ctr_save) (void)hipFree(E->ctr_save);
+  E->ctr = E->ctr_save = nullptr;
+  for (auto& e : E->ev)
+    if (e) (void)hipEventDestroy(e);
+  if (E->stream) (void)hipStreamDestroy(E->stream);
+  E->stream = nullptr;
+}
+
+static int ensure_big(otm_engine* E, std::string* err) {
+  const size_t n = (size_t)BIG_SLOTS * BIG_TABLE_CAP;
+  int rc;
+  if ((rc = ensure(E->big_key, n * 4, err))) return rc;
+  if ((rc = ensure(E->big_lab, n * 8, err))) return rc;
+  if ((rc = ensure(E->big_inq, n * 4, err))) return rc;
+  if ((rc = ensure(E->big_fr, n * 8, err))) return rc;
+  return OTM_OK;
+}
+
+int engine_match(otm_engine* E, const DevBatch& b, hipStream_t s, std::string* err) {
+  if (!s) s = E->stream;
+  const int64_t NP = b.n_points;
+  const int32_t NT = b.n_traces;
+  const size_t Pn = (size_t)NP + 1;
+  int rc;
+#define ENS(buf, bytes) \
+  if ((rc = ensure(E->buf, (bytes), err))) return rc;
+  ENS(pt_trace, Pn * 4);
+  ENS(is_col, Pn);
+  ENS(prevc, Pn * 4);
+  ENS(gc, Pn * 4);
+  ENS(ncand, Pn * 4);
+  ENS(cand_edge, Pn * KMAX * 4);
+  ENS(cand_off, Pn * KMAX * 4);
+  ENS(cand_emis, Pn * KMAX * 4);
+  ENS(col_prev, Pn * 4);
+  ENS(trans_off, Pn * 8);
+  ENS(bp, Pn * KMAX);
+  ENS(state, Pn * 4);
+  ENS(chain_start, Pn);
+  ENS(route_dist, Pn * 4);
+  ENS(path_off, Pn * 4);
+  ENS(path_len, Pn * 4);
+  ENS(trace_err, ((size_t)NT + 1) * 4);
+  ENS(overflow_list, Pn * 4);
+  ENS(counters_i32, 64);
+  ENS(o_traces, ((size_t)NT + 1) * sizeof(otm_trace_result));
+  ENS(o_seg_cnt, ((size_t)NT + 1) * 4);
+  ENS(o_way_cnt, ((size_t)NT + 1) * 4);
+  ENS(scan_tmp, scan_tmp_bytes(NP > NT ? NP : NT) + 256);
+  if (E->pool_cap == 0) {
+    E->pool_cap = (int32_t)(Pn * 8 < (1u << 30) ? Pn * 8 : (1u << 30));
+  }
+  ENS(path_pool, (size_t)E->pool_cap * 4);
+
+  DevWork w{};
+  w.pt_trace = P<int32_t>(E->pt_trace);
+  w.is_col = P<uint8_t>(E->is_col);
+  w.prevc = P<int32_t>(E->prevc);
+  w.gc = P<float>(E->gc);
+  w.ncand = P<int32_t>(E->ncand);
+  w.cand_edge = P<int32_t>(E->cand_edge);
+  w.cand_off = P<float>(E->cand_off);
+  w.cand_emis = P<float>(E->cand_emis);
+  w.col_prev = P<int32_t>(E->col_prev);
+  w.trans_off = P<int64_t>(E->trans_off);
+  w.bp = P<uint8_t>(E->bp);
+  w.state = P<int32_t>(E->state);
+  w.chain_start = P<uint8_t>(E->chain_start);
+  w.route_dist = P<float>(E->route_dist);
+  w.path_off = P<int32_t>(E->path_off);
+  w.path_len = P<int32_t>(E->path_len);
+  w.path_pool = P<int32_t>(E->path_pool);
+  w.pool_cap = E->pool_cap;
+  w.trace_err = P<int32_t>(E->trace_err);
+  w.overflow_list = P<int32_t>(E->overflow_list);
+  w.counters_i32 = P<int32_t>(E->counters_i32);
+  w.ctr = E->counting ? E->ctr : nullptr;
+  if (E->counting) HIPCHK(hipMemsetAsync(E->ctr, 0, sizeof(DevCounters), s));
+  if (E->timing) HIPCHK(hipEventRecord(E->ev[0], s));
+
+  launch_columns(b, E->dp, w, s);
+  if (E->timing) HIPCHK(hipEventRecord(E->ev[1], s));
+  launch_candidates(E->g, b, E->dp, w, s);
+  if (E->timing) HIPCHK(hipEventRecord(E->ev[2], s));
+  launch_links(b, E->dp, w, s);
+  scan_i64(w.trans_off, NP, E->scan_tmp.p, E->scan_tmp.cap, s);
+  int64_t ttotal = 0;
+  HIPCHK(hipMemcpyAsync(&ttotal, w.trans_off + NP, 8, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemsetAsync(w.counters_i32, 0, 64, s));
+  HIPCHK(hipStreamSynchronize(s));
+  E->last_trans = ttotal;
+  ENS(trans, ((size_t)ttotal + 1) * 4);
+  w.trans = P<float>(E->trans);
+  if (E->timing) HIPCHK(hipEventRecord(E->ev[3], s));
+  launch_transitions(E->g, b, E->dp, w, 0, false, s);
+  int32_t nover = 0;
+  HIPCHK(hipMemcpyAsync(&nover, w.counters_i32, 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  if (nover > 0) {
+    if ((rc = ensure_big(E, err))) return rc;
+    w.big_key = P<uint32_t>(E->big_key);
+    w.big_lab = P<unsigned long long>(E->big_lab);
+    w.big_inq = P<uint32_t>(E->big_inq);
+    w.big_fr = P<uint32_t>(E->big_fr);
+    launch_transitions(E->g, b, E->dp, w, nover, true, s);
+  }
+  if (E->timing) HIPCHK(hipEventRecord(E->ev[4], s));
+  launch_viterbi(b, w, s);
+  if (E->timing) HIPCHK(hipEventRecord(E->ev[5], s));
+  // a path-pool overflow redoes the whole stage: restore the work counters
+  // so the redone searches are counted once
+  if (E->counting) HIPCHK(hipMemcpyAsync(E->ctr_save, E->ctr, sizeof(DevCounters), hipMemcpyDeviceToDevice, s));
+  for (int attempt = 0; attempt < 4; ++attempt) {
+    if (E->counting && attempt > 0)
+      HIPCHK(hipMemcpyAsync(E->ctr, E->ctr_save, sizeof(DevCounters), hipMemcpyDeviceToDevice, s));
+    HIPCHK(hipMemsetAsync(w.counters_i32, 0, 64, s));
+    launch_route(E->g, b, E->dp, w, 0, false, s);
+    int32_t cnt[3] = {0, 0, 0};
+    HIPCHK(hipMemcpyAsync(cnt, w.counters_i32, 12, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (cnt[0] > 0) {
+      if ((rc = ensure_big(E, err))) return rc;
+      w.big_key = P<uint32_t>(E->big_key);
+      w.big_lab = P<unsigned long long>(E->big_lab);
+      w.big_inq = P<uint32_t>(E->big_inq);
+      w.big_fr = P<uint32_t>(E->big_fr);
+      launch_route(E->g, b, E->dp, w, cnt[0], true, s);
+      HIPCHK(hipMemcpyAsync(cnt, w.counters_i32, 12, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipStreamSynchronize(s));
+    }
+    if (!cnt[2]) break;
+    // path pool too small: grow to what was requested and redo the stage
+    E->pool_cap = (int32_t)((size_t)cnt[1] * 2 + 1024);
+    ENS(path_pool, (size_t)E->pool_cap * 4);
+    w.path_pool = P<int32_t>(E->path_pool);
+    w.pool_cap = E->pool_cap;
+    if (attempt == 3) {
+      *err = "route path pool could not be sized";
+      return OTM_EDEVICE;
+    }
+  }
+  if (E->timing) HIPCHK(hipEventRecord(E->ev[6], s));
+
+  DevOut o{};
+  o.traces = E->o_traces.p;
+  o.seg_cnt = P<int32_t>(E->o_seg_cnt);
+  o.way_cnt = P<int32_t>(E->o_way_cnt);
+  o.hist = E->hist;
+  o.nbins = E->nbins;
+  o.bin_kph = E->bin_kph;
+  HIPCHK(hipMemsetAsync(o.seg_cnt + NT, 0, 4, s));
+  HIPCHK(hipMemsetAsync(o.way_cnt + NT, 0, 4, s));
+  launch_segments(E->g, b, w, o, false, s);
+  scan_i32(o.seg_cnt, NT, E->scan_tmp.p, E->scan_tmp.cap, s);
+  scan_i32(o.way_cnt, NT, E->scan_tmp.p, E->scan_tmp.cap, s);
+  int32_t tot[2] = {0, 0};
+  HIPCHK(hipMemcpyAsync(&tot[0], o.seg_cnt + NT, 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(&tot[1], o.way_cnt + NT, 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  ENS(o_segments, ((size_t)tot[0] + 1) * sizeof(otm_segment));
+  ENS(o_seg_gidx, ((size_t)tot[0] + 1) * 4);
+  ENS(o_reports, ((size_t)tot[0] + 1) * sizeof(otm_report_rec));
+  ENS(o_way_ids, ((size_t)tot[1] + 1) * 8);
+  o.segments = E->o_segments.p;
+  o.seg_gidx = P<int32_t>(E->o_seg_gidx);
+  o.reports = E->o_reports.p;
+  o.way_ids = P<int64_t>(E->o_way_ids);
+  launch_segments(E->g, b, w, o, true, s);
+  if (E->timing) HIPCHK(hipEventRecord(E->ev[7], s));
+  launch_report(b, E->drc, w, o, s);
+  if (E->timing) HIPCHK(hipEventRecord(E->ev[8], s));
+  HIPCHK(hipGetLastError());
+  E->last_T = NT;
+  E->last_P = NP;
+  E->last_S = tot[0];
+  E->last_W = tot[1];
+  if (E->timing) {
+    HIPCHK(hipEventSynchronize(E->ev[8]));
+    for (int k = 0; k < 8; ++k) HIPCHK(hipEventElapsedTime(&E->stage_ms[k], E->ev[k], E->ev[k + 1]));
+  }
+#undef ENS
+  return OTM_OK;
+}
+
+int engine_match_host(otm_engine* E, const otm_batch* in, std::string* err) {
+  const int32_t NT = in->n_traces;
+  if (NT < 0 || !in->trace_off) {
+    *err = "invalid batch";
+    return OTM_EINVAL;
+  }
+  const int64_t NP = in->trace_off[NT];
+  if (in->trace_off[0] != 0 || NP < 0 || (in->n_points && in->n_points != NP)) {
+    *err = "batch trace_off inconsistent with n_points";
+    return OTM_EINVAL;
+  }
+  for (int32_t t = 0; t < NT; ++t)
+    if (in->trace_off[t + 1] < in->trace_off[t]) {
+      *err = "batch trace_off not monotonic";
+      return OTM_EINVAL;
+    }
+  int rc;
+  if ((rc = ensure(E->in_off, ((size_t)NT + 1) * 8, err))) return rc;
+  if ((rc = ensure(E->in_lat, (size_t)NP * 4, err))) return rc;
+  if ((rc = ensure(E->in_lon, (size_t)NP * 4, err))) return rc;
+  if ((rc = ensure(E->in_time, (size_t)NP * 8, err))) return rc;
+  if ((rc = ensure(E->in_acc, (size_t)NP * 4, err))) return rc;
+  hipStream_t s = E->stream;
+  HIPCHK(hipMemcpyAsync(E->in_off.p, in->trace_off, ((size_t)NT + 1) * 8, hipMemcpyHostToDevice, s));
+  if (NP) {
+    HIPCHK(hipMemcpyAsync(E->in_lat.p, in->lat, (size_t)NP * 4, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(E->in_lon.p, in->lon, (size_t)NP * 4, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(E->in_time.p, in->time, (size_t)NP * 8, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(E->in_acc.p, in->accuracy, (size_t)NP * 4, hipMemcpyHostToDevice, s));
+  }
+  DevBatch b;
+  b.n_traces = NT;
+  b.n_points = NP;
+  b.trace_off = (const int64_t*)E->in_off.p;
+  b.lat = (const float*)E->in_lat.p;
+  b.lon = (const float*)E->in_lon.p;
+  b.time = (const double*)E->in_time.p;
+  b.acc = (const float*)E->in_acc.p;
+  return engine_match(E, b, s, err);
+}
+
+int engine_fetch(otm_engine* E, otm_results* out, std::string* err) {
+  hipStream_t s = E->stream;
+  const int32_t NT = E->last_T, NS = E->last_S, NW = E->last_W;
+  E->h_traces.resize((size_t)NT + 1);
+  E->h_segs.resize((size_t)NS + 1);
+  E->h_reps.resize((size_t)NS + 1);
+  E->h_ways.resize((size_t)NW + 1);
+  if (NT) HIPCHK(hipMemcpyAsync(E->h_traces.data(), E->o_traces.p, (size_t)NT * sizeof(otm_trace_result),
+                                hipMemcpyDeviceToHost, s));
+  if (NS) {
+    HIPCHK(hipMemcpyAsync(E->h_segs.data(), E->o_segments.p, (size_t)NS * sizeof(otm_segment), hipMemcpyDeviceToHost,
+                          s));
+    HIPCHK(hipMemcpyAsync(E->h_reps.data(), E->o_reports.p, (size_t)NS * sizeof(otm_report_rec),
+                          hipMemcpyDeviceToHost, s));
+  }
+  if (NW) HIPCHK(hipMemcpyAsync(E->h_ways.data(), E->o_way_ids.p, (size_t)NW * 8, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  // reports are written at their trace's segment offset; compact them
+  E->h_reps_dense.clear();
+  for (int32_t t = 0; t < NT; ++t) {
+    otm_trace_result& r = E->h_traces[t];
+    const int32_t base = r.rep_off;
+    r.rep_off = (int32_t)E->h_reps_dense.size();
+    for (int32_t k = 0; k < r.rep_cnt; ++k) E->h_reps_dense.push_back(E->h_reps[(size_t)base + k]);
+  }
+  out->n_traces = NT;
+  out->n_segments = NS;
+  out->n_reports = (int32_t)E->h_reps_dense.size();
+  out->n_way_ids = NW;
+  out->traces = E->h_traces.data();
+  out->segments = E->h_segs.data();
+  out->reports = E->h_reps_dense.data();
+  out->way_ids = E->h_ways.data();
+  return OTM_OK;
+}
+
+int engine_debug_fetch(otm_engine* E, int what, void* dst, size_t bytes, size_t* needed, std::string* err) {
+  const size_t Pn = (size_t)E->last_P;
+  const void* src = nullptr;
+  size_t n = 0;
+  switch (what) {
+    case 0: src = E->ncand.p; n = Pn * 4; break;
+    case 1: src = E->cand_edge.p; n = Pn * KMAX * 4; break;
+    case 2: src = E->cand_off.p; n = Pn * KMAX * 4; break;
+    case 3: src = E->cand_emis.p; n = Pn * KMAX * 4; break;
+    case 4: src = E->trans_off.p; n = (Pn + 1) * 8; break;
+    case 5: src = E->trans.p; n = (size_t)E->last_trans * 4; break;
+    case 6: src = E->state.p; n = Pn * 4; break;
+    case 7: src = E->col_prev.p; n = Pn * 4; break;
+    case 8: src = E->route_dist.p; n = Pn * 4; break;
+    case 9: src = E->gc.p; n = Pn * 4; break;
+    default: *err = "unknown debug buffer"; return OTM_EINVAL;
+  }
+  if (needed) *needed = n;
+  if (!dst) return OTM_OK;
+  if (bytes < n) {
+    *err = "debug buffer too small";
+    return OTM_EINVAL;
+  }
+  if (n) HIPCHK(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, E->stream));
+  HIPCHK(hipStreamSynchronize(E->stream));
+  return OTM_OK;
+}
+
+int engine_counters(otm_engine* E, otm_work_counters* out) {
+  DevCounters c;
+  if (hipMemcpy(&c, E->ctr, sizeof c, hipMemcpyDeviceToHost) != hipSuccess) return OTM_EDEVICE;
+  static_assert(sizeof(DevCounters) == sizeof(otm_work_counters), "counter layout");
+  std::memcpy(out, &c, sizeof c);
+  return OTM_OK;
+}
+
+}  // namespace otm

@@ -1,0 +1,89 @@
+// engine.h -- the otm_engine: one GPU, its HBM-resident graph, batch buffers.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <condition_variable>
+#include <deque>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "kernels.h"
+#include "otm_internal.h"
+#include "otmatch.h"
+
+struct otm_engine {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  otm::HostGraph host;
+  otm::DevGraph g{};
+  std::vector<void*> graph_allocs;
+  otm::MatchConfig mc;
+  otm::ReportConfig rc;
+  otm::DevParams dp{};
+  otm::DevReportCfg drc{};
+  std::mutex mu;  // one batch at a time per engine
+
+  struct Buf {
+    void* p = nullptr;
+    size_t cap = 0;
+  };
+  // batch inputs (host batches are staged here)
+  Buf in_off, in_lat, in_lon, in_time, in_acc;
+  // work
+  Buf pt_trace, is_col, prevc, gc, ncand, cand_edge, cand_off, cand_emis, col_prev, trans_off, trans, bp, state,
+      chain_start, route_dist, path_off, path_len, path_pool, trace_err, overflow_list, counters_i32, scan_tmp;
+  Buf big_key, big_lab, big_inq, big_fr;
+  // outputs
+  Buf o_traces, o_seg_cnt, o_way_cnt, o_segments, o_seg_gidx, o_way_ids, o_reports;
+  otm::DevCounters* ctr = nullptr;
+  otm::DevCounters* ctr_save = nullptr;
+  bool counting = false;
+  // histogram (caller-owned device memory)
+  uint32_t* hist = nullptr;
+  int nbins = 0;
+  float bin_kph = 5.0f;
+  // last batch
+  int32_t last_T = 0;
+  int64_t last_P = 0;
+  int32_t last_S = 0, last_W = 0;
+  int64_t last_trans = 0;
+  int32_t pool_cap = 0;
+  // host copies of the last fetched results
+  std::vector<otm_trace_result> h_traces;
+  std::vector<otm_segment> h_segs;
+  std::vector<otm_report_rec> h_reps, h_reps_dense;
+  std::vector<int64_t> h_ways;
+  // timing
+  bool timing = false;
+  hipEvent_t ev[9] = {};
+  float stage_ms[8] = {};
+  // async submit/poll
+  struct Pending {
+    uint64_t tag;
+    std::string body;
+  };
+  std::mutex qmu;
+  std::condition_variable qcv;
+  std::deque<Pending> queue;
+  std::deque<otm_result> done;
+  std::thread worker;
+  bool stop = false;
+  bool worker_started = false;
+};
+
+namespace otm {
+
+int engine_init(otm_engine* E, const char* graph_path, int device, std::string* err);
+void engine_free(otm_engine* E);
+// match a device-resident batch; returns 0 or OTM_EDEVICE (message in *err)
+int engine_match(otm_engine* E, const DevBatch& b, hipStream_t s, std::string* err);
+// stage a host batch to the device and match it
+int engine_match_host(otm_engine* E, const otm_batch* in, std::string* err);
+// copy results of the last batch to host vectors and describe them
+int engine_fetch(otm_engine* E, otm_results* out, std::string* err);
+int engine_debug_fetch(otm_engine* E, int what, void* dst, size_t bytes, size_t* needed, std::string* err);
+int engine_counters(otm_engine* E, otm_work_counters* out);
+
+}  // namespace otm

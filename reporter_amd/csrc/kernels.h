@@ -1,0 +1,140 @@
+// kernels.h -- device data views and launch wrappers of the matcher kernels.
+//
+// Pipeline of one batch, all on one HIP stream:
+//   K1 k_columns      thread / trace   interpolation filter, gc to previous column
+//   K2 k_candidates   wave / probe     grid cells -> projections -> LDS edge hash
+//                                      -> bitonic sort -> top-K + emission
+//   K3 k_links        thread / point   chain links + transition-matrix sizes, scan
+//   K4 k_transitions  wave / column    bounded label-correcting search per source
+//                                      node, frontier + labels in LDS (global
+//                                      tier on LDS overflow)
+//   K5 k_viterbi      wave / trace     min-sum decode, lanes = states
+//   K6 k_route        wave / step      re-run the winning search, predecessors
+//   K7 k_segments     thread / trace   traversals -> OSMLR segments (count+write)
+//   K8 k_report       thread / trace   reporter_service.py:110-215 + histogram
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace otm {
+
+constexpr int KMAX = 32;           // max candidates per column (== ORC_KMAX)
+constexpr int MAX_HITS = 256;      // distinct edges within one radius (spec limit)
+constexpr int SEARCH_LIMIT = 24576;  // nodes settled by one search (spec limit)
+constexpr int LDS_TABLE_CAP = 256;   // K4/K6 LDS tier: table slots
+constexpr int LDS_TABLE_LIMIT = 192; // ... nodes before spilling to the global tier
+constexpr int BIG_TABLE_CAP = 32768; // global tier table slots (> SEARCH_LIMIT / 0.75)
+constexpr int BIG_SLOTS = 128;       // concurrent global-tier searches
+
+struct DevGraph {
+  const float *node_lat, *node_lon;
+  const int32_t* out_off;
+  const int32_t *e_from, *e_to;
+  const float* e_len;
+  const int32_t* e_shape_off;
+  const int64_t* e_way;
+  const int32_t *e_seg, *e_seg_pos;
+  const uint8_t* e_flags;
+  const float *s_lat, *s_lon, *s_cum;
+  const uint64_t* g_id;
+  const float* g_len;
+  const int64_t* cell_off;
+  const uint32_t* cell_ent;
+  int32_t n_nodes, n_edges, n_segments, grid_rows, grid_cols;
+  double lat0, lon0, cell;
+};
+
+struct DevParams {
+  float sigma_z, beta, factor, breakage, interp, search_radius, max_search_radius, gps_accuracy;
+  int max_candidates;
+};
+
+struct DevReportCfg {
+  int n_report, n_transition;
+  int64_t report_levels[16];
+  int64_t transition_levels[16];
+  double threshold_sec;
+};
+
+struct DevBatch {
+  int32_t n_traces;
+  int64_t n_points;
+  const int64_t* trace_off;
+  const float *lat, *lon;
+  const double* time;
+  const float* acc;
+};
+
+// device counters, same order as otm_work_counters
+struct DevCounters {
+  unsigned long long points, columns, cells_visited, cell_entries_scanned;
+  unsigned long long edges_projected_unique, shape_points_projected, candidates;
+  unsigned long long searches, nodes_settled, edges_relaxed, transitions;
+  unsigned long long route_searches, route_edges, segments_out, reports_out;
+};
+
+// per-point / per-trace work arrays of one batch (device pointers)
+struct DevWork {
+  int32_t* pt_trace;     // [P] trace of point
+  uint8_t* is_col;       // [P]
+  int32_t* prevc;        // [P] previous column (unlinked), -1
+  float* gc;             // [P]
+  int32_t* ncand;        // [P]
+  int32_t* cand_edge;    // [P*KMAX]
+  float* cand_off;       // [P*KMAX]
+  float* cand_emis;      // [P*KMAX]
+  int32_t* col_prev;     // [P] linked previous column, -1
+  int64_t* trans_off;    // [P+1]
+  float* trans;          // [total]
+  uint8_t* bp;           // [P*KMAX]
+  int32_t* state;        // [P]
+  uint8_t* chain_start;  // [P]
+  float* route_dist;     // [P]
+  int32_t* path_off;     // [P]
+  int32_t* path_len;     // [P]
+  int32_t* path_pool;    // [pool_cap]
+  int32_t pool_cap;
+  int32_t* trace_err;    // [T]
+  int32_t* overflow_list;  // [P] points whose search spilled
+  int32_t* counters_i32;   // [0] overflow count, [1] pool used, [2] pool overflow flag
+  // global-tier scratch
+  uint32_t* big_key;
+  unsigned long long* big_lab;
+  uint32_t* big_inq;
+  uint32_t* big_fr;
+  DevCounters* ctr;        // nullptr when counting is off
+};
+
+struct DevOut {
+  // per trace
+  void* traces;          // otm_trace_result[T]
+  int32_t* seg_cnt;      // [T+1] counts -> scanned offsets
+  int32_t* way_cnt;      // [T+1]
+  // flat
+  void* segments;        // otm_segment[S]
+  int32_t* seg_gidx;     // [S] segment index in graph (-1 none)
+  int64_t* way_ids;      // [W]
+  void* reports;         // otm_report_rec[S] (capacity = segments)
+  uint32_t* hist;        // [n_segments * nbins] or nullptr
+  int nbins;
+  float bin_kph;
+};
+
+// ---- launch wrappers (kernels.hip)
+void launch_columns(const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s);
+void launch_candidates(const DevGraph& g, const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s);
+void launch_links(const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s);
+void launch_transitions(const DevGraph& g, const DevBatch& b, const DevParams& p, DevWork& w, int32_t n_overflow,
+                        bool big_tier, hipStream_t s);
+void launch_viterbi(const DevBatch& b, DevWork& w, hipStream_t s);
+void launch_route(const DevGraph& g, const DevBatch& b, const DevParams& p, DevWork& w, int32_t n_overflow,
+                  bool big_tier, hipStream_t s);
+void launch_segments(const DevGraph& g, const DevBatch& b, DevWork& w, DevOut& o, bool write, hipStream_t s);
+void launch_report(const DevBatch& b, const DevReportCfg& rc, DevWork& w, DevOut& o, hipStream_t s);
+// exclusive scan helpers (in place over n+1 elements: out[n] = total)
+void scan_i64(int64_t* d, int64_t n, void* tmp, size_t tmp_bytes, hipStream_t s);
+void scan_i32(int32_t* d, int64_t n, void* tmp, size_t tmp_bytes, hipStream_t s);
+size_t scan_tmp_bytes(int64_t n);
+
+}  // namespace otm

@@ -1,0 +1,1134 @@
+// kernels.hip -- the map-matching hot path as HIP kernels for gfx950 (CDNA4).
+//
+// Replaces valhalla.SegmentMatcher().Match (py/reporter_service.py:112) and
+// report() (:110-215).  Every float expression below follows the evaluation
+// order of the written spec (oracle/otm_oracle.c) and the file
+// is compiled with -ffp-contract=off, so results are bit-identical to the CPU
+// oracle: no FMA contraction, IEEE division and sqrt, and order-independent
+// fixed points (label-correcting search == Dijkstra, see K4).
+//
+// Execution model: wave64.  The irregular stages run one wavefront per unit
+// of work (probe, column pair, trace) in 64-thread workgroups, grid-striding,
+// with their working sets (edge hash, search labels, frontiers) in LDS.  No
+// stage is a dense contraction; MFMA is deliberately unused.  Graph arrays are
+// read-only and small enough (tens of MB at city scale) to live in L2 / the
+// 256 MB Infinity Cache after first touch.
+#include <hip/hip_runtime.h>
+
+#include <hipcub/hipcub.hpp>
+
+#include "kernels.h"
+#include "otmatch.h"
+
+namespace otm {
+
+namespace {
+
+#define MPD_F 111319.4954833f  // (float)(20037581.187 / 180), Batch.java:33
+constexpr uint32_t EMPTY = 0xFFFFFFFFu;
+constexpr unsigned long long LAB_NONE = ~0ull;
+constexpr int TB = 64;  // one wavefront per workgroup for the wave kernels
+
+__device__ __forceinline__ float cos_deg(float deg) {
+  const float x = deg * 0.017453292519943295f;
+  const float x2 = x * x;
+  float c = -1.1470745597729725e-11f;
+  c = c * x2 + 2.08767569878681e-09f;
+  c = c * x2 - 2.755731922398589e-07f;
+  c = c * x2 + 2.48015873015873e-05f;
+  c = c * x2 - 0.001388888888888889f;
+  c = c * x2 + 0.041666666666666664f;
+  c = c * x2 - 0.5f;
+  c = c * x2 + 1.0f;
+  return c;
+}
+
+__device__ __forceinline__ float gc_dist(float la, float lo, float lb, float lob) {
+  const float ls = MPD_F * cos_deg((la + lb) * 0.5f);
+  const float dx = (lob - lo) * ls;
+  const float dy = (lb - la) * MPD_F;
+  return sqrtf(dx * dx + dy * dy);
+}
+
+__device__ __forceinline__ void project(const DevGraph& g, int32_t e, int32_t k, float lat, float lon, float ls,
+                                        float& sqd, float& off_out) {
+  const int32_t a = g.e_shape_off[e] + k, b = a + 1;
+  const float ax = (g.s_lon[a] - lon) * ls;
+  const float ay = (g.s_lat[a] - lat) * MPD_F;
+  const float bx = (g.s_lon[b] - lon) * ls;
+  const float by = (g.s_lat[b] - lat) * MPD_F;
+  const float vx = bx - ax;
+  const float vy = by - ay;
+  const float l2 = vx * vx + vy * vy;
+  float t = 0.0f;
+  if (l2 > 0.0f) {
+    const float dot = ax * vx + ay * vy;
+    t = -dot / l2;
+    t = t < 0.0f ? 0.0f : (t > 1.0f ? 1.0f : t);
+  }
+  const float px = ax + t * vx;
+  const float py = ay + t * vy;
+  sqd = px * px + py * py;
+  float off = g.s_cum[a] + t * (g.s_cum[b] - g.s_cum[a]);
+  const float len = g.e_len[e];
+  off_out = off > len ? len : off;
+}
+
+__device__ __forceinline__ float probe_radius(const DevParams& P, float acc) {
+  const float a = acc > 0.0f ? acc : P.gps_accuracy;
+  const float r = a > P.search_radius ? a : P.search_radius;
+  return r < P.max_search_radius ? r : P.max_search_radius;
+}
+
+__device__ __forceinline__ uint32_t fbits(float f) { return __float_as_uint(f); }
+__device__ __forceinline__ float bitsf(uint32_t u) { return __uint_as_float(u); }
+__device__ __forceinline__ uint32_t hash32(uint32_t x) { return x * 2654435761u; }
+
+__device__ __forceinline__ void cadd(unsigned long long* c, unsigned long long v) {
+  if (c && v) atomicAdd(c, v);
+}
+
+// wave-wide inclusive scan of an int (64 lanes)
+__device__ __forceinline__ int wave_incl_scan(int v, int lane) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    int n = __shfl_up(v, o, 64);
+    if (lane >= o) v += n;
+  }
+  return v;
+}
+
+// ============================================================== K1 columns
+__global__ __launch_bounds__(256) void k_columns(DevBatch b, DevParams P, DevWork w) {
+  const int32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= b.n_traces) return;
+  const int64_t a = b.trace_off[t], e = b.trace_off[t + 1];
+  int64_t last = -1;
+  unsigned long long ncols = 0;
+  for (int64_t p = a; p < e; ++p) {
+    w.pt_trace[p] = t;
+    w.is_col[p] = 0;
+    w.prevc[p] = -1;
+    w.gc[p] = 0.0f;
+    float gcv = 0.0f;
+    if (last >= 0) {
+      gcv = gc_dist(b.lat[last], b.lon[last], b.lat[p], b.lon[p]);
+      if (!(gcv >= P.interp)) continue;
+    }
+    w.is_col[p] = 1;
+    w.gc[p] = gcv;
+    w.prevc[p] = (int32_t)last;
+    last = p;
+    ++ncols;
+  }
+  w.trace_err[t] = 0;
+  if (w.ctr) {
+    cadd(&w.ctr->points, (unsigned long long)(e - a));
+    cadd(&w.ctr->columns, ncols);
+  }
+}
+
+// ============================================================== K2 candidates
+constexpr int HCAP = 512;  // edge hash slots (>= 2 * MAX_HITS)
+
+__global__ __launch_bounds__(TB) void k_candidates(DevGraph g, DevBatch b, DevParams P, DevWork w) {
+  __shared__ uint32_t hkey[HCAP];
+  __shared__ unsigned long long hval[HCAP];
+  __shared__ unsigned long long skey[MAX_HITS];
+  __shared__ int64_t cstart[64];
+  __shared__ int cexcl[64];
+  __shared__ int s_count, s_over, s_n;
+  const int lane = threadIdx.x;
+  for (int64_t p = blockIdx.x; p < b.n_points; p += gridDim.x) {
+    if (!w.is_col[p]) {
+      if (lane == 0) w.ncand[p] = 0;
+      continue;
+    }
+    const float lat = b.lat[p], lon = b.lon[p];
+    const float r = probe_radius(P, b.acc[p]);
+    const float r2 = r * r;
+    const float ls = MPD_F * cos_deg(lat);
+    const float dlat = r / MPD_F;
+    const float dlon = r / ls;
+    const double la_lo = ((double)lat - (double)dlat - g.lat0) / g.cell;
+    const double la_hi = ((double)lat + (double)dlat - g.lat0) / g.cell;
+    const double lo_lo = ((double)lon - (double)dlon - g.lon0) / g.cell;
+    const double lo_hi = ((double)lon + (double)dlon - g.lon0) / g.cell;
+    const double R = g.grid_rows, Cn = g.grid_cols;
+    int r0 = 0, r1 = -1, c0 = 0, c1 = -1;
+    if (!(la_hi < 0.0 || lo_hi < 0.0 || la_lo >= R || lo_lo >= Cn)) {
+      r0 = la_lo < 0.0 ? 0 : (int)floor(la_lo);
+      r1 = la_hi >= R ? (int)R - 1 : (int)floor(la_hi);
+      c0 = lo_lo < 0.0 ? 0 : (int)floor(lo_lo);
+      c1 = lo_hi >= Cn ? (int)Cn - 1 : (int)floor(lo_hi);
+    }
+    const int ncols = c1 - c0 + 1;
+    const int ncells = (r1 - r0 + 1) * ncols;
+    for (int i = lane; i < HCAP; i += TB) {
+      hkey[i] = EMPTY;
+      hval[i] = LAB_NONE;
+    }
+    if (lane == 0) {
+      s_count = 0;
+      s_over = 0;
+      s_n = 0;
+    }
+    __syncthreads();
+    unsigned long long scanned = 0;
+    for (int cb = 0; cb < ncells; cb += TB) {
+      const int c = cb + lane;
+      int cnt = 0;
+      int64_t cs = 0;
+      if (c < ncells) {
+        const int rr = r0 + c / ncols, cc = c0 + c % ncols;
+        const size_t cidx = (size_t)rr * (size_t)g.grid_cols + (size_t)cc;
+        cs = g.cell_off[cidx];
+        cnt = (int)(g.cell_off[cidx + 1] - cs);
+      }
+      const int incl = wave_incl_scan(cnt, lane);
+      const int total = __shfl(incl, 63, 64);
+      cexcl[lane] = incl - cnt;
+      cstart[lane] = cs;
+      __syncthreads();
+      const int nc_here = min(TB, ncells - cb);
+      for (int gi = lane; gi < total; gi += TB) {
+        // cell holding entry gi: largest k with cexcl[k] <= gi
+        int lo = 0, hi = nc_here - 1;
+        while (lo < hi) {
+          const int mid = (lo + hi + 1) >> 1;
+          if (cexcl[mid] <= gi) lo = mid;
+          else hi = mid - 1;
+        }
+        const uint32_t ent = g.cell_ent[cstart[lo] + (gi - cexcl[lo])];
+        const int32_t e = (int32_t)(ent >> 4), k = (int32_t)(ent & 15u);
+        float sqd, off;
+        project(g, e, k, lat, lon, ls, sqd, off);
+        if (!(sqd <= r2)) continue;
+        uint32_t slot = hash32((uint32_t)e) >> (32 - 9);
+        bool placed = false;
+        for (int probe = 0; probe < HCAP; ++probe) {
+          const uint32_t old = atomicCAS(&hkey[slot], EMPTY, (uint32_t)e);
+          if (old == EMPTY) {
+            if (atomicAdd(&s_count, 1) >= MAX_HITS) s_over = 1;
+            placed = true;
+            break;
+          }
+          if (old == (uint32_t)e) {
+            placed = true;
+            break;
+          }
+          slot = (slot + 1) & (HCAP - 1);
+        }
+        if (!placed) {
+          s_over = 1;
+          continue;
+        }
+        atomicMin(&hval[slot], ((unsigned long long)fbits(sqd) << 32) | (unsigned long long)k);
+      }
+      scanned += (unsigned long long)total;
+      __syncthreads();
+    }
+    if (s_over) {
+      if (lane == 0) {
+        w.ncand[p] = 0;
+        atomicCAS(&w.trace_err[w.pt_trace[p]], 0, OTM_TERR_CAND_OVERFLOW);
+      }
+      __syncthreads();
+      continue;
+    }
+    // compact the distinct edges: key = sqdist bits << 32 | edge
+    for (int i = lane; i < HCAP; i += TB) {
+      if (hkey[i] != EMPTY) {
+        const int idx = atomicAdd(&s_n, 1);
+        skey[idx] = (hval[i] & 0xFFFFFFFF00000000ull) | (unsigned long long)hkey[i];
+      }
+    }
+    __syncthreads();
+    const int n = s_n;
+    int N = 1;
+    while (N < n) N <<= 1;
+    for (int i = n + lane; i < N; i += TB) skey[i] = LAB_NONE;
+    __syncthreads();
+    // bitonic sort ascending
+    for (int kk = 2; kk <= N; kk <<= 1) {
+      for (int j = kk >> 1; j > 0; j >>= 1) {
+        for (int i = lane; i < N; i += TB) {
+          const int ixj = i ^ j;
+          if (ixj > i) {
+            const unsigned long long x = skey[i], y = skey[ixj];
+            const bool up = (i & kk) == 0;
+            if ((x > y) == up) {
+              skey[i] = y;
+              skey[ixj] = x;
+            }
+          }
+        }
+        __syncthreads();
+      }
+    }
+    const int K = n < P.max_candidates ? n : P.max_candidates;
+    if (lane < K) {
+      const unsigned long long key = skey[lane];
+      const int32_t e = (int32_t)(key & 0xFFFFFFFFull);
+      uint32_t slot = hash32((uint32_t)e) >> (32 - 9);
+      while (hkey[slot] != (uint32_t)e) slot = (slot + 1) & (HCAP - 1);
+      const int32_t kseg = (int32_t)(hval[slot] & 15ull);
+      float sqd, off;
+      project(g, e, kseg, lat, lon, ls, sqd, off);
+      const float ds = (2.0f * P.sigma_z) * P.sigma_z;
+      w.cand_edge[p * KMAX + lane] = e;
+      w.cand_off[p * KMAX + lane] = off;
+      w.cand_emis[p * KMAX + lane] = sqd / ds;
+    }
+    if (lane == 0) {
+      w.ncand[p] = K;
+      if (w.ctr) {
+        cadd(&w.ctr->cells_visited, (unsigned long long)ncells);
+        cadd(&w.ctr->cell_entries_scanned, scanned);
+        cadd(&w.ctr->candidates, (unsigned long long)K);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// ============================================================== K3 links
+__global__ __launch_bounds__(256) void k_links(DevBatch b, DevParams P, DevWork w) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p > b.n_points) return;
+  if (p == b.n_points) {
+    w.trans_off[p] = 0;
+    return;
+  }
+  int32_t cp = -1;
+  int64_t cnt = 0;
+  if (w.is_col[p]) {
+    const int32_t q = w.prevc[p];
+    if (q >= 0 && w.ncand[p] > 0 && w.ncand[q] > 0 && w.gc[p] <= P.breakage) {
+      cp = q;
+      cnt = (int64_t)w.ncand[q] * (int64_t)w.ncand[p];
+    }
+  }
+  w.col_prev[p] = cp;
+  w.trans_off[p] = cnt;
+}
+
+// ============================================================== bounded search
+// Label-correcting single-source search in one wavefront.  Labels are 64-bit
+// (float distance bits << 32 | predecessor edge) updated with atomicMin, so
+// every label converges to the lexicographic minimum of (D(w)+len(e), e) over
+// in-edges: the unique fixed point, equal to what the oracle's Dijkstra (with
+// its (distance, edge) tie rule) computes, whatever the relaxation order.
+// Non-negative weights and monotone float rounding make "D(v) <= B" a
+// property of v alone, so the set of nodes ever inserted is exactly
+// {v : D(v) <= B} and the node count is order-independent too.
+struct Table {
+  uint32_t* key;            // node id or EMPTY
+  unsigned long long* lab;  // (dist bits << 32) | pred edge
+  uint32_t* inq;            // in next frontier
+  uint32_t* fr0;            // frontier A (slot ids)
+  uint32_t* fr1;            // frontier B
+  int cap_log2;
+  int limit;                // max nodes before overflow
+};
+
+template <bool BIG>
+struct Mem;
+template <>
+struct Mem<false> {  // LDS
+  template <class T>
+  __device__ static T ld(const T* p) {
+    return *p;
+  }
+  template <class T>
+  __device__ static void st(T* p, T v) {
+    *p = v;
+  }
+};
+template <>
+struct Mem<true> {  // global scratch: keep every access at L2 (agent scope)
+  template <class T>
+  __device__ static T ld(const T* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  template <class T>
+  __device__ static void st(T* p, T v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+};
+
+struct SearchShared {
+  int nfr, nnext, count, over;
+};
+
+template <bool BIG>
+__device__ __forceinline__ int table_find(const Table& T, uint32_t v) {
+  const uint32_t mask = (1u << T.cap_log2) - 1u;
+  uint32_t slot = hash32(v) >> (32 - T.cap_log2);
+  for (int i = 0; i <= (int)mask; ++i) {
+    const uint32_t k = Mem<BIG>::ld(&T.key[slot]);
+    if (k == v) return (int)slot;
+    if (k == EMPTY) return -1;
+    slot = (slot + 1) & mask;
+  }
+  return -1;
+}
+
+// returns >= 0 nodes settled, or -1 on overflow (more than T.limit nodes)
+template <bool BIG>
+__device__ int wave_search(const DevGraph& g, const Table& T, SearchShared& S, int32_t u, float B, int lane) {
+  const int cap = 1 << T.cap_log2;
+  const uint32_t mask = (uint32_t)cap - 1u;
+  for (int i = lane; i < cap; i += TB) {
+    Mem<BIG>::st(&T.key[i], EMPTY);
+    Mem<BIG>::st(&T.lab[i], LAB_NONE);
+    Mem<BIG>::st(&T.inq[i], 0u);
+  }
+  __syncthreads();
+  if (lane == 0) {
+    const uint32_t slot = hash32((uint32_t)u) >> (32 - T.cap_log2);
+    Mem<BIG>::st(&T.key[slot], (uint32_t)u);
+    Mem<BIG>::st(&T.lab[slot], ((unsigned long long)fbits(0.0f) << 32) | 0xFFFFFFFFull);
+    Mem<BIG>::st(&T.inq[slot], 1u);
+    Mem<BIG>::st(&T.fr0[0], slot);
+    S.nfr = 1;
+    S.count = 1;
+    S.over = 0;
+  }
+  __syncthreads();
+  uint32_t* cur = T.fr0;
+  uint32_t* nxt = T.fr1;
+  while (true) {
+    const int nfr = S.nfr;
+    if (nfr == 0) break;
+    if (lane == 0) S.nnext = 0;
+    __syncthreads();
+    for (int f = lane; f < nfr; f += TB) {
+      const uint32_t s = Mem<BIG>::ld(&cur[f]);
+      if (BIG) atomicExch(&T.inq[s], 0u);
+      else T.inq[s] = 0u;
+      const int32_t n = (int32_t)Mem<BIG>::ld(&T.key[s]);
+      const float d = bitsf((uint32_t)(Mem<BIG>::ld(&T.lab[s]) >> 32));
+      const int32_t e0 = g.out_off[n], e1 = g.out_off[n + 1];
+      for (int32_t e = e0; e < e1; ++e) {
+        const float nd = d + g.e_len[e];
+        if (!(nd <= B)) continue;
+        const uint32_t v = (uint32_t)g.e_to[e];
+        uint32_t slot = hash32(v) >> (32 - T.cap_log2);
+        int found = -1;
+        for (int i = 0; i < cap; ++i) {
+          const uint32_t old = atomicCAS(&T.key[slot], EMPTY, v);
+          if (old == EMPTY) {
+            if (atomicAdd(&S.count, 1) >= T.limit) S.over = 1;
+            found = (int)slot;
+            break;
+          }
+          if (old == v) {
+            found = (int)slot;
+            break;
+          }
+          slot = (slot + 1) & mask;
+        }
+        if (found < 0) {
+          S.over = 1;
+          continue;
+        }
+        const unsigned long long nl = ((unsigned long long)fbits(nd) << 32) | (unsigned long long)(uint32_t)e;
+        const unsigned long long old = atomicMin(&T.lab[found], nl);
+        if (nl < old && (uint32_t)(old >> 32) != fbits(nd)) {
+          if (atomicExch(&T.inq[found], 1u) == 0u) {
+            const int idx = atomicAdd(&S.nnext, 1);
+            Mem<BIG>::st(&nxt[idx], (uint32_t)found);
+          }
+        }
+      }
+    }
+    __syncthreads();
+    const bool over = S.over != 0;
+    if (lane == 0) S.nfr = S.nnext;
+    uint32_t* tmp = cur;
+    cur = nxt;
+    nxt = tmp;
+    __syncthreads();
+    if (over) return -1;
+  }
+  return S.count;
+}
+
+// edges relaxed by the equivalent Dijkstra = sum of out-degrees of settled nodes
+template <bool BIG>
+__device__ unsigned long long settled_outdeg(const DevGraph& g, const Table& T, int lane) {
+  unsigned long long s = 0;
+  const int cap = 1 << T.cap_log2;
+  for (int i = lane; i < cap; i += TB) {
+    const uint32_t k = Mem<BIG>::ld(&T.key[i]);
+    if (k != EMPTY) s += (unsigned long long)(g.out_off[k + 1] - g.out_off[k]);
+  }
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  return s;
+}
+
+// ============================================================== K4 transitions
+template <bool BIG>
+__global__ __launch_bounds__(TB) void k_transitions(DevGraph g, DevBatch b, DevParams P, DevWork w,
+                                                     int32_t n_overflow) {
+  __shared__ uint32_t lkey[BIG ? 1 : LDS_TABLE_CAP];
+  __shared__ unsigned long long llab[BIG ? 1 : LDS_TABLE_CAP];
+  __shared__ uint32_t linq[BIG ? 1 : LDS_TABLE_CAP];
+  __shared__ uint32_t lfr0[BIG ? 1 : LDS_TABLE_CAP];
+  __shared__ uint32_t lfr1[BIG ? 1 : LDS_TABLE_CAP];
+  __shared__ int32_t eq[KMAX], ep[KMAX];
+  __shared__ float oq[KMAX], op[KMAX];
+  __shared__ SearchShared S;
+  const int lane = threadIdx.x;
+  Table T;
+  if (BIG) {
+    const size_t base = (size_t)blockIdx.x * BIG_TABLE_CAP;
+    T = Table{w.big_key + base, w.big_lab + base, w.big_inq + base, w.big_fr + 2 * base,
+              w.big_fr + 2 * base + BIG_TABLE_CAP, 15, SEARCH_LIMIT};
+  } else {
+    T = Table{lkey, llab, linq, lfr0, lfr1, 8, LDS_TABLE_LIMIT};
+  }
+  const int64_t nwork = BIG ? (int64_t)n_overflow : b.n_points;
+  for (int64_t it = blockIdx.x; it < nwork; it += gridDim.x) {
+    const int64_t p = BIG ? (int64_t)w.overflow_list[it] : it;
+    const int32_t q = w.col_prev[p];
+    if (q < 0) continue;
+    const int Kq = w.ncand[q], Kp = w.ncand[p];
+    const float gcv = w.gc[p];
+    const float bound = P.factor * gcv;
+    if (lane < Kq) {
+      eq[lane] = w.cand_edge[(int64_t)q * KMAX + lane];
+      oq[lane] = w.cand_off[(int64_t)q * KMAX + lane];
+    }
+    if (lane < Kp) {
+      ep[lane] = w.cand_edge[p * KMAX + lane];
+      op[lane] = w.cand_off[p * KMAX + lane];
+    }
+    __syncthreads();
+    // distinct source nodes (first occurrence order)
+    const int32_t u_l = lane < Kq ? g.e_to[eq[lane]] : -1;
+    bool first = lane < Kq;
+    for (int k = 0; k < Kq; ++k) {
+      const int32_t uk = __shfl(u_l, k, 64);
+      if (k < lane && uk == u_l) first = false;
+    }
+    unsigned long long srcmask = __ballot(first);
+    float* Tm = w.trans + w.trans_off[p];
+    bool failed = false;
+    // work counts of this column, committed only if no search spilled (the
+    // global tier redoes every source of a spilled column)
+    unsigned long long c_search = 0, c_settled = 0, c_relaxed = 0, c_trans = 0;
+    while (srcmask) {
+      const int sl = __ffsll((long long)srcmask) - 1;
+      srcmask &= srcmask - 1;
+      const int32_t u = __shfl(u_l, sl, 64);
+      const int settled = wave_search<BIG>(g, T, S, u, bound, lane);
+      if (settled < 0) {
+        failed = true;
+        break;
+      }
+      unsigned long long ntr = 0;
+      for (int idx = lane; idx < Kq * Kp; idx += TB) {
+        const int i = idx / Kp, j = idx - (idx / Kp) * Kp;
+        if (g.e_to[eq[i]] != u) continue;
+        const float start = g.e_len[eq[i]] - oq[i];
+        float r;
+        bool ok = true;
+        if (ep[j] == eq[i] && op[j] >= oq[i]) {
+          r = op[j] - oq[i];
+        } else {
+          const int slot = table_find<BIG>(T, (uint32_t)g.e_from[ep[j]]);
+          if (slot < 0) {
+            ok = false;
+            r = 0.0f;
+          } else {
+            const float D = bitsf((uint32_t)(Mem<BIG>::ld(&T.lab[slot]) >> 32));
+            const float sd = start + D;
+            r = sd + op[j];
+          }
+        }
+        float cost = INFINITY;
+        if (ok && r <= bound) {
+          const float diff = fabsf(r - gcv);
+          cost = diff / P.beta;
+          ++ntr;
+        }
+        Tm[i * Kp + j] = cost;
+      }
+      if (w.ctr) {
+        const unsigned long long od = settled_outdeg<BIG>(g, T, lane);
+        for (int o = 32; o > 0; o >>= 1) ntr += __shfl_xor(ntr, o, 64);
+        c_search += 1;
+        c_settled += (unsigned long long)settled;
+        c_relaxed += od;
+        c_trans += ntr;
+      }
+      __syncthreads();
+    }
+    if (w.ctr && !failed && lane == 0) {
+      cadd(&w.ctr->searches, c_search);
+      cadd(&w.ctr->nodes_settled, c_settled);
+      cadd(&w.ctr->edges_relaxed, c_relaxed);
+      cadd(&w.ctr->transitions, c_trans);
+    }
+    if (failed && lane == 0) {
+      if (!BIG) {
+        const int slot = atomicAdd(&w.counters_i32[0], 1);
+        w.overflow_list[slot] = (int32_t)p;
+      } else {
+        atomicCAS(&w.trace_err[w.pt_trace[p]], 0, OTM_TERR_SEARCH_OVERFLOW);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// ============================================================== K5 viterbi
+__device__ __forceinline__ void wave_argmin(float v, int idx, float& bv, int& bi) {
+  // lexicographic (value, index) minimum over the wave; +inf never wins
+  bv = v;
+  bi = idx;
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ov = __shfl_xor(bv, o, 64);
+    const int oi = __shfl_xor(bi, o, 64);
+    if (ov < bv || (ov == bv && oi < bi)) {
+      bv = ov;
+      bi = oi;
+    }
+  }
+}
+
+__global__ __launch_bounds__(TB) void k_viterbi(DevBatch b, DevWork w) {
+  const int lane = threadIdx.x;
+  for (int32_t t = blockIdx.x; t < b.n_traces; t += gridDim.x) {
+    const int64_t a = b.trace_off[t], e = b.trace_off[t + 1];
+    for (int64_t p = a + lane; p < e; p += TB) {
+      w.state[p] = -1;
+      w.chain_start[p] = 0;
+    }
+    __syncthreads();
+    if (w.trace_err[t] != 0) continue;
+    float prev = INFINITY;
+    bool open = false;
+    int64_t last = -1;
+    auto backtrack = [&](int64_t endp) {
+      const int Ke = w.ncand[endp];
+      float bv;
+      int bi;
+      wave_argmin(lane < Ke ? prev : INFINITY, lane, bv, bi);
+      __syncthreads();
+      if (lane == 0) {
+        int64_t pp = endp;
+        int jj = bi;
+        while (true) {
+          w.state[pp] = jj;
+          if (w.chain_start[pp]) break;
+          jj = w.bp[pp * KMAX + jj];
+          pp = w.col_prev[pp];
+        }
+      }
+    };
+    for (int64_t p = a; p < e; ++p) {
+      if (!w.is_col[p]) continue;
+      const int Kp = w.ncand[p];
+      if (Kp == 0) {
+        if (open) backtrack(last);
+        open = false;
+        continue;
+      }
+      bool started = false;
+      float cur = INFINITY;
+      if (open && w.col_prev[p] == (int32_t)last) {
+        const int Kq = w.ncand[last];
+        const float* Tm = w.trans + w.trans_off[p];
+        float best = INFINITY;
+        int bi = -1;
+        for (int i = 0; i < Kq; ++i) {
+          const float pi = __shfl(prev, i, 64);
+          if (lane < Kp) {
+            const float v = pi + Tm[i * Kp + lane];
+            if (v < best) {
+              best = v;
+              bi = i;
+            }
+          }
+        }
+        const bool alive = lane < Kp && bi >= 0;
+        if (lane < Kp) {
+          cur = alive ? best + w.cand_emis[p * KMAX + lane] : INFINITY;
+          w.bp[p * KMAX + lane] = alive ? (uint8_t)bi : (uint8_t)0xFF;
+        }
+        if (__ballot(alive) == 0ull) {
+          backtrack(last);
+        } else {
+          started = true;
+        }
+      } else if (open) {
+        backtrack(last);
+      }
+      if (!started) {
+        cur = lane < Kp ? w.cand_emis[p * KMAX + lane] : INFINITY;
+        if (lane == 0) w.chain_start[p] = 1;
+      }
+      prev = cur;
+      open = true;
+      last = p;
+    }
+    __syncthreads();
+    if (open) backtrack(last);
+    __syncthreads();
+  }
+}
+
+// ============================================================== K6 route
+template <bool BIG>
+__global__ __launch_bounds__(TB) void k_route(DevGraph g, DevBatch b, DevParams P, DevWork w, int32_t n_overflow) {
+  __shared__ uint32_t lkey[BIG ? 1 : LDS_TABLE_CAP];
+  __shared__ unsigned long long llab[BIG ? 1 : LDS_TABLE_CAP];
+  __shared__ uint32_t linq[BIG ? 1 : LDS_TABLE_CAP];
+  __shared__ uint32_t lfr0[BIG ? 1 : LDS_TABLE_CAP];
+  __shared__ uint32_t lfr1[BIG ? 1 : LDS_TABLE_CAP];
+  __shared__ SearchShared S;
+  const int lane = threadIdx.x;
+  Table T;
+  if (BIG) {
+    const size_t base = (size_t)blockIdx.x * BIG_TABLE_CAP;
+    T = Table{w.big_key + base, w.big_lab + base, w.big_inq + base, w.big_fr + 2 * base,
+              w.big_fr + 2 * base + BIG_TABLE_CAP, 15, SEARCH_LIMIT};
+  } else {
+    T = Table{lkey, llab, linq, lfr0, lfr1, 8, LDS_TABLE_LIMIT};
+  }
+  const int64_t nwork = BIG ? (int64_t)n_overflow : b.n_points;
+  for (int64_t it = blockIdx.x; it < nwork; it += gridDim.x) {
+    const int64_t p = BIG ? (int64_t)w.overflow_list[it] : it;
+    if (!BIG) {
+      if (lane == 0) {
+        w.route_dist[p] = 0.0f;
+        w.path_len[p] = 0;
+        w.path_off[p] = 0;
+      }
+      if (w.state[p] < 0 || w.chain_start[p]) continue;
+    }
+    const int32_t q = w.col_prev[p];
+    const int i = w.state[q], j = w.state[p];
+    const int32_t ei = w.cand_edge[(int64_t)q * KMAX + i], ej = w.cand_edge[p * KMAX + j];
+    const float oi = w.cand_off[(int64_t)q * KMAX + i], oj = w.cand_off[p * KMAX + j];
+    if (ei == ej && oj >= oi) {
+      if (lane == 0) w.route_dist[p] = oj - oi;
+      continue;
+    }
+    const float bound = P.factor * w.gc[p];
+    const int32_t u = g.e_to[ei], v = g.e_from[ej];
+    const int settled = wave_search<BIG>(g, T, S, u, bound, lane);
+    if (settled < 0) {
+      if (lane == 0) {
+        if (!BIG) {
+          const int slot = atomicAdd(&w.counters_i32[0], 1);
+          w.overflow_list[slot] = (int32_t)p;
+        } else {
+          atomicCAS(&w.trace_err[w.pt_trace[p]], 0, OTM_TERR_SEARCH_OVERFLOW);
+        }
+      }
+      __syncthreads();
+      continue;
+    }
+    unsigned long long od = 0;
+    if (w.ctr) od = settled_outdeg<BIG>(g, T, lane);
+    if (lane == 0) {
+      const int vs = table_find<BIG>(T, (uint32_t)v);
+      const float D = bitsf((uint32_t)(Mem<BIG>::ld(&T.lab[vs]) >> 32));
+      int n = 0;
+      for (int32_t x = v; x != u;) {
+        const int sx = table_find<BIG>(T, (uint32_t)x);
+        const int32_t pe = (int32_t)(uint32_t)(Mem<BIG>::ld(&T.lab[sx]) & 0xFFFFFFFFull);
+        ++n;
+        x = g.e_from[pe];
+      }
+      const int off = atomicAdd(&w.counters_i32[1], n);
+      if (off + n > w.pool_cap) {
+        w.counters_i32[2] = 1;
+        w.path_len[p] = -1;
+      } else {
+        int k = n;
+        for (int32_t x = v; x != u;) {
+          const int sx = table_find<BIG>(T, (uint32_t)x);
+          const int32_t pe = (int32_t)(uint32_t)(Mem<BIG>::ld(&T.lab[sx]) & 0xFFFFFFFFull);
+          w.path_pool[off + (--k)] = pe;
+          x = g.e_from[pe];
+        }
+        w.path_off[p] = off;
+        w.path_len[p] = n;
+      }
+      const float start = g.e_len[ei] - oi;
+      const float sd = start + D;
+      w.route_dist[p] = sd + oj;
+      if (w.ctr) {
+        cadd(&w.ctr->searches, 1);
+        cadd(&w.ctr->route_searches, 1);
+        cadd(&w.ctr->nodes_settled, (unsigned long long)settled);
+        cadd(&w.ctr->edges_relaxed, od);
+        cadd(&w.ctr->route_edges, (unsigned long long)n);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// ============================================================== K7 segments
+struct Trav {
+  int32_t edge;
+  float off0, off1;
+  double t0, t1;
+  int32_t sh0, sh1;
+};
+
+template <bool WRITE>
+struct SegEmitter {
+  const DevGraph* g;
+  DevOut* o;
+  int32_t seg_base, way_base;  // write positions (WRITE)
+  int32_t nseg = 0, nway = 0;
+  // open group
+  bool has = false;
+  Trav first, last;
+  int32_t way_start = 0;
+  int64_t last_way = 0;
+
+  __device__ void add_way(int32_t edge) {
+    const int64_t way = g->e_way[edge];
+    if (nway > way_start && last_way == way) return;
+    if (WRITE) o->way_ids[way_base + nway] = way;
+    last_way = way;
+    ++nway;
+  }
+  __device__ void flush() {
+    if (!has) return;
+    if (WRITE) {
+      otm_segment s;
+      const int32_t sg = g->e_seg[first.edge];
+      bool sv, ev;
+      s.flags = 0u;
+      if (sg >= 0) {
+        sv = first.off0 == 0.0f && (g->e_flags[first.edge] & OTM_EDGE_SEG_BEGIN_D);
+        ev = last.off1 == g->e_len[last.edge] && (g->e_flags[last.edge] & OTM_EDGE_SEG_END_D);
+        s.segment_id = (int64_t)g->g_id[sg];
+        s.length = (sv && ev) ? (int32_t)floor((double)g->g_len[sg] + 0.5) : -1;
+      } else {
+        sv = first.off0 == 0.0f;
+        ev = last.off1 == g->e_len[last.edge];
+        s.segment_id = -1;
+        s.length = -1;
+        if (g->e_flags[first.edge] & OTM_EDGE_INTERNAL_D) s.flags |= OTM_SEG_INTERNAL;
+      }
+      s.start_time = 0.0;
+      s.end_time = 0.0;
+      if (sv) {
+        s.flags |= OTM_SEG_START_VALID;
+        s.start_time = first.t0;
+      }
+      if (ev) {
+        s.flags |= OTM_SEG_END_VALID;
+        s.end_time = last.t1;
+      }
+      s.queue_length = 0;
+      s.begin_shape_index = first.sh0;
+      s.end_shape_index = last.sh1;
+      s.way_off = way_base + way_start;
+      s.way_cnt = nway - way_start;
+      s.pad = 0u;
+      ((otm_segment*)o->segments)[seg_base + nseg] = s;
+      o->seg_gidx[seg_base + nseg] = sg;
+    }
+    ++nseg;
+    has = false;
+  }
+  __device__ void push(const Trav& t) {
+    bool join = false;
+    if (has) {
+      const int32_t e = t.edge, pe = last.edge;
+      const int32_t s = g->e_seg[e], ps = g->e_seg[pe];
+      if (s >= 0) join = ps == s && g->e_seg_pos[e] == g->e_seg_pos[pe] + 1;
+      else join = ps < 0 && ((g->e_flags[e] ^ g->e_flags[pe]) & OTM_EDGE_INTERNAL_D) == 0;
+    }
+    if (!join) {
+      flush();
+      has = true;
+      first = t;
+      way_start = nway;
+    }
+    last = t;
+    add_way(t.edge);
+  }
+  static constexpr uint8_t OTM_EDGE_INTERNAL_D = 0x01, OTM_EDGE_SEG_BEGIN_D = 0x02, OTM_EDGE_SEG_END_D = 0x04;
+};
+
+__device__ __forceinline__ double time_at(double ta, double tb, float x, float R) {
+  if (R > 0.0f) return ta + (tb - ta) * ((double)x / (double)R);
+  return ta;
+}
+
+template <bool WRITE>
+__global__ __launch_bounds__(256) void k_segments(DevGraph g, DevBatch b, DevWork w, DevOut o) {
+  const int32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= b.n_traces) return;
+  SegEmitter<WRITE> em;
+  em.g = &g;
+  em.o = &o;
+  em.seg_base = WRITE ? o.seg_cnt[t] : 0;
+  em.way_base = WRITE ? o.way_cnt[t] : 0;
+  const int err = w.trace_err[t];
+  if (err == 0) {
+    const int64_t a = b.trace_off[t], e = b.trace_off[t + 1];
+    bool open = false;
+    int nstate = 0;
+    Trav cur{};
+    int64_t lastp = -1;
+    for (int64_t p = a; p <= e; ++p) {
+      const bool is_state = p < e && w.is_col[p] && w.state[p] >= 0;
+      if (p < e && !is_state) continue;
+      const bool new_chain = p == e || w.chain_start[p];
+      if (open && new_chain) {
+        const int sl = w.state[lastp];
+        cur.off1 = w.cand_off[lastp * KMAX + sl];
+        cur.t1 = b.time[lastp];
+        cur.sh1 = (int32_t)(lastp - a);
+        if (nstate >= 2) {
+          em.push(cur);
+          em.flush();
+        }
+        open = false;
+      }
+      if (p == e) break;
+      const int j = w.state[p];
+      const int32_t ej = w.cand_edge[p * KMAX + j];
+      const float oj = w.cand_off[p * KMAX + j];
+      if (new_chain) {
+        cur.edge = ej;
+        cur.off0 = oj;
+        cur.t0 = b.time[p];
+        cur.sh0 = (int32_t)(p - a);
+        open = true;
+        nstate = 1;
+        lastp = p;
+        continue;
+      }
+      const float Rd = w.route_dist[p];
+      const double ta = b.time[lastp], tb = b.time[p];
+      const int32_t ca = (int32_t)(lastp - a), cb = (int32_t)(p - a);
+      const int32_t ei = cur.edge;
+      const float oi = w.cand_off[lastp * KMAX + w.state[lastp]];
+      const bool same = ei == ej && oj >= oi;
+      if (!same) {
+        const float start = g.e_len[ei] - oi;
+        float x = start;
+        cur.off1 = g.e_len[ei];
+        cur.t1 = time_at(ta, tb, x, Rd);
+        cur.sh1 = x >= Rd ? cb : ca;
+        em.push(cur);
+        float dd = 0.0f;
+        const int32_t po = w.path_off[p], pl = w.path_len[p];
+        for (int k = 0; k < pl; ++k) {
+          const int32_t pe = w.path_pool[po + k];
+          Trav m;
+          m.edge = pe;
+          m.off0 = 0.0f;
+          m.off1 = g.e_len[pe];
+          const float xb = start + dd;
+          dd = dd + g.e_len[pe];
+          const float xe = start + dd;
+          m.t0 = time_at(ta, tb, xb, Rd);
+          m.t1 = time_at(ta, tb, xe, Rd);
+          m.sh0 = xb >= Rd ? cb : ca;
+          m.sh1 = xe >= Rd ? cb : ca;
+          em.push(m);
+        }
+        x = start + dd;
+        cur.edge = ej;
+        cur.off0 = 0.0f;
+        cur.t0 = time_at(ta, tb, x, Rd);
+        cur.sh0 = x >= Rd ? cb : ca;
+      }
+      ++nstate;
+      lastp = p;
+    }
+  }
+  if (!WRITE) {
+    o.seg_cnt[t] = em.nseg;
+    o.way_cnt[t] = em.nway;
+  }
+}
+
+// ============================================================== K8 report
+__device__ __forceinline__ bool in_lv(const int64_t* lv, int n, int64_t x) {
+  for (int k = 0; k < n; ++k)
+    if (lv[k] == x) return true;
+  return false;
+}
+
+__global__ __launch_bounds__(256) void k_report(DevBatch b, DevReportCfg rc, DevWork w, DevOut o, int32_t n_seg_total) {
+  const int32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= b.n_traces) return;
+  otm_trace_result r;
+  r.code = 200;
+  r.error_kind = w.trace_err[t];
+  r.seg_off = o.seg_cnt[t];
+  r.seg_cnt = o.seg_cnt[t + 1] - o.seg_cnt[t];
+  r.rep_off = r.seg_off;
+  r.rep_cnt = 0;
+  r.shape_used = -1;
+  r.successful_count = r.unreported_count = r.discontinuities = r.invalid_speeds = r.unassociated = 0;
+  r.successful_length = r.unreported_length = -1;
+  const otm_segment* S = (const otm_segment*)o.segments + r.seg_off;
+  otm_report_rec* REP = (otm_report_rec*)o.reports + r.rep_off;
+  if (r.error_kind != 0) {
+    r.code = 500;
+    ((otm_trace_result*)o.traces)[t] = r;
+    return;
+  }
+  const double end_time = b.time[b.trace_off[t + 1] - 1];
+  auto ST = [&](const otm_segment& s) { return (s.flags & OTM_SEG_START_VALID) ? s.start_time : -1.0; };
+  auto ET = [&](const otm_segment& s) { return (s.flags & OTM_SEG_END_VALID) ? s.end_time : -1.0; };
+  int last_idx = r.seg_cnt - 1;
+  while (last_idx >= 0 && end_time - ST(S[last_idx]) < rc.threshold_sec) --last_idx;
+  r.shape_used = last_idx >= 0 ? S[last_idx].begin_shape_index : -1;
+  bool have = false, first = true;
+  int prior = -1;
+  int64_t prior_level = -1;
+  int nrep = 0;
+  bool zerodiv = false;
+  for (int idx = 0; idx <= last_idx; ++idx) {
+    const otm_segment& s = S[idx];
+    const bool internal = (s.flags & OTM_SEG_INTERNAL) != 0;
+    if (idx != 0 && ST(s) == -1.0 && ET(S[idx - 1]) == -1.0) r.discontinuities++;
+    const int64_t level = s.segment_id >= 0 ? (s.segment_id & 7) : -1;
+    if (have && S[prior].segment_id >= 0 && S[prior].length > 0 && !internal) {
+      const otm_segment& ps = S[prior];
+      if (in_lv(rc.report_levels, rc.n_report, prior_level)) {
+        const bool trans = in_lv(rc.transition_levels, rc.n_transition, level);
+        const double t0 = ST(ps);
+        const double t1 = trans ? ST(s) : ET(ps);
+        const double den = t1 - t0;
+        if (den == 0.0) {
+          zerodiv = true;
+          break;
+        }
+        const double speed = ((double)ps.length / den) * 3.6;
+        if (speed < 200.0) {
+          otm_report_rec rep;
+          rep.id = ps.segment_id;
+          rep.next_id = (trans && s.segment_id >= 0) ? s.segment_id : -1;
+          rep.t0 = t0;
+          rep.t1 = t1;
+          rep.flags = (trans && !(s.flags & OTM_SEG_START_VALID)) ? OTM_REP_T1_INT_MINUS1 : 0u;
+          rep.length = ps.length;
+          rep.queue_length = ps.queue_length;
+          rep.pad = 0u;
+          REP[nrep++] = rep;
+          r.successful_count++;
+          r.successful_length = ps.length;
+          if (o.hist && !(rep.flags & OTM_REP_T1_INT_MINUS1) && speed >= 0.0) {
+            const int32_t gi = o.seg_gidx[r.seg_off + prior];
+            if (gi >= 0) {
+              int bin = (int)(speed / (double)o.bin_kph);
+              bin = bin < 0 ? 0 : (bin >= o.nbins ? o.nbins - 1 : bin);
+              atomicAdd(&o.hist[(size_t)gi * o.nbins + bin], 1u);
+            }
+          }
+        } else {
+          r.invalid_speeds++;
+        }
+      } else {
+        r.unreported_count++;
+        r.unreported_length = ps.length;
+      }
+    }
+    if (!(internal && !first)) {
+      prior = idx;
+      prior_level = level;
+      have = true;
+    }
+    first = false;
+    if (s.segment_id < 0 && !internal) r.unassociated++;
+  }
+  if (zerodiv) {
+    r.code = 500;
+    r.error_kind = OTM_TERR_ZERODIV;
+    r.rep_cnt = 0;
+    r.shape_used = -1;
+    r.successful_count = r.unreported_count = r.discontinuities = r.invalid_speeds = r.unassociated = 0;
+    r.successful_length = r.unreported_length = -1;
+  } else {
+    r.rep_cnt = nrep;
+    if (w.ctr) {
+      cadd(&w.ctr->segments_out, (unsigned long long)r.seg_cnt);
+      cadd(&w.ctr->reports_out, (unsigned long long)nrep);
+    }
+  }
+  ((otm_trace_result*)o.traces)[t] = r;
+}
+
+int grid_for(int64_t n, int per_block, int cap) {
+  int64_t g = (n + per_block - 1) / per_block;
+  if (g < 1) g = 1;
+  return (int)(g > cap ? cap : g);
+}
+
+}  // namespace
+
+// ============================================================== launchers
+constexpr int WAVE_GRID_CAP = 256 * 64;  // grid-stride cap for wave kernels
+
+void launch_columns(const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s) {
+  hipLaunchKernelGGL(k_columns, dim3(grid_for(b.n_traces, 256, 1 << 30)), dim3(256), 0, s, b, p, w);
+}
+void launch_candidates(const DevGraph& g, const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s) {
+  hipLaunchKernelGGL(k_candidates, dim3(grid_for(b.n_points, 1, WAVE_GRID_CAP)), dim3(TB), 0, s, g, b, p, w);
+}
+void launch_links(const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s) {
+  hipLaunchKernelGGL(k_links, dim3(grid_for(b.n_points + 1, 256, 1 << 30)), dim3(256), 0, s, b, p, w);
+}
+void launch_transitions(const DevGraph& g, const DevBatch& b, const DevParams& p, DevWork& w, int32_t n_overflow,
+                        bool big_tier, hipStream_t s) {
+  if (big_tier)
+    hipLaunchKernelGGL(k_transitions<true>, dim3(grid_for(n_overflow, 1, BIG_SLOTS)), dim3(TB), 0, s, g, b, p, w,
+                       n_overflow);
+  else
+    hipLaunchKernelGGL(k_transitions<false>, dim3(grid_for(b.n_points, 1, WAVE_GRID_CAP)), dim3(TB), 0, s, g, b, p,
+                       w, 0);
+}
+void launch_viterbi(const DevBatch& b, DevWork& w, hipStream_t s) {
+  hipLaunchKernelGGL(k_viterbi, dim3(grid_for(b.n_traces, 1, WAVE_GRID_CAP)), dim3(TB), 0, s, b, w);
+}
+void launch_route(const DevGraph& g, const DevBatch& b, const DevParams& p, DevWork& w, int32_t n_overflow,
+                  bool big_tier, hipStream_t s) {
+  if (big_tier)
+    hipLaunchKernelGGL(k_route<true>, dim3(grid_for(n_overflow, 1, BIG_SLOTS)), dim3(TB), 0, s, g, b, p, w,
+                       n_overflow);
+  else
+    hipLaunchKernelGGL(k_route<false>, dim3(grid_for(b.n_points, 1, WAVE_GRID_CAP)), dim3(TB), 0, s, g, b, p, w, 0);
+}
+void launch_segments(const DevGraph& g, const DevBatch& b, DevWork& w, DevOut& o, bool write, hipStream_t s) {
+  if (write)
+    hipLaunchKernelGGL(k_segments<true>, dim3(grid_for(b.n_traces, 64, 1 << 30)), dim3(64), 0, s, g, b, w, o);
+  else
+    hipLaunchKernelGGL(k_segments<false>, dim3(grid_for(b.n_traces, 64, 1 << 30)), dim3(64), 0, s, g, b, w, o);
+}
+void launch_report(const DevBatch& b, const DevReportCfg& rc, DevWork& w, DevOut& o, hipStream_t s) {
+  hipLaunchKernelGGL(k_report, dim3(grid_for(b.n_traces, 64, 1 << 30)), dim3(64), 0, s, b, rc, w, o, 0);
+}
+
+size_t scan_tmp_bytes(int64_t n) {
+  size_t a = 0, c = 0;
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, a, (int64_t*)nullptr, (int64_t*)nullptr, (int)(n + 1));
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, c, (int32_t*)nullptr, (int32_t*)nullptr, (int)(n + 1));
+  return a > c ? a : c;
+}
+void scan_i64(int64_t* d, int64_t n, void* tmp, size_t tmp_bytes, hipStream_t s) {
+  (void)hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, d, d, (int)(n + 1), s);
+}
+void scan_i32(int32_t* d, int64_t n, void* tmp, size_t tmp_bytes, hipStream_t s) {
+  (void)hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, d, d, (int)(n + 1), s);
+}
+
+}  // namespace otm

@@ -1,0 +1,572 @@
+// report.cpp -- see report.h.
+#include "report.h"
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+
+namespace otm {
+
+using json::Kind;
+using json::Value;
+
+std::string error_body(const std::string& msg) { return "{\"error\":\"" + msg + "\"}"; }
+
+const char* trace_error_text(int kind) {
+  switch (kind) {
+    case OTM_TERR_ZERODIV: return "float division by zero";
+    case OTM_TERR_CAND_OVERFLOW: return "too many candidate edges within search radius";
+    case OTM_TERR_SEARCH_OVERFLOW: return "route search exceeded node limit";
+  }
+  return "";
+}
+
+static size_t cp_len(const std::string& s) {
+  size_t n = 0;
+  for (unsigned char c : s)
+    if ((c & 0xC0) != 0x80) ++n;
+  return n;
+}
+
+int parse_request(const char* path, std::string_view body, Value* trace, std::string* resp) {
+  // :88-96 -- the action is the last path component
+  if (path) {
+    std::string_view pv(path);
+    pv = pv.substr(0, pv.find_first_of("?#"));
+    const size_t slash = pv.rfind('/');
+    const std::string_view last = slash == std::string_view::npos ? pv : pv.substr(slash + 1);
+    if (last != "report") {
+      *resp = error_body("Try a valid action: ['report']");
+      return 400;
+    }
+  }
+  // :99-100
+  std::string uerr = json::utf8_error(body);
+  if (!uerr.empty()) {
+    *resp = error_body(uerr);
+    return 400;
+  }
+  std::string perr;
+  if (!json::parse(body, trace, &perr)) {
+    *resp = error_body(perr);
+    return 400;
+  }
+  // :226 trace.get('uuid') runs outside the try: do() answers 400 str(e)
+  if (trace->kind != Kind::Obj) {
+    *resp = std::string("'") + trace->type_name() + "' object has no attribute 'get'";
+    return 400;
+  }
+  const Value* uuid = trace->get("uuid");
+  if (!uuid || uuid->kind == Kind::Null) {
+    *resp = error_body("uuid is required");
+    return 400;
+  }
+  // :231-234 trace['trace'][1]
+  const Value* tr = trace->get("trace");
+  bool ok = false;
+  if (tr) {
+    if (tr->kind == Kind::Arr) ok = tr->items.size() >= 2;
+    else if (tr->kind == Kind::Str) ok = cp_len(tr->s) >= 2;
+  }
+  if (!ok) {
+    *resp = error_body(
+        "trace must be a non zero length array of object each of which must have at least lat, lon and time");
+    return 400;
+  }
+  return 0;
+}
+
+// ------------------------------------------------------------ python values
+namespace {
+
+struct PV {  // a borrowed Python value
+  const Value* v;  // nullptr == None
+  Kind kind() const { return v ? v->kind : Kind::Null; }
+  bool num() const { return v && v->is_num(); }
+  bool integral() const { return v && (v->kind == Kind::Int || v->kind == Kind::Bool); }
+  bool big() const { return v && v->bigint; }
+  double d() const { return v->num(); }
+  int64_t i() const { return v->kind == Kind::Bool ? (v->b ? 1 : 0) : v->i; }
+  const char* tn() const { return v ? v->type_name() : "NoneType"; }
+};
+
+// a computed number: int or float
+struct Num {
+  bool is_int;
+  int64_t i;
+  double f;
+  double d() const { return is_int ? (double)i : f; }
+};
+
+const Value kTrue = [] {
+  Value v;
+  v.kind = Kind::Bool;
+  v.b = true;
+  return v;
+}();
+const Value kFalse = [] {
+  Value v;
+  v.kind = Kind::Bool;
+  v.b = false;
+  return v;
+}();
+
+std::string fmt2(const char* f, const char* a, const char* b) {
+  char buf[256];
+  std::snprintf(buf, sizeof buf, f, a, b);
+  return buf;
+}
+
+bool to_num(PV a, Num* n) {
+  if (!a.num()) return false;
+  if (a.integral() && !a.big()) *n = Num{true, a.i(), 0.0};
+  else *n = Num{false, 0, a.d()};
+  return true;
+}
+
+bool py_sub(PV a, PV b, Num* r, std::string* exc) {
+  Num x, y;
+  if (!to_num(a, &x) || !to_num(b, &y)) {
+    *exc = fmt2("unsupported operand type(s) for -: '%s' and '%s'", a.tn(), b.tn());
+    return false;
+  }
+  if (x.is_int && y.is_int) *r = Num{true, x.i - y.i, 0.0};
+  else *r = Num{false, 0, x.d() - y.d()};
+  return true;
+}
+
+bool py_eq(PV a, PV b);
+bool value_eq(const Value& a, const Value& b) {
+  if (a.kind == Kind::Str) return a.s == b.s;
+  if (a.kind == Kind::Arr) {
+    if (a.items.size() != b.items.size()) return false;
+    for (size_t k = 0; k < a.items.size(); ++k)
+      if (!py_eq(PV{&a.items[k]}, PV{&b.items[k]})) return false;
+    return true;
+  }
+  if (a.kind == Kind::Obj) {
+    if (a.items.size() != b.items.size()) return false;
+    for (size_t k = 0; k < a.items.size(); ++k) {
+      const Value* o = b.get(a.keys[k]);
+      if (!o || !py_eq(PV{&a.items[k]}, PV{o})) return false;
+    }
+    return true;
+  }
+  return false;
+}
+bool py_eq(PV a, PV b) {
+  if (a.num() && b.num()) {
+    Num x, y;
+    to_num(a, &x);
+    to_num(b, &y);
+    if (x.is_int && y.is_int) return x.i == y.i;
+    return x.d() == y.d();
+  }
+  if (a.kind() == Kind::Null || b.kind() == Kind::Null) return a.kind() == b.kind();
+  if (a.kind() != b.kind()) return false;
+  return value_eq(*a.v, *b.v);
+}
+bool py_eq_int(PV a, int64_t k) {
+  if (!a.num()) return false;
+  Num x;
+  to_num(a, &x);
+  return x.is_int ? x.i == k : x.f == (double)k;
+}
+
+// a < b / a > b for Num-or-PV left operands against an int or threshold
+bool num_cmp(Num a, Num b, char op) {
+  if (a.is_int && b.is_int) return op == '<' ? a.i < b.i : a.i > b.i;
+  return op == '<' ? a.d() < b.d() : a.d() > b.d();
+}
+bool py_cmp_int(PV a, int64_t k, char op, bool* res, std::string* exc) {
+  Num x;
+  if (!to_num(a, &x)) {
+    char buf[256];
+    std::snprintf(buf, sizeof buf, "'%c' not supported between instances of '%s' and 'int'", op, a.tn());
+    *exc = buf;
+    return false;
+  }
+  *res = num_cmp(x, Num{true, k, 0.0}, op);
+  return true;
+}
+bool truthy(PV a) {
+  switch (a.kind()) {
+    case Kind::Null: return false;
+    case Kind::Bool: return a.v->b;
+    case Kind::Int: return a.v->bigint ? true : a.v->i != 0;
+    case Kind::Float: return a.v->f != 0.0;
+    case Kind::Str: return !a.v->s.empty();
+    default: return !a.v->items.empty();
+  }
+}
+const Value* getitem(const Value* x, const char* key, std::string* exc) {
+  if (!x || x->kind == Kind::Null) {
+    *exc = "'NoneType' object is not subscriptable";
+    return nullptr;
+  }
+  if (x->kind == Kind::Obj) {
+    const Value* v = x->get(key);
+    if (!v) *exc = std::string("'") + key + "'";
+    return v;
+  }
+  if (x->kind == Kind::Arr) *exc = "list indices must be integers or slices, not str";
+  else if (x->kind == Kind::Str) *exc = "string indices must be integers";
+  else *exc = std::string("'") + x->type_name() + "' object is not subscriptable";
+  return nullptr;
+}
+const Value* index(const Value& x, int64_t k, std::string* exc) {
+  if (x.kind == Kind::Arr) return &x.items[(size_t)k];
+  if (x.kind == Kind::Obj) *exc = std::to_string(k);
+  else *exc = "string indices must be integers";
+  return nullptr;
+}
+bool in_set(const std::vector<int64_t>& s, int64_t x) {
+  for (auto v : s)
+    if (v == x) return true;
+  return false;
+}
+
+}  // namespace
+
+bool report_dom(const ReportConfig& rc, const Value& trace, Value* segments, std::string* resp,
+                std::string* stderr_text, std::string* exc) {
+  // :116
+  const Value* tr = trace.get("trace");
+  if (tr->kind != Kind::Arr) {
+    *exc = "string indices must be integers";
+    return false;
+  }
+  const Value* et = getitem(&tr->items.back(), "time", exc);
+  if (!et) return false;
+  PV end_time{et};
+  // :120
+  const Value* segs = getitem(segments, "segments", exc);
+  if (!segs) return false;
+  int64_t nseg;
+  if (segs->kind == Kind::Arr || segs->kind == Kind::Obj) nseg = (int64_t)segs->items.size();
+  else if (segs->kind == Kind::Str) nseg = (int64_t)cp_len(segs->s);
+  else {
+    *exc = std::string("object of type '") + segs->type_name() + "' has no len()";
+    return false;
+  }
+  int64_t last_idx = nseg - 1;
+  // threshold: int 15, or the bool True / False strtobool produced
+  const Value thr_v = [&] {
+    Value v;
+    if (rc.threshold_sec == 15.0) {
+      v.kind = Kind::Int;
+      v.i = 15;
+    } else {
+      v.kind = Kind::Bool;
+      v.b = rc.threshold_sec != 0.0;
+    }
+    return v;
+  }();
+  Num thr;
+  to_num(PV{&thr_v}, &thr);
+  // :121-122
+  while (last_idx >= 0) {
+    const Value* s = index(*segs, last_idx, exc);
+    if (!s) return false;
+    const Value* st = getitem(s, "start_time", exc);
+    if (!st) return false;
+    Num diff;
+    if (!py_sub(end_time, PV{st}, &diff, exc)) return false;
+    if (!num_cmp(diff, thr, '<')) break;
+    --last_idx;
+  }
+  // :125-127
+  const Value* shape_used = nullptr;
+  if (last_idx >= 0) {
+    const Value* s = index(*segs, last_idx, exc);
+    if (!s) return false;
+    shape_used = getitem(s, "begin_shape_index", exc);
+    if (!shape_used) return false;
+  }
+  // :131
+  {
+    Value mode;
+    mode.kind = Kind::Str;
+    mode.s = "auto";
+    segments->set("mode", std::move(mode));
+  }
+  segs = segments->get("segments");
+  // :132-196
+  bool have = false, first_seg = true;
+  PV prior_id{nullptr}, prior_start{nullptr}, prior_end{nullptr}, prior_len{nullptr}, prior_ql{nullptr};
+  int64_t prior_level = -1;
+  int64_t successful = 0, unreported = 0, disc = 0, invalid = 0, unassoc = 0;
+  bool succ_set = false, unrep_set = false;
+  double succ_len = 0, unrep_len = 0;
+  std::string reps;
+  int nreps = 0;
+  for (int64_t idx = 0; idx <= last_idx; ++idx) {
+    const Value* seg = index(*segs, idx, exc);
+    if (!seg) return false;
+    if (seg->kind != Kind::Obj) {
+      *exc = std::string("'") + seg->type_name() + "' object has no attribute 'get'";
+      return false;
+    }
+    PV segment_id{seg->get("segment_id")}, start_time{seg->get("start_time")}, end_time_s{seg->get("end_time")};
+    const Value* iv = seg->get("internal");
+    PV internal{iv ? iv : &kFalse}, queue_length{seg->get("queue_length")}, length{seg->get("length")};
+    // :150
+    if (idx != 0) {
+      const Value* a = getitem(seg, "start_time", exc);
+      if (!a) return false;
+      if (py_eq_int(PV{a}, -1)) {
+        const Value* prev = index(*segs, idx - 1, exc);
+        if (!prev) return false;
+        const Value* b = getitem(prev, "end_time", exc);
+        if (!b) return false;
+        if (py_eq_int(PV{b}, -1)) ++disc;
+      }
+    }
+    // :154
+    int64_t level = -1;
+    if (segment_id.kind() != Kind::Null) {
+      if (!segment_id.integral() || segment_id.big()) {
+        *exc = fmt2("unsupported operand type(s) for &: '%s' and '%s'", segment_id.tn(), "int");
+        return false;
+      }
+      level = segment_id.i() & 0x7;
+    }
+    // :157
+    if (have && prior_id.kind() != Kind::Null) {
+      bool gt;
+      if (!py_cmp_int(prior_len, 0, '>', &gt, exc)) return false;
+      if (gt && !py_eq(internal, PV{&kTrue})) {
+        if (in_set(rc.report_levels, prior_level)) {
+          const bool trans = in_set(rc.transition_levels, level);
+          PV t1 = trans ? start_time : prior_end;
+          Num diff;
+          if (!py_sub(t1, prior_start, &diff, exc)) return false;
+          Num len;
+          to_num(prior_len, &len);
+          if (diff.d() == 0.0) {
+            *exc = (len.is_int && diff.is_int) ? "division by zero" : "float division by zero";
+            return false;
+          }
+          const double speed = (len.d() / diff.d()) * 3.6;
+          if (speed < 200.0) {
+            reps.append(nreps ? ",{\"id\":" : "{\"id\":");
+            json::dump(*prior_id.v, &reps);
+            reps.append(",\"t0\":");
+            if (prior_start.v) json::dump(*prior_start.v, &reps);
+            else reps.append("null");
+            reps.append(",\"t1\":");
+            if (t1.v) json::dump(*t1.v, &reps);
+            else reps.append("null");
+            reps.append(",\"length\":");
+            json::dump(*prior_len.v, &reps);
+            reps.append(",\"queue_length\":");
+            if (prior_ql.v) json::dump(*prior_ql.v, &reps);
+            else reps.append("null");
+            if (trans && segment_id.kind() != Kind::Null) {
+              reps.append(",\"next_id\":");
+              json::dump(*segment_id.v, &reps);
+            }
+            reps.push_back('}');
+            ++nreps;
+            ++successful;
+            succ_len = json::py_round3(len.d() * 0.001);
+            succ_set = true;
+          } else {
+            stderr_text->append("Speed exceeds 200kph\n");
+            ++invalid;
+          }
+        } else {
+          ++unreported;
+          Num len;
+          to_num(prior_len, &len);
+          unrep_len = json::py_round3(len.d() * 0.001);
+          unrep_set = true;
+        }
+      }
+    }
+    // :179-189
+    if (!(py_eq(internal, PV{&kTrue}) && !first_seg)) {
+      prior_id = segment_id;
+      prior_start = start_time;
+      prior_end = end_time_s;
+      prior_len = length;
+      prior_level = level;
+      prior_ql = queue_length;
+      have = true;
+    }
+    first_seg = false;
+    // :195
+    if (segment_id.kind() == Kind::Null && py_eq(internal, PV{&kFalse})) ++unassoc;
+  }
+  // :198-215
+  std::string& o = *resp;
+  o.clear();
+  o.append("{\"stats\":{\"successful_matches\":{\"count\":");
+  json::put_int(successful, &o);
+  o.append(",\"length\":");
+  if (succ_set) json::put_float(succ_len, &o);
+  else o.push_back('0');
+  o.append("},\"unreported_matches\":{\"count\":");
+  json::put_int(unreported, &o);
+  o.append(",\"length\":");
+  if (unrep_set) json::put_float(unrep_len, &o);
+  else o.push_back('0');
+  o.append("},\"match_errors\":{\"discontinuities\":");
+  json::put_int(disc, &o);
+  o.append(",\"invalid_speeds\":");
+  json::put_int(invalid, &o);
+  o.append("},\"unassociated_segments\":");
+  json::put_int(unassoc, &o);
+  o.push_back('}');
+  if (shape_used && truthy(PV{shape_used})) {
+    o.append(",\"shape_used\":");
+    json::dump(*shape_used, &o);
+  }
+  o.append(",\"segment_matcher\":");
+  json::dump(*segments, &o);
+  o.append(",\"datastore\":{\"mode\":\"auto\"");
+  if (nreps) {
+    o.append(",\"reports\":[");
+    o.append(reps);
+    o.push_back(']');
+  }
+  o.append("}}");
+  return true;
+}
+
+bool extract_points(const Value& trace, TracePoints* out, std::string* err) {
+  const Value* tr = trace.get("trace");
+  if (!tr || tr->kind != Kind::Arr) {
+    *err = "trace must be an array of points";
+    return false;
+  }
+  const size_t n = tr->items.size();
+  out->lat.resize(n);
+  out->lon.resize(n);
+  out->acc.resize(n);
+  out->time.resize(n);
+  auto num = [](const Value* v, double* d) {
+    if (!v || (v->kind != Kind::Int && v->kind != Kind::Float)) return false;
+    *d = v->kind == Kind::Int ? (v->bigint ? v->f : (double)v->i) : v->f;
+    return true;
+  };
+  for (size_t k = 0; k < n; ++k) {
+    const Value& pt = tr->items[k];
+    double la, lo, ti, ac;
+    if (pt.kind != Kind::Obj || !num(pt.get("lat"), &la) || !num(pt.get("lon"), &lo) || !num(pt.get("time"), &ti)) {
+      *err = "trace point " + std::to_string(k) + " must have numeric lat, lon and time";
+      return false;
+    }
+    out->lat[k] = (float)la;
+    out->lon[k] = (float)lo;
+    out->time[k] = ti;
+    out->acc[k] = num(pt.get("accuracy"), &ac) ? (float)ac : 0.0f;
+  }
+  return true;
+}
+
+// ------------------------------------------------------------ typed writers
+static void put_time(bool valid, double t, std::string* o) {
+  if (valid) json::put_float(t, o);
+  else o->append("-1");
+}
+
+static void write_segments_array(const otm_results& r, const otm_trace_result& tr, std::string* o) {
+  o->push_back('[');
+  for (int32_t k = 0; k < tr.seg_cnt; ++k) {
+    const otm_segment& s = r.segments[tr.seg_off + k];
+    if (k) o->push_back(',');
+    o->push_back('{');
+    if (s.segment_id >= 0) {
+      o->append("\"segment_id\":");
+      json::put_int(s.segment_id, o);
+      o->push_back(',');
+    }
+    o->append("\"way_ids\":[");
+    for (int32_t w = 0; w < s.way_cnt; ++w) {
+      if (w) o->push_back(',');
+      json::put_int(r.way_ids[s.way_off + w], o);
+    }
+    o->append("],\"start_time\":");
+    put_time(s.flags & OTM_SEG_START_VALID, s.start_time, o);
+    o->append(",\"end_time\":");
+    put_time(s.flags & OTM_SEG_END_VALID, s.end_time, o);
+    o->append(",\"queue_length\":");
+    json::put_int(s.queue_length, o);
+    o->append(",\"length\":");
+    json::put_int(s.length, o);
+    o->append((s.flags & OTM_SEG_INTERNAL) ? ",\"internal\":true" : ",\"internal\":false");
+    o->append(",\"begin_shape_index\":");
+    json::put_int(s.begin_shape_index, o);
+    o->append(",\"end_shape_index\":");
+    json::put_int(s.end_shape_index, o);
+    o->push_back('}');
+  }
+  o->push_back(']');
+}
+
+void write_match_json(const otm_results& r, int32_t t, std::string* o) {
+  o->append("{\"segments\":");
+  write_segments_array(r, r.traces[t], o);
+  o->push_back('}');
+}
+
+int write_report_response(const otm_results& r, int32_t t, std::string* o) {
+  const otm_trace_result& tr = r.traces[t];
+  if (tr.code != 200) {
+    *o = error_body(trace_error_text(tr.error_kind));
+    return 500;
+  }
+  o->append("{\"stats\":{\"successful_matches\":{\"count\":");
+  json::put_int(tr.successful_count, o);
+  o->append(",\"length\":");
+  if (tr.successful_length >= 0) json::put_float(json::py_round3((double)tr.successful_length * 0.001), o);
+  else o->push_back('0');
+  o->append("},\"unreported_matches\":{\"count\":");
+  json::put_int(tr.unreported_count, o);
+  o->append(",\"length\":");
+  if (tr.unreported_length >= 0) json::put_float(json::py_round3((double)tr.unreported_length * 0.001), o);
+  else o->push_back('0');
+  o->append("},\"match_errors\":{\"discontinuities\":");
+  json::put_int(tr.discontinuities, o);
+  o->append(",\"invalid_speeds\":");
+  json::put_int(tr.invalid_speeds, o);
+  o->append("},\"unassociated_segments\":");
+  json::put_int(tr.unassociated, o);
+  o->push_back('}');
+  if (tr.shape_used > 0) {
+    o->append(",\"shape_used\":");
+    json::put_int(tr.shape_used, o);
+  }
+  o->append(",\"segment_matcher\":{\"segments\":");
+  write_segments_array(r, tr, o);
+  o->append(",\"mode\":\"auto\"},\"datastore\":{\"mode\":\"auto\"");
+  if (tr.rep_cnt > 0) {
+    o->append(",\"reports\":[");
+    for (int32_t k = 0; k < tr.rep_cnt; ++k) {
+      const otm_report_rec& p = r.reports[tr.rep_off + k];
+      if (k) o->push_back(',');
+      o->append("{\"id\":");
+      json::put_int(p.id, o);
+      o->append(",\"t0\":");
+      json::put_float(p.t0, o);
+      o->append(",\"t1\":");
+      if (p.flags & OTM_REP_T1_INT_MINUS1) o->append("-1");
+      else json::put_float(p.t1, o);
+      o->append(",\"length\":");
+      json::put_int(p.length, o);
+      o->append(",\"queue_length\":");
+      json::put_int(p.queue_length, o);
+      if (p.next_id >= 0) {
+        o->append(",\"next_id\":");
+        json::put_int(p.next_id, o);
+      }
+      o->push_back('}');
+    }
+    o->push_back(']');
+  }
+  o->append("}}");
+  return 200;
+}
+
+}  // namespace otm

@@ -1,0 +1,37 @@
+// report.h -- reporter_service.py's request/response layer on the host.
+#pragma once
+#include <string>
+#include <vector>
+
+#include "json.h"
+#include "otm_internal.h"
+#include "otmatch.h"
+
+namespace otm {
+
+// parse_trace + handle_request validation (py/reporter_service.py:85-106,
+// :218-234).  Returns 0 with *trace filled, or the HTTP code with *resp set.
+int parse_request(const char* path, std::string_view body, json::Value* trace, std::string* resp);
+
+// report() (py/reporter_service.py:110-215) over any matcher output, with
+// Python value semantics.  Returns true and *resp, or false and *exc =
+// str(exception).  *stderr_text gets "Speed exceeds 200kph\n" per invalid speed.
+bool report_dom(const ReportConfig& rc, const json::Value& trace, json::Value* segments, std::string* resp,
+                std::string* stderr_text, std::string* exc);
+
+// Points of a parsed request for the matcher (the Match input contract).
+struct TracePoints {
+  std::vector<float> lat, lon, acc;
+  std::vector<double> time;
+};
+bool extract_points(const json::Value& trace, TracePoints* out, std::string* err);
+
+// Typed writers over one trace of a results set.
+void write_match_json(const otm_results& r, int32_t t, std::string* out);
+// Full /report response for trace t; returns the HTTP code.
+int write_report_response(const otm_results& r, int32_t t, std::string* out);
+const char* trace_error_text(int kind);
+
+std::string error_body(const std::string& msg);
+
+}  // namespace otm

@@ -1,0 +1,222 @@
+"""Engine: one MI355X, its HBM-resident road graph, the /report hot path.
+
+Python face of libotmatch.so's C ABI (include/otmatch.h).  Mirrors the
+reference's matcher interface (py/reporter_service.py): Engine.report(body)
+answers like SegmentMatcherHandler.handle_request (:218-240) and
+Engine.match_json(body) like valhalla.SegmentMatcher().Match (:112); the
+binary entry points (match, match_device) are the benchmark path.
+"""
+import ctypes as C
+import json
+import os
+import tempfile
+
+import numpy as np
+
+from . import _lib
+from ._lib import lib, take
+
+
+class OtmError(RuntimeError):
+    pass
+
+
+def _check(rc):
+    if rc != _lib.OTM_OK:
+        raise OtmError("libotmatch error %d: %s" % (rc, _lib.last_error()))
+
+
+def write_config(path, graph_path, **meili):
+    """Write an engine config: {"otm":{"graph":...},"meili":{"default":{...}}}."""
+    cfg = {"otm": {"graph": os.path.abspath(graph_path)}, "meili": {"default": meili}}
+    with open(path, "w") as f:
+        json.dump(cfg, f)
+    return path
+
+
+class Results(object):
+    """Host copy of one batch's results (numpy structured arrays)."""
+
+    def __init__(self, r):
+        self.traces = _lib.as_array(r.traces, _lib.TRACE_DTYPE, r.n_traces)
+        self.segments = _lib.as_array(r.segments, _lib.SEGMENT_DTYPE, r.n_segments)
+        self.reports = _lib.as_array(r.reports, _lib.REPORT_DTYPE, r.n_reports)
+        self.way_ids = _lib.as_array(r.way_ids, np.int64, r.n_way_ids)
+
+
+class Engine(object):
+    def __init__(self, config_path=None, graph_path=None, device=0, **meili):
+        """Either a config file (valhalla.Configure-style) or a graph path."""
+        L = lib()
+        self._tmp = None
+        if config_path is None:
+            if graph_path is None:
+                raise ValueError("config_path or graph_path required")
+            fd, self._tmp = tempfile.mkstemp(suffix=".json", prefix="otm_cfg_")
+            os.close(fd)
+            config_path = write_config(self._tmp, graph_path, **meili)
+        h = C.c_void_p()
+        dev = (C.c_int * 1)(device)
+        rc = L.otm_engine_create(config_path.encode(), dev, 1, C.byref(h))
+        if rc != _lib.OTM_OK:
+            raise OtmError("otm_engine_create failed (%d): %s" % (rc, _lib.last_error()))
+        self.h = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().otm_engine_destroy(self.h)
+            self.h = None
+        if getattr(self, "_tmp", None):
+            try:
+                os.unlink(self._tmp)
+            except OSError:
+                pass
+            self._tmp = None
+
+    def __del__(self):
+        self.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # ------------------------------------------------------------ request level
+    def report(self, body):
+        """-> (http_code, body_str), exactly as reporter_service.py answers /report."""
+        b = body.encode("utf-8") if isinstance(body, str) else body
+        out = C.c_void_p()
+        n = C.c_size_t()
+        code = lib().otm_report(self.h, b, len(b), C.byref(out), C.byref(n))
+        return code, take(out, n.value).decode("utf-8")
+
+    def report_batch(self, bodies):
+        bs = [b.encode("utf-8") if isinstance(b, str) else b for b in bodies]
+        n = len(bs)
+        arr = (C.c_char_p * n)(*bs)
+        lens = (C.c_size_t * n)(*[len(b) for b in bs])
+        outs = (C.c_void_p * n)()
+        olens = (C.c_size_t * n)()
+        codes = (C.c_int * n)()
+        _check(lib().otm_report_batch(self.h, n, arr, lens, outs, olens, codes))
+        return [(codes[i], take(outs[i], olens[i]).decode("utf-8")) for i in range(n)]
+
+    def match_json(self, body):
+        b = body.encode("utf-8") if isinstance(body, str) else body
+        out = C.c_void_p()
+        n = C.c_size_t()
+        code = lib().otm_match_json(self.h, b, len(b), C.byref(out), C.byref(n))
+        return code, take(out, n.value).decode("utf-8")
+
+    def report_segments(self, body, match_output):
+        return report_segments(body, match_output, self)
+
+    def submit(self, body, tag):
+        b = body.encode("utf-8") if isinstance(body, str) else body
+        _check(lib().otm_submit(self.h, b, len(b), tag))
+
+    def poll(self, max_results=1024, timeout_us=0):
+        res = (_lib.Result * max_results)()
+        n = lib().otm_poll(self.h, res, max_results, timeout_us)
+        if n < 0:
+            _check(n)
+        return [(res[i].tag, res[i].code, take(res[i].body, res[i].body_len).decode("utf-8")) for i in range(n)]
+
+    # ------------------------------------------------------------ binary level
+    def match(self, batch):
+        """Host batch (dict of numpy arrays) -> Results."""
+        off = np.ascontiguousarray(batch["trace_off"], dtype=np.int64)
+        lat = np.ascontiguousarray(batch["lat"], dtype=np.float32)
+        lon = np.ascontiguousarray(batch["lon"], dtype=np.float32)
+        tm = np.ascontiguousarray(batch["time"], dtype=np.float64)
+        acc = np.ascontiguousarray(batch["accuracy"], dtype=np.float32)
+        b = _lib.Batch(len(off) - 1, int(off[-1]), off.ctypes.data, lat.ctypes.data, lon.ctypes.data,
+                       tm.ctypes.data, acc.ctypes.data)
+        r = _lib.Results()
+        _check(lib().otm_match_soa(self.h, C.byref(b), C.byref(r)))
+        return Results(r)
+
+    def match_device(self, trace_off, lat, lon, time, accuracy, stream=None):
+        """Device batch: torch tensors already in this GPU's HBM.  Results
+        stay on the device; call fetch() for a host copy."""
+        n_traces = trace_off.numel() - 1
+        b = _lib.Batch(n_traces, int(lat.numel()), trace_off.data_ptr(), lat.data_ptr(), lon.data_ptr(),
+                       time.data_ptr(), accuracy.data_ptr())
+        _check(lib().otm_match_device(self.h, C.byref(b), stream))
+
+    def fetch(self):
+        r = _lib.Results()
+        _check(lib().otm_fetch_results(self.h, C.byref(r)))
+        return Results(r)
+
+    def hist_bind(self, tensor, nbins, bin_kph):
+        ptr = None if tensor is None else tensor.data_ptr()
+        _check(lib().otm_hist_bind(self.h, ptr, nbins, bin_kph))
+
+    def graph_info(self):
+        a, b, c = C.c_int64(), C.c_int64(), C.c_int64()
+        _check(lib().otm_graph_info(self.h, C.byref(a), C.byref(b), C.byref(c)))
+        return {"nodes": a.value, "edges": b.value, "segments": c.value}
+
+    def set_counting(self, on):
+        _check(lib().otm_set_counting(self.h, 1 if on else 0))
+
+    def counters(self):
+        c = _lib.WorkCounters()
+        _check(lib().otm_get_counters(self.h, C.byref(c)))
+        return {n: getattr(c, n) for n in _lib.COUNTER_NAMES}
+
+    def set_timing(self, on):
+        _check(lib().otm_set_timing(self.h, 1 if on else 0))
+
+    STAGES = ("columns", "candidates", "trans_size", "transitions", "viterbi", "route", "segments", "report")
+
+    def stage_ms(self):
+        ms = (C.c_float * 8)()
+        _check(lib().otm_get_stage_ms(self.h, ms, 8))
+        return dict(zip(self.STAGES, list(ms)))
+
+    _DEBUG = {"ncand": (0, np.int32), "cand_edge": (1, np.int32), "cand_off": (2, np.float32),
+              "cand_emis": (3, np.float32), "trans_off": (4, np.int64), "trans": (5, np.float32),
+              "state": (6, np.int32), "col_prev": (7, np.int32), "route_dist": (8, np.float32),
+              "gc": (9, np.float32)}
+
+    def debug(self, name):
+        what, dt = self._DEBUG[name]
+        need = C.c_size_t()
+        _check(lib().otm_debug_fetch(self.h, what, None, 0, C.byref(need)))
+        out = np.zeros(need.value // np.dtype(dt).itemsize, dtype=dt)
+        _check(lib().otm_debug_fetch(self.h, what, out.ctypes.data, out.nbytes, None))
+        return out
+
+
+def report_segments(body, match_output, engine=None):
+    """report() (py/reporter_service.py:110-215) over any matcher's output."""
+    b = body.encode("utf-8") if isinstance(body, str) else body
+    m = match_output.encode("utf-8") if isinstance(match_output, str) else match_output
+    out = C.c_void_p()
+    n = C.c_size_t()
+    code = lib().otm_report_segments(engine.h if engine is not None else None, b, len(b), m, len(m), C.byref(out),
+                                     C.byref(n))
+    return code, take(out, n.value).decode("utf-8")
+
+
+def encode_request(uuid, lat, lon, time, accuracy):
+    """The Java batcher's request bytes (Batch.java:52-61, Point.java:39-45)."""
+    lat = np.ascontiguousarray(lat, dtype=np.float32)
+    lon = np.ascontiguousarray(lon, dtype=np.float32)
+    tm = np.ascontiguousarray(time, dtype=np.int64)
+    acc = np.ascontiguousarray(accuracy, dtype=np.int32)
+    out = C.c_void_p()
+    n = C.c_size_t()
+    _check(lib().otm_encode_request(uuid.encode("utf-8"), len(lat), lat.ctypes.data, lon.ctypes.data,
+                                    tm.ctypes.data, acc.ctypes.data, C.byref(out), C.byref(n)))
+    return take(out, n.value)
+
+
+def murmur2_partition(key, n):
+    """Kafka DefaultPartitioner shard of a uuid (Reporter.java:97 keys by uuid)."""
+    b = key.encode("utf-8") if isinstance(key, str) else key
+    return (lib().otm_murmur2(b, len(b)) & 0x7fffffff) % n

@@ -1,0 +1,89 @@
+"""Synthetic inputs -- harness tooling over libotmatch.
+
+No Valhalla tiles or real probe data exist here, so every workload is a
+seeded synthetic road network plus seeded probe traces:
+
+  config 1  small extract (5 x 5 km), synthesize_gps-style traces (one point
+            per edge end, stddev 0: py/generate_test_trace.py:31-73)
+  config 2  city 20 x 20 km, 10k vehicles x 100 points, 5 s, sigma 15 m
+  config 3  metro 100 x 100 km, 1M vehicles x 100 points (uuid-sharded)
+  config 4  state 500 x 500 km highway-heavy, 30 s, sigma 50 m, radius 100 m
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import _lib
+from ._lib import lib
+
+CONFIGS = {
+    1: dict(graph=dict(width_m=5000, height_m=5000), traces=dict(n_vehicles=100, points_per_vehicle=60,
+                                                                 interval_s=5.0, noise_sigma_m=0.0, accuracy=0.0)),
+    2: dict(graph=dict(width_m=20000, height_m=20000), traces=dict(n_vehicles=10000, points_per_vehicle=100,
+                                                                   interval_s=5.0, noise_sigma_m=15.0, accuracy=15.0)),
+    3: dict(graph=dict(width_m=100000, height_m=100000), traces=dict(n_vehicles=1000000, points_per_vehicle=100,
+                                                                     interval_s=5.0, noise_sigma_m=15.0,
+                                                                     accuracy=15.0)),
+    4: dict(graph=dict(width_m=500000, height_m=500000, block_m=1200, jitter_m=150, arterial_every=4,
+                       highway_every=8, complex_every=0, seg_max_m=5000),
+            traces=dict(n_vehicles=100000, points_per_vehicle=100, interval_s=30.0, noise_sigma_m=50.0,
+                        accuracy=50.0),
+            meili=dict(search_radius=100.0, max_search_radius=100.0)),
+}
+
+
+def graph_params(**kw):
+    p = _lib.SynthGraphParams()
+    lib().otm_synth_graph_defaults(C.byref(p))
+    for k, v in kw.items():
+        setattr(p, k, v)
+    return p
+
+
+def make_graph(path, **kw):
+    p = graph_params(**kw)
+    rc = lib().otm_synth_graph(C.byref(p), path.encode())
+    if rc != 0:
+        raise RuntimeError("otm_synth_graph failed: %s" % _lib.last_error())
+    return path
+
+
+def make_traces(graph_path, n_vehicles, points_per_vehicle, interval_s=5.0, noise_sigma_m=15.0, accuracy=15.0,
+                t0=1500000000.0, seed=7, vehicle_offset=0):
+    """-> dict of numpy arrays: trace_off, lat, lon, time, accuracy, true_edge, true_off."""
+    tp = _lib.SynthTraceParams(n_vehicles, points_per_vehicle, interval_s, noise_sigma_m, accuracy, t0, seed,
+                               vehicle_offset)
+    P = n_vehicles * points_per_vehicle
+    out = dict(trace_off=np.zeros(n_vehicles + 1, np.int64), lat=np.zeros(P, np.float32),
+               lon=np.zeros(P, np.float32), time=np.zeros(P, np.float64), accuracy=np.zeros(P, np.float32),
+               true_edge=np.zeros(P, np.int32), true_off=np.zeros(P, np.float32))
+    rc = lib().otm_synth_traces(graph_path.encode(), C.byref(tp), out["trace_off"].ctypes.data,
+                                out["lat"].ctypes.data, out["lon"].ctypes.data, out["time"].ctypes.data,
+                                out["accuracy"].ctypes.data, out["true_edge"].ctypes.data,
+                                out["true_off"].ctypes.data)
+    if rc != 0:
+        raise RuntimeError("otm_synth_traces failed: %s" % _lib.last_error())
+    return out
+
+
+def cached_graph(config, cache_dir=None):
+    """Generate (once) the graph of a config under cache_dir; returns its path."""
+    cache_dir = cache_dir or os.environ.get("OTM_CACHE", "/tmp/otm_cache")
+    os.makedirs(cache_dir, exist_ok=True)
+    g = CONFIGS[config]["graph"]
+    tag = "_".join("%s%s" % (k, v) for k, v in sorted(g.items()))
+    path = os.path.join(cache_dir, "cfg%d_%s.otmg" % (config, tag))
+    if not os.path.exists(path):
+        tmp = path + ".%d.tmp" % os.getpid()
+        make_graph(tmp, **g)
+        os.replace(tmp, path)
+    return path
+
+
+def slice_batch(b, t0, t1):
+    """Traces [t0, t1) of a batch as a new batch (offsets rebased)."""
+    a, e = int(b["trace_off"][t0]), int(b["trace_off"][t1])
+    out = {k: b[k][a:e] for k in ("lat", "lon", "time", "accuracy", "true_edge", "true_off") if k in b}
+    out["trace_off"] = b["trace_off"][t0:t1 + 1] - a
+    return out

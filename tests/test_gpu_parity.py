@@ -1,0 +1,176 @@
+"""GPU parity: libotmatch's HIP path vs the CPU oracle, bit for bit.
+
+Every comparison goes through the C ABI (reporter_amd.Engine ->
+libotmatch.so).  Integer / index outputs and the float stage outputs are
+compared exactly: the kernels follow the oracle's float evaluation order with
+FMA contraction off.  Times and speeds are doubles computed by
+the same expressions, also compared exactly (north star allows 1e-3
+relative; we hold ourselves to 0).
+"""
+import json
+
+import numpy as np
+import numpy.testing as npt
+import pytest
+
+from reporter_amd import Engine, encode_request, synth
+
+pytestmark = pytest.mark.gpu
+
+KMAX = 32
+
+
+def _stage_compare(eng, orc, batch):
+    P = len(batch["lat"])
+    nc_g = eng.debug("ncand")[:P]
+    npt.assert_array_equal(nc_g, orc["ncand"], err_msg="ncand")
+    mask = (np.arange(KMAX)[None, :] < nc_g[:, None]).ravel()
+    for name in ("cand_edge", "cand_off", "cand_emis"):
+        g = eng.debug(name)[:P * KMAX]
+        npt.assert_array_equal(g[mask], orc[name][mask], err_msg=name)
+    npt.assert_array_equal(eng.debug("gc")[:P], orc["gc"], err_msg="gc")
+    npt.assert_array_equal(eng.debug("col_prev")[:P], orc["col_prev"], err_msg="col_prev")
+    toff = eng.debug("trans_off")[:P + 1]
+    npt.assert_array_equal(toff, orc["trans_off"], err_msg="trans_off")
+    # transitions of traces without errors (the oracle skips errored traces)
+    ok_pts = np.zeros(P, bool)
+    tr = orc["traces"]
+    off = batch["trace_off"]
+    for t in range(len(tr)):
+        if tr["error_kind"][t] == 0:
+            ok_pts[off[t]:off[t + 1]] = True
+    tg = eng.debug("trans")
+    sel = np.zeros(int(toff[-1]), bool)
+    for p in np.nonzero(ok_pts & (orc["col_prev"] >= 0))[0]:
+        sel[toff[p]:toff[p + 1]] = True
+    npt.assert_array_equal(tg[:len(sel)][sel], orc["trans"][sel], err_msg="trans")
+    npt.assert_array_equal(eng.debug("state")[:P], orc["state"], err_msg="state")
+    npt.assert_array_equal(eng.debug("route_dist")[:P], orc["route_dist"], err_msg="route_dist")
+
+
+def _run_both(graph, batch, oracle, results_equal, meili=None, stages=True, counters=True):
+    meili = meili or {}
+    with Engine(graph_path=graph, **meili) as eng:
+        eng.set_counting(counters)
+        res = eng.match(batch)
+        p = oracle.params(**meili)
+        orc = oracle.match_batch(oracle.Graph(graph), batch, p=p, keep_stages=True, nthreads=4)
+        if stages:
+            _stage_compare(eng, orc, batch)
+        results_equal(orc, res, "final")
+        if counters:
+            c = eng.counters()
+            for k, v in orc["counters"].items():
+                if k in ("edges_projected_unique", "shape_points_projected"):
+                    continue
+                assert c[k] == v, "counter %s gpu %d oracle %d" % (k, c[k], v)
+        return res, orc
+
+
+def test_city_sample_sigma15(small_graph, oracle, results_equal):
+    b = synth.make_traces(small_graph, 200, 100, interval_s=5.0, noise_sigma_m=15.0, accuracy=15.0, seed=11)
+    res, orc = _run_both(small_graph, b, oracle, results_equal)
+    assert (res.traces["code"] == 200).mean() > 0.95
+    assert len(res.segments) > 1000 and len(res.reports) > 50
+
+
+def test_noise_free_traces(small_graph, oracle, results_equal):
+    b = synth.make_traces(small_graph, 100, 60, interval_s=5.0, noise_sigma_m=0.0, accuracy=0.0, seed=3)
+    _run_both(small_graph, b, oracle, results_equal)
+
+
+def test_high_noise_sparse_rural(rural_graph, oracle, results_equal):
+    b = synth.make_traces(rural_graph, 100, 100, interval_s=30.0, noise_sigma_m=50.0, accuracy=50.0, seed=5)
+    _run_both(rural_graph, b, oracle, results_equal, meili=dict(search_radius=100.0, max_search_radius=100.0))
+
+
+def test_long_gaps_force_global_tier(small_graph, oracle, results_equal):
+    # 120 s sampling: bounds of 5 x gc reach kilometres -> searches overflow
+    # the LDS tier and finish in the global-memory tier, same fixed point
+    b = synth.make_traces(small_graph, 60, 30, interval_s=120.0, noise_sigma_m=10.0, accuracy=10.0, seed=9)
+    _run_both(small_graph, b, oracle, results_equal)
+
+
+def test_edge_cases(small_graph, oracle, results_equal):
+    base = synth.make_traces(small_graph, 8, 20, interval_s=5.0, noise_sigma_m=15.0, accuracy=15.0, seed=21)
+    lat, lon, tm, acc = (list(base[k]) for k in ("lat", "lon", "time", "accuracy"))
+    off = list(base["trace_off"])
+    # one-point trace, stationary duplicate points, far-off-graph points, a big gap
+    extra = [
+        ([lat[0]], [lon[0]], [tm[0]], [15.0]),
+        ([lat[1]] * 5, [lon[1]] * 5, [tm[1] + k for k in range(5)], [15.0] * 5),
+        ([lat[2] + 1.0, lat[2] + 1.0001], [lon[2], lon[2]], [tm[2], tm[2] + 5], [15.0, 15.0]),
+        ([lat[3], lat[60], lat[61]], [lon[3], lon[60], lon[61]], [tm[3], tm[3] + 10, tm[3] + 15], [0.0, -1.0, 500.0]),
+    ]
+    for la, lo, t, a in extra:
+        lat += la
+        lon += lo
+        tm += t
+        acc += a
+        off.append(off[-1] + len(la))
+    b = dict(trace_off=np.array(off, np.int64), lat=np.array(lat, np.float32), lon=np.array(lon, np.float32),
+             time=np.array(tm, np.float64), accuracy=np.array(acc, np.float32))
+    _run_both(small_graph, b, oracle, results_equal)
+
+
+def test_empty_batch(small_graph):
+    with Engine(graph_path=small_graph) as eng:
+        r = eng.match(dict(trace_off=np.zeros(1, np.int64), lat=np.zeros(0, np.float32),
+                           lon=np.zeros(0, np.float32), time=np.zeros(0), accuracy=np.zeros(0, np.float32)))
+        assert len(r.traces) == 0 and len(r.segments) == 0
+
+
+def test_deterministic_repeat(small_graph):
+    b = synth.make_traces(small_graph, 100, 100, seed=13)
+    with Engine(graph_path=small_graph) as eng:
+        r1 = eng.match(b)
+        r2 = eng.match(b)
+    for a, c in ((r1.traces, r2.traces), (r1.segments, r2.segments), (r1.reports, r2.reports)):
+        assert a.tobytes() == c.tobytes()
+
+
+def test_json_report_path_byte_equal(small_graph, oracle):
+    b = synth.make_traces(small_graph, 40, 60, seed=17)
+    bodies = []
+    for t in range(40):
+        a, e = b["trace_off"][t], b["trace_off"][t + 1]
+        bodies.append(encode_request("veh%d" % t, b["lat"][a:e], b["lon"][a:e], b["time"][a:e].astype(np.int64),
+                                     b["accuracy"][a:e].astype(np.int32)))
+    bodies += [b"", b"[]", b'{"uuid":"x","trace":[]}', b'{"uuid":"x","trace":[{"lat":1}]}',
+               b'{"uuid":"x","trace":[{"lat":1},{"lon":2}]}']
+    g = oracle.Graph(small_graph)
+    with Engine(graph_path=small_graph) as eng:
+        got = eng.report_batch(bodies)
+        single = eng.report(bodies[0])
+        for body, (code, resp) in zip(bodies, got):
+            ecode, eresp = oracle.handle_request(g, body)
+            assert (code, resp) == (ecode, eresp), body[:80]
+        assert single == got[0]
+        # Match JSON (valhalla.SegmentMatcher().Match equivalent)
+        for body in bodies[:5]:
+            assert eng.match_json(body) == oracle.match_json(g, body)
+        # async submit/poll returns the same bodies
+        for k, body in enumerate(bodies[:10]):
+            eng.submit(body, k)
+        seen = {}
+        while len(seen) < 10:
+            for tag, code, resp in eng.poll(64, 2000000):
+                seen[tag] = (code, resp)
+        for k in range(10):
+            assert seen[k] == got[k]
+
+
+def test_histogram_matches_reports(small_graph):
+    import torch
+    b = synth.make_traces(small_graph, 300, 100, seed=23)
+    with Engine(graph_path=small_graph) as eng:
+        nseg = eng.graph_info()["segments"]
+        h = torch.zeros(nseg * 16, dtype=torch.int32, device="cuda:0")
+        eng.hist_bind(h, 16, 10.0)
+        r = eng.match(b)
+        eng.hist_bind(None, 0, 1.0)
+        torch.cuda.synchronize()
+        ok = (r.reports["flags"] & 1) == 0
+        speed = r.reports["length"] / (r.reports["t1"] - r.reports["t0"]) * 3.6
+        ok &= speed >= 0
+        assert int(h.sum().item()) == int(ok.sum())

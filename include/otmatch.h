@@ -222,12 +222,21 @@ int otm_hist_bind(otm_engine* eng, void* dev_counts, int nbins, float bin_kph);
 int otm_graph_info(const otm_engine* eng, int64_t* n_nodes, int64_t* n_edges,
                    int64_t* n_segments);
 
+/* The bounded distance index built at engine creation (config
+ * "otm":{"index_radius_m": R}, default 1000, 0 = none): for every node, all
+ * nodes within R road metres with their distance and predecessor edge.
+ * Transition and route queries whose bound 5 x gc exceeds R, or whose row
+ * overflowed the builder, run the online bounded search instead; the results
+ * are identical either way. */
+int otm_index_info(const otm_engine* eng, float* rmax, int64_t* entries,
+                   int32_t* incomplete_rows, float* build_ms);
+
 /* Work counters of the last batch (for the roofline's algorithmic bytes). */
 typedef struct otm_work_counters {
-  int64_t points, columns, cells_visited, cell_entries_scanned;
-  int64_t edges_projected_unique, shape_points_projected, candidates;
-  int64_t searches, nodes_settled, edges_relaxed, transitions;
-  int64_t route_searches, route_edges, segments_out, reports_out;
+  int64_t points, columns, cells_visited, cell_entries_scanned, candidates;
+  int64_t searches, nodes_settled, edges_relaxed, transitions; /* K4 */
+  int64_t route_searches, route_nodes_settled, route_edges_relaxed, route_edges; /* K6 */
+  int64_t segments_out, reports_out;
 } otm_work_counters;
 /* Enable (1) or disable (0) counting; counting runs extra atomics, so timed
  * runs keep it off. */
@@ -280,6 +289,7 @@ typedef struct otm_synth_trace_params {
   double t0;
   uint64_t seed;
   int32_t vehicle_offset; /* global index of vehicle 0 (for sharding) */
+  const int32_t* vehicle_ids; /* optional: global index of each vehicle */
 } otm_synth_trace_params;
 /* Fills caller-allocated arrays sized n_vehicles*points_per_vehicle (lat,
  * lon, time, accuracy, true_edge, true_off) and n_vehicles+1 (trace_off).

@@ -335,7 +335,7 @@ static hnode hpop(ws* w) {
 /* Labels D(v) for every v with D(v) <= B from source node u (D(u) = 0).
  * pred(v) = the lexicographically smallest (D(w) + len(e), e) over in-edges.
  * Returns 0, or -1 when more than ORC_SEARCH_LIMIT nodes are labelled. */
-static int dijkstra(const orc_graph* g, ws* w, int32_t u, float B, orc_counters* C) {
+static int dijkstra(const orc_graph* g, ws* w, int32_t u, float B, orc_counters* C, int route) {
   if (++w->stamp == 0) {
     memset(w->lab, 0, sizeof(uint32_t) * (size_t)g->h.n_nodes);
     memset(w->done, 0, sizeof(uint32_t) * (size_t)g->h.n_nodes);
@@ -375,9 +375,15 @@ static int dijkstra(const orc_graph* g, ws* w, int32_t u, float B, orc_counters*
       }
     }
   }
-  C->searches++;
-  C->nodes_settled += w->nlab;
-  C->edges_relaxed += relaxed;
+  if (route) {
+    C->route_searches++;
+    C->route_nodes_settled += w->nlab;
+    C->route_edges_relaxed += relaxed;
+  } else {
+    C->searches++;
+    C->nodes_settled += w->nlab;
+    C->edges_relaxed += relaxed;
+  }
   return 0;
 }
 
@@ -477,7 +483,7 @@ static int transitions(batch* B, ws* w, int64_t p, orc_counters* C) {
   }
   for (int s = 0; s < ns; ++s) {
     const int32_t u = srcs[s];
-    if (dijkstra(g, w, u, bound, C) < 0) return -1;
+    if (dijkstra(g, w, u, bound, C, 0) < 0) return -1;
     for (int i = 0; i < Kq; ++i) {
       if (g->eto[eq[i]] != u) continue;
       const float start = g->elen[eq[i]] - oq[i];
@@ -678,8 +684,7 @@ static int route_step(batch* B, ws* w, int64_t p, int32_t* path, int* plen, int*
   *same = 0;
   const float bound = B->P->max_route_distance_factor * B->gc[p];
   const int32_t u = g->eto[ei], v = g->efrom[ej];
-  if (dijkstra(g, w, u, bound, C) < 0) return -1;
-  C->route_searches++;
+  if (dijkstra(g, w, u, bound, C, 1) < 0) return -1;
   int n = 0;
   for (int32_t x = v; x != u;) {
     const int32_t e = w->pred[x];

@@ -65,10 +65,10 @@ typedef struct orc_trace_result {
 } orc_trace_result;
 
 typedef struct orc_counters {
-  int64_t points, columns, cells_visited, cell_entries_scanned;
-  int64_t edges_projected_unique, shape_points_projected, candidates;
+  int64_t points, columns, cells_visited, cell_entries_scanned, candidates;
   int64_t searches, nodes_settled, edges_relaxed, transitions;
-  int64_t route_searches, route_edges, segments_out, reports_out;
+  int64_t route_searches, route_nodes_settled, route_edges_relaxed, route_edges;
+  int64_t segments_out, reports_out;
 } orc_counters;
 
 typedef struct orc_results {

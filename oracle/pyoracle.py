@@ -21,9 +21,9 @@ TRACE_DTYPE = np.dtype([(n, "<i4") for n in (
     "code", "error_kind", "seg_off", "seg_cnt", "rep_off", "rep_cnt", "shape_used", "successful_count",
     "unreported_count", "discontinuities", "invalid_speeds", "unassociated", "successful_length",
     "unreported_length")])
-COUNTER_NAMES = ("points", "columns", "cells_visited", "cell_entries_scanned", "edges_projected_unique",
-                 "shape_points_projected", "candidates", "searches", "nodes_settled", "edges_relaxed",
-                 "transitions", "route_searches", "route_edges", "segments_out", "reports_out")
+COUNTER_NAMES = ("points", "columns", "cells_visited", "cell_entries_scanned", "candidates", "searches", "nodes_settled",
+                 "edges_relaxed", "transitions", "route_searches", "route_nodes_settled", "route_edges_relaxed",
+                 "route_edges", "segments_out", "reports_out")
 
 
 class Params(C.Structure):
@@ -203,8 +203,8 @@ def handle_request(graph, body, p=None, rc=None, path="/report"):
         body = body.encode("utf-8")
     out = C.c_void_p()
     n = C.c_size_t()
-    code = lib().orc_handle_request(graph.h, C.byref(p), C.byref(rc), path.encode(), body, len(body),
-                                    C.byref(out), C.byref(n))
+    code = lib().orc_handle_request(graph.h if graph is not None else None, C.byref(p), C.byref(rc), path.encode(),
+                                    body, len(body), C.byref(out), C.byref(n))
     return code, _take(out, n.value).decode("utf-8")
 
 

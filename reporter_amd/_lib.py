@@ -32,9 +32,9 @@ class Result(C.Structure):
     _fields_ = [("tag", C.c_uint64), ("code", C.c_int), ("body", C.c_void_p), ("body_len", C.c_size_t)]
 
 
-COUNTER_NAMES = ("points", "columns", "cells_visited", "cell_entries_scanned", "edges_projected_unique",
-                 "shape_points_projected", "candidates", "searches", "nodes_settled", "edges_relaxed",
-                 "transitions", "route_searches", "route_edges", "segments_out", "reports_out")
+COUNTER_NAMES = ("points", "columns", "cells_visited", "cell_entries_scanned", "candidates", "searches", "nodes_settled",
+                 "edges_relaxed", "transitions", "route_searches", "route_nodes_settled", "route_edges_relaxed",
+                 "route_edges", "segments_out", "reports_out")
 
 
 class WorkCounters(C.Structure):
@@ -52,7 +52,7 @@ class SynthGraphParams(C.Structure):
 class SynthTraceParams(C.Structure):
     _fields_ = [("n_vehicles", C.c_int32), ("points_per_vehicle", C.c_int32), ("interval_s", C.c_double),
                 ("noise_sigma_m", C.c_double), ("accuracy", C.c_float), ("t0", C.c_double), ("seed", C.c_uint64),
-                ("vehicle_offset", C.c_int32)]
+                ("vehicle_offset", C.c_int32), ("vehicle_ids", C.c_void_p)]
 
 
 SEGMENT_DTYPE = np.dtype([("segment_id", "<i8"), ("start_time", "<f8"), ("end_time", "<f8"), ("length", "<i4"),
@@ -92,6 +92,8 @@ def _declare(L):
         "otm_fetch_results": (C.c_int, [vp, C.POINTER(Results)]),
         "otm_hist_bind": (C.c_int, [vp, vp, C.c_int, C.c_float]),
         "otm_graph_info": (C.c_int, [vp, C.POINTER(i64), C.POINTER(i64), C.POINTER(i64)]),
+        "otm_index_info": (C.c_int, [vp, C.POINTER(C.c_float), C.POINTER(i64), C.POINTER(i32),
+                                     C.POINTER(C.c_float)]),
         "otm_set_counting": (C.c_int, [vp, C.c_int]),
         "otm_get_counters": (C.c_int, [vp, C.POINTER(WorkCounters)]),
         "otm_set_timing": (C.c_int, [vp, C.c_int]),

@@ -243,6 +243,8 @@ int otm_engine_create(const char* cfg_path, const int* devices, int ndev, otm_en
     if (sl != std::string::npos) graph = c.substr(0, sl + 1) + graph;
   }
   auto* E = new otm_engine();
+  const Value* ir = o->get("index_radius_m");
+  if (ir && ir->is_num()) E->index_rmax = (float)ir->num();
   const Value* meili = cfg.get("meili");
   const Value* dflt = meili ? meili->get("default") : nullptr;
   if (dflt && dflt->kind == Kind::Obj) {
@@ -466,6 +468,15 @@ int otm_graph_info(const otm_engine* E, int64_t* n_nodes, int64_t* n_edges, int6
   if (n_nodes) *n_nodes = E->host.h.n_nodes;
   if (n_edges) *n_edges = E->host.h.n_edges;
   if (n_segments) *n_segments = E->host.h.n_segments;
+  return OTM_OK;
+}
+
+int otm_index_info(const otm_engine* E, float* rmax, int64_t* entries, int32_t* incomplete_rows, float* build_ms) {
+  if (!E) return fail(OTM_EINVAL, "engine is NULL");
+  if (rmax) *rmax = E->idx.rmax;
+  if (entries) *entries = E->index_entries;
+  if (incomplete_rows) *incomplete_rows = E->index_incomplete_rows;
+  if (build_ms) *build_ms = E->index_build_ms;
   return OTM_OK;
 }
 

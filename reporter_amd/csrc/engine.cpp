@@ -35,6 +35,8 @@ static T* P(otm_engine::Buf& b) {
   return (T*)b.p;
 }
 
+int build_index(otm_engine* E, std::string* err);
+
 int engine_init(otm_engine* E, const char* graph_path, int device, std::string* err) {
   int rc = load_graph(graph_path, &E->host, err);
   if (rc) return rc;
@@ -87,6 +89,65 @@ int engine_init(otm_engine* E, const char* graph_path, int device, std::string* 
   HIPCHK(hipMalloc((void**)&E->ctr_save, sizeof(DevCounters)));
   HIPCHK(hipMemset(E->ctr, 0, sizeof(DevCounters)));
   for (auto& e : E->ev) HIPCHK(hipEventCreate(&e));
+  return build_index(E, err);
+}
+
+// Bounded distance index: part of flattening the graph into HBM, like the
+// tile preprocessing behind valhalla.Configure (py/reporter_service.py:279).
+// Row u = every node within rmax road metres of u, with D and predecessor
+// edge, sorted by node id.  Two passes of the same deterministic search:
+// count, scan, write.
+int build_index(otm_engine* E, std::string* err) {
+  E->idx = DevIndex{};
+  E->idx.rmax = 0.0f;
+  if (!(E->index_rmax > 0.0f)) return OTM_OK;
+  const int32_t N = E->g.n_nodes;
+  hipStream_t s = E->stream;
+  hipEvent_t a, z;
+  HIPCHK(hipEventCreate(&a));
+  HIPCHK(hipEventCreate(&z));
+  HIPCHK(hipEventRecord(a, s));
+  int32_t* row_cnt = nullptr;
+  int64_t* row_off = nullptr;
+  HIPCHK(hipMalloc(&row_cnt, ((size_t)N + 1) * 4));
+  E->graph_allocs.push_back(row_cnt);
+  HIPCHK(hipMalloc(&row_off, ((size_t)N + 1) * 8));
+  E->graph_allocs.push_back(row_off);
+  launch_index_build(E->g, E->index_rmax, row_cnt, nullptr, nullptr, nullptr, nullptr, false, s);
+  launch_row_sizes(row_cnt, row_off, N, s);
+  size_t tmpb = scan_tmp_bytes(N) + 256;
+  void* tmp = nullptr;
+  HIPCHK(hipMalloc(&tmp, tmpb));
+  scan_i64(row_off, N, tmp, tmpb, s);
+  int64_t total = 0;
+  HIPCHK(hipMemcpyAsync(&total, row_off + N, 8, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  (void)hipFree(tmp);
+  void *node = nullptr, *dist = nullptr, *pred = nullptr;
+  HIPCHK(hipMalloc(&node, ((size_t)total + 1) * 4));
+  E->graph_allocs.push_back(node);
+  HIPCHK(hipMalloc(&dist, ((size_t)total + 1) * 4));
+  E->graph_allocs.push_back(dist);
+  HIPCHK(hipMalloc(&pred, ((size_t)total + 1) * 4));
+  E->graph_allocs.push_back(pred);
+  launch_index_build(E->g, E->index_rmax, row_cnt, row_off, (uint32_t*)node, (float*)dist, (int32_t*)pred, true, s);
+  HIPCHK(hipEventRecord(z, s));
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventSynchronize(z));
+  HIPCHK(hipEventElapsedTime(&E->index_build_ms, a, z));
+  (void)hipEventDestroy(a);
+  (void)hipEventDestroy(z);
+  std::vector<int32_t> cnt((size_t)N);
+  HIPCHK(hipMemcpy(cnt.data(), row_cnt, (size_t)N * 4, hipMemcpyDeviceToHost));
+  E->index_incomplete_rows = 0;
+  for (int32_t c : cnt) E->index_incomplete_rows += c < 0;
+  E->index_entries = total;
+  E->idx.rmax = E->index_rmax;
+  E->idx.row_cnt = row_cnt;
+  E->idx.row_off = row_off;
+  E->idx.node = (const uint32_t*)node;
+  E->idx.dist = (const float*)dist;
+  E->idx.pred = (const int32_t*)pred;
   return OTM_OK;
 }
 
@@ -94,14 +155,14 @@ void engine_free(otm_engine* E) {
   if (E->device >= 0) (void)hipSetDevice(E->device);
   for (void* p : E->graph_allocs) (void)hipFree(p);
   E->graph_allocs.clear();
-  otm_engine::Buf* bufs[] = {&E->in_off,      &E->in_lat,      &E->in_lon,     &E->in_time,       &E->in_acc,
-                             &E->pt_trace,    &E->is_col,      &E->prevc,      &E->gc,            &E->ncand,
-                             &E->cand_edge,   &E->cand_off,    &E->cand_emis,  &E->col_prev,      &E->trans_off,
-                             &E->trans,       &E->bp,          &E->state,      &E->chain_start,   &E->route_dist,
-                             &E->path_off,    &E->path_len,    &E->path_pool,  &E->trace_err,     &E->overflow_list,
-                             &E->counters_i32, &E->scan_tmp,   &E->big_key,    &E->big_lab,       &E->big_inq,
-                             &E->big_fr,      &E->o_traces,    &E->o_seg_cnt,  &E->o_way_cnt,     &E->o_segments,
-                             &E->o_seg_gidx,  &E->o_way_ids,   &E->o_reports};
+  otm_engine::Buf* bufs[] = {
+      &E->in_off,        &E->in_lat,       &E->in_lon,         &E->in_time,        &E->in_acc,     &E->pt_trace,
+      &E->is_col,        &E->prevc,        &E->gc,             &E->ncand,          &E->cand_edge,  &E->cand_off,
+      &E->cand_emis,     &E->col_prev,     &E->trans_off,      &E->trans,          &E->bp,         &E->state,
+      &E->chain_start,   &E->route_dist,   &E->path_off,       &E->path_len,       &E->path_pool,  &E->trace_err,
+      &E->overflow_list0, &E->overflow_list, &E->overflow_list2, &E->counters_i32, &E->scan_tmp,   &E->big_key,
+      &E->big_lab,       &E->big_inq,      &E->big_fr,         &E->o_traces,       &E->o_seg_cnt,  &E->o_way_cnt,
+      &E->o_segments,    &E->o_seg_gidx,   &E->o_way_ids,      &E->o_reports};
   for (auto* b : bufs) {
     if (b->p) (void)hipFree(b->p);
     b->p = nullptr;
@@ -151,7 +212,9 @@ int engine_match(otm_engine* E, const DevBatch& b, hipStream_t s, std::string* e
   ENS(path_off, Pn * 4);
   ENS(path_len, Pn * 4);
   ENS(trace_err, ((size_t)NT + 1) * 4);
+  ENS(overflow_list0, Pn * 4);
   ENS(overflow_list, Pn * 4);
+  ENS(overflow_list2, Pn * 4);
   ENS(counters_i32, 64);
   ENS(o_traces, ((size_t)NT + 1) * sizeof(otm_trace_result));
   ENS(o_seg_cnt, ((size_t)NT + 1) * 4);
@@ -182,18 +245,25 @@ int engine_match(otm_engine* E, const DevBatch& b, hipStream_t s, std::string* e
   w.path_pool = P<int32_t>(E->path_pool);
   w.pool_cap = E->pool_cap;
   w.trace_err = P<int32_t>(E->trace_err);
+  w.overflow_list0 = P<int32_t>(E->overflow_list0);
   w.overflow_list = P<int32_t>(E->overflow_list);
+  w.overflow_list2 = P<int32_t>(E->overflow_list2);
+  w.idx = E->idx;
   w.counters_i32 = P<int32_t>(E->counters_i32);
   w.ctr = E->counting ? E->ctr : nullptr;
   if (E->counting) HIPCHK(hipMemsetAsync(E->ctr, 0, sizeof(DevCounters), s));
-  if (E->timing) HIPCHK(hipEventRecord(E->ev[0], s));
-
+#define EV(k) \
+  if (E->timing) HIPCHK(hipEventRecord(E->ev[k], s));
+  EV(0);
   launch_columns(b, E->dp, w, s);
-  if (E->timing) HIPCHK(hipEventRecord(E->ev[1], s));
+  EV(1);
+  EV(2);
   launch_candidates(E->g, b, E->dp, w, s);
-  if (E->timing) HIPCHK(hipEventRecord(E->ev[2], s));
+  EV(3);
+  EV(4);
   launch_links(b, E->dp, w, s);
   scan_i64(w.trans_off, NP, E->scan_tmp.p, E->scan_tmp.cap, s);
+  EV(5);
   int64_t ttotal = 0;
   HIPCHK(hipMemcpyAsync(&ttotal, w.trans_off + NP, 8, hipMemcpyDeviceToHost, s));
   HIPCHK(hipMemsetAsync(w.counters_i32, 0, 64, s));
@@ -201,22 +271,17 @@ int engine_match(otm_engine* E, const DevBatch& b, hipStream_t s, std::string* e
   E->last_trans = ttotal;
   ENS(trans, ((size_t)ttotal + 1) * 4);
   w.trans = P<float>(E->trans);
-  if (E->timing) HIPCHK(hipEventRecord(E->ev[3], s));
-  launch_transitions(E->g, b, E->dp, w, 0, false, s);
-  int32_t nover = 0;
-  HIPCHK(hipMemcpyAsync(&nover, w.counters_i32, 4, hipMemcpyDeviceToHost, s));
-  HIPCHK(hipStreamSynchronize(s));
-  if (nover > 0) {
-    if ((rc = ensure_big(E, err))) return rc;
-    w.big_key = P<uint32_t>(E->big_key);
-    w.big_lab = P<unsigned long long>(E->big_lab);
-    w.big_inq = P<uint32_t>(E->big_inq);
-    w.big_fr = P<uint32_t>(E->big_fr);
-    launch_transitions(E->g, b, E->dp, w, nover, true, s);
-  }
-  if (E->timing) HIPCHK(hipEventRecord(E->ev[4], s));
+  if ((rc = ensure_big(E, err))) return rc;
+  w.big_key = P<uint32_t>(E->big_key);
+  w.big_lab = P<unsigned long long>(E->big_lab);
+  w.big_inq = P<uint32_t>(E->big_inq);
+  w.big_fr = P<uint32_t>(E->big_fr);
+  EV(6);
+  launch_transitions(E->g, b, E->dp, w, s);
+  EV(7);
+  EV(8);
   launch_viterbi(b, w, s);
-  if (E->timing) HIPCHK(hipEventRecord(E->ev[5], s));
+  EV(9);
   // a path-pool overflow redoes the whole stage: restore the work counters
   // so the redone searches are counted once
   if (E->counting) HIPCHK(hipMemcpyAsync(E->ctr_save, E->ctr, sizeof(DevCounters), hipMemcpyDeviceToDevice, s));
@@ -224,20 +289,12 @@ int engine_match(otm_engine* E, const DevBatch& b, hipStream_t s, std::string* e
     if (E->counting && attempt > 0)
       HIPCHK(hipMemcpyAsync(E->ctr, E->ctr_save, sizeof(DevCounters), hipMemcpyDeviceToDevice, s));
     HIPCHK(hipMemsetAsync(w.counters_i32, 0, 64, s));
-    launch_route(E->g, b, E->dp, w, 0, false, s);
+    EV(10);
+    launch_route(E->g, b, E->dp, w, s);
+    EV(11);
     int32_t cnt[3] = {0, 0, 0};
     HIPCHK(hipMemcpyAsync(cnt, w.counters_i32, 12, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
-    if (cnt[0] > 0) {
-      if ((rc = ensure_big(E, err))) return rc;
-      w.big_key = P<uint32_t>(E->big_key);
-      w.big_lab = P<unsigned long long>(E->big_lab);
-      w.big_inq = P<uint32_t>(E->big_inq);
-      w.big_fr = P<uint32_t>(E->big_fr);
-      launch_route(E->g, b, E->dp, w, cnt[0], true, s);
-      HIPCHK(hipMemcpyAsync(cnt, w.counters_i32, 12, hipMemcpyDeviceToHost, s));
-      HIPCHK(hipStreamSynchronize(s));
-    }
     if (!cnt[2]) break;
     // path pool too small: grow to what was requested and redo the stage
     E->pool_cap = (int32_t)((size_t)cnt[1] * 2 + 1024);
@@ -249,7 +306,6 @@ int engine_match(otm_engine* E, const DevBatch& b, hipStream_t s, std::string* e
       return OTM_EDEVICE;
     }
   }
-  if (E->timing) HIPCHK(hipEventRecord(E->ev[6], s));
 
   DevOut o{};
   o.traces = E->o_traces.p;
@@ -260,7 +316,9 @@ int engine_match(otm_engine* E, const DevBatch& b, hipStream_t s, std::string* e
   o.bin_kph = E->bin_kph;
   HIPCHK(hipMemsetAsync(o.seg_cnt + NT, 0, 4, s));
   HIPCHK(hipMemsetAsync(o.way_cnt + NT, 0, 4, s));
+  EV(12);
   launch_segments(E->g, b, w, o, false, s);
+  EV(13);
   scan_i32(o.seg_cnt, NT, E->scan_tmp.p, E->scan_tmp.cap, s);
   scan_i32(o.way_cnt, NT, E->scan_tmp.p, E->scan_tmp.cap, s);
   int32_t tot[2] = {0, 0};
@@ -276,17 +334,23 @@ int engine_match(otm_engine* E, const DevBatch& b, hipStream_t s, std::string* e
   o.reports = E->o_reports.p;
   o.way_ids = P<int64_t>(E->o_way_ids);
   launch_segments(E->g, b, w, o, true, s);
-  if (E->timing) HIPCHK(hipEventRecord(E->ev[7], s));
+  EV(14);
   launch_report(b, E->drc, w, o, s);
-  if (E->timing) HIPCHK(hipEventRecord(E->ev[8], s));
+  EV(15);
+#undef EV
   HIPCHK(hipGetLastError());
   E->last_T = NT;
   E->last_P = NP;
   E->last_S = tot[0];
   E->last_W = tot[1];
   if (E->timing) {
-    HIPCHK(hipEventSynchronize(E->ev[8]));
-    for (int k = 0; k < 8; ++k) HIPCHK(hipEventElapsedTime(&E->stage_ms[k], E->ev[k], E->ev[k + 1]));
+    // kernel-only spans on the launch stream (host syncs between stages excluded):
+    // columns, candidates, links+scan, transitions (LDS tier), viterbi, route
+    // (final attempt, LDS tier), segments count, segments write + report
+    HIPCHK(hipEventSynchronize(E->ev[15]));
+    const int a[8] = {0, 2, 4, 6, 8, 10, 12, 13};
+    const int z[8] = {1, 3, 5, 7, 9, 11, 13, 15};
+    for (int k = 0; k < 8; ++k) HIPCHK(hipEventElapsedTime(&E->stage_ms[k], E->ev[a[k]], E->ev[z[k]]));
   }
 #undef ENS
   return OTM_OK;

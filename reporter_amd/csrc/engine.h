@@ -19,6 +19,12 @@ struct otm_engine {
   otm::HostGraph host;
   otm::DevGraph g{};
   std::vector<void*> graph_allocs;
+  // bounded distance index (built at create time; rmax 0 disables)
+  float index_rmax = 1000.0f;
+  otm::DevIndex idx{};
+  int64_t index_entries = 0;
+  int32_t index_incomplete_rows = 0;
+  float index_build_ms = 0.0f;
   otm::MatchConfig mc;
   otm::ReportConfig rc;
   otm::DevParams dp{};
@@ -33,7 +39,8 @@ struct otm_engine {
   Buf in_off, in_lat, in_lon, in_time, in_acc;
   // work
   Buf pt_trace, is_col, prevc, gc, ncand, cand_edge, cand_off, cand_emis, col_prev, trans_off, trans, bp, state,
-      chain_start, route_dist, path_off, path_len, path_pool, trace_err, overflow_list, counters_i32, scan_tmp;
+      chain_start, route_dist, path_off, path_len, path_pool, trace_err, overflow_list0, overflow_list, overflow_list2,
+      counters_i32, scan_tmp;
   Buf big_key, big_lab, big_inq, big_fr;
   // outputs
   Buf o_traces, o_seg_cnt, o_way_cnt, o_segments, o_seg_gidx, o_way_ids, o_reports;
@@ -57,7 +64,7 @@ struct otm_engine {
   std::vector<int64_t> h_ways;
   // timing
   bool timing = false;
-  hipEvent_t ev[9] = {};
+  hipEvent_t ev[16] = {};
   float stage_ms[8] = {};
   // async submit/poll
   struct Pending {

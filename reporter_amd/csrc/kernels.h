@@ -45,6 +45,21 @@ struct DevGraph {
   double lat0, lon0, cell;
 };
 
+// Bounded distance index (built once per engine): for every
+// node u the nodes v with D(u,v) <= rmax, sorted by v, with D and the
+// predecessor edge of the search fixed point.  row_cnt[u] < 0 marks a row
+// whose search exceeded the build table (queries on it use the online tiers).
+struct DevIndex {
+  float rmax;  // 0: no index
+  const int32_t* row_cnt;
+  const int64_t* row_off;
+  const uint32_t* node;
+  const float* dist;
+  const int32_t* pred;
+};
+constexpr int INDEX_BUILD_CAP = 2048;   // LDS table of the index builder
+constexpr int INDEX_BUILD_LIMIT = 1536; // nodes per row before the row is left incomplete
+
 struct DevParams {
   float sigma_z, beta, factor, breakage, interp, search_radius, max_search_radius, gps_accuracy;
   int max_candidates;
@@ -68,10 +83,10 @@ struct DevBatch {
 
 // device counters, same order as otm_work_counters
 struct DevCounters {
-  unsigned long long points, columns, cells_visited, cell_entries_scanned;
-  unsigned long long edges_projected_unique, shape_points_projected, candidates;
+  unsigned long long points, columns, cells_visited, cell_entries_scanned, candidates;
   unsigned long long searches, nodes_settled, edges_relaxed, transitions;
-  unsigned long long route_searches, route_edges, segments_out, reports_out;
+  unsigned long long route_searches, route_nodes_settled, route_edges_relaxed, route_edges;
+  unsigned long long segments_out, reports_out;
 };
 
 // per-point / per-trace work arrays of one batch (device pointers)
@@ -96,8 +111,12 @@ struct DevWork {
   int32_t* path_pool;    // [pool_cap]
   int32_t pool_cap;
   int32_t* trace_err;    // [T]
-  int32_t* overflow_list;  // [P] points whose search spilled
-  int32_t* counters_i32;   // [0] overflow count, [1] pool used, [2] pool overflow flag
+  int32_t* overflow_list0; // [P] columns/steps the index could not answer
+  int32_t* overflow_list;  // [P] columns/steps the lane tier spilled
+  int32_t* overflow_list2; // [P] ... the LDS wave tier spilled
+  int32_t* counters_i32;   // [0] list 1 count, [1] pool used, [2] pool overflow flag, [3] list 2 count,
+                           // [4] list 0 count
+  DevIndex idx;
   // global-tier scratch
   uint32_t* big_key;
   unsigned long long* big_lab;
@@ -125,13 +144,17 @@ struct DevOut {
 void launch_columns(const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s);
 void launch_candidates(const DevGraph& g, const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s);
 void launch_links(const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s);
-void launch_transitions(const DevGraph& g, const DevBatch& b, const DevParams& p, DevWork& w, int32_t n_overflow,
-                        bool big_tier, hipStream_t s);
+// lane tier -> wave LDS tier -> global tier, spill lists on the device
+// (counters_i32[0] / [3] must be zero on entry)
+void launch_transitions(const DevGraph& g, const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s);
 void launch_viterbi(const DevBatch& b, DevWork& w, hipStream_t s);
-void launch_route(const DevGraph& g, const DevBatch& b, const DevParams& p, DevWork& w, int32_t n_overflow,
-                  bool big_tier, hipStream_t s);
+void launch_route(const DevGraph& g, const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s);
 void launch_segments(const DevGraph& g, const DevBatch& b, DevWork& w, DevOut& o, bool write, hipStream_t s);
 void launch_report(const DevBatch& b, const DevReportCfg& rc, DevWork& w, DevOut& o, hipStream_t s);
+// index build: pass 0 counts rows (row_cnt), pass 1 writes them at row_off
+void launch_index_build(const DevGraph& g, float rmax, int32_t* row_cnt, const int64_t* row_off, uint32_t* node,
+                        float* dist, int32_t* pred, bool write, hipStream_t s);
+void launch_row_sizes(const int32_t* row_cnt, int64_t* row_sizes, int32_t n, hipStream_t s);
 // exclusive scan helpers (in place over n+1 elements: out[n] = total)
 void scan_i64(int64_t* d, int64_t n, void* tmp, size_t tmp_bytes, hipStream_t s);
 void scan_i32(int32_t* d, int64_t n, void* tmp, size_t tmp_bytes, hipStream_t s);

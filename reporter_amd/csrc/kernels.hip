@@ -468,7 +468,508 @@ __device__ unsigned long long settled_outdeg(const DevGraph& g, const Table& T, 
   return s;
 }
 
-// ============================================================== K4 transitions
+// ============================================================== lane tier
+// Most bounded searches are tiny (city config: ~9 nodes settled, ~35 edges
+// relaxed), so the first tier runs one search per LANE: a plain Dijkstra with
+// linear-scan selection over a private table of LANE_CAP slots in LDS,
+// interleaved by thread (slot k of thread t at [k * blockDim + t]) so the 64
+// lanes of a wave hit 64 different banks.  Same fixed point as the wave tiers
+// (labels are the lexicographic min of (D(w)+len(e), e)); a search that needs
+// more than LANE_CAP nodes spills its whole column to the wave tier.
+constexpr uint32_t DONE = 0x80000000u;
+constexpr int LANE_TB = 128;
+
+// PRED: keep predecessor edges (the route stage needs them, transitions only
+// need distances -- 8 instead of 12 bytes per slot buys a larger table)
+template <int CAP, bool PRED>
+__device__ __forceinline__ int lane_search(const DevGraph& g, uint32_t* K, float* D, int32_t* Pd, int32_t u, float B,
+                                           unsigned long long& relaxed) {
+  constexpr int S = LANE_TB;
+  K[0] = (uint32_t)u;
+  D[0] = 0.0f;
+  if (PRED) Pd[0] = -1;
+  int n = 1;
+  while (true) {
+    int best = -1;
+    float bd = 0.0f;
+    for (int k = 0; k < n; ++k) {
+      if (!(K[k * S] & DONE)) {
+        const float d = D[k * S];
+        if (best < 0 || d < bd) {
+          best = k;
+          bd = d;
+        }
+      }
+    }
+    if (best < 0) break;
+    const uint32_t x = K[best * S];
+    K[best * S] = x | DONE;
+    const int32_t e0 = g.out_off[x], e1 = g.out_off[x + 1];
+    relaxed += (unsigned long long)(e1 - e0);
+    for (int32_t e = e0; e < e1; ++e) {
+      const float nd = bd + g.e_len[e];
+      if (!(nd <= B)) continue;
+      const uint32_t v = (uint32_t)g.e_to[e];
+      int f = -1;
+      for (int k = 0; k < n; ++k)
+        if ((K[k * S] & ~DONE) == v) {
+          f = k;
+          break;
+        }
+      if (f < 0) {
+        if (n == CAP) return -1;
+        K[n * S] = v;
+        D[n * S] = nd;
+        if (PRED) Pd[n * S] = e;
+        ++n;
+      } else {
+        const float dv = D[f * S];
+        if (nd < dv) {
+          D[f * S] = nd;
+          if (PRED) Pd[f * S] = e;
+        } else if (PRED && nd == dv && e < Pd[f * S]) {
+          Pd[f * S] = e;
+        }
+      }
+    }
+  }
+  return n;
+}
+
+template <int CAP>
+__device__ __forceinline__ int lane_find(const uint32_t* K, int n, uint32_t v) {
+  for (int k = 0; k < n; ++k)
+    if ((K[k * LANE_TB] & ~DONE) == v) return k;
+  return -1;
+}
+
+template <int CAP>
+__global__ __launch_bounds__(LANE_TB) void k_trans_lane(DevGraph g, DevBatch b, DevParams P, DevWork w) {
+  __shared__ uint32_t sK[CAP * LANE_TB];
+  __shared__ float sD[CAP * LANE_TB];
+  uint32_t* K = sK + threadIdx.x;
+  float* D = sD + threadIdx.x;
+  unsigned long long c_search = 0, c_settled = 0, c_relaxed = 0, c_trans = 0;
+  const int64_t nwork = w.counters_i32[4];  // columns the index could not answer
+  for (int64_t it = (int64_t)blockIdx.x * LANE_TB + threadIdx.x; it < nwork; it += (int64_t)gridDim.x * LANE_TB) {
+    const int64_t p = w.overflow_list0[it];
+    const int32_t q = w.col_prev[p];
+    const int Kq = w.ncand[q], Kp = w.ncand[p];
+    const float gcv = w.gc[p];
+    const float bound = P.factor * gcv;
+    const int32_t* eq = w.cand_edge + (int64_t)q * KMAX;
+    const float* oq = w.cand_off + (int64_t)q * KMAX;
+    const int32_t* ep = w.cand_edge + p * KMAX;
+    const float* op = w.cand_off + p * KMAX;
+    float* Tm = w.trans + w.trans_off[p];
+    unsigned long long s_search = 0, s_settled = 0, s_relaxed = 0, s_trans = 0;
+    bool failed = false;
+    for (int i = 0; i < Kq && !failed; ++i) {
+      const int32_t u = g.e_to[eq[i]];
+      bool first = true;
+      for (int k = 0; k < i; ++k)
+        if (g.e_to[eq[k]] == u) {
+          first = false;
+          break;
+        }
+      if (!first) continue;
+      unsigned long long rel = 0;
+      const int n = lane_search<CAP, false>(g, K, D, nullptr, u, bound, rel);
+      if (n < 0) {
+        failed = true;
+        break;
+      }
+      ++s_search;
+      s_settled += (unsigned long long)n;
+      s_relaxed += rel;
+      for (int ii = i; ii < Kq; ++ii) {
+        if (g.e_to[eq[ii]] != u) continue;
+        const float start = g.e_len[eq[ii]] - oq[ii];
+        for (int j = 0; j < Kp; ++j) {
+          float r;
+          bool ok = true;
+          if (ep[j] == eq[ii] && op[j] >= oq[ii]) {
+            r = op[j] - oq[ii];
+          } else {
+            const int f = lane_find<CAP>(K, n, (uint32_t)g.e_from[ep[j]]);
+            if (f < 0) {
+              ok = false;
+              r = 0.0f;
+            } else {
+              const float sd = start + D[f * LANE_TB];
+              r = sd + op[j];
+            }
+          }
+          float cost = INFINITY;
+          if (ok && r <= bound) {
+            const float diff = fabsf(r - gcv);
+            cost = diff / P.beta;
+            ++s_trans;
+          }
+          Tm[ii * Kp + j] = cost;
+        }
+      }
+    }
+    if (failed) {
+      const int slot = atomicAdd(&w.counters_i32[0], 1);
+      w.overflow_list[slot] = (int32_t)p;
+    } else {
+      c_search += s_search;
+      c_settled += s_settled;
+      c_relaxed += s_relaxed;
+      c_trans += s_trans;
+    }
+  }
+  if (w.ctr) {
+    cadd(&w.ctr->searches, c_search);
+    cadd(&w.ctr->nodes_settled, c_settled);
+    cadd(&w.ctr->edges_relaxed, c_relaxed);
+    cadd(&w.ctr->transitions, c_trans);
+  }
+}
+
+template <int CAP>
+__global__ __launch_bounds__(LANE_TB) void k_route_lane(DevGraph g, DevBatch b, DevParams P, DevWork w) {
+  __shared__ uint32_t sK[CAP * LANE_TB];
+  __shared__ float sD[CAP * LANE_TB];
+  __shared__ int32_t sP[CAP * LANE_TB];
+  uint32_t* K = sK + threadIdx.x;
+  float* D = sD + threadIdx.x;
+  int32_t* Pd = sP + threadIdx.x;
+  unsigned long long c_search = 0, c_settled = 0, c_relaxed = 0, c_edges = 0;
+  const int64_t nwork = w.counters_i32[4];  // steps the index could not answer
+  for (int64_t it = (int64_t)blockIdx.x * LANE_TB + threadIdx.x; it < nwork; it += (int64_t)gridDim.x * LANE_TB) {
+    const int64_t p = w.overflow_list0[it];
+    const int32_t q = w.col_prev[p];
+    const int i = w.state[q], j = w.state[p];
+    const int32_t ei = w.cand_edge[(int64_t)q * KMAX + i], ej = w.cand_edge[p * KMAX + j];
+    const float oi = w.cand_off[(int64_t)q * KMAX + i], oj = w.cand_off[p * KMAX + j];
+    const float bound = P.factor * w.gc[p];
+    const int32_t u = g.e_to[ei], v = g.e_from[ej];
+    unsigned long long rel = 0;
+    const int n = lane_search<CAP, true>(g, K, D, Pd, u, bound, rel);
+    if (n < 0) {
+      const int slot = atomicAdd(&w.counters_i32[0], 1);
+      w.overflow_list[slot] = (int32_t)p;
+      continue;
+    }
+    const int fv = lane_find<CAP>(K, n, (uint32_t)v);
+    int len = 0;
+    for (int f = fv; (K[f * LANE_TB] & ~DONE) != (uint32_t)u;) {
+      ++len;
+      f = lane_find<CAP>(K, n, (uint32_t)g.e_from[Pd[f * LANE_TB]]);
+    }
+    const int off = len ? atomicAdd(&w.counters_i32[1], len) : 0;
+    if (off + len > w.pool_cap) {
+      w.counters_i32[2] = 1;
+      w.path_len[p] = -1;
+    } else {
+      int k = len;
+      for (int f = fv; (K[f * LANE_TB] & ~DONE) != (uint32_t)u;) {
+        const int32_t pe = Pd[f * LANE_TB];
+        w.path_pool[off + (--k)] = pe;
+        f = lane_find<CAP>(K, n, (uint32_t)g.e_from[pe]);
+      }
+      w.path_off[p] = off;
+      w.path_len[p] = len;
+    }
+    const float start = g.e_len[ei] - oi;
+    const float sd = start + D[fv * LANE_TB];
+    w.route_dist[p] = sd + oj;
+    ++c_search;
+    c_settled += (unsigned long long)n;
+    c_relaxed += rel;
+    c_edges += (unsigned long long)len;
+  }
+  if (w.ctr) {
+    cadd(&w.ctr->route_searches, c_search);
+    cadd(&w.ctr->route_nodes_settled, c_settled);
+    cadd(&w.ctr->route_edges_relaxed, c_relaxed);
+    cadd(&w.ctr->route_edges, c_edges);
+  }
+}
+
+// ============================================================== distance index
+// Row lookup: binary search of v in u's row (sorted by node id).
+// Returns 1 found (D, pred set), 0 absent (D(u,v) > rmax), -1 row incomplete.
+__device__ __forceinline__ int idx_lookup(const DevIndex& X, int32_t u, uint32_t v, float& D, int32_t& pred) {
+  const int32_t n = X.row_cnt[u];
+  if (n < 0) return -1;
+  int64_t lo = X.row_off[u], hi = lo + n - 1;
+  while (lo <= hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    const uint32_t x = X.node[mid];
+    if (x == v) {
+      D = X.dist[mid];
+      pred = X.pred[mid];
+      return 1;
+    }
+    if (x < v) lo = mid + 1;
+    else hi = mid - 1;
+  }
+  return 0;
+}
+
+// Index build: one wavefront per source node u runs the bounded search with
+// bound rmax in an LDS table of INDEX_BUILD_CAP slots (same fixed point as the
+// online tiers), then writes the settled nodes sorted by id.
+template <bool WRITE>
+__global__ __launch_bounds__(TB) void k_index_build(DevGraph g, float rmax, int32_t* row_cnt, const int64_t* row_off,
+                                                    uint32_t* out_node, float* out_dist, int32_t* out_pred) {
+  __shared__ uint32_t lkey[INDEX_BUILD_CAP];
+  __shared__ unsigned long long llab[INDEX_BUILD_CAP];
+  __shared__ uint32_t linq[INDEX_BUILD_CAP];
+  __shared__ uint32_t lfr0[INDEX_BUILD_CAP];
+  __shared__ uint32_t lfr1[INDEX_BUILD_CAP];
+  __shared__ unsigned long long sortk[WRITE ? INDEX_BUILD_CAP : 1];
+  __shared__ SearchShared S;
+  __shared__ int s_n;
+  const int lane = threadIdx.x;
+  const Table T{lkey, llab, linq, lfr0, lfr1, 11, INDEX_BUILD_LIMIT};
+  for (int32_t u = blockIdx.x; u < g.n_nodes; u += gridDim.x) {
+    const int settled = wave_search<false>(g, T, S, u, rmax, lane);
+    if (!WRITE) {
+      if (lane == 0) row_cnt[u] = settled;  // -1: incomplete row
+      continue;
+    }
+    if (settled < 0) continue;
+    if (lane == 0) s_n = 0;
+    __syncthreads();
+    for (int i = lane; i < INDEX_BUILD_CAP; i += TB) {
+      const uint32_t k = lkey[i];
+      if (k != EMPTY) {
+        const int idx = atomicAdd(&s_n, 1);
+        sortk[idx] = ((unsigned long long)k << 11) | (unsigned long long)i;
+      }
+    }
+    __syncthreads();
+    const int n = s_n;
+    int N = 1;
+    while (N < n) N <<= 1;
+    for (int i = n + lane; i < N; i += TB) sortk[i] = LAB_NONE;
+    __syncthreads();
+    for (int kk = 2; kk <= N; kk <<= 1) {
+      for (int j = kk >> 1; j > 0; j >>= 1) {
+        for (int i = lane; i < N; i += TB) {
+          const int ixj = i ^ j;
+          if (ixj > i) {
+            const unsigned long long x = sortk[i], y = sortk[ixj];
+            const bool up = (i & kk) == 0;
+            if ((x > y) == up) {
+              sortk[i] = y;
+              sortk[ixj] = x;
+            }
+          }
+        }
+        __syncthreads();
+      }
+    }
+    const int64_t base = row_off[u];
+    for (int i = lane; i < n; i += TB) {
+      const unsigned long long sk = sortk[i];
+      const int slot = (int)(sk & 2047ull);
+      const unsigned long long lab = llab[slot];
+      out_node[base + i] = (uint32_t)(sk >> 11);
+      out_dist[base + i] = bitsf((uint32_t)(lab >> 32));
+      out_pred[base + i] = (int32_t)(uint32_t)(lab & 0xFFFFFFFFull);
+    }
+    __syncthreads();
+  }
+}
+
+__global__ void k_row_sizes(const int32_t* row_cnt, int64_t* sizes, int32_t n) {
+  const int32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+  if (u < n) sizes[u] = row_cnt[u] > 0 ? row_cnt[u] : 0;
+  if (u == n) sizes[n] = 0;
+}
+
+// K4 index tier: one wavefront per column pair, lanes over the Kq x Kp
+// (source candidate, target candidate) pairs; each pair is one binary search
+// in the source node's index row.  Columns the index cannot answer (bound >
+// rmax, or a source row incomplete) go to the search tiers.
+__global__ __launch_bounds__(TB) void k_trans_index(DevGraph g, DevBatch b, DevParams P, DevWork w) {
+  __shared__ int32_t eq[KMAX], ep[KMAX], uq[KMAX], vp[KMAX];
+  __shared__ float oq[KMAX], op[KMAX];
+  const int lane = threadIdx.x;
+  const DevIndex& X = w.idx;
+  unsigned long long c_search = 0, c_settled = 0, c_relaxed = 0, c_trans = 0;
+  for (int64_t p = blockIdx.x; p < b.n_points; p += gridDim.x) {
+    const int32_t q = w.col_prev[p];
+    if (q < 0) continue;
+    const int Kq = w.ncand[q], Kp = w.ncand[p];
+    const float gcv = w.gc[p];
+    const float bound = P.factor * gcv;
+    bool usable = bound <= X.rmax;
+    if (lane < Kq) {
+      eq[lane] = w.cand_edge[(int64_t)q * KMAX + lane];
+      oq[lane] = w.cand_off[(int64_t)q * KMAX + lane];
+      uq[lane] = g.e_to[eq[lane]];
+      usable = usable && X.row_cnt[uq[lane]] >= 0;
+    }
+    if (lane < Kp) {
+      ep[lane] = w.cand_edge[p * KMAX + lane];
+      op[lane] = w.cand_off[p * KMAX + lane];
+      vp[lane] = g.e_from[ep[lane]];
+    }
+    if (__ballot(!usable) != 0ull) {
+      if (lane == 0) {
+        const int slot = atomicAdd(&w.counters_i32[4], 1);
+        w.overflow_list0[slot] = (int32_t)p;
+      }
+      __syncthreads();
+      continue;
+    }
+    __syncthreads();
+    float* Tm = w.trans + w.trans_off[p];
+    unsigned long long ntr = 0;
+    for (int idx = lane; idx < Kq * Kp; idx += TB) {
+      const int i = idx / Kp, j = idx - (idx / Kp) * Kp;
+      float r = 0.0f;
+      bool ok = true;
+      if (ep[j] == eq[i] && op[j] >= oq[i]) {
+        r = op[j] - oq[i];
+      } else {
+        float D;
+        int32_t pr;
+        if (idx_lookup(X, uq[i], (uint32_t)vp[j], D, pr) == 1) {
+          const float start = g.e_len[eq[i]] - oq[i];
+          const float sd = start + D;
+          r = sd + op[j];
+        } else {
+          ok = false;
+        }
+      }
+      float cost = INFINITY;
+      if (ok && r <= bound) {
+        const float diff = fabsf(r - gcv);
+        cost = diff / P.beta;
+        ++ntr;
+      }
+      Tm[i * Kp + j] = cost;
+    }
+    if (w.ctr) {
+      // algorithmic counts of the equivalent searches: per distinct source,
+      // the row entries with D <= bound and their out-degrees
+      for (int i = 0; i < Kq; ++i) {
+        bool first = true;
+        for (int k = 0; k < i; ++k) first = first && uq[k] != uq[i];
+        if (!first) continue;
+        const int64_t o = X.row_off[uq[i]];
+        const int32_t n = X.row_cnt[uq[i]];
+        unsigned long long st = 0, rl = 0;
+        for (int k = lane; k < n; k += TB) {
+          if (X.dist[o + k] <= bound) {
+            ++st;
+            const uint32_t v = X.node[o + k];
+            rl += (unsigned long long)(g.out_off[v + 1] - g.out_off[v]);
+          }
+        }
+        for (int sh = 32; sh > 0; sh >>= 1) {
+          st += __shfl_xor(st, sh, 64);
+          rl += __shfl_xor(rl, sh, 64);
+        }
+        c_search += 1;
+        c_settled += st;
+        c_relaxed += rl;
+      }
+      for (int sh = 32; sh > 0; sh >>= 1) ntr += __shfl_xor(ntr, sh, 64);
+      c_trans += ntr;
+    }
+    __syncthreads();
+  }
+  if (w.ctr && lane == 0) {
+    cadd(&w.ctr->searches, c_search);
+    cadd(&w.ctr->nodes_settled, c_settled);
+    cadd(&w.ctr->edges_relaxed, c_relaxed);
+    cadd(&w.ctr->transitions, c_trans);
+  }
+}
+
+// K6 index tier: one lane per matched step; the path is read back from the
+// index row of the source node (predecessor edges), one binary search per edge.
+__global__ __launch_bounds__(256) void k_route_index(DevGraph g, DevBatch b, DevParams P, DevWork w) {
+  const DevIndex& X = w.idx;
+  unsigned long long c_search = 0, c_settled = 0, c_relaxed = 0, c_edges = 0;
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < b.n_points;
+       p += (int64_t)gridDim.x * blockDim.x) {
+    w.route_dist[p] = 0.0f;
+    w.path_len[p] = 0;
+    w.path_off[p] = 0;
+    if (w.state[p] < 0 || w.chain_start[p]) continue;
+    const int32_t q = w.col_prev[p];
+    const int i = w.state[q], j = w.state[p];
+    const int32_t ei = w.cand_edge[(int64_t)q * KMAX + i], ej = w.cand_edge[p * KMAX + j];
+    const float oi = w.cand_off[(int64_t)q * KMAX + i], oj = w.cand_off[p * KMAX + j];
+    if (ei == ej && oj >= oi) {
+      w.route_dist[p] = oj - oi;
+      continue;
+    }
+    const float bound = P.factor * w.gc[p];
+    const int32_t u = g.e_to[ei], v = g.e_from[ej];
+    float Dv;
+    int32_t pe;
+    if (!(bound <= X.rmax) || idx_lookup(X, u, (uint32_t)v, Dv, pe) != 1) {
+      const int slot = atomicAdd(&w.counters_i32[4], 1);
+      w.overflow_list0[slot] = (int32_t)p;
+      continue;
+    }
+    int len = 0;
+    const int32_t rowlen = X.row_cnt[u];
+    for (int32_t x = v; x != u && len <= rowlen;) {
+      float dd;
+      int32_t px;
+      idx_lookup(X, u, (uint32_t)x, dd, px);
+      ++len;
+      x = g.e_from[px];
+    }
+    const int off = len ? atomicAdd(&w.counters_i32[1], len) : 0;
+    if (off + len > w.pool_cap) {
+      w.counters_i32[2] = 1;
+      w.path_len[p] = -1;
+    } else {
+      int k = len;
+      for (int32_t x = v; x != u;) {
+        float dd;
+        int32_t px;
+        idx_lookup(X, u, (uint32_t)x, dd, px);
+        w.path_pool[off + (--k)] = px;
+        x = g.e_from[px];
+      }
+      w.path_off[p] = off;
+      w.path_len[p] = len;
+    }
+    const float start = g.e_len[ei] - oi;
+    const float sd = start + Dv;
+    w.route_dist[p] = sd + oj;
+    if (w.ctr) {
+      const int64_t o = X.row_off[u];
+      const int32_t n = X.row_cnt[u];
+      unsigned long long st = 0, rl = 0;
+      for (int k = 0; k < n; ++k)
+        if (X.dist[o + k] <= bound) {
+          ++st;
+          const uint32_t y = X.node[o + k];
+          rl += (unsigned long long)(g.out_off[y + 1] - g.out_off[y]);
+        }
+      ++c_search;
+      c_settled += st;
+      c_relaxed += rl;
+      c_edges += (unsigned long long)len;
+    }
+  }
+  if (w.ctr) {
+    cadd(&w.ctr->route_searches, c_search);
+    cadd(&w.ctr->route_nodes_settled, c_settled);
+    cadd(&w.ctr->route_edges_relaxed, c_relaxed);
+    cadd(&w.ctr->route_edges, c_edges);
+  }
+}
+
+// ============================================================== K4 transitions (wave tiers)
+// Columns spilled by the lane tier (list in w.overflow_list, count in
+// w.counters_i32[0], read on the device: no host round trip).  The LDS wave
+// tier spills further to `w.overflow_list2` / counters_i32[3], which the
+// global-memory tier (BIG) drains.
 template <bool BIG>
 __global__ __launch_bounds__(TB) void k_transitions(DevGraph g, DevBatch b, DevParams P, DevWork w,
                                                      int32_t n_overflow) {
@@ -489,9 +990,11 @@ __global__ __launch_bounds__(TB) void k_transitions(DevGraph g, DevBatch b, DevP
   } else {
     T = Table{lkey, llab, linq, lfr0, lfr1, 8, LDS_TABLE_LIMIT};
   }
-  const int64_t nwork = BIG ? (int64_t)n_overflow : b.n_points;
+  (void)n_overflow;
+  const int32_t* list = BIG ? w.overflow_list2 : w.overflow_list;
+  const int64_t nwork = BIG ? (int64_t)w.counters_i32[3] : (int64_t)w.counters_i32[0];
   for (int64_t it = blockIdx.x; it < nwork; it += gridDim.x) {
-    const int64_t p = BIG ? (int64_t)w.overflow_list[it] : it;
+    const int64_t p = (int64_t)list[it];
     const int32_t q = w.col_prev[p];
     if (q < 0) continue;
     const int Kq = w.ncand[q], Kp = w.ncand[p];
@@ -574,8 +1077,8 @@ __global__ __launch_bounds__(TB) void k_transitions(DevGraph g, DevBatch b, DevP
     }
     if (failed && lane == 0) {
       if (!BIG) {
-        const int slot = atomicAdd(&w.counters_i32[0], 1);
-        w.overflow_list[slot] = (int32_t)p;
+        const int slot = atomicAdd(&w.counters_i32[3], 1);
+        w.overflow_list2[slot] = (int32_t)p;
       } else {
         atomicCAS(&w.trace_err[w.pt_trace[p]], 0, OTM_TERR_SEARCH_OVERFLOW);
       }
@@ -699,17 +1202,11 @@ __global__ __launch_bounds__(TB) void k_route(DevGraph g, DevBatch b, DevParams 
   } else {
     T = Table{lkey, llab, linq, lfr0, lfr1, 8, LDS_TABLE_LIMIT};
   }
-  const int64_t nwork = BIG ? (int64_t)n_overflow : b.n_points;
+  (void)n_overflow;
+  const int32_t* list = BIG ? w.overflow_list2 : w.overflow_list;
+  const int64_t nwork = BIG ? (int64_t)w.counters_i32[3] : (int64_t)w.counters_i32[0];
   for (int64_t it = blockIdx.x; it < nwork; it += gridDim.x) {
-    const int64_t p = BIG ? (int64_t)w.overflow_list[it] : it;
-    if (!BIG) {
-      if (lane == 0) {
-        w.route_dist[p] = 0.0f;
-        w.path_len[p] = 0;
-        w.path_off[p] = 0;
-      }
-      if (w.state[p] < 0 || w.chain_start[p]) continue;
-    }
+    const int64_t p = (int64_t)list[it];
     const int32_t q = w.col_prev[p];
     const int i = w.state[q], j = w.state[p];
     const int32_t ei = w.cand_edge[(int64_t)q * KMAX + i], ej = w.cand_edge[p * KMAX + j];
@@ -724,8 +1221,8 @@ __global__ __launch_bounds__(TB) void k_route(DevGraph g, DevBatch b, DevParams 
     if (settled < 0) {
       if (lane == 0) {
         if (!BIG) {
-          const int slot = atomicAdd(&w.counters_i32[0], 1);
-          w.overflow_list[slot] = (int32_t)p;
+          const int slot = atomicAdd(&w.counters_i32[3], 1);
+          w.overflow_list2[slot] = (int32_t)p;
         } else {
           atomicCAS(&w.trace_err[w.pt_trace[p]], 0, OTM_TERR_SEARCH_OVERFLOW);
         }
@@ -764,10 +1261,9 @@ __global__ __launch_bounds__(TB) void k_route(DevGraph g, DevBatch b, DevParams 
       const float sd = start + D;
       w.route_dist[p] = sd + oj;
       if (w.ctr) {
-        cadd(&w.ctr->searches, 1);
         cadd(&w.ctr->route_searches, 1);
-        cadd(&w.ctr->nodes_settled, (unsigned long long)settled);
-        cadd(&w.ctr->edges_relaxed, od);
+        cadd(&w.ctr->route_nodes_settled, (unsigned long long)settled);
+        cadd(&w.ctr->route_edges_relaxed, od);
         cadd(&w.ctr->route_edges, (unsigned long long)n);
       }
     }
@@ -1088,25 +1584,29 @@ void launch_candidates(const DevGraph& g, const DevBatch& b, const DevParams& p,
 void launch_links(const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s) {
   hipLaunchKernelGGL(k_links, dim3(grid_for(b.n_points + 1, 256, 1 << 30)), dim3(256), 0, s, b, p, w);
 }
-void launch_transitions(const DevGraph& g, const DevBatch& b, const DevParams& p, DevWork& w, int32_t n_overflow,
-                        bool big_tier, hipStream_t s) {
-  if (big_tier)
-    hipLaunchKernelGGL(k_transitions<true>, dim3(grid_for(n_overflow, 1, BIG_SLOTS)), dim3(TB), 0, s, g, b, p, w,
-                       n_overflow);
-  else
-    hipLaunchKernelGGL(k_transitions<false>, dim3(grid_for(b.n_points, 1, WAVE_GRID_CAP)), dim3(TB), 0, s, g, b, p,
-                       w, 0);
+// The spill tiers run on lists the previous tier filled on the device; they
+// read the list length themselves (fixed grids, no host round trip) and exit
+// at once when the list is empty.
+constexpr int LANE_CAP = 24;        // route stage: 12 B per slot
+constexpr int LANE_CAP_TRANS = 32;  // transitions: 8 B per slot (no predecessors)
+constexpr int SPILL_GRID = 4096;
+
+constexpr int LANE_GRID = 2048;
+
+void launch_transitions(const DevGraph& g, const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s) {
+  hipLaunchKernelGGL(k_trans_index, dim3(grid_for(b.n_points, 1, WAVE_GRID_CAP)), dim3(TB), 0, s, g, b, p, w);
+  hipLaunchKernelGGL(k_trans_lane<LANE_CAP_TRANS>, dim3(LANE_GRID), dim3(LANE_TB), 0, s, g, b, p, w);
+  hipLaunchKernelGGL(k_transitions<false>, dim3(SPILL_GRID), dim3(TB), 0, s, g, b, p, w, 0);
+  hipLaunchKernelGGL(k_transitions<true>, dim3(BIG_SLOTS), dim3(TB), 0, s, g, b, p, w, 0);
 }
 void launch_viterbi(const DevBatch& b, DevWork& w, hipStream_t s) {
   hipLaunchKernelGGL(k_viterbi, dim3(grid_for(b.n_traces, 1, WAVE_GRID_CAP)), dim3(TB), 0, s, b, w);
 }
-void launch_route(const DevGraph& g, const DevBatch& b, const DevParams& p, DevWork& w, int32_t n_overflow,
-                  bool big_tier, hipStream_t s) {
-  if (big_tier)
-    hipLaunchKernelGGL(k_route<true>, dim3(grid_for(n_overflow, 1, BIG_SLOTS)), dim3(TB), 0, s, g, b, p, w,
-                       n_overflow);
-  else
-    hipLaunchKernelGGL(k_route<false>, dim3(grid_for(b.n_points, 1, WAVE_GRID_CAP)), dim3(TB), 0, s, g, b, p, w, 0);
+void launch_route(const DevGraph& g, const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s) {
+  hipLaunchKernelGGL(k_route_index, dim3(grid_for(b.n_points, 256, 1 << 30)), dim3(256), 0, s, g, b, p, w);
+  hipLaunchKernelGGL(k_route_lane<LANE_CAP>, dim3(LANE_GRID), dim3(LANE_TB), 0, s, g, b, p, w);
+  hipLaunchKernelGGL(k_route<false>, dim3(SPILL_GRID), dim3(TB), 0, s, g, b, p, w, 0);
+  hipLaunchKernelGGL(k_route<true>, dim3(BIG_SLOTS), dim3(TB), 0, s, g, b, p, w, 0);
 }
 void launch_segments(const DevGraph& g, const DevBatch& b, DevWork& w, DevOut& o, bool write, hipStream_t s) {
   if (write)
@@ -1116,6 +1616,19 @@ void launch_segments(const DevGraph& g, const DevBatch& b, DevWork& w, DevOut& o
 }
 void launch_report(const DevBatch& b, const DevReportCfg& rc, DevWork& w, DevOut& o, hipStream_t s) {
   hipLaunchKernelGGL(k_report, dim3(grid_for(b.n_traces, 64, 1 << 30)), dim3(64), 0, s, b, rc, w, o, 0);
+}
+
+void launch_index_build(const DevGraph& g, float rmax, int32_t* row_cnt, const int64_t* row_off, uint32_t* node,
+                        float* dist, int32_t* pred, bool write, hipStream_t s) {
+  const int grid = grid_for(g.n_nodes, 1, 256 * 16);
+  if (write)
+    hipLaunchKernelGGL(k_index_build<true>, dim3(grid), dim3(TB), 0, s, g, rmax, row_cnt, row_off, node, dist, pred);
+  else
+    hipLaunchKernelGGL(k_index_build<false>, dim3(grid), dim3(TB), 0, s, g, rmax, row_cnt, row_off, node, dist, pred);
+}
+void launch_row_sizes(const int32_t* row_cnt, int64_t* row_sizes, int32_t n, hipStream_t s) {
+  hipLaunchKernelGGL(k_row_sizes, dim3(grid_for((int64_t)n + 1, 256, 1 << 30)), dim3(256), 0, s, row_cnt, row_sizes,
+                     n);
 }
 
 size_t scan_tmp_bytes(int64_t n) {

@@ -38,7 +38,7 @@ int synth_traces(const HostGraph& g, const otm_synth_trace_params* p, int64_t* t
   int64_t P = 0;
   for (int v = 0; v < p->n_vehicles; ++v) {
     trace_off[v] = P;
-    uint64_t gv = (uint64_t)(p->vehicle_offset + v);
+    uint64_t gv = (uint64_t)(p->vehicle_ids ? p->vehicle_ids[v] : p->vehicle_offset + v);
     Rng rng(p->seed * 0x9E3779B97F4A7C15ull ^ (gv + 1) * 0xD1B54A32D192ED03ull);
     rng.next();
     int e = starts[rng.next() % starts.size()];

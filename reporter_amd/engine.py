@@ -26,9 +26,12 @@ def _check(rc):
         raise OtmError("libotmatch error %d: %s" % (rc, _lib.last_error()))
 
 
-def write_config(path, graph_path, **meili):
-    """Write an engine config: {"otm":{"graph":...},"meili":{"default":{...}}}."""
-    cfg = {"otm": {"graph": os.path.abspath(graph_path)}, "meili": {"default": meili}}
+def write_config(path, graph_path, index_radius_m=None, **meili):
+    """Write an engine config: {"otm":{"graph":...,"index_radius_m":R},"meili":{"default":{...}}}."""
+    otm = {"graph": os.path.abspath(graph_path)}
+    if index_radius_m is not None:
+        otm["index_radius_m"] = index_radius_m
+    cfg = {"otm": otm, "meili": {"default": meili}}
     with open(path, "w") as f:
         json.dump(cfg, f)
     return path
@@ -45,7 +48,7 @@ class Results(object):
 
 
 class Engine(object):
-    def __init__(self, config_path=None, graph_path=None, device=0, **meili):
+    def __init__(self, config_path=None, graph_path=None, device=0, index_radius_m=None, **meili):
         """Either a config file (valhalla.Configure-style) or a graph path."""
         L = lib()
         self._tmp = None
@@ -54,7 +57,7 @@ class Engine(object):
                 raise ValueError("config_path or graph_path required")
             fd, self._tmp = tempfile.mkstemp(suffix=".json", prefix="otm_cfg_")
             os.close(fd)
-            config_path = write_config(self._tmp, graph_path, **meili)
+            config_path = write_config(self._tmp, graph_path, index_radius_m=index_radius_m, **meili)
         h = C.c_void_p()
         dev = (C.c_int * 1)(device)
         rc = L.otm_engine_create(config_path.encode(), dev, 1, C.byref(h))
@@ -144,7 +147,7 @@ class Engine(object):
         n_traces = trace_off.numel() - 1
         b = _lib.Batch(n_traces, int(lat.numel()), trace_off.data_ptr(), lat.data_ptr(), lon.data_ptr(),
                        time.data_ptr(), accuracy.data_ptr())
-        _check(lib().otm_match_device(self.h, C.byref(b), stream))
+        _check(lib().otm_match_device(self.h, C.byref(b), C.c_void_p(stream) if stream else None))
 
     def fetch(self):
         r = _lib.Results()
@@ -160,6 +163,11 @@ class Engine(object):
         _check(lib().otm_graph_info(self.h, C.byref(a), C.byref(b), C.byref(c)))
         return {"nodes": a.value, "edges": b.value, "segments": c.value}
 
+    def index_info(self):
+        r, e, i, ms = C.c_float(), C.c_int64(), C.c_int32(), C.c_float()
+        _check(lib().otm_index_info(self.h, C.byref(r), C.byref(e), C.byref(i), C.byref(ms)))
+        return {"radius_m": r.value, "entries": e.value, "incomplete_rows": i.value, "build_ms": ms.value}
+
     def set_counting(self, on):
         _check(lib().otm_set_counting(self.h, 1 if on else 0))
 
@@ -171,7 +179,8 @@ class Engine(object):
     def set_timing(self, on):
         _check(lib().otm_set_timing(self.h, 1 if on else 0))
 
-    STAGES = ("columns", "candidates", "trans_size", "transitions", "viterbi", "route", "segments", "report")
+    STAGES = ("columns", "candidates", "links_scan", "transitions", "viterbi", "route", "segments_count",
+              "segments_write_report")
 
     def stage_ms(self):
         ms = (C.c_float * 8)()

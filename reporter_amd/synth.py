@@ -50,10 +50,17 @@ def make_graph(path, **kw):
 
 
 def make_traces(graph_path, n_vehicles, points_per_vehicle, interval_s=5.0, noise_sigma_m=15.0, accuracy=15.0,
-                t0=1500000000.0, seed=7, vehicle_offset=0):
-    """-> dict of numpy arrays: trace_off, lat, lon, time, accuracy, true_edge, true_off."""
+                t0=1500000000.0, seed=7, vehicle_offset=0, vehicle_ids=None):
+    """-> dict of numpy arrays: trace_off, lat, lon, time, accuracy, true_edge, true_off.
+
+    Vehicle v's stream depends only on (seed, global id), the global id being
+    vehicle_offset + v or vehicle_ids[v]: uuid shards regenerate identically."""
+    ids = None
+    if vehicle_ids is not None:
+        ids = np.ascontiguousarray(vehicle_ids, dtype=np.int32)
+        n_vehicles = len(ids)
     tp = _lib.SynthTraceParams(n_vehicles, points_per_vehicle, interval_s, noise_sigma_m, accuracy, t0, seed,
-                               vehicle_offset)
+                               vehicle_offset, ids.ctypes.data if ids is not None else None)
     P = n_vehicles * points_per_vehicle
     out = dict(trace_off=np.zeros(n_vehicles + 1, np.int64), lat=np.zeros(P, np.float32),
                lon=np.zeros(P, np.float32), time=np.zeros(P, np.float64), accuracy=np.zeros(P, np.float32),
@@ -87,3 +94,16 @@ def slice_batch(b, t0, t1):
     out = {k: b[k][a:e] for k in ("lat", "lon", "time", "accuracy", "true_edge", "true_off") if k in b}
     out["trace_off"] = b["trace_off"][t0:t1 + 1] - a
     return out
+
+
+def shard_vehicle_ids(n_per_rank, rank, world, prefix="veh"):
+    """Global vehicle ids whose uuid ("veh<id>") lands on `rank` under Kafka's
+    murmur2 key partitioner -- the uuid sharding of SURVEY.md §8(e)."""
+    from .engine import murmur2_partition
+    out = []
+    v = 0
+    while len(out) < n_per_rank:
+        if world == 1 or murmur2_partition("%s%d" % (prefix, v), world) == rank:
+            out.append(v)
+        v += 1
+    return np.array(out, np.int32)

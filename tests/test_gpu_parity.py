@@ -48,9 +48,9 @@ def _stage_compare(eng, orc, batch):
     npt.assert_array_equal(eng.debug("route_dist")[:P], orc["route_dist"], err_msg="route_dist")
 
 
-def _run_both(graph, batch, oracle, results_equal, meili=None, stages=True, counters=True):
+def _run_both(graph, batch, oracle, results_equal, meili=None, stages=True, counters=True, index_radius_m=None):
     meili = meili or {}
-    with Engine(graph_path=graph, **meili) as eng:
+    with Engine(graph_path=graph, index_radius_m=index_radius_m, **meili) as eng:
         eng.set_counting(counters)
         res = eng.match(batch)
         p = oracle.params(**meili)
@@ -61,17 +61,29 @@ def _run_both(graph, batch, oracle, results_equal, meili=None, stages=True, coun
         if counters:
             c = eng.counters()
             for k, v in orc["counters"].items():
-                if k in ("edges_projected_unique", "shape_points_projected"):
-                    continue
                 assert c[k] == v, "counter %s gpu %d oracle %d" % (k, c[k], v)
         return res, orc
 
 
-def test_city_sample_sigma15(small_graph, oracle, results_equal):
+@pytest.mark.parametrize("radius", [None, 0.0, 300.0], ids=["index1000", "no_index", "index300"])
+def test_city_sample_sigma15(small_graph, oracle, results_equal, radius):
+    # the distance index answers columns whose bound fits its radius; the rest
+    # (and everything when it is disabled) run the online search tiers --
+    # results must be identical in all three configurations
     b = synth.make_traces(small_graph, 200, 100, interval_s=5.0, noise_sigma_m=15.0, accuracy=15.0, seed=11)
-    res, orc = _run_both(small_graph, b, oracle, results_equal)
+    res, orc = _run_both(small_graph, b, oracle, results_equal, index_radius_m=radius)
     assert (res.traces["code"] == 200).mean() > 0.95
     assert len(res.segments) > 1000 and len(res.reports) > 50
+
+
+def test_index_info(small_graph):
+    with Engine(graph_path=small_graph) as eng:
+        info = eng.index_info()
+        n = eng.graph_info()["nodes"]
+        assert info["radius_m"] == 1000.0 and info["incomplete_rows"] == 0
+        assert info["entries"] > 10 * n
+    with Engine(graph_path=small_graph, index_radius_m=0) as eng:
+        assert eng.index_info()["entries"] == 0
 
 
 def test_noise_free_traces(small_graph, oracle, results_equal):

@@ -1,0 +1,110 @@
+"""Host-side checks that need no GPU: the C ABI surface, the Java request
+encoder, sharding, synthetic inputs and the oracle's own invariants."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from reporter_amd import _lib, encode_request, murmur2_partition, synth, tracegen
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_functions():
+    txt = open(os.path.join(ROOT, "include", "otmatch.h")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(otm_[a-z0-9_]+)\s*\(", txt)))
+
+
+def test_library_exports_every_declared_symbol():
+    L = _lib.lib()
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True).stdout
+    exported = set(l.split()[-1] for l in out.splitlines() if " T " in l)
+    for fn in header_functions():
+        assert fn in exported, "%s declared in include/otmatch.h but not exported" % fn
+        assert getattr(L, fn) is not None
+    # and the binding declares a signature for each
+    assert set(header_functions()) == set(_lib.EXPORTED)
+
+
+def test_library_is_gfx950_code():
+    data = open(_lib.LIB_PATH, "rb").read()
+    assert b"hipv4-amdgcn-amd-amdhsa--gfx950" in data  # the offload bundle's code object entry
+
+
+def test_engine_create_fails_loudly_without_gpu_or_bad_config(tmp_path):
+    from reporter_amd import Engine, OtmError
+    cfg = tmp_path / "c.json"
+    cfg.write_text('{"otm":{}}')
+    with pytest.raises(OtmError):
+        Engine(config_path=str(cfg))
+
+
+def test_encode_request_java_format():
+    # Batch.java:52-61 + Point.java:39-45 (DecimalFormat "###.######", HALF_EVEN on the float value)
+    b = encode_request("u1", [37.98, -0.5, 0.0, 1.0000005, 14.543087], [23.72, 0.25, -0.0, 100.0, 121.021019],
+                       [1500000000, 1, 2, 3, 4], [15, 5, 0, 1, 9])
+    assert b == (b'{"uuid":"u1","trace":[{"lat":37.98,"lon":23.719999,"time":1500000000,"accuracy":15},'
+                 b'{"lat":-.5,"lon":.25,"time":1,"accuracy":5},{"lat":0,"lon":-0,"time":2,"accuracy":0},'
+                 b'{"lat":1,"lon":100,"time":3,"accuracy":1},{"lat":14.543087,"lon":121.021019,"time":4,'
+                 b'"accuracy":9}]}')
+    # the service's parser accepts the ordinary case; the "-.5" quirk of "###" is kept on purpose
+    assert encode_request("k", [], [], [], []) == b'{"uuid":"k","trace":]}'
+
+
+def test_murmur2_sharding_is_kafka_partitioner():
+    # Kafka Utils.murmur2 known answers (kafka-clients test vectors)
+    L = _lib.lib()
+    vec = {b"21": -973932308, b"foobar": -790332482, b"a-little-bit-long-string": -985981536,
+           b"a-little-bit-longer-string": -1486304829,
+           b"lkjh234lh9fiuh90y23oiuhsafujhadof229phr9h19h89h8": -58897971, b"abc": 479470107}
+    for k, v in vec.items():
+        assert L.otm_murmur2(k, len(k)) == v, k
+    ids0 = synth.shard_vehicle_ids(500, 0, 4)
+    ids1 = synth.shard_vehicle_ids(500, 1, 4)
+    assert not set(ids0.tolist()) & set(ids1.tolist())
+    assert all(murmur2_partition("veh%d" % v, 4) == 0 for v in ids0[:50])
+
+
+def test_synthetic_inputs_deterministic(small_graph):
+    a = synth.make_traces(small_graph, 20, 30, seed=5)
+    b = synth.make_traces(small_graph, 20, 30, seed=5)
+    for k in a:
+        assert np.array_equal(a[k], b[k])
+    # a vehicle depends only on its global id
+    c = synth.make_traces(small_graph, 1, 30, seed=5, vehicle_ids=[7])
+    assert np.array_equal(c["lat"], a["lat"][7 * 30:8 * 30])
+
+
+def test_oracle_loads_graph_and_matches(small_graph, oracle):
+    g = oracle.Graph(small_graph)
+    b = synth.make_traces(small_graph, 50, 80, seed=2)
+    r1 = oracle.match_batch(g, b, nthreads=1, keep_stages=True)
+    r4 = oracle.match_batch(g, b, nthreads=4)
+    for k in ("traces", "segments", "reports", "way_ids"):
+        assert r1[k].tobytes() == r4[k].tobytes(), k
+    st = r1["state"]
+    ok = st >= 0
+    assert ok.mean() > 0.95
+    edges = r1["cand_edge"].reshape(-1, 32)[np.arange(len(st)), np.maximum(st, 0)]
+    assert (edges[ok] == b["true_edge"][ok]).mean() > 0.8  # matched to the true directed edge
+    c = r1["counters"]
+    assert c["points"] == len(b["lat"]) and c["searches"] > 0 and c["nodes_settled"] >= c["searches"]
+
+
+def test_oracle_json_path_config1(small_graph, oracle):
+    """Config 1 plumbing: synthesize_gps traces -> handle_request -> 200s."""
+    g = oracle.Graph(small_graph)
+    bodies = tracegen.config1_requests(small_graph, n_traces=10, edges_per_trace=20)
+    for body in bodies:
+        code, resp = oracle.handle_request(g, body)
+        assert code == 200, resp
+        assert resp.startswith('{"stats":{"successful_matches":{"count":')
+
+
+def test_cos_deg_accuracy(oracle):
+    for d in np.linspace(-89.9, 89.9, 41):
+        assert abs(oracle.cos_deg(float(d)) - np.cos(np.radians(d))) < 2e-7

@@ -77,6 +77,29 @@ int engine_init(otm_engine* E, const char* graph_path, int device, std::string* 
   UP(OTMG_CELL_OFF, cell_off, int64_t);
   UP(OTMG_CELL_ENT, cell_ent, uint32_t);
 #undef UP
+  {
+    // per cell entry: the shape segment's endpoints (lat_a, lon_a, lat_b,
+    // lon_b), laid out in cell order so a probe's scan of one grid row is
+    // one contiguous float4 stream (no edge -> shape indirection)
+    const size_t ne = h.sec[OTMG_CELL_ENT].bytes / 4;
+    const uint32_t* ent = (const uint32_t*)E->host.section(OTMG_CELL_ENT);
+    const int32_t* soff = (const int32_t*)E->host.section(OTMG_EDGE_SHAPE_OFF);
+    const float* slat = (const float*)E->host.section(OTMG_SHAPE_LAT);
+    const float* slon = (const float*)E->host.section(OTMG_SHAPE_LON);
+    std::vector<float> geo(ne * 4 + 4);
+    for (size_t q = 0; q < ne; ++q) {
+      const int32_t a = soff[ent[q] >> 4] + (int32_t)(ent[q] & 15u);
+      geo[q * 4 + 0] = slat[a];
+      geo[q * 4 + 1] = slon[a];
+      geo[q * 4 + 2] = slat[a + 1];
+      geo[q * 4 + 3] = slon[a + 1];
+    }
+    void* d = nullptr;
+    HIPCHK(hipMalloc(&d, geo.size() * 4));
+    HIPCHK(hipMemcpy(d, geo.data(), geo.size() * 4, hipMemcpyHostToDevice));
+    E->graph_allocs.push_back(d);
+    g.ent_geo = (const float4*)d;
+  }
   g.n_nodes = h.n_nodes;
   g.n_edges = h.n_edges;
   g.n_segments = h.n_segments;
@@ -252,6 +275,7 @@ int engine_match(otm_engine* E, const DevBatch& b, hipStream_t s, std::string* e
   w.counters_i32 = P<int32_t>(E->counters_i32);
   w.ctr = E->counting ? E->ctr : nullptr;
   if (E->counting) HIPCHK(hipMemsetAsync(E->ctr, 0, sizeof(DevCounters), s));
+  HIPCHK(hipMemsetAsync(w.counters_i32, 0, 64, s));  // [5] = candidate spill count
 #define EV(k) \
   if (E->timing) HIPCHK(hipEventRecord(E->ev[k], s));
   EV(0);

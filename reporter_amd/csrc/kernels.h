@@ -41,6 +41,7 @@ struct DevGraph {
   const float* g_len;
   const int64_t* cell_off;
   const uint32_t* cell_ent;
+  const float4* ent_geo;  // per cell entry: shape segment endpoints (lat_a, lon_a, lat_b, lon_b)
   int32_t n_nodes, n_edges, n_segments, grid_rows, grid_cols;
   double lat0, lon0, cell;
 };

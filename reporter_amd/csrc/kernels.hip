@@ -50,6 +50,28 @@ __device__ __forceinline__ float gc_dist(float la, float lo, float lb, float lob
   return sqrtf(dx * dx + dy * dy);
 }
 
+// squared distance from the probe to shape segment a-b: the sqd half of
+// project() below, same float evaluation order
+__device__ __forceinline__ float seg_sqdist(float alat, float alon, float blat, float blon, float lat, float lon,
+                                            float ls) {
+  const float ax = (alon - lon) * ls;
+  const float ay = (alat - lat) * MPD_F;
+  const float bx = (blon - lon) * ls;
+  const float by = (blat - lat) * MPD_F;
+  const float vx = bx - ax;
+  const float vy = by - ay;
+  const float l2 = vx * vx + vy * vy;
+  float t = 0.0f;
+  if (l2 > 0.0f) {
+    const float dot = ax * vx + ay * vy;
+    t = -dot / l2;
+    t = t < 0.0f ? 0.0f : (t > 1.0f ? 1.0f : t);
+  }
+  const float px = ax + t * vx;
+  const float py = ay + t * vy;
+  return px * px + py * py;
+}
+
 __device__ __forceinline__ void project(const DevGraph& g, int32_t e, int32_t k, float lat, float lon, float ls,
                                         float& sqd, float& off_out) {
   const int32_t a = g.e_shape_off[e] + k, b = a + 1;
@@ -130,7 +152,157 @@ __global__ __launch_bounds__(256) void k_columns(DevBatch b, DevParams P, DevWor
 
 // ============================================================== K2 candidates
 constexpr int HCAP = 512;  // edge hash slots (>= 2 * MAX_HITS)
+#ifndef OTM_CAND_LANE_CAP
+#define OTM_CAND_LANE_CAP 16
+#endif
+constexpr int CAND_LANE_CAP = OTM_CAND_LANE_CAP;  // lane tier: distinct edges kept per probe
+constexpr int CAND_TB = 128;
 
+// wave-reduce a per-lane count and add it to a device counter (all 64 lanes active)
+__device__ __forceinline__ void wave_cadd(unsigned long long* c, unsigned long long v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  if ((threadIdx.x & 63) == 0 && v) atomicAdd(c, v);
+}
+
+// Lane tier of the candidate search: one probe per LANE.  The lane walks its
+// probe's grid cells serially (the same cell range, entries and projection as
+// the wave kernel below), keeps each edge's best (sqdist, shape segment) in a
+// private LDS list of CAND_LANE_CAP slots (interleaved by thread), then
+// selection-sorts the first max_candidates by (sqdist, edge).  Probes with
+// more distinct edges in range spill to the wave kernel, which also applies
+// the MAX_HITS spec limit.
+__global__ __launch_bounds__(CAND_TB) void k_cand_lane(DevGraph g, DevBatch b, DevParams P, DevWork w) {
+  __shared__ uint32_t sE[CAND_LANE_CAP * CAND_TB];  // edge << 4 | shape segment
+  __shared__ float sQ[CAND_LANE_CAP * CAND_TB];     // best squared distance
+  uint32_t* E = sE + threadIdx.x;
+  float* Q = sQ + threadIdx.x;
+  constexpr int S = CAND_TB;
+  unsigned long long c_cells = 0, c_ent = 0, c_cand = 0;
+  for (int64_t p = (int64_t)blockIdx.x * CAND_TB + threadIdx.x; p < b.n_points; p += (int64_t)gridDim.x * CAND_TB) {
+    if (!w.is_col[p]) {
+      w.ncand[p] = 0;
+      continue;
+    }
+    const float lat = b.lat[p], lon = b.lon[p];
+    const float r = probe_radius(P, b.acc[p]);
+    const float r2 = r * r;
+    const float ls = MPD_F * cos_deg(lat);
+    const float dlat = r / MPD_F;
+    const float dlon = r / ls;
+    const double la_lo = ((double)lat - (double)dlat - g.lat0) / g.cell;
+    const double la_hi = ((double)lat + (double)dlat - g.lat0) / g.cell;
+    const double lo_lo = ((double)lon - (double)dlon - g.lon0) / g.cell;
+    const double lo_hi = ((double)lon + (double)dlon - g.lon0) / g.cell;
+    const double R = g.grid_rows, Cn = g.grid_cols;
+    int r0 = 0, r1 = -1, c0 = 0, c1 = -1;
+    if (!(la_hi < 0.0 || lo_hi < 0.0 || la_lo >= R || lo_lo >= Cn)) {
+      r0 = la_lo < 0.0 ? 0 : (int)floor(la_lo);
+      r1 = la_hi >= R ? (int)R - 1 : (int)floor(la_hi);
+      c0 = lo_lo < 0.0 ? 0 : (int)floor(lo_lo);
+      c1 = lo_hi >= Cn ? (int)Cn - 1 : (int)floor(lo_hi);
+    }
+    int n = 0;
+    bool spill = false;
+    // cells c0..c1 of one grid row are adjacent in the row-major cell CSR:
+    // each row's entries are one contiguous range
+    const unsigned long long cells = (unsigned long long)(r1 - r0 + 1) * (unsigned long long)(c1 - c0 + 1);
+    unsigned long long ents = 0;
+    for (int rr = r0; rr <= r1 && !spill; ++rr) {
+      {
+        const size_t rbase = (size_t)rr * (size_t)g.grid_cols;
+        const int64_t q0 = g.cell_off[rbase + c0], q1 = g.cell_off[rbase + c1 + 1];
+        ents += (unsigned long long)(q1 - q0);
+        // 4 entries' loads in flight per step, inserted in entry order
+        for (int64_t q = q0; q < q1 && !spill; q += 4) {
+          float sq[4];
+          uint32_t en[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            sq[u] = INFINITY;
+            en[u] = 0;
+            if (q + u < q1) {
+              const float4 G = g.ent_geo[q + u];
+              en[u] = g.cell_ent[q + u];
+              sq[u] = seg_sqdist(G.x, G.y, G.z, G.w, lat, lon, ls);
+            }
+          }
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const float sqd = sq[u];
+            if (spill || !(sqd <= r2)) continue;
+            const uint32_t ent = en[u];
+            const uint32_t e = ent >> 4;
+            int f = -1;
+            for (int m = 0; m < n; ++m)
+              if ((E[m * S] >> 4) == e) {
+                f = m;
+                break;
+              }
+            if (f < 0) {
+              if (n == CAND_LANE_CAP) {
+                spill = true;
+                continue;
+              }
+              E[n * S] = ent;
+              Q[n * S] = sqd;
+              ++n;
+            } else {
+              const float qf = Q[f * S];
+              if (sqd < qf || (sqd == qf && (ent & 15u) < (E[f * S] & 15u))) {
+                Q[f * S] = sqd;
+                E[f * S] = ent;
+              }
+            }
+          }
+        }
+      }
+    }
+    if (spill) {
+      const int slot = atomicAdd(&w.counters_i32[5], 1);
+      w.overflow_list0[slot] = (int32_t)p;
+      continue;
+    }
+    const int K = n < P.max_candidates ? n : P.max_candidates;
+    const float ds = (2.0f * P.sigma_z) * P.sigma_z;
+    for (int j = 0; j < K; ++j) {
+      int m = j;
+      float qm = Q[j * S];
+      uint32_t em = E[j * S];
+      for (int t = j + 1; t < n; ++t) {
+        const float qt = Q[t * S];
+        const uint32_t et = E[t * S];
+        if (qt < qm || (qt == qm && (et >> 4) < (em >> 4))) {
+          m = t;
+          qm = qt;
+          em = et;
+        }
+      }
+      if (m != j) {
+        Q[m * S] = Q[j * S];
+        E[m * S] = E[j * S];
+        Q[j * S] = qm;
+        E[j * S] = em;
+      }
+      const int32_t e = (int32_t)(em >> 4);
+      float sqd, off;
+      project(g, e, (int32_t)(em & 15u), lat, lon, ls, sqd, off);
+      w.cand_edge[p * KMAX + j] = e;
+      w.cand_off[p * KMAX + j] = off;
+      w.cand_emis[p * KMAX + j] = sqd / ds;
+    }
+    w.ncand[p] = K;
+    c_cells += cells;
+    c_ent += ents;
+    c_cand += (unsigned long long)K;
+  }
+  if (w.ctr) {
+    wave_cadd(&w.ctr->cells_visited, c_cells);
+    wave_cadd(&w.ctr->cell_entries_scanned, c_ent);
+    wave_cadd(&w.ctr->candidates, c_cand);
+  }
+}
+
+// Wave tier: one wavefront per spilled probe (list from the lane tier).
 __global__ __launch_bounds__(TB) void k_candidates(DevGraph g, DevBatch b, DevParams P, DevWork w) {
   __shared__ uint32_t hkey[HCAP];
   __shared__ unsigned long long hval[HCAP];
@@ -139,11 +311,9 @@ __global__ __launch_bounds__(TB) void k_candidates(DevGraph g, DevBatch b, DevPa
   __shared__ int cexcl[64];
   __shared__ int s_count, s_over, s_n;
   const int lane = threadIdx.x;
-  for (int64_t p = blockIdx.x; p < b.n_points; p += gridDim.x) {
-    if (!w.is_col[p]) {
-      if (lane == 0) w.ncand[p] = 0;
-      continue;
-    }
+  const int64_t nwork = w.counters_i32[5];
+  for (int64_t it = blockIdx.x; it < nwork; it += gridDim.x) {
+    const int64_t p = w.overflow_list0[it];
     const float lat = b.lat[p], lon = b.lon[p];
     const float r = probe_radius(P, b.acc[p]);
     const float r2 = r * r;
@@ -1102,16 +1272,10 @@ __device__ __forceinline__ void wave_argmin(float v, int idx, float& bv, int& bi
   }
 }
 
-__global__ __launch_bounds__(TB) void k_viterbi(DevBatch b, DevWork w) {
+// Global-memory form for one trace (traces too large for the LDS form).
+__device__ void viterbi_trace_global(int64_t a, int64_t e, DevWork& w) {
   const int lane = threadIdx.x;
-  for (int32_t t = blockIdx.x; t < b.n_traces; t += gridDim.x) {
-    const int64_t a = b.trace_off[t], e = b.trace_off[t + 1];
-    for (int64_t p = a + lane; p < e; p += TB) {
-      w.state[p] = -1;
-      w.chain_start[p] = 0;
-    }
-    __syncthreads();
-    if (w.trace_err[t] != 0) continue;
+  {
     float prev = INFINITY;
     bool open = false;
     int64_t last = -1;
@@ -1180,6 +1344,235 @@ __global__ __launch_bounds__(TB) void k_viterbi(DevBatch b, DevWork w) {
     }
     __syncthreads();
     if (open) backtrack(last);
+    __syncthreads();
+  }
+}
+// LDS form: one wavefront per trace.  The trace's column metadata (and its
+// backpointers, which never touch HBM) live in LDS for the whole trace; the
+// transition block and emissions are streamed through LDS in windows of
+// consecutive columns, each staged with coalesced loads.  The forward pass
+// runs out of LDS with the previous column's scores broadcast by readlane;
+// the backtrack walks LDS; state / chain_start go out coalesced.  Same
+// recurrence, tie rules and chain breaks as viterbi_trace_global.
+constexpr int VIT_PTS = 256;   // points per trace (metadata held for the whole trace)
+constexpr int VIT_BP = 2048;   // candidates per trace (backpointers)
+constexpr int VIT_TW = 1024;   // transition floats per window (>= KMAX * KMAX)
+constexpr int VIT_EW = 512;    // emission floats per window (>= KMAX)
+
+__global__ __launch_bounds__(TB) void k_viterbi(DevBatch b, DevWork w) {
+  __shared__ float sT[VIT_TW];
+  __shared__ float sEm[VIT_EW];
+  __shared__ uint8_t sBp[VIT_BP];
+  __shared__ int32_t sToff[VIT_PTS + 1];
+  __shared__ int16_t sEoff[VIT_PTS + 1];
+  __shared__ int16_t sCprev[VIT_PTS];
+  __shared__ int8_t sKc[VIT_PTS];  // ncand of a column, -1 for a non-column point
+  __shared__ int8_t sState[VIT_PTS];
+  __shared__ uint8_t sCs[VIT_PTS];
+  const int lane = threadIdx.x;
+  for (int32_t t = blockIdx.x; t < b.n_traces; t += gridDim.x) {
+    const int64_t a = b.trace_off[t], e = b.trace_off[t + 1];
+    const int n = (int)(e - a);
+    if (w.trace_err[t] != 0) {
+      for (int64_t p = a + lane; p < e; p += TB) {
+        w.state[p] = -1;
+        w.chain_start[p] = 0;
+      }
+      continue;
+    }
+    const int64_t t0 = w.trans_off[a];
+    int etot = 0;
+    bool fits = n <= VIT_PTS;
+    if (fits) {
+      // column metadata + emission offsets (wave scan of ncand)
+      for (int c = 0; c < n; c += TB) {
+        const int pl = c + lane;
+        int kc = -1, cp = -1, to = 0;
+        if (pl < n) {
+          // independent loads (ncand / col_prev are defined for every point)
+          const int64_t p = a + pl;
+          const uint8_t ic = w.is_col[p];
+          const int32_t nc = w.ncand[p];
+          const int32_t q = w.col_prev[p];
+          const int64_t tp = w.trans_off[p];
+          if (ic) {
+            kc = nc;
+            cp = q >= 0 ? (int)(q - a) : -1;
+          }
+          to = (int)(tp - t0);
+        }
+        const int k = kc > 0 ? kc : 0;
+        const int incl = wave_incl_scan(k, lane);
+        if (pl < n) {
+          sKc[pl] = (int8_t)kc;
+          sCprev[pl] = (int16_t)cp;
+          sToff[pl] = to;
+          sEoff[pl] = (int16_t)min(etot + incl - k, 32767);
+          sState[pl] = -1;
+          sCs[pl] = 0;
+        }
+        etot += __shfl(incl, 63, 64);
+      }
+      fits = etot <= VIT_BP;
+    }
+    if (!fits) {
+      __syncthreads();
+      for (int64_t p = a + lane; p < e; p += TB) {
+        w.state[p] = -1;
+        w.chain_start[p] = 0;
+      }
+      __syncthreads();
+      viterbi_trace_global(a, e, w);
+      continue;
+    }
+    if (lane == 0) {
+      sToff[n] = n > 0 ? (int)(w.trans_off[e] - t0) : 0;
+      sEoff[n] = (int16_t)etot;
+    }
+    __syncthreads();
+    float prev = INFINITY;
+    bool open = false;
+    int last = -1;
+    int win_end = 0, wt0 = 0, we0 = 0;
+    auto backtrack = [&](int endl) {
+      const int Ke = sKc[endl];
+      float bv;
+      int bi;
+      wave_argmin(lane < Ke ? prev : INFINITY, lane, bv, bi);
+      __syncthreads();  // backpointers written by other lanes
+      if (lane == 0) {
+        int pl = endl;
+        int jj = bi;
+        while (true) {
+          sState[pl] = (int8_t)jj;
+          if (sCs[pl]) break;
+          jj = sBp[sEoff[pl] + jj];
+          pl = sCprev[pl];
+        }
+      }
+    };
+    for (int pl = 0; pl < n; ++pl) {
+      const int Kp = sKc[pl];
+      if (Kp < 0) continue;
+      if (Kp == 0) {
+        if (open) backtrack(last);
+        open = false;
+        continue;
+      }
+      if (pl >= win_end) {
+        // next window: the longest run of points from pl whose transitions
+        // and emissions fit (one point always does)
+        __syncthreads();
+        wt0 = sToff[pl];
+        we0 = sEoff[pl];
+        int lo = pl + 1, hi = n;
+        while (lo < hi) {
+          const int mid = (lo + hi + 1) >> 1;
+          if (sToff[mid] - wt0 <= VIT_TW && sEoff[mid] - we0 <= VIT_EW) lo = mid;
+          else hi = mid - 1;
+        }
+        win_end = lo;
+        const int nt = sToff[win_end] - wt0, ne = sEoff[win_end] - we0;
+        for (int f0 = 0; f0 < nt; f0 += 8 * TB) {
+          float v[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            const int f = f0 + u * TB + lane;
+            v[u] = f < nt ? w.trans[t0 + wt0 + f] : 0.0f;
+          }
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            const int f = f0 + u * TB + lane;
+            if (f < nt) sT[f] = v[u];
+          }
+        }
+        for (int f0 = 0; f0 < ne; f0 += 4 * TB) {
+          float v[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int f = f0 + u * TB + lane;
+            v[u] = 0.0f;
+            if (f < ne) {
+              // point holding window candidate f: last q with sEoff[q] <= we0 + f
+              int l2 = pl, h2 = win_end - 1;
+              while (l2 < h2) {
+                const int mid = (l2 + h2 + 1) >> 1;
+                if (sEoff[mid] <= we0 + f) l2 = mid;
+                else h2 = mid - 1;
+              }
+              v[u] = w.cand_emis[(a + l2) * KMAX + (we0 + f - sEoff[l2])];
+            }
+          }
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int f = f0 + u * TB + lane;
+            if (f < ne) sEm[f] = v[u];
+          }
+        }
+        __syncthreads();
+      }
+      const int eo = sEoff[pl];
+      const float em = sEm[eo - we0 + (lane < Kp ? lane : 0)];
+      bool started = false;
+      float cur = INFINITY;
+      if (open && sCprev[pl] == last) {
+        const int Kq = sKc[last];
+        const float* Tm = sT + (sToff[pl] - wt0) + (lane < Kp ? lane : 0);
+        float best = INFINITY;
+        int bi = -1;
+        const int pbits = __float_as_int(prev);
+        int i = 0;
+        for (; i + 4 <= Kq; i += 4) {
+          // four independent LDS reads in flight; visited in i order
+          float tv[4], pv[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            tv[u] = Tm[(i + u) * Kp];
+            pv[u] = __int_as_float(__builtin_amdgcn_readlane(pbits, i + u));
+          }
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const float v = pv[u] + tv[u];
+            if (v < best) {
+              best = v;
+              bi = i + u;
+            }
+          }
+        }
+        for (; i < Kq; ++i) {
+          const float v = __int_as_float(__builtin_amdgcn_readlane(pbits, i)) + Tm[i * Kp];
+          if (v < best) {
+            best = v;
+            bi = i;
+          }
+        }
+        const bool alive = lane < Kp && bi >= 0;
+        if (lane < Kp) {
+          cur = alive ? best + em : INFINITY;
+          sBp[eo + lane] = alive ? (uint8_t)bi : (uint8_t)0xFF;
+        }
+        if (__ballot(alive) == 0ull) {
+          backtrack(last);
+        } else {
+          started = true;
+        }
+      } else if (open) {
+        backtrack(last);
+      }
+      if (!started) {
+        cur = lane < Kp ? em : INFINITY;
+        if (lane == 0) sCs[pl] = 1;
+      }
+      prev = cur;
+      open = true;
+      last = pl;
+    }
+    if (open) backtrack(last);
+    __syncthreads();
+    for (int pl = lane; pl < n; pl += TB) {
+      w.state[a + pl] = sState[pl];
+      w.chain_start[a + pl] = sCs[pl];
+    }
     __syncthreads();
   }
 }
@@ -1579,7 +1972,8 @@ void launch_columns(const DevBatch& b, const DevParams& p, DevWork& w, hipStream
   hipLaunchKernelGGL(k_columns, dim3(grid_for(b.n_traces, 256, 1 << 30)), dim3(256), 0, s, b, p, w);
 }
 void launch_candidates(const DevGraph& g, const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s) {
-  hipLaunchKernelGGL(k_candidates, dim3(grid_for(b.n_points, 1, WAVE_GRID_CAP)), dim3(TB), 0, s, g, b, p, w);
+  hipLaunchKernelGGL(k_cand_lane, dim3(grid_for(b.n_points, CAND_TB, 1 << 30)), dim3(CAND_TB), 0, s, g, b, p, w);
+  hipLaunchKernelGGL(k_candidates, dim3(4096), dim3(TB), 0, s, g, b, p, w);
 }
 void launch_links(const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s) {
   hipLaunchKernelGGL(k_links, dim3(grid_for(b.n_points + 1, 256, 1 << 30)), dim3(256), 0, s, b, p, w);

@@ -103,6 +103,26 @@ def test_long_gaps_force_global_tier(small_graph, oracle, results_equal):
     _run_both(small_graph, b, oracle, results_equal)
 
 
+def test_long_traces_mixed_lengths(small_graph, oracle, results_equal):
+    # traces longer than the Viterbi LDS window (256 points) take the
+    # global-memory form; mixed with short ones in one batch
+    long_b = synth.make_traces(small_graph, 12, 400, interval_s=5.0, noise_sigma_m=15.0, accuracy=15.0, seed=31)
+    short_b = synth.make_traces(small_graph, 40, 30, interval_s=5.0, noise_sigma_m=15.0, accuracy=15.0, seed=32)
+    off = np.concatenate([long_b["trace_off"], short_b["trace_off"][1:] + long_b["trace_off"][-1]])
+    b = {k: np.concatenate([long_b[k], short_b[k]]) for k in ("lat", "lon", "time", "accuracy")}
+    b["trace_off"] = off
+    _run_both(small_graph, b, oracle, results_equal)
+
+
+def test_dense_candidates_spill_tiers(small_graph, oracle, results_equal):
+    # a 300 m search radius puts dozens of distinct edges in range: probes
+    # spill from the lane candidate tier to the wave tier, and the candidate
+    # count per trace outgrows the Viterbi LDS window
+    b = synth.make_traces(small_graph, 30, 60, interval_s=5.0, noise_sigma_m=15.0, accuracy=15.0, seed=33)
+    _run_both(small_graph, b, oracle, results_equal,
+              meili=dict(search_radius=300.0, max_search_radius=300.0, max_candidates=32))
+
+
 def test_edge_cases(small_graph, oracle, results_equal):
     base = synth.make_traces(small_graph, 8, 20, interval_s=5.0, noise_sigma_m=15.0, accuracy=15.0, seed=21)
     lat, lon, tm, acc = (list(base[k]) for k in ("lat", "lon", "time", "accuracy"))

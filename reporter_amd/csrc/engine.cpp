@@ -118,8 +118,8 @@ int engine_init(otm_engine* E, const char* graph_path, int device, std::string* 
 // Bounded distance index: part of flattening the graph into HBM, like the
 // tile preprocessing behind valhalla.Configure (py/reporter_service.py:279).
 // Row u = every node within rmax road metres of u, with D and predecessor
-// edge, sorted by node id.  Two passes of the same deterministic search:
-// count, scan, write.
+// edge, in a per-row open-addressing table.  Two passes of the same
+// deterministic search: count, size + scan, insert.
 int build_index(otm_engine* E, std::string* err) {
   E->idx = DevIndex{};
   E->idx.rmax = 0.0f;
@@ -132,28 +132,31 @@ int build_index(otm_engine* E, std::string* err) {
   HIPCHK(hipEventRecord(a, s));
   int32_t* row_cnt = nullptr;
   int64_t* row_off = nullptr;
+  IdxRow* rows = nullptr;
   HIPCHK(hipMalloc(&row_cnt, ((size_t)N + 1) * 4));
   E->graph_allocs.push_back(row_cnt);
   HIPCHK(hipMalloc(&row_off, ((size_t)N + 1) * 8));
   E->graph_allocs.push_back(row_off);
-  launch_index_build(E->g, E->index_rmax, row_cnt, nullptr, nullptr, nullptr, nullptr, false, s);
+  HIPCHK(hipMalloc(&rows, ((size_t)N + 1) * sizeof(IdxRow)));
+  E->graph_allocs.push_back(rows);
+  launch_index_build(E->g, E->index_rmax, row_cnt, nullptr, nullptr, nullptr, false, s);
   launch_row_sizes(row_cnt, row_off, N, s);
   size_t tmpb = scan_tmp_bytes(N) + 256;
   void* tmp = nullptr;
   HIPCHK(hipMalloc(&tmp, tmpb));
   scan_i64(row_off, N, tmp, tmpb, s);
+  launch_row_pack(row_cnt, row_off, rows, N, s);
   int64_t total = 0;
   HIPCHK(hipMemcpyAsync(&total, row_off + N, 8, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
   (void)hipFree(tmp);
-  void *node = nullptr, *dist = nullptr, *pred = nullptr;
-  HIPCHK(hipMalloc(&node, ((size_t)total + 1) * 4));
-  E->graph_allocs.push_back(node);
-  HIPCHK(hipMalloc(&dist, ((size_t)total + 1) * 4));
-  E->graph_allocs.push_back(dist);
+  void *slot = nullptr, *pred = nullptr;
+  HIPCHK(hipMalloc(&slot, ((size_t)total + 1) * 8));
+  E->graph_allocs.push_back(slot);
+  HIPCHK(hipMemsetAsync(slot, 0xFF, ((size_t)total + 1) * 8, s));
   HIPCHK(hipMalloc(&pred, ((size_t)total + 1) * 4));
   E->graph_allocs.push_back(pred);
-  launch_index_build(E->g, E->index_rmax, row_cnt, row_off, (uint32_t*)node, (float*)dist, (int32_t*)pred, true, s);
+  launch_index_build(E->g, E->index_rmax, row_cnt, rows, (uint2*)slot, (int32_t*)pred, true, s);
   HIPCHK(hipEventRecord(z, s));
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventSynchronize(z));
@@ -163,13 +166,15 @@ int build_index(otm_engine* E, std::string* err) {
   std::vector<int32_t> cnt((size_t)N);
   HIPCHK(hipMemcpy(cnt.data(), row_cnt, (size_t)N * 4, hipMemcpyDeviceToHost));
   E->index_incomplete_rows = 0;
-  for (int32_t c : cnt) E->index_incomplete_rows += c < 0;
-  E->index_entries = total;
+  E->index_entries = 0;
+  for (int32_t c : cnt) {
+    E->index_incomplete_rows += c < 0;
+    E->index_entries += c > 0 ? c : 0;
+  }
+  E->index_slots = total;
   E->idx.rmax = E->index_rmax;
-  E->idx.row_cnt = row_cnt;
-  E->idx.row_off = row_off;
-  E->idx.node = (const uint32_t*)node;
-  E->idx.dist = (const float*)dist;
+  E->idx.row = rows;
+  E->idx.slot = (const uint2*)slot;
   E->idx.pred = (const int32_t*)pred;
   return OTM_OK;
 }

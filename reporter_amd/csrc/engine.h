@@ -23,6 +23,7 @@ struct otm_engine {
   float index_rmax = 1000.0f;
   otm::DevIndex idx{};
   int64_t index_entries = 0;
+  int64_t index_slots = 0;  // hash-table slots (8 B each + 4 B predecessor)
   int32_t index_incomplete_rows = 0;
   float index_build_ms = 0.0f;
   otm::MatchConfig mc;

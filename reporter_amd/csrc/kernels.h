@@ -47,16 +47,21 @@ struct DevGraph {
 };
 
 // Bounded distance index (built once per engine): for every
-// node u the nodes v with D(u,v) <= rmax, sorted by v, with D and the
-// predecessor edge of the search fixed point.  row_cnt[u] < 0 marks a row
-// whose search exceeded the build table (queries on it use the online tiers).
+// node u the nodes v with D(u,v) <= rmax, with D and the predecessor edge of
+// the search fixed point, held as one open-addressing hash table per row
+// (capacity a power of two >= 2 x entries, linear probing) so a lookup is
+// about one 8-byte read.  cnt < 0 marks a row whose search exceeded the build
+// table (queries on it use the online tiers).
+struct IdxRow {
+  int64_t off;    // first slot of the row's table
+  int32_t cnt;    // entries, -1 incomplete
+  uint32_t mask;  // capacity - 1
+};
 struct DevIndex {
   float rmax;  // 0: no index
-  const int32_t* row_cnt;
-  const int64_t* row_off;
-  const uint32_t* node;
-  const float* dist;
-  const int32_t* pred;
+  const IdxRow* row;
+  const uint2* slot;     // {node (0xFFFFFFFF empty), D bits}
+  const int32_t* pred;   // per slot
 };
 constexpr int INDEX_BUILD_CAP = 2048;   // LDS table of the index builder
 constexpr int INDEX_BUILD_LIMIT = 1536; // nodes per row before the row is left incomplete
@@ -152,10 +157,12 @@ void launch_viterbi(const DevBatch& b, DevWork& w, hipStream_t s);
 void launch_route(const DevGraph& g, const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s);
 void launch_segments(const DevGraph& g, const DevBatch& b, DevWork& w, DevOut& o, bool write, hipStream_t s);
 void launch_report(const DevBatch& b, const DevReportCfg& rc, DevWork& w, DevOut& o, hipStream_t s);
-// index build: pass 0 counts rows (row_cnt), pass 1 writes them at row_off
-void launch_index_build(const DevGraph& g, float rmax, int32_t* row_cnt, const int64_t* row_off, uint32_t* node,
-                        float* dist, int32_t* pred, bool write, hipStream_t s);
+// index build: pass 0 counts rows (row_cnt), pass 1 inserts them into the
+// row tables (slot array pre-filled with 0xFF)
+void launch_index_build(const DevGraph& g, float rmax, int32_t* row_cnt, const IdxRow* rows, uint2* slot,
+                        int32_t* pred, bool write, hipStream_t s);
 void launch_row_sizes(const int32_t* row_cnt, int64_t* row_sizes, int32_t n, hipStream_t s);
+void launch_row_pack(const int32_t* row_cnt, const int64_t* row_off, IdxRow* rows, int32_t n, hipStream_t s);
 // exclusive scan helpers (in place over n+1 elements: out[n] = total)
 void scan_i64(int64_t* d, int64_t n, void* tmp, size_t tmp_bytes, hipStream_t s);
 void scan_i32(int32_t* d, int64_t n, void* tmp, size_t tmp_bytes, hipStream_t s);

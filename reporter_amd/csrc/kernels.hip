@@ -860,40 +860,44 @@ __global__ __launch_bounds__(LANE_TB) void k_route_lane(DevGraph g, DevBatch b, 
 }
 
 // ============================================================== distance index
-// Row lookup: binary search of v in u's row (sorted by node id).
-// Returns 1 found (D, pred set), 0 absent (D(u,v) > rmax), -1 row incomplete.
-__device__ __forceinline__ int idx_lookup(const DevIndex& X, int32_t u, uint32_t v, float& D, int32_t& pred) {
-  const int32_t n = X.row_cnt[u];
-  if (n < 0) return -1;
-  int64_t lo = X.row_off[u], hi = lo + n - 1;
-  while (lo <= hi) {
-    const int64_t mid = (lo + hi) >> 1;
-    const uint32_t x = X.node[mid];
-    if (x == v) {
-      D = X.dist[mid];
-      pred = X.pred[mid];
-      return 1;
+__device__ __forceinline__ uint32_t idx_hash(uint32_t v) {
+  v ^= v >> 16;
+  v *= 0x85ebca6bu;
+  v ^= v >> 13;
+  v *= 0xc2b2ae35u;
+  v ^= v >> 16;
+  return v;
+}
+
+// Row lookup: linear probing in u's table.  Returns the slot (D set) when v is
+// in the row, -1 when absent (D(u,v) > rmax), -2 when the row is incomplete.
+__device__ __forceinline__ int64_t idx_find(const DevIndex& X, const IdxRow& R, uint32_t v, float& D) {
+  if (R.cnt < 0) return -2;
+  if (R.cnt == 0) return -1;
+  uint32_t h = idx_hash(v) & R.mask;
+  while (true) {
+    const uint2 sl = X.slot[R.off + h];
+    if (sl.x == v) {
+      D = bitsf(sl.y);
+      return R.off + h;
     }
-    if (x < v) lo = mid + 1;
-    else hi = mid - 1;
+    if (sl.x == EMPTY) return -1;
+    h = (h + 1) & R.mask;
   }
-  return 0;
 }
 
 // Index build: one wavefront per source node u runs the bounded search with
 // bound rmax in an LDS table of INDEX_BUILD_CAP slots (same fixed point as the
 // online tiers), then writes the settled nodes sorted by id.
 template <bool WRITE>
-__global__ __launch_bounds__(TB) void k_index_build(DevGraph g, float rmax, int32_t* row_cnt, const int64_t* row_off,
-                                                    uint32_t* out_node, float* out_dist, int32_t* out_pred) {
+__global__ __launch_bounds__(TB) void k_index_build(DevGraph g, float rmax, int32_t* row_cnt, const IdxRow* rows,
+                                                    uint2* slot, int32_t* pred) {
   __shared__ uint32_t lkey[INDEX_BUILD_CAP];
   __shared__ unsigned long long llab[INDEX_BUILD_CAP];
   __shared__ uint32_t linq[INDEX_BUILD_CAP];
   __shared__ uint32_t lfr0[INDEX_BUILD_CAP];
   __shared__ uint32_t lfr1[INDEX_BUILD_CAP];
-  __shared__ unsigned long long sortk[WRITE ? INDEX_BUILD_CAP : 1];
   __shared__ SearchShared S;
-  __shared__ int s_n;
   const int lane = threadIdx.x;
   const Table T{lkey, llab, linq, lfr0, lfr1, 11, INDEX_BUILD_LIMIT};
   for (int32_t u = blockIdx.x; u < g.n_nodes; u += gridDim.x) {
@@ -903,83 +907,100 @@ __global__ __launch_bounds__(TB) void k_index_build(DevGraph g, float rmax, int3
       continue;
     }
     if (settled < 0) continue;
-    if (lane == 0) s_n = 0;
-    __syncthreads();
+    // insert the settled nodes into the row's table (slot order depends on
+    // CAS order; lookups do not)
+    const IdxRow R = rows[u];
     for (int i = lane; i < INDEX_BUILD_CAP; i += TB) {
       const uint32_t k = lkey[i];
-      if (k != EMPTY) {
-        const int idx = atomicAdd(&s_n, 1);
-        sortk[idx] = ((unsigned long long)k << 11) | (unsigned long long)i;
-      }
-    }
-    __syncthreads();
-    const int n = s_n;
-    int N = 1;
-    while (N < n) N <<= 1;
-    for (int i = n + lane; i < N; i += TB) sortk[i] = LAB_NONE;
-    __syncthreads();
-    for (int kk = 2; kk <= N; kk <<= 1) {
-      for (int j = kk >> 1; j > 0; j >>= 1) {
-        for (int i = lane; i < N; i += TB) {
-          const int ixj = i ^ j;
-          if (ixj > i) {
-            const unsigned long long x = sortk[i], y = sortk[ixj];
-            const bool up = (i & kk) == 0;
-            if ((x > y) == up) {
-              sortk[i] = y;
-              sortk[ixj] = x;
-            }
-          }
-        }
-        __syncthreads();
-      }
-    }
-    const int64_t base = row_off[u];
-    for (int i = lane; i < n; i += TB) {
-      const unsigned long long sk = sortk[i];
-      const int slot = (int)(sk & 2047ull);
-      const unsigned long long lab = llab[slot];
-      out_node[base + i] = (uint32_t)(sk >> 11);
-      out_dist[base + i] = bitsf((uint32_t)(lab >> 32));
-      out_pred[base + i] = (int32_t)(uint32_t)(lab & 0xFFFFFFFFull);
+      if (k == EMPTY) continue;
+      const unsigned long long lab = llab[i];
+      uint32_t h = idx_hash(k) & R.mask;
+      while (atomicCAS(&slot[R.off + h].x, EMPTY, k) != EMPTY) h = (h + 1) & R.mask;
+      slot[R.off + h].y = (uint32_t)(lab >> 32);
+      pred[R.off + h] = (int32_t)(uint32_t)(lab & 0xFFFFFFFFull);
     }
     __syncthreads();
   }
 }
 
+// table capacity of a row: the power of two >= 2 x entries
 __global__ void k_row_sizes(const int32_t* row_cnt, int64_t* sizes, int32_t n) {
   const int32_t u = blockIdx.x * blockDim.x + threadIdx.x;
-  if (u < n) sizes[u] = row_cnt[u] > 0 ? row_cnt[u] : 0;
+  if (u < n) {
+    const int32_t c = row_cnt[u];
+    int64_t cap = 0;
+    if (c > 0) {
+      cap = 2;
+      while (cap < 2 * (int64_t)c) cap <<= 1;
+    }
+    sizes[u] = cap;
+  }
   if (u == n) sizes[n] = 0;
 }
 
+__global__ void k_row_pack(const int32_t* row_cnt, const int64_t* row_off, IdxRow* rows, int32_t n) {
+  const int32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= n) return;
+  const int64_t cap = row_off[u + 1] - row_off[u];
+  rows[u] = IdxRow{row_off[u], row_cnt[u], (uint32_t)(cap > 0 ? cap - 1 : 0)};
+}
+
 // K4 index tier: one wavefront per column pair, lanes over the Kq x Kp
-// (source candidate, target candidate) pairs; each pair is one binary search
-// in the source node's index row.  Columns the index cannot answer (bound >
-// rmax, or a source row incomplete) go to the search tiers.
+// (source candidate, target candidate) pairs; each pair is one probe of the
+// source node's index row.  Loads are grouped by what they depend on (point p,
+// then column q, then edges, then rows) so a column costs ~5 memory round
+// trips.  Columns the index cannot answer (bound > rmax, or a source row
+// incomplete) go to the search tiers.
 __global__ __launch_bounds__(TB) void k_trans_index(DevGraph g, DevBatch b, DevParams P, DevWork w) {
-  __shared__ int32_t eq[KMAX], ep[KMAX], uq[KMAX], vp[KMAX];
-  __shared__ float oq[KMAX], op[KMAX];
+  __shared__ int32_t ep[KMAX], vp[KMAX], eq[KMAX];
+  __shared__ float op[KMAX], oq[KMAX], sq[KMAX];
+  __shared__ IdxRow rq[KMAX];
   const int lane = threadIdx.x;
   const DevIndex& X = w.idx;
   unsigned long long c_search = 0, c_settled = 0, c_relaxed = 0, c_trans = 0;
   for (int64_t p = blockIdx.x; p < b.n_points; p += gridDim.x) {
+    // by p
     const int32_t q = w.col_prev[p];
-    if (q < 0) continue;
-    const int Kq = w.ncand[q], Kp = w.ncand[p];
+    const int Kp = w.ncand[p];
     const float gcv = w.gc[p];
-    const float bound = P.factor * gcv;
-    bool usable = bound <= X.rmax;
+    const int64_t toff = w.trans_off[p];
+    int32_t e_p = 0;
+    float o_p = 0.0f;
+    if (lane < KMAX) {
+      e_p = w.cand_edge[p * KMAX + lane];
+      o_p = w.cand_off[p * KMAX + lane];
+    }
+    if (q < 0) continue;
+    // by q
+    const int Kq = w.ncand[q];
+    int32_t e_q = 0;
+    float o_q = 0.0f;
+    if (lane < KMAX) {
+      e_q = w.cand_edge[(int64_t)q * KMAX + lane];
+      o_q = w.cand_off[(int64_t)q * KMAX + lane];
+    }
+    // by edge
+    int32_t u = 0;
+    float len_q = 0.0f;
     if (lane < Kq) {
-      eq[lane] = w.cand_edge[(int64_t)q * KMAX + lane];
-      oq[lane] = w.cand_off[(int64_t)q * KMAX + lane];
-      uq[lane] = g.e_to[eq[lane]];
-      usable = usable && X.row_cnt[uq[lane]] >= 0;
+      u = g.e_to[e_q];
+      len_q = g.e_len[e_q];
     }
     if (lane < Kp) {
-      ep[lane] = w.cand_edge[p * KMAX + lane];
-      op[lane] = w.cand_off[p * KMAX + lane];
-      vp[lane] = g.e_from[ep[lane]];
+      ep[lane] = e_p;
+      op[lane] = o_p;
+      vp[lane] = g.e_from[e_p];
+    }
+    // by row
+    const float bound = P.factor * gcv;
+    bool usable = X.rmax > 0.0f && bound <= X.rmax;
+    if (lane < Kq && usable) {  // (no rows at all when the index is off)
+      const IdxRow R = X.row[u];
+      usable = R.cnt >= 0;
+      eq[lane] = e_q;
+      oq[lane] = o_q;
+      sq[lane] = len_q - o_q;
+      rq[lane] = R;
     }
     if (__ballot(!usable) != 0ull) {
       if (lane == 0) {
@@ -990,7 +1011,7 @@ __global__ __launch_bounds__(TB) void k_trans_index(DevGraph g, DevBatch b, DevP
       continue;
     }
     __syncthreads();
-    float* Tm = w.trans + w.trans_off[p];
+    float* Tm = w.trans + toff;
     unsigned long long ntr = 0;
     for (int idx = lane; idx < Kq * Kp; idx += TB) {
       const int i = idx / Kp, j = idx - (idx / Kp) * Kp;
@@ -1000,10 +1021,8 @@ __global__ __launch_bounds__(TB) void k_trans_index(DevGraph g, DevBatch b, DevP
         r = op[j] - oq[i];
       } else {
         float D;
-        int32_t pr;
-        if (idx_lookup(X, uq[i], (uint32_t)vp[j], D, pr) == 1) {
-          const float start = g.e_len[eq[i]] - oq[i];
-          const float sd = start + D;
+        if (idx_find(X, rq[i], (uint32_t)vp[j], D) >= 0) {
+          const float sd = sq[i] + D;
           r = sd + op[j];
         } else {
           ok = false;
@@ -1022,16 +1041,15 @@ __global__ __launch_bounds__(TB) void k_trans_index(DevGraph g, DevBatch b, DevP
       // the row entries with D <= bound and their out-degrees
       for (int i = 0; i < Kq; ++i) {
         bool first = true;
-        for (int k = 0; k < i; ++k) first = first && uq[k] != uq[i];
+        for (int k = 0; k < i; ++k) first = first && rq[k].off != rq[i].off;
         if (!first) continue;
-        const int64_t o = X.row_off[uq[i]];
-        const int32_t n = X.row_cnt[uq[i]];
+        const IdxRow R = rq[i];
         unsigned long long st = 0, rl = 0;
-        for (int k = lane; k < n; k += TB) {
-          if (X.dist[o + k] <= bound) {
+        for (int64_t k = lane; k <= (int64_t)R.mask && R.cnt > 0; k += TB) {
+          const uint2 sl = X.slot[R.off + k];
+          if (sl.x != EMPTY && bitsf(sl.y) <= bound) {
             ++st;
-            const uint32_t v = X.node[o + k];
-            rl += (unsigned long long)(g.out_off[v + 1] - g.out_off[v]);
+            rl += (unsigned long long)(g.out_off[sl.x + 1] - g.out_off[sl.x]);
           }
         }
         for (int sh = 32; sh > 0; sh >>= 1) {
@@ -1056,7 +1074,7 @@ __global__ __launch_bounds__(TB) void k_trans_index(DevGraph g, DevBatch b, DevP
 }
 
 // K6 index tier: one lane per matched step; the path is read back from the
-// index row of the source node (predecessor edges), one binary search per edge.
+// index row of the source node (predecessor edges), one table probe per edge.
 __global__ __launch_bounds__(256) void k_route_index(DevGraph g, DevBatch b, DevParams P, DevWork w) {
   const DevIndex& X = w.idx;
   unsigned long long c_search = 0, c_settled = 0, c_relaxed = 0, c_edges = 0;
@@ -1076,21 +1094,28 @@ __global__ __launch_bounds__(256) void k_route_index(DevGraph g, DevBatch b, Dev
     }
     const float bound = P.factor * w.gc[p];
     const int32_t u = g.e_to[ei], v = g.e_from[ej];
-    float Dv;
-    int32_t pe;
-    if (!(bound <= X.rmax) || idx_lookup(X, u, (uint32_t)v, Dv, pe) != 1) {
+    const float len_i = g.e_len[ei];
+    float Dv = 0.0f;
+    IdxRow R{};
+    int64_t sv = -1;
+    if (X.rmax > 0.0f && bound <= X.rmax) {
+      R = X.row[u];
+      sv = idx_find(X, R, (uint32_t)v, Dv);
+    }
+    if (sv < 0) {
       const int slot = atomicAdd(&w.counters_i32[4], 1);
       w.overflow_list0[slot] = (int32_t)p;
       continue;
     }
     int len = 0;
-    const int32_t rowlen = X.row_cnt[u];
-    for (int32_t x = v; x != u && len <= rowlen;) {
-      float dd;
-      int32_t px;
-      idx_lookup(X, u, (uint32_t)x, dd, px);
+    for (int32_t x = v, px = w.idx.pred[sv]; x != u && len <= R.cnt;) {
       ++len;
       x = g.e_from[px];
+      if (x == u) break;
+      float dd;
+      const int64_t sx = idx_find(X, R, (uint32_t)x, dd);
+      if (sx < 0) break;  // (cannot happen: predecessor chains stay in the row)
+      px = X.pred[sx];
     }
     const int off = len ? atomicAdd(&w.counters_i32[1], len) : 0;
     if (off + len > w.pool_cap) {
@@ -1098,29 +1123,30 @@ __global__ __launch_bounds__(256) void k_route_index(DevGraph g, DevBatch b, Dev
       w.path_len[p] = -1;
     } else {
       int k = len;
-      for (int32_t x = v; x != u;) {
-        float dd;
-        int32_t px;
-        idx_lookup(X, u, (uint32_t)x, dd, px);
+      for (int32_t x = v, px = X.pred[sv]; x != u;) {
         w.path_pool[off + (--k)] = px;
         x = g.e_from[px];
+        if (x == u) break;
+        float dd;
+        const int64_t sx = idx_find(X, R, (uint32_t)x, dd);
+        if (sx < 0 || k == 0) break;
+        px = X.pred[sx];
       }
       w.path_off[p] = off;
       w.path_len[p] = len;
     }
-    const float start = g.e_len[ei] - oi;
+    const float start = len_i - oi;
     const float sd = start + Dv;
     w.route_dist[p] = sd + oj;
     if (w.ctr) {
-      const int64_t o = X.row_off[u];
-      const int32_t n = X.row_cnt[u];
       unsigned long long st = 0, rl = 0;
-      for (int k = 0; k < n; ++k)
-        if (X.dist[o + k] <= bound) {
+      for (int64_t k = 0; k <= (int64_t)R.mask; ++k) {
+        const uint2 sl = X.slot[R.off + k];
+        if (sl.x != EMPTY && bitsf(sl.y) <= bound) {
           ++st;
-          const uint32_t y = X.node[o + k];
-          rl += (unsigned long long)(g.out_off[y + 1] - g.out_off[y]);
+          rl += (unsigned long long)(g.out_off[sl.x + 1] - g.out_off[sl.x]);
         }
+      }
       ++c_search;
       c_settled += st;
       c_relaxed += rl;
@@ -2012,17 +2038,20 @@ void launch_report(const DevBatch& b, const DevReportCfg& rc, DevWork& w, DevOut
   hipLaunchKernelGGL(k_report, dim3(grid_for(b.n_traces, 64, 1 << 30)), dim3(64), 0, s, b, rc, w, o, 0);
 }
 
-void launch_index_build(const DevGraph& g, float rmax, int32_t* row_cnt, const int64_t* row_off, uint32_t* node,
-                        float* dist, int32_t* pred, bool write, hipStream_t s) {
+void launch_index_build(const DevGraph& g, float rmax, int32_t* row_cnt, const IdxRow* rows, uint2* slot,
+                        int32_t* pred, bool write, hipStream_t s) {
   const int grid = grid_for(g.n_nodes, 1, 256 * 16);
   if (write)
-    hipLaunchKernelGGL(k_index_build<true>, dim3(grid), dim3(TB), 0, s, g, rmax, row_cnt, row_off, node, dist, pred);
+    hipLaunchKernelGGL(k_index_build<true>, dim3(grid), dim3(TB), 0, s, g, rmax, row_cnt, rows, slot, pred);
   else
-    hipLaunchKernelGGL(k_index_build<false>, dim3(grid), dim3(TB), 0, s, g, rmax, row_cnt, row_off, node, dist, pred);
+    hipLaunchKernelGGL(k_index_build<false>, dim3(grid), dim3(TB), 0, s, g, rmax, row_cnt, rows, slot, pred);
 }
 void launch_row_sizes(const int32_t* row_cnt, int64_t* row_sizes, int32_t n, hipStream_t s) {
   hipLaunchKernelGGL(k_row_sizes, dim3(grid_for((int64_t)n + 1, 256, 1 << 30)), dim3(256), 0, s, row_cnt, row_sizes,
                      n);
+}
+void launch_row_pack(const int32_t* row_cnt, const int64_t* row_off, IdxRow* rows, int32_t n, hipStream_t s) {
+  hipLaunchKernelGGL(k_row_pack, dim3(grid_for((int64_t)n, 256, 1 << 30)), dim3(256), 0, s, row_cnt, row_off, rows, n);
 }
 
 size_t scan_tmp_bytes(int64_t n) {

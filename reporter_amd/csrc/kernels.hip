@@ -121,32 +121,80 @@ __device__ __forceinline__ int wave_incl_scan(int v, int lane) {
 }
 
 // ============================================================== K1 columns
-__global__ __launch_bounds__(256) void k_columns(DevBatch b, DevParams P, DevWork w) {
-  const int32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= b.n_traces) return;
-  const int64_t a = b.trace_off[t], e = b.trace_off[t + 1];
-  int64_t last = -1;
-  unsigned long long ncols = 0;
-  for (int64_t p = a; p < e; ++p) {
-    w.pt_trace[p] = t;
-    w.is_col[p] = 0;
-    w.prevc[p] = -1;
-    w.gc[p] = 0.0f;
-    float gcv = 0.0f;
-    if (last >= 0) {
-      gcv = gc_dist(b.lat[last], b.lon[last], b.lat[p], b.lon[p]);
-      if (!(gcv >= P.interp)) continue;
+// One wavefront per trace: lanes stage the trace's coordinates in LDS and
+// compute the distance of every point to its predecessor in parallel; lane 0
+// then runs the interpolation filter (a point is a column iff it lies at least
+// interpolation_distance from the last column) out of LDS, recomputing the
+// distance only where the last column is not the immediate predecessor.
+constexpr int COL_PTS = 512;
+__global__ __launch_bounds__(TB) void k_columns(DevBatch b, DevParams P, DevWork w) {
+  __shared__ float sLat[COL_PTS], sLon[COL_PTS], sGc[COL_PTS];
+  __shared__ int32_t sPrev[COL_PTS];
+  __shared__ uint8_t sCol[COL_PTS];
+  const int lane = threadIdx.x;
+  for (int32_t t = blockIdx.x; t < b.n_traces; t += gridDim.x) {
+    const int64_t a = b.trace_off[t], e = b.trace_off[t + 1];
+    const int n = (int)(e - a);
+    int ncols = 0;
+    if (n > COL_PTS) {
+      // long trace: the same filter straight from HBM
+      if (lane == 0) {
+        int64_t last = -1;
+        for (int64_t p = a; p < e; ++p) {
+          float gcv = 0.0f;
+          if (last >= 0) gcv = gc_dist(b.lat[last], b.lon[last], b.lat[p], b.lon[p]);
+          const bool col = last < 0 || gcv >= P.interp;
+          w.is_col[p] = col ? 1 : 0;
+          w.gc[p] = col ? gcv : 0.0f;
+          w.prevc[p] = col ? (int32_t)last : -1;
+          if (col) {
+            last = p;
+            ++ncols;
+          }
+        }
+      }
+      for (int64_t p = a + lane; p < e; p += TB) w.pt_trace[p] = t;
+    } else {
+      for (int pl = lane; pl < n; pl += TB) {
+        sLat[pl] = b.lat[a + pl];
+        sLon[pl] = b.lon[a + pl];
+      }
+      __syncthreads();
+      for (int pl = lane; pl < n; pl += TB)
+        sGc[pl] = pl > 0 ? gc_dist(sLat[pl - 1], sLon[pl - 1], sLat[pl], sLon[pl]) : 0.0f;
+      __syncthreads();
+      if (lane == 0) {
+        int last = -1;
+        for (int pl = 0; pl < n; ++pl) {
+          float gcv = 0.0f;
+          if (last >= 0) gcv = last == pl - 1 ? sGc[pl] : gc_dist(sLat[last], sLon[last], sLat[pl], sLon[pl]);
+          const bool col = last < 0 || gcv >= P.interp;
+          sCol[pl] = col ? 1 : 0;
+          sGc[pl] = col ? gcv : 0.0f;
+          sPrev[pl] = col && last >= 0 ? (int32_t)(a + last) : -1;
+          if (col) {
+            last = pl;
+            ++ncols;
+          }
+        }
+      }
+      __syncthreads();
+      for (int pl = lane; pl < n; pl += TB) {
+        const int64_t p = a + pl;
+        w.pt_trace[p] = t;
+        w.is_col[p] = sCol[pl];
+        w.gc[p] = sGc[pl];
+        w.prevc[p] = sPrev[pl];
+      }
+      __syncthreads();
     }
-    w.is_col[p] = 1;
-    w.gc[p] = gcv;
-    w.prevc[p] = (int32_t)last;
-    last = p;
-    ++ncols;
-  }
-  w.trace_err[t] = 0;
-  if (w.ctr) {
-    cadd(&w.ctr->points, (unsigned long long)(e - a));
-    cadd(&w.ctr->columns, ncols);
+    if (lane == 0) {
+      w.trace_err[t] = 0;
+      if (w.ctr) {
+        cadd(&w.ctr->points, (unsigned long long)n);
+        cadd(&w.ctr->columns, (unsigned long long)ncols);
+      }
+    }
   }
 }
 
@@ -1691,16 +1739,39 @@ __global__ __launch_bounds__(TB) void k_route(DevGraph g, DevBatch b, DevParams 
 }
 
 // ============================================================== K7 segments
+// Per-edge attributes the emitter needs, carried with each traversal so the
+// serial grouping never goes back to HBM for a state edge.
+struct EAttr {
+  float len;
+  int32_t seg, seg_pos;
+  uint32_t flags;
+  int64_t way;
+  uint64_t gid;  // segment id / length of e_seg (when seg >= 0)
+  float glen;
+};
+
+__device__ __forceinline__ EAttr edge_attr(const DevGraph& g, int32_t e) {
+  EAttr a;
+  a.len = g.e_len[e];
+  a.seg = g.e_seg[e];
+  a.seg_pos = g.e_seg_pos[e];
+  a.flags = g.e_flags[e];
+  a.way = g.e_way[e];
+  a.gid = a.seg >= 0 ? g.g_id[a.seg] : 0ull;
+  a.glen = a.seg >= 0 ? g.g_len[a.seg] : 0.0f;
+  return a;
+}
+
 struct Trav {
   int32_t edge;
   float off0, off1;
   double t0, t1;
   int32_t sh0, sh1;
+  EAttr at;
 };
 
 template <bool WRITE>
 struct SegEmitter {
-  const DevGraph* g;
   DevOut* o;
   int32_t seg_base, way_base;  // write positions (WRITE)
   int32_t nseg = 0, nway = 0;
@@ -1710,8 +1781,8 @@ struct SegEmitter {
   int32_t way_start = 0;
   int64_t last_way = 0;
 
-  __device__ void add_way(int32_t edge) {
-    const int64_t way = g->e_way[edge];
+  __device__ void add_way(const EAttr& at) {
+    const int64_t way = at.way;
     if (nway > way_start && last_way == way) return;
     if (WRITE) o->way_ids[way_base + nway] = way;
     last_way = way;
@@ -1721,20 +1792,20 @@ struct SegEmitter {
     if (!has) return;
     if (WRITE) {
       otm_segment s;
-      const int32_t sg = g->e_seg[first.edge];
+      const int32_t sg = first.at.seg;
       bool sv, ev;
       s.flags = 0u;
       if (sg >= 0) {
-        sv = first.off0 == 0.0f && (g->e_flags[first.edge] & OTM_EDGE_SEG_BEGIN_D);
-        ev = last.off1 == g->e_len[last.edge] && (g->e_flags[last.edge] & OTM_EDGE_SEG_END_D);
-        s.segment_id = (int64_t)g->g_id[sg];
-        s.length = (sv && ev) ? (int32_t)floor((double)g->g_len[sg] + 0.5) : -1;
+        sv = first.off0 == 0.0f && (first.at.flags & OTM_EDGE_SEG_BEGIN_D);
+        ev = last.off1 == last.at.len && (last.at.flags & OTM_EDGE_SEG_END_D);
+        s.segment_id = (int64_t)first.at.gid;
+        s.length = (sv && ev) ? (int32_t)floor((double)first.at.glen + 0.5) : -1;
       } else {
         sv = first.off0 == 0.0f;
-        ev = last.off1 == g->e_len[last.edge];
+        ev = last.off1 == last.at.len;
         s.segment_id = -1;
         s.length = -1;
-        if (g->e_flags[first.edge] & OTM_EDGE_INTERNAL_D) s.flags |= OTM_SEG_INTERNAL;
+        if (first.at.flags & OTM_EDGE_INTERNAL_D) s.flags |= OTM_SEG_INTERNAL;
       }
       s.start_time = 0.0;
       s.end_time = 0.0;
@@ -1761,10 +1832,9 @@ struct SegEmitter {
   __device__ void push(const Trav& t) {
     bool join = false;
     if (has) {
-      const int32_t e = t.edge, pe = last.edge;
-      const int32_t s = g->e_seg[e], ps = g->e_seg[pe];
-      if (s >= 0) join = ps == s && g->e_seg_pos[e] == g->e_seg_pos[pe] + 1;
-      else join = ps < 0 && ((g->e_flags[e] ^ g->e_flags[pe]) & OTM_EDGE_INTERNAL_D) == 0;
+      const int32_t s = t.at.seg, ps = last.at.seg;
+      if (s >= 0) join = ps == s && t.at.seg_pos == last.at.seg_pos + 1;
+      else join = ps < 0 && ((t.at.flags ^ last.at.flags) & OTM_EDGE_INTERNAL_D) == 0;
     }
     if (!join) {
       flush();
@@ -1773,9 +1843,9 @@ struct SegEmitter {
       way_start = nway;
     }
     last = t;
-    add_way(t.edge);
+    add_way(t.at);
   }
-  static constexpr uint8_t OTM_EDGE_INTERNAL_D = 0x01, OTM_EDGE_SEG_BEGIN_D = 0x02, OTM_EDGE_SEG_END_D = 0x04;
+  static constexpr uint32_t OTM_EDGE_INTERNAL_D = 0x01, OTM_EDGE_SEG_BEGIN_D = 0x02, OTM_EDGE_SEG_END_D = 0x04;
 };
 
 __device__ __forceinline__ double time_at(double ta, double tb, float x, float R) {
@@ -1783,94 +1853,200 @@ __device__ __forceinline__ double time_at(double ta, double tb, float x, float R
   return ta;
 }
 
-template <bool WRITE>
-__global__ __launch_bounds__(256) void k_segments(DevGraph g, DevBatch b, DevWork w, DevOut o) {
-  const int32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= b.n_traces) return;
+// Point data of one trace as the emitter reads it: straight from HBM ...
+struct SegSrcGlobal {
+  const DevGraph* g;
+  const DevBatch* b;
+  const DevWork* w;
+  int64_t a;
+  __device__ int state(int pl) const {
+    const int64_t p = a + pl;
+    return w->is_col[p] ? w->state[p] : -1;
+  }
+  __device__ bool cs(int pl) const { return w->chain_start[a + pl] != 0; }
+  __device__ double time(int pl) const { return b->time[a + pl]; }
+  __device__ float rd(int pl) const { return w->route_dist[a + pl]; }
+  __device__ int32_t poff(int pl) const { return w->path_off[a + pl]; }
+  __device__ int32_t plen(int pl) const { return w->path_len[a + pl]; }
+  __device__ int32_t edge(int pl) const { return w->cand_edge[(a + pl) * KMAX + w->state[a + pl]]; }
+  __device__ float off(int pl) const { return w->cand_off[(a + pl) * KMAX + w->state[a + pl]]; }
+  __device__ EAttr attr(int pl) const { return edge_attr(*g, edge(pl)); }
+};
+
+// ... or staged in LDS by the whole wavefront (traces up to SEG_PTS points)
+constexpr int SEG_PTS = 256;
+struct SegLds {
+  double time[SEG_PTS];
+  int64_t way[SEG_PTS];
+  uint64_t gid[SEG_PTS];
+  float rd[SEG_PTS], off[SEG_PTS], len[SEG_PTS], glen[SEG_PTS];
+  int32_t poff[SEG_PTS], plen[SEG_PTS], edge[SEG_PTS], seg[SEG_PTS], seg_pos[SEG_PTS];
+  int8_t state[SEG_PTS];
+  uint8_t cs[SEG_PTS], flags[SEG_PTS];
+};
+struct SegSrcLds {
+  const SegLds* L;
+  __device__ int state(int pl) const { return L->state[pl]; }
+  __device__ bool cs(int pl) const { return L->cs[pl] != 0; }
+  __device__ double time(int pl) const { return L->time[pl]; }
+  __device__ float rd(int pl) const { return L->rd[pl]; }
+  __device__ int32_t poff(int pl) const { return L->poff[pl]; }
+  __device__ int32_t plen(int pl) const { return L->plen[pl]; }
+  __device__ int32_t edge(int pl) const { return L->edge[pl]; }
+  __device__ float off(int pl) const { return L->off[pl]; }
+  __device__ EAttr attr(int pl) const {
+    EAttr x;
+    x.len = L->len[pl];
+    x.seg = L->seg[pl];
+    x.seg_pos = L->seg_pos[pl];
+    x.flags = L->flags[pl];
+    x.way = L->way[pl];
+    x.gid = L->gid[pl];
+    x.glen = L->glen[pl];
+    return x;
+  }
+};
+
+// The traversal walk of one trace (one thread): states in order, chains,
+// per step the close of the open traversal, the route's path edges and the
+// re-open on the new edge; traversals grouped into OSMLR segments.
+template <bool WRITE, class Src>
+__device__ void segments_trace(const DevGraph& g, const DevWork& w, DevOut& o, int32_t t, int n, const Src& S) {
   SegEmitter<WRITE> em;
-  em.g = &g;
   em.o = &o;
   em.seg_base = WRITE ? o.seg_cnt[t] : 0;
   em.way_base = WRITE ? o.way_cnt[t] : 0;
-  const int err = w.trace_err[t];
-  if (err == 0) {
-    const int64_t a = b.trace_off[t], e = b.trace_off[t + 1];
-    bool open = false;
-    int nstate = 0;
-    Trav cur{};
-    int64_t lastp = -1;
-    for (int64_t p = a; p <= e; ++p) {
-      const bool is_state = p < e && w.is_col[p] && w.state[p] >= 0;
-      if (p < e && !is_state) continue;
-      const bool new_chain = p == e || w.chain_start[p];
-      if (open && new_chain) {
-        const int sl = w.state[lastp];
-        cur.off1 = w.cand_off[lastp * KMAX + sl];
-        cur.t1 = b.time[lastp];
-        cur.sh1 = (int32_t)(lastp - a);
-        if (nstate >= 2) {
-          em.push(cur);
-          em.flush();
-        }
-        open = false;
-      }
-      if (p == e) break;
-      const int j = w.state[p];
-      const int32_t ej = w.cand_edge[p * KMAX + j];
-      const float oj = w.cand_off[p * KMAX + j];
-      if (new_chain) {
-        cur.edge = ej;
-        cur.off0 = oj;
-        cur.t0 = b.time[p];
-        cur.sh0 = (int32_t)(p - a);
-        open = true;
-        nstate = 1;
-        lastp = p;
-        continue;
-      }
-      const float Rd = w.route_dist[p];
-      const double ta = b.time[lastp], tb = b.time[p];
-      const int32_t ca = (int32_t)(lastp - a), cb = (int32_t)(p - a);
-      const int32_t ei = cur.edge;
-      const float oi = w.cand_off[lastp * KMAX + w.state[lastp]];
-      const bool same = ei == ej && oj >= oi;
-      if (!same) {
-        const float start = g.e_len[ei] - oi;
-        float x = start;
-        cur.off1 = g.e_len[ei];
-        cur.t1 = time_at(ta, tb, x, Rd);
-        cur.sh1 = x >= Rd ? cb : ca;
+  bool open = false;
+  int nstate = 0;
+  Trav cur{};
+  int lastp = -1;
+  for (int p = 0; p <= n; ++p) {
+    const int st = p < n ? S.state(p) : -1;
+    if (p < n && st < 0) continue;
+    const bool new_chain = p == n || S.cs(p);
+    if (open && new_chain) {
+      cur.off1 = S.off(lastp);
+      cur.t1 = S.time(lastp);
+      cur.sh1 = lastp;
+      if (nstate >= 2) {
         em.push(cur);
-        float dd = 0.0f;
-        const int32_t po = w.path_off[p], pl = w.path_len[p];
-        for (int k = 0; k < pl; ++k) {
-          const int32_t pe = w.path_pool[po + k];
-          Trav m;
-          m.edge = pe;
-          m.off0 = 0.0f;
-          m.off1 = g.e_len[pe];
-          const float xb = start + dd;
-          dd = dd + g.e_len[pe];
-          const float xe = start + dd;
-          m.t0 = time_at(ta, tb, xb, Rd);
-          m.t1 = time_at(ta, tb, xe, Rd);
-          m.sh0 = xb >= Rd ? cb : ca;
-          m.sh1 = xe >= Rd ? cb : ca;
-          em.push(m);
-        }
-        x = start + dd;
-        cur.edge = ej;
-        cur.off0 = 0.0f;
-        cur.t0 = time_at(ta, tb, x, Rd);
-        cur.sh0 = x >= Rd ? cb : ca;
+        em.flush();
       }
-      ++nstate;
-      lastp = p;
+      open = false;
     }
+    if (p == n) break;
+    const int32_t ej = S.edge(p);
+    const float oj = S.off(p);
+    if (new_chain) {
+      cur.edge = ej;
+      cur.at = S.attr(p);
+      cur.off0 = oj;
+      cur.t0 = S.time(p);
+      cur.sh0 = p;
+      open = true;
+      nstate = 1;
+      lastp = p;
+      continue;
+    }
+    const float Rd = S.rd(p);
+    const double ta = S.time(lastp), tb = S.time(p);
+    const int32_t ca = lastp, cb = p;
+    const int32_t ei = cur.edge;
+    const float oi = S.off(lastp);
+    const bool same = ei == ej && oj >= oi;
+    if (!same) {
+      const float elen = cur.at.len;  // == e_len[ei]
+      const float start = elen - oi;
+      float x = start;
+      cur.off1 = elen;
+      cur.t1 = time_at(ta, tb, x, Rd);
+      cur.sh1 = x >= Rd ? cb : ca;
+      em.push(cur);
+      float dd = 0.0f;
+      const int32_t po = S.poff(p), pl = S.plen(p);
+      for (int k = 0; k < pl; ++k) {
+        const int32_t pe = w.path_pool[po + k];
+        Trav m;
+        m.edge = pe;
+        m.at = edge_attr(g, pe);
+        m.off0 = 0.0f;
+        m.off1 = m.at.len;
+        const float xb = start + dd;
+        dd = dd + m.at.len;
+        const float xe = start + dd;
+        m.t0 = time_at(ta, tb, xb, Rd);
+        m.t1 = time_at(ta, tb, xe, Rd);
+        m.sh0 = xb >= Rd ? cb : ca;
+        m.sh1 = xe >= Rd ? cb : ca;
+        em.push(m);
+      }
+      x = start + dd;
+      cur.edge = ej;
+      cur.at = S.attr(p);
+      cur.off0 = 0.0f;
+      cur.t0 = time_at(ta, tb, x, Rd);
+      cur.sh0 = x >= Rd ? cb : ca;
+    }
+    ++nstate;
+    lastp = p;
   }
   if (!WRITE) {
     o.seg_cnt[t] = em.nseg;
     o.way_cnt[t] = em.nway;
+  }
+}
+
+// One wavefront per trace: lanes stage the trace's points (state, chain
+// flags, times, route results, state edges and their attributes) into LDS
+// with a few rounds of parallel loads; lane 0 then runs the walk out of LDS.
+template <bool WRITE>
+__global__ __launch_bounds__(TB) void k_segments(DevGraph g, DevBatch b, DevWork w, DevOut o) {
+  __shared__ SegLds L;
+  const int lane = threadIdx.x;
+  for (int32_t t = blockIdx.x; t < b.n_traces; t += gridDim.x) {
+    const int64_t a = b.trace_off[t];
+    const int n = (int)(b.trace_off[t + 1] - a);
+    if (w.trace_err[t] != 0) {
+      if (!WRITE && lane == 0) {
+        o.seg_cnt[t] = 0;
+        o.way_cnt[t] = 0;
+      }
+      continue;
+    }
+    if (n > SEG_PTS) {
+      if (lane == 0) segments_trace<WRITE>(g, w, o, t, n, SegSrcGlobal{&g, &b, &w, a});
+      continue;
+    }
+    for (int pl = lane; pl < n; pl += TB) {
+      const int64_t p = a + pl;
+      // round 1: by point
+      const uint8_t ic = w.is_col[p];
+      const int32_t s0 = w.state[p];
+      const int st = ic ? s0 : -1;
+      L.state[pl] = (int8_t)st;
+      L.cs[pl] = w.chain_start[p];
+      L.time[pl] = b.time[p];
+      L.rd[pl] = w.route_dist[p];
+      L.poff[pl] = w.path_off[p];
+      L.plen[pl] = w.path_len[p];
+      if (st >= 0) {
+        // round 2: the state's candidate; rounds 3-4: its edge, its segment
+        const int32_t e = w.cand_edge[p * KMAX + st];
+        L.off[pl] = w.cand_off[p * KMAX + st];
+        L.edge[pl] = e;
+        const EAttr x = edge_attr(g, e);
+        L.len[pl] = x.len;
+        L.seg[pl] = x.seg;
+        L.seg_pos[pl] = x.seg_pos;
+        L.flags[pl] = (uint8_t)x.flags;
+        L.way[pl] = x.way;
+        L.gid[pl] = x.gid;
+        L.glen[pl] = x.glen;
+      }
+    }
+    __syncthreads();
+    if (lane == 0) segments_trace<WRITE>(g, w, o, t, n, SegSrcLds{&L});
+    __syncthreads();
   }
 }
 
@@ -1995,7 +2171,7 @@ int grid_for(int64_t n, int per_block, int cap) {
 constexpr int WAVE_GRID_CAP = 256 * 64;  // grid-stride cap for wave kernels
 
 void launch_columns(const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s) {
-  hipLaunchKernelGGL(k_columns, dim3(grid_for(b.n_traces, 256, 1 << 30)), dim3(256), 0, s, b, p, w);
+  hipLaunchKernelGGL(k_columns, dim3(grid_for(b.n_traces, 1, WAVE_GRID_CAP)), dim3(TB), 0, s, b, p, w);
 }
 void launch_candidates(const DevGraph& g, const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s) {
   hipLaunchKernelGGL(k_cand_lane, dim3(grid_for(b.n_points, CAND_TB, 1 << 30)), dim3(CAND_TB), 0, s, g, b, p, w);
@@ -2030,9 +2206,9 @@ void launch_route(const DevGraph& g, const DevBatch& b, const DevParams& p, DevW
 }
 void launch_segments(const DevGraph& g, const DevBatch& b, DevWork& w, DevOut& o, bool write, hipStream_t s) {
   if (write)
-    hipLaunchKernelGGL(k_segments<true>, dim3(grid_for(b.n_traces, 64, 1 << 30)), dim3(64), 0, s, g, b, w, o);
+    hipLaunchKernelGGL(k_segments<true>, dim3(grid_for(b.n_traces, 1, WAVE_GRID_CAP)), dim3(TB), 0, s, g, b, w, o);
   else
-    hipLaunchKernelGGL(k_segments<false>, dim3(grid_for(b.n_traces, 64, 1 << 30)), dim3(64), 0, s, g, b, w, o);
+    hipLaunchKernelGGL(k_segments<false>, dim3(grid_for(b.n_traces, 1, WAVE_GRID_CAP)), dim3(TB), 0, s, g, b, w, o);
 }
 void launch_report(const DevBatch& b, const DevReportCfg& rc, DevWork& w, DevOut& o, hipStream_t s) {
   hipLaunchKernelGGL(k_report, dim3(grid_for(b.n_traces, 64, 1 << 30)), dim3(64), 0, s, b, rc, w, o, 0);

@@ -10,6 +10,11 @@ rank matches its own uuid shard (Kafka murmur2 partitioner) and the step ends
 with the one collective of the design: an RCCL reduce-scatter of the
 per-segment histograms (weak scaling).
 
+Roofline: algorithmic bytes per stage come from the CPU
+oracle's work counters on the same batch (independent of
+the GPU implementation); kernel times from HIP events around each launch on
+the launch stream.  The line's `roofline` object is the dominant kernel's.
+
 Prints ONE JSON line (rank 0).  Run:
   python bench.py                      # N=1, defaults
   python -m torch.distributed.run --nproc-per-node N bench.py --gpus N
@@ -27,6 +32,17 @@ sys.path.insert(0, ROOT)
 
 METRIC = "GPS points matched/sec (whole node) at 1/2/4/8 MI355X; % segment-ID agreement vs meili"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+DEFAULT_TRAFFIC = os.path.join(ROOT, "profiles", "pmc_traffic_latest.json")
+
+# kernel -> (stage, main tier of the stage?)
+KERNEL_STAGE = {
+    "k_columns": "columns", "k_cand_lane": "candidates", "k_candidates": "candidates", "k_links": "links_scan",
+    "scan_trans_off": "links_scan", "k_trans_index": "transitions", "k_trans_lane": "transitions",
+    "k_transitions": "transitions", "k_transitions_big": "transitions", "k_viterbi": "viterbi",
+    "k_route_index": "route", "k_route_lane": "route", "k_route": "route", "k_route_big": "route",
+    "k_segments_count": "segments", "scan_seg_counts": "segments", "k_segments_write": "segments",
+    "k_report": "report",
+}
 
 
 def parse():
@@ -38,8 +54,8 @@ def parse():
     ap.add_argument("--points", type=int, default=100, help="per vehicle")
     ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (0: min(16, cores))")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-check", action="store_true", help="skip the untimed oracle agreement check")
-    ap.add_argument("--traffic-json", default=None, help="rocprofv3 PMC traffic summary (profiles/)")
+    ap.add_argument("--no-check", action="store_true", help="skip the untimed oracle pass (agreement, bytes)")
+    ap.add_argument("--traffic-json", default=DEFAULT_TRAFFIC, help="PMC traffic summary (scripts/pmc_summary.py)")
     return ap.parse_args()
 
 
@@ -48,24 +64,38 @@ def log(rank, *a):
         print(*a, file=sys.stderr, flush=True)
 
 
-def algorithmic_bytes_transitions(eng, batch_pts):
-    """Algorithmic bytes of one K4 (transitions) launch, from the work
-    counters of an untimed counting pass over the same batch:
-      per column pair : 8 B x (Kq + Kp) candidate (edge, offset) reads
-                        + 4 B x Kq x Kp transition-cost writes
-      per search      : 8 B per settled node (CSR offset pair)
-                        + 8 B per relaxed edge (head node + length)
-    DESIGN.md §5 derives the figure."""
-    c = eng.counters()
-    ncand = eng.debug("ncand")[:batch_pts].astype(np.int64)
-    colp = eng.debug("col_prev")[:batch_pts]
-    linked = np.nonzero(colp >= 0)[0]
-    kq = ncand[colp[linked]]
-    kp = ncand[linked]
+def stage_bytes(c, ncand, col_prev, n_points):
+    """Algorithmic bytes per stage of one launch, from the
+    oracle's work counters `c` and its candidate counts / chain links:
+      columns      8 B/point read (lat, lon) + 13 B/point written
+      candidates   12 B/column probe + 8 B/cell visited (CSR offsets)
+                   + 20 B/cell entry scanned (entry id + shape segment)
+                   + 12 B/candidate written (edge, offset, emission)
+      transitions  8 B x (Kq + Kp) candidates + 4 B x Kq x Kp costs
+                   + 8 B/settled node + 12 B/relaxed edge
+      viterbi      4 B x Kq x Kp costs + 5 B/candidate (emission, backptr)
+      route        8 B/settled node + 12 B/relaxed edge + 4 B/path edge
+      segments     16 B/segment"""
+    linked = np.nonzero(col_prev >= 0)[0]
+    kq = ncand[col_prev[linked]].astype(np.int64)
+    kp = ncand[linked].astype(np.int64)
+    pairs = int((kq * kp).sum())
     return {
-        "bytes": int(8 * (kq + kp).sum() + 4 * (kq * kp).sum() + 8 * c["nodes_settled"] + 8 * c["edges_relaxed"]),
-        "counters": c,
+        "columns": 21 * n_points,
+        "candidates": 12 * c["columns"] + 8 * c["cells_visited"] + 20 * c["cell_entries_scanned"]
+        + 12 * c["candidates"],
+        "transitions": int(8 * (kq + kp).sum()) + 4 * pairs + 8 * c["nodes_settled"] + 12 * c["edges_relaxed"],
+        "viterbi": 4 * pairs + 5 * c["candidates"],
+        "route": 8 * c["route_nodes_settled"] + 12 * c["route_edges_relaxed"] + 4 * c["route_edges"],
+        "segments": 16 * c["segments_out"],
     }
+
+
+def load_traffic(path):
+    if not path or not os.path.exists(path):
+        return None
+    with open(path) as f:
+        return json.load(f)
 
 
 def main():
@@ -124,17 +154,17 @@ def main():
         step()
     torch.cuda.synchronize(dev)
 
-    # timed region: K steps between barriers, kernel spans from HIP events
+    # timed region: K steps between barriers; kernel spans from HIP events
     eng.set_timing(True)
-    stage_tot = {k: 0.0 for k in Engine.STAGES}
+    kern_tot = {}
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t_start = time.perf_counter()
     for _ in range(args.steps):
         step()
-        for k, v in eng.stage_ms().items():
-            stage_tot[k] += v
+        for k, v in eng.kernel_ms().items():
+            kern_tot[k] = kern_tot.get(k, 0.0) + v
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -144,44 +174,62 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    stage_avg = {k: v / args.steps for k, v in stage_tot.items()}
+    kern_avg = {k: v / args.steps for k, v in kern_tot.items()}
     total_points = P * world * args.steps
     value = total_points / elapsed
     ms_per_step = elapsed * 1e3 / args.steps
+    spill = eng.spill_stats()
 
-    # ---- untimed: algorithmic bytes of the dominant kernel (counting pass)
-    eng.set_counting(True)
-    eng.match_device(d_off, d_lat, d_lon, d_time, d_acc, stream=stream.cuda_stream)
-    torch.cuda.synchronize(dev)
-    eng.set_counting(False)
-    dom = max(stage_avg, key=lambda k: stage_avg[k])
-    ab = algorithmic_bytes_transitions(eng, P)
-    k4_ms = stage_avg["transitions"]
-    achieved_gbs = ab["bytes"] / (k4_ms * 1e-3) / 1e9 if k4_ms > 0 else 0.0
-    traffic = None
-    if args.traffic_json and os.path.exists(args.traffic_json):
-        with open(args.traffic_json) as f:
-            traffic = json.load(f).get("k_transitions_bytes_per_launch")
-
-    # ---- untimed: agreement with the CPU oracle on a sample, and vs truth
-    agreement = None
+    # ---- untimed: the CPU oracle over this rank's whole batch -> agreement
+    # with the GPU result and the algorithmic bytes of every stage
     res = eng.fetch()
+    agreement, sbytes, stages = None, None, None
     if rank == 0 and not args.no_check:
-        try:
-            from oracle import pyoracle
-            nsample = min(500, len(ids))
-            sb = synth.slice_batch(batch, 0, nsample)
-            orc = pyoracle.match_batch(pyoracle.Graph(graph), sb, nthreads=8)
-            seq_eq = 0
-            for t in range(nsample):
-                a, n = res.traces["seg_off"][t], res.traces["seg_cnt"][t]
-                oa, on = orc["traces"]["seg_off"][t], orc["traces"]["seg_cnt"][t]
-                seq_eq += int(np.array_equal(res.segments["segment_id"][a:a + n],
-                                             orc["segments"]["segment_id"][oa:oa + on]))
-            agreement = {"segment_id_sequences_equal_vs_oracle": seq_eq / float(nsample),
-                         "sample_traces": nsample, "meili": "unavailable (parity vs meili unpinned)"}
-        except Exception as e:  # the check is informational; the bench line still prints
-            agreement = {"error": str(e)}
+        from oracle import pyoracle
+        torc = time.perf_counter()
+        orc = pyoracle.match_batch(pyoracle.Graph(graph), batch, nthreads=min(16, os.cpu_count() or 1),
+                                   keep_stages=True)
+        log(rank, "[bench] oracle pass over %d points: %.1fs" % (P, time.perf_counter() - torc))
+        nt = len(res.traces)
+        seq_eq = 0
+        for t in range(nt):
+            a, n = res.traces["seg_off"][t], res.traces["seg_cnt"][t]
+            oa, on = orc["traces"]["seg_off"][t], orc["traces"]["seg_cnt"][t]
+            seq_eq += int(np.array_equal(res.segments["segment_id"][a:a + n],
+                                         orc["segments"]["segment_id"][oa:oa + on]))
+        same = all(getattr(res, k).tobytes() == orc[k].tobytes() for k in ("traces", "segments", "reports",
+                                                                            "way_ids"))
+        agreement = {"segment_id_sequences_equal_vs_oracle": seq_eq / float(max(nt, 1)), "traces": nt,
+                     "all_outputs_bit_identical": bool(same),
+                     "meili": "unavailable (parity vs meili unpinned)"}
+        sbytes = stage_bytes(orc["counters"], orc["ncand"], orc["col_prev"], P)
+        stage_ms = {}
+        for k, v in kern_avg.items():
+            st = KERNEL_STAGE[k]
+            stage_ms[st] = stage_ms.get(st, 0.0) + v
+        stages = {}
+        for st, ms in stage_ms.items():
+            b = sbytes.get(st)
+            stages[st] = {"ms": ms, "algorithmic_bytes": b,
+                          "GB_per_s": (b / (ms * 1e-3) / 1e9) if (b is not None and ms > 0) else None}
+
+    # ---- roofline of the dominant kernel
+    dom = max(kern_avg, key=lambda k: kern_avg[k])
+    roof = None
+    if sbytes is not None:
+        st = KERNEL_STAGE[dom]
+        b = sbytes.get(st)
+        # the stage's units all go through its main tier save for the spilled
+        # few (spill stats); attribute the stage's bytes to the main kernel
+        achieved = b / (kern_avg[dom] * 1e-3) / 1e9 if b else None
+        traffic = None
+        tj = load_traffic(args.traffic_json)
+        if tj and dom in tj.get("kernels", {}):
+            traffic = tj["kernels"][dom].get("hbm_bytes_per_launch")
+        roof = {"bound": "hbm", "kernel": dom, "stage": st, "achieved": achieved, "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
+                "algorithmic_bytes_per_launch": b, "launch_ms": kern_avg[dom],
+                "traffic_source": os.path.relpath(args.traffic_json, ROOT) if traffic is not None else None}
 
     # ---- CPU baseline: the oracle on this GPU's batch, host threads
     cpu = None
@@ -230,12 +278,10 @@ def main():
                        "points_per_gpu": P, "vehicles_per_gpu": len(ids), "graph": ginfo,
                        "parallelism": "uuid shards x%d, RCCL reduce-scatter of %dx%d histograms" %
                                       (world, nseg, nbins)},
-            "roofline": {"bound": "hbm", "kernel": "k_transitions", "achieved": achieved_gbs,
-                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved_gbs / HBM_PEAK_GBS,
-                         "traffic": traffic, "algorithmic_bytes_per_launch": ab["bytes"],
-                         "launch_ms": k4_ms},
-            "stage_ms": stage_avg,
-            "dominant_stage": dom,
+            "roofline": roof,
+            "kernel_ms": kern_avg,
+            "stages": stages,
+            "spill": spill,
             "cpu_baseline": cpu,
             "agreement": agreement,
             "hip_runtime": _lib.runtime_info(),

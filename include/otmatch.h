@@ -249,6 +249,27 @@ int otm_get_counters(otm_engine* eng, otm_work_counters* out);
 int otm_set_timing(otm_engine* eng, int on);
 int otm_get_stage_ms(otm_engine* eng, float* ms, int n);
 
+/* Per-kernel timings (ms) of the last otm_match_device call (same HIP events,
+ * one pair around each launch; enabled with otm_set_timing).  Kernel k is
+ * named by otm_kernel_name(k), 0 <= k < OTM_NUM_KERNELS; the stage timings
+ * above are sums of these. */
+#define OTM_NUM_KERNELS 18
+int otm_get_kernel_ms(otm_engine* eng, float* ms, int n);
+const char* otm_kernel_name(int k);
+
+/* How much work of the last batch each fallback tier took:
+ * probes the lane candidate tier handed to the wave tier; transition columns
+ * the distance index could not answer, then those the lane search spilled to
+ * the LDS wave search, then to the global-memory search; the same for the
+ * route stage's steps. */
+typedef struct otm_spill_stats {
+  int32_t cand_wave;
+  int32_t trans_online, trans_wave, trans_global;
+  int32_t route_online, route_wave, route_global;
+  int32_t pad;
+} otm_spill_stats;
+int otm_get_spill_stats(otm_engine* eng, otm_spill_stats* out);
+
 /* Stage outputs of the last batch, for parity tests (device -> host copy).
  * what: 0 ncand i32[P], 1 cand_edge i32[P*KMAX], 2 cand_off f32[P*KMAX],
  * 3 cand_emis f32[P*KMAX], 4 trans_off i64[P+1], 5 trans f32[total],

@@ -41,6 +41,11 @@ class WorkCounters(C.Structure):
     _fields_ = [(n, C.c_int64) for n in COUNTER_NAMES]
 
 
+class SpillStats(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in ("cand_wave", "trans_online", "trans_wave", "trans_global", "route_online",
+                                         "route_wave", "route_global", "pad")]
+
+
 class SynthGraphParams(C.Structure):
     _fields_ = [("center_lat", C.c_double), ("center_lon", C.c_double), ("width_m", C.c_double),
                 ("height_m", C.c_double), ("block_m", C.c_double), ("jitter_m", C.c_double),
@@ -98,6 +103,9 @@ def _declare(L):
         "otm_get_counters": (C.c_int, [vp, C.POINTER(WorkCounters)]),
         "otm_set_timing": (C.c_int, [vp, C.c_int]),
         "otm_get_stage_ms": (C.c_int, [vp, C.POINTER(C.c_float), C.c_int]),
+        "otm_get_kernel_ms": (C.c_int, [vp, C.POINTER(C.c_float), C.c_int]),
+        "otm_kernel_name": (C.c_char_p, [C.c_int]),
+        "otm_get_spill_stats": (C.c_int, [vp, C.POINTER(SpillStats)]),
         "otm_debug_fetch": (C.c_int, [vp, C.c_int, vp, sz, psz]),
         "otm_kmax": (C.c_int, []),
         "otm_synth_graph_defaults": (None, [C.POINTER(SynthGraphParams)]),

@@ -504,6 +504,21 @@ int otm_get_stage_ms(otm_engine* E, float* ms, int n) {
   return OTM_OK;
 }
 
+int otm_get_kernel_ms(otm_engine* E, float* ms, int n) {
+  if (!E || !ms) return fail(OTM_EINVAL, "bad arguments");
+  for (int k = 0; k < n && k < otm::KN_COUNT; ++k) ms[k] = E->kernel_ms[k];
+  return OTM_OK;
+}
+
+static_assert(OTM_NUM_KERNELS == otm::KN_COUNT, "kernel table");
+const char* otm_kernel_name(int k) { return k >= 0 && k < otm::KN_COUNT ? otm::kKernelNames[k] : nullptr; }
+
+int otm_get_spill_stats(otm_engine* E, otm_spill_stats* out) {
+  if (!E || !out) return fail(OTM_EINVAL, "bad arguments");
+  std::lock_guard<std::mutex> lk(E->mu);
+  return otm::engine_spill_stats(E, out) ? fail(OTM_EDEVICE, "spill stats copy failed") : OTM_OK;
+}
+
 int otm_debug_fetch(otm_engine* E, int what, void* dst, size_t bytes, size_t* needed) {
   if (!E) return fail(OTM_EINVAL, "engine is NULL");
   std::lock_guard<std::mutex> lk(E->mu);

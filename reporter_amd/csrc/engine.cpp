@@ -111,7 +111,7 @@ int engine_init(otm_engine* E, const char* graph_path, int device, std::string* 
   HIPCHK(hipMalloc((void**)&E->ctr, sizeof(DevCounters)));
   HIPCHK(hipMalloc((void**)&E->ctr_save, sizeof(DevCounters)));
   HIPCHK(hipMemset(E->ctr, 0, sizeof(DevCounters)));
-  for (auto& e : E->ev) HIPCHK(hipEventCreate(&e));
+  for (auto& e : E->kev) HIPCHK(hipEventCreate(&e));
   return build_index(E, err);
 }
 
@@ -188,7 +188,7 @@ void engine_free(otm_engine* E) {
       &E->is_col,        &E->prevc,        &E->gc,             &E->ncand,          &E->cand_edge,  &E->cand_off,
       &E->cand_emis,     &E->col_prev,     &E->trans_off,      &E->trans,          &E->bp,         &E->state,
       &E->chain_start,   &E->route_dist,   &E->path_off,       &E->path_len,       &E->path_pool,  &E->trace_err,
-      &E->overflow_list0, &E->overflow_list, &E->overflow_list2, &E->counters_i32, &E->scan_tmp,   &E->big_key,
+      &E->overflow_list0, &E->overflow_list, &E->overflow_list2, &E->counters_i32, &E->scan_tmp, &E->snap,   &E->big_key,
       &E->big_lab,       &E->big_inq,      &E->big_fr,         &E->o_traces,       &E->o_seg_cnt,  &E->o_way_cnt,
       &E->o_segments,    &E->o_seg_gidx,   &E->o_way_ids,      &E->o_reports};
   for (auto* b : bufs) {
@@ -199,7 +199,7 @@ void engine_free(otm_engine* E) {
   if (E->ctr) (void)hipFree(E->ctr);
   if (E->ctr_save) (void)hipFree(E->ctr_save);
   E->ctr = E->ctr_save = nullptr;
-  for (auto& e : E->ev)
+  for (auto& e : E->kev)
     if (e) (void)hipEventDestroy(e);
   if (E->stream) (void)hipStreamDestroy(E->stream);
   E->stream = nullptr;
@@ -244,6 +244,7 @@ int engine_match(otm_engine* E, const DevBatch& b, hipStream_t s, std::string* e
   ENS(overflow_list, Pn * 4);
   ENS(overflow_list2, Pn * 4);
   ENS(counters_i32, 64);
+  ENS(snap, 192);
   ENS(o_traces, ((size_t)NT + 1) * sizeof(otm_trace_result));
   ENS(o_seg_cnt, ((size_t)NT + 1) * 4);
   ENS(o_way_cnt, ((size_t)NT + 1) * 4);
@@ -281,18 +282,16 @@ int engine_match(otm_engine* E, const DevBatch& b, hipStream_t s, std::string* e
   w.ctr = E->counting ? E->ctr : nullptr;
   if (E->counting) HIPCHK(hipMemsetAsync(E->ctr, 0, sizeof(DevCounters), s));
   HIPCHK(hipMemsetAsync(w.counters_i32, 0, 64, s));  // [5] = candidate spill count
-#define EV(k) \
-  if (E->timing) HIPCHK(hipEventRecord(E->ev[k], s));
-  EV(0);
-  launch_columns(b, E->dp, w, s);
-  EV(1);
-  EV(2);
-  launch_candidates(E->g, b, E->dp, w, s);
-  EV(3);
-  EV(4);
-  launch_links(b, E->dp, w, s);
+  Marks mk;
+  mk.ev = E->timing ? E->kev : nullptr;
+  launch_columns(b, E->dp, w, s, mk);
+  launch_candidates(E->g, b, E->dp, w, s, mk);
+  // spill snapshot A: candidate probes the lane tier handed to the wave tier
+  HIPCHK(hipMemcpyAsync(E->snap.p, w.counters_i32, 64, hipMemcpyDeviceToDevice, s));
+  launch_links(b, E->dp, w, s, mk);
+  mk.begin(KN_SCAN_TRANS, s);
   scan_i64(w.trans_off, NP, E->scan_tmp.p, E->scan_tmp.cap, s);
-  EV(5);
+  mk.end(KN_SCAN_TRANS, s);
   int64_t ttotal = 0;
   HIPCHK(hipMemcpyAsync(&ttotal, w.trans_off + NP, 8, hipMemcpyDeviceToHost, s));
   HIPCHK(hipMemsetAsync(w.counters_i32, 0, 64, s));
@@ -305,12 +304,10 @@ int engine_match(otm_engine* E, const DevBatch& b, hipStream_t s, std::string* e
   w.big_lab = P<unsigned long long>(E->big_lab);
   w.big_inq = P<uint32_t>(E->big_inq);
   w.big_fr = P<uint32_t>(E->big_fr);
-  EV(6);
-  launch_transitions(E->g, b, E->dp, w, s);
-  EV(7);
-  EV(8);
-  launch_viterbi(b, w, s);
-  EV(9);
+  launch_transitions(E->g, b, E->dp, w, s, mk);
+  // spill snapshot B: columns per transition tier
+  HIPCHK(hipMemcpyAsync(P<char>(E->snap) + 64, w.counters_i32, 64, hipMemcpyDeviceToDevice, s));
+  launch_viterbi(b, w, s, mk);
   // a path-pool overflow redoes the whole stage: restore the work counters
   // so the redone searches are counted once
   if (E->counting) HIPCHK(hipMemcpyAsync(E->ctr_save, E->ctr, sizeof(DevCounters), hipMemcpyDeviceToDevice, s));
@@ -318,9 +315,9 @@ int engine_match(otm_engine* E, const DevBatch& b, hipStream_t s, std::string* e
     if (E->counting && attempt > 0)
       HIPCHK(hipMemcpyAsync(E->ctr, E->ctr_save, sizeof(DevCounters), hipMemcpyDeviceToDevice, s));
     HIPCHK(hipMemsetAsync(w.counters_i32, 0, 64, s));
-    EV(10);
-    launch_route(E->g, b, E->dp, w, s);
-    EV(11);
+    launch_route(E->g, b, E->dp, w, s, mk);
+    // spill snapshot C: steps per route tier (final attempt)
+    HIPCHK(hipMemcpyAsync(P<char>(E->snap) + 128, w.counters_i32, 64, hipMemcpyDeviceToDevice, s));
     int32_t cnt[3] = {0, 0, 0};
     HIPCHK(hipMemcpyAsync(cnt, w.counters_i32, 12, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
@@ -345,11 +342,11 @@ int engine_match(otm_engine* E, const DevBatch& b, hipStream_t s, std::string* e
   o.bin_kph = E->bin_kph;
   HIPCHK(hipMemsetAsync(o.seg_cnt + NT, 0, 4, s));
   HIPCHK(hipMemsetAsync(o.way_cnt + NT, 0, 4, s));
-  EV(12);
-  launch_segments(E->g, b, w, o, false, s);
-  EV(13);
+  launch_segments(E->g, b, w, o, false, s, mk);
+  mk.begin(KN_SEG_SCAN, s);
   scan_i32(o.seg_cnt, NT, E->scan_tmp.p, E->scan_tmp.cap, s);
   scan_i32(o.way_cnt, NT, E->scan_tmp.p, E->scan_tmp.cap, s);
+  mk.end(KN_SEG_SCAN, s);
   int32_t tot[2] = {0, 0};
   HIPCHK(hipMemcpyAsync(&tot[0], o.seg_cnt + NT, 4, hipMemcpyDeviceToHost, s));
   HIPCHK(hipMemcpyAsync(&tot[1], o.way_cnt + NT, 4, hipMemcpyDeviceToHost, s));
@@ -362,24 +359,30 @@ int engine_match(otm_engine* E, const DevBatch& b, hipStream_t s, std::string* e
   o.seg_gidx = P<int32_t>(E->o_seg_gidx);
   o.reports = E->o_reports.p;
   o.way_ids = P<int64_t>(E->o_way_ids);
-  launch_segments(E->g, b, w, o, true, s);
-  EV(14);
-  launch_report(b, E->drc, w, o, s);
-  EV(15);
-#undef EV
+  launch_segments(E->g, b, w, o, true, s, mk);
+  launch_report(b, E->drc, w, o, s, mk);
   HIPCHK(hipGetLastError());
   E->last_T = NT;
   E->last_P = NP;
   E->last_S = tot[0];
   E->last_W = tot[1];
   if (E->timing) {
-    // kernel-only spans on the launch stream (host syncs between stages excluded):
-    // columns, candidates, links+scan, transitions (LDS tier), viterbi, route
-    // (final attempt, LDS tier), segments count, segments write + report
-    HIPCHK(hipEventSynchronize(E->ev[15]));
-    const int a[8] = {0, 2, 4, 6, 8, 10, 12, 13};
-    const int z[8] = {1, 3, 5, 7, 9, 11, 13, 15};
-    for (int k = 0; k < 8; ++k) HIPCHK(hipEventElapsedTime(&E->stage_ms[k], E->ev[a[k]], E->ev[z[k]]));
+    // kernel-only spans on the launch stream (host syncs between stages
+    // excluded; the route stage's final attempt).  Stages are sums of their
+    // kernels: columns | candidates (lane + wave tier) | links + scan |
+    // transitions (index, lane, wave, global tiers) | viterbi | route (4 tiers)
+    // | segments count + scans | segments write + report
+    HIPCHK(hipEventSynchronize(E->kev[2 * KN_REPORT + 1]));
+    for (int k = 0; k < KN_COUNT; ++k)
+      HIPCHK(hipEventElapsedTime(&E->kernel_ms[k], E->kev[2 * k], E->kev[2 * k + 1]));
+    const int first[8] = {KN_COLUMNS, KN_CAND_LANE, KN_LINKS, KN_TRANS_INDEX, KN_VITERBI, KN_ROUTE_INDEX, KN_SEG_COUNT,
+                          KN_SEG_WRITE};
+    const int last[8] = {KN_COLUMNS, KN_CAND_WAVE, KN_SCAN_TRANS, KN_TRANS_GLOBAL, KN_VITERBI, KN_ROUTE_GLOBAL,
+                         KN_SEG_SCAN, KN_REPORT};
+    for (int k = 0; k < 8; ++k) {
+      E->stage_ms[k] = 0.0f;
+      for (int q = first[k]; q <= last[k]; ++q) E->stage_ms[k] += E->kernel_ms[q];
+    }
   }
 #undef ENS
   return OTM_OK;
@@ -487,6 +490,22 @@ int engine_debug_fetch(otm_engine* E, int what, void* dst, size_t bytes, size_t*
   }
   if (n) HIPCHK(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, E->stream));
   HIPCHK(hipStreamSynchronize(E->stream));
+  return OTM_OK;
+}
+
+int engine_spill_stats(otm_engine* E, otm_spill_stats* out) {
+  int32_t v[48] = {};
+  if (E->snap.p && hipMemcpy(v, E->snap.p, sizeof v, hipMemcpyDeviceToHost) != hipSuccess) return OTM_EDEVICE;
+  // counters_i32 layout: [5] candidate spills; [4] index misses, [0] lane
+  // spills, [3] LDS-wave spills (per stage)
+  out->cand_wave = v[5];
+  out->trans_online = v[16 + 4];
+  out->trans_wave = v[16 + 0];
+  out->trans_global = v[16 + 3];
+  out->route_online = v[32 + 4];
+  out->route_wave = v[32 + 0];
+  out->route_global = v[32 + 3];
+  out->pad = 0;
   return OTM_OK;
 }
 

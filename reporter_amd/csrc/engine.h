@@ -41,7 +41,7 @@ struct otm_engine {
   // work
   Buf pt_trace, is_col, prevc, gc, ncand, cand_edge, cand_off, cand_emis, col_prev, trans_off, trans, bp, state,
       chain_start, route_dist, path_off, path_len, path_pool, trace_err, overflow_list0, overflow_list, overflow_list2,
-      counters_i32, scan_tmp;
+      counters_i32, scan_tmp, snap;
   Buf big_key, big_lab, big_inq, big_fr;
   // outputs
   Buf o_traces, o_seg_cnt, o_way_cnt, o_segments, o_seg_gidx, o_way_ids, o_reports;
@@ -65,7 +65,8 @@ struct otm_engine {
   std::vector<int64_t> h_ways;
   // timing
   bool timing = false;
-  hipEvent_t ev[16] = {};
+  hipEvent_t kev[2 * otm::KN_COUNT] = {};
+  float kernel_ms[otm::KN_COUNT] = {};
   float stage_ms[8] = {};
   // async submit/poll
   struct Pending {
@@ -93,5 +94,6 @@ int engine_match_host(otm_engine* E, const otm_batch* in, std::string* err);
 int engine_fetch(otm_engine* E, otm_results* out, std::string* err);
 int engine_debug_fetch(otm_engine* E, int what, void* dst, size_t bytes, size_t* needed, std::string* err);
 int engine_counters(otm_engine* E, otm_work_counters* out);
+int engine_spill_stats(otm_engine* E, otm_spill_stats* out);
 
 }  // namespace otm

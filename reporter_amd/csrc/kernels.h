@@ -146,17 +146,56 @@ struct DevOut {
   float bin_kph;
 };
 
+// Per-kernel timing (otm_get_kernel_ms): when ev != nullptr the launchers
+// record ev[2k] just before and ev[2k+1] just after kernel k, on the launch
+// stream.  Order and names: kKernelNames in kernels.hip.
+enum KernelId {
+  KN_COLUMNS,
+  KN_CAND_LANE,
+  KN_CAND_WAVE,
+  KN_LINKS,
+  KN_SCAN_TRANS,
+  KN_TRANS_INDEX,
+  KN_TRANS_LANE,
+  KN_TRANS_WAVE,
+  KN_TRANS_GLOBAL,
+  KN_VITERBI,
+  KN_ROUTE_INDEX,
+  KN_ROUTE_LANE,
+  KN_ROUTE_WAVE,
+  KN_ROUTE_GLOBAL,
+  KN_SEG_COUNT,
+  KN_SEG_SCAN,
+  KN_SEG_WRITE,
+  KN_REPORT,
+  KN_COUNT
+};
+extern const char* const kKernelNames[KN_COUNT];
+struct Marks {
+  hipEvent_t* ev = nullptr;
+  void begin(int k, hipStream_t s) const {
+    if (ev) (void)hipEventRecord(ev[2 * k], s);
+  }
+  void end(int k, hipStream_t s) const {
+    if (ev) (void)hipEventRecord(ev[2 * k + 1], s);
+  }
+};
+
 // ---- launch wrappers (kernels.hip)
-void launch_columns(const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s);
-void launch_candidates(const DevGraph& g, const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s);
-void launch_links(const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s);
+void launch_columns(const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s, const Marks& mk);
+void launch_candidates(const DevGraph& g, const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s,
+                       const Marks& mk);
+void launch_links(const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s, const Marks& mk);
 // lane tier -> wave LDS tier -> global tier, spill lists on the device
 // (counters_i32[0] / [3] must be zero on entry)
-void launch_transitions(const DevGraph& g, const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s);
-void launch_viterbi(const DevBatch& b, DevWork& w, hipStream_t s);
-void launch_route(const DevGraph& g, const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s);
-void launch_segments(const DevGraph& g, const DevBatch& b, DevWork& w, DevOut& o, bool write, hipStream_t s);
-void launch_report(const DevBatch& b, const DevReportCfg& rc, DevWork& w, DevOut& o, hipStream_t s);
+void launch_transitions(const DevGraph& g, const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s,
+                        const Marks& mk);
+void launch_viterbi(const DevBatch& b, DevWork& w, hipStream_t s, const Marks& mk);
+void launch_route(const DevGraph& g, const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s,
+                  const Marks& mk);
+void launch_segments(const DevGraph& g, const DevBatch& b, DevWork& w, DevOut& o, bool write, hipStream_t s,
+                     const Marks& mk);
+void launch_report(const DevBatch& b, const DevReportCfg& rc, DevWork& w, DevOut& o, hipStream_t s, const Marks& mk);
 // index build: pass 0 counts rows (row_cnt), pass 1 inserts them into the
 // row tables (slot array pre-filled with 0xFF)
 void launch_index_build(const DevGraph& g, float rmax, int32_t* row_cnt, const IdxRow* rows, uint2* slot,

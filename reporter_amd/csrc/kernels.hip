@@ -696,6 +696,10 @@ __device__ unsigned long long settled_outdeg(const DevGraph& g, const Table& T, 
 // more than LANE_CAP nodes spills its whole column to the wave tier.
 constexpr uint32_t DONE = 0x80000000u;
 constexpr int LANE_TB = 128;
+// Below this many index misses the lane tier forwards its list to the wave
+// tier untouched: a few serial single-lane searches (~100+ us of dependent
+// LDS and global latency) would cost more than the wave tier's parallel ones.
+constexpr int64_t LANE_TIER_MIN = 4096;
 
 // PRED: keep predecessor edges (the route stage needs them, transitions only
 // need distances -- 8 instead of 12 bytes per slot buys a larger table)
@@ -769,6 +773,13 @@ __global__ __launch_bounds__(LANE_TB) void k_trans_lane(DevGraph g, DevBatch b, 
   float* D = sD + threadIdx.x;
   unsigned long long c_search = 0, c_settled = 0, c_relaxed = 0, c_trans = 0;
   const int64_t nwork = w.counters_i32[4];  // columns the index could not answer
+  if (nwork < LANE_TIER_MIN) {
+    // a handful of misses: one lane's serial search would set the stage's
+    // latency, so hand them all to the wave tier as they are
+    for (int64_t it = (int64_t)blockIdx.x * LANE_TB + threadIdx.x; it < nwork; it += (int64_t)gridDim.x * LANE_TB)
+      w.overflow_list[atomicAdd(&w.counters_i32[0], 1)] = w.overflow_list0[it];
+    return;
+  }
   for (int64_t it = (int64_t)blockIdx.x * LANE_TB + threadIdx.x; it < nwork; it += (int64_t)gridDim.x * LANE_TB) {
     const int64_t p = w.overflow_list0[it];
     const int32_t q = w.col_prev[p];
@@ -856,6 +867,11 @@ __global__ __launch_bounds__(LANE_TB) void k_route_lane(DevGraph g, DevBatch b, 
   int32_t* Pd = sP + threadIdx.x;
   unsigned long long c_search = 0, c_settled = 0, c_relaxed = 0, c_edges = 0;
   const int64_t nwork = w.counters_i32[4];  // steps the index could not answer
+  if (nwork < LANE_TIER_MIN) {  // as in k_trans_lane
+    for (int64_t it = (int64_t)blockIdx.x * LANE_TB + threadIdx.x; it < nwork; it += (int64_t)gridDim.x * LANE_TB)
+      w.overflow_list[atomicAdd(&w.counters_i32[0], 1)] = w.overflow_list0[it];
+    return;
+  }
   for (int64_t it = (int64_t)blockIdx.x * LANE_TB + threadIdx.x; it < nwork; it += (int64_t)gridDim.x * LANE_TB) {
     const int64_t p = w.overflow_list0[it];
     const int32_t q = w.col_prev[p];
@@ -2165,54 +2181,82 @@ int grid_for(int64_t n, int per_block, int cap) {
   return (int)(g > cap ? cap : g);
 }
 
-}  // namespace
-
 // ============================================================== launchers
 constexpr int WAVE_GRID_CAP = 256 * 64;  // grid-stride cap for wave kernels
 
-void launch_columns(const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s) {
-  hipLaunchKernelGGL(k_columns, dim3(grid_for(b.n_traces, 1, WAVE_GRID_CAP)), dim3(TB), 0, s, b, p, w);
-}
-void launch_candidates(const DevGraph& g, const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s) {
-  hipLaunchKernelGGL(k_cand_lane, dim3(grid_for(b.n_points, CAND_TB, 1 << 30)), dim3(CAND_TB), 0, s, g, b, p, w);
-  hipLaunchKernelGGL(k_candidates, dim3(4096), dim3(TB), 0, s, g, b, p, w);
-}
-void launch_links(const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s) {
-  hipLaunchKernelGGL(k_links, dim3(grid_for(b.n_points + 1, 256, 1 << 30)), dim3(256), 0, s, b, p, w);
-}
+}  // namespace
+
+const char* const kKernelNames[KN_COUNT] = {
+    "k_columns",       "k_cand_lane",    "k_candidates",     "k_links",         "scan_trans_off",  "k_trans_index",
+    "k_trans_lane",    "k_transitions",  "k_transitions_big", "k_viterbi",      "k_route_index",   "k_route_lane",
+    "k_route",         "k_route_big",    "k_segments_count", "scan_seg_counts", "k_segments_write", "k_report"};
+
+namespace {
 // The spill tiers run on lists the previous tier filled on the device; they
 // read the list length themselves (fixed grids, no host round trip) and exit
 // at once when the list is empty.
 constexpr int LANE_CAP = 24;        // route stage: 12 B per slot
 constexpr int LANE_CAP_TRANS = 32;  // transitions: 8 B per slot (no predecessors)
 constexpr int SPILL_GRID = 4096;
-
 constexpr int LANE_GRID = 2048;
+}  // namespace
 
-void launch_transitions(const DevGraph& g, const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s) {
-  hipLaunchKernelGGL(k_trans_index, dim3(grid_for(b.n_points, 1, WAVE_GRID_CAP)), dim3(TB), 0, s, g, b, p, w);
-  hipLaunchKernelGGL(k_trans_lane<LANE_CAP_TRANS>, dim3(LANE_GRID), dim3(LANE_TB), 0, s, g, b, p, w);
-  hipLaunchKernelGGL(k_transitions<false>, dim3(SPILL_GRID), dim3(TB), 0, s, g, b, p, w, 0);
-  hipLaunchKernelGGL(k_transitions<true>, dim3(BIG_SLOTS), dim3(TB), 0, s, g, b, p, w, 0);
+#define TIMED(k, launch) \
+  do {                   \
+    mk.begin(k, s);      \
+    launch;              \
+    mk.end(k, s);        \
+  } while (0)
+
+void launch_columns(const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s, const Marks& mk) {
+  TIMED(KN_COLUMNS, hipLaunchKernelGGL(k_columns, dim3(grid_for(b.n_traces, 1, WAVE_GRID_CAP)), dim3(TB), 0, s, b,
+                                       p, w));
 }
-void launch_viterbi(const DevBatch& b, DevWork& w, hipStream_t s) {
-  hipLaunchKernelGGL(k_viterbi, dim3(grid_for(b.n_traces, 1, WAVE_GRID_CAP)), dim3(TB), 0, s, b, w);
+void launch_candidates(const DevGraph& g, const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s,
+                       const Marks& mk) {
+  TIMED(KN_CAND_LANE, hipLaunchKernelGGL(k_cand_lane, dim3(grid_for(b.n_points, CAND_TB, 1 << 30)), dim3(CAND_TB), 0,
+                                         s, g, b, p, w));
+  TIMED(KN_CAND_WAVE, hipLaunchKernelGGL(k_candidates, dim3(4096), dim3(TB), 0, s, g, b, p, w));
 }
-void launch_route(const DevGraph& g, const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s) {
-  hipLaunchKernelGGL(k_route_index, dim3(grid_for(b.n_points, 256, 1 << 30)), dim3(256), 0, s, g, b, p, w);
-  hipLaunchKernelGGL(k_route_lane<LANE_CAP>, dim3(LANE_GRID), dim3(LANE_TB), 0, s, g, b, p, w);
-  hipLaunchKernelGGL(k_route<false>, dim3(SPILL_GRID), dim3(TB), 0, s, g, b, p, w, 0);
-  hipLaunchKernelGGL(k_route<true>, dim3(BIG_SLOTS), dim3(TB), 0, s, g, b, p, w, 0);
+void launch_links(const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s, const Marks& mk) {
+  TIMED(KN_LINKS, hipLaunchKernelGGL(k_links, dim3(grid_for(b.n_points + 1, 256, 1 << 30)), dim3(256), 0, s, b, p,
+                                     w));
 }
-void launch_segments(const DevGraph& g, const DevBatch& b, DevWork& w, DevOut& o, bool write, hipStream_t s) {
+void launch_transitions(const DevGraph& g, const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s,
+                        const Marks& mk) {
+  TIMED(KN_TRANS_INDEX, hipLaunchKernelGGL(k_trans_index, dim3(grid_for(b.n_points, 1, WAVE_GRID_CAP)), dim3(TB), 0,
+                                           s, g, b, p, w));
+  TIMED(KN_TRANS_LANE, hipLaunchKernelGGL(k_trans_lane<LANE_CAP_TRANS>, dim3(LANE_GRID), dim3(LANE_TB), 0, s, g, b,
+                                          p, w));
+  TIMED(KN_TRANS_WAVE, hipLaunchKernelGGL(k_transitions<false>, dim3(SPILL_GRID), dim3(TB), 0, s, g, b, p, w, 0));
+  TIMED(KN_TRANS_GLOBAL, hipLaunchKernelGGL(k_transitions<true>, dim3(BIG_SLOTS), dim3(TB), 0, s, g, b, p, w, 0));
+}
+void launch_viterbi(const DevBatch& b, DevWork& w, hipStream_t s, const Marks& mk) {
+  TIMED(KN_VITERBI, hipLaunchKernelGGL(k_viterbi, dim3(grid_for(b.n_traces, 1, WAVE_GRID_CAP)), dim3(TB), 0, s, b,
+                                       w));
+}
+void launch_route(const DevGraph& g, const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s,
+                  const Marks& mk) {
+  TIMED(KN_ROUTE_INDEX, hipLaunchKernelGGL(k_route_index, dim3(grid_for(b.n_points, 256, 1 << 30)), dim3(256), 0, s,
+                                           g, b, p, w));
+  TIMED(KN_ROUTE_LANE, hipLaunchKernelGGL(k_route_lane<LANE_CAP>, dim3(LANE_GRID), dim3(LANE_TB), 0, s, g, b, p, w));
+  TIMED(KN_ROUTE_WAVE, hipLaunchKernelGGL(k_route<false>, dim3(SPILL_GRID), dim3(TB), 0, s, g, b, p, w, 0));
+  TIMED(KN_ROUTE_GLOBAL, hipLaunchKernelGGL(k_route<true>, dim3(BIG_SLOTS), dim3(TB), 0, s, g, b, p, w, 0));
+}
+void launch_segments(const DevGraph& g, const DevBatch& b, DevWork& w, DevOut& o, bool write, hipStream_t s,
+                     const Marks& mk) {
+  const dim3 grid(grid_for(b.n_traces, 1, WAVE_GRID_CAP));
   if (write)
-    hipLaunchKernelGGL(k_segments<true>, dim3(grid_for(b.n_traces, 1, WAVE_GRID_CAP)), dim3(TB), 0, s, g, b, w, o);
+    TIMED(KN_SEG_WRITE, hipLaunchKernelGGL(k_segments<true>, grid, dim3(TB), 0, s, g, b, w, o));
   else
-    hipLaunchKernelGGL(k_segments<false>, dim3(grid_for(b.n_traces, 1, WAVE_GRID_CAP)), dim3(TB), 0, s, g, b, w, o);
+    TIMED(KN_SEG_COUNT, hipLaunchKernelGGL(k_segments<false>, grid, dim3(TB), 0, s, g, b, w, o));
 }
-void launch_report(const DevBatch& b, const DevReportCfg& rc, DevWork& w, DevOut& o, hipStream_t s) {
-  hipLaunchKernelGGL(k_report, dim3(grid_for(b.n_traces, 64, 1 << 30)), dim3(64), 0, s, b, rc, w, o, 0);
+void launch_report(const DevBatch& b, const DevReportCfg& rc, DevWork& w, DevOut& o, hipStream_t s,
+                   const Marks& mk) {
+  TIMED(KN_REPORT, hipLaunchKernelGGL(k_report, dim3(grid_for(b.n_traces, 64, 1 << 30)), dim3(64), 0, s, b, rc, w,
+                                      o, 0));
 }
+#undef TIMED
 
 void launch_index_build(const DevGraph& g, float rmax, int32_t* row_cnt, const IdxRow* rows, uint2* slot,
                         int32_t* pred, bool write, hipStream_t s) {

@@ -187,6 +187,19 @@ class Engine(object):
         _check(lib().otm_get_stage_ms(self.h, ms, 8))
         return dict(zip(self.STAGES, list(ms)))
 
+    def kernel_ms(self):
+        """Per-kernel times (ms) of the last timed match_device call, by kernel name."""
+        n = 18
+        ms = (C.c_float * n)()
+        _check(lib().otm_get_kernel_ms(self.h, ms, n))
+        return {lib().otm_kernel_name(k).decode(): ms[k] for k in range(n)}
+
+    def spill_stats(self):
+        """Work units of the last batch that each fallback tier took."""
+        st = _lib.SpillStats()
+        _check(lib().otm_get_spill_stats(self.h, C.byref(st)))
+        return {n: getattr(st, n) for n, _ in _lib.SpillStats._fields_ if n != "pad"}
+
     _DEBUG = {"ncand": (0, np.int32), "cand_edge": (1, np.int32), "cand_off": (2, np.float32),
               "cand_emis": (3, np.float32), "trans_off": (4, np.int64), "trans": (5, np.float32),
               "state": (6, np.int32), "col_prev": (7, np.int32), "route_dist": (8, np.float32),

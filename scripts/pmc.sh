@@ -1,0 +1,22 @@
+#!/bin/bash
+# PMC passes over a short bench run (one counter group per rocprofv3 run, as
+# MI355X_MICROARCH.md's rocprofv3 section prescribes), then a JSON summary.
+# Usage (on the GPU box, from the repo root): bash scripts/pmc.sh <out_dir> [tag]
+set -e
+R=$(pwd)
+OUT=$R/${1:-gpurun_out/pmc}
+TAG=${2:-latest}
+mkdir -p $OUT
+cd /tmp && export TMPDIR=/tmp
+BENCH="python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-check --traffic-json none"
+pass() {
+  local name=$1; shift
+  timeout -s KILL 120 rocprofv3 --pmc "$@" --output-format csv -d $OUT/$name -o $name -- $BENCH > $OUT/$name.log 2>&1
+}
+pass fetch FETCH_SIZE
+pass write WRITE_SIZE
+pass tcc TCC_HIT_sum TCC_MISS_sum
+pass sq SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS
+pass lds SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE
+cd $R
+python3 scripts/pmc_summary.py $OUT $TAG > $OUT/pmc_traffic_$TAG.json

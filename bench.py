@@ -40,7 +40,7 @@ KERNEL_STAGE = {
     "scan_trans_off": "links_scan", "k_trans_index": "transitions", "k_trans_lane": "transitions",
     "k_transitions": "transitions", "k_transitions_big": "transitions", "k_viterbi": "viterbi",
     "k_route_index": "route", "k_route_lane": "route", "k_route": "route", "k_route_big": "route",
-    "k_segments_count": "segments", "scan_seg_counts": "segments", "k_segments_write": "segments",
+    "k_seg_bound": "segments", "scan_seg_bound": "segments", "k_segments": "segments",
     "k_report": "report",
 }
 

@@ -18,6 +18,10 @@ namespace otm {
     }                                                                          \
   } while (0)
 
+static int ensure(otm_engine::Buf& b, size_t bytes, std::string* err);
+#define ENS_F(buf, bytes) \
+  if ((rc = ensure(E->buf, (bytes), err))) return rc;
+
 static int ensure(otm_engine::Buf& b, size_t bytes, std::string* err) {
   if (bytes == 0) bytes = 16;
   if (b.cap >= bytes) return OTM_OK;
@@ -190,7 +194,8 @@ void engine_free(otm_engine* E) {
       &E->chain_start,   &E->route_dist,   &E->path_off,       &E->path_len,       &E->path_pool,  &E->trace_err,
       &E->overflow_list0, &E->overflow_list, &E->overflow_list2, &E->counters_i32, &E->scan_tmp, &E->snap,   &E->big_key,
       &E->big_lab,       &E->big_inq,      &E->big_fr,         &E->o_traces,       &E->o_seg_cnt,  &E->o_way_cnt,
-      &E->o_segments,    &E->o_seg_gidx,   &E->o_way_ids,      &E->o_reports};
+      &E->o_segments,    &E->o_seg_gidx,   &E->o_way_ids,      &E->o_reports,  &E->o_rep_cnt,  &E->seg_ub,
+      &E->f_seg_off,     &E->f_way_off,    &E->f_rep_off,      &E->f_segs,     &E->f_ways,     &E->f_reps};
   for (auto* b : bufs) {
     if (b->p) (void)hipFree(b->p);
     b->p = nullptr;
@@ -311,6 +316,7 @@ int engine_match(otm_engine* E, const DevBatch& b, hipStream_t s, std::string* e
   // a path-pool overflow redoes the whole stage: restore the work counters
   // so the redone searches are counted once
   if (E->counting) HIPCHK(hipMemcpyAsync(E->ctr_save, E->ctr, sizeof(DevCounters), hipMemcpyDeviceToDevice, s));
+  int32_t cnt[3] = {0, 0, 0};
   for (int attempt = 0; attempt < 4; ++attempt) {
     if (E->counting && attempt > 0)
       HIPCHK(hipMemcpyAsync(E->ctr, E->ctr_save, sizeof(DevCounters), hipMemcpyDeviceToDevice, s));
@@ -318,7 +324,6 @@ int engine_match(otm_engine* E, const DevBatch& b, hipStream_t s, std::string* e
     launch_route(E->g, b, E->dp, w, s, mk);
     // spill snapshot C: steps per route tier (final attempt)
     HIPCHK(hipMemcpyAsync(P<char>(E->snap) + 128, w.counters_i32, 64, hipMemcpyDeviceToDevice, s));
-    int32_t cnt[3] = {0, 0, 0};
     HIPCHK(hipMemcpyAsync(cnt, w.counters_i32, 12, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     if (!cnt[2]) break;
@@ -333,39 +338,45 @@ int engine_match(otm_engine* E, const DevBatch& b, hipStream_t s, std::string* e
     }
   }
 
+  // Segments, way ids and reports in ONE walk per trace, each trace writing
+  // into a region sized by an upper bound (DevOut); the bound's total is known
+  // on the host without another sync: every matched point adds <= 2 + its path
+  // length, and the path lengths sum to the pool use read above.
+  const size_t cap = 2 * (size_t)NP + (size_t)cnt[1] + 1;
+  if (cap >= (size_t)INT32_MAX) {
+    *err = "batch too large for one launch (segment regions exceed 2^31)";
+    return OTM_EINVAL;
+  }
+  ENS(seg_ub, Pn * 8 + 8);
+  ENS(o_segments, cap * sizeof(otm_segment));
+  ENS(o_seg_gidx, cap * 4);
+  ENS(o_reports, cap * sizeof(otm_report_rec));
+  ENS(o_way_ids, cap * 8);
+  ENS(o_rep_cnt, ((size_t)NT + 1) * 4);
   DevOut o{};
   o.traces = E->o_traces.p;
   o.seg_cnt = P<int32_t>(E->o_seg_cnt);
   o.way_cnt = P<int32_t>(E->o_way_cnt);
-  o.hist = E->hist;
-  o.nbins = E->nbins;
-  o.bin_kph = E->bin_kph;
-  HIPCHK(hipMemsetAsync(o.seg_cnt + NT, 0, 4, s));
-  HIPCHK(hipMemsetAsync(o.way_cnt + NT, 0, 4, s));
-  launch_segments(E->g, b, w, o, false, s, mk);
-  mk.begin(KN_SEG_SCAN, s);
-  scan_i32(o.seg_cnt, NT, E->scan_tmp.p, E->scan_tmp.cap, s);
-  scan_i32(o.way_cnt, NT, E->scan_tmp.p, E->scan_tmp.cap, s);
-  mk.end(KN_SEG_SCAN, s);
-  int32_t tot[2] = {0, 0};
-  HIPCHK(hipMemcpyAsync(&tot[0], o.seg_cnt + NT, 4, hipMemcpyDeviceToHost, s));
-  HIPCHK(hipMemcpyAsync(&tot[1], o.way_cnt + NT, 4, hipMemcpyDeviceToHost, s));
-  HIPCHK(hipStreamSynchronize(s));
-  ENS(o_segments, ((size_t)tot[0] + 1) * sizeof(otm_segment));
-  ENS(o_seg_gidx, ((size_t)tot[0] + 1) * 4);
-  ENS(o_reports, ((size_t)tot[0] + 1) * sizeof(otm_report_rec));
-  ENS(o_way_ids, ((size_t)tot[1] + 1) * 8);
+  o.rep_cnt = P<int32_t>(E->o_rep_cnt);
+  o.seg_base = P<int64_t>(E->seg_ub);
   o.segments = E->o_segments.p;
   o.seg_gidx = P<int32_t>(E->o_seg_gidx);
   o.reports = E->o_reports.p;
   o.way_ids = P<int64_t>(E->o_way_ids);
+  o.hist = E->hist;
+  o.nbins = E->nbins;
+  o.bin_kph = E->bin_kph;
+  launch_seg_bound(b, w, P<int64_t>(E->seg_ub), s, mk);
+  mk.begin(KN_SEG_SCAN, s);
+  scan_i64(P<int64_t>(E->seg_ub), NP, E->scan_tmp.p, E->scan_tmp.cap, s);
+  mk.end(KN_SEG_SCAN, s);
   launch_segments(E->g, b, w, o, true, s, mk);
   launch_report(b, E->drc, w, o, s, mk);
   HIPCHK(hipGetLastError());
   E->last_T = NT;
   E->last_P = NP;
-  E->last_S = tot[0];
-  E->last_W = tot[1];
+  E->last_S = -1;  // known after compaction (engine_fetch)
+  E->last_W = -1;
   if (E->timing) {
     // kernel-only spans on the launch stream (host syncs between stages
     // excluded; the route stage's final attempt).  Stages are sums of their
@@ -375,7 +386,7 @@ int engine_match(otm_engine* E, const DevBatch& b, hipStream_t s, std::string* e
     HIPCHK(hipEventSynchronize(E->kev[2 * KN_REPORT + 1]));
     for (int k = 0; k < KN_COUNT; ++k)
       HIPCHK(hipEventElapsedTime(&E->kernel_ms[k], E->kev[2 * k], E->kev[2 * k + 1]));
-    const int first[8] = {KN_COLUMNS, KN_CAND_LANE, KN_LINKS, KN_TRANS_INDEX, KN_VITERBI, KN_ROUTE_INDEX, KN_SEG_COUNT,
+    const int first[8] = {KN_COLUMNS, KN_CAND_LANE, KN_LINKS, KN_TRANS_INDEX, KN_VITERBI, KN_ROUTE_INDEX, KN_SEG_BOUND,
                           KN_SEG_WRITE};
     const int last[8] = {KN_COLUMNS, KN_CAND_WAVE, KN_SCAN_TRANS, KN_TRANS_GLOBAL, KN_VITERBI, KN_ROUTE_GLOBAL,
                          KN_SEG_SCAN, KN_REPORT};
@@ -431,32 +442,65 @@ int engine_match_host(otm_engine* E, const otm_batch* in, std::string* err) {
 
 int engine_fetch(otm_engine* E, otm_results* out, std::string* err) {
   hipStream_t s = E->stream;
-  const int32_t NT = E->last_T, NS = E->last_S, NW = E->last_W;
+  const int32_t NT = E->last_T;
+  int rc;
+  // dense offsets: exclusive scans of the per-trace counts, then one
+  // compaction pass out of the per-trace regions
+  ENS_F(f_seg_off, ((size_t)NT + 1) * 4);
+  ENS_F(f_way_off, ((size_t)NT + 1) * 4);
+  ENS_F(f_rep_off, ((size_t)NT + 1) * 4);
+  int32_t* so = P<int32_t>(E->f_seg_off);
+  int32_t* wo = P<int32_t>(E->f_way_off);
+  int32_t* ro = P<int32_t>(E->f_rep_off);
+  int32_t tot[3] = {0, 0, 0};
+  if (NT) {
+    HIPCHK(hipMemcpyAsync(so, E->o_seg_cnt.p, (size_t)NT * 4, hipMemcpyDeviceToDevice, s));
+    HIPCHK(hipMemcpyAsync(wo, E->o_way_cnt.p, (size_t)NT * 4, hipMemcpyDeviceToDevice, s));
+    HIPCHK(hipMemcpyAsync(ro, E->o_rep_cnt.p, (size_t)NT * 4, hipMemcpyDeviceToDevice, s));
+    HIPCHK(hipMemsetAsync(so + NT, 0, 4, s));
+    HIPCHK(hipMemsetAsync(wo + NT, 0, 4, s));
+    HIPCHK(hipMemsetAsync(ro + NT, 0, 4, s));
+    scan_i32(so, NT, E->scan_tmp.p, E->scan_tmp.cap, s);
+    scan_i32(wo, NT, E->scan_tmp.p, E->scan_tmp.cap, s);
+    scan_i32(ro, NT, E->scan_tmp.p, E->scan_tmp.cap, s);
+    HIPCHK(hipMemcpyAsync(&tot[0], so + NT, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(&tot[1], wo + NT, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(&tot[2], ro + NT, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+  }
+  const int32_t NS = tot[0], NW = tot[1], NR = tot[2];
+  ENS_F(f_segs, ((size_t)NS + 1) * sizeof(otm_segment));
+  ENS_F(f_ways, ((size_t)NW + 1) * 8);
+  ENS_F(f_reps, ((size_t)NR + 1) * sizeof(otm_report_rec));
+  if (NT) {
+    DevOut o{};
+    o.traces = E->o_traces.p;
+    o.seg_cnt = P<int32_t>(E->o_seg_cnt);
+    o.way_cnt = P<int32_t>(E->o_way_cnt);
+    o.rep_cnt = P<int32_t>(E->o_rep_cnt);
+    o.segments = E->o_segments.p;
+    o.way_ids = P<int64_t>(E->o_way_ids);
+    o.reports = E->o_reports.p;
+    launch_compact(NT, o, so, wo, ro, E->f_segs.p, P<int64_t>(E->f_ways), E->f_reps.p, s);
+    HIPCHK(hipGetLastError());
+  }
+  E->last_S = NS;
+  E->last_W = NW;
   E->h_traces.resize((size_t)NT + 1);
   E->h_segs.resize((size_t)NS + 1);
-  E->h_reps.resize((size_t)NS + 1);
+  E->h_reps_dense.resize((size_t)NR + 1);
   E->h_ways.resize((size_t)NW + 1);
   if (NT) HIPCHK(hipMemcpyAsync(E->h_traces.data(), E->o_traces.p, (size_t)NT * sizeof(otm_trace_result),
                                 hipMemcpyDeviceToHost, s));
-  if (NS) {
-    HIPCHK(hipMemcpyAsync(E->h_segs.data(), E->o_segments.p, (size_t)NS * sizeof(otm_segment), hipMemcpyDeviceToHost,
-                          s));
-    HIPCHK(hipMemcpyAsync(E->h_reps.data(), E->o_reports.p, (size_t)NS * sizeof(otm_report_rec),
-                          hipMemcpyDeviceToHost, s));
-  }
-  if (NW) HIPCHK(hipMemcpyAsync(E->h_ways.data(), E->o_way_ids.p, (size_t)NW * 8, hipMemcpyDeviceToHost, s));
+  if (NS) HIPCHK(hipMemcpyAsync(E->h_segs.data(), E->f_segs.p, (size_t)NS * sizeof(otm_segment), hipMemcpyDeviceToHost,
+                                s));
+  if (NR) HIPCHK(hipMemcpyAsync(E->h_reps_dense.data(), E->f_reps.p, (size_t)NR * sizeof(otm_report_rec),
+                                hipMemcpyDeviceToHost, s));
+  if (NW) HIPCHK(hipMemcpyAsync(E->h_ways.data(), E->f_ways.p, (size_t)NW * 8, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
-  // reports are written at their trace's segment offset; compact them
-  E->h_reps_dense.clear();
-  for (int32_t t = 0; t < NT; ++t) {
-    otm_trace_result& r = E->h_traces[t];
-    const int32_t base = r.rep_off;
-    r.rep_off = (int32_t)E->h_reps_dense.size();
-    for (int32_t k = 0; k < r.rep_cnt; ++k) E->h_reps_dense.push_back(E->h_reps[(size_t)base + k]);
-  }
   out->n_traces = NT;
   out->n_segments = NS;
-  out->n_reports = (int32_t)E->h_reps_dense.size();
+  out->n_reports = NR;
   out->n_way_ids = NW;
   out->traces = E->h_traces.data();
   out->segments = E->h_segs.data();

@@ -44,7 +44,9 @@ struct otm_engine {
       counters_i32, scan_tmp, snap;
   Buf big_key, big_lab, big_inq, big_fr;
   // outputs
-  Buf o_traces, o_seg_cnt, o_way_cnt, o_segments, o_seg_gidx, o_way_ids, o_reports;
+  Buf o_traces, o_seg_cnt, o_way_cnt, o_rep_cnt, seg_ub, o_segments, o_seg_gidx, o_way_ids, o_reports;
+  // dense copies made by engine_fetch
+  Buf f_seg_off, f_way_off, f_rep_off, f_segs, f_ways, f_reps;
   otm::DevCounters* ctr = nullptr;
   otm::DevCounters* ctr_save = nullptr;
   bool counting = false;
@@ -61,7 +63,7 @@ struct otm_engine {
   // host copies of the last fetched results
   std::vector<otm_trace_result> h_traces;
   std::vector<otm_segment> h_segs;
-  std::vector<otm_report_rec> h_reps, h_reps_dense;
+  std::vector<otm_report_rec> h_reps_dense;
   std::vector<int64_t> h_ways;
   // timing
   bool timing = false;

@@ -131,16 +131,22 @@ struct DevWork {
   DevCounters* ctr;        // nullptr when counting is off
 };
 
+// Outputs of one batch.  Segments, way ids and reports are written in one
+// pass into per-trace regions sized by an upper bound (2 traversals per
+// matched point + its route's path edges, scanned over points: trace t's
+// region starts at seg_base[trace_off[t]]); otm_fetch_results compacts them.
 struct DevOut {
   // per trace
-  void* traces;          // otm_trace_result[T]
-  int32_t* seg_cnt;      // [T+1] counts -> scanned offsets
-  int32_t* way_cnt;      // [T+1]
-  // flat
-  void* segments;        // otm_segment[S]
-  int32_t* seg_gidx;     // [S] segment index in graph (-1 none)
-  int64_t* way_ids;      // [W]
-  void* reports;         // otm_report_rec[S] (capacity = segments)
+  void* traces;          // otm_trace_result[T] (seg_off / rep_off = region start)
+  int32_t* seg_cnt;      // [T+1] segments per trace
+  int32_t* way_cnt;      // [T+1] way ids per trace
+  int32_t* rep_cnt;      // [T+1] reports per trace
+  const int64_t* seg_base;  // [P+1] exclusive scan of the per-point bound
+  // regions (capacity = bound total)
+  void* segments;        // otm_segment[]
+  int32_t* seg_gidx;     // [] segment index in graph (-1 none)
+  int64_t* way_ids;      // []
+  void* reports;         // otm_report_rec[]
   uint32_t* hist;        // [n_segments * nbins] or nullptr
   int nbins;
   float bin_kph;
@@ -164,7 +170,7 @@ enum KernelId {
   KN_ROUTE_LANE,
   KN_ROUTE_WAVE,
   KN_ROUTE_GLOBAL,
-  KN_SEG_COUNT,
+  KN_SEG_BOUND,
   KN_SEG_SCAN,
   KN_SEG_WRITE,
   KN_REPORT,
@@ -196,6 +202,13 @@ void launch_route(const DevGraph& g, const DevBatch& b, const DevParams& p, DevW
 void launch_segments(const DevGraph& g, const DevBatch& b, DevWork& w, DevOut& o, bool write, hipStream_t s,
                      const Marks& mk);
 void launch_report(const DevBatch& b, const DevReportCfg& rc, DevWork& w, DevOut& o, hipStream_t s, const Marks& mk);
+// per-point bound of the segments / way ids a matched point can emit (scanned
+// into DevOut::seg_base)
+void launch_seg_bound(const DevBatch& b, DevWork& w, int64_t* ub, hipStream_t s, const Marks& mk);
+// fetch-time compaction of the per-trace regions into dense arrays; offsets
+// are the exclusive scans of seg_cnt / way_cnt / rep_cnt
+void launch_compact(int32_t n_traces, const DevOut& o, const int32_t* seg_off, const int32_t* way_off,
+                    const int32_t* rep_off, void* segs_out, int64_t* ways_out, void* reps_out, hipStream_t s);
 // index build: pass 0 counts rows (row_cnt), pass 1 inserts them into the
 // row tables (slot array pre-filled with 0xFF)
 void launch_index_build(const DevGraph& g, float rmax, int32_t* row_cnt, const IdxRow* rows, uint2* slot,

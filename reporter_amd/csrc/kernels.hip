@@ -1927,11 +1927,12 @@ struct SegSrcLds {
 // per step the close of the open traversal, the route's path edges and the
 // re-open on the new edge; traversals grouped into OSMLR segments.
 template <bool WRITE, class Src>
-__device__ void segments_trace(const DevGraph& g, const DevWork& w, DevOut& o, int32_t t, int n, const Src& S) {
+__device__ void segments_trace(const DevGraph& g, const DevWork& w, DevOut& o, int32_t t, int n, int32_t base,
+                               const Src& S) {
   SegEmitter<WRITE> em;
   em.o = &o;
-  em.seg_base = WRITE ? o.seg_cnt[t] : 0;
-  em.way_base = WRITE ? o.way_cnt[t] : 0;
+  em.seg_base = base;
+  em.way_base = base;
   bool open = false;
   int nstate = 0;
   Trav cur{};
@@ -2006,10 +2007,8 @@ __device__ void segments_trace(const DevGraph& g, const DevWork& w, DevOut& o, i
     ++nstate;
     lastp = p;
   }
-  if (!WRITE) {
-    o.seg_cnt[t] = em.nseg;
-    o.way_cnt[t] = em.nway;
-  }
+  o.seg_cnt[t] = em.nseg;
+  o.way_cnt[t] = em.nway;
 }
 
 // One wavefront per trace: lanes stage the trace's points (state, chain
@@ -2022,15 +2021,16 @@ __global__ __launch_bounds__(TB) void k_segments(DevGraph g, DevBatch b, DevWork
   for (int32_t t = blockIdx.x; t < b.n_traces; t += gridDim.x) {
     const int64_t a = b.trace_off[t];
     const int n = (int)(b.trace_off[t + 1] - a);
+    const int32_t base = (int32_t)o.seg_base[a];
     if (w.trace_err[t] != 0) {
-      if (!WRITE && lane == 0) {
+      if (lane == 0) {
         o.seg_cnt[t] = 0;
         o.way_cnt[t] = 0;
       }
       continue;
     }
     if (n > SEG_PTS) {
-      if (lane == 0) segments_trace<WRITE>(g, w, o, t, n, SegSrcGlobal{&g, &b, &w, a});
+      if (lane == 0) segments_trace<WRITE>(g, w, o, t, n, base, SegSrcGlobal{&g, &b, &w, a});
       continue;
     }
     for (int pl = lane; pl < n; pl += TB) {
@@ -2061,7 +2061,7 @@ __global__ __launch_bounds__(TB) void k_segments(DevGraph g, DevBatch b, DevWork
       }
     }
     __syncthreads();
-    if (lane == 0) segments_trace<WRITE>(g, w, o, t, n, SegSrcLds{&L});
+    if (lane == 0) segments_trace<WRITE>(g, w, o, t, n, base, SegSrcLds{&L});
     __syncthreads();
   }
 }
@@ -2079,8 +2079,8 @@ __global__ __launch_bounds__(256) void k_report(DevBatch b, DevReportCfg rc, Dev
   otm_trace_result r;
   r.code = 200;
   r.error_kind = w.trace_err[t];
-  r.seg_off = o.seg_cnt[t];
-  r.seg_cnt = o.seg_cnt[t + 1] - o.seg_cnt[t];
+  r.seg_off = (int32_t)o.seg_base[b.trace_off[t]];
+  r.seg_cnt = o.seg_cnt[t];
   r.rep_off = r.seg_off;
   r.rep_cnt = 0;
   r.shape_used = -1;
@@ -2091,6 +2091,7 @@ __global__ __launch_bounds__(256) void k_report(DevBatch b, DevReportCfg rc, Dev
   if (r.error_kind != 0) {
     r.code = 500;
     ((otm_trace_result*)o.traces)[t] = r;
+    o.rep_cnt[t] = 0;
     return;
   }
   const double end_time = b.time[b.trace_off[t + 1] - 1];
@@ -2173,6 +2174,49 @@ __global__ __launch_bounds__(256) void k_report(DevBatch b, DevReportCfg rc, Dev
     }
   }
   ((otm_trace_result*)o.traces)[t] = r;
+  o.rep_cnt[t] = r.rep_cnt;
+}
+
+// ============================================================== segment bound / compaction
+// Traversals a matched point can add: the close of the open traversal, its
+// route's path edges, the re-open (+ the chain's final close): <= 2 + path.
+__global__ __launch_bounds__(256) void k_seg_bound(DevBatch b, DevWork w, int64_t* ub) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p > b.n_points) return;
+  int64_t v = 0;
+  if (p < b.n_points && w.is_col[p] && w.state[p] >= 0) {
+    const int32_t pl = w.path_len[p];
+    v = 2 + (pl > 0 ? pl : 0);
+  }
+  ub[p] = v;
+}
+
+// One wavefront per trace: copy its segments (way offsets rebased), way ids
+// and reports from the trace's region to the dense arrays; rewrite the
+// trace's offsets.
+__global__ __launch_bounds__(TB) void k_compact(int32_t n_traces, DevOut o, const int32_t* seg_off, const int32_t* way_off,
+                                                const int32_t* rep_off, otm_segment* so, int64_t* wo,
+                                                otm_report_rec* ro) {
+  const int lane = threadIdx.x;
+  otm_trace_result* TR = (otm_trace_result*)o.traces;
+  const otm_segment* SI = (const otm_segment*)o.segments;
+  const otm_report_rec* RI = (const otm_report_rec*)o.reports;
+  for (int32_t t = blockIdx.x; t < n_traces; t += gridDim.x) {
+    const int32_t base = TR[t].seg_off;  // the region start k_report recorded
+    const int32_t ns = o.seg_cnt[t], nw = o.way_cnt[t], nr = o.rep_cnt[t];
+    const int32_t ds = seg_off[t], dw = way_off[t], dr = rep_off[t];
+    for (int k = lane; k < ns; k += TB) {
+      otm_segment x = SI[base + k];
+      x.way_off = x.way_off - base + dw;
+      so[ds + k] = x;
+    }
+    for (int k = lane; k < nw; k += TB) wo[dw + k] = o.way_ids[base + k];
+    for (int k = lane; k < nr; k += TB) ro[dr + k] = RI[base + k];
+    if (lane == 0) {
+      TR[t].seg_off = ds;
+      TR[t].rep_off = dr;
+    }
+  }
 }
 
 int grid_for(int64_t n, int per_block, int cap) {
@@ -2189,7 +2233,7 @@ constexpr int WAVE_GRID_CAP = 256 * 64;  // grid-stride cap for wave kernels
 const char* const kKernelNames[KN_COUNT] = {
     "k_columns",       "k_cand_lane",    "k_candidates",     "k_links",         "scan_trans_off",  "k_trans_index",
     "k_trans_lane",    "k_transitions",  "k_transitions_big", "k_viterbi",      "k_route_index",   "k_route_lane",
-    "k_route",         "k_route_big",    "k_segments_count", "scan_seg_counts", "k_segments_write", "k_report"};
+    "k_route",         "k_route_big",    "k_seg_bound",      "scan_seg_bound",  "k_segments",       "k_report"};
 
 namespace {
 // The spill tiers run on lists the previous tier filled on the device; they
@@ -2245,11 +2289,18 @@ void launch_route(const DevGraph& g, const DevBatch& b, const DevParams& p, DevW
 }
 void launch_segments(const DevGraph& g, const DevBatch& b, DevWork& w, DevOut& o, bool write, hipStream_t s,
                      const Marks& mk) {
+  (void)write;
   const dim3 grid(grid_for(b.n_traces, 1, WAVE_GRID_CAP));
-  if (write)
-    TIMED(KN_SEG_WRITE, hipLaunchKernelGGL(k_segments<true>, grid, dim3(TB), 0, s, g, b, w, o));
-  else
-    TIMED(KN_SEG_COUNT, hipLaunchKernelGGL(k_segments<false>, grid, dim3(TB), 0, s, g, b, w, o));
+  TIMED(KN_SEG_WRITE, hipLaunchKernelGGL(k_segments<true>, grid, dim3(TB), 0, s, g, b, w, o));
+}
+void launch_seg_bound(const DevBatch& b, DevWork& w, int64_t* ub, hipStream_t s, const Marks& mk) {
+  TIMED(KN_SEG_BOUND, hipLaunchKernelGGL(k_seg_bound, dim3(grid_for(b.n_points + 1, 256, 1 << 30)), dim3(256), 0, s,
+                                         b, w, ub));
+}
+void launch_compact(int32_t n_traces, const DevOut& o, const int32_t* seg_off, const int32_t* way_off,
+                    const int32_t* rep_off, void* segs_out, int64_t* ways_out, void* reps_out, hipStream_t s) {
+  hipLaunchKernelGGL(k_compact, dim3(grid_for(n_traces, 1, WAVE_GRID_CAP)), dim3(TB), 0, s, n_traces, o, seg_off, way_off,
+                     rep_off, (otm_segment*)segs_out, ways_out, (otm_report_rec*)reps_out);
 }
 void launch_report(const DevBatch& b, const DevReportCfg& rc, DevWork& w, DevOut& o, hipStream_t s,
                    const Marks& mk) {

@@ -179,8 +179,8 @@ class Engine(object):
     def set_timing(self, on):
         _check(lib().otm_set_timing(self.h, 1 if on else 0))
 
-    STAGES = ("columns", "candidates", "links_scan", "transitions", "viterbi", "route", "segments_count",
-              "segments_write_report")
+    STAGES = ("columns", "candidates", "links_scan", "transitions", "viterbi", "route", "segment_bound",
+              "segments_report")
 
     def stage_ms(self):
         ms = (C.c_float * 8)()

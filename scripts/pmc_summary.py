@@ -19,8 +19,7 @@ def short(name):
     n = n.replace("void ", "")
     alias = {"k_trans_lane<32>": "k_trans_lane", "k_transitions<false>": "k_transitions",
              "k_transitions<true>": "k_transitions_big", "k_route_lane<24>": "k_route_lane",
-             "k_route<false>": "k_route", "k_route<true>": "k_route_big", "k_segments<false>": "k_segments_count",
-             "k_segments<true>": "k_segments_write"}
+             "k_route<false>": "k_route", "k_route<true>": "k_route_big", "k_segments<true>": "k_segments"}
     return alias.get(n, n)
 
 

@@ -36,7 +36,7 @@ DEFAULT_TRAFFIC = os.path.join(ROOT, "profiles", "pmc_traffic_latest.json")
 
 # kernel -> (stage, main tier of the stage?)
 KERNEL_STAGE = {
-    "k_columns": "columns", "k_cand_lane": "candidates", "k_candidates": "candidates", "k_links": "links_scan",
+    "k_columns": "columns", "spatial_order": "candidates", "k_cand_lane": "candidates", "k_candidates": "candidates", "k_links": "links_scan",
     "scan_trans_off": "links_scan", "k_trans_index": "transitions", "k_trans_lane": "transitions",
     "k_transitions": "transitions", "k_transitions_big": "transitions", "k_viterbi": "viterbi",
     "k_route_index": "route", "k_route_lane": "route", "k_route": "route", "k_route_big": "route",

@@ -109,6 +109,14 @@ int engine_init(otm_engine* E, const char* graph_path, int device, std::string* 
   g.n_segments = h.n_segments;
   g.grid_rows = h.grid_rows;
   g.grid_cols = h.grid_cols;
+  {
+    // spatial-order tiles over the node bbox (a hair wider so max lands inside)
+    const double h_deg = (h.bbox[2] - h.bbox[0]) * 1.0001 + 1e-9, w_deg = (h.bbox[3] - h.bbox[1]) * 1.0001 + 1e-9;
+    g.bb_lat0 = (float)h.bbox[0];
+    g.bb_lon0 = (float)h.bbox[1];
+    g.bb_inv_h = (float)(ORDER_SIDE / h_deg);
+    g.bb_inv_w = (float)(ORDER_SIDE / w_deg);
+  }
   g.lat0 = h.grid_lat0;
   g.lon0 = h.grid_lon0;
   g.cell = h.grid_cell_deg;
@@ -195,7 +203,8 @@ void engine_free(otm_engine* E) {
       &E->overflow_list0, &E->overflow_list, &E->overflow_list2, &E->counters_i32, &E->scan_tmp, &E->snap,   &E->big_key,
       &E->big_lab,       &E->big_inq,      &E->big_fr,         &E->o_traces,       &E->o_seg_cnt,  &E->o_way_cnt,
       &E->o_segments,    &E->o_seg_gidx,   &E->o_way_ids,      &E->o_reports,  &E->o_rep_cnt,  &E->seg_ub,
-      &E->f_seg_off,     &E->f_way_off,    &E->f_rep_off,      &E->f_segs,     &E->f_ways,     &E->f_reps};
+      &E->f_seg_off,     &E->f_way_off,    &E->f_rep_off,      &E->f_segs,     &E->f_ways,     &E->f_reps,
+      &E->ord_tile,      &E->ord_cnt,      &E->ord_cursor,     &E->ord_grp,    &E->ord_item};
   for (auto* b : bufs) {
     if (b->p) (void)hipFree(b->p);
     b->p = nullptr;
@@ -289,7 +298,23 @@ int engine_match(otm_engine* E, const DevBatch& b, hipStream_t s, std::string* e
   HIPCHK(hipMemsetAsync(w.counters_i32, 0, 64, s));  // [5] = candidate spill count
   Marks mk;
   mk.ev = E->timing ? E->kev : nullptr;
-  launch_columns(b, E->dp, w, s, mk);
+  ENS(ord_tile, Pn * 2);
+  ENS(ord_cnt, ORDER_TILES * 4);
+  ENS(ord_cursor, ORDER_TILES * 4);
+  ENS(ord_grp, (ORDER_GROUPS + 1) * 4);
+  ENS(ord_item, Pn * 4);
+  w.ord.item = P<int32_t>(E->ord_item);
+  w.ord.grp = P<int32_t>(E->ord_grp);
+  w.ord.tile = P<uint16_t>(E->ord_tile);
+  w.ord.tile_cnt = E->dp.order_mask ? P<int32_t>(E->ord_cnt) : nullptr;
+  w.ord.cursor = P<int32_t>(E->ord_cursor);
+  launch_columns(E->g, b, E->dp, w, s, mk);
+  if (E->dp.order_mask) {
+    launch_order(b, w, s, mk);
+  } else if (E->timing) {
+    mk.begin(KN_ORDER, s);
+    mk.end(KN_ORDER, s);
+  }
   launch_candidates(E->g, b, E->dp, w, s, mk);
   // spill snapshot A: candidate probes the lane tier handed to the wave tier
   HIPCHK(hipMemcpyAsync(E->snap.p, w.counters_i32, 64, hipMemcpyDeviceToDevice, s));
@@ -386,7 +411,7 @@ int engine_match(otm_engine* E, const DevBatch& b, hipStream_t s, std::string* e
     HIPCHK(hipEventSynchronize(E->kev[2 * KN_REPORT + 1]));
     for (int k = 0; k < KN_COUNT; ++k)
       HIPCHK(hipEventElapsedTime(&E->kernel_ms[k], E->kev[2 * k], E->kev[2 * k + 1]));
-    const int first[8] = {KN_COLUMNS, KN_CAND_LANE, KN_LINKS, KN_TRANS_INDEX, KN_VITERBI, KN_ROUTE_INDEX, KN_SEG_BOUND,
+    const int first[8] = {KN_COLUMNS, KN_ORDER, KN_LINKS, KN_TRANS_INDEX, KN_VITERBI, KN_ROUTE_INDEX, KN_SEG_BOUND,
                           KN_SEG_WRITE};
     const int last[8] = {KN_COLUMNS, KN_CAND_WAVE, KN_SCAN_TRANS, KN_TRANS_GLOBAL, KN_VITERBI, KN_ROUTE_GLOBAL,
                          KN_SEG_SCAN, KN_REPORT};

@@ -43,6 +43,7 @@ struct otm_engine {
       chain_start, route_dist, path_off, path_len, path_pool, trace_err, overflow_list0, overflow_list, overflow_list2,
       counters_i32, scan_tmp, snap;
   Buf big_key, big_lab, big_inq, big_fr;
+  Buf ord_tile, ord_cnt, ord_cursor, ord_grp, ord_item;  // spatial work order
   // outputs
   Buf o_traces, o_seg_cnt, o_way_cnt, o_rep_cnt, seg_ub, o_segments, o_seg_gidx, o_way_ids, o_reports;
   // dense copies made by engine_fetch

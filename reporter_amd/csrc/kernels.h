@@ -44,6 +44,26 @@ struct DevGraph {
   const float4* ent_geo;  // per cell entry: shape segment endpoints (lat_a, lon_a, lat_b, lon_b)
   int32_t n_nodes, n_edges, n_segments, grid_rows, grid_cols;
   double lat0, lon0, cell;
+  // spatial work order tiles: the node bbox cut into ORDER_SIDE^2 tiles
+  float bb_lat0, bb_lon0, bb_inv_h, bb_inv_w;  // tile row = (lat - bb_lat0) * bb_inv_h, ...
+};
+
+// Spatial work order of a batch's columns: column points
+// bucketed by the Hilbert index of their tile, the tiles cut into 8
+// equal-count groups.  Group g runs on the blocks with blockIdx % 8 == g,
+// which the dispatcher deals to one XCD, so each XCD's L2 holds one region's
+// grid cells and index rows; inside a group, neighbouring lanes and waves get
+// neighbouring probes.
+constexpr int ORDER_BITS = 6;
+constexpr int ORDER_SIDE = 1 << ORDER_BITS;  // 64 x 64 tiles
+constexpr int ORDER_TILES = ORDER_SIDE * ORDER_SIDE;
+constexpr int ORDER_GROUPS = 8;
+struct DevOrder {
+  int32_t* item;      // [n] column points, grouped
+  int32_t* grp;       // [ORDER_GROUPS + 1] group starts in item space
+  uint16_t* tile;     // [P] tile of each column (K1)
+  int32_t* tile_cnt;  // [ORDER_TILES] columns per tile (K1); nullptr: no order this batch
+  int32_t* cursor;    // [ORDER_TILES] scatter cursors
 };
 
 // Bounded distance index (built once per engine): for every
@@ -66,9 +86,12 @@ struct DevIndex {
 constexpr int INDEX_BUILD_CAP = 2048;   // LDS table of the index builder
 constexpr int INDEX_BUILD_LIMIT = 1536; // nodes per row before the row is left incomplete
 
+// which kernels walk the spatial work order (env OTM_ORDER_MASK)
+constexpr int ORDER_CAND = 1, ORDER_TRANS = 2, ORDER_ROUTE = 4;
 struct DevParams {
   float sigma_z, beta, factor, breakage, interp, search_radius, max_search_radius, gps_accuracy;
   int max_candidates;
+  int order_mask;
 };
 
 struct DevReportCfg {
@@ -123,6 +146,7 @@ struct DevWork {
   int32_t* counters_i32;   // [0] list 1 count, [1] pool used, [2] pool overflow flag, [3] list 2 count,
                            // [4] list 0 count
   DevIndex idx;
+  DevOrder ord;
   // global-tier scratch
   uint32_t* big_key;
   unsigned long long* big_lab;
@@ -157,6 +181,7 @@ struct DevOut {
 // stream.  Order and names: kKernelNames in kernels.hip.
 enum KernelId {
   KN_COLUMNS,
+  KN_ORDER,
   KN_CAND_LANE,
   KN_CAND_WAVE,
   KN_LINKS,
@@ -188,7 +213,8 @@ struct Marks {
 };
 
 // ---- launch wrappers (kernels.hip)
-void launch_columns(const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s, const Marks& mk);
+void launch_columns(const DevGraph& g, const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s,
+                    const Marks& mk);
 void launch_candidates(const DevGraph& g, const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s,
                        const Marks& mk);
 void launch_links(const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s, const Marks& mk);
@@ -202,6 +228,8 @@ void launch_route(const DevGraph& g, const DevBatch& b, const DevParams& p, DevW
 void launch_segments(const DevGraph& g, const DevBatch& b, DevWork& w, DevOut& o, bool write, hipStream_t s,
                      const Marks& mk);
 void launch_report(const DevBatch& b, const DevReportCfg& rc, DevWork& w, DevOut& o, hipStream_t s, const Marks& mk);
+// spatial work order: tile counts, plan (group cuts), scatter of the columns
+void launch_order(const DevBatch& b, DevWork& w, hipStream_t s, const Marks& mk);
 // per-point bound of the segments / way ids a matched point can emit (scanned
 // into DevOut::seg_base)
 void launch_seg_bound(const DevBatch& b, DevWork& w, int64_t* ub, hipStream_t s, const Marks& mk);

@@ -15,6 +15,9 @@
 // 256 MB Infinity Cache after first touch.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cstdlib>
+
 #include <hipcub/hipcub.hpp>
 
 #include "kernels.h"
@@ -120,6 +123,114 @@ __device__ __forceinline__ int wave_incl_scan(int v, int lane) {
   return v;
 }
 
+// ============================================================== spatial work order
+__device__ __forceinline__ int hilbert_d(int x, int y) {
+  int d = 0;
+  for (int sft = ORDER_SIDE / 2; sft > 0; sft >>= 1) {
+    const int rx = (x & sft) > 0;
+    const int ry = (y & sft) > 0;
+    d += sft * sft * ((3 * rx) ^ ry);
+    if (ry == 0) {
+      if (rx == 1) {
+        x = ORDER_SIDE - 1 - x;
+        y = ORDER_SIDE - 1 - y;
+      }
+      const int tmp = x;
+      x = y;
+      y = tmp;
+    }
+  }
+  return d;
+}
+
+__device__ __forceinline__ int tile_of(const DevGraph& g, float lat, float lon) {
+  int ty = (int)((lat - g.bb_lat0) * g.bb_inv_h);
+  int tx = (int)((lon - g.bb_lon0) * g.bb_inv_w);
+  ty = ty < 0 ? 0 : (ty >= ORDER_SIDE ? ORDER_SIDE - 1 : ty);
+  tx = tx < 0 ? 0 : (tx >= ORDER_SIDE ? ORDER_SIDE - 1 : tx);
+  return hilbert_d(tx, ty);
+}
+
+// Wave-aggregated atomicAdd(&ctr[key], 1): one atomic per distinct key in
+// the wave; returns this lane's slot (consecutive points of a trace usually
+// share a tile, so a wave makes one to three atomics).  All 64 lanes call it.
+__device__ __forceinline__ int wave_agg_slot(int32_t* ctr, int key, bool active) {
+  const int lane = threadIdx.x & 63;
+  unsigned long long pending = __ballot(active);
+  int pos = 0;
+  while (pending) {
+    const int leader = __ffsll((long long)pending) - 1;
+    const int k = __shfl(key, leader, 64);
+    const unsigned long long grp = __ballot(((pending >> lane) & 1ull) && key == k);
+    int base = 0;
+    if (lane == leader) base = atomicAdd(&ctr[k], (int)__popcll(grp));
+    base = __shfl(base, leader, 64);
+    if ((grp >> lane) & 1ull) pos = base + (int)__popcll(grp & ((1ull << lane) - 1ull));
+    pending &= ~grp;
+  }
+  return pos;
+}
+
+// one block: exclusive scan of the tile counts (Hilbert order), cursors, and
+// the 8 group cuts at the tile boundaries nearest k/8 of the columns
+__global__ __launch_bounds__(1024) void k_order_plan(const int32_t* tile_cnt, int32_t* cursor, int32_t* grp) {
+  __shared__ int32_t part[1024];
+  __shared__ int32_t cut[ORDER_GROUPS + 1];
+  constexpr int PER = ORDER_TILES / 1024;
+  const int tid = threadIdx.x;
+  int32_t v[PER], sum = 0;
+  for (int k = 0; k < PER; ++k) {
+    v[k] = tile_cnt[tid * PER + k];
+    sum += v[k];
+  }
+  part[tid] = sum;
+  if (tid <= ORDER_GROUPS) cut[tid] = 0x7fffffff;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {
+    const int32_t x = tid >= o ? part[tid - o] : 0;
+    __syncthreads();
+    part[tid] += x;
+    __syncthreads();
+  }
+  const int32_t total = part[1023];
+  int32_t run = part[tid] - sum;
+  // start of the tile before this thread's first one (-1 before tile 0)
+  int32_t prev_start = tid == 0 ? -1 : run - tile_cnt[tid * PER - 1];
+  for (int k = 0; k < PER; ++k) {
+    cursor[tid * PER + k] = run;
+    // group gi starts at the first tile whose start reaches gi/8 of the
+    // columns: exactly one tile sees prev_start < want <= run
+    for (int gi = 1; gi < ORDER_GROUPS; ++gi) {
+      const int64_t want = ((int64_t)total * gi + ORDER_GROUPS - 1) / ORDER_GROUPS;
+      if (run >= want && prev_start < want) cut[gi] = run;
+    }
+    prev_start = run;
+    run += v[k];
+  }
+  __syncthreads();
+  if (tid == 0) {
+    grp[0] = 0;
+    int32_t prev = 0;
+    for (int gi = 1; gi < ORDER_GROUPS; ++gi) {
+      const int32_t c = cut[gi] > total ? total : cut[gi];
+      prev = c > prev ? c : prev;
+      grp[gi] = prev;
+    }
+    grp[ORDER_GROUPS] = total;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_order_scatter(DevBatch b, DevWork w, const uint16_t* tile, int32_t* cursor,
+                                                       int32_t* item) {
+  for (int64_t p0 = (int64_t)blockIdx.x * 256; p0 < b.n_points; p0 += (int64_t)gridDim.x * 256) {
+    const int64_t p = p0 + threadIdx.x;
+    const bool col = p < b.n_points && w.is_col[p];
+    const int t = col ? (int)tile[p] : 0;
+    const int pos = wave_agg_slot(cursor, t, col);
+    if (col) item[pos] = (int32_t)p;
+  }
+}
+
 // ============================================================== K1 columns
 // One wavefront per trace: lanes stage the trace's coordinates in LDS and
 // compute the distance of every point to its predecessor in parallel; lane 0
@@ -127,7 +238,7 @@ __device__ __forceinline__ int wave_incl_scan(int v, int lane) {
 // interpolation_distance from the last column) out of LDS, recomputing the
 // distance only where the last column is not the immediate predecessor.
 constexpr int COL_PTS = 512;
-__global__ __launch_bounds__(TB) void k_columns(DevBatch b, DevParams P, DevWork w) {
+__global__ __launch_bounds__(TB) void k_columns(DevGraph g, DevBatch b, DevParams P, DevWork w) {
   __shared__ float sLat[COL_PTS], sLon[COL_PTS], sGc[COL_PTS];
   __shared__ int32_t sPrev[COL_PTS];
   __shared__ uint8_t sCol[COL_PTS];
@@ -150,10 +261,21 @@ __global__ __launch_bounds__(TB) void k_columns(DevBatch b, DevParams P, DevWork
           if (col) {
             last = p;
             ++ncols;
+            if (w.ord.tile_cnt) {  // spatial order tile (serial here: long traces are rare)
+              const int tl = tile_of(g, b.lat[p], b.lon[p]);
+              w.ord.tile[p] = (uint16_t)tl;
+              atomicAdd(&w.ord.tile_cnt[tl], 1);
+            }
           }
         }
       }
-      for (int64_t p = a + lane; p < e; p += TB) w.pt_trace[p] = t;
+      for (int64_t p = a + lane; p < e; p += TB) {
+        w.pt_trace[p] = t;
+        w.ncand[p] = 0;
+        w.route_dist[p] = 0.0f;
+        w.path_len[p] = 0;
+        w.path_off[p] = 0;
+      }
     } else {
       for (int pl = lane; pl < n; pl += TB) {
         sLat[pl] = b.lat[a + pl];
@@ -179,12 +301,27 @@ __global__ __launch_bounds__(TB) void k_columns(DevBatch b, DevParams P, DevWork
         }
       }
       __syncthreads();
-      for (int pl = lane; pl < n; pl += TB) {
-        const int64_t p = a + pl;
-        w.pt_trace[p] = t;
-        w.is_col[p] = sCol[pl];
-        w.gc[p] = sGc[pl];
-        w.prevc[p] = sPrev[pl];
+      for (int c0 = 0; c0 < n; c0 += TB) {
+        const int pl = c0 + lane;
+        const bool in = pl < n;
+        const bool col = in && sCol[pl];
+        if (in) {
+          const int64_t p = a + pl;
+          w.pt_trace[p] = t;
+          w.is_col[p] = sCol[pl];
+          w.gc[p] = sGc[pl];
+          w.prevc[p] = sPrev[pl];
+          // later stages write these for columns only (spatial work order)
+          w.ncand[p] = 0;
+          w.route_dist[p] = 0.0f;
+          w.path_len[p] = 0;
+          w.path_off[p] = 0;
+        }
+        if (w.ord.tile_cnt) {  // spatial order: this column's tile, counted per wave
+          const int tl = col ? tile_of(g, sLat[pl], sLon[pl]) : 0;
+          if (col) w.ord.tile[a + pl] = (uint16_t)tl;
+          (void)wave_agg_slot(w.ord.tile_cnt, tl, col);
+        }
       }
       __syncthreads();
     }
@@ -196,6 +333,30 @@ __global__ __launch_bounds__(TB) void k_columns(DevBatch b, DevParams P, DevWork
       }
     }
   }
+}
+
+// The items a block walks: the spatial order's group blockIdx % 8 (lanes
+// or waves over it), or every point in natural order.  per_block = items
+// per block per step (threads for lane kernels, 1 for wave kernels).
+struct ItemRange {
+  int64_t i0, i1, stride;
+  bool ordered;
+};
+__device__ __forceinline__ ItemRange item_range(const DevWork& w, const DevBatch& b, bool ordered, int per_block) {
+  ItemRange r;
+  r.ordered = ordered;
+  const int tid = per_block > 1 ? (int)threadIdx.x : 0;
+  if (ordered) {
+    const int grp = blockIdx.x % ORDER_GROUPS;
+    r.i0 = w.ord.grp[grp] + (int64_t)(blockIdx.x / ORDER_GROUPS) * per_block + tid;
+    r.i1 = w.ord.grp[grp + 1];
+    r.stride = (int64_t)(gridDim.x / ORDER_GROUPS) * per_block;
+  } else {
+    r.i0 = (int64_t)blockIdx.x * per_block + tid;
+    r.i1 = b.n_points;
+    r.stride = (int64_t)gridDim.x * per_block;
+  }
+  return r;
 }
 
 // ============================================================== K2 candidates
@@ -226,11 +387,10 @@ __global__ __launch_bounds__(CAND_TB) void k_cand_lane(DevGraph g, DevBatch b, D
   float* Q = sQ + threadIdx.x;
   constexpr int S = CAND_TB;
   unsigned long long c_cells = 0, c_ent = 0, c_cand = 0;
-  for (int64_t p = (int64_t)blockIdx.x * CAND_TB + threadIdx.x; p < b.n_points; p += (int64_t)gridDim.x * CAND_TB) {
-    if (!w.is_col[p]) {
-      w.ncand[p] = 0;
-      continue;
-    }
+  const ItemRange R = item_range(w, b, (P.order_mask & ORDER_CAND) != 0, CAND_TB);
+  for (int64_t it = R.i0; it < R.i1; it += R.stride) {
+    const int64_t p = R.ordered ? (int64_t)w.ord.item[it] : it;
+    if (!R.ordered && !w.is_col[p]) continue;
     const float lat = b.lat[p], lon = b.lon[p];
     const float r = probe_radius(P, b.acc[p]);
     const float r2 = r * r;
@@ -1015,14 +1175,17 @@ __global__ void k_row_pack(const int32_t* row_cnt, const int64_t* row_off, IdxRo
 // then column q, then edges, then rows) so a column costs ~5 memory round
 // trips.  Columns the index cannot answer (bound > rmax, or a source row
 // incomplete) go to the search tiers.
-__global__ __launch_bounds__(TB) void k_trans_index(DevGraph g, DevBatch b, DevParams P, DevWork w) {
+__global__ __launch_bounds__(TB, 8) void k_trans_index(DevGraph g, DevBatch b, DevParams P, DevWork w) {
   __shared__ int32_t ep[KMAX], vp[KMAX], eq[KMAX];
   __shared__ float op[KMAX], oq[KMAX], sq[KMAX];
   __shared__ IdxRow rq[KMAX];
   const int lane = threadIdx.x;
   const DevIndex& X = w.idx;
   unsigned long long c_search = 0, c_settled = 0, c_relaxed = 0, c_trans = 0;
-  for (int64_t p = blockIdx.x; p < b.n_points; p += gridDim.x) {
+  const ItemRange IR = item_range(w, b, (P.order_mask & ORDER_TRANS) != 0, 1);
+  for (int64_t it = IR.i0; it < IR.i1; it += IR.stride) {
+    // wave-uniform: keep p (and every load indexed by it) scalar
+    const int64_t p = IR.ordered ? (int64_t)__builtin_amdgcn_readfirstlane(w.ord.item[it]) : it;
     // by p
     const int32_t q = w.col_prev[p];
     const int Kp = w.ncand[p];
@@ -1142,8 +1305,12 @@ __global__ __launch_bounds__(TB) void k_trans_index(DevGraph g, DevBatch b, DevP
 __global__ __launch_bounds__(256) void k_route_index(DevGraph g, DevBatch b, DevParams P, DevWork w) {
   const DevIndex& X = w.idx;
   unsigned long long c_search = 0, c_settled = 0, c_relaxed = 0, c_edges = 0;
-  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < b.n_points;
-       p += (int64_t)gridDim.x * blockDim.x) {
+  const ItemRange R = item_range(w, b, (P.order_mask & ORDER_ROUTE) != 0, 256);
+  for (int64_t it = R.i0; it < R.i1; it += R.stride) {
+    const int64_t p = R.ordered ? (int64_t)w.ord.item[it] : it;
+    if (!R.ordered && !w.is_col[p]) continue;
+    // (non-column points keep the zeros K1 wrote; a re-run after a path-pool
+    // overflow rewrites every column)
     w.route_dist[p] = 0.0f;
     w.path_len[p] = 0;
     w.path_off[p] = 0;
@@ -2227,11 +2394,12 @@ int grid_for(int64_t n, int per_block, int cap) {
 
 // ============================================================== launchers
 constexpr int WAVE_GRID_CAP = 256 * 64;  // grid-stride cap for wave kernels
+constexpr int TRANS_GRID_CAP = 65536;  // k_trans_index waves (one per column, grid-striding beyond)
 
 }  // namespace
 
 const char* const kKernelNames[KN_COUNT] = {
-    "k_columns",       "k_cand_lane",    "k_candidates",     "k_links",         "scan_trans_off",  "k_trans_index",
+    "k_columns",       "spatial_order",  "k_cand_lane",    "k_candidates",     "k_links",         "scan_trans_off",  "k_trans_index",
     "k_trans_lane",    "k_transitions",  "k_transitions_big", "k_viterbi",      "k_route_index",   "k_route_lane",
     "k_route",         "k_route_big",    "k_seg_bound",      "scan_seg_bound",  "k_segments",       "k_report"};
 
@@ -2252,14 +2420,36 @@ constexpr int LANE_GRID = 2048;
     mk.end(k, s);        \
   } while (0)
 
-void launch_columns(const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s, const Marks& mk) {
-  TIMED(KN_COLUMNS, hipLaunchKernelGGL(k_columns, dim3(grid_for(b.n_traces, 1, WAVE_GRID_CAP)), dim3(TB), 0, s, b,
-                                       p, w));
+void launch_columns(const DevGraph& g, const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s,
+                    const Marks& mk) {
+  if (w.ord.tile_cnt) (void)hipMemsetAsync(w.ord.tile_cnt, 0, ORDER_TILES * 4, s);
+  TIMED(KN_COLUMNS, hipLaunchKernelGGL(k_columns, dim3(grid_for(b.n_traces, 1, WAVE_GRID_CAP)), dim3(TB), 0, s, g,
+                                       b, p, w));
 }
+// grid for a kernel over the spatial order: a multiple of ORDER_GROUPS, with
+// 25 % headroom per group over an even split
+static int order_grid(int64_t n, int per_block, int cap) {
+  const int64_t per_group = (n + ORDER_GROUPS - 1) / ORDER_GROUPS;
+  int64_t gb = (per_group + per_group / 4 + per_block - 1) / per_block;
+  if (gb < 1) gb = 1;
+  int64_t gtot = gb * ORDER_GROUPS;
+  if (gtot > cap) gtot = cap / ORDER_GROUPS * ORDER_GROUPS;
+  return (int)gtot;
+}
+
+void launch_order(const DevBatch& b, DevWork& w, hipStream_t s, const Marks& mk) {
+  // (the tile counts were made by K1)
+  mk.begin(KN_ORDER, s);
+  hipLaunchKernelGGL(k_order_plan, dim3(1), dim3(1024), 0, s, w.ord.tile_cnt, w.ord.cursor, w.ord.grp);
+  hipLaunchKernelGGL(k_order_scatter, dim3(grid_for(b.n_points, 256, 8192)), dim3(256), 0, s, b, w, w.ord.tile,
+                     w.ord.cursor, w.ord.item);
+  mk.end(KN_ORDER, s);
+}
+
 void launch_candidates(const DevGraph& g, const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s,
                        const Marks& mk) {
-  TIMED(KN_CAND_LANE, hipLaunchKernelGGL(k_cand_lane, dim3(grid_for(b.n_points, CAND_TB, 1 << 30)), dim3(CAND_TB), 0,
-                                         s, g, b, p, w));
+  TIMED(KN_CAND_LANE, hipLaunchKernelGGL(k_cand_lane, dim3(order_grid(b.n_points, CAND_TB, 1 << 30)), dim3(CAND_TB),
+                                         0, s, g, b, p, w));
   TIMED(KN_CAND_WAVE, hipLaunchKernelGGL(k_candidates, dim3(4096), dim3(TB), 0, s, g, b, p, w));
 }
 void launch_links(const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s, const Marks& mk) {
@@ -2268,8 +2458,13 @@ void launch_links(const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t
 }
 void launch_transitions(const DevGraph& g, const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s,
                         const Marks& mk) {
-  TIMED(KN_TRANS_INDEX, hipLaunchKernelGGL(k_trans_index, dim3(grid_for(b.n_points, 1, WAVE_GRID_CAP)), dim3(TB), 0,
-                                           s, g, b, p, w));
+  // many more waves than fit at once (each column is a few dependent
+  // round trips): measured 0.78 ms at 16K waves, 0.67 ms at 64K; a grid of
+  // one resident round was slowest (0.92 ms, partial rounds at 7 waves/SIMD)
+  static const char* genv = std::getenv("OTM_TRANS_GRID");
+  const int grid = genv ? std::max(ORDER_GROUPS, std::atoi(genv) / ORDER_GROUPS * ORDER_GROUPS)
+                        : order_grid(b.n_points, 1, TRANS_GRID_CAP);
+  TIMED(KN_TRANS_INDEX, hipLaunchKernelGGL(k_trans_index, dim3(grid), dim3(TB), 0, s, g, b, p, w));
   TIMED(KN_TRANS_LANE, hipLaunchKernelGGL(k_trans_lane<LANE_CAP_TRANS>, dim3(LANE_GRID), dim3(LANE_TB), 0, s, g, b,
                                           p, w));
   TIMED(KN_TRANS_WAVE, hipLaunchKernelGGL(k_transitions<false>, dim3(SPILL_GRID), dim3(TB), 0, s, g, b, p, w, 0));
@@ -2281,8 +2476,8 @@ void launch_viterbi(const DevBatch& b, DevWork& w, hipStream_t s, const Marks& m
 }
 void launch_route(const DevGraph& g, const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s,
                   const Marks& mk) {
-  TIMED(KN_ROUTE_INDEX, hipLaunchKernelGGL(k_route_index, dim3(grid_for(b.n_points, 256, 1 << 30)), dim3(256), 0, s,
-                                           g, b, p, w));
+  TIMED(KN_ROUTE_INDEX, hipLaunchKernelGGL(k_route_index, dim3(order_grid(b.n_points, 256, 1 << 30)), dim3(256), 0,
+                                           s, g, b, p, w));
   TIMED(KN_ROUTE_LANE, hipLaunchKernelGGL(k_route_lane<LANE_CAP>, dim3(LANE_GRID), dim3(LANE_TB), 0, s, g, b, p, w));
   TIMED(KN_ROUTE_WAVE, hipLaunchKernelGGL(k_route<false>, dim3(SPILL_GRID), dim3(TB), 0, s, g, b, p, w, 0));
   TIMED(KN_ROUTE_GLOBAL, hipLaunchKernelGGL(k_route<true>, dim3(BIG_SLOTS), dim3(TB), 0, s, g, b, p, w, 0));

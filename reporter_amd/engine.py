@@ -189,7 +189,7 @@ class Engine(object):
 
     def kernel_ms(self):
         """Per-kernel times (ms) of the last timed match_device call, by kernel name."""
-        n = 18
+        n = 19
         ms = (C.c_float * n)()
         _check(lib().otm_get_kernel_ms(self.h, ms, n))
         return {lib().otm_kernel_name(k).decode(): ms[k] for k in range(n)}

@@ -1300,6 +1300,145 @@ __global__ __launch_bounds__(TB, 8) void k_trans_index(DevGraph g, DevBatch b, D
   }
 }
 
+// K4 index tier, sub-wave form: S lanes per column, TB / S columns in flight
+// per wave.  Same per-pair work as k_trans_index; a column is a chain of ~5
+// dependent round trips (point -> previous column -> edges -> rows ->
+// slots), so several columns per wave multiply the misses in flight at the
+// same occupancy.  Columns with more pairs than S loop within their group.
+template <int S>
+__global__ __launch_bounds__(TB, 8) void k_trans_sub(DevGraph g, DevBatch b, DevParams P, DevWork w) {
+  constexpr int NS = TB / S;
+  __shared__ int32_t ep[NS][KMAX], vp[NS][KMAX], eq[NS][KMAX];
+  __shared__ float op[NS][KMAX], oq[NS][KMAX], sq[NS][KMAX];
+  __shared__ IdxRow rq[NS][KMAX];
+  const int lane = threadIdx.x, sg = lane / S, sl = lane % S;
+  const unsigned long long smask = (S == 64 ? ~0ull : ((1ull << S) - 1ull)) << (sg * S);
+  const DevIndex& X = w.idx;
+  unsigned long long c_search = 0, c_settled = 0, c_relaxed = 0, c_trans = 0;
+  const bool ordered = (P.order_mask & ORDER_TRANS) != 0;
+  int64_t base, end, stride;
+  if (ordered) {
+    const int grp = blockIdx.x % ORDER_GROUPS;
+    base = w.ord.grp[grp] + (int64_t)(blockIdx.x / ORDER_GROUPS) * NS;
+    end = w.ord.grp[grp + 1];
+    stride = (int64_t)(gridDim.x / ORDER_GROUPS) * NS;
+  } else {
+    base = (int64_t)blockIdx.x * NS;
+    end = b.n_points;
+    stride = (int64_t)gridDim.x * NS;
+  }
+  for (; base < end; base += stride) {
+    const int64_t it = base + sg;
+    bool act = it < end;
+    int64_t p = 0;
+    if (act) p = ordered ? (int64_t)w.ord.item[it] : it;
+    const int32_t q = act ? w.col_prev[p] : -1;
+    act = act && q >= 0;
+    int Kp = 0, Kq = 0;
+    float gcv = 0.0f;
+    int64_t toff = 0;
+    if (act) {
+      Kp = w.ncand[p];
+      gcv = w.gc[p];
+      toff = w.trans_off[p];
+      Kq = w.ncand[q];
+    }
+    const float bound = P.factor * gcv;
+    const bool idx_ok = X.rmax > 0.0f && bound <= X.rmax;
+    bool bad = act && !idx_ok;
+    // candidates of p (targets) and of q (sources), then edges, then rows
+    for (int k = sl; k < KMAX; k += S) {
+      if (act && k < Kp) {
+        const int32_t e = w.cand_edge[p * KMAX + k];
+        ep[sg][k] = e;
+        op[sg][k] = w.cand_off[p * KMAX + k];
+        vp[sg][k] = g.e_from[e];
+      }
+      if (act && k < Kq) {
+        const int32_t e = w.cand_edge[(int64_t)q * KMAX + k];
+        const float o = w.cand_off[(int64_t)q * KMAX + k];
+        eq[sg][k] = e;
+        oq[sg][k] = o;
+        sq[sg][k] = g.e_len[e] - o;
+        if (idx_ok) {
+          const IdxRow R = X.row[g.e_to[e]];
+          rq[sg][k] = R;
+          bad = bad || R.cnt < 0;
+        }
+      }
+    }
+    const bool spill = (__ballot(bad) & smask) != 0ull;
+    if (spill && act && sl == 0) {
+      const int slot = atomicAdd(&w.counters_i32[4], 1);
+      w.overflow_list0[slot] = (int32_t)p;
+    }
+    act = act && !spill;
+    __syncthreads();
+    if (act) {
+      float* Tm = w.trans + toff;
+      unsigned long long ntr = 0;
+      for (int idx = sl; idx < Kq * Kp; idx += S) {
+        const int i = idx / Kp, j = idx - (idx / Kp) * Kp;
+        float r = 0.0f;
+        bool ok = true;
+        if (ep[sg][j] == eq[sg][i] && op[sg][j] >= oq[sg][i]) {
+          r = op[sg][j] - oq[sg][i];
+        } else {
+          float D;
+          if (idx_find(X, rq[sg][i], (uint32_t)vp[sg][j], D) >= 0) {
+            const float sd = sq[sg][i] + D;
+            r = sd + op[sg][j];
+          } else {
+            ok = false;
+          }
+        }
+        float cost = INFINITY;
+        if (ok && r <= bound) {
+          const float diff = fabsf(r - gcv);
+          cost = diff / P.beta;
+          ++ntr;
+        }
+        Tm[i * Kp + j] = cost;
+      }
+      if (w.ctr) {
+        // algorithmic counts of the equivalent searches (per-lane partials,
+        // summed over the wave at the end): per distinct source, the row
+        // entries with D <= bound and their out-degrees
+        for (int i = 0; i < Kq; ++i) {
+          bool first = true;
+          for (int k = 0; k < i; ++k) first = first && rq[sg][k].off != rq[sg][i].off;
+          if (!first) continue;
+          const IdxRow R = rq[sg][i];
+          for (int64_t k = sl; k <= (int64_t)R.mask && R.cnt > 0; k += S) {
+            const uint2 slt = X.slot[R.off + k];
+            if (slt.x != EMPTY && bitsf(slt.y) <= bound) {
+              ++c_settled;
+              c_relaxed += (unsigned long long)(g.out_off[slt.x + 1] - g.out_off[slt.x]);
+            }
+          }
+          if (sl == 0) ++c_search;
+        }
+        c_trans += ntr;
+      }
+    }
+    __syncthreads();
+  }
+  if (w.ctr) {
+    for (int sh = 32; sh > 0; sh >>= 1) {
+      c_search += __shfl_xor(c_search, sh, 64);
+      c_settled += __shfl_xor(c_settled, sh, 64);
+      c_relaxed += __shfl_xor(c_relaxed, sh, 64);
+      c_trans += __shfl_xor(c_trans, sh, 64);
+    }
+    if (lane == 0) {
+      cadd(&w.ctr->searches, c_search);
+      cadd(&w.ctr->nodes_settled, c_settled);
+      cadd(&w.ctr->edges_relaxed, c_relaxed);
+      cadd(&w.ctr->transitions, c_trans);
+    }
+  }
+}
+
 // K6 index tier: one lane per matched step; the path is read back from the
 // index row of the source node (predecessor edges), one table probe per edge.
 __global__ __launch_bounds__(256) void k_route_index(DevGraph g, DevBatch b, DevParams P, DevWork w) {
@@ -2462,9 +2601,22 @@ void launch_transitions(const DevGraph& g, const DevBatch& b, const DevParams& p
   // round trips): measured 0.78 ms at 16K waves, 0.67 ms at 64K; a grid of
   // one resident round was slowest (0.92 ms, partial rounds at 7 waves/SIMD)
   static const char* genv = std::getenv("OTM_TRANS_GRID");
+  static const int sub = [] {
+    const char* e = std::getenv("OTM_TRANS_SUB");
+    const int v = e ? std::atoi(e) : 16;
+    return v == 8 || v == 16 || v == 32 ? v : 64;
+  }();
+  const int per = TB / sub;  // columns per wave step
   const int grid = genv ? std::max(ORDER_GROUPS, std::atoi(genv) / ORDER_GROUPS * ORDER_GROUPS)
-                        : order_grid(b.n_points, 1, TRANS_GRID_CAP);
-  TIMED(KN_TRANS_INDEX, hipLaunchKernelGGL(k_trans_index, dim3(grid), dim3(TB), 0, s, g, b, p, w));
+                        : order_grid((b.n_points + per - 1) / per, 1, TRANS_GRID_CAP);
+  if (sub == 32)
+    TIMED(KN_TRANS_INDEX, hipLaunchKernelGGL(k_trans_sub<32>, dim3(grid), dim3(TB), 0, s, g, b, p, w));
+  else if (sub == 16)
+    TIMED(KN_TRANS_INDEX, hipLaunchKernelGGL(k_trans_sub<16>, dim3(grid), dim3(TB), 0, s, g, b, p, w));
+  else if (sub == 8)
+    TIMED(KN_TRANS_INDEX, hipLaunchKernelGGL(k_trans_sub<8>, dim3(grid), dim3(TB), 0, s, g, b, p, w));
+  else
+    TIMED(KN_TRANS_INDEX, hipLaunchKernelGGL(k_trans_index, dim3(grid), dim3(TB), 0, s, g, b, p, w));
   TIMED(KN_TRANS_LANE, hipLaunchKernelGGL(k_trans_lane<LANE_CAP_TRANS>, dim3(LANE_GRID), dim3(LANE_TB), 0, s, g, b,
                                           p, w));
   TIMED(KN_TRANS_WAVE, hipLaunchKernelGGL(k_transitions<false>, dim3(SPILL_GRID), dim3(TB), 0, s, g, b, p, w, 0));

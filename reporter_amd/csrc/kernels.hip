@@ -1830,8 +1830,7 @@ __global__ __launch_bounds__(TB) void k_viterbi(DevBatch b, DevWork w) {
     bool open = false;
     int last = -1;
     int win_end = 0, wt0 = 0, we0 = 0;
-    auto backtrack = [&](int endl) {
-      const int Ke = sKc[endl];
+    auto backtrack = [&](int endl, int Ke) {
       float bv;
       int bi;
       wave_argmin(lane < Ke ? prev : INFINITY, lane, bv, bi);
@@ -1847,123 +1846,138 @@ __global__ __launch_bounds__(TB) void k_viterbi(DevBatch b, DevWork w) {
         }
       }
     };
-    for (int pl = 0; pl < n; ++pl) {
-      const int Kp = sKc[pl];
-      if (Kp < 0) continue;
-      if (Kp == 0) {
-        if (open) backtrack(last);
-        open = false;
-        continue;
-      }
-      if (pl >= win_end) {
-        // next window: the longest run of points from pl whose transitions
-        // and emissions fit (one point always does)
-        __syncthreads();
-        wt0 = sToff[pl];
-        we0 = sEoff[pl];
-        int lo = pl + 1, hi = n;
-        while (lo < hi) {
-          const int mid = (lo + hi + 1) >> 1;
-          if (sToff[mid] - wt0 <= VIT_TW && sEoff[mid] - we0 <= VIT_EW) lo = mid;
-          else hi = mid - 1;
+    // The forward pass walks the points in chunks of 64 whose metadata sits
+    // in registers (lane k holds point c0 + k) and is read with readlane: the
+    // per-column chain keeps one LDS round trip (emission + transition reads,
+    // issued together) instead of five dependent ones.
+    int lastK = 0;  // candidates of column `last`
+    for (int c0 = 0; c0 < n; c0 += TB) {
+      const int pk = c0 + lane;
+      const int r_kc = pk < n ? (int)sKc[pk] : -1;
+      const int r_eo = pk < n ? (int)sEoff[pk] : 0;
+      const int r_cp = pk < n ? (int)sCprev[pk] : -1;
+      const int r_to = pk < n ? sToff[pk] : 0;
+      const int cend = n - c0 < TB ? n - c0 : TB;
+      for (int k = 0; k < cend; ++k) {
+        const int pl = c0 + k;
+        const int Kp = __builtin_amdgcn_readlane(r_kc, k);
+        if (Kp < 0) continue;
+        if (Kp == 0) {
+          if (open) backtrack(last, lastK);
+          open = false;
+          continue;
         }
-        win_end = lo;
-        const int nt = sToff[win_end] - wt0, ne = sEoff[win_end] - we0;
-        for (int f0 = 0; f0 < nt; f0 += 8 * TB) {
-          float v[8];
-#pragma unroll
-          for (int u = 0; u < 8; ++u) {
-            const int f = f0 + u * TB + lane;
-            v[u] = f < nt ? w.trans[t0 + wt0 + f] : 0.0f;
+        if (pl >= win_end) {
+          // next window: the longest run of points from pl whose transitions
+          // and emissions fit (one point always does)
+          __syncthreads();
+          wt0 = sToff[pl];
+          we0 = sEoff[pl];
+          int lo = pl + 1, hi = n;
+          while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (sToff[mid] - wt0 <= VIT_TW && sEoff[mid] - we0 <= VIT_EW) lo = mid;
+            else hi = mid - 1;
           }
+          win_end = lo;
+          const int nt = sToff[win_end] - wt0, ne = sEoff[win_end] - we0;
+          for (int f0 = 0; f0 < nt; f0 += 8 * TB) {
+            float v[8];
 #pragma unroll
-          for (int u = 0; u < 8; ++u) {
-            const int f = f0 + u * TB + lane;
-            if (f < nt) sT[f] = v[u];
-          }
-        }
-        for (int f0 = 0; f0 < ne; f0 += 4 * TB) {
-          float v[4];
+            for (int u = 0; u < 8; ++u) {
+              const int f = f0 + u * TB + lane;
+              v[u] = f < nt ? w.trans[t0 + wt0 + f] : 0.0f;
+            }
 #pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const int f = f0 + u * TB + lane;
-            v[u] = 0.0f;
-            if (f < ne) {
-              // point holding window candidate f: last q with sEoff[q] <= we0 + f
-              int l2 = pl, h2 = win_end - 1;
-              while (l2 < h2) {
-                const int mid = (l2 + h2 + 1) >> 1;
-                if (sEoff[mid] <= we0 + f) l2 = mid;
-                else h2 = mid - 1;
-              }
-              v[u] = w.cand_emis[(a + l2) * KMAX + (we0 + f - sEoff[l2])];
+            for (int u = 0; u < 8; ++u) {
+              const int f = f0 + u * TB + lane;
+              if (f < nt) sT[f] = v[u];
             }
           }
+          for (int f0 = 0; f0 < ne; f0 += 4 * TB) {
+            float v[4];
 #pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const int f = f0 + u * TB + lane;
-            if (f < ne) sEm[f] = v[u];
+            for (int u = 0; u < 4; ++u) {
+              const int f = f0 + u * TB + lane;
+              v[u] = 0.0f;
+              if (f < ne) {
+                // point holding window candidate f: last q with sEoff[q] <= we0 + f
+                int l2 = pl, h2 = win_end - 1;
+                while (l2 < h2) {
+                  const int mid = (l2 + h2 + 1) >> 1;
+                  if (sEoff[mid] <= we0 + f) l2 = mid;
+                  else h2 = mid - 1;
+                }
+                v[u] = w.cand_emis[(a + l2) * KMAX + (we0 + f - sEoff[l2])];
+              }
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              const int f = f0 + u * TB + lane;
+              if (f < ne) sEm[f] = v[u];
+            }
           }
+          __syncthreads();
         }
-        __syncthreads();
-      }
-      const int eo = sEoff[pl];
-      const float em = sEm[eo - we0 + (lane < Kp ? lane : 0)];
-      bool started = false;
-      float cur = INFINITY;
-      if (open && sCprev[pl] == last) {
-        const int Kq = sKc[last];
-        const float* Tm = sT + (sToff[pl] - wt0) + (lane < Kp ? lane : 0);
-        float best = INFINITY;
-        int bi = -1;
-        const int pbits = __float_as_int(prev);
-        int i = 0;
-        for (; i + 4 <= Kq; i += 4) {
-          // four independent LDS reads in flight; visited in i order
-          float tv[4], pv[4];
+        const int eo = __builtin_amdgcn_readlane(r_eo, k);
+        const float em = sEm[eo - we0 + (lane < Kp ? lane : 0)];
+        bool started = false;
+        float cur = INFINITY;
+        if (open && __builtin_amdgcn_readlane(r_cp, k) == last) {
+          const int Kq = lastK;
+          const float* Tm = sT + (__builtin_amdgcn_readlane(r_to, k) - wt0) + (lane < Kp ? lane : 0);
+          float best = INFINITY;
+          int bi = -1;
+          const int pbits = __float_as_int(prev);
+          int i = 0;
+          for (; i + 4 <= Kq; i += 4) {
+            // four independent LDS reads in flight; visited in i order
+            float tv[4], pv[4];
 #pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            tv[u] = Tm[(i + u) * Kp];
-            pv[u] = __int_as_float(__builtin_amdgcn_readlane(pbits, i + u));
+            for (int u = 0; u < 4; ++u) {
+              tv[u] = Tm[(i + u) * Kp];
+              pv[u] = __int_as_float(__builtin_amdgcn_readlane(pbits, i + u));
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              const float v = pv[u] + tv[u];
+              if (v < best) {
+                best = v;
+                bi = i + u;
+              }
+            }
           }
-#pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const float v = pv[u] + tv[u];
+          for (; i < Kq; ++i) {
+            const float v = __int_as_float(__builtin_amdgcn_readlane(pbits, i)) + Tm[i * Kp];
             if (v < best) {
               best = v;
-              bi = i + u;
+              bi = i;
             }
           }
-        }
-        for (; i < Kq; ++i) {
-          const float v = __int_as_float(__builtin_amdgcn_readlane(pbits, i)) + Tm[i * Kp];
-          if (v < best) {
-            best = v;
-            bi = i;
+          const bool alive = lane < Kp && bi >= 0;
+          if (lane < Kp) {
+            cur = alive ? best + em : INFINITY;
+            sBp[eo + lane] = alive ? (uint8_t)bi : (uint8_t)0xFF;
           }
+          if (__ballot(alive) == 0ull) {
+            backtrack(last, lastK);
+          } else {
+            started = true;
+          }
+        } else if (open) {
+          backtrack(last, lastK);
         }
-        const bool alive = lane < Kp && bi >= 0;
-        if (lane < Kp) {
-          cur = alive ? best + em : INFINITY;
-          sBp[eo + lane] = alive ? (uint8_t)bi : (uint8_t)0xFF;
+        if (!started) {
+          cur = lane < Kp ? em : INFINITY;
+          if (lane == 0) sCs[pl] = 1;
         }
-        if (__ballot(alive) == 0ull) {
-          backtrack(last);
-        } else {
-          started = true;
-        }
-      } else if (open) {
-        backtrack(last);
+        prev = cur;
+        open = true;
+        last = pl;
+        lastK = Kp;
       }
-      if (!started) {
-        cur = lane < Kp ? em : INFINITY;
-        if (lane == 0) sCs[pl] = 1;
-      }
-      prev = cur;
-      open = true;
-      last = pl;
     }
-    if (open) backtrack(last);
+    if (open) backtrack(last, lastK);
     __syncthreads();
     for (int pl = lane; pl < n; pl += TB) {
       w.state[a + pl] = sState[pl];

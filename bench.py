@@ -154,26 +154,33 @@ def main():
         step()
     torch.cuda.synchronize(dev)
 
-    # timed region: K steps between barriers; kernel spans from HIP events
-    eng.set_timing(True)
-    kern_tot = {}
+    # timed region: K steps between barriers, no per-kernel events inside
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t_start = time.perf_counter()
     for _ in range(args.steps):
         step()
-        for k, v in eng.kernel_ms().items():
-            kern_tot[k] = kern_tot.get(k, 0.0) + v
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t_start
-    eng.set_timing(False)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+
+    # kernel spans: the same K steps again with HIP events around every launch
+    # (on the launch stream); kept out of the timed region, whose throughput
+    # the ~40 event records per step would perturb
+    eng.set_timing(True)
+    kern_tot = {}
+    for _ in range(args.steps):
+        step()
+        for k, v in eng.kernel_ms().items():
+            kern_tot[k] = kern_tot.get(k, 0.0) + v
+    torch.cuda.synchronize(dev)
+    eng.set_timing(False)
     kern_avg = {k: v / args.steps for k, v in kern_tot.items()}
     total_points = P * world * args.steps
     value = total_points / elapsed

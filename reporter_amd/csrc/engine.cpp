@@ -5,6 +5,8 @@
 // holds the flattened graph in HBM and matches whole batches of traces.
 #include "engine.h"
 
+#include <algorithm>
+
 #include <cstring>
 
 namespace otm {
@@ -204,7 +206,7 @@ void engine_free(otm_engine* E) {
       &E->big_lab,       &E->big_inq,      &E->big_fr,         &E->o_traces,       &E->o_seg_cnt,  &E->o_way_cnt,
       &E->o_segments,    &E->o_seg_gidx,   &E->o_way_ids,      &E->o_reports,  &E->o_rep_cnt,  &E->seg_ub,
       &E->f_seg_off,     &E->f_way_off,    &E->f_rep_off,      &E->f_segs,     &E->f_ways,     &E->f_reps,
-      &E->ord_tile,      &E->ord_cnt,      &E->ord_cursor,     &E->ord_grp,    &E->ord_item};
+      &E->abort_flag,    &E->ord_tile,      &E->ord_cnt,      &E->ord_cursor,     &E->ord_grp,    &E->ord_item};
   for (auto* b : bufs) {
     if (b->p) (void)hipFree(b->p);
     b->p = nullptr;
@@ -229,8 +231,11 @@ static int ensure_big(otm_engine* E, std::string* err) {
   return OTM_OK;
 }
 
-int engine_match(otm_engine* E, const DevBatch& b, hipStream_t s, std::string* err) {
-  if (!s) s = E->stream;
+// One attempt at a batch, enqueued with no host synchronisation: buffers are
+// sized from capacities (transition matrices, path pool) that the kernels
+// check; an overflow sets w.abort, every later kernel returns at once, and
+// engine_match grows the capacity and runs the batch again.
+static int engine_match_once(otm_engine* E, const DevBatch& b, hipStream_t s, std::string* err) {
   const int64_t NP = b.n_points;
   const int32_t NT = b.n_traces;
   const size_t Pn = (size_t)NP + 1;
@@ -259,6 +264,8 @@ int engine_match(otm_engine* E, const DevBatch& b, hipStream_t s, std::string* e
   ENS(overflow_list2, Pn * 4);
   ENS(counters_i32, 64);
   ENS(snap, 192);
+  ENS(abort_flag, 16);
+  if (E->trans_cap == 0) E->trans_cap = (int64_t)Pn * 48 + 4096;
   ENS(o_traces, ((size_t)NT + 1) * sizeof(otm_trace_result));
   ENS(o_seg_cnt, ((size_t)NT + 1) * 4);
   ENS(o_way_cnt, ((size_t)NT + 1) * 4);
@@ -296,6 +303,8 @@ int engine_match(otm_engine* E, const DevBatch& b, hipStream_t s, std::string* e
   w.ctr = E->counting ? E->ctr : nullptr;
   if (E->counting) HIPCHK(hipMemsetAsync(E->ctr, 0, sizeof(DevCounters), s));
   HIPCHK(hipMemsetAsync(w.counters_i32, 0, 64, s));  // [5] = candidate spill count
+  w.abort = P<int32_t>(E->abort_flag);
+  HIPCHK(hipMemsetAsync(w.abort, 0, 4, s));
   Marks mk;
   mk.ev = E->timing ? E->kev : nullptr;
   ENS(ord_tile, Pn * 2);
@@ -322,13 +331,11 @@ int engine_match(otm_engine* E, const DevBatch& b, hipStream_t s, std::string* e
   mk.begin(KN_SCAN_TRANS, s);
   scan_i64(w.trans_off, NP, E->scan_tmp.p, E->scan_tmp.cap, s);
   mk.end(KN_SCAN_TRANS, s);
-  int64_t ttotal = 0;
-  HIPCHK(hipMemcpyAsync(&ttotal, w.trans_off + NP, 8, hipMemcpyDeviceToHost, s));
-  HIPCHK(hipMemsetAsync(w.counters_i32, 0, 64, s));
-  HIPCHK(hipStreamSynchronize(s));
-  E->last_trans = ttotal;
-  ENS(trans, ((size_t)ttotal + 1) * 4);
+  ENS(trans, ((size_t)E->trans_cap + 1) * 4);
   w.trans = P<float>(E->trans);
+  w.trans_cap = E->trans_cap;
+  launch_cap_check(b, w, s);
+  HIPCHK(hipMemsetAsync(w.counters_i32, 0, 64, s));
   if ((rc = ensure_big(E, err))) return rc;
   w.big_key = P<uint32_t>(E->big_key);
   w.big_lab = P<unsigned long long>(E->big_lab);
@@ -338,36 +345,15 @@ int engine_match(otm_engine* E, const DevBatch& b, hipStream_t s, std::string* e
   // spill snapshot B: columns per transition tier
   HIPCHK(hipMemcpyAsync(P<char>(E->snap) + 64, w.counters_i32, 64, hipMemcpyDeviceToDevice, s));
   launch_viterbi(b, w, s, mk);
-  // a path-pool overflow redoes the whole stage: restore the work counters
-  // so the redone searches are counted once
-  if (E->counting) HIPCHK(hipMemcpyAsync(E->ctr_save, E->ctr, sizeof(DevCounters), hipMemcpyDeviceToDevice, s));
-  int32_t cnt[3] = {0, 0, 0};
-  for (int attempt = 0; attempt < 4; ++attempt) {
-    if (E->counting && attempt > 0)
-      HIPCHK(hipMemcpyAsync(E->ctr, E->ctr_save, sizeof(DevCounters), hipMemcpyDeviceToDevice, s));
-    HIPCHK(hipMemsetAsync(w.counters_i32, 0, 64, s));
-    launch_route(E->g, b, E->dp, w, s, mk);
-    // spill snapshot C: steps per route tier (final attempt)
-    HIPCHK(hipMemcpyAsync(P<char>(E->snap) + 128, w.counters_i32, 64, hipMemcpyDeviceToDevice, s));
-    HIPCHK(hipMemcpyAsync(cnt, w.counters_i32, 12, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
-    if (!cnt[2]) break;
-    // path pool too small: grow to what was requested and redo the stage
-    E->pool_cap = (int32_t)((size_t)cnt[1] * 2 + 1024);
-    ENS(path_pool, (size_t)E->pool_cap * 4);
-    w.path_pool = P<int32_t>(E->path_pool);
-    w.pool_cap = E->pool_cap;
-    if (attempt == 3) {
-      *err = "route path pool could not be sized";
-      return OTM_EDEVICE;
-    }
-  }
+  HIPCHK(hipMemsetAsync(w.counters_i32, 0, 64, s));
+  launch_route(E->g, b, E->dp, w, s, mk);
+  // spill snapshot C: steps per route tier
+  HIPCHK(hipMemcpyAsync(P<char>(E->snap) + 128, w.counters_i32, 64, hipMemcpyDeviceToDevice, s));
 
   // Segments, way ids and reports in ONE walk per trace, each trace writing
-  // into a region sized by an upper bound (DevOut); the bound's total is known
-  // on the host without another sync: every matched point adds <= 2 + its path
-  // length, and the path lengths sum to the pool use read above.
-  const size_t cap = 2 * (size_t)NP + (size_t)cnt[1] + 1;
+  // into a region sized by an upper bound (DevOut): every matched point adds
+  // <= 2 + its path length, and the path lengths sum to at most the pool.
+  const size_t cap = 2 * (size_t)NP + (size_t)E->pool_cap + 1;
   if (cap >= (size_t)INT32_MAX) {
     *err = "batch too large for one launch (segment regions exceed 2^31)";
     return OTM_EINVAL;
@@ -402,9 +388,34 @@ int engine_match(otm_engine* E, const DevBatch& b, hipStream_t s, std::string* e
   E->last_P = NP;
   E->last_S = -1;  // known after compaction (engine_fetch)
   E->last_W = -1;
+#undef ENS
+  return OTM_OK;
+}
+
+int engine_match(otm_engine* E, const DevBatch& b, hipStream_t s, std::string* err) {
+  if (!s) s = E->stream;
+  const int64_t NP = b.n_points;
+  int rc;
+  for (int attempt = 0;; ++attempt) {
+    if ((rc = engine_match_once(E, b, s, err))) return rc;
+    // the one synchronisation of a batch: did every capacity hold?
+    int32_t ab = 0, cnt[3] = {0, 0, 0};
+    int64_t ttotal = 0;
+    HIPCHK(hipMemcpyAsync(&ab, E->abort_flag.p, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(&ttotal, P<int64_t>(E->trans_off) + NP, 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(cnt, E->counters_i32.p, 12, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    E->last_trans = ttotal;
+    if (!ab) break;
+    if (attempt == 3) {
+      *err = "batch capacities could not be sized";
+      return OTM_EDEVICE;
+    }
+    if (ttotal > E->trans_cap) E->trans_cap = ttotal + ttotal / 4 + 4096;
+    if (cnt[2]) E->pool_cap = (int32_t)std::min<size_t>((size_t)cnt[1] * 2 + 1024, (size_t)INT32_MAX / 2);
+  }
   if (E->timing) {
-    // kernel-only spans on the launch stream (host syncs between stages
-    // excluded; the route stage's final attempt).  Stages are sums of their
+    // kernel-only spans on the launch stream (the final attempt).  Stages are sums of their
     // kernels: columns | candidates (lane + wave tier) | links + scan |
     // transitions (index, lane, wave, global tiers) | viterbi | route (4 tiers)
     // | segments count + scans | segments write + report

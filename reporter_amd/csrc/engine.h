@@ -44,6 +44,8 @@ struct otm_engine {
       counters_i32, scan_tmp, snap;
   Buf big_key, big_lab, big_inq, big_fr;
   Buf ord_tile, ord_cnt, ord_cursor, ord_grp, ord_item;  // spatial work order
+  Buf abort_flag;                                       // capacity overflow of the batch in flight
+  int64_t trans_cap = 0;                                // floats in `trans` (grown on overflow)
   // outputs
   Buf o_traces, o_seg_cnt, o_way_cnt, o_rep_cnt, seg_ub, o_segments, o_seg_gidx, o_way_ids, o_reports;
   // dense copies made by engine_fetch

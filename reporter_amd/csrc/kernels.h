@@ -145,6 +145,9 @@ struct DevWork {
   int32_t* overflow_list2; // [P] ... the LDS wave tier spilled
   int32_t* counters_i32;   // [0] list 1 count, [1] pool used, [2] pool overflow flag, [3] list 2 count,
                            // [4] list 0 count
+  int32_t* abort;          // [1] set when a capacity (transition matrices, path pool) was exceeded:
+                           // every later kernel returns at once and the host redoes the batch
+  int64_t trans_cap;       // floats allocated for w.trans
   DevIndex idx;
   DevOrder ord;
   // global-tier scratch
@@ -218,6 +221,8 @@ void launch_columns(const DevGraph& g, const DevBatch& b, const DevParams& p, De
 void launch_candidates(const DevGraph& g, const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s,
                        const Marks& mk);
 void launch_links(const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s, const Marks& mk);
+// sets *w.abort when the scanned transition total exceeds w.trans_cap
+void launch_cap_check(const DevBatch& b, DevWork& w, hipStream_t s);
 // lane tier -> wave LDS tier -> global tier, spill lists on the device
 // (counters_i32[0] / [3] must be zero on entry)
 void launch_transitions(const DevGraph& g, const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s,

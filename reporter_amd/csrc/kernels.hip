@@ -691,6 +691,11 @@ __global__ __launch_bounds__(256) void k_links(DevBatch b, DevParams P, DevWork 
   w.trans_off[p] = cnt;
 }
 
+// the transition matrices' total (scan of K3's sizes) against the buffer
+__global__ void k_cap_check(DevBatch b, DevWork w) {
+  if (w.trans_off[b.n_points] > w.trans_cap) *w.abort = 1;
+}
+
 // ============================================================== bounded search
 // Label-correcting single-source search in one wavefront.  Labels are 64-bit
 // (float distance bits << 32 | predecessor edge) updated with atomicMin, so
@@ -927,6 +932,7 @@ __device__ __forceinline__ int lane_find(const uint32_t* K, int n, uint32_t v) {
 
 template <int CAP>
 __global__ __launch_bounds__(LANE_TB) void k_trans_lane(DevGraph g, DevBatch b, DevParams P, DevWork w) {
+  if (*w.abort) return;  // a capacity was exceeded: the host redoes the batch
   __shared__ uint32_t sK[CAP * LANE_TB];
   __shared__ float sD[CAP * LANE_TB];
   uint32_t* K = sK + threadIdx.x;
@@ -1019,6 +1025,7 @@ __global__ __launch_bounds__(LANE_TB) void k_trans_lane(DevGraph g, DevBatch b, 
 
 template <int CAP>
 __global__ __launch_bounds__(LANE_TB) void k_route_lane(DevGraph g, DevBatch b, DevParams P, DevWork w) {
+  if (*w.abort) return;  // a capacity was exceeded: the host redoes the batch
   __shared__ uint32_t sK[CAP * LANE_TB];
   __shared__ float sD[CAP * LANE_TB];
   __shared__ int32_t sP[CAP * LANE_TB];
@@ -1056,6 +1063,7 @@ __global__ __launch_bounds__(LANE_TB) void k_route_lane(DevGraph g, DevBatch b, 
     const int off = len ? atomicAdd(&w.counters_i32[1], len) : 0;
     if (off + len > w.pool_cap) {
       w.counters_i32[2] = 1;
+      *w.abort = 1;
       w.path_len[p] = -1;
     } else {
       int k = len;
@@ -1176,6 +1184,7 @@ __global__ void k_row_pack(const int32_t* row_cnt, const int64_t* row_off, IdxRo
 // trips.  Columns the index cannot answer (bound > rmax, or a source row
 // incomplete) go to the search tiers.
 __global__ __launch_bounds__(TB, 8) void k_trans_index(DevGraph g, DevBatch b, DevParams P, DevWork w) {
+  if (*w.abort) return;  // a capacity was exceeded: the host redoes the batch
   __shared__ int32_t ep[KMAX], vp[KMAX], eq[KMAX];
   __shared__ float op[KMAX], oq[KMAX], sq[KMAX];
   __shared__ IdxRow rq[KMAX];
@@ -1307,6 +1316,7 @@ __global__ __launch_bounds__(TB, 8) void k_trans_index(DevGraph g, DevBatch b, D
 // same occupancy.  Columns with more pairs than S loop within their group.
 template <int S>
 __global__ __launch_bounds__(TB, 8) void k_trans_sub(DevGraph g, DevBatch b, DevParams P, DevWork w) {
+  if (*w.abort) return;  // a capacity was exceeded: the host redoes the batch
   constexpr int NS = TB / S;
   __shared__ int32_t ep[NS][KMAX], vp[NS][KMAX], eq[NS][KMAX];
   __shared__ float op[NS][KMAX], oq[NS][KMAX], sq[NS][KMAX];
@@ -1442,6 +1452,7 @@ __global__ __launch_bounds__(TB, 8) void k_trans_sub(DevGraph g, DevBatch b, Dev
 // K6 index tier: one lane per matched step; the path is read back from the
 // index row of the source node (predecessor edges), one table probe per edge.
 __global__ __launch_bounds__(256) void k_route_index(DevGraph g, DevBatch b, DevParams P, DevWork w) {
+  if (*w.abort) return;  // a capacity was exceeded: the host redoes the batch
   const DevIndex& X = w.idx;
   unsigned long long c_search = 0, c_settled = 0, c_relaxed = 0, c_edges = 0;
   const ItemRange R = item_range(w, b, (P.order_mask & ORDER_ROUTE) != 0, 256);
@@ -1490,6 +1501,7 @@ __global__ __launch_bounds__(256) void k_route_index(DevGraph g, DevBatch b, Dev
     const int off = len ? atomicAdd(&w.counters_i32[1], len) : 0;
     if (off + len > w.pool_cap) {
       w.counters_i32[2] = 1;
+      *w.abort = 1;
       w.path_len[p] = -1;
     } else {
       int k = len;
@@ -1539,6 +1551,7 @@ __global__ __launch_bounds__(256) void k_route_index(DevGraph g, DevBatch b, Dev
 template <bool BIG>
 __global__ __launch_bounds__(TB) void k_transitions(DevGraph g, DevBatch b, DevParams P, DevWork w,
                                                      int32_t n_overflow) {
+  if (*w.abort) return;
   __shared__ uint32_t lkey[BIG ? 1 : LDS_TABLE_CAP];
   __shared__ unsigned long long llab[BIG ? 1 : LDS_TABLE_CAP];
   __shared__ uint32_t linq[BIG ? 1 : LDS_TABLE_CAP];
@@ -1756,6 +1769,7 @@ constexpr int VIT_TW = 1024;   // transition floats per window (>= KMAX * KMAX)
 constexpr int VIT_EW = 512;    // emission floats per window (>= KMAX)
 
 __global__ __launch_bounds__(TB) void k_viterbi(DevBatch b, DevWork w) {
+  if (*w.abort) return;  // a capacity was exceeded: the host redoes the batch
   __shared__ float sT[VIT_TW];
   __shared__ float sEm[VIT_EW];
   __shared__ uint8_t sBp[VIT_BP];
@@ -1990,6 +2004,7 @@ __global__ __launch_bounds__(TB) void k_viterbi(DevBatch b, DevWork w) {
 // ============================================================== K6 route
 template <bool BIG>
 __global__ __launch_bounds__(TB) void k_route(DevGraph g, DevBatch b, DevParams P, DevWork w, int32_t n_overflow) {
+  if (*w.abort) return;
   __shared__ uint32_t lkey[BIG ? 1 : LDS_TABLE_CAP];
   __shared__ unsigned long long llab[BIG ? 1 : LDS_TABLE_CAP];
   __shared__ uint32_t linq[BIG ? 1 : LDS_TABLE_CAP];
@@ -2048,6 +2063,7 @@ __global__ __launch_bounds__(TB) void k_route(DevGraph g, DevBatch b, DevParams 
       const int off = atomicAdd(&w.counters_i32[1], n);
       if (off + n > w.pool_cap) {
         w.counters_i32[2] = 1;
+      *w.abort = 1;
         w.path_len[p] = -1;
       } else {
         int k = n;
@@ -2336,6 +2352,7 @@ __device__ void segments_trace(const DevGraph& g, const DevWork& w, DevOut& o, i
 // with a few rounds of parallel loads; lane 0 then runs the walk out of LDS.
 template <bool WRITE>
 __global__ __launch_bounds__(TB) void k_segments(DevGraph g, DevBatch b, DevWork w, DevOut o) {
+  if (*w.abort) return;  // a capacity was exceeded: the host redoes the batch
   __shared__ SegLds L;
   const int lane = threadIdx.x;
   for (int32_t t = blockIdx.x; t < b.n_traces; t += gridDim.x) {
@@ -2394,6 +2411,7 @@ __device__ __forceinline__ bool in_lv(const int64_t* lv, int n, int64_t x) {
 }
 
 __global__ __launch_bounds__(256) void k_report(DevBatch b, DevReportCfg rc, DevWork w, DevOut o, int32_t n_seg_total) {
+  if (*w.abort) return;  // a capacity was exceeded: the host redoes the batch
   const int32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= b.n_traces) return;
   otm_trace_result r;
@@ -2501,6 +2519,7 @@ __global__ __launch_bounds__(256) void k_report(DevBatch b, DevReportCfg rc, Dev
 // Traversals a matched point can add: the close of the open traversal, its
 // route's path edges, the re-open (+ the chain's final close): <= 2 + path.
 __global__ __launch_bounds__(256) void k_seg_bound(DevBatch b, DevWork w, int64_t* ub) {
+  if (*w.abort) return;  // a capacity was exceeded: the host redoes the batch
   const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p > b.n_points) return;
   int64_t v = 0;
@@ -2609,6 +2628,9 @@ void launch_links(const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t
   TIMED(KN_LINKS, hipLaunchKernelGGL(k_links, dim3(grid_for(b.n_points + 1, 256, 1 << 30)), dim3(256), 0, s, b, p,
                                      w));
 }
+void launch_cap_check(const DevBatch& b, DevWork& w, hipStream_t s) {
+  hipLaunchKernelGGL(k_cap_check, dim3(1), dim3(1), 0, s, b, w);
+}
 void launch_transitions(const DevGraph& g, const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s,
                         const Marks& mk) {
   // many more waves than fit at once (each column is a few dependent
@@ -2618,7 +2640,7 @@ void launch_transitions(const DevGraph& g, const DevBatch& b, const DevParams& p
   static const int sub = [] {
     const char* e = std::getenv("OTM_TRANS_SUB");
     const int v = e ? std::atoi(e) : 16;
-    return v == 8 || v == 16 || v == 32 ? v : 64;
+    return v == 16 || v == 32 ? v : 64;
   }();
   const int per = TB / sub;  // columns per wave step
   const int grid = genv ? std::max(ORDER_GROUPS, std::atoi(genv) / ORDER_GROUPS * ORDER_GROUPS)
@@ -2627,8 +2649,6 @@ void launch_transitions(const DevGraph& g, const DevBatch& b, const DevParams& p
     TIMED(KN_TRANS_INDEX, hipLaunchKernelGGL(k_trans_sub<32>, dim3(grid), dim3(TB), 0, s, g, b, p, w));
   else if (sub == 16)
     TIMED(KN_TRANS_INDEX, hipLaunchKernelGGL(k_trans_sub<16>, dim3(grid), dim3(TB), 0, s, g, b, p, w));
-  else if (sub == 8)
-    TIMED(KN_TRANS_INDEX, hipLaunchKernelGGL(k_trans_sub<8>, dim3(grid), dim3(TB), 0, s, g, b, p, w));
   else
     TIMED(KN_TRANS_INDEX, hipLaunchKernelGGL(k_trans_index, dim3(grid), dim3(TB), 0, s, g, b, p, w));
   TIMED(KN_TRANS_LANE, hipLaunchKernelGGL(k_trans_lane<LANE_CAP_TRANS>, dim3(LANE_GRID), dim3(LANE_TB), 0, s, g, b,

@@ -2225,40 +2225,6 @@ struct SegSrcGlobal {
   __device__ EAttr attr(int pl) const { return edge_attr(*g, edge(pl)); }
 };
 
-// ... or staged in LDS by the whole wavefront (traces up to SEG_PTS points)
-constexpr int SEG_PTS = 256;
-struct SegLds {
-  double time[SEG_PTS];
-  int64_t way[SEG_PTS];
-  uint64_t gid[SEG_PTS];
-  float rd[SEG_PTS], off[SEG_PTS], len[SEG_PTS], glen[SEG_PTS];
-  int32_t poff[SEG_PTS], plen[SEG_PTS], edge[SEG_PTS], seg[SEG_PTS], seg_pos[SEG_PTS];
-  int8_t state[SEG_PTS];
-  uint8_t cs[SEG_PTS], flags[SEG_PTS];
-};
-struct SegSrcLds {
-  const SegLds* L;
-  __device__ int state(int pl) const { return L->state[pl]; }
-  __device__ bool cs(int pl) const { return L->cs[pl] != 0; }
-  __device__ double time(int pl) const { return L->time[pl]; }
-  __device__ float rd(int pl) const { return L->rd[pl]; }
-  __device__ int32_t poff(int pl) const { return L->poff[pl]; }
-  __device__ int32_t plen(int pl) const { return L->plen[pl]; }
-  __device__ int32_t edge(int pl) const { return L->edge[pl]; }
-  __device__ float off(int pl) const { return L->off[pl]; }
-  __device__ EAttr attr(int pl) const {
-    EAttr x;
-    x.len = L->len[pl];
-    x.seg = L->seg[pl];
-    x.seg_pos = L->seg_pos[pl];
-    x.flags = L->flags[pl];
-    x.way = L->way[pl];
-    x.gid = L->gid[pl];
-    x.glen = L->glen[pl];
-    return x;
-  }
-};
-
 // The traversal walk of one trace (one thread): states in order, chains,
 // per step the close of the open traversal, the route's path edges and the
 // re-open on the new edge; traversals grouped into OSMLR segments.
@@ -2347,14 +2313,86 @@ __device__ void segments_trace(const DevGraph& g, const DevWork& w, DevOut& o, i
   o.way_cnt[t] = em.nway;
 }
 
-// One wavefront per trace: lanes stage the trace's points (state, chain
-// flags, times, route results, state edges and their attributes) into LDS
-// with a few rounds of parallel loads; lane 0 then runs the walk out of LDS.
-template <bool WRITE>
+// One wavefront per trace, wave-parallel.  The serial walk
+// above is a scan in disguise:
+//  * the open traversal's edge at every step is the previous state's edge,
+//    and it was opened by the latest "opener" state (a chain start, or a step
+//    that left the edge) -- a max-scan over the states;
+//  * each state emits a known number of traversals (close + route edges when
+//    it leaves the edge, + the chain's final close) -- a sum-scan gives each
+//    its slot; the lanes then write the traversals in parallel;
+//  * a traversal joins its predecessor's group by a test of the two alone --
+//    segment and way-id slots are counts of group starts / way changes.
+// Float and double expressions are the walk's, in the walk's order (the route
+// edges' f32 prefix sum stays sequential per state), so the records are
+// bit-identical.  Traces beyond SEGP_PTS points or SEGP_TRAV traversals take
+// the serial walk out of global memory (lane 0).
+constexpr int SEGP_PTS = 256;
+constexpr int SEGP_TRAV = 512;
+struct SegPar {
+  double o_t0[SEGP_PTS];  // per state: start time of the traversal it opens
+  double t_t0[SEGP_TRAV], t_t1[SEGP_TRAV];
+  float o_off0[SEGP_PTS];
+  int32_t tbase[SEGP_PTS + 1];  // first traversal slot of each state
+  int32_t t_edge[SEGP_TRAV];
+  float t_off0[SEGP_TRAV], t_off1[SEGP_TRAV];
+  int16_t sidx[SEGP_PTS + 1];  // point of each state
+  int16_t o_sh0[SEGP_PTS];
+  int16_t lopen[SEGP_PTS];  // latest opener <= k
+  int16_t chain[SEGP_PTS];
+  int16_t t_sh0[SEGP_TRAV], t_sh1[SEGP_TRAV], t_chain[SEGP_TRAV];
+  int16_t g_first[SEGP_TRAV], g_last[SEGP_TRAV], g_w0[SEGP_TRAV + 1];
+  int32_t nt;
+};
+
+__device__ __forceinline__ int wave_incl_max(int v, int lane) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int n = __shfl_up(v, o, 64);
+    if (lane >= o) v = n > v ? n : v;
+  }
+  return v;
+}
+
+// what a state contributes (recomputed in the two passes that need it)
+struct StateStep {
+  int pl, lp;      // point, previous state's point
+  bool cs, last;   // chain start, last state of its chain
+  bool step, same; // a step from lp; stays on the open edge
+  int32_t ei, ej;  // previous state's edge (== the open traversal's), own edge
+  float oi, oj;
+  int32_t plen, poff;
+};
+__device__ __forceinline__ StateStep state_step(const DevWork& w, int64_t a, const SegPar& S, int k, int ns) {
+  StateStep r;
+  r.pl = S.sidx[k];
+  const int64_t p = a + r.pl;
+  r.cs = w.chain_start[p] != 0;
+  r.last = k == ns - 1 || w.chain_start[a + S.sidx[k + 1]] != 0;
+  r.step = !r.cs && k > 0;
+  r.lp = r.step ? S.sidx[k - 1] : r.pl;
+  const int sj = w.state[p];
+  r.ej = w.cand_edge[p * KMAX + sj];
+  r.oj = w.cand_off[p * KMAX + sj];
+  const int64_t q = a + r.lp;
+  const int si = w.state[q];
+  r.ei = w.cand_edge[q * KMAX + si];
+  r.oi = w.cand_off[q * KMAX + si];
+  r.same = r.step && r.ei == r.ej && r.oj >= r.oi;
+  r.plen = 0;
+  r.poff = 0;
+  if (r.step && !r.same) {
+    r.plen = w.path_len[p] > 0 ? w.path_len[p] : 0;
+    r.poff = w.path_off[p];
+  }
+  return r;
+}
+
 __global__ __launch_bounds__(TB) void k_segments(DevGraph g, DevBatch b, DevWork w, DevOut o) {
   if (*w.abort) return;  // a capacity was exceeded: the host redoes the batch
-  __shared__ SegLds L;
+  __shared__ SegPar S;
   const int lane = threadIdx.x;
+  const unsigned long long lt = (1ull << lane) - 1ull;
   for (int32_t t = blockIdx.x; t < b.n_traces; t += gridDim.x) {
     const int64_t a = b.trace_off[t];
     const int n = (int)(b.trace_off[t + 1] - a);
@@ -2366,39 +2404,228 @@ __global__ __launch_bounds__(TB) void k_segments(DevGraph g, DevBatch b, DevWork
       }
       continue;
     }
-    if (n > SEG_PTS) {
-      if (lane == 0) segments_trace<WRITE>(g, w, o, t, n, base, SegSrcGlobal{&g, &b, &w, a});
+    if (n > SEGP_PTS) {
+      if (lane == 0) segments_trace<true>(g, w, o, t, n, base, SegSrcGlobal{&g, &b, &w, a});
       continue;
     }
-    for (int pl = lane; pl < n; pl += TB) {
-      const int64_t p = a + pl;
-      // round 1: by point
-      const uint8_t ic = w.is_col[p];
-      const int32_t s0 = w.state[p];
-      const int st = ic ? s0 : -1;
-      L.state[pl] = (int8_t)st;
-      L.cs[pl] = w.chain_start[p];
-      L.time[pl] = b.time[p];
-      L.rd[pl] = w.route_dist[p];
-      L.poff[pl] = w.path_off[p];
-      L.plen[pl] = w.path_len[p];
-      if (st >= 0) {
-        // round 2: the state's candidate; rounds 3-4: its edge, its segment
-        const int32_t e = w.cand_edge[p * KMAX + st];
-        L.off[pl] = w.cand_off[p * KMAX + st];
-        L.edge[pl] = e;
-        const EAttr x = edge_attr(g, e);
-        L.len[pl] = x.len;
-        L.seg[pl] = x.seg;
-        L.seg_pos[pl] = x.seg_pos;
-        L.flags[pl] = (uint8_t)x.flags;
-        L.way[pl] = x.way;
-        L.gid[pl] = x.gid;
-        L.glen[pl] = x.glen;
+    // ---- states in point order
+    int ns = 0;
+    for (int c0 = 0; c0 < n; c0 += TB) {
+      const int pl = c0 + lane;
+      const bool st = pl < n && w.is_col[a + pl] && w.state[a + pl] >= 0;
+      const unsigned long long m = __ballot(st);
+      if (st) S.sidx[ns + __popcll(m & lt)] = (int16_t)pl;
+      ns += __popcll(m);
+    }
+    __syncthreads();
+    // ---- per state: opener fields, chain index, latest opener, slot counts
+    int c_chain = 0, c_open = -1, c_base = 0;
+    for (int k0 = 0; k0 < ns; k0 += TB) {
+      const int k = k0 + lane;
+      const bool valid = k < ns;
+      int cs = 0, opener = -1, nem = 0;
+      if (valid) {
+        const StateStep r = state_step(w, a, S, k, ns);
+        cs = r.cs ? 1 : 0;
+        if (r.cs || !r.same) {
+          opener = k;
+          if (r.cs) {
+            S.o_t0[k] = b.time[a + r.pl];
+            S.o_off0[k] = r.oj;
+            S.o_sh0[k] = (int16_t)r.pl;
+          } else {
+            const float Rd = w.route_dist[a + r.pl];
+            const double ta = b.time[a + r.lp], tb = b.time[a + r.pl];
+            const float start = g.e_len[r.ei] - r.oi;
+            float dd = 0.0f;
+            for (int i = 0; i < r.plen; ++i) dd = dd + g.e_len[w.path_pool[r.poff + i]];
+            const float x = start + dd;
+            S.o_t0[k] = time_at(ta, tb, x, Rd);
+            S.o_off0[k] = 0.0f;
+            S.o_sh0[k] = (int16_t)(x >= Rd ? r.pl : r.lp);
+          }
+        }
+        nem = (r.step && !r.same ? 1 + r.plen : 0) + (r.last && !r.cs ? 1 : 0);
+      }
+      const int ch = c_chain + wave_incl_scan(cs, lane);
+      int lo = wave_incl_max(opener, lane);
+      lo = lo > c_open ? lo : c_open;
+      const int inc = wave_incl_scan(nem, lane);
+      if (valid) {
+        S.chain[k] = (int16_t)(ch - 1);
+        S.lopen[k] = (int16_t)lo;
+        S.tbase[k] = c_base + inc - nem;
+      }
+      c_chain = __shfl(ch, 63, 64);
+      c_open = __shfl(lo, 63, 64);
+      c_base += __shfl(inc, 63, 64);
+    }
+    const int nt = c_base;
+    __syncthreads();
+    if (nt > SEGP_TRAV) {
+      if (lane == 0) segments_trace<true>(g, w, o, t, n, base, SegSrcGlobal{&g, &b, &w, a});
+      __syncthreads();
+      continue;
+    }
+    // ---- traversals, each state writing its own
+    for (int k0 = 0; k0 < ns; k0 += TB) {
+      const int k = k0 + lane;
+      if (k >= ns) continue;
+      const StateStep r = state_step(w, a, S, k, ns);
+      int slot = S.tbase[k];
+      const int16_t chk = S.chain[k];
+      if (r.step && !r.same) {
+        const float Rd = w.route_dist[a + r.pl];
+        const double ta = b.time[a + r.lp], tb = b.time[a + r.pl];
+        const float elen = g.e_len[r.ei];
+        const float start = elen - r.oi;
+        const int jo = S.lopen[k - 1];
+        S.t_edge[slot] = r.ei;
+        S.t_off0[slot] = S.o_off0[jo];
+        S.t_t0[slot] = S.o_t0[jo];
+        S.t_sh0[slot] = S.o_sh0[jo];
+        S.t_off1[slot] = elen;
+        S.t_t1[slot] = time_at(ta, tb, start, Rd);
+        S.t_sh1[slot] = (int16_t)(start >= Rd ? r.pl : r.lp);
+        S.t_chain[slot] = chk;
+        ++slot;
+        float dd = 0.0f;
+        for (int i = 0; i < r.plen; ++i) {
+          const int32_t pe = w.path_pool[r.poff + i];
+          const float len = g.e_len[pe];
+          const float xb = start + dd;
+          dd = dd + len;
+          const float xe = start + dd;
+          S.t_edge[slot] = pe;
+          S.t_off0[slot] = 0.0f;
+          S.t_off1[slot] = len;
+          S.t_t0[slot] = time_at(ta, tb, xb, Rd);
+          S.t_t1[slot] = time_at(ta, tb, xe, Rd);
+          S.t_sh0[slot] = (int16_t)(xb >= Rd ? r.pl : r.lp);
+          S.t_sh1[slot] = (int16_t)(xe >= Rd ? r.pl : r.lp);
+          S.t_chain[slot] = chk;
+          ++slot;
+        }
+      }
+      if (r.last && !r.cs) {
+        const int jo = S.lopen[k];
+        S.t_edge[slot] = r.ej;
+        S.t_off0[slot] = S.o_off0[jo];
+        S.t_t0[slot] = S.o_t0[jo];
+        S.t_sh0[slot] = S.o_sh0[jo];
+        S.t_off1[slot] = r.oj;
+        S.t_t1[slot] = b.time[a + r.pl];
+        S.t_sh1[slot] = (int16_t)r.pl;
+        S.t_chain[slot] = chk;
       }
     }
     __syncthreads();
-    if (lane == 0) segments_trace<WRITE>(g, w, o, t, n, base, SegSrcLds{&L});
+    // ---- groups (OSMLR segments) and way ids
+    int c_seg = 0, c_way = 0;
+    int32_t p_seg = 0, p_pos = 0, p_ch = -1;
+    uint32_t p_fl = 0;
+    int64_t p_way = 0;
+    for (int k0 = 0; k0 < nt; k0 += TB) {
+      const int k = k0 + lane;
+      const bool valid = k < nt;
+      int32_t seg = -1, pos = 0, ch = -2;
+      uint32_t fl = 0;
+      int64_t way = 0;
+      if (valid) {
+        const int32_t e = S.t_edge[k];
+        seg = g.e_seg[e];
+        pos = g.e_seg_pos[e];
+        fl = g.e_flags[e];
+        way = g.e_way[e];
+        ch = S.t_chain[k];
+      }
+      int32_t qs = __shfl_up(seg, 1, 64), qp = __shfl_up(pos, 1, 64), qc = __shfl_up(ch, 1, 64);
+      uint32_t qf = __shfl_up(fl, 1, 64);
+      int64_t qw = __shfl_up(way, 1, 64);
+      if (lane == 0) {
+        qs = p_seg;
+        qp = p_pos;
+        qc = p_ch;
+        qf = p_fl;
+        qw = p_way;
+      }
+      bool join = false;
+      if (valid && qc == ch) {
+        if (seg >= 0) join = qs == seg && pos == qp + 1;
+        else join = qs < 0 && ((fl ^ qf) & SegEmitter<true>::OTM_EDGE_INTERNAL_D) == 0;
+      }
+      const bool start = valid && !join;
+      const bool wemit = valid && (start || way != qw);
+      const unsigned long long ms = __ballot(start), mw = __ballot(wemit);
+      const int gi = c_seg + __popcll(ms & lt) + (start ? 0 : -1);  // this traversal's group
+      const int wi = c_way + __popcll(mw & lt);
+      if (wemit) o.way_ids[base + wi] = way;
+      if (start) {
+        S.g_first[gi] = (int16_t)k;
+        S.g_w0[gi] = (int16_t)wi;
+        if (gi > 0) S.g_last[gi - 1] = (int16_t)(k - 1);
+      }
+      c_seg += __popcll(ms);
+      c_way += __popcll(mw);
+      p_seg = __shfl(seg, 63, 64);
+      p_pos = __shfl(pos, 63, 64);
+      p_ch = __shfl(ch, 63, 64);
+      p_fl = __shfl(fl, 63, 64);
+      p_way = __shfl(way, 63, 64);
+    }
+    if (lane == 0 && c_seg > 0) {
+      S.g_last[c_seg - 1] = (int16_t)(nt - 1);
+      S.g_w0[c_seg] = (int16_t)c_way;
+    }
+    __syncthreads();
+    // ---- one record per group (SegEmitter::flush)
+    for (int s0 = 0; s0 < c_seg; s0 += TB) {
+      const int si = s0 + lane;
+      if (si >= c_seg) continue;
+      const int kf = S.g_first[si], kl = S.g_last[si];
+      const EAttr fa = edge_attr(g, S.t_edge[kf]);
+      const int32_t el = S.t_edge[kl];
+      const float llen = g.e_len[el];
+      const uint32_t lfl = g.e_flags[el];
+      otm_segment sr;
+      const int32_t sg = fa.seg;
+      bool sv, ev;
+      sr.flags = 0u;
+      if (sg >= 0) {
+        sv = S.t_off0[kf] == 0.0f && (fa.flags & SegEmitter<true>::OTM_EDGE_SEG_BEGIN_D);
+        ev = S.t_off1[kl] == llen && (lfl & SegEmitter<true>::OTM_EDGE_SEG_END_D);
+        sr.segment_id = (int64_t)fa.gid;
+        sr.length = (sv && ev) ? (int32_t)floor((double)fa.glen + 0.5) : -1;
+      } else {
+        sv = S.t_off0[kf] == 0.0f;
+        ev = S.t_off1[kl] == llen;
+        sr.segment_id = -1;
+        sr.length = -1;
+        if (fa.flags & SegEmitter<true>::OTM_EDGE_INTERNAL_D) sr.flags |= OTM_SEG_INTERNAL;
+      }
+      sr.start_time = 0.0;
+      sr.end_time = 0.0;
+      if (sv) {
+        sr.flags |= OTM_SEG_START_VALID;
+        sr.start_time = S.t_t0[kf];
+      }
+      if (ev) {
+        sr.flags |= OTM_SEG_END_VALID;
+        sr.end_time = S.t_t1[kl];
+      }
+      sr.queue_length = 0;
+      sr.begin_shape_index = S.t_sh0[kf];
+      sr.end_shape_index = S.t_sh1[kl];
+      sr.way_off = base + S.g_w0[si];
+      sr.way_cnt = S.g_w0[si + 1] - S.g_w0[si];
+      sr.pad = 0u;
+      ((otm_segment*)o.segments)[base + si] = sr;
+      o.seg_gidx[base + si] = sg;
+    }
+    if (lane == 0) {
+      o.seg_cnt[t] = c_seg;
+      o.way_cnt[t] = c_way;
+    }
     __syncthreads();
   }
 }
@@ -2672,7 +2899,7 @@ void launch_segments(const DevGraph& g, const DevBatch& b, DevWork& w, DevOut& o
                      const Marks& mk) {
   (void)write;
   const dim3 grid(grid_for(b.n_traces, 1, WAVE_GRID_CAP));
-  TIMED(KN_SEG_WRITE, hipLaunchKernelGGL(k_segments<true>, grid, dim3(TB), 0, s, g, b, w, o));
+  TIMED(KN_SEG_WRITE, hipLaunchKernelGGL(k_segments, grid, dim3(TB), 0, s, g, b, w, o));
 }
 void launch_seg_bound(const DevBatch& b, DevWork& w, int64_t* ub, hipStream_t s, const Marks& mk) {
   TIMED(KN_SEG_BOUND, hipLaunchKernelGGL(k_seg_bound, dim3(grid_for(b.n_points + 1, 256, 1 << 30)), dim3(256), 0, s,

@@ -10,7 +10,8 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libotmatch.so")
+# OTM_LIB selects another in-tree build of the same library (A/B of compile-time variants)
+LIB_PATH = os.environ.get("OTM_LIB") or os.path.join(_HERE, "lib", "libotmatch.so")
 
 OTM_OK = 0
 

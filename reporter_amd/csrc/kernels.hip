@@ -362,9 +362,12 @@ __device__ __forceinline__ ItemRange item_range(const DevWork& w, const DevBatch
 // ============================================================== K2 candidates
 constexpr int HCAP = 512;  // edge hash slots (>= 2 * MAX_HITS)
 #ifndef OTM_CAND_LANE_CAP
-#define OTM_CAND_LANE_CAP 16
+#define OTM_CAND_LANE_CAP 8
 #endif
-constexpr int CAND_LANE_CAP = OTM_CAND_LANE_CAP;  // lane tier: distinct edges kept per probe
+// lane tier: distinct edges kept per probe.  8 measured best on config 2
+// (0.39 ms with the wave tier vs 0.40 at 12, 0.45 at 16): a smaller LDS list
+// buys occupancy; the ~1 % of probes with more edges in range spill.
+constexpr int CAND_LANE_CAP = OTM_CAND_LANE_CAP;
 constexpr int CAND_TB = 128;
 
 // wave-reduce a per-lane count and add it to a device counter (all 64 lanes active)

@@ -1,0 +1,13 @@
+#!/bin/bash
+# Build libotmatch.so with extra compile flags into reporter_amd/lib/variants/<name>/ (A/B of compile-time knobs):
+#   bash scripts/build_variant.sh cap8 -DOTM_CAND_LANE_CAP=8
+set -e
+NAME=$1; shift
+ROOT=$(cd "$(dirname "$0")/.." && pwd)
+OUT=$ROOT/reporter_amd/lib/variants/$NAME
+mkdir -p $OUT/obj
+cd $ROOT/reporter_amd/csrc
+FLAGS="-O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -I../../include -I. $*"
+/opt/rocm/bin/hipcc $FLAGS --offload-arch=gfx950 -c kernels.hip -o $OUT/obj/kernels.o
+/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o $OUT/libotmatch.so $(ls ../lib/obj/*.o | grep -v kernels.o) $OUT/obj/kernels.o -lpthread
+echo $OUT/libotmatch.so

@@ -251,6 +251,7 @@ int otm_engine_create(const char* cfg_path, const int* devices, int ndev, otm_en
   auto* E = new otm_engine();
   const Value* ir = o->get("index_radius_m");
   if (ir && ir->is_num()) E->index_rmax = (float)ir->num();
+  if (const char* er = std::getenv("OTM_INDEX_RADIUS")) E->index_rmax = (float)std::atof(er);  // A/B override
   const Value* meili = cfg.get("meili");
   const Value* dflt = meili ? meili->get("default") : nullptr;
   if (dflt && dflt->kind == Kind::Obj) {

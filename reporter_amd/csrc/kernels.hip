@@ -1766,10 +1766,19 @@ __device__ void viterbi_trace_global(int64_t a, int64_t e, DevWork& w) {
 // runs out of LDS with the previous column's scores broadcast by readlane;
 // the backtrack walks LDS; state / chain_start go out coalesced.  Same
 // recurrence, tie rules and chain breaks as viterbi_trace_global.
-constexpr int VIT_PTS = 256;   // points per trace (metadata held for the whole trace)
-constexpr int VIT_BP = 2048;   // candidates per trace (backpointers)
-constexpr int VIT_TW = 1024;   // transition floats per window (>= KMAX * KMAX)
-constexpr int VIT_EW = 512;    // emission floats per window (>= KMAX)
+// LDS per trace (~6.8 KB at these sizes) sets how many traces a CU holds;
+// a trace whose candidates exceed VIT_BP, or with one column pair's block
+// beyond VIT_TW, takes the global-memory form.
+#ifndef OTM_VIT_TW
+#define OTM_VIT_TW 512
+#endif
+#ifndef OTM_VIT_BP
+#define OTM_VIT_BP 1024
+#endif
+constexpr int VIT_PTS = 256;         // points per trace (metadata held for the whole trace)
+constexpr int VIT_BP = OTM_VIT_BP;   // candidates per trace (backpointers)
+constexpr int VIT_TW = OTM_VIT_TW;   // transition floats per window (>= one column pair's block)
+constexpr int VIT_EW = 256;          // emission floats per window (>= KMAX)
 
 __global__ __launch_bounds__(TB) void k_viterbi(DevBatch b, DevWork w) {
   if (*w.abort) return;  // a capacity was exceeded: the host redoes the batch
@@ -1798,6 +1807,7 @@ __global__ __launch_bounds__(TB) void k_viterbi(DevBatch b, DevWork w) {
     bool fits = n <= VIT_PTS;
     if (fits) {
       // column metadata + emission offsets (wave scan of ncand)
+      bool big = false;  // a column pair's block beyond the window
       for (int c = 0; c < n; c += TB) {
         const int pl = c + lane;
         int kc = -1, cp = -1, to = 0;
@@ -1808,11 +1818,13 @@ __global__ __launch_bounds__(TB) void k_viterbi(DevBatch b, DevWork w) {
           const int32_t nc = w.ncand[p];
           const int32_t q = w.col_prev[p];
           const int64_t tp = w.trans_off[p];
+          const int64_t tn = w.trans_off[p + 1];
           if (ic) {
             kc = nc;
             cp = q >= 0 ? (int)(q - a) : -1;
           }
           to = (int)(tp - t0);
+          big = big || tn - tp > VIT_TW;
         }
         const int k = kc > 0 ? kc : 0;
         const int incl = wave_incl_scan(k, lane);
@@ -1826,7 +1838,7 @@ __global__ __launch_bounds__(TB) void k_viterbi(DevBatch b, DevWork w) {
         }
         etot += __shfl(incl, 63, 64);
       }
-      fits = etot <= VIT_BP;
+      fits = etot <= VIT_BP && __ballot(big) == 0ull;
     }
     if (!fits) {
       __syncthreads();

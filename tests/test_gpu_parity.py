@@ -65,7 +65,7 @@ def _run_both(graph, batch, oracle, results_equal, meili=None, stages=True, coun
         return res, orc
 
 
-@pytest.mark.parametrize("radius", [None, 0.0, 300.0], ids=["index1000", "no_index", "index300"])
+@pytest.mark.parametrize("radius", [None, 0.0, 300.0], ids=["index_default", "no_index", "index300"])
 def test_city_sample_sigma15(small_graph, oracle, results_equal, radius):
     # the distance index answers columns whose bound fits its radius; the rest
     # (and everything when it is disabled) run the online search tiers --
@@ -80,7 +80,7 @@ def test_index_info(small_graph):
     with Engine(graph_path=small_graph) as eng:
         info = eng.index_info()
         n = eng.graph_info()["nodes"]
-        assert info["radius_m"] == 1000.0 and info["incomplete_rows"] == 0
+        assert info["radius_m"] == 1250.0 and info["incomplete_rows"] == 0
         assert info["entries"] > 10 * n
     with Engine(graph_path=small_graph, index_radius_m=0) as eng:
         assert eng.index_info()["entries"] == 0

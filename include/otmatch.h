@@ -281,6 +281,67 @@ int otm_kmax(void);
  * a host that also runs torch must load torch first so both share one. */
 const char* otm_runtime_info(void);
 
+/* ------------------------------------------------------------- host batcher */
+/* Native restatement of the reference's Kafka Streams batcher -- Batch
+ * (Batch.java:16-84) and BatchingProcessor (BatchingProcessor.java:19-133):
+ * per-uuid batches, the 500 m / 10 points / 60 s report gates, the trim at
+ * shape_used, the session-gap clean() with its relaxed (0, 2, 0) reports and
+ * close().  A key's operations run in the reference's serial order; the
+ * requests of all keys that are ready go to the matcher as one GPU batch.
+ * Used as the config-5 driver (sustained ingest) and as a native host. */
+typedef struct otm_batcher otm_batcher;
+typedef struct otm_batcher_cfg {
+  int32_t report_dist;    /* REPORT_DIST, metres (BatchingProcessor.java:30)  */
+  int32_t report_count;   /* REPORT_COUNT, points (:29)                      */
+  int64_t report_time_s;  /* REPORT_TIME, seconds (:28)                      */
+  int64_t session_gap_ms; /* SESSION_GAP, ms of record time (:31)            */
+  int32_t max_batch;      /* requests per matcher call (0: all ready ones)   */
+  int32_t json_path;      /* 1: engine requests go through the JSON /report
+                             path (otm_report_batch) instead of the binary one */
+  int64_t max_pending;    /* otm_batcher_process drains once this many
+                             operations are queued (0: only on flush/close)  */
+} otm_batcher_cfg;
+void otm_batcher_defaults(otm_batcher_cfg* cfg);
+/* A /report handler for n request bodies (the HttpClient.POST of
+ * Batch.java:63): fills codes / bodies; bodies must be malloc'd (the batcher
+ * frees or forwards them).  Returns 0. */
+typedef int (*otm_report_fn)(void* ctx, int n, const char* const* reqs, const size_t* lens, char** resps,
+                             size_t* resp_lens, int* codes);
+/* eng: the matcher (fn == NULL); or fn/ctx: any /report handler (eng may be NULL). */
+int otm_batcher_create(otm_engine* eng, const otm_batcher_cfg* cfg, otm_report_fn fn, void* ctx,
+                       otm_batcher** out);
+void otm_batcher_destroy(otm_batcher* b);
+/* Formatted records in stream order: (key, Point, record timestamp in ms)
+ * (BatchingProcessor.process, :56-85, with context.timestamp() = ts_ms). */
+int otm_batcher_process(otm_batcher* b, int n, const char* const* keys, const size_t* key_lens, const float* lat,
+                        const float* lon, const int32_t* accuracy, const int64_t* time, const int64_t* ts_ms);
+/* Run every queued operation to completion (matcher calls included). */
+int otm_batcher_flush(otm_batcher* b);
+/* BatchingProcessor.close (:120-130): flush, then a relaxed report of every
+ * stored batch (responses discarded). */
+int otm_batcher_close(otm_batcher* b);
+/* context.forward(key, response) of process() (:70-71), in completion order;
+ * seq = the record's position in the stream (per key increasing).  key and
+ * body are released with otm_free. */
+typedef struct otm_forward {
+  char* key;
+  size_t key_len;
+  char* body;
+  size_t body_len;
+  int64_t seq;
+} otm_forward;
+int otm_batcher_take(otm_batcher* b, otm_forward* out, int max);
+typedef struct otm_batcher_stats {
+  int64_t records, clean_ops, close_ops, requests, request_points, match_batches, forwarded;
+  int64_t null_batch_in_clean; /* clean() on a key with no stored batch: the reference throws */
+  int64_t keys, stored_batches, stored_points;
+} otm_batcher_stats;
+int otm_batcher_get_stats(const otm_batcher* b, otm_batcher_stats* out);
+/* A key's stored batch (points in order, max_separation); returns its size
+ * (copies at most max points) or -1 when the store has no batch for it. */
+int otm_batcher_batch(const otm_batcher* b, const char* key, size_t key_len, int max, float* lat, float* lon,
+                      int32_t* accuracy, int64_t* time, float* max_separation);
+
 /* --------------------------------------------------- synthetic inputs ---- */
 /* Harness tooling, not the hot path: the seeded synthetic road network and
  * probe traces of SURVEY.md §8(d) (no real Valhalla tiles exist here). */

@@ -47,6 +47,31 @@ class SpillStats(C.Structure):
                                          "route_wave", "route_global", "pad")]
 
 
+class BatcherCfg(C.Structure):
+    _fields_ = [("report_dist", C.c_int32), ("report_count", C.c_int32), ("report_time_s", C.c_int64),
+                ("session_gap_ms", C.c_int64), ("max_batch", C.c_int32), ("json_path", C.c_int32),
+                ("max_pending", C.c_int64)]
+
+
+class Forward(C.Structure):
+    _fields_ = [("key", C.c_void_p), ("key_len", C.c_size_t), ("body", C.c_void_p), ("body_len", C.c_size_t),
+                ("seq", C.c_int64)]
+
+
+BATCHER_STATS = ("records", "clean_ops", "close_ops", "requests", "request_points", "match_batches", "forwarded",
+                 "null_batch_in_clean", "keys", "stored_batches", "stored_points")
+
+
+class BatcherStats(C.Structure):
+    _fields_ = [(n, C.c_int64) for n in BATCHER_STATS]
+
+
+# int (*otm_report_fn)(void* ctx, int n, const char* const* reqs, const size_t* lens, char** resps,
+#                      size_t* resp_lens, int* codes)
+REPORT_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int, C.POINTER(C.c_char_p), C.POINTER(C.c_size_t),
+                        C.POINTER(C.c_void_p), C.POINTER(C.c_size_t), C.POINTER(C.c_int))
+
+
 class SynthGraphParams(C.Structure):
     _fields_ = [("center_lat", C.c_double), ("center_lon", C.c_double), ("width_m", C.c_double),
                 ("height_m", C.c_double), ("block_m", C.c_double), ("jitter_m", C.c_double),
@@ -109,6 +134,15 @@ def _declare(L):
         "otm_get_spill_stats": (C.c_int, [vp, C.POINTER(SpillStats)]),
         "otm_debug_fetch": (C.c_int, [vp, C.c_int, vp, sz, psz]),
         "otm_kmax": (C.c_int, []),
+        "otm_batcher_defaults": (None, [C.POINTER(BatcherCfg)]),
+        "otm_batcher_create": (C.c_int, [vp, C.POINTER(BatcherCfg), REPORT_FN, vp, pp]),
+        "otm_batcher_destroy": (None, [vp]),
+        "otm_batcher_process": (C.c_int, [vp, C.c_int, C.POINTER(C.c_char_p), psz, vp, vp, vp, vp, vp]),
+        "otm_batcher_flush": (C.c_int, [vp]),
+        "otm_batcher_close": (C.c_int, [vp]),
+        "otm_batcher_take": (C.c_int, [vp, C.POINTER(Forward), C.c_int]),
+        "otm_batcher_get_stats": (C.c_int, [vp, C.POINTER(BatcherStats)]),
+        "otm_batcher_batch": (C.c_int, [vp, C.c_char_p, sz, C.c_int, vp, vp, vp, vp, C.POINTER(C.c_float)]),
         "otm_synth_graph_defaults": (None, [C.POINTER(SynthGraphParams)]),
         "otm_synth_graph": (C.c_int, [C.POINTER(SynthGraphParams), C.c_char_p]),
         "otm_synth_traces": (C.c_int, [C.c_char_p, C.POINTER(SynthTraceParams), vp, vp, vp, vp, vp, vp, vp]),
@@ -152,6 +186,16 @@ def lib():
         EXPORTED = sorted(_declare(L).keys())
         _lib = L
     return _lib
+
+
+def malloc_bytes(b):
+    """A malloc'd copy of `b` (for bodies handed to the library, released by otm_free)."""
+    libc = C.CDLL(None)
+    libc.malloc.restype = C.c_void_p
+    libc.malloc.argtypes = [C.c_size_t]
+    p = libc.malloc(len(b) + 1)
+    C.memmove(p, b + b"\0", len(b) + 1)
+    return p
 
 
 def last_error():

@@ -190,26 +190,6 @@ void worker_loop(otm_engine* E) {
   }
 }
 
-// Java DecimalFormat("###.######", HALF_EVEN) of a float widened to double
-// (Point.java:29,41-42).  "###" sets no minimum integer digit, so |x| < 1
-// prints without its leading zero (".5", "-.5"); a value that rounds to zero
-// prints "0" (with the sign of a negative input).  No JVM exists here to pin
-// this against: the rules are DecimalFormat's documented behaviour.
-void java_decimal6(float f, std::string* o) {
-  char buf[64];
-  std::snprintf(buf, sizeof buf, "%.6f", (double)f);  // exact binary value, half-even
-  std::string s(buf);
-  const bool neg = s[0] == '-';
-  std::string mag = neg ? s.substr(1) : s;
-  size_t end = mag.size();
-  while (end > 0 && mag[end - 1] == '0') --end;
-  if (end > 0 && mag[end - 1] == '.') --end;
-  mag.resize(end);
-  if (mag.size() > 1 && mag[0] == '0' && mag[1] == '.') mag = mag.substr(1);
-  if (neg) o->push_back('-');
-  o->append(mag);
-}
-
 }  // namespace
 
 extern "C" {
@@ -408,9 +388,9 @@ int otm_encode_request(const char* uuid, int n, const float* lat, const float* l
   s.append("\",\"trace\":[");
   for (int k = 0; k < n; ++k) {
     s.append("{\"lat\":");
-    java_decimal6(lat[k], &s);
+    otm::java_decimal6(lat[k], &s);
     s.append(",\"lon\":");
-    java_decimal6(lon[k], &s);
+    otm::java_decimal6(lon[k], &s);
     s.append(",\"time\":");
     otm::json::put_int(time[k], &s);
     s.append(",\"accuracy\":");

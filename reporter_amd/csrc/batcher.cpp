@@ -1,0 +1,546 @@
+// batcher.cpp -- native restatement of the reference's Kafka Streams batcher
+// (BASELINE config 5), driving the matcher in GPU batches.
+//
+// What it restates (reference = burritojustice/reporter):
+//   Batch            src/main/java/org/opentraffic/reporter/Batch.java:16-84
+//     distance       :31-38   equirectangular, float lat/lon, double math
+//     update         :40-44   max_separation = (float)max(.., distance(p, first))
+//     report         :46-84   gates, request bytes (Point.java:39-45), POST,
+//                             trim by findValue("shape_used"), clear on error
+//   BatchingProcessor src/main/java/org/opentraffic/reporter/BatchingProcessor.java
+//     constants      :28-31   REPORT_TIME 60 s, REPORT_COUNT 10, REPORT_DIST 500 m, SESSION_GAP 60000 ms
+//     process        :56-85   clean(key); store.delete; new Batch | update + report -> forward;
+//                             put back if non-empty
+//     clean          :87-112  pop keys idle > SESSION_GAP (by record timestamp), report(k, 0, 2, 0);
+//                             time_to_key.remove(iter) removes nothing (a ListIterator is never equal
+//                             to a Pair), so EVERY record's entry expires 60 s later and triggers a
+//                             relaxed report of its key; a popped key with no stored batch makes
+//                             store.get return null and the reference throws (NPE, stream thread
+//                             dies) -- here it is counted (null_batch_in_clean) and skipped
+//     close          :120-130 relaxed report of every stored batch, keys in TreeMap order
+//
+// Serial semantics, batched execution: a key's operations (its records'
+// process() and the clean()/close() reports that name it) run in exactly the
+// serial order, but a key waiting for a match does not hold up the others.
+// Which keys clean() pops depends only on record timestamps (the time_to_key
+// list never changes on a response), so the operation list of every key is
+// known when its records arrive.  Requests of all runnable keys go to the
+// matcher together: one GPU batch per round.
+#include <algorithm>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <deque>
+#include <map>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "engine.h"
+#include "json.h"
+#include "report.h"
+
+namespace {
+
+using otm::json::Kind;
+using otm::json::Value;
+
+struct JPoint {  // Point.java:15-17
+  float lat, lon;
+  int32_t acc;
+  int64_t time;
+};
+
+struct JBatch {  // Batch.java:18-19
+  float max_sep = 0.0f;
+  std::vector<JPoint> pts;
+};
+
+const double kRadPerDeg = 3.14159265358979323846 / 180.0;  // Math.PI / 180.0
+const double kMetersPerDeg = 20037581.187 / 180.0;
+
+// Batch.distance (Batch.java:34-38), Java evaluation order: float lon/lat
+// differences and .5f * (lat_a + lat_b) in float, the rest in double.
+double jdistance(const JPoint& a, const JPoint& b) {
+  const float dlon = a.lon - b.lon;
+  const float mlat = 0.5f * (a.lat + b.lat);
+  const double x = (double)dlon * kMetersPerDeg * std::cos((double)mlat * kRadPerDeg);
+  const double y = (double)(float)(a.lat - b.lat) * kMetersPerDeg;
+  return std::sqrt(x * x + y * y);
+}
+
+void jupdate(JBatch& b, const JPoint& p) {  // Batch.update
+  if (!b.pts.empty()) b.max_sep = (float)std::max((double)b.max_sep, jdistance(p, b.pts[0]));
+  b.pts.push_back(p);
+}
+
+bool jgates(const JBatch& b, int min_dist, int min_size, int64_t min_elapsed) {  // Batch.java:48-50
+  if (b.max_sep < (float)min_dist) return false;
+  if ((int64_t)b.pts.size() < min_size) return false;
+  return !(b.pts.back().time - b.pts.front().time < min_elapsed);
+}
+
+// Jackson JsonNode.findValue: depth-first, a node's own fields before their
+// children, in field order.
+const Value* find_value(const Value& v, const std::string& name) {
+  if (v.kind == Kind::Obj) {
+    for (size_t k = 0; k < v.keys.size(); ++k)
+      if (v.keys[k] == name) return &v.items[k];
+    for (const Value& c : v.items)
+      if (const Value* r = find_value(c, name)) return r;
+  } else if (v.kind == Kind::Arr) {
+    for (const Value& c : v.items)
+      if (const Value* r = find_value(c, name)) return r;
+  }
+  return nullptr;
+}
+
+// Batch.java:64-81 after the POST: trim_to = shape_used or everything; any
+// exception (unparsable body, out-of-range trim) clears the batch.
+void japply(JBatch& b, int trim_to_or_neg) {
+  const int64_t n = (int64_t)b.pts.size();
+  const int64_t trim = trim_to_or_neg < 0 ? n : trim_to_or_neg;
+  if (trim > n) {  // subList IndexOutOfBoundsException -> catch
+    b.max_sep = 0.0f;
+    b.pts.clear();
+    return;
+  }
+  b.pts.erase(b.pts.begin(), b.pts.begin() + trim);
+  b.max_sep = 0.0f;
+  for (size_t i = 1; i < b.pts.size(); ++i)
+    b.max_sep = (float)std::max((double)b.max_sep, jdistance(b.pts[i], b.pts[0]));
+}
+
+// trim target of a response body, as Batch.report parses it: -1 = findValue
+// returned null (trim all); -2 = the body did not parse (clear)
+int parse_trim(const char* body, size_t len) {
+  Value v;
+  std::string err;
+  if (!body || !otm::json::parse(std::string_view(body, len), &v, &err)) return -2;
+  const Value* su = find_value(v, "shape_used");
+  if (!su) return -1;
+  if (su->kind == Kind::Int && !su->bigint) return su->i < 0 ? -2 : (int)std::min<int64_t>(su->i, INT32_MAX);
+  if (su->kind == Kind::Float) return su->f < 0 ? -2 : (int)su->f;  // JsonNode.intValue truncates
+  return 0;  // non-numeric node: intValue() is 0
+}
+
+enum OpKind : uint8_t { OP_PROCESS = 0, OP_CLEAN = 1, OP_CLOSE = 2 };
+struct Op {
+  OpKind kind;
+  JPoint pt;
+  int64_t seq;  // stream position of the record (forward order)
+};
+
+struct KeyState {
+  std::string key;
+  JBatch batch;
+  bool in_store = false;
+  std::deque<Op> ops;
+  bool waiting = false;
+  bool queued = false;  // in the run queue
+  Op wop{};             // the op whose request is outstanding
+};
+
+struct Request {
+  uint32_t key;
+  std::string body;  // filled on the JSON path
+  int npts;
+};
+
+}  // namespace
+
+struct otm_batcher {
+  otm_engine* eng = nullptr;
+  otm_batcher_cfg cfg{};
+  otm_report_fn fn = nullptr;
+  void* ctx = nullptr;
+  std::unordered_map<std::string, uint32_t> index;
+  std::vector<KeyState> keys;
+  std::deque<std::pair<int64_t, uint32_t>> time_to_key;  // BatchingProcessor.time_to_key
+  int64_t seq = 0;
+  std::vector<uint32_t> runq;
+  std::vector<Request> reqs;
+  std::deque<otm_forward> out;
+  otm_batcher_stats st{};
+  std::string err;
+};
+
+namespace {
+
+uint32_t key_id(otm_batcher* B, const char* k, size_t n) {
+  std::string s(k, n);
+  auto it = B->index.find(s);
+  if (it != B->index.end()) return it->second;
+  const uint32_t id = (uint32_t)B->keys.size();
+  B->keys.emplace_back();
+  B->keys.back().key = s;
+  B->index.emplace(std::move(s), id);
+  return id;
+}
+
+void enqueue(otm_batcher* B, uint32_t k, const Op& op) {
+  KeyState& ks = B->keys[k];
+  ks.ops.push_back(op);
+  if (!ks.waiting && !ks.queued) {
+    ks.queued = true;
+    B->runq.push_back(k);
+  }
+}
+
+// Run a key's operations until one needs the matcher.
+void run_key(otm_batcher* B, uint32_t k) {
+  KeyState& ks = B->keys[k];
+  ks.queued = false;
+  while (!ks.waiting && !ks.ops.empty()) {
+    const Op op = ks.ops.front();
+    ks.ops.pop_front();
+    int min_dist, min_size;
+    int64_t min_elapsed;
+    if (op.kind == OP_PROCESS) {
+      if (!ks.in_store) {  // store.delete -> null: a new batch, no report
+        ks.batch = JBatch{};
+        ks.batch.pts.push_back(op.pt);
+        ks.in_store = true;
+        continue;
+      }
+      jupdate(ks.batch, op.pt);
+      min_dist = B->cfg.report_dist;
+      min_size = B->cfg.report_count;
+      min_elapsed = B->cfg.report_time_s;
+    } else {
+      if (!ks.in_store) {  // clean(): store.get -> null (the reference throws); close(): not iterated
+        if (op.kind == OP_CLEAN) B->st.null_batch_in_clean++;
+        continue;
+      }
+      min_dist = 0;
+      min_size = 2;
+      min_elapsed = 0;
+    }
+    if (!jgates(ks.batch, min_dist, min_size, min_elapsed)) {
+      // report() returned null: nothing forwarded; process() puts the batch back
+      continue;
+    }
+    ks.waiting = true;
+    ks.wop = op;
+    Request r;
+    r.key = k;
+    r.npts = (int)ks.batch.pts.size();
+    B->reqs.push_back(std::move(r));
+    return;
+  }
+}
+
+// Apply one response to its key (Batch.java:64-83, BatchingProcessor.java:69-81)
+void complete(otm_batcher* B, uint32_t k, int trim, int code, char* body, size_t body_len) {
+  KeyState& ks = B->keys[k];
+  if (trim == -2) {
+    ks.batch.max_sep = 0.0f;
+    ks.batch.pts.clear();
+  } else {
+    japply(ks.batch, trim);
+  }
+  (void)code;
+  if (ks.wop.kind == OP_PROCESS) {
+    // context.forward(key, response); store.put only if non-empty
+    otm_forward f;
+    f.key = (char*)std::malloc(ks.key.size() + 1);
+    std::memcpy(f.key, ks.key.data(), ks.key.size());
+    f.key[ks.key.size()] = 0;
+    f.key_len = ks.key.size();
+    f.body = body;
+    f.body_len = body_len;
+    f.seq = ks.wop.seq;
+    B->out.push_back(f);
+    B->st.forwarded++;
+    ks.in_store = !ks.batch.pts.empty();
+  } else {
+    // clean()/close() discard the response; the batch object stays in the
+    // store even when emptied (store.get returned it, nothing puts it back)
+    std::free(body);
+  }
+  ks.waiting = false;
+  if (!ks.ops.empty() && !ks.queued) {
+    ks.queued = true;
+    B->runq.push_back(k);
+  }
+}
+
+// The quantisation a point's coordinates go through on the JSON path:
+// DecimalFormat("###.######") in Java, json.loads in Python, float in the matcher
+float quantize(float v) {
+  std::string s;
+  otm::java_decimal6(v, &s);
+  return (float)std::strtod(s.c_str(), nullptr);
+}
+
+int issue_binary(otm_batcher* B, size_t r0, size_t r1) {
+  otm_engine* E = B->eng;
+  std::vector<int64_t> off(1, 0);
+  std::vector<float> lat, lon, acc;
+  std::vector<double> tm;
+  for (size_t i = r0; i < r1; ++i) {
+    const JBatch& jb = B->keys[B->reqs[i].key].batch;
+    for (const JPoint& p : jb.pts) {
+      lat.push_back(quantize(p.lat));
+      lon.push_back(quantize(p.lon));
+      tm.push_back((double)p.time);
+      acc.push_back((float)p.acc);
+    }
+    off.push_back((int64_t)lat.size());
+  }
+  otm_batch b;
+  b.n_traces = (int32_t)(r1 - r0);
+  b.n_points = off.back();
+  b.trace_off = off.data();
+  b.lat = lat.data();
+  b.lon = lon.data();
+  b.time = tm.data();
+  b.accuracy = acc.data();
+  std::string err;
+  otm_results res;
+  int rc;
+  {
+    std::lock_guard<std::mutex> lk(E->mu);
+    (void)hipSetDevice(E->device);
+    rc = otm::engine_match_host(E, &b, &err);
+    if (!rc) rc = otm::engine_fetch(E, &res, &err);
+    if (!rc) {
+      for (size_t i = r0; i < r1; ++i) {
+        const int32_t t = (int32_t)(i - r0);
+        const otm_trace_result& tr = res.traces[t];
+        // shape_used is written only when 200 and truthy (reporter_service.py:202)
+        const int trim = tr.code == 200 && tr.shape_used > 0 ? tr.shape_used : -1;
+        char* body = nullptr;
+        size_t blen = 0;
+        if (B->keys[B->reqs[i].key].wop.kind == OP_PROCESS) {
+          std::string s;
+          const int code = otm::write_report_response(res, t, &s);
+          (void)code;
+          body = (char*)std::malloc(s.size() + 1);
+          std::memcpy(body, s.data(), s.size());
+          body[s.size()] = 0;
+          blen = s.size();
+        }
+        complete(B, B->reqs[i].key, trim, tr.code, body, blen);
+      }
+    }
+  }
+  if (rc) {
+    // a device failure fails the batch like a 500 from the service: every
+    // request gets {"error":...}, whose missing shape_used clears its batch
+    for (size_t i = r0; i < r1; ++i) {
+      std::string s = otm::error_body(err);
+      char* body = nullptr;
+      size_t blen = 0;
+      if (B->keys[B->reqs[i].key].wop.kind == OP_PROCESS) {
+        body = (char*)std::malloc(s.size() + 1);
+        std::memcpy(body, s.data(), s.size() + 1);
+        blen = s.size();
+      }
+      complete(B, B->reqs[i].key, -1, 500, body, blen);
+    }
+  }
+  return OTM_OK;
+}
+
+int issue_json(otm_batcher* B, size_t r0, size_t r1) {
+  const int n = (int)(r1 - r0);
+  std::vector<const char*> rp((size_t)n);
+  std::vector<size_t> rl((size_t)n), ol((size_t)n);
+  std::vector<char*> outs((size_t)n, nullptr);
+  std::vector<int> codes((size_t)n, 0);
+  for (size_t i = r0; i < r1; ++i) {
+    KeyState& ks = B->keys[B->reqs[i].key];
+    std::vector<float> la, lo;
+    std::vector<int64_t> tm;
+    std::vector<int32_t> ac;
+    for (const JPoint& p : ks.batch.pts) {
+      la.push_back(p.lat);
+      lo.push_back(p.lon);
+      tm.push_back(p.time);
+      ac.push_back(p.acc);
+    }
+    char* body = nullptr;
+    size_t blen = 0;
+    otm_encode_request(ks.key.c_str(), (int)la.size(), la.data(), lo.data(), tm.data(), ac.data(), &body, &blen);
+    B->reqs[i].body.assign(body, blen);
+    std::free(body);
+    rp[i - r0] = B->reqs[i].body.data();
+    rl[i - r0] = B->reqs[i].body.size();
+  }
+  int rc = B->fn ? B->fn(B->ctx, n, rp.data(), rl.data(), outs.data(), ol.data(), codes.data())
+                 : otm_report_batch(B->eng, n, rp.data(), rl.data(), outs.data(), ol.data(), codes.data());
+  if (rc != OTM_OK) {
+    B->err = "matcher callback failed";
+    return rc;
+  }
+  for (size_t i = r0; i < r1; ++i) {
+    char* body = outs[i - r0];
+    const size_t blen = ol[i - r0];
+    const int trim = parse_trim(body, blen);
+    // a callback must hand back malloc'd bodies (otm_free releases them)
+    complete(B, B->reqs[i].key, trim, codes[i - r0], body, blen);
+  }
+  return OTM_OK;
+}
+
+int drain(otm_batcher* B) {
+  while (true) {
+    while (!B->runq.empty()) {
+      std::vector<uint32_t> q;
+      q.swap(B->runq);
+      for (uint32_t k : q) run_key(B, k);
+    }
+    if (B->reqs.empty()) return OTM_OK;
+    std::vector<Request> reqs;
+    reqs.swap(B->reqs);
+    B->reqs = std::move(reqs);
+    const size_t n = B->reqs.size();
+    const size_t chunk = B->cfg.max_batch > 0 ? (size_t)B->cfg.max_batch : n;
+    for (size_t r0 = 0; r0 < n; r0 += chunk) {
+      const size_t r1 = std::min(n, r0 + chunk);
+      for (size_t i = r0; i < r1; ++i) B->st.request_points += B->reqs[i].npts;
+      B->st.requests += (int64_t)(r1 - r0);
+      B->st.match_batches++;
+      int rc = (B->fn || B->cfg.json_path) ? issue_json(B, r0, r1) : issue_binary(B, r0, r1);
+      if (rc) return rc;
+    }
+    B->reqs.clear();
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+void otm_batcher_defaults(otm_batcher_cfg* c) {
+  c->report_dist = 500;           // BatchingProcessor.java:30
+  c->report_count = 10;           // :29
+  c->report_time_s = 60;          // :28
+  c->session_gap_ms = 60000;      // :31
+  c->max_batch = 0;
+  c->json_path = 0;
+}
+
+int otm_batcher_create(otm_engine* eng, const otm_batcher_cfg* cfg, otm_report_fn fn, void* ctx,
+                       otm_batcher** out) {
+  if (!out || (!eng && !fn)) return OTM_EINVAL;
+  auto* B = new otm_batcher();
+  B->eng = eng;
+  if (cfg) B->cfg = *cfg;
+  else otm_batcher_defaults(&B->cfg);
+  B->fn = fn;
+  B->ctx = ctx;
+  *out = B;
+  return OTM_OK;
+}
+
+void otm_batcher_destroy(otm_batcher* B) {
+  if (!B) return;
+  for (auto& f : B->out) {
+    std::free(f.key);
+    std::free(f.body);
+  }
+  delete B;
+}
+
+int otm_batcher_process(otm_batcher* B, int n, const char* const* keys, const size_t* key_lens, const float* lat,
+                        const float* lon, const int32_t* accuracy, const int64_t* time, const int64_t* ts_ms) {
+  if (!B || n < 0) return OTM_EINVAL;
+  for (int i = 0; i < n; ++i) {
+    const uint32_t k = key_id(B, keys[i], key_lens[i]);
+    const int64_t ts = ts_ms[i];
+    // clean(key): keys whose entry is older than the session gap, stalest
+    // first (BatchingProcessor.java:96-103)
+    while (!B->time_to_key.empty() && ts - B->time_to_key.front().first > B->cfg.session_gap_ms) {
+      const uint32_t kk = B->time_to_key.front().second;
+      B->time_to_key.pop_front();
+      Op c{};
+      c.kind = OP_CLEAN;
+      c.seq = B->seq;
+      enqueue(B, kk, c);
+      B->st.clean_ops++;
+    }
+    B->time_to_key.emplace_back(ts, k);  // (:106-111; the remove(iter) before it is a no-op)
+    Op p{};
+    p.kind = OP_PROCESS;
+    p.pt = JPoint{lat[i], lon[i], accuracy[i], time[i]};
+    p.seq = B->seq++;
+    enqueue(B, k, p);
+    B->st.records++;
+  }
+  if (B->cfg.max_pending > 0 && (int64_t)n > 0) {
+    int64_t pend = 0;
+    for (uint32_t k : B->runq) pend += (int64_t)B->keys[k].ops.size();
+    if (pend > B->cfg.max_pending) return drain(B);
+  }
+  return OTM_OK;
+}
+
+int otm_batcher_flush(otm_batcher* B) {
+  if (!B) return OTM_EINVAL;
+  return drain(B);
+}
+
+int otm_batcher_close(otm_batcher* B) {
+  if (!B) return OTM_EINVAL;
+  int rc = drain(B);
+  if (rc) return rc;
+  // store.all() of the in-memory store: keys in TreeMap (String) order
+  std::vector<uint32_t> ks;
+  for (uint32_t k = 0; k < (uint32_t)B->keys.size(); ++k)
+    if (B->keys[k].in_store) ks.push_back(k);
+  std::sort(ks.begin(), ks.end(), [&](uint32_t a, uint32_t b) { return B->keys[a].key < B->keys[b].key; });
+  for (uint32_t k : ks) {
+    Op c{};
+    c.kind = OP_CLOSE;
+    c.seq = B->seq;
+    enqueue(B, k, c);
+    B->st.close_ops++;
+  }
+  return drain(B);
+}
+
+int otm_batcher_take(otm_batcher* B, otm_forward* out, int max) {
+  if (!B || max < 0) return OTM_EINVAL;
+  int n = 0;
+  while (n < max && !B->out.empty()) {
+    out[n++] = B->out.front();
+    B->out.pop_front();
+  }
+  return n;
+}
+
+int otm_batcher_get_stats(const otm_batcher* B, otm_batcher_stats* s) {
+  if (!B || !s) return OTM_EINVAL;
+  *s = B->st;
+  int64_t stored = 0, pts = 0;
+  for (const KeyState& k : B->keys)
+    if (k.in_store) {
+      ++stored;
+      pts += (int64_t)k.batch.pts.size();
+    }
+  s->stored_batches = stored;
+  s->stored_points = pts;
+  s->keys = (int64_t)B->keys.size();
+  return OTM_OK;
+}
+
+int otm_batcher_batch(const otm_batcher* B, const char* key, size_t key_len, int max, float* lat, float* lon,
+                      int32_t* accuracy, int64_t* time, float* max_separation) {
+  if (!B || !key) return OTM_EINVAL;
+  auto it = B->index.find(std::string(key, key_len));
+  if (it == B->index.end() || !B->keys[it->second].in_store) return -1;
+  const JBatch& b = B->keys[it->second].batch;
+  const int n = (int)b.pts.size();
+  for (int i = 0; i < n && i < max; ++i) {
+    lat[i] = b.pts[(size_t)i].lat;
+    lon[i] = b.pts[(size_t)i].lon;
+    accuracy[i] = b.pts[(size_t)i].acc;
+    time[i] = b.pts[(size_t)i].time;
+  }
+  if (max_separation) *max_separation = b.max_sep;
+  return n;
+}
+
+}  // extern "C"

@@ -34,4 +34,7 @@ const char* trace_error_text(int kind);
 
 std::string error_body(const std::string& msg);
 
+// Java DecimalFormat("###.######") of a float (Point.java:29,41-42)
+void java_decimal6(float f, std::string* o);
+
 }  // namespace otm

@@ -1,0 +1,69 @@
+#!/usr/bin/env python3
+"""BASELINE config 5: the reference's batcher feeding the GPU matcher.
+
+The config-2 fleet (10k vehicles x 100 points, 5 s sampling) becomes one
+interleaved record stream ordered by record time -- what the `formatted`
+topic carries -- and goes through the native batcher (BatchingProcessor +
+Batch semantics, reporter_amd/csrc/batcher.cpp) with the engine as matcher.
+Reports sustained records/s (ingest) and matched points/s (sum of request
+trace lengths), with the request mix the reference's gates and its clean()
+quirk produce.  Prints one JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--vehicles", type=int, default=10000)
+    ap.add_argument("--points", type=int, default=100)
+    ap.add_argument("--chunk", type=int, default=200000, help="records per otm_batcher_process call")
+    ap.add_argument("--json-path", action="store_true")
+    ap.add_argument("--max-pending", type=int, default=0)
+    args = ap.parse_args()
+    import torch  # noqa: F401  (binds the HIP runtime torch ships)
+    from reporter_amd import Engine, synth
+    from reporter_amd.batcher import Batcher
+    graph = synth.cached_graph(2)
+    tr = dict(synth.CONFIGS[2]["traces"], n_vehicles=args.vehicles, points_per_vehicle=args.points)
+    b = synth.make_traces(graph, **tr)
+    nv, npt = args.vehicles, args.points
+    veh = np.repeat(np.arange(nv), npt)
+    t = b["time"].astype(np.int64) + (veh % 5)  # stagger the fleet a little
+    order = np.lexsort((veh, t))
+    keys = np.array(["veh%d" % v for v in range(nv)], dtype=object)[veh[order]]
+    lat, lon = b["lat"][order], b["lon"][order]
+    acc = np.ceil(b["accuracy"][order]).astype(np.int32)
+    tm = t[order]
+    ts = tm * 1000
+    with Engine(graph_path=graph) as eng:
+        bt = Batcher(engine=eng, json_path=args.json_path, max_pending=args.max_pending)
+        # warm the engine (allocations, code objects) outside the timed region
+        eng.match(synth.slice_batch(b, 0, min(100, nv)))
+        t0 = time.perf_counter()
+        n = len(keys)
+        for i in range(0, n, args.chunk):
+            j = min(n, i + args.chunk)
+            bt.process(list(keys[i:j]), lat[i:j], lon[i:j], acc[i:j], tm[i:j], ts[i:j])
+        bt.flush()
+        bt.close()
+        dt = time.perf_counter() - t0
+        st = bt.stats()
+        fwd = len(bt.forwarded())
+    line = {"metric": "config5 sustained ingest through the native batcher + GPU matcher",
+            "records_per_s": n / dt, "matched_points_per_s": st["request_points"] / dt, "seconds": dt,
+            "records": n, "forwarded": fwd, "path": "json" if args.json_path else "binary", "stats": st,
+            "workload": "config-2 fleet (%d vehicles x %d points, 5 s) as one time-ordered stream" % (nv, npt)}
+    print(json.dumps(line), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,125 @@
+"""The native batcher (otm_batcher, BatchingProcessor + Batch restated in C++)
+against the serial Python restatement in oracle/pybatcher.py.
+
+The native batcher runs every key's operations in the reference's serial
+order but sends the requests of all ready keys to the matcher together; the
+Python one runs record by record with a synchronous matcher, as the Java host
+does.  Same stream, same matcher => the same forwarded (record, key, response)
+triples, the same requests, the same final store.  CPU: the matcher is the
+CPU oracle's /report handler; GPU (test_gpu_batcher.py): the engine.
+"""
+import numpy as np
+import pytest
+
+from reporter_amd import synth
+from reporter_amd.batcher import Batcher
+
+
+def make_stream(graph, n_veh=24, n_pts=70, seed=41):
+    """Interleaved records (key, lat, lon, accuracy, time, ts_ms) ordered by
+    record time, with session gaps and an off-network vehicle."""
+    b = synth.make_traces(graph, n_veh, n_pts, interval_s=5.0, noise_sigma_m=15.0, accuracy=15.0, seed=seed)
+    recs = []
+    for v in range(n_veh):
+        a, e = b["trace_off"][v], b["trace_off"][v + 1]
+        for k, i in enumerate(range(a, e)):
+            t = int(b["time"][i]) + 3 * v
+            if v % 5 == 1 and k >= n_pts // 2:
+                t += 150  # idle longer than the session gap, then resume
+            lat, lon = float(b["lat"][i]), float(b["lon"][i])
+            if v == 3:
+                lat += 0.5  # off the network: empty matches, shape_used None -> batch cleared
+            recs.append(("veh%02d" % v, lat, lon, int(np.ceil(b["accuracy"][i])), t))
+    recs.sort(key=lambda r: (r[4], r[0]))
+    return recs
+
+
+def run_python(recs, post):
+    from oracle import pybatcher
+    bp = pybatcher.BatchingProcessor(post)
+    for key, lat, lon, acc, t in recs:
+        bp.process(key, pybatcher.Point(lat, lon, acc, t), t * 1000)
+    bp.close()
+    return bp
+
+
+def run_native(recs, batcher, chunk=97):
+    for i in range(0, len(recs), chunk):
+        part = recs[i:i + chunk]
+        batcher.process([r[0] for r in part], [r[1] for r in part], [r[2] for r in part], [r[3] for r in part],
+                        [r[4] for r in part], [r[4] * 1000 for r in part])
+    batcher.close()
+    return batcher
+
+
+def compare(bp, nb, recs):
+    fwd = sorted(nb.forwarded())
+    ref = sorted((s, k, r) for s, k, r in bp.forwarded)
+    assert len(fwd) == len(ref)
+    for a, b in zip(fwd, ref):
+        assert a == b
+    st = nb.stats()
+    assert st["records"] == len(recs)
+    assert st["requests"] == bp.requests
+    assert st["null_batch_in_clean"] == bp.null_batch_in_clean
+    assert st["stored_batches"] == len(bp.store)
+    for key, batch in bp.store.items():
+        got = nb.batch(key)
+        assert got is not None
+        pts, ms = got
+        assert np.float32(ms) == batch.max_separation
+        assert [(np.float32(a), np.float32(b), c, d) for a, b, c, d in pts] == \
+            [(p.lat, p.lon, p.accuracy, p.time) for p in batch.points]
+    return st
+
+
+def test_native_batcher_matches_serial_restatement(small_graph, oracle):
+    g = oracle.Graph(small_graph)
+    post = lambda body: oracle.handle_request(g, body)[1]  # noqa: E731
+    recs = make_stream(small_graph)
+    bp = run_python(recs, post)
+    nb = run_native(recs, Batcher(handler=lambda bodies: [oracle.handle_request(g, x) for x in bodies]))
+    st = compare(bp, nb, recs)
+    # the stream exercised every path: gated reports, relaxed clean() reports,
+    # emptied batches, the reference's clean() null case, close()
+    assert st["forwarded"] > 10 and st["clean_ops"] > 100 and st["close_ops"] > 0, st
+    assert bp.null_batch_in_clean > 0
+    assert st["match_batches"] < st["requests"]  # requests of several keys shared matcher calls
+
+
+@pytest.mark.parametrize("max_batch", [1, 5])
+def test_native_batcher_batch_limits(small_graph, oracle, max_batch):
+    g = oracle.Graph(small_graph)
+    recs = make_stream(small_graph, n_veh=10, n_pts=40, seed=43)
+    bp = run_python(recs, lambda body: oracle.handle_request(g, body)[1])
+    nb = run_native(recs, Batcher(handler=lambda bodies: [oracle.handle_request(g, x) for x in bodies],
+                                  max_batch=max_batch), chunk=13)
+    compare(bp, nb, recs)
+
+
+def test_request_bytes_match_java_encoding():
+    """Point.Serder.put_json + Batch.report's body (Batch.java:52-61) from the
+    restatement agree with the product encoder on awkward values."""
+    from oracle import pybatcher
+    from reporter_amd import encode_request
+    vals = [37.98, -0.5, 0.0, 1.0000005, 14.543087, 121.021019, -122.4194155, 0.0000004, -0.0000006, 179.9999995]
+    b = pybatcher.Batch()
+    for i, v in enumerate(vals):
+        b.points.append(pybatcher.Point(v, -v / 2, i, 1500000000 + i))
+    got = encode_request("k1", [p.lat for p in b.points], [p.lon for p in b.points], [p.time for p in b.points],
+                         [p.accuracy for p in b.points])
+    assert got == b.body("k1")
+
+
+def test_gates_and_trim_unit():
+    """Batch.report gates (Batch.java:48-50) and the shape_used trim (:64-76)."""
+    from oracle import pybatcher
+    resp = {"v": '{"stats":{},"shape_used":3,"segment_matcher":{}}'}
+    b = pybatcher.Batch(pybatcher.Point(37.0, -122.0, 5, 1000))
+    for i in range(1, 12):
+        b.update(pybatcher.Point(37.0 + 0.001 * i, -122.0, 5, 1000 + 10 * i))
+    assert b.max_separation > 1000
+    assert b.report("k", lambda body: resp["v"], 500, 10, 60) is not None
+    assert len(b.points) == 9
+    resp["v"] = '{"error":"boom"}'  # no shape_used: everything trimmed
+    assert b.report("k", lambda body: resp["v"], 0, 2, 0) is not None and b.points == []

@@ -1,0 +1,22 @@
+"""The native batcher on the GPU engine: its binary fast path (SoA batches,
+responses written only for forwarded records) and its JSON path (the exact
+request bodies through otm_report_batch) against the serial Python
+restatement of BatchingProcessor posting each body to Engine.report."""
+import pytest
+
+from reporter_amd import Engine
+from reporter_amd.batcher import Batcher
+
+from test_batcher import compare, make_stream, run_native, run_python
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("json_path", [False, True], ids=["binary", "json"])
+def test_gpu_batcher_matches_serial_restatement(small_graph, json_path):
+    recs = make_stream(small_graph, n_veh=30, n_pts=80, seed=47)
+    with Engine(graph_path=small_graph) as eng:
+        bp = run_python(recs, lambda body: eng.report(body)[1])
+        nb = run_native(recs, Batcher(engine=eng, json_path=json_path))
+        st = compare(bp, nb, recs)
+        assert st["forwarded"] > 10 and st["match_batches"] < st["requests"]

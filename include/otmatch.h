@@ -40,6 +40,7 @@ extern "C" {
 #define OTM_EDEVICE (-3)  /* HIP runtime error (no device, OOM, fault)      */
 #define OTM_ECONFIG (-4)  /* env config rejected (reporter_service.py:55-62) */
 #define OTM_EAGAIN (-5)   /* async queue full                               */
+#define OTM_ENOMEM (-6)   /* host allocation failed                         */
 
 typedef struct otm_engine otm_engine;
 
@@ -335,12 +336,60 @@ typedef struct otm_batcher_stats {
   int64_t records, clean_ops, close_ops, requests, request_points, match_batches, forwarded;
   int64_t null_batch_in_clean; /* clean() on a key with no stored batch: the reference throws */
   int64_t keys, stored_batches, stored_points;
+  /* host time (us) in: queueing records, running keys' operations, building
+   * the matcher batches, the matcher itself, applying responses */
+  int64_t us_enqueue, us_run, us_prepare, us_match, us_apply;
+  /* otm_batcher_process_raw: messages in, messages the formatter dropped,
+   * host time (us) formatting */
+  int64_t raw_messages, raw_dropped, us_format;
 } otm_batcher_stats;
 int otm_batcher_get_stats(const otm_batcher* b, otm_batcher_stats* out);
 /* A key's stored batch (points in order, max_separation); returns its size
  * (copies at most max points) or -1 when the store has no batch for it. */
 int otm_batcher_batch(const otm_batcher* b, const char* key, size_t key_len, int max, float* lat, float* lon,
                       int32_t* accuracy, int64_t* time, float* max_separation);
+
+/* ------------------------------------------------------- ingest formatter */
+/* The reference's raw-message Formatter, native:
+ * src/main/java/org/opentraffic/reporter/Formatter.java.  `spec` is the
+ * --formatter string (Reporter.java:33-43, Formatter.GetFormatter :36-51):
+ *   "<c>sv<c><separator regex><c>uuid<c>lat<c>lon<c>time<c>accuracy[<c>time pattern]"
+ *   "<c>json<c>uuid key<c>lat key<c>lon key<c>time key<c>accuracy key[<c>time pattern]"
+ * with <c> the spec's own first character.  Fails (OTM_EINVAL, message in
+ * err) where GetFormatter throws, and for separator regexes / joda patterns
+ * outside the supported subset (reporter_amd/csrc/formatter.h). */
+typedef struct otm_formatter otm_formatter;
+int otm_formatter_create(const char* spec, otm_formatter** out, char* err, size_t err_len);
+void otm_formatter_destroy(otm_formatter* f);
+/* Formatter.format (:86-124) of n raw messages, message i = msgs[off[i],
+ * off[i+1]).  ok[i] = 0 where the reference throws and
+ * KeyedFormattingProcessor (:30-37) logs and drops the message.  Key i (the
+ * uuid) = keys[key_off[i], key_off[i+1]).  Arrays are library-owned: release
+ * with otm_formatted_free.  nthreads > 1 splits large calls across threads. */
+typedef struct otm_formatted {
+  int32_t n, n_ok;
+  uint8_t* ok;
+  int64_t* key_off;
+  char* keys;
+  float* lat;
+  float* lon;
+  int32_t* accuracy;
+  int64_t* time;
+} otm_formatted;
+int otm_format(const otm_formatter* f, int32_t n, const char* msgs, const int64_t* off, int nthreads,
+               otm_formatted* out);
+void otm_formatted_free(otm_formatted* r);
+/* KeyedFormattingProcessor -> BatchingProcessor: format n raw messages and
+ * feed every formatted one to the batcher (otm_batcher_process), message i
+ * with record timestamp ts_ms[i]; dropped messages are counted (raw_dropped). */
+int otm_batcher_process_raw(otm_batcher* b, const otm_formatter* f, int32_t n, const char* msgs,
+                            const int64_t* off, const int64_t* ts_ms, int nthreads);
+
+/* The coordinate a request body carries to the matcher: DecimalFormat
+ * ("###.######", HALF_EVEN on the exact value; Point.java:29) parsed back to
+ * float.  The batcher's binary path applies it so that it matches what the
+ * JSON path (and the reference's HTTP hop) delivers. */
+void otm_quantize_decimal6(const float* in, float* out, int64_t n);
 
 /* --------------------------------------------------- synthetic inputs ---- */
 /* Harness tooling, not the hot path: the seeded synthetic road network and

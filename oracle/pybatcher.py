@@ -20,7 +20,7 @@ notice).
 import json
 import math
 from collections import deque
-from decimal import ROUND_HALF_EVEN, Decimal
+from decimal import ROUND_HALF_EVEN, Context, Decimal
 
 import numpy as np
 
@@ -31,7 +31,7 @@ METERS_PER_DEG = 20037581.187 / 180.0
 
 def decimal6(v):
     """DecimalFormat("###.######") of a float (Point.java:29)."""
-    d = Decimal(float(f32(v))).quantize(Decimal("0.000001"), rounding=ROUND_HALF_EVEN)
+    d = Decimal(float(f32(v))).quantize(Decimal("0.000001"), rounding=ROUND_HALF_EVEN, context=Context(prec=400))
     s = format(d, "f")
     neg = s.startswith("-")
     if neg:

@@ -59,11 +59,18 @@ class Forward(C.Structure):
 
 
 BATCHER_STATS = ("records", "clean_ops", "close_ops", "requests", "request_points", "match_batches", "forwarded",
-                 "null_batch_in_clean", "keys", "stored_batches", "stored_points")
+                 "null_batch_in_clean", "keys", "stored_batches", "stored_points", "us_enqueue", "us_run",
+                 "us_prepare", "us_match", "us_apply", "raw_messages", "raw_dropped", "us_format")
 
 
 class BatcherStats(C.Structure):
     _fields_ = [(n, C.c_int64) for n in BATCHER_STATS]
+
+
+class Formatted(C.Structure):
+    _fields_ = [("n", C.c_int32), ("n_ok", C.c_int32), ("ok", C.c_void_p), ("key_off", C.c_void_p),
+                ("keys", C.c_void_p), ("lat", C.c_void_p), ("lon", C.c_void_p), ("accuracy", C.c_void_p),
+                ("time", C.c_void_p)]
 
 
 # int (*otm_report_fn)(void* ctx, int n, const char* const* reqs, const size_t* lens, char** resps,
@@ -143,6 +150,12 @@ def _declare(L):
         "otm_batcher_take": (C.c_int, [vp, C.POINTER(Forward), C.c_int]),
         "otm_batcher_get_stats": (C.c_int, [vp, C.POINTER(BatcherStats)]),
         "otm_batcher_batch": (C.c_int, [vp, C.c_char_p, sz, C.c_int, vp, vp, vp, vp, C.POINTER(C.c_float)]),
+        "otm_quantize_decimal6": (None, [vp, vp, C.c_int64]),
+        "otm_formatter_create": (C.c_int, [C.c_char_p, C.POINTER(vp), C.c_char_p, sz]),
+        "otm_formatter_destroy": (None, [vp]),
+        "otm_format": (C.c_int, [vp, C.c_int32, vp, vp, C.c_int, C.POINTER(Formatted)]),
+        "otm_formatted_free": (None, [C.POINTER(Formatted)]),
+        "otm_batcher_process_raw": (C.c_int, [vp, vp, C.c_int32, vp, vp, vp, C.c_int]),
         "otm_synth_graph_defaults": (None, [C.POINTER(SynthGraphParams)]),
         "otm_synth_graph": (C.c_int, [C.POINTER(SynthGraphParams), C.c_char_p]),
         "otm_synth_traces": (C.c_int, [C.c_char_p, C.POINTER(SynthTraceParams), vp, vp, vp, vp, vp, vp, vp]),

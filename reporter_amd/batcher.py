@@ -18,6 +18,18 @@ from . import _lib
 from ._lib import lib
 
 
+class KeyBlock(object):
+    """Record keys packed for otm_batcher_process (char* array + lengths), so a
+    caller replaying a stream can pay the conversion once."""
+
+    def __init__(self, keys):
+        kb = [k.encode("utf-8") if isinstance(k, str) else k for k in keys]
+        self.n = len(kb)
+        self._keep = kb
+        self.arr = (C.c_char_p * self.n)(*kb)
+        self.lens = (C.c_size_t * self.n)(*[len(k) for k in kb])
+
+
 class Batcher(object):
     def __init__(self, engine=None, handler=None, json_path=False, max_batch=0, **cfg):
         if engine is None and handler is None:
@@ -56,11 +68,10 @@ class Batcher(object):
         self.close_handle()
 
     def process(self, keys, lat, lon, accuracy, time, ts_ms):
-        """Records in stream order (BatchingProcessor.process)."""
-        kb = [k.encode("utf-8") if isinstance(k, str) else k for k in keys]
-        n = len(kb)
-        arr = (C.c_char_p * n)(*kb)
-        lens = (C.c_size_t * n)(*[len(k) for k in kb])
+        """Records in stream order (BatchingProcessor.process); keys: strings,
+        bytes or a KeyBlock."""
+        kb = keys if isinstance(keys, KeyBlock) else KeyBlock(keys)
+        n, arr, lens = kb.n, kb.arr, kb.lens
         lat = np.ascontiguousarray(lat, np.float32)
         lon = np.ascontiguousarray(lon, np.float32)
         acc = np.ascontiguousarray(accuracy, np.int32)
@@ -70,6 +81,19 @@ class Batcher(object):
                                        tm.ctypes.data, ts.ctypes.data)
         if rc != 0:
             raise RuntimeError("otm_batcher_process failed (%d)" % rc)
+
+    def process_raw(self, formatter, messages, ts_ms, nthreads=1):
+        """Raw messages through the formatter into the batcher (the
+        KeyedFormattingProcessor -> BatchingProcessor topology, Reporter.java:95-103)."""
+        from .formatter import pack_messages
+        buf, off = pack_messages(messages)
+        ts = np.ascontiguousarray(ts_ms, np.int64)
+        if len(ts) != len(off) - 1:
+            raise ValueError("one record timestamp per message")
+        rc = lib().otm_batcher_process_raw(self.h, formatter.h, len(ts), buf.ctypes.data, off.ctypes.data,
+                                           ts.ctypes.data, nthreads)
+        if rc != 0:
+            raise RuntimeError("otm_batcher_process_raw failed (%d)" % rc)
 
     def flush(self):
         if lib().otm_batcher_flush(self.h) != 0:

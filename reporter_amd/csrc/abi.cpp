@@ -59,6 +59,10 @@ void fill_device_params(otm_engine* E) {
   // default: all three (measured on config 2: candidates 0.60 -> 0.44 ms,
   // route 0.107 -> 0.089, transitions 0.408 -> 0.388)
   E->dp.order_mask = om ? (int)std::strtol(om, nullptr, 0) : otm::ORDER_CAND | otm::ORDER_TRANS | otm::ORDER_ROUTE;
+  E->dp.cand_wave_all = 0;
+  // batches under this many points take the small-batch (latency) path
+  const char* sp = std::getenv("OTM_SMALL_POINTS");
+  E->small_points = sp ? (int64_t)std::strtoll(sp, nullptr, 0) : 65536;
   const otm::ReportConfig& r = E->rc;
   std::memset(&E->drc, 0, sizeof E->drc);
   E->drc.n_report = (int)std::min<size_t>(r.report_levels.size(), 16);

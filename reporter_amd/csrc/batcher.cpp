@@ -27,12 +27,14 @@
 // known when its records arrive.  Requests of all runnable keys go to the
 // matcher together: one GPU batch per round.
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <map>
 #include <string>
+#include <string_view>
 #include <unordered_map>
 #include <vector>
 
@@ -126,6 +128,7 @@ int parse_trim(const char* body, size_t len) {
 
 enum OpKind : uint8_t { OP_PROCESS = 0, OP_CLEAN = 1, OP_CLOSE = 2 };
 struct Op {
+  uint32_t key;
   OpKind kind;
   JPoint pt;
   int64_t seq;  // stream position of the record (forward order)
@@ -135,7 +138,7 @@ struct KeyState {
   std::string key;
   JBatch batch;
   bool in_store = false;
-  std::deque<Op> ops;
+  uint32_t ob = 0, oe = 0;  // pending operations: otm_batcher::ops[ob, oe)
   bool waiting = false;
   bool queued = false;  // in the run queue
   Op wop{};             // the op whose request is outstanding
@@ -154,10 +157,14 @@ struct otm_batcher {
   otm_batcher_cfg cfg{};
   otm_report_fn fn = nullptr;
   void* ctx = nullptr;
-  std::unordered_map<std::string, uint32_t> index;
+  std::deque<std::string> key_text;                    // stable storage behind the index's views
+  std::unordered_map<std::string_view, uint32_t> index;  // record key -> keys[]
   std::vector<KeyState> keys;
   std::deque<std::pair<int64_t, uint32_t>> time_to_key;  // BatchingProcessor.time_to_key
   int64_t seq = 0;
+  std::vector<Op> log;       // operations in stream order since the last drain
+  std::vector<Op> ops;       // ... grouped by key (stable), each key's range in KeyState
+  std::vector<uint32_t> cnt;
   std::vector<uint32_t> runq;
   std::vector<Request> reqs;
   std::deque<otm_forward> out;
@@ -168,22 +175,53 @@ struct otm_batcher {
 namespace {
 
 uint32_t key_id(otm_batcher* B, const char* k, size_t n) {
-  std::string s(k, n);
-  auto it = B->index.find(s);
+  auto it = B->index.find(std::string_view(k, n));
   if (it != B->index.end()) return it->second;
   const uint32_t id = (uint32_t)B->keys.size();
+  B->key_text.emplace_back(k, n);
   B->keys.emplace_back();
-  B->keys.back().key = s;
-  B->index.emplace(std::move(s), id);
+  B->keys.back().key = B->key_text.back();
+  B->index.emplace(std::string_view(B->key_text.back()), id);
   return id;
 }
 
 void enqueue(otm_batcher* B, uint32_t k, const Op& op) {
-  KeyState& ks = B->keys[k];
-  ks.ops.push_back(op);
-  if (!ks.waiting && !ks.queued) {
-    ks.queued = true;
-    B->runq.push_back(k);
+  B->log.push_back(op);
+  B->log.back().key = k;
+}
+
+// Group the log by key (a stable counting sort: each key's operations stay in
+// stream order, after any it still had pending) and queue every key that can run.
+void distribute(otm_batcher* B) {
+  const size_t nk = B->keys.size();
+  B->cnt.assign(nk + 1, 0);
+  size_t total = B->log.size();
+  for (size_t k = 0; k < nk; ++k) {
+    const KeyState& ks = B->keys[k];
+    B->cnt[k] = ks.oe - ks.ob;
+    total += B->cnt[k];
+  }
+  for (const Op& op : B->log) B->cnt[op.key]++;
+  std::vector<Op> ops(total);
+  uint32_t run = 0;
+  for (size_t k = 0; k < nk; ++k) {
+    KeyState& ks = B->keys[k];
+    const uint32_t c = B->cnt[k];
+    std::copy(B->ops.begin() + ks.ob, B->ops.begin() + ks.oe, ops.begin() + run);
+    B->cnt[k] = run + (ks.oe - ks.ob);  // write cursor for the new operations
+    ks.ob = run;
+    ks.oe = run + c;
+    run += c;
+  }
+  for (const Op& op : B->log) ops[B->cnt[op.key]++] = op;
+  B->ops.swap(ops);
+  B->log.clear();
+  for (uint32_t k = 0; k < (uint32_t)nk; ++k) {
+    KeyState& ks = B->keys[k];
+    if (ks.ob < ks.oe && !ks.waiting && !ks.queued) {
+      ks.queued = true;
+      B->runq.push_back(k);
+    }
   }
 }
 
@@ -191,9 +229,8 @@ void enqueue(otm_batcher* B, uint32_t k, const Op& op) {
 void run_key(otm_batcher* B, uint32_t k) {
   KeyState& ks = B->keys[k];
   ks.queued = false;
-  while (!ks.waiting && !ks.ops.empty()) {
-    const Op op = ks.ops.front();
-    ks.ops.pop_front();
+  while (!ks.waiting && ks.ob < ks.oe) {
+    const Op op = B->ops[ks.ob++];
     int min_dist, min_size;
     int64_t min_elapsed;
     if (op.kind == OP_PROCESS) {
@@ -259,30 +296,51 @@ void complete(otm_batcher* B, uint32_t k, int trim, int code, char* body, size_t
     std::free(body);
   }
   ks.waiting = false;
-  if (!ks.ops.empty() && !ks.queued) {
+  if (ks.ob < ks.oe && !ks.queued) {
     ks.queued = true;
     B->runq.push_back(k);
   }
 }
 
+int64_t now_us() {
+  return std::chrono::duration_cast<std::chrono::microseconds>(
+             std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+}  // namespace
+
+namespace otm {
 // The quantisation a point's coordinates go through on the JSON path:
-// DecimalFormat("###.######") in Java, json.loads in Python, float in the matcher
-float quantize(float v) {
+// DecimalFormat("###.######") in Java, json.loads in Python, float in the
+// matcher.  Without the string: a float has 24 significant bits and 1e6 =
+// 2^6 * 15625 needs 14, so v * 1e6 is exact in double; nearbyint (round to
+// nearest, ties to even) is HALF_EVEN on the exact value; n / 1e6 with both
+// operands exact is the correctly rounded double of the decimal n * 10^-6,
+// which is what strtod returns for its text.  The string form stays for
+// values the shortcut does not cover (|v| * 1e6 >= 2^53, NaN, Inf).
+float quantize_decimal6(float v) {
+  const double d = (double)v * 1e6;
+  if (std::fabs(d) < 9.0e15) return (float)(std::nearbyint(d) / 1e6);
   std::string s;
-  otm::java_decimal6(v, &s);
+  java_decimal6(v, &s);
   return (float)std::strtod(s.c_str(), nullptr);
 }
+}  // namespace otm
+
+namespace {
 
 int issue_binary(otm_batcher* B, size_t r0, size_t r1) {
   otm_engine* E = B->eng;
+  const int64_t t0 = now_us();
   std::vector<int64_t> off(1, 0);
   std::vector<float> lat, lon, acc;
   std::vector<double> tm;
   for (size_t i = r0; i < r1; ++i) {
     const JBatch& jb = B->keys[B->reqs[i].key].batch;
     for (const JPoint& p : jb.pts) {
-      lat.push_back(quantize(p.lat));
-      lon.push_back(quantize(p.lon));
+      lat.push_back(otm::quantize_decimal6(p.lat));
+      lon.push_back(otm::quantize_decimal6(p.lon));
       tm.push_back((double)p.time);
       acc.push_back((float)p.acc);
     }
@@ -302,8 +360,12 @@ int issue_binary(otm_batcher* B, size_t r0, size_t r1) {
   {
     std::lock_guard<std::mutex> lk(E->mu);
     (void)hipSetDevice(E->device);
+    const int64_t t1 = now_us();
+    B->st.us_prepare += t1 - t0;
     rc = otm::engine_match_host(E, &b, &err);
     if (!rc) rc = otm::engine_fetch(E, &res, &err);
+    const int64_t t2 = now_us();
+    B->st.us_match += t2 - t1;
     if (!rc) {
       for (size_t i = r0; i < r1; ++i) {
         const int32_t t = (int32_t)(i - r0);
@@ -324,6 +386,7 @@ int issue_binary(otm_batcher* B, size_t r0, size_t r1) {
         complete(B, B->reqs[i].key, trim, tr.code, body, blen);
       }
     }
+    B->st.us_apply += now_us() - t2;
   }
   if (rc) {
     // a device failure fails the batch like a 500 from the service: every
@@ -344,6 +407,7 @@ int issue_binary(otm_batcher* B, size_t r0, size_t r1) {
 }
 
 int issue_json(otm_batcher* B, size_t r0, size_t r1) {
+  const int64_t t0 = now_us();
   const int n = (int)(r1 - r0);
   std::vector<const char*> rp((size_t)n);
   std::vector<size_t> rl((size_t)n), ol((size_t)n);
@@ -368,8 +432,12 @@ int issue_json(otm_batcher* B, size_t r0, size_t r1) {
     rp[i - r0] = B->reqs[i].body.data();
     rl[i - r0] = B->reqs[i].body.size();
   }
+  const int64_t t1 = now_us();
+  B->st.us_prepare += t1 - t0;
   int rc = B->fn ? B->fn(B->ctx, n, rp.data(), rl.data(), outs.data(), ol.data(), codes.data())
                  : otm_report_batch(B->eng, n, rp.data(), rl.data(), outs.data(), ol.data(), codes.data());
+  const int64_t t2 = now_us();
+  B->st.us_match += t2 - t1;
   if (rc != OTM_OK) {
     B->err = "matcher callback failed";
     return rc;
@@ -381,16 +449,44 @@ int issue_json(otm_batcher* B, size_t r0, size_t r1) {
     // a callback must hand back malloc'd bodies (otm_free releases them)
     complete(B, B->reqs[i].key, trim, codes[i - r0], body, blen);
   }
+  B->st.us_apply += now_us() - t2;
   return OTM_OK;
 }
 
+// One formatted record (BatchingProcessor.process, :56-85): the clean()
+// pops its timestamp causes, then the record's own operation.
+void ingest(otm_batcher* B, const char* key, size_t key_len, const JPoint& pt, int64_t ts) {
+  const uint32_t k = key_id(B, key, key_len);
+  // clean(key): keys whose entry is older than the session gap, stalest
+  // first (BatchingProcessor.java:96-103)
+  while (!B->time_to_key.empty() && ts - B->time_to_key.front().first > B->cfg.session_gap_ms) {
+    const uint32_t kk = B->time_to_key.front().second;
+    B->time_to_key.pop_front();
+    Op c{};
+    c.kind = OP_CLEAN;
+    c.seq = B->seq;
+    enqueue(B, kk, c);
+    B->st.clean_ops++;
+  }
+  B->time_to_key.emplace_back(ts, k);  // (:106-111; the remove(iter) before it is a no-op)
+  Op p{};
+  p.kind = OP_PROCESS;
+  p.pt = pt;
+  p.seq = B->seq++;
+  enqueue(B, k, p);
+  B->st.records++;
+}
+
 int drain(otm_batcher* B) {
+  distribute(B);
   while (true) {
+    const int64_t t0 = now_us();
     while (!B->runq.empty()) {
       std::vector<uint32_t> q;
       q.swap(B->runq);
       for (uint32_t k : q) run_key(B, k);
     }
+    B->st.us_run += now_us() - t0;
     if (B->reqs.empty()) return OTM_OK;
     std::vector<Request> reqs;
     reqs.swap(B->reqs);
@@ -447,33 +543,33 @@ void otm_batcher_destroy(otm_batcher* B) {
 int otm_batcher_process(otm_batcher* B, int n, const char* const* keys, const size_t* key_lens, const float* lat,
                         const float* lon, const int32_t* accuracy, const int64_t* time, const int64_t* ts_ms) {
   if (!B || n < 0) return OTM_EINVAL;
-  for (int i = 0; i < n; ++i) {
-    const uint32_t k = key_id(B, keys[i], key_lens[i]);
-    const int64_t ts = ts_ms[i];
-    // clean(key): keys whose entry is older than the session gap, stalest
-    // first (BatchingProcessor.java:96-103)
-    while (!B->time_to_key.empty() && ts - B->time_to_key.front().first > B->cfg.session_gap_ms) {
-      const uint32_t kk = B->time_to_key.front().second;
-      B->time_to_key.pop_front();
-      Op c{};
-      c.kind = OP_CLEAN;
-      c.seq = B->seq;
-      enqueue(B, kk, c);
-      B->st.clean_ops++;
-    }
-    B->time_to_key.emplace_back(ts, k);  // (:106-111; the remove(iter) before it is a no-op)
-    Op p{};
-    p.kind = OP_PROCESS;
-    p.pt = JPoint{lat[i], lon[i], accuracy[i], time[i]};
-    p.seq = B->seq++;
-    enqueue(B, k, p);
-    B->st.records++;
+  const int64_t t0 = now_us();
+  for (int i = 0; i < n; ++i)
+    ingest(B, keys[i], key_lens[i], JPoint{lat[i], lon[i], accuracy[i], time[i]}, ts_ms[i]);
+  B->st.us_enqueue += now_us() - t0;
+  if (B->cfg.max_pending > 0 && (int64_t)B->log.size() > B->cfg.max_pending) return drain(B);
+  return OTM_OK;
+}
+
+int otm_batcher_process_raw(otm_batcher* B, const otm_formatter* f, int32_t n, const char* msgs, const int64_t* off,
+                            const int64_t* ts_ms, int nthreads) {
+  if (!B || !f || n < 0 || (n > 0 && !ts_ms)) return OTM_EINVAL;
+  const int64_t t0 = now_us();
+  otm_formatted r;
+  int rc = otm_format(f, n, msgs, off, nthreads, &r);
+  if (rc) return rc;
+  const int64_t t1 = now_us();
+  B->st.us_format += t1 - t0;
+  B->st.raw_messages += n;
+  B->st.raw_dropped += n - r.n_ok;
+  for (int32_t i = 0; i < n; ++i) {
+    if (!r.ok[i]) continue;
+    ingest(B, r.keys + r.key_off[i], (size_t)(r.key_off[i + 1] - r.key_off[i]),
+           JPoint{r.lat[i], r.lon[i], r.accuracy[i], r.time[i]}, ts_ms[i]);
   }
-  if (B->cfg.max_pending > 0 && (int64_t)n > 0) {
-    int64_t pend = 0;
-    for (uint32_t k : B->runq) pend += (int64_t)B->keys[k].ops.size();
-    if (pend > B->cfg.max_pending) return drain(B);
-  }
+  otm_formatted_free(&r);
+  B->st.us_enqueue += now_us() - t1;
+  if (B->cfg.max_pending > 0 && (int64_t)B->log.size() > B->cfg.max_pending) return drain(B);
   return OTM_OK;
 }
 
@@ -499,6 +595,10 @@ int otm_batcher_close(otm_batcher* B) {
     B->st.close_ops++;
   }
   return drain(B);
+}
+
+void otm_quantize_decimal6(const float* in, float* out, int64_t n) {
+  for (int64_t i = 0; i < n; ++i) out[i] = otm::quantize_decimal6(in[i]);
 }
 
 int otm_batcher_take(otm_batcher* B, otm_forward* out, int max) {
@@ -529,7 +629,7 @@ int otm_batcher_get_stats(const otm_batcher* B, otm_batcher_stats* s) {
 int otm_batcher_batch(const otm_batcher* B, const char* key, size_t key_len, int max, float* lat, float* lon,
                       int32_t* accuracy, int64_t* time, float* max_separation) {
   if (!B || !key) return OTM_EINVAL;
-  auto it = B->index.find(std::string(key, key_len));
+  auto it = B->index.find(std::string_view(key, key_len));
   if (it == B->index.end() || !B->keys[it->second].in_store) return -1;
   const JBatch& b = B->keys[it->second].batch;
   const int n = (int)b.pts.size();

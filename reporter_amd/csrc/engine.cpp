@@ -275,6 +275,15 @@ static int engine_match_once(otm_engine* E, const DevBatch& b, hipStream_t s, st
   }
   ENS(path_pool, (size_t)E->pool_cap * 4);
 
+  // Small batches (the batcher's rounds) are latency bound: too few probes
+  // to hide a lane's serial cell walk, and the spatial order's fixed cost
+  // buys nothing.  They run in natural order with one wave per probe.
+  DevParams dp = E->dp;
+  if (NP < E->small_points) {
+    dp.order_mask = 0;
+    dp.cand_wave_all = 1;
+  }
+
   DevWork w{};
   w.pt_trace = P<int32_t>(E->pt_trace);
   w.is_col = P<uint8_t>(E->is_col);
@@ -315,19 +324,19 @@ static int engine_match_once(otm_engine* E, const DevBatch& b, hipStream_t s, st
   w.ord.item = P<int32_t>(E->ord_item);
   w.ord.grp = P<int32_t>(E->ord_grp);
   w.ord.tile = P<uint16_t>(E->ord_tile);
-  w.ord.tile_cnt = E->dp.order_mask ? P<int32_t>(E->ord_cnt) : nullptr;
+  w.ord.tile_cnt = dp.order_mask ? P<int32_t>(E->ord_cnt) : nullptr;
   w.ord.cursor = P<int32_t>(E->ord_cursor);
-  launch_columns(E->g, b, E->dp, w, s, mk);
-  if (E->dp.order_mask) {
+  launch_columns(E->g, b, dp, w, s, mk);
+  if (dp.order_mask) {
     launch_order(b, w, s, mk);
   } else if (E->timing) {
     mk.begin(KN_ORDER, s);
     mk.end(KN_ORDER, s);
   }
-  launch_candidates(E->g, b, E->dp, w, s, mk);
+  launch_candidates(E->g, b, dp, w, s, mk);
   // spill snapshot A: candidate probes the lane tier handed to the wave tier
   HIPCHK(hipMemcpyAsync(E->snap.p, w.counters_i32, 64, hipMemcpyDeviceToDevice, s));
-  launch_links(b, E->dp, w, s, mk);
+  launch_links(b, dp, w, s, mk);
   mk.begin(KN_SCAN_TRANS, s);
   scan_i64(w.trans_off, NP, E->scan_tmp.p, E->scan_tmp.cap, s);
   mk.end(KN_SCAN_TRANS, s);
@@ -341,12 +350,12 @@ static int engine_match_once(otm_engine* E, const DevBatch& b, hipStream_t s, st
   w.big_lab = P<unsigned long long>(E->big_lab);
   w.big_inq = P<uint32_t>(E->big_inq);
   w.big_fr = P<uint32_t>(E->big_fr);
-  launch_transitions(E->g, b, E->dp, w, s, mk);
+  launch_transitions(E->g, b, dp, w, s, mk);
   // spill snapshot B: columns per transition tier
   HIPCHK(hipMemcpyAsync(P<char>(E->snap) + 64, w.counters_i32, 64, hipMemcpyDeviceToDevice, s));
   launch_viterbi(b, w, s, mk);
   HIPCHK(hipMemsetAsync(w.counters_i32, 0, 64, s));
-  launch_route(E->g, b, E->dp, w, s, mk);
+  launch_route(E->g, b, dp, w, s, mk);
   // spill snapshot C: steps per route tier
   HIPCHK(hipMemcpyAsync(P<char>(E->snap) + 128, w.counters_i32, 64, hipMemcpyDeviceToDevice, s));
 

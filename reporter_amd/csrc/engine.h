@@ -24,6 +24,7 @@ struct otm_engine {
   // 50 m/s at 5 s sampling; measured on config 2, 1000 m left one column in 1M to
   // the online tiers at a cost of 0.13 ms per batch
   float index_rmax = 1250.0f;
+  int64_t small_points = 0;  // batches below this many points: natural order, wave-tier candidates
   otm::DevIndex idx{};
   int64_t index_entries = 0;
   int64_t index_slots = 0;  // hash-table slots (8 B each + 4 B predecessor)

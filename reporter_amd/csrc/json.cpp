@@ -54,6 +54,7 @@ struct Parser {
   std::string_view t;
   size_t i = 0;
   std::string err;
+  bool jackson = false;  // no NaN / Infinity literals (Jackson's default)
 
   void fail(const char* msg, size_t at) {
     if (!err.empty()) return;
@@ -311,6 +312,11 @@ struct Parser {
       v->b = false;
       return true;
     }
+    if (jackson) {
+      if (number(v)) return true;
+      fail("Expecting value", i);
+      return false;
+    }
     if (starts("NaN")) {
       i += 3;
       v->kind = Kind::Float;
@@ -349,6 +355,15 @@ bool parse(std::string_view text, Value* out, std::string* err) {
   }
   *err = p.err.empty() ? std::string("Expecting value: line 1 column 1 (char 0)") : p.err;
   return false;
+}
+
+bool parse_jackson(std::string_view text, Value* out) {
+  Parser p;
+  p.t = text;
+  p.jackson = true;
+  p.ws();
+  *out = Value();
+  return p.value(out, 0);  // ObjectMapper.readTree: content after the first value is not read
 }
 
 std::string utf8_error(std::string_view s) {

@@ -39,6 +39,9 @@ struct Value {
 
 // json.loads; on failure returns false and *err = str(JSONDecodeError)
 bool parse(std::string_view text, Value* out, std::string* err);
+// Jackson 2.8 ObjectMapper.readTree of a String: the first JSON value, no
+// NaN / Infinity literals, trailing content ignored
+bool parse_jackson(std::string_view text, Value* out);
 // bytes.decode('utf-8') check: empty string when valid, else str(UnicodeDecodeError)
 std::string utf8_error(std::string_view bytes);
 

@@ -92,6 +92,7 @@ struct DevParams {
   float sigma_z, beta, factor, breakage, interp, search_radius, max_search_radius, gps_accuracy;
   int max_candidates;
   int order_mask;
+  int cand_wave_all;  // small batch: every probe to the wave tier (latency, not throughput, bound)
 };
 
 struct DevReportCfg {

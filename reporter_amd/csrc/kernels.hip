@@ -394,6 +394,11 @@ __global__ __launch_bounds__(CAND_TB) void k_cand_lane(DevGraph g, DevBatch b, D
   for (int64_t it = R.i0; it < R.i1; it += R.stride) {
     const int64_t p = R.ordered ? (int64_t)w.ord.item[it] : it;
     if (!R.ordered && !w.is_col[p]) continue;
+    if (P.cand_wave_all) {
+      const int slot = atomicAdd(&w.counters_i32[5], 1);
+      w.overflow_list0[slot] = (int32_t)p;
+      continue;
+    }
     const float lat = b.lat[p], lon = b.lon[p];
     const float r = probe_radius(P, b.acc[p]);
     const float r2 = r * r;

@@ -16,6 +16,37 @@ using json::Value;
 // prints "0" (with the sign of a negative input).  No JVM exists here to pin
 // this against: the rules are DecimalFormat's documented behaviour.
 void java_decimal6(float f, std::string* o) {
+  // n = the value in millionths, HALF_EVEN on the exact binary value: f * 1e6
+  // is exact in double (24 + 14 significant bits) and nearbyint rounds ties
+  // to even; the text is then n's digits with the point six from the right.
+  const double d = (double)f * 1e6;
+  if (std::fabs(d) < 9.0e15) {
+    const double r = std::nearbyint(d);
+    uint64_t n = (uint64_t)std::fabs(r);
+    char buf[32];
+    int p = (int)sizeof buf;
+    uint64_t ip = n / 1000000u;
+    uint32_t fr = (uint32_t)(n % 1000000u);
+    int fd = 6;
+    while (fd > 0 && fr % 10u == 0) {
+      fr /= 10u;
+      --fd;
+    }
+    for (int k = 0; k < fd; ++k) {
+      buf[--p] = (char)('0' + fr % 10u);
+      fr /= 10u;
+    }
+    if (fd > 0) buf[--p] = '.';
+    if (ip > 0 || fd == 0) {
+      do {
+        buf[--p] = (char)('0' + ip % 10u);
+        ip /= 10u;
+      } while (ip > 0);
+    }
+    if (std::signbit(r)) o->push_back('-');
+    o->append(buf + p, sizeof buf - (size_t)p);
+    return;
+  }
   char buf[64];
   std::snprintf(buf, sizeof buf, "%.6f", (double)f);  // exact binary value, half-even
   std::string s(buf);

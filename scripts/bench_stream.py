@@ -25,13 +25,16 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--vehicles", type=int, default=10000)
     ap.add_argument("--points", type=int, default=100)
-    ap.add_argument("--chunk", type=int, default=200000, help="records per otm_batcher_process call")
+    ap.add_argument("--chunk", type=int, default=20000, help="records per otm_batcher_process call (one poll)")
     ap.add_argument("--json-path", action="store_true")
-    ap.add_argument("--max-pending", type=int, default=0)
+    ap.add_argument("--max-pending", type=int, default=100000, help="queued operations that trigger a drain")
+    ap.add_argument("--raw", choices=["json", "sv"], default=None,
+                    help="feed raw messages through the native formatter (README's json / sv layouts)")
+    ap.add_argument("--format-threads", type=int, default=8)
     args = ap.parse_args()
     import torch  # noqa: F401  (binds the HIP runtime torch ships)
     from reporter_amd import Engine, synth
-    from reporter_amd.batcher import Batcher
+    from reporter_amd.batcher import Batcher, KeyBlock
     graph = synth.cached_graph(2)
     tr = dict(synth.CONFIGS[2]["traces"], n_vehicles=args.vehicles, points_per_vehicle=args.points)
     b = synth.make_traces(graph, **tr)
@@ -48,11 +51,36 @@ def main():
         bt = Batcher(engine=eng, json_path=args.json_path, max_pending=args.max_pending)
         # warm the engine (allocations, code objects) outside the timed region
         eng.match(synth.slice_batch(b, 0, min(100, nv)))
-        t0 = time.perf_counter()
         n = len(keys)
-        for i in range(0, n, args.chunk):
-            j = min(n, i + args.chunk)
-            bt.process(list(keys[i:j]), lat[i:j], lon[i:j], acc[i:j], tm[i:j], ts[i:j])
+        if args.raw:
+            from reporter_amd.formatter import Formatter, pack_messages
+            if args.raw == "json":
+                spec = ",json,id,latitude,longitude,timestamp,accuracy"
+                msgs = ['{"timestamp":%d,"id":"%s","accuracy":%d,"latitude":%r,"longitude":%r}'
+                        % (tm[i], keys[i], acc[i], float(lat[i]), float(lon[i])) for i in range(n)]
+            else:
+                import datetime
+                spec = ",sv,\\|,1,9,10,0,5,yyyy-MM-dd HH:mm:ss"
+                ep = datetime.datetime(1970, 1, 1)
+                msgs = ["%s|%s|x|x|x|%d|x|x|x|%r|%r|x|x|x"
+                        % ((ep + datetime.timedelta(seconds=int(tm[i]))).strftime("%Y-%m-%d %H:%M:%S"), keys[i],
+                           acc[i], float(lat[i]), float(lon[i])) for i in range(n)]
+            fmt = Formatter(spec)
+            blocks = [(i, min(n, i + args.chunk), pack_messages(msgs[i:min(n, i + args.chunk)]))
+                      for i in range(0, n, args.chunk)]
+            from reporter_amd._lib import lib
+            t0 = time.perf_counter()
+            for i, j, (buf, off) in blocks:
+                tsb = np.ascontiguousarray(ts[i:j])
+                rc = lib().otm_batcher_process_raw(bt.h, fmt.h, j - i, buf.ctypes.data, off.ctypes.data,
+                                                   tsb.ctypes.data, args.format_threads)
+                assert rc == 0, rc
+        else:
+            blocks = [(i, min(n, i + args.chunk), KeyBlock(list(keys[i:min(n, i + args.chunk)])))
+                      for i in range(0, n, args.chunk)]
+            t0 = time.perf_counter()
+            for i, j, kb in blocks:
+                bt.process(kb, lat[i:j], lon[i:j], acc[i:j], tm[i:j], ts[i:j])
         bt.flush()
         bt.close()
         dt = time.perf_counter() - t0
@@ -60,7 +88,9 @@ def main():
         fwd = len(bt.forwarded())
     line = {"metric": "config5 sustained ingest through the native batcher + GPU matcher",
             "records_per_s": n / dt, "matched_points_per_s": st["request_points"] / dt, "seconds": dt,
-            "records": n, "forwarded": fwd, "path": "json" if args.json_path else "binary", "stats": st,
+            "records": n, "forwarded": fwd, "path": "json" if args.json_path else "binary",
+            "input": "raw %s messages via the native formatter (%d threads)" % (args.raw, args.format_threads)
+            if args.raw else "formatted records", "stats": st,
             "workload": "config-2 fleet (%d vehicles x %d points, 5 s) as one time-ordered stream" % (nv, npt)}
     print(json.dumps(line), flush=True)
 

@@ -123,3 +123,37 @@ def test_gates_and_trim_unit():
     assert len(b.points) == 9
     resp["v"] = '{"error":"boom"}'  # no shape_used: everything trimmed
     assert b.report("k", lambda body: resp["v"], 0, 2, 0) is not None and b.points == []
+
+
+def test_quantize_decimal6_matches_text_round_trip():
+    """otm_quantize_decimal6 (string-free) == float(DecimalFormat text) on
+    coordinates, exact ties (k/128: HALF_EVEN at the 7th digit), signed zeros
+    and values past the shortcut's range."""
+    import ctypes as C
+    from oracle import pybatcher
+    from reporter_amd._lib import lib
+    rng = np.random.default_rng(5)
+    v = np.concatenate([rng.uniform(-180, 180, 20000), rng.uniform(-1e-5, 1e-5, 2000),
+                        np.arange(-4096, 4096) / 128.0, np.arange(-300, 300) / 1024.0,
+                        [0.0, -0.0, 5e-7, -5e-7, 1.5e-6, 2.5e-6, 1e9, -3e10, 1e30, 179.9999995]]).astype(np.float32)
+    out = np.empty_like(v)
+    lib().otm_quantize_decimal6(v.ctypes.data, out.ctypes.data, C.c_int64(len(v)))
+    want = np.array([np.float32(float(pybatcher.decimal6(x) or "0")) for x in v.tolist()], np.float32)
+    assert np.array_equal(out.view(np.uint32), want.view(np.uint32))
+
+
+def test_request_bytes_match_java_encoding_wide():
+    """The integer-digit DecimalFormat text against Decimal HALF_EVEN over
+    coordinates, 7th-digit ties, tiny and signed-zero values, and values past
+    the integer shortcut."""
+    from oracle import pybatcher
+    from reporter_amd import encode_request
+    rng = np.random.default_rng(9)
+    v = np.concatenate([rng.uniform(-180, 180, 3000), rng.uniform(-2e-6, 2e-6, 500), np.arange(-512, 512) / 128.0,
+                        [0.0, -0.0, 5e-7, -5e-7, 1.5e-6, 2.5e-6, 1e9, -3e10, 1e30, 999999.5]]).astype(np.float32)
+    b = pybatcher.Batch()
+    for i in range(0, len(v) - 1, 2):
+        b.points.append(pybatcher.Point(v[i], v[i + 1], i % 7, 1500000000 + i))
+    got = encode_request("k2", [p.lat for p in b.points], [p.lon for p in b.points], [p.time for p in b.points],
+                         [p.accuracy for p in b.points])
+    assert got == b.body("k2")

@@ -20,6 +20,16 @@ pytestmark = pytest.mark.gpu
 KMAX = 32
 
 
+@pytest.fixture(params=["large", "small"])
+def batch_path(request, monkeypatch):
+    """The two launch plans of a batch: "large" = spatial work
+    order + lane-tier candidates, "small" (under OTM_SMALL_POINTS points,
+    the batcher's rounds) = natural order, one wave per probe.  The tests'
+    batches are small, so the threshold is forced either way."""
+    monkeypatch.setenv("OTM_SMALL_POINTS", "0" if request.param == "large" else str(1 << 40))
+    return request.param
+
+
 def _stage_compare(eng, orc, batch):
     P = len(batch["lat"])
     nc_g = eng.debug("ncand")[:P]
@@ -66,7 +76,7 @@ def _run_both(graph, batch, oracle, results_equal, meili=None, stages=True, coun
 
 
 @pytest.mark.parametrize("radius", [None, 0.0, 300.0], ids=["index_default", "no_index", "index300"])
-def test_city_sample_sigma15(small_graph, oracle, results_equal, radius):
+def test_city_sample_sigma15(small_graph, oracle, results_equal, batch_path, radius):
     # the distance index answers columns whose bound fits its radius; the rest
     # (and everything when it is disabled) run the online search tiers --
     # results must be identical in all three configurations
@@ -86,24 +96,24 @@ def test_index_info(small_graph):
         assert eng.index_info()["entries"] == 0
 
 
-def test_noise_free_traces(small_graph, oracle, results_equal):
+def test_noise_free_traces(small_graph, oracle, results_equal, batch_path):
     b = synth.make_traces(small_graph, 100, 60, interval_s=5.0, noise_sigma_m=0.0, accuracy=0.0, seed=3)
     _run_both(small_graph, b, oracle, results_equal)
 
 
-def test_high_noise_sparse_rural(rural_graph, oracle, results_equal):
+def test_high_noise_sparse_rural(rural_graph, oracle, results_equal, batch_path):
     b = synth.make_traces(rural_graph, 100, 100, interval_s=30.0, noise_sigma_m=50.0, accuracy=50.0, seed=5)
     _run_both(rural_graph, b, oracle, results_equal, meili=dict(search_radius=100.0, max_search_radius=100.0))
 
 
-def test_long_gaps_force_global_tier(small_graph, oracle, results_equal):
+def test_long_gaps_force_global_tier(small_graph, oracle, results_equal, batch_path):
     # 120 s sampling: bounds of 5 x gc reach kilometres -> searches overflow
     # the LDS tier and finish in the global-memory tier, same fixed point
     b = synth.make_traces(small_graph, 60, 30, interval_s=120.0, noise_sigma_m=10.0, accuracy=10.0, seed=9)
     _run_both(small_graph, b, oracle, results_equal)
 
 
-def test_long_traces_mixed_lengths(small_graph, oracle, results_equal):
+def test_long_traces_mixed_lengths(small_graph, oracle, results_equal, batch_path):
     # traces longer than the Viterbi LDS window (256 points) take the
     # global-memory form; mixed with short ones in one batch
     long_b = synth.make_traces(small_graph, 12, 400, interval_s=5.0, noise_sigma_m=15.0, accuracy=15.0, seed=31)
@@ -114,7 +124,7 @@ def test_long_traces_mixed_lengths(small_graph, oracle, results_equal):
     _run_both(small_graph, b, oracle, results_equal)
 
 
-def test_dense_candidates_spill_tiers(small_graph, oracle, results_equal):
+def test_dense_candidates_spill_tiers(small_graph, oracle, results_equal, batch_path):
     # a 300 m search radius puts dozens of distinct edges in range: probes
     # spill from the lane candidate tier to the wave tier, and the candidate
     # count per trace outgrows the Viterbi LDS window
@@ -123,7 +133,7 @@ def test_dense_candidates_spill_tiers(small_graph, oracle, results_equal):
               meili=dict(search_radius=300.0, max_search_radius=300.0, max_candidates=32))
 
 
-def test_edge_cases(small_graph, oracle, results_equal):
+def test_edge_cases(small_graph, oracle, results_equal, batch_path):
     base = synth.make_traces(small_graph, 8, 20, interval_s=5.0, noise_sigma_m=15.0, accuracy=15.0, seed=21)
     lat, lon, tm, acc = (list(base[k]) for k in ("lat", "lon", "time", "accuracy"))
     off = list(base["trace_off"])

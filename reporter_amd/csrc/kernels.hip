@@ -1771,16 +1771,20 @@ __device__ void viterbi_trace_global(int64_t a, int64_t e, DevWork& w) {
 // runs out of LDS with the previous column's scores broadcast by readlane;
 // the backtrack walks LDS; state / chain_start go out coalesced.  Same
 // recurrence, tie rules and chain breaks as viterbi_trace_global.
-// LDS per trace (~6.8 KB at these sizes) sets how many traces a CU holds;
-// a trace whose candidates exceed VIT_BP, or with one column pair's block
-// beyond VIT_TW, takes the global-memory form.
+// LDS per trace (~5.5 KB at these sizes) sets how many traces a CU holds
+// (128 points of metadata: 0.218 -> 0.207 ms on config 2 against 256); a
+// trace longer than VIT_PTS, whose candidates exceed VIT_BP, or with one
+// column pair's block beyond VIT_TW, takes the global-memory form.
 #ifndef OTM_VIT_TW
 #define OTM_VIT_TW 512
 #endif
 #ifndef OTM_VIT_BP
 #define OTM_VIT_BP 1024
 #endif
-constexpr int VIT_PTS = 256;         // points per trace (metadata held for the whole trace)
+#ifndef OTM_VIT_PTS
+#define OTM_VIT_PTS 128
+#endif
+constexpr int VIT_PTS = OTM_VIT_PTS; // points per trace (metadata held for the whole trace)
 constexpr int VIT_BP = OTM_VIT_BP;   // candidates per trace (backpointers)
 constexpr int VIT_TW = OTM_VIT_TW;   // transition floats per window (>= one column pair's block)
 constexpr int VIT_EW = 256;          // emission floats per window (>= KMAX)
@@ -1907,14 +1911,18 @@ __global__ __launch_bounds__(TB) void k_viterbi(DevBatch b, DevWork w) {
           __syncthreads();
           wt0 = sToff[pl];
           we0 = sEoff[pl];
-          int lo = pl + 1, hi = n;
-          while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (sToff[mid] - wt0 <= VIT_TW && sEoff[mid] - we0 <= VIT_EW) lo = mid;
-            else hi = mid - 1;
+          // window end: Toff / Eoff are monotone, so the points that fit are
+          // a prefix -- 64 candidates per LDS round trip, counted by ballot
+          int we = pl + 1;
+          while (we < n) {
+            const int q = we + 1 + lane;
+            const bool ok = q <= n && sToff[q] - wt0 <= VIT_TW && sEoff[q] - we0 <= VIT_EW;
+            const int cnt = __popcll(__ballot(ok));
+            we += cnt;
+            if (cnt < TB) break;
           }
-          win_end = lo;
-          const int nt = sToff[win_end] - wt0, ne = sEoff[win_end] - we0;
+          win_end = we;
+          const int nt = sToff[win_end] - wt0;
           for (int f0 = 0; f0 < nt; f0 += 8 * TB) {
             float v[8];
 #pragma unroll
@@ -1928,27 +1936,23 @@ __global__ __launch_bounds__(TB) void k_viterbi(DevBatch b, DevWork w) {
               if (f < nt) sT[f] = v[u];
             }
           }
-          for (int f0 = 0; f0 < ne; f0 += 4 * TB) {
-            float v[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-              const int f = f0 + u * TB + lane;
-              v[u] = 0.0f;
-              if (f < ne) {
-                // point holding window candidate f: last q with sEoff[q] <= we0 + f
-                int l2 = pl, h2 = win_end - 1;
-                while (l2 < h2) {
-                  const int mid = (l2 + h2 + 1) >> 1;
-                  if (sEoff[mid] <= we0 + f) l2 = mid;
-                  else h2 = mid - 1;
-                }
-                v[u] = w.cand_emis[(a + l2) * KMAX + (we0 + f - sEoff[l2])];
-              }
+          // emissions point-parallel: lane q copies point q's candidates
+          // (independent loads, no search for a candidate's point)
+          for (int q0 = pl; q0 < win_end; q0 += TB) {
+            const int q = q0 + lane;
+            int kq = 0, eq = 0;
+            if (q < win_end) {
+              kq = sKc[q];
+              eq = sEoff[q] - we0;
             }
+            for (int j0 = 0; __ballot(j0 < kq) != 0ull; j0 += 4) {
+              float v[4];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-              const int f = f0 + u * TB + lane;
-              if (f < ne) sEm[f] = v[u];
+              for (int u = 0; u < 4; ++u)
+                v[u] = j0 + u < kq ? w.cand_emis[(a + q) * KMAX + j0 + u] : 0.0f;
+#pragma unroll
+              for (int u = 0; u < 4; ++u)
+                if (j0 + u < kq) sEm[eq + j0 + u] = v[u];
             }
           }
           __syncthreads();

@@ -114,7 +114,7 @@ def test_long_gaps_force_global_tier(small_graph, oracle, results_equal, batch_p
 
 
 def test_long_traces_mixed_lengths(small_graph, oracle, results_equal, batch_path):
-    # traces longer than the Viterbi LDS window (256 points) take the
+    # traces longer than the Viterbi LDS window (128 points) take the
     # global-memory form; mixed with short ones in one batch
     long_b = synth.make_traces(small_graph, 12, 400, interval_s=5.0, noise_sigma_m=15.0, accuracy=15.0, seed=31)
     short_b = synth.make_traces(small_graph, 40, 30, interval_s=5.0, noise_sigma_m=15.0, accuracy=15.0, seed=32)

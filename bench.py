@@ -5,7 +5,9 @@ One step = one pass of libotmatch over one batch of 10k vehicles x 100
 probes = 1M GPS points per GPU (city 20 x 20 km, 5 s sampling, sigma 15 m,
 accuracy 15, radius 50 m), inputs already resident in HBM: candidate search,
 emission, bounded-route transitions, Viterbi, route recovery, OSMLR segment
-stitching, report() and the per-segment speed histogram.  With N GPUs each
+stitching, report() and the per-segment speed histogram.  Steps run three
+batches in flight per GPU (engine clones on their own HIP streams, one host
+thread each).  With N GPUs each
 rank matches its own uuid shard (Kafka murmur2 partitioner) and the step ends
 with the one collective of the design: an RCCL reduce-scatter of the
 per-segment histograms (weak scaling).
@@ -56,6 +58,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-check", action="store_true", help="skip the untimed oracle pass (agreement, bytes)")
     ap.add_argument("--traffic-json", default=DEFAULT_TRAFFIC, help="PMC traffic summary (scripts/pmc_summary.py)")
+    ap.add_argument("--inflight", type=int, default=3,
+                    help="batches in flight per GPU: engine clones on their own HIP streams, one host thread each")
     return ap.parse_args()
 
 
@@ -135,6 +139,10 @@ def main():
     hist = torch.zeros(nseg_pad * nbins, dtype=torch.int32, device=dev)
     hist_shard = torch.zeros(nseg_pad * nbins // world, dtype=torch.int32, device=dev)
     eng.hist_bind(hist, nbins, bin_kph)
+    # batches in flight: clones share the graph, index and histogram binding
+    inflight = max(1, args.inflight)
+    engines = [eng] + [eng.clone() for _ in range(inflight - 1)]
+    streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(inflight - 1)]
 
     d_off = torch.from_numpy(batch["trace_off"]).to(dev)
     d_lat = torch.from_numpy(batch["lat"]).to(dev)
@@ -144,25 +152,44 @@ def main():
     stream = torch.cuda.current_stream(dev)
     torch.cuda.synchronize(dev)
 
-    def step():
-        hist.zero_()
-        eng.match_device(d_off, d_lat, d_lon, d_time, d_acc, stream=stream.cuda_stream)
-        if world > 1:
-            flush.reduce_histograms(hist, out=hist_shard)
+    def step(i=0):
+        engines[i].match_device(d_off, d_lat, d_lon, d_time, d_acc, stream=streams[i].cuda_stream)
 
-    for _ in range(args.warmup):
-        step()
+    for i in range(inflight):
+        for _ in range(args.warmup):
+            step(i)
+    torch.cuda.synchronize(dev)
+    hist.zero_()
     torch.cuda.synchronize(dev)
 
-    # timed region: K steps between barriers, no per-kernel events inside
+    # timed region: K steps spread over the in-flight contexts (one host
+    # thread each; ctypes releases the GIL, every batch keeps its one host
+    # synchronisation), then the histogram flush (RCCL reduce-scatter when
+    # N > 1), between barriers; no per-kernel events inside
+    import itertools
+    import threading
+    ticket = itertools.count()  # next step to run; next() is atomic under the GIL
+    gate = threading.Barrier(inflight + 1)
+
+    def worker(i):
+        gate.wait()
+        while next(ticket) < args.steps:
+            step(i)
+
+    threads = [threading.Thread(target=worker, args=(i,)) for i in range(inflight)]
+    for t in threads:
+        t.start()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t_start = time.perf_counter()
-    for _ in range(args.steps):
-        step()
+    gate.wait()
+    for t in threads:
+        t.join()
     torch.cuda.synchronize(dev)
     if world > 1:
+        flush.reduce_histograms(hist, out=hist_shard)
+        torch.cuda.synchronize(dev)
         dist.barrier()
     elapsed = time.perf_counter() - t_start
     if world > 1:
@@ -176,7 +203,7 @@ def main():
     eng.set_timing(True)
     kern_tot = {}
     for _ in range(args.steps):
-        step()
+        step(0)
         for k, v in eng.kernel_ms().items():
             kern_tot[k] = kern_tot.get(k, 0.0) + v
     torch.cuda.synchronize(dev)
@@ -283,8 +310,10 @@ def main():
             "config": {"workload": "config2-city: 10k vehicles x 100 GPS points per GPU (1M points), 5 s, "
                                    "sigma 15 m, accuracy 15 m, radius 50 m, uuid-sharded",
                        "points_per_gpu": P, "vehicles_per_gpu": len(ids), "graph": ginfo,
-                       "parallelism": "uuid shards x%d, RCCL reduce-scatter of %dx%d histograms" %
-                                      (world, nseg, nbins)},
+                       "batches_in_flight": inflight,
+                       "parallelism": "uuid shards x%d, %d batches in flight per GPU (HIP streams), RCCL "
+                                      "reduce-scatter of %dx%d histograms per timed window" %
+                                      (world, inflight, nseg, nbins)},
             "roofline": roof,
             "kernel_ms": kern_avg,
             "stages": stages,
@@ -294,6 +323,8 @@ def main():
             "hip_runtime": _lib.runtime_info(),
         }
         print(json.dumps(line), flush=True)
+    for e in engines[1:]:
+        e.close()
     eng.hist_bind(None, 0, 1.0)
     eng.close()
     if world > 1:

@@ -62,6 +62,13 @@ typedef struct otm_engine otm_engine;
  * multi-GPU runs one engine per process/GPU. */
 int otm_engine_create(const char* cfg_path, const int* devices, int ndev,
                       otm_engine** out);
+/* A second batch context on the same GPU (extension): its own HIP stream and
+ * work buffers over the parent's HBM-resident graph, distance index and
+ * configuration.  Batches on a parent and its clones run concurrently when
+ * issued from different host threads (each handle serialises its own
+ * calls), so one kernel's tail overlaps the next batch's head.  Destroy
+ * clones before their parent. */
+int otm_engine_clone(otm_engine* eng, otm_engine** out);
 void otm_engine_destroy(otm_engine* eng);
 
 /* Last error message for this thread (eng may be NULL). */

@@ -151,6 +151,7 @@ def _declare(L):
         "otm_batcher_get_stats": (C.c_int, [vp, C.POINTER(BatcherStats)]),
         "otm_batcher_batch": (C.c_int, [vp, C.c_char_p, sz, C.c_int, vp, vp, vp, vp, C.POINTER(C.c_float)]),
         "otm_quantize_decimal6": (None, [vp, vp, C.c_int64]),
+        "otm_engine_clone": (C.c_int, [vp, C.POINTER(vp)]),
         "otm_formatter_create": (C.c_int, [C.c_char_p, C.POINTER(vp), C.c_char_p, sz]),
         "otm_formatter_destroy": (None, [vp]),
         "otm_format": (C.c_int, [vp, C.c_int32, vp, vp, C.c_int, C.POINTER(Formatted)]),

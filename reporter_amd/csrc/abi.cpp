@@ -274,6 +274,22 @@ int otm_engine_create(const char* cfg_path, const int* devices, int ndev, otm_en
   return OTM_OK;
 }
 
+int otm_engine_clone(otm_engine* P, otm_engine** out) {
+  if (!P || !out) return fail(OTM_EINVAL, "engine or out is NULL");
+  *out = nullptr;
+  if (P->parent) return fail(OTM_EINVAL, "clone the parent engine, not a clone");
+  auto* C = new otm_engine();
+  std::string err;
+  int rc = otm::engine_clone(P, C, &err);
+  if (rc) {
+    otm::engine_free(C);
+    delete C;
+    return fail(rc, err);
+  }
+  *out = C;
+  return OTM_OK;
+}
+
 void otm_engine_destroy(otm_engine* E) {
   if (!E) return;
   if (E->worker_started) {

@@ -129,6 +129,35 @@ int engine_init(otm_engine* E, const char* graph_path, int device, std::string* 
   return build_index(E, err);
 }
 
+int engine_clone(const otm_engine* P, otm_engine* C, std::string* err) {
+  C->parent = P;
+  C->device = P->device;
+  HIPCHK(hipSetDevice(C->device));
+  HIPCHK(hipStreamCreateWithFlags(&C->stream, hipStreamNonBlocking));
+  C->host.h = P->host.h;  // the header only: a clone reads no host graph sections
+  C->g = P->g;
+  C->idx = P->idx;
+  C->index_rmax = P->index_rmax;
+  C->index_entries = P->index_entries;
+  C->index_slots = P->index_slots;
+  C->index_incomplete_rows = P->index_incomplete_rows;
+  C->index_build_ms = P->index_build_ms;
+  C->small_points = P->small_points;
+  C->mc = P->mc;
+  C->rc = P->rc;
+  C->dp = P->dp;
+  C->drc = P->drc;
+  C->hist = P->hist;
+  C->nbins = P->nbins;
+  C->bin_kph = P->bin_kph;
+  HIPCHK(hipMalloc((void**)&C->ctr, sizeof(DevCounters)));
+  HIPCHK(hipMalloc((void**)&C->ctr_save, sizeof(DevCounters)));
+  HIPCHK(hipMemset(C->ctr, 0, sizeof(DevCounters)));
+  for (auto& e : C->kev) HIPCHK(hipEventCreate(&e));
+  (void)err;
+  return OTM_OK;
+}
+
 // Bounded distance index: part of flattening the graph into HBM, like the
 // tile preprocessing behind valhalla.Configure (py/reporter_service.py:279).
 // Row u = every node within rmax road metres of u, with D and predecessor

@@ -14,6 +14,7 @@
 #include "otmatch.h"
 
 struct otm_engine {
+  const otm_engine* parent = nullptr;  // a clone shares its parent's graph and index (otm_engine_clone)
   int device = 0;
   hipStream_t stream = nullptr;
   otm::HostGraph host;
@@ -94,6 +95,9 @@ struct otm_engine {
 namespace otm {
 
 int engine_init(otm_engine* E, const char* graph_path, int device, std::string* err);
+// a second batch context on the same GPU: own stream and buffers, the
+// parent's HBM graph, index and configuration
+int engine_clone(const otm_engine* parent, otm_engine* C, std::string* err);
 void engine_free(otm_engine* E);
 // match a device-resident batch; returns 0 or OTM_EDEVICE (message in *err)
 int engine_match(otm_engine* E, const DevBatch& b, hipStream_t s, std::string* err);

@@ -66,6 +66,21 @@ class Engine(object):
         self.h = h
         self.device = device
 
+    def clone(self):
+        """A second batch context on this GPU sharing the graph and index
+        (otm_engine_clone): its own stream and buffers, so batches on the two
+        run concurrently from different host threads.  Close it before self."""
+        h = C.c_void_p()
+        rc = lib().otm_engine_clone(self.h, C.byref(h))
+        if rc != _lib.OTM_OK:
+            raise OtmError("otm_engine_clone failed (%d): %s" % (rc, _lib.last_error()))
+        e = Engine.__new__(Engine)
+        e._tmp = None
+        e.h = h
+        e.device = self.device
+        e.parent = self
+        return e
+
     def close(self):
         if getattr(self, "h", None):
             lib().otm_engine_destroy(self.h)

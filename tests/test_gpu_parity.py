@@ -216,3 +216,32 @@ def test_histogram_matches_reports(small_graph):
         speed = r.reports["length"] / (r.reports["t1"] - r.reports["t0"]) * 3.6
         ok &= speed >= 0
         assert int(h.sum().item()) == int(ok.sum())
+
+
+def test_clone_concurrent_batches_identical(small_graph):
+    """otm_engine_clone: batches on a parent and its clone, issued from two
+    host threads at once, give the same bytes as the parent alone."""
+    import threading
+    a = synth.make_traces(small_graph, 300, 60, interval_s=5.0, noise_sigma_m=15.0, accuracy=15.0, seed=51)
+    b = synth.make_traces(small_graph, 250, 80, interval_s=5.0, noise_sigma_m=15.0, accuracy=15.0, seed=52)
+    with Engine(graph_path=small_graph) as eng:
+        ra = eng.match(a)
+        want_a = [getattr(ra, k).tobytes() for k in ("traces", "segments", "reports", "way_ids")]
+        rb = eng.match(b)
+        want_b = [getattr(rb, k).tobytes() for k in ("traces", "segments", "reports", "way_ids")]
+        cl = eng.clone()
+        try:
+            got = {}
+
+            def run(e, batch, key):
+                for _ in range(3):
+                    r = e.match(batch)
+                got[key] = [getattr(r, k).tobytes() for k in ("traces", "segments", "reports", "way_ids")]
+            th = [threading.Thread(target=run, args=(eng, a, "a")), threading.Thread(target=run, args=(cl, b, "b"))]
+            for t in th:
+                t.start()
+            for t in th:
+                t.join()
+            assert got["a"] == want_a and got["b"] == want_b
+        finally:
+            cl.close()

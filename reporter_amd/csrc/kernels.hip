@@ -2351,23 +2351,28 @@ __device__ void segments_trace(const DevGraph& g, const DevWork& w, DevOut& o, i
 // edges' f32 prefix sum stays sequential per state), so the records are
 // bit-identical.  Traces beyond SEGP_PTS points or SEGP_TRAV traversals take
 // the serial walk out of global memory (lane 0).
-constexpr int SEGP_PTS = 256;
-constexpr int SEGP_TRAV = 512;
-struct SegPar {
-  double o_t0[SEGP_PTS];  // per state: start time of the traversal it opens
-  double t_t0[SEGP_TRAV], t_t1[SEGP_TRAV];
-  float o_off0[SEGP_PTS];
-  int32_t tbase[SEGP_PTS + 1];  // first traversal slot of each state
-  int32_t t_edge[SEGP_TRAV];
-  float t_off0[SEGP_TRAV], t_off1[SEGP_TRAV];
-  int16_t sidx[SEGP_PTS + 1];  // point of each state
-  int16_t o_sh0[SEGP_PTS];
-  int16_t lopen[SEGP_PTS];  // latest opener <= k
-  int16_t chain[SEGP_PTS];
-  int16_t t_sh0[SEGP_TRAV], t_sh1[SEGP_TRAV], t_chain[SEGP_TRAV];
-  int16_t g_first[SEGP_TRAV], g_last[SEGP_TRAV], g_w0[SEGP_TRAV + 1];
+// Two LDS plans: a trace first tries the small one (128 states, 256
+// traversals: 13.6 KB, 3 waves per SIMD); one that does not fit goes to a
+// list for the large one (256 / 512: 26.6 KB); beyond that, the serial walk.
+// Measured on config 2: 0.131 -> 0.111 ms against the large plan alone.
+template <int PT, int TR>
+struct SegParT {
+  double o_t0[PT];  // per state: start time of the traversal it opens
+  double t_t0[TR], t_t1[TR];
+  float o_off0[PT];
+  int32_t tbase[PT + 1];  // first traversal slot of each state
+  int32_t t_edge[TR];
+  float t_off0[TR], t_off1[TR];
+  int16_t sidx[PT + 1];  // point of each state
+  int16_t o_sh0[PT];
+  int16_t lopen[PT];  // latest opener <= k
+  int16_t chain[PT];
+  int16_t t_sh0[TR], t_sh1[TR], t_chain[TR];
+  int16_t g_first[TR], g_last[TR], g_w0[TR + 1];
   int32_t nt;
 };
+constexpr int SEGP_PTS_S = 128, SEGP_TRAV_S = 256;
+constexpr int SEGP_PTS = 256, SEGP_TRAV = 512;
 
 __device__ __forceinline__ int wave_incl_max(int v, int lane) {
 #pragma unroll
@@ -2387,7 +2392,8 @@ struct StateStep {
   float oi, oj;
   int32_t plen, poff;
 };
-__device__ __forceinline__ StateStep state_step(const DevWork& w, int64_t a, const SegPar& S, int k, int ns) {
+template <class SP>
+__device__ __forceinline__ StateStep state_step(const DevWork& w, int64_t a, const SP& S, int k, int ns) {
   StateStep r;
   r.pl = S.sidx[k];
   const int64_t p = a + r.pl;
@@ -2412,12 +2418,18 @@ __device__ __forceinline__ StateStep state_step(const DevWork& w, int64_t a, con
   return r;
 }
 
-__global__ __launch_bounds__(TB) void k_segments(DevGraph g, DevBatch b, DevWork w, DevOut o) {
+// list / list_n: the traces to walk (null: all); spill / spill_n: where a
+// trace beyond this plan goes (null: the serial walk)
+template <int PT, int TR>
+__global__ __launch_bounds__(TB) void k_segments(DevGraph g, DevBatch b, DevWork w, DevOut o, const int32_t* list,
+                                                 const int32_t* list_n, int32_t* spill, int32_t* spill_n) {
   if (*w.abort) return;  // a capacity was exceeded: the host redoes the batch
-  __shared__ SegPar S;
+  __shared__ SegParT<PT, TR> S;
   const int lane = threadIdx.x;
   const unsigned long long lt = (1ull << lane) - 1ull;
-  for (int32_t t = blockIdx.x; t < b.n_traces; t += gridDim.x) {
+  const int32_t nwork = list ? *list_n : b.n_traces;
+  for (int32_t it = blockIdx.x; it < nwork; it += gridDim.x) {
+    const int32_t t = list ? list[it] : it;
     const int64_t a = b.trace_off[t];
     const int n = (int)(b.trace_off[t + 1] - a);
     const int32_t base = (int32_t)o.seg_base[a];
@@ -2428,8 +2440,11 @@ __global__ __launch_bounds__(TB) void k_segments(DevGraph g, DevBatch b, DevWork
       }
       continue;
     }
-    if (n > SEGP_PTS) {
-      if (lane == 0) segments_trace<true>(g, w, o, t, n, base, SegSrcGlobal{&g, &b, &w, a});
+    if (n > PT) {
+      if (lane == 0) {
+        if (spill) spill[atomicAdd(spill_n, 1)] = t;
+        else segments_trace<true>(g, w, o, t, n, base, SegSrcGlobal{&g, &b, &w, a});
+      }
       continue;
     }
     // ---- states in point order
@@ -2486,8 +2501,11 @@ __global__ __launch_bounds__(TB) void k_segments(DevGraph g, DevBatch b, DevWork
     }
     const int nt = c_base;
     __syncthreads();
-    if (nt > SEGP_TRAV) {
-      if (lane == 0) segments_trace<true>(g, w, o, t, n, base, SegSrcGlobal{&g, &b, &w, a});
+    if (nt > TR) {
+      if (lane == 0) {
+        if (spill) spill[atomicAdd(spill_n, 1)] = t;
+        else segments_trace<true>(g, w, o, t, n, base, SegSrcGlobal{&g, &b, &w, a});
+      }
       __syncthreads();
       continue;
     }
@@ -2923,7 +2941,16 @@ void launch_segments(const DevGraph& g, const DevBatch& b, DevWork& w, DevOut& o
                      const Marks& mk) {
   (void)write;
   const dim3 grid(grid_for(b.n_traces, 1, WAVE_GRID_CAP));
-  TIMED(KN_SEG_WRITE, hipLaunchKernelGGL(k_segments, grid, dim3(TB), 0, s, g, b, w, o));
+  // small LDS plan over every trace, the large one over its spills
+  // (list in overflow_list0, count in counters_i32[8]: free after the route stage)
+  int32_t* lst = w.overflow_list0;
+  int32_t* cnt = w.counters_i32 + 8;
+  mk.begin(KN_SEG_WRITE, s);
+  hipLaunchKernelGGL((k_segments<SEGP_PTS_S, SEGP_TRAV_S>), grid, dim3(TB), 0, s, g, b, w, o, (const int32_t*)nullptr,
+                     (const int32_t*)nullptr, lst, cnt);
+  hipLaunchKernelGGL((k_segments<SEGP_PTS, SEGP_TRAV>), dim3(grid_for(b.n_traces, 1, 2048)), dim3(TB), 0, s, g, b, w,
+                     o, (const int32_t*)lst, (const int32_t*)cnt, (int32_t*)nullptr, (int32_t*)nullptr);
+  mk.end(KN_SEG_WRITE, s);
 }
 void launch_seg_bound(const DevBatch& b, DevWork& w, int64_t* ub, hipStream_t s, const Marks& mk) {
   TIMED(KN_SEG_BOUND, hipLaunchKernelGGL(k_seg_bound, dim3(grid_for(b.n_points + 1, 256, 1 << 30)), dim3(256), 0, s,

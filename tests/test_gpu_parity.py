@@ -115,12 +115,18 @@ def test_long_gaps_force_global_tier(small_graph, oracle, results_equal, batch_p
 
 def test_long_traces_mixed_lengths(small_graph, oracle, results_equal, batch_path):
     # traces longer than the Viterbi LDS window (128 points) take the
-    # global-memory form; mixed with short ones in one batch
+    # global-memory form, and the segment walk's large LDS plan (129-256
+    # points) or its serial walk (longer); mixed with short ones in one batch
     long_b = synth.make_traces(small_graph, 12, 400, interval_s=5.0, noise_sigma_m=15.0, accuracy=15.0, seed=31)
+    mid_b = synth.make_traces(small_graph, 10, 200, interval_s=5.0, noise_sigma_m=15.0, accuracy=15.0, seed=34)
     short_b = synth.make_traces(small_graph, 40, 30, interval_s=5.0, noise_sigma_m=15.0, accuracy=15.0, seed=32)
-    off = np.concatenate([long_b["trace_off"], short_b["trace_off"][1:] + long_b["trace_off"][-1]])
-    b = {k: np.concatenate([long_b[k], short_b[k]]) for k in ("lat", "lon", "time", "accuracy")}
-    b["trace_off"] = off
+    parts = [long_b, mid_b, short_b]
+    offs, base = [np.zeros(1, np.int64)], 0
+    for pb in parts:
+        offs.append(pb["trace_off"][1:] + base)
+        base += pb["trace_off"][-1]
+    b = {k: np.concatenate([pb[k] for pb in parts]) for k in ("lat", "lon", "time", "accuracy")}
+    b["trace_off"] = np.concatenate(offs)
     _run_both(small_graph, b, oracle, results_equal)
 
 

@@ -369,6 +369,9 @@ constexpr int HCAP = 512;  // edge hash slots (>= 2 * MAX_HITS)
 // buys occupancy; the ~1 % of probes with more edges in range spill.
 constexpr int CAND_LANE_CAP = OTM_CAND_LANE_CAP;
 constexpr int CAND_TB = 128;
+#ifndef OTM_CAND_FIND
+#define OTM_CAND_FIND 1
+#endif
 
 // wave-reduce a per-lane count and add it to a device counter (all 64 lanes active)
 __device__ __forceinline__ void wave_cadd(unsigned long long* c, unsigned long long v) {
@@ -449,11 +452,21 @@ __global__ __launch_bounds__(CAND_TB) void k_cand_lane(DevGraph g, DevBatch b, D
             const uint32_t ent = en[u];
             const uint32_t e = ent >> 4;
             int f = -1;
+#if OTM_CAND_FIND
+            // every slot's edge read at once (independent LDS reads, no
+            // early exit): one LDS round trip per hit instead of up to 8
+#pragma unroll
+            for (int m = 0; m < CAND_LANE_CAP; ++m) {
+              const uint32_t em = E[m * S];
+              if (m < n && (em >> 4) == e) f = m;
+            }
+#else
             for (int m = 0; m < n; ++m)
               if ((E[m * S] >> 4) == e) {
                 f = m;
                 break;
               }
+#endif
             if (f < 0) {
               if (n == CAND_LANE_CAP) {
                 spill = true;
@@ -2963,7 +2976,14 @@ void launch_compact(int32_t n_traces, const DevOut& o, const int32_t* seg_off, c
 }
 void launch_report(const DevBatch& b, const DevReportCfg& rc, DevWork& w, DevOut& o, hipStream_t s,
                    const Marks& mk) {
-  TIMED(KN_REPORT, hipLaunchKernelGGL(k_report, dim3(grid_for(b.n_traces, 64, 1 << 30)), dim3(64), 0, s, b, rc, w,
+  // thread per trace; the serial segment walk is latency-bound, so small
+  // blocks spread the traces over more waves (env OTM_REPORT_TB)
+  static const int tb = [] {
+    const char* e = std::getenv("OTM_REPORT_TB");
+    const int v = e ? std::atoi(e) : 16;  // 0.053 -> 0.050 ms against 64 on config 2
+    return v == 16 || v == 32 || v == 64 || v == 128 ? v : 16;
+  }();
+  TIMED(KN_REPORT, hipLaunchKernelGGL(k_report, dim3(grid_for(b.n_traces, tb, 1 << 30)), dim3(tb), 0, s, b, rc, w,
                                       o, 0));
 }
 #undef TIMED

@@ -31,6 +31,8 @@ def main():
     ap.add_argument("--raw", choices=["json", "sv"], default=None,
                     help="feed raw messages through the native formatter (README's json / sv layouts)")
     ap.add_argument("--format-threads", type=int, default=8)
+    ap.add_argument("--cpu-sample", type=int, default=100000,
+                    help="records of the same stream for the CPU baseline (0: skip)")
     args = ap.parse_args()
     import torch  # noqa: F401  (binds the HIP runtime torch ships)
     from reporter_amd import Engine, synth
@@ -86,11 +88,29 @@ def main():
         dt = time.perf_counter() - t0
         st = bt.stats()
         fwd = len(bt.forwarded())
+    cpu = None
+    if args.cpu_sample > 0:
+        # CPU baseline: the reference's topology restated record at a time
+        # (oracle/pybatcher.py) with a synchronous /report per request into the
+        # C oracle's handler -- what one Kafka Streams thread does
+        sys.path.insert(0, ROOT)
+        from oracle import pybatcher, pyoracle
+        g = pyoracle.Graph(graph)
+        bp = pybatcher.BatchingProcessor(lambda body: pyoracle.handle_request(g, body)[1])
+        m = min(args.cpu_sample, n)
+        tc = time.perf_counter()
+        for i in range(m):
+            bp.process(keys[i], pybatcher.Point(lat[i], lon[i], acc[i], tm[i]), int(ts[i]))
+        dtc = time.perf_counter() - tc
+        cpu = {"value": m / dtc, "unit": "records/s", "cores": 1, "kind": "port",
+               "sample": "first %d records of the same stream: Python restatement of BatchingProcessor + the C "
+                         "oracle's /report handler per request, one thread (one Kafka Streams thread)" % m,
+               "requests": bp.requests}
     line = {"metric": "config5 sustained ingest through the native batcher + GPU matcher",
             "records_per_s": n / dt, "matched_points_per_s": st["request_points"] / dt, "seconds": dt,
             "records": n, "forwarded": fwd, "path": "json" if args.json_path else "binary",
             "input": "raw %s messages via the native formatter (%d threads)" % (args.raw, args.format_threads)
-            if args.raw else "formatted records", "stats": st,
+            if args.raw else "formatted records", "stats": st, "cpu_baseline": cpu,
             "workload": "config-2 fleet (%d vehicles x %d points, 5 s) as one time-ordered stream" % (nv, npt)}
     print(json.dumps(line), flush=True)
 

@@ -308,6 +308,9 @@ typedef struct otm_batcher_cfg {
                              path (otm_report_batch) instead of the binary one */
   int64_t max_pending;    /* otm_batcher_process drains once this many
                              operations are queued (0: only on flush/close)  */
+  int32_t threads;        /* host threads for running keys, building batches
+                             and applying responses (0 or 1: the caller's) */
+  int32_t reserved;
 } otm_batcher_cfg;
 void otm_batcher_defaults(otm_batcher_cfg* cfg);
 /* A /report handler for n request bodies (the HttpClient.POST of

@@ -50,7 +50,7 @@ class SpillStats(C.Structure):
 class BatcherCfg(C.Structure):
     _fields_ = [("report_dist", C.c_int32), ("report_count", C.c_int32), ("report_time_s", C.c_int64),
                 ("session_gap_ms", C.c_int64), ("max_batch", C.c_int32), ("json_path", C.c_int32),
-                ("max_pending", C.c_int64)]
+                ("max_pending", C.c_int64), ("threads", C.c_int32), ("reserved", C.c_int32)]
 
 
 class Forward(C.Structure):

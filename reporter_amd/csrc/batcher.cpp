@@ -29,6 +29,10 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <condition_variable>
+#include <functional>
+#include <memory>
+#include <thread>
 #include <cstdlib>
 #include <cstring>
 #include <deque>
@@ -150,6 +154,94 @@ struct Request {
   int npts;
 };
 
+// A fixed team of host threads for the per-key phases of a round (the
+// caller is member 0).  run(n, fn) calls fn(member, begin, end) over [0, n)
+// in contiguous chunks, one per member, and returns when all are done.
+class Pool {
+ public:
+  explicit Pool(int n) : n_(n < 1 ? 1 : n) {
+    for (int t = 1; t < n_; ++t) th_.emplace_back([this, t] { loop(t); });
+  }
+  ~Pool() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+      ++gen_;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+  int size() const { return n_; }
+  void run(size_t n, const std::function<void(int, size_t, size_t)>& fn) {
+    if (n_ == 1 || n < 2) {
+      fn(0, 0, n);
+      return;
+    }
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      fn_ = &fn;
+      n_items_ = n;
+      pending_ = n_ - 1;
+      ++gen_;
+    }
+    cv_.notify_all();
+    chunk(0, n, fn);
+    std::unique_lock<std::mutex> lk(mu_);
+    done_.wait(lk, [this] { return pending_ == 0; });
+    fn_ = nullptr;
+  }
+
+ private:
+  void chunk(int t, size_t n, const std::function<void(int, size_t, size_t)>& fn) const {
+    const size_t per = (n + (size_t)n_ - 1) / (size_t)n_;
+    const size_t a = std::min(n, (size_t)t * per), e = std::min(n, a + per);
+    fn(t, a, e);
+  }
+  void loop(int t) {
+    uint64_t seen = 0;
+    while (true) {
+      const std::function<void(int, size_t, size_t)>* fn;
+      size_t n;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return gen_ != seen; });
+        seen = gen_;
+        if (stop_) return;
+        fn = fn_;
+        n = n_items_;
+      }
+      chunk(t, n, *fn);
+      {
+        std::lock_guard<std::mutex> lk(mu_);
+        if (--pending_ == 0) done_.notify_one();
+      }
+    }
+  }
+  int n_;
+  std::vector<std::thread> th_;
+  std::mutex mu_;
+  std::condition_variable cv_, done_;
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+  const std::function<void(int, size_t, size_t)>* fn_ = nullptr;
+  size_t n_items_ = 0;
+  int pending_ = 0;
+};
+
+// What one member of the pool produces while applying responses
+struct Sink {
+  std::vector<Request> reqs;
+  std::vector<otm_forward> out;
+  std::vector<uint32_t> runq;
+  int64_t nulls = 0, forwarded = 0;
+  void clear() {
+    reqs.clear();
+    out.clear();
+    runq.clear();
+    nulls = forwarded = 0;
+  }
+};
+
 }  // namespace
 
 struct otm_batcher {
@@ -170,6 +262,8 @@ struct otm_batcher {
   std::deque<otm_forward> out;
   otm_batcher_stats st{};
   std::string err;
+  std::unique_ptr<Pool> pool;  // cfg.threads > 1
+  std::vector<Sink> sinks;     // one per pool member
 };
 
 namespace {
@@ -225,8 +319,9 @@ void distribute(otm_batcher* B) {
   }
 }
 
-// Run a key's operations until one needs the matcher.
-void run_key(otm_batcher* B, uint32_t k) {
+// Run a key's operations until one needs the matcher (its request goes to
+// the sink).
+void run_key(otm_batcher* B, uint32_t k, Sink& sk) {
   KeyState& ks = B->keys[k];
   ks.queued = false;
   while (!ks.waiting && ks.ob < ks.oe) {
@@ -246,7 +341,7 @@ void run_key(otm_batcher* B, uint32_t k) {
       min_elapsed = B->cfg.report_time_s;
     } else {
       if (!ks.in_store) {  // clean(): store.get -> null (the reference throws); close(): not iterated
-        if (op.kind == OP_CLEAN) B->st.null_batch_in_clean++;
+        if (op.kind == OP_CLEAN) sk.nulls++;
         continue;
       }
       min_dist = 0;
@@ -262,13 +357,13 @@ void run_key(otm_batcher* B, uint32_t k) {
     Request r;
     r.key = k;
     r.npts = (int)ks.batch.pts.size();
-    B->reqs.push_back(std::move(r));
+    sk.reqs.push_back(std::move(r));
     return;
   }
 }
 
 // Apply one response to its key (Batch.java:64-83, BatchingProcessor.java:69-81)
-void complete(otm_batcher* B, uint32_t k, int trim, int code, char* body, size_t body_len) {
+void complete(otm_batcher* B, uint32_t k, int trim, int code, char* body, size_t body_len, Sink& sk) {
   KeyState& ks = B->keys[k];
   if (trim == -2) {
     ks.batch.max_sep = 0.0f;
@@ -287,8 +382,8 @@ void complete(otm_batcher* B, uint32_t k, int trim, int code, char* body, size_t
     f.body = body;
     f.body_len = body_len;
     f.seq = ks.wop.seq;
-    B->out.push_back(f);
-    B->st.forwarded++;
+    sk.out.push_back(f);
+    sk.forwarded++;
     ks.in_store = !ks.batch.pts.empty();
   } else {
     // clean()/close() discard the response; the batch object stays in the
@@ -298,7 +393,27 @@ void complete(otm_batcher* B, uint32_t k, int trim, int code, char* body, size_t
   ks.waiting = false;
   if (ks.ob < ks.oe && !ks.queued) {
     ks.queued = true;
-    B->runq.push_back(k);
+    sk.runq.push_back(k);
+  }
+}
+
+// the pool over [0, n) (or the caller alone), sinks cleared first
+void par(otm_batcher* B, size_t n, const std::function<void(Sink&, size_t, size_t)>& fn) {
+  for (Sink& sk : B->sinks) sk.clear();
+  if (!B->pool) {
+    fn(B->sinks[0], 0, n);
+    return;
+  }
+  B->pool->run(n, [&](int t, size_t a, size_t e) { fn(B->sinks[(size_t)t], a, e); });
+}
+
+// fold the sinks' forwards, re-queued keys and counts into the batcher
+void merge_sinks(otm_batcher* B) {
+  for (Sink& sk : B->sinks) {
+    for (const otm_forward& f : sk.out) B->out.push_back(f);
+    B->runq.insert(B->runq.end(), sk.runq.begin(), sk.runq.end());
+    B->st.forwarded += sk.forwarded;
+    B->st.null_batch_in_clean += sk.nulls;
   }
 }
 
@@ -333,22 +448,27 @@ namespace {
 int issue_binary(otm_batcher* B, size_t r0, size_t r1) {
   otm_engine* E = B->eng;
   const int64_t t0 = now_us();
-  std::vector<int64_t> off(1, 0);
-  std::vector<float> lat, lon, acc;
-  std::vector<double> tm;
-  for (size_t i = r0; i < r1; ++i) {
-    const JBatch& jb = B->keys[B->reqs[i].key].batch;
-    for (const JPoint& p : jb.pts) {
-      lat.push_back(otm::quantize_decimal6(p.lat));
-      lon.push_back(otm::quantize_decimal6(p.lon));
-      tm.push_back((double)p.time);
-      acc.push_back((float)p.acc);
+  const size_t n = r1 - r0;
+  std::vector<int64_t> off(n + 1, 0);
+  for (size_t i = 0; i < n; ++i) off[i + 1] = off[i] + (int64_t)B->keys[B->reqs[r0 + i].key].batch.pts.size();
+  const size_t np = (size_t)off[n];
+  std::vector<float> lat(np), lon(np), acc(np);
+  std::vector<double> tm(np);
+  par(B, n, [&](Sink&, size_t a, size_t e) {
+    for (size_t i = a; i < e; ++i) {
+      size_t o = (size_t)off[i];
+      for (const JPoint& p : B->keys[B->reqs[r0 + i].key].batch.pts) {
+        lat[o] = otm::quantize_decimal6(p.lat);
+        lon[o] = otm::quantize_decimal6(p.lon);
+        tm[o] = (double)p.time;
+        acc[o] = (float)p.acc;
+        ++o;
+      }
     }
-    off.push_back((int64_t)lat.size());
-  }
+  });
   otm_batch b;
-  b.n_traces = (int32_t)(r1 - r0);
-  b.n_points = off.back();
+  b.n_traces = (int32_t)n;
+  b.n_points = (int64_t)np;
   b.trace_off = off.data();
   b.lat = lat.data();
   b.lon = lon.data();
@@ -367,41 +487,50 @@ int issue_binary(otm_batcher* B, size_t r0, size_t r1) {
     const int64_t t2 = now_us();
     B->st.us_match += t2 - t1;
     if (!rc) {
-      for (size_t i = r0; i < r1; ++i) {
-        const int32_t t = (int32_t)(i - r0);
-        const otm_trace_result& tr = res.traces[t];
-        // shape_used is written only when 200 and truthy (reporter_service.py:202)
-        const int trim = tr.code == 200 && tr.shape_used > 0 ? tr.shape_used : -1;
-        char* body = nullptr;
-        size_t blen = 0;
-        if (B->keys[B->reqs[i].key].wop.kind == OP_PROCESS) {
-          std::string s;
-          const int code = otm::write_report_response(res, t, &s);
-          (void)code;
-          body = (char*)std::malloc(s.size() + 1);
-          std::memcpy(body, s.data(), s.size());
-          body[s.size()] = 0;
-          blen = s.size();
+      // per request (each a different key): the trim, and the response body
+      // where process() forwards it
+      par(B, n, [&](Sink& sk, size_t a, size_t e) {
+        std::string s;
+        for (size_t i = a; i < e; ++i) {
+          const uint32_t k = B->reqs[r0 + i].key;
+          const otm_trace_result& tr = res.traces[i];
+          // shape_used is written only when 200 and truthy (reporter_service.py:202)
+          const int trim = tr.code == 200 && tr.shape_used > 0 ? tr.shape_used : -1;
+          char* body = nullptr;
+          size_t blen = 0;
+          if (B->keys[k].wop.kind == OP_PROCESS) {
+            s.clear();
+            (void)otm::write_report_response(res, (int32_t)i, &s);
+            body = (char*)std::malloc(s.size() + 1);
+            std::memcpy(body, s.data(), s.size());
+            body[s.size()] = 0;
+            blen = s.size();
+          }
+          complete(B, k, trim, tr.code, body, blen, sk);
         }
-        complete(B, B->reqs[i].key, trim, tr.code, body, blen);
-      }
+      });
+      merge_sinks(B);
     }
     B->st.us_apply += now_us() - t2;
   }
   if (rc) {
     // a device failure fails the batch like a 500 from the service: every
     // request gets {"error":...}, whose missing shape_used clears its batch
-    for (size_t i = r0; i < r1; ++i) {
-      std::string s = otm::error_body(err);
-      char* body = nullptr;
-      size_t blen = 0;
-      if (B->keys[B->reqs[i].key].wop.kind == OP_PROCESS) {
-        body = (char*)std::malloc(s.size() + 1);
-        std::memcpy(body, s.data(), s.size() + 1);
-        blen = s.size();
+    const std::string s = otm::error_body(err);
+    par(B, n, [&](Sink& sk, size_t a, size_t e) {
+      for (size_t i = a; i < e; ++i) {
+        const uint32_t k = B->reqs[r0 + i].key;
+        char* body = nullptr;
+        size_t blen = 0;
+        if (B->keys[k].wop.kind == OP_PROCESS) {
+          body = (char*)std::malloc(s.size() + 1);
+          std::memcpy(body, s.data(), s.size() + 1);
+          blen = s.size();
+        }
+        complete(B, k, -1, 500, body, blen, sk);
       }
-      complete(B, B->reqs[i].key, -1, 500, body, blen);
-    }
+    });
+    merge_sinks(B);
   }
   return OTM_OK;
 }
@@ -412,26 +541,33 @@ int issue_json(otm_batcher* B, size_t r0, size_t r1) {
   std::vector<const char*> rp((size_t)n);
   std::vector<size_t> rl((size_t)n), ol((size_t)n);
   std::vector<char*> outs((size_t)n, nullptr);
-  std::vector<int> codes((size_t)n, 0);
-  for (size_t i = r0; i < r1; ++i) {
-    KeyState& ks = B->keys[B->reqs[i].key];
+  std::vector<int> codes((size_t)n, 0), trims((size_t)n, 0);
+  // request bodies (Batch.java:52-61), per request
+  par(B, (size_t)n, [&](Sink&, size_t a, size_t e) {
     std::vector<float> la, lo;
     std::vector<int64_t> tm;
     std::vector<int32_t> ac;
-    for (const JPoint& p : ks.batch.pts) {
-      la.push_back(p.lat);
-      lo.push_back(p.lon);
-      tm.push_back(p.time);
-      ac.push_back(p.acc);
+    for (size_t i = r0 + a; i < r0 + e; ++i) {
+      KeyState& ks = B->keys[B->reqs[i].key];
+      la.clear();
+      lo.clear();
+      tm.clear();
+      ac.clear();
+      for (const JPoint& p : ks.batch.pts) {
+        la.push_back(p.lat);
+        lo.push_back(p.lon);
+        tm.push_back(p.time);
+        ac.push_back(p.acc);
+      }
+      char* body = nullptr;
+      size_t blen = 0;
+      otm_encode_request(ks.key.c_str(), (int)la.size(), la.data(), lo.data(), tm.data(), ac.data(), &body, &blen);
+      B->reqs[i].body.assign(body, blen);
+      std::free(body);
+      rp[i - r0] = B->reqs[i].body.data();
+      rl[i - r0] = B->reqs[i].body.size();
     }
-    char* body = nullptr;
-    size_t blen = 0;
-    otm_encode_request(ks.key.c_str(), (int)la.size(), la.data(), lo.data(), tm.data(), ac.data(), &body, &blen);
-    B->reqs[i].body.assign(body, blen);
-    std::free(body);
-    rp[i - r0] = B->reqs[i].body.data();
-    rl[i - r0] = B->reqs[i].body.size();
-  }
+  });
   const int64_t t1 = now_us();
   B->st.us_prepare += t1 - t0;
   int rc = B->fn ? B->fn(B->ctx, n, rp.data(), rl.data(), outs.data(), ol.data(), codes.data())
@@ -442,21 +578,19 @@ int issue_json(otm_batcher* B, size_t r0, size_t r1) {
     B->err = "matcher callback failed";
     return rc;
   }
-  for (size_t i = r0; i < r1; ++i) {
-    char* body = outs[i - r0];
-    const size_t blen = ol[i - r0];
-    const int trim = parse_trim(body, blen);
-    // a callback must hand back malloc'd bodies (otm_free releases them)
-    complete(B, B->reqs[i].key, trim, codes[i - r0], body, blen);
-  }
+  // a callback must hand back malloc'd bodies (otm_free releases them)
+  par(B, (size_t)n, [&](Sink& sk, size_t a, size_t e) {
+    for (size_t i = a; i < e; ++i)
+      complete(B, B->reqs[r0 + i].key, parse_trim(outs[i], ol[i]), codes[i], outs[i], ol[i], sk);
+  });
+  merge_sinks(B);
   B->st.us_apply += now_us() - t2;
   return OTM_OK;
 }
 
 // One formatted record (BatchingProcessor.process, :56-85): the clean()
 // pops its timestamp causes, then the record's own operation.
-void ingest(otm_batcher* B, const char* key, size_t key_len, const JPoint& pt, int64_t ts) {
-  const uint32_t k = key_id(B, key, key_len);
+void ingest(otm_batcher* B, uint32_t k, const JPoint& pt, int64_t ts) {
   // clean(key): keys whose entry is older than the session gap, stalest
   // first (BatchingProcessor.java:96-103)
   while (!B->time_to_key.empty() && ts - B->time_to_key.front().first > B->cfg.session_gap_ms) {
@@ -477,6 +611,32 @@ void ingest(otm_batcher* B, const char* key, size_t key_len, const JPoint& pt, i
   B->st.records++;
 }
 
+// Key ids of n records: known keys looked up by the pool (read-only on the
+// index), new ones inserted in record order by the caller.
+template <class KeyAt>
+void key_ids(otm_batcher* B, size_t n, const KeyAt& key_at, std::vector<uint32_t>* ids) {
+  ids->resize(n);
+  constexpr uint32_t kNew = 0xFFFFFFFFu;
+  if (B->pool && n >= 16384) {
+    par(B, n, [&](Sink&, size_t a, size_t e) {
+      for (size_t i = a; i < e; ++i) {
+        auto it = B->index.find(key_at(i));
+        (*ids)[i] = it != B->index.end() ? it->second : kNew;
+      }
+    });
+    for (size_t i = 0; i < n; ++i)
+      if ((*ids)[i] == kNew) {
+        const std::string_view k = key_at(i);
+        (*ids)[i] = key_id(B, k.data(), k.size());
+      }
+    return;
+  }
+  for (size_t i = 0; i < n; ++i) {
+    const std::string_view k = key_at(i);
+    (*ids)[i] = key_id(B, k.data(), k.size());
+  }
+}
+
 int drain(otm_batcher* B) {
   distribute(B);
   while (true) {
@@ -484,7 +644,14 @@ int drain(otm_batcher* B) {
     while (!B->runq.empty()) {
       std::vector<uint32_t> q;
       q.swap(B->runq);
-      for (uint32_t k : q) run_key(B, k);
+      par(B, q.size(), [&](Sink& sk, size_t a, size_t e) {
+        for (size_t i = a; i < e; ++i) run_key(B, q[i], sk);
+      });
+      for (Sink& sk : B->sinks) {
+        B->reqs.insert(B->reqs.end(), std::make_move_iterator(sk.reqs.begin()),
+                       std::make_move_iterator(sk.reqs.end()));
+        B->st.null_batch_in_clean += sk.nulls;
+      }
     }
     B->st.us_run += now_us() - t0;
     if (B->reqs.empty()) return OTM_OK;
@@ -516,6 +683,9 @@ void otm_batcher_defaults(otm_batcher_cfg* c) {
   c->session_gap_ms = 60000;      // :31
   c->max_batch = 0;
   c->json_path = 0;
+  c->max_pending = 0;
+  c->threads = 0;
+  c->reserved = 0;
 }
 
 int otm_batcher_create(otm_engine* eng, const otm_batcher_cfg* cfg, otm_report_fn fn, void* ctx,
@@ -527,6 +697,9 @@ int otm_batcher_create(otm_engine* eng, const otm_batcher_cfg* cfg, otm_report_f
   else otm_batcher_defaults(&B->cfg);
   B->fn = fn;
   B->ctx = ctx;
+  const int nt = B->cfg.threads > 1 ? std::min(B->cfg.threads, 256) : 1;
+  if (nt > 1) B->pool.reset(new Pool(nt));
+  B->sinks.resize((size_t)nt);
   *out = B;
   return OTM_OK;
 }
@@ -544,8 +717,9 @@ int otm_batcher_process(otm_batcher* B, int n, const char* const* keys, const si
                         const float* lon, const int32_t* accuracy, const int64_t* time, const int64_t* ts_ms) {
   if (!B || n < 0) return OTM_EINVAL;
   const int64_t t0 = now_us();
-  for (int i = 0; i < n; ++i)
-    ingest(B, keys[i], key_lens[i], JPoint{lat[i], lon[i], accuracy[i], time[i]}, ts_ms[i]);
+  std::vector<uint32_t> ids;
+  key_ids(B, (size_t)n, [&](size_t i) { return std::string_view(keys[i], key_lens[i]); }, &ids);
+  for (int i = 0; i < n; ++i) ingest(B, ids[(size_t)i], JPoint{lat[i], lon[i], accuracy[i], time[i]}, ts_ms[i]);
   B->st.us_enqueue += now_us() - t0;
   if (B->cfg.max_pending > 0 && (int64_t)B->log.size() > B->cfg.max_pending) return drain(B);
   return OTM_OK;
@@ -562,10 +736,20 @@ int otm_batcher_process_raw(otm_batcher* B, const otm_formatter* f, int32_t n, c
   B->st.us_format += t1 - t0;
   B->st.raw_messages += n;
   B->st.raw_dropped += n - r.n_ok;
-  for (int32_t i = 0; i < n; ++i) {
-    if (!r.ok[i]) continue;
-    ingest(B, r.keys + r.key_off[i], (size_t)(r.key_off[i + 1] - r.key_off[i]),
-           JPoint{r.lat[i], r.lon[i], r.accuracy[i], r.time[i]}, ts_ms[i]);
+  std::vector<int32_t> okm;  // the formatted messages, in stream order
+  okm.reserve((size_t)r.n_ok);
+  for (int32_t i = 0; i < n; ++i)
+    if (r.ok[i]) okm.push_back(i);
+  std::vector<uint32_t> ids;
+  key_ids(B, okm.size(),
+          [&](size_t j) {
+            const int32_t i = okm[j];
+            return std::string_view(r.keys + r.key_off[i], (size_t)(r.key_off[i + 1] - r.key_off[i]));
+          },
+          &ids);
+  for (size_t j = 0; j < okm.size(); ++j) {
+    const int32_t i = okm[j];
+    ingest(B, ids[j], JPoint{r.lat[i], r.lon[i], r.accuracy[i], r.time[i]}, ts_ms[i]);
   }
   otm_formatted_free(&r);
   B->st.us_enqueue += now_us() - t1;

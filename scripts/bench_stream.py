@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--raw", choices=["json", "sv"], default=None,
                     help="feed raw messages through the native formatter (README's json / sv layouts)")
     ap.add_argument("--format-threads", type=int, default=8)
+    ap.add_argument("--threads", type=int, default=8, help="batcher host threads (otm_batcher_cfg.threads)")
     ap.add_argument("--cpu-sample", type=int, default=100000,
                     help="records of the same stream for the CPU baseline (0: skip)")
     args = ap.parse_args()
@@ -50,7 +51,7 @@ def main():
     tm = t[order]
     ts = tm * 1000
     with Engine(graph_path=graph) as eng:
-        bt = Batcher(engine=eng, json_path=args.json_path, max_pending=args.max_pending)
+        bt = Batcher(engine=eng, json_path=args.json_path, max_pending=args.max_pending, threads=args.threads)
         # warm the engine (allocations, code objects) outside the timed region
         eng.match(synth.slice_batch(b, 0, min(100, nv)))
         n = len(keys)
@@ -109,6 +110,7 @@ def main():
     line = {"metric": "config5 sustained ingest through the native batcher + GPU matcher",
             "records_per_s": n / dt, "matched_points_per_s": st["request_points"] / dt, "seconds": dt,
             "records": n, "forwarded": fwd, "path": "json" if args.json_path else "binary",
+            "batcher_threads": args.threads,
             "input": "raw %s messages via the native formatter (%d threads)" % (args.raw, args.format_threads)
             if args.raw else "formatted records", "stats": st, "cpu_baseline": cpu,
             "workload": "config-2 fleet (%d vehicles x %d points, 5 s) as one time-ordered stream" % (nv, npt)}

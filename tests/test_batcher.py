@@ -73,12 +73,14 @@ def compare(bp, nb, recs):
     return st
 
 
-def test_native_batcher_matches_serial_restatement(small_graph, oracle):
+@pytest.mark.parametrize("threads", [0, 4])
+def test_native_batcher_matches_serial_restatement(small_graph, oracle, threads):
     g = oracle.Graph(small_graph)
     post = lambda body: oracle.handle_request(g, body)[1]  # noqa: E731
     recs = make_stream(small_graph)
     bp = run_python(recs, post)
-    nb = run_native(recs, Batcher(handler=lambda bodies: [oracle.handle_request(g, x) for x in bodies]))
+    nb = run_native(recs, Batcher(handler=lambda bodies: [oracle.handle_request(g, x) for x in bodies],
+                                  threads=threads))
     st = compare(bp, nb, recs)
     # the stream exercised every path: gated reports, relaxed clean() reports,
     # emptied batches, the reference's clean() null case, close()
@@ -87,13 +89,13 @@ def test_native_batcher_matches_serial_restatement(small_graph, oracle):
     assert st["match_batches"] < st["requests"]  # requests of several keys shared matcher calls
 
 
-@pytest.mark.parametrize("max_batch", [1, 5])
-def test_native_batcher_batch_limits(small_graph, oracle, max_batch):
+@pytest.mark.parametrize("max_batch,threads", [(1, 0), (5, 0), (5, 3)])
+def test_native_batcher_batch_limits(small_graph, oracle, max_batch, threads):
     g = oracle.Graph(small_graph)
     recs = make_stream(small_graph, n_veh=10, n_pts=40, seed=43)
     bp = run_python(recs, lambda body: oracle.handle_request(g, body)[1])
     nb = run_native(recs, Batcher(handler=lambda bodies: [oracle.handle_request(g, x) for x in bodies],
-                                  max_batch=max_batch), chunk=13)
+                                  max_batch=max_batch, threads=threads), chunk=13)
     compare(bp, nb, recs)
 
 
@@ -157,3 +159,15 @@ def test_request_bytes_match_java_encoding_wide():
     got = encode_request("k2", [p.lat for p in b.points], [p.lon for p in b.points], [p.time for p in b.points],
                          [p.accuracy for p in b.points])
     assert got == b.body("k2")
+
+
+def test_threaded_batcher_large_calls(small_graph, oracle):
+    """Calls above the parallel key-lookup threshold (16k records), with a
+    4-thread batcher, against the serial restatement."""
+    g = oracle.Graph(small_graph)
+    recs = make_stream(small_graph, n_veh=300, n_pts=70, seed=49)
+    assert len(recs) > 16384
+    bp = run_python(recs, lambda body: oracle.handle_request(g, body)[1])
+    nb = run_native(recs, Batcher(handler=lambda bodies: [oracle.handle_request(g, x) for x in bodies], threads=4,
+                                  max_pending=50000), chunk=20000)
+    compare(bp, nb, recs)

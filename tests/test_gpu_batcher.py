@@ -12,11 +12,12 @@ from test_batcher import compare, make_stream, run_native, run_python
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("json_path", [False, True], ids=["binary", "json"])
-def test_gpu_batcher_matches_serial_restatement(small_graph, json_path):
+@pytest.mark.parametrize("json_path,threads", [(False, 0), (True, 0), (False, 6), (True, 6)],
+                         ids=["binary", "json", "binary_threads", "json_threads"])
+def test_gpu_batcher_matches_serial_restatement(small_graph, json_path, threads):
     recs = make_stream(small_graph, n_veh=30, n_pts=80, seed=47)
     with Engine(graph_path=small_graph) as eng:
         bp = run_python(recs, lambda body: eng.report(body)[1])
-        nb = run_native(recs, Batcher(engine=eng, json_path=json_path))
+        nb = run_native(recs, Batcher(engine=eng, json_path=json_path, threads=threads))
         st = compare(bp, nb, recs)
         assert st["forwarded"] > 10 and st["match_batches"] < st["requests"]

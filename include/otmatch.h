@@ -318,7 +318,10 @@ void otm_batcher_defaults(otm_batcher_cfg* cfg);
  * frees or forwards them).  Returns 0. */
 typedef int (*otm_report_fn)(void* ctx, int n, const char* const* reqs, const size_t* lens, char** resps,
                              size_t* resp_lens, int* codes);
-/* eng: the matcher (fn == NULL); or fn/ctx: any /report handler (eng may be NULL). */
+/* eng: the matcher (fn == NULL); or fn/ctx: any /report handler (eng may be NULL).
+ * A batcher is one stream task, like the processor it restates: call it from
+ * one thread at a time (its own thread team, cfg.threads, is internal; the
+ * handler fn is only ever called from the calling thread). */
 int otm_batcher_create(otm_engine* eng, const otm_batcher_cfg* cfg, otm_report_fn fn, void* ctx,
                        otm_batcher** out);
 void otm_batcher_destroy(otm_batcher* b);

@@ -369,6 +369,9 @@ constexpr int HCAP = 512;  // edge hash slots (>= 2 * MAX_HITS)
 // buys occupancy; the ~1 % of probes with more edges in range spill.
 constexpr int CAND_LANE_CAP = OTM_CAND_LANE_CAP;
 constexpr int CAND_TB = 128;
+#ifndef OTM_TRANS_PACK
+#define OTM_TRANS_PACK 1
+#endif
 #ifndef OTM_CAND_FIND
 #define OTM_CAND_FIND 1
 #endif
@@ -1339,9 +1342,19 @@ template <int S>
 __global__ __launch_bounds__(TB, 8) void k_trans_sub(DevGraph g, DevBatch b, DevParams P, DevWork w) {
   if (*w.abort) return;  // a capacity was exceeded: the host redoes the batch
   constexpr int NS = TB / S;
+#if OTM_TRANS_PACK
+  // a pair reads its target and source as one 16-byte LDS word each;
+  // columns with more than KC candidates go to the online tiers
+  constexpr int KC = 16;
+  __shared__ int4 tg[NS][KC];  // target: edge, offset bits, from-node
+  __shared__ int4 sr[NS][KC];  // source: edge, offset bits, remaining-length bits
+  __shared__ IdxRow rq[NS][KC];
+#else
+  constexpr int KC = KMAX;
   __shared__ int32_t ep[NS][KMAX], vp[NS][KMAX], eq[NS][KMAX];
   __shared__ float op[NS][KMAX], oq[NS][KMAX], sq[NS][KMAX];
   __shared__ IdxRow rq[NS][KMAX];
+#endif
   const int lane = threadIdx.x, sg = lane / S, sl = lane % S;
   const unsigned long long smask = (S == 64 ? ~0ull : ((1ull << S) - 1ull)) << (sg * S);
   const DevIndex& X = w.idx;
@@ -1376,21 +1389,29 @@ __global__ __launch_bounds__(TB, 8) void k_trans_sub(DevGraph g, DevBatch b, Dev
     }
     const float bound = P.factor * gcv;
     const bool idx_ok = X.rmax > 0.0f && bound <= X.rmax;
-    bool bad = act && !idx_ok;
+    bool bad = act && (!idx_ok || Kp > KC || Kq > KC);
     // candidates of p (targets) and of q (sources), then edges, then rows
-    for (int k = sl; k < KMAX; k += S) {
+    for (int k = sl; k < KC; k += S) {
       if (act && k < Kp) {
         const int32_t e = w.cand_edge[p * KMAX + k];
+#if OTM_TRANS_PACK
+        tg[sg][k] = make_int4(e, __float_as_int(w.cand_off[p * KMAX + k]), g.e_from[e], 0);
+#else
         ep[sg][k] = e;
         op[sg][k] = w.cand_off[p * KMAX + k];
         vp[sg][k] = g.e_from[e];
+#endif
       }
       if (act && k < Kq) {
         const int32_t e = w.cand_edge[(int64_t)q * KMAX + k];
         const float o = w.cand_off[(int64_t)q * KMAX + k];
+#if OTM_TRANS_PACK
+        sr[sg][k] = make_int4(e, __float_as_int(o), __float_as_int(g.e_len[e] - o), 0);
+#else
         eq[sg][k] = e;
         oq[sg][k] = o;
         sq[sg][k] = g.e_len[e] - o;
+#endif
         if (idx_ok) {
           const IdxRow R = X.row[g.e_to[e]];
           rq[sg][k] = R;
@@ -1412,13 +1433,21 @@ __global__ __launch_bounds__(TB, 8) void k_trans_sub(DevGraph g, DevBatch b, Dev
         const int i = idx / Kp, j = idx - (idx / Kp) * Kp;
         float r = 0.0f;
         bool ok = true;
-        if (ep[sg][j] == eq[sg][i] && op[sg][j] >= oq[sg][i]) {
-          r = op[sg][j] - oq[sg][i];
+#if OTM_TRANS_PACK
+        const int4 T = tg[sg][j], Sx = sr[sg][i];
+        const int32_t ej = T.x, vj = T.z, ei = Sx.x;
+        const float oj = __int_as_float(T.y), oi = __int_as_float(Sx.y), si = __int_as_float(Sx.z);
+#else
+        const int32_t ej = ep[sg][j], vj = vp[sg][j], ei = eq[sg][i];
+        const float oj = op[sg][j], oi = oq[sg][i], si = sq[sg][i];
+#endif
+        if (ej == ei && oj >= oi) {
+          r = oj - oi;
         } else {
           float D;
-          if (idx_find(X, rq[sg][i], (uint32_t)vp[sg][j], D) >= 0) {
-            const float sd = sq[sg][i] + D;
-            r = sd + op[sg][j];
+          if (idx_find(X, rq[sg][i], (uint32_t)vj, D) >= 0) {
+            const float sd = si + D;
+            r = sd + oj;
           } else {
             ok = false;
           }

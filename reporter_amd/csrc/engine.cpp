@@ -228,8 +228,8 @@ void engine_free(otm_engine* E) {
   E->graph_allocs.clear();
   otm_engine::Buf* bufs[] = {
       &E->in_off,        &E->in_lat,       &E->in_lon,         &E->in_time,        &E->in_acc,     &E->pt_trace,
-      &E->is_col,        &E->prevc,        &E->gc,             &E->ncand,          &E->cand_edge,  &E->cand_off,
-      &E->cand_emis,     &E->col_prev,     &E->trans_off,      &E->trans,          &E->bp,         &E->state,
+      &E->is_col,        &E->prevc,        &E->gc,             &E->ncand,          &E->cand_edge,
+      &E->col_prev,     &E->trans_off,      &E->trans,          &E->bp,         &E->state,
       &E->chain_start,   &E->route_dist,   &E->path_off,       &E->path_len,       &E->path_pool,  &E->trace_err,
       &E->overflow_list0, &E->overflow_list, &E->overflow_list2, &E->counters_i32, &E->scan_tmp, &E->snap,   &E->big_key,
       &E->big_lab,       &E->big_inq,      &E->big_fr,         &E->o_traces,       &E->o_seg_cnt,  &E->o_way_cnt,
@@ -276,9 +276,7 @@ static int engine_match_once(otm_engine* E, const DevBatch& b, hipStream_t s, st
   ENS(prevc, Pn * 4);
   ENS(gc, Pn * 4);
   ENS(ncand, Pn * 4);
-  ENS(cand_edge, Pn * KMAX * 4);
-  ENS(cand_off, Pn * KMAX * 4);
-  ENS(cand_emis, Pn * KMAX * 4);
+  ENS(cand_edge, Pn * KMAX * 4 * CSTRIDE);  // the interleaved {edge, offset, emission} records
   ENS(col_prev, Pn * 4);
   ENS(trans_off, Pn * 8);
   ENS(bp, Pn * KMAX);
@@ -320,8 +318,8 @@ static int engine_match_once(otm_engine* E, const DevBatch& b, hipStream_t s, st
   w.gc = P<float>(E->gc);
   w.ncand = P<int32_t>(E->ncand);
   w.cand_edge = P<int32_t>(E->cand_edge);
-  w.cand_off = P<float>(E->cand_off);
-  w.cand_emis = P<float>(E->cand_emis);
+  w.cand_off = P<float>(E->cand_edge) + 1;
+  w.cand_emis = P<float>(E->cand_edge) + 2;
   w.col_prev = P<int32_t>(E->col_prev);
   w.trans_off = P<int64_t>(E->trans_off);
   w.bp = P<uint8_t>(E->bp);
@@ -589,9 +587,22 @@ int engine_debug_fetch(otm_engine* E, int what, void* dst, size_t bytes, size_t*
   size_t n = 0;
   switch (what) {
     case 0: src = E->ncand.p; n = Pn * 4; break;
-    case 1: src = E->cand_edge.p; n = Pn * KMAX * 4; break;
-    case 2: src = E->cand_off.p; n = Pn * KMAX * 4; break;
-    case 3: src = E->cand_emis.p; n = Pn * KMAX * 4; break;
+    case 1:
+    case 2:
+    case 3: {
+      // word (what - 1) of each interleaved candidate record, as [P*KMAX]
+      n = Pn * KMAX * 4;
+      if (needed) *needed = n;
+      if (!dst) return OTM_OK;
+      if (bytes < n) {
+        *err = "debug buffer too small";
+        return OTM_EINVAL;
+      }
+      const char* base = (const char*)E->cand_edge.p + 4 * (what - 1);
+      if (n) HIPCHK(hipMemcpy2DAsync(dst, 4, base, 4 * CSTRIDE, 4, Pn * KMAX, hipMemcpyDeviceToHost, E->stream));
+      HIPCHK(hipStreamSynchronize(E->stream));
+      return OTM_OK;
+    }
     case 4: src = E->trans_off.p; n = (Pn + 1) * 8; break;
     case 5: src = E->trans.p; n = (size_t)E->last_trans * 4; break;
     case 6: src = E->state.p; n = Pn * 4; break;

@@ -20,6 +20,7 @@
 namespace otm {
 
 constexpr int KMAX = 32;           // max candidates per column (== ORC_KMAX)
+constexpr int CSTRIDE = 3;         // words per candidate record (DevWork::cand_*)
 constexpr int MAX_HITS = 256;      // distinct edges within one radius (spec limit)
 constexpr int SEARCH_LIMIT = 24576;  // nodes settled by one search (spec limit)
 constexpr int LDS_TABLE_CAP = 256;   // K4/K6 LDS tier: table slots
@@ -126,9 +127,12 @@ struct DevWork {
   int32_t* prevc;        // [P] previous column (unlinked), -1
   float* gc;             // [P]
   int32_t* ncand;        // [P]
-  int32_t* cand_edge;    // [P*KMAX]
-  float* cand_off;       // [P*KMAX]
-  float* cand_emis;      // [P*KMAX]
+  // one interleaved record per candidate slot, {edge, offset, emission}
+  // (12 B): slot j of point p is element CSTRIDE * (p * KMAX + j) of each
+  // view, so a point's candidates share cache lines across the three
+  int32_t* cand_edge;    // [P*KMAX*3], view at word 0
+  float* cand_off;       // view at word 1
+  float* cand_emis;      // view at word 2
   int32_t* col_prev;     // [P] linked previous column, -1
   int64_t* trans_off;    // [P+1]
   float* trans;          // [total]

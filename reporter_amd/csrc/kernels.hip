@@ -518,9 +518,9 @@ __global__ __launch_bounds__(CAND_TB) void k_cand_lane(DevGraph g, DevBatch b, D
       const int32_t e = (int32_t)(em >> 4);
       float sqd, off;
       project(g, e, (int32_t)(em & 15u), lat, lon, ls, sqd, off);
-      w.cand_edge[p * KMAX + j] = e;
-      w.cand_off[p * KMAX + j] = off;
-      w.cand_emis[p * KMAX + j] = sqd / ds;
+      w.cand_edge[CSTRIDE * (p * KMAX + j)] = e;
+      w.cand_off[CSTRIDE * (p * KMAX + j)] = off;
+      w.cand_emis[CSTRIDE * (p * KMAX + j)] = sqd / ds;
     }
     w.ncand[p] = K;
     c_cells += cells;
@@ -678,9 +678,9 @@ __global__ __launch_bounds__(TB) void k_candidates(DevGraph g, DevBatch b, DevPa
       float sqd, off;
       project(g, e, kseg, lat, lon, ls, sqd, off);
       const float ds = (2.0f * P.sigma_z) * P.sigma_z;
-      w.cand_edge[p * KMAX + lane] = e;
-      w.cand_off[p * KMAX + lane] = off;
-      w.cand_emis[p * KMAX + lane] = sqd / ds;
+      w.cand_edge[CSTRIDE * (p * KMAX + lane)] = e;
+      w.cand_off[CSTRIDE * (p * KMAX + lane)] = off;
+      w.cand_emis[CSTRIDE * (p * KMAX + lane)] = sqd / ds;
     }
     if (lane == 0) {
       w.ncand[p] = K;
@@ -976,18 +976,19 @@ __global__ __launch_bounds__(LANE_TB) void k_trans_lane(DevGraph g, DevBatch b, 
     const int Kq = w.ncand[q], Kp = w.ncand[p];
     const float gcv = w.gc[p];
     const float bound = P.factor * gcv;
-    const int32_t* eq = w.cand_edge + (int64_t)q * KMAX;
-    const float* oq = w.cand_off + (int64_t)q * KMAX;
-    const int32_t* ep = w.cand_edge + p * KMAX;
-    const float* op = w.cand_off + p * KMAX;
+    // this point's and the previous column's candidate records (CSTRIDE words apart)
+    const int32_t* eq = w.cand_edge + CSTRIDE * ((int64_t)q * KMAX);
+    const float* oq = w.cand_off + CSTRIDE * ((int64_t)q * KMAX);
+    const int32_t* ep = w.cand_edge + CSTRIDE * (p * KMAX);
+    const float* op = w.cand_off + CSTRIDE * (p * KMAX);
     float* Tm = w.trans + w.trans_off[p];
     unsigned long long s_search = 0, s_settled = 0, s_relaxed = 0, s_trans = 0;
     bool failed = false;
     for (int i = 0; i < Kq && !failed; ++i) {
-      const int32_t u = g.e_to[eq[i]];
+      const int32_t u = g.e_to[eq[CSTRIDE * (i)]];
       bool first = true;
       for (int k = 0; k < i; ++k)
-        if (g.e_to[eq[k]] == u) {
+        if (g.e_to[eq[CSTRIDE * (k)]] == u) {
           first = false;
           break;
         }
@@ -1002,21 +1003,21 @@ __global__ __launch_bounds__(LANE_TB) void k_trans_lane(DevGraph g, DevBatch b, 
       s_settled += (unsigned long long)n;
       s_relaxed += rel;
       for (int ii = i; ii < Kq; ++ii) {
-        if (g.e_to[eq[ii]] != u) continue;
-        const float start = g.e_len[eq[ii]] - oq[ii];
+        if (g.e_to[eq[CSTRIDE * (ii)]] != u) continue;
+        const float start = g.e_len[eq[CSTRIDE * (ii)]] - oq[CSTRIDE * (ii)];
         for (int j = 0; j < Kp; ++j) {
           float r;
           bool ok = true;
-          if (ep[j] == eq[ii] && op[j] >= oq[ii]) {
-            r = op[j] - oq[ii];
+          if (ep[CSTRIDE * (j)] == eq[CSTRIDE * (ii)] && op[CSTRIDE * (j)] >= oq[CSTRIDE * (ii)]) {
+            r = op[CSTRIDE * (j)] - oq[CSTRIDE * (ii)];
           } else {
-            const int f = lane_find<CAP>(K, n, (uint32_t)g.e_from[ep[j]]);
+            const int f = lane_find<CAP>(K, n, (uint32_t)g.e_from[ep[CSTRIDE * (j)]]);
             if (f < 0) {
               ok = false;
               r = 0.0f;
             } else {
               const float sd = start + D[f * LANE_TB];
-              r = sd + op[j];
+              r = sd + op[CSTRIDE * (j)];
             }
           }
           float cost = INFINITY;
@@ -1067,8 +1068,8 @@ __global__ __launch_bounds__(LANE_TB) void k_route_lane(DevGraph g, DevBatch b, 
     const int64_t p = w.overflow_list0[it];
     const int32_t q = w.col_prev[p];
     const int i = w.state[q], j = w.state[p];
-    const int32_t ei = w.cand_edge[(int64_t)q * KMAX + i], ej = w.cand_edge[p * KMAX + j];
-    const float oi = w.cand_off[(int64_t)q * KMAX + i], oj = w.cand_off[p * KMAX + j];
+    const int32_t ei = w.cand_edge[CSTRIDE * ((int64_t)q * KMAX + i)], ej = w.cand_edge[CSTRIDE * (p * KMAX + j)];
+    const float oi = w.cand_off[CSTRIDE * ((int64_t)q * KMAX + i)], oj = w.cand_off[CSTRIDE * (p * KMAX + j)];
     const float bound = P.factor * w.gc[p];
     const int32_t u = g.e_to[ei], v = g.e_from[ej];
     unsigned long long rel = 0;
@@ -1227,8 +1228,8 @@ __global__ __launch_bounds__(TB, 8) void k_trans_index(DevGraph g, DevBatch b, D
     int32_t e_p = 0;
     float o_p = 0.0f;
     if (lane < KMAX) {
-      e_p = w.cand_edge[p * KMAX + lane];
-      o_p = w.cand_off[p * KMAX + lane];
+      e_p = w.cand_edge[CSTRIDE * (p * KMAX + lane)];
+      o_p = w.cand_off[CSTRIDE * (p * KMAX + lane)];
     }
     if (q < 0) continue;
     // by q
@@ -1236,8 +1237,8 @@ __global__ __launch_bounds__(TB, 8) void k_trans_index(DevGraph g, DevBatch b, D
     int32_t e_q = 0;
     float o_q = 0.0f;
     if (lane < KMAX) {
-      e_q = w.cand_edge[(int64_t)q * KMAX + lane];
-      o_q = w.cand_off[(int64_t)q * KMAX + lane];
+      e_q = w.cand_edge[CSTRIDE * ((int64_t)q * KMAX + lane)];
+      o_q = w.cand_off[CSTRIDE * ((int64_t)q * KMAX + lane)];
     }
     // by edge
     int32_t u = 0;
@@ -1393,18 +1394,18 @@ __global__ __launch_bounds__(TB, 8) void k_trans_sub(DevGraph g, DevBatch b, Dev
     // candidates of p (targets) and of q (sources), then edges, then rows
     for (int k = sl; k < KC; k += S) {
       if (act && k < Kp) {
-        const int32_t e = w.cand_edge[p * KMAX + k];
+        const int32_t e = w.cand_edge[CSTRIDE * (p * KMAX + k)];
 #if OTM_TRANS_PACK
-        tg[sg][k] = make_int4(e, __float_as_int(w.cand_off[p * KMAX + k]), g.e_from[e], 0);
+        tg[sg][k] = make_int4(e, __float_as_int(w.cand_off[CSTRIDE * (p * KMAX + k)]), g.e_from[e], 0);
 #else
         ep[sg][k] = e;
-        op[sg][k] = w.cand_off[p * KMAX + k];
+        op[sg][k] = w.cand_off[CSTRIDE * (p * KMAX + k)];
         vp[sg][k] = g.e_from[e];
 #endif
       }
       if (act && k < Kq) {
-        const int32_t e = w.cand_edge[(int64_t)q * KMAX + k];
-        const float o = w.cand_off[(int64_t)q * KMAX + k];
+        const int32_t e = w.cand_edge[CSTRIDE * ((int64_t)q * KMAX + k)];
+        const float o = w.cand_off[CSTRIDE * ((int64_t)q * KMAX + k)];
 #if OTM_TRANS_PACK
         sr[sg][k] = make_int4(e, __float_as_int(o), __float_as_int(g.e_len[e] - o), 0);
 #else
@@ -1517,8 +1518,8 @@ __global__ __launch_bounds__(256) void k_route_index(DevGraph g, DevBatch b, Dev
     if (w.state[p] < 0 || w.chain_start[p]) continue;
     const int32_t q = w.col_prev[p];
     const int i = w.state[q], j = w.state[p];
-    const int32_t ei = w.cand_edge[(int64_t)q * KMAX + i], ej = w.cand_edge[p * KMAX + j];
-    const float oi = w.cand_off[(int64_t)q * KMAX + i], oj = w.cand_off[p * KMAX + j];
+    const int32_t ei = w.cand_edge[CSTRIDE * ((int64_t)q * KMAX + i)], ej = w.cand_edge[CSTRIDE * (p * KMAX + j)];
+    const float oi = w.cand_off[CSTRIDE * ((int64_t)q * KMAX + i)], oj = w.cand_off[CSTRIDE * (p * KMAX + j)];
     if (ei == ej && oj >= oi) {
       w.route_dist[p] = oj - oi;
       continue;
@@ -1630,12 +1631,12 @@ __global__ __launch_bounds__(TB) void k_transitions(DevGraph g, DevBatch b, DevP
     const float gcv = w.gc[p];
     const float bound = P.factor * gcv;
     if (lane < Kq) {
-      eq[lane] = w.cand_edge[(int64_t)q * KMAX + lane];
-      oq[lane] = w.cand_off[(int64_t)q * KMAX + lane];
+      eq[lane] = w.cand_edge[CSTRIDE * ((int64_t)q * KMAX + lane)];
+      oq[lane] = w.cand_off[CSTRIDE * ((int64_t)q * KMAX + lane)];
     }
     if (lane < Kp) {
-      ep[lane] = w.cand_edge[p * KMAX + lane];
-      op[lane] = w.cand_off[p * KMAX + lane];
+      ep[lane] = w.cand_edge[CSTRIDE * (p * KMAX + lane)];
+      op[lane] = w.cand_off[CSTRIDE * (p * KMAX + lane)];
     }
     __syncthreads();
     // distinct source nodes (first occurrence order)
@@ -1782,7 +1783,7 @@ __device__ void viterbi_trace_global(int64_t a, int64_t e, DevWork& w) {
         }
         const bool alive = lane < Kp && bi >= 0;
         if (lane < Kp) {
-          cur = alive ? best + w.cand_emis[p * KMAX + lane] : INFINITY;
+          cur = alive ? best + w.cand_emis[CSTRIDE * (p * KMAX + lane)] : INFINITY;
           w.bp[p * KMAX + lane] = alive ? (uint8_t)bi : (uint8_t)0xFF;
         }
         if (__ballot(alive) == 0ull) {
@@ -1794,7 +1795,7 @@ __device__ void viterbi_trace_global(int64_t a, int64_t e, DevWork& w) {
         backtrack(last);
       }
       if (!started) {
-        cur = lane < Kp ? w.cand_emis[p * KMAX + lane] : INFINITY;
+        cur = lane < Kp ? w.cand_emis[CSTRIDE * (p * KMAX + lane)] : INFINITY;
         if (lane == 0) w.chain_start[p] = 1;
       }
       prev = cur;
@@ -1991,7 +1992,7 @@ __global__ __launch_bounds__(TB) void k_viterbi(DevBatch b, DevWork w) {
               float v[4];
 #pragma unroll
               for (int u = 0; u < 4; ++u)
-                v[u] = j0 + u < kq ? w.cand_emis[(a + q) * KMAX + j0 + u] : 0.0f;
+                v[u] = j0 + u < kq ? w.cand_emis[CSTRIDE * ((a + q) * KMAX + j0 + u)] : 0.0f;
 #pragma unroll
               for (int u = 0; u < 4; ++u)
                 if (j0 + u < kq) sEm[eq + j0 + u] = v[u];
@@ -2093,8 +2094,8 @@ __global__ __launch_bounds__(TB) void k_route(DevGraph g, DevBatch b, DevParams 
     const int64_t p = (int64_t)list[it];
     const int32_t q = w.col_prev[p];
     const int i = w.state[q], j = w.state[p];
-    const int32_t ei = w.cand_edge[(int64_t)q * KMAX + i], ej = w.cand_edge[p * KMAX + j];
-    const float oi = w.cand_off[(int64_t)q * KMAX + i], oj = w.cand_off[p * KMAX + j];
+    const int32_t ei = w.cand_edge[CSTRIDE * ((int64_t)q * KMAX + i)], ej = w.cand_edge[CSTRIDE * (p * KMAX + j)];
+    const float oi = w.cand_off[CSTRIDE * ((int64_t)q * KMAX + i)], oj = w.cand_off[CSTRIDE * (p * KMAX + j)];
     if (ei == ej && oj >= oi) {
       if (lane == 0) w.route_dist[p] = oj - oi;
       continue;
@@ -2286,8 +2287,8 @@ struct SegSrcGlobal {
   __device__ float rd(int pl) const { return w->route_dist[a + pl]; }
   __device__ int32_t poff(int pl) const { return w->path_off[a + pl]; }
   __device__ int32_t plen(int pl) const { return w->path_len[a + pl]; }
-  __device__ int32_t edge(int pl) const { return w->cand_edge[(a + pl) * KMAX + w->state[a + pl]]; }
-  __device__ float off(int pl) const { return w->cand_off[(a + pl) * KMAX + w->state[a + pl]]; }
+  __device__ int32_t edge(int pl) const { return w->cand_edge[CSTRIDE * ((a + pl) * KMAX + w->state[a + pl])]; }
+  __device__ float off(int pl) const { return w->cand_off[CSTRIDE * ((a + pl) * KMAX + w->state[a + pl])]; }
   __device__ EAttr attr(int pl) const { return edge_attr(*g, edge(pl)); }
 };
 
@@ -2444,12 +2445,12 @@ __device__ __forceinline__ StateStep state_step(const DevWork& w, int64_t a, con
   r.step = !r.cs && k > 0;
   r.lp = r.step ? S.sidx[k - 1] : r.pl;
   const int sj = w.state[p];
-  r.ej = w.cand_edge[p * KMAX + sj];
-  r.oj = w.cand_off[p * KMAX + sj];
+  r.ej = w.cand_edge[CSTRIDE * (p * KMAX + sj)];
+  r.oj = w.cand_off[CSTRIDE * (p * KMAX + sj)];
   const int64_t q = a + r.lp;
   const int si = w.state[q];
-  r.ei = w.cand_edge[q * KMAX + si];
-  r.oi = w.cand_off[q * KMAX + si];
+  r.ei = w.cand_edge[CSTRIDE * (q * KMAX + si)];
+  r.oi = w.cand_off[CSTRIDE * (q * KMAX + si)];
   r.same = r.step && r.ei == r.ej && r.oj >= r.oi;
   r.plen = 0;
   r.poff = 0;

@@ -50,8 +50,8 @@ KERNEL_STAGE = {
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--vehicles", type=int, default=10000, help="per GPU")
     ap.add_argument("--points", type=int, default=100, help="per vehicle")
     ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (0: min(16, cores))")

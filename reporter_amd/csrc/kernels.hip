@@ -282,10 +282,22 @@ __global__ __launch_bounds__(TB) void k_columns(DevGraph g, DevBatch b, DevParam
         sLon[pl] = b.lon[a + pl];
       }
       __syncthreads();
-      for (int pl = lane; pl < n; pl += TB)
-        sGc[pl] = pl > 0 ? gc_dist(sLat[pl - 1], sLon[pl - 1], sLat[pl], sLon[pl]) : 0.0f;
+      bool near = false;  // some step shorter than the interpolation distance
+      for (int pl = lane; pl < n; pl += TB) {
+        const float d = pl > 0 ? gc_dist(sLat[pl - 1], sLon[pl - 1], sLat[pl], sLon[pl]) : 0.0f;
+        sGc[pl] = d;
+        near = near || (pl > 0 && !(d >= P.interp));
+      }
       __syncthreads();
-      if (lane == 0) {
+      if (__ballot(near) == 0ull) {
+        // every step is at least the interpolation distance: every point is a
+        // column linked to the one before (what the serial filter below gives)
+        for (int pl = lane; pl < n; pl += TB) {
+          sCol[pl] = 1;
+          sPrev[pl] = pl > 0 ? (int32_t)(a + pl - 1) : -1;
+        }
+        ncols = n;
+      } else if (lane == 0) {
         int last = -1;
         for (int pl = 0; pl < n; ++pl) {
           float gcv = 0.0f;

@@ -21,6 +21,18 @@ namespace otm {
   } while (0)
 
 static int ensure(otm_engine::Buf& b, size_t bytes, std::string* err);
+// host-pinned buffer of at least `bytes` (contents not kept on growth)
+static int ensure_pinned(otm_engine::Buf& b, size_t bytes, std::string* err) {
+  if (bytes == 0) bytes = 16;
+  if (b.cap >= bytes) return OTM_OK;
+  if (b.p) (void)hipHostFree(b.p);
+  b.p = nullptr;
+  b.cap = 0;
+  const size_t want = bytes + bytes / 4;
+  HIPCHK(hipHostMalloc(&b.p, want, hipHostMallocDefault));
+  b.cap = want;
+  return OTM_OK;
+}
 #define ENS_F(buf, bytes) \
   if ((rc = ensure(E->buf, (bytes), err))) return rc;
 
@@ -227,7 +239,8 @@ void engine_free(otm_engine* E) {
   for (void* p : E->graph_allocs) (void)hipFree(p);
   E->graph_allocs.clear();
   otm_engine::Buf* bufs[] = {
-      &E->in_off,        &E->in_lat,       &E->in_lon,         &E->in_time,        &E->in_acc,     &E->pt_trace,
+      &E->in_off,        &E->in_lat,       &E->in_lon,         &E->in_time,        &E->in_acc,     &E->in_blob,
+      &E->pt_trace,
       &E->is_col,        &E->prevc,        &E->gc,             &E->ncand,          &E->cand_edge,
       &E->col_prev,     &E->trans_off,      &E->trans,          &E->bp,         &E->state,
       &E->chain_start,   &E->route_dist,   &E->path_off,       &E->path_len,       &E->path_pool,  &E->trace_err,
@@ -238,6 +251,11 @@ void engine_free(otm_engine* E) {
       &E->abort_flag,    &E->ord_tile,      &E->ord_cnt,      &E->ord_cursor,     &E->ord_grp,    &E->ord_item};
   for (auto* b : bufs) {
     if (b->p) (void)hipFree(b->p);
+    b->p = nullptr;
+    b->cap = 0;
+  }
+  for (auto* b : {&E->h_traces, &E->h_segs, &E->h_reps_dense, &E->h_ways, &E->h_tot, &E->h_in}) {
+    if (b->p) (void)hipHostFree(b->p);
     b->p = nullptr;
     b->cap = 0;
   }
@@ -494,16 +512,39 @@ int engine_match_host(otm_engine* E, const otm_batch* in, std::string* err) {
   if ((rc = ensure(E->in_time, (size_t)NP * 8, err))) return rc;
   if ((rc = ensure(E->in_acc, (size_t)NP * 4, err))) return rc;
   hipStream_t s = E->stream;
-  HIPCHK(hipMemcpyAsync(E->in_off.p, in->trace_off, ((size_t)NT + 1) * 8, hipMemcpyHostToDevice, s));
-  if (NP) {
-    HIPCHK(hipMemcpyAsync(E->in_lat.p, in->lat, (size_t)NP * 4, hipMemcpyHostToDevice, s));
-    HIPCHK(hipMemcpyAsync(E->in_lon.p, in->lon, (size_t)NP * 4, hipMemcpyHostToDevice, s));
-    HIPCHK(hipMemcpyAsync(E->in_time.p, in->time, (size_t)NP * 8, hipMemcpyHostToDevice, s));
-    HIPCHK(hipMemcpyAsync(E->in_acc.p, in->accuracy, (size_t)NP * 4, hipMemcpyHostToDevice, s));
-  }
+  const size_t b_off = ((size_t)NT + 1) * 8, b_pt = (size_t)NP * 4, b_tm = (size_t)NP * 8;
   DevBatch b;
   b.n_traces = NT;
   b.n_points = NP;
+  if (NP <= (int64_t)1 << 18) {
+    // small batches: one host copy into pinned staging, then ONE DMA into a
+    // device blob laid out the same way (offsets, times, lat, lon, accuracy:
+    // every section stays 8-byte aligned) -- the batcher's rounds, single requests
+    const size_t total = b_off + b_tm + 3 * b_pt;
+    if ((rc = ensure_pinned(E->h_in, total, err))) return rc;
+    if ((rc = ensure(E->in_blob, total, err))) return rc;
+    char* h = (char*)E->h_in.p;
+    std::memcpy(h, in->trace_off, b_off);
+    if (NP) {
+      std::memcpy(h + b_off, in->time, b_tm);
+      std::memcpy(h + b_off + b_tm, in->lat, b_pt);
+      std::memcpy(h + b_off + b_tm + b_pt, in->lon, b_pt);
+      std::memcpy(h + b_off + b_tm + 2 * b_pt, in->accuracy, b_pt);
+    }
+    HIPCHK(hipMemcpyAsync(E->in_blob.p, h, total, hipMemcpyHostToDevice, s));
+    const char* d = (const char*)E->in_blob.p;
+    b.trace_off = (const int64_t*)d;
+    b.time = (const double*)(d + b_off);
+    b.lat = (const float*)(d + b_off + b_tm);
+    b.lon = (const float*)(d + b_off + b_tm + b_pt);
+    b.acc = (const float*)(d + b_off + b_tm + 2 * b_pt);
+    return engine_match(E, b, s, err);
+  }
+  HIPCHK(hipMemcpyAsync(E->in_off.p, in->trace_off, b_off, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(E->in_lat.p, in->lat, b_pt, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(E->in_lon.p, in->lon, b_pt, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(E->in_time.p, in->time, b_tm, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(E->in_acc.p, in->accuracy, b_pt, hipMemcpyHostToDevice, s));
   b.trace_off = (const int64_t*)E->in_off.p;
   b.lat = (const float*)E->in_lat.p;
   b.lon = (const float*)E->in_lon.p;
@@ -524,8 +565,17 @@ int engine_fetch(otm_engine* E, otm_results* out, std::string* err) {
   int32_t* so = P<int32_t>(E->f_seg_off);
   int32_t* wo = P<int32_t>(E->f_way_off);
   int32_t* ro = P<int32_t>(E->f_rep_off);
-  int32_t tot[3] = {0, 0, 0};
-  if (NT) {
+  if ((rc = ensure_pinned(E->h_tot, 16, err))) return rc;
+  int32_t* tot = (int32_t*)E->h_tot.p;
+  tot[0] = tot[1] = tot[2] = 0;
+  if (NT && NT <= FETCH_SCAN_MAX) {
+    // small batches (the batcher's rounds): the three scans in one launch
+    launch_fetch_scan(NT, P<int32_t>(E->o_seg_cnt), P<int32_t>(E->o_way_cnt), P<int32_t>(E->o_rep_cnt), so, wo, ro, s);
+    HIPCHK(hipMemcpyAsync(tot, so + NT, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(tot + 1, wo + NT, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(tot + 2, ro + NT, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+  } else if (NT) {
     HIPCHK(hipMemcpyAsync(so, E->o_seg_cnt.p, (size_t)NT * 4, hipMemcpyDeviceToDevice, s));
     HIPCHK(hipMemcpyAsync(wo, E->o_way_cnt.p, (size_t)NT * 4, hipMemcpyDeviceToDevice, s));
     HIPCHK(hipMemcpyAsync(ro, E->o_rep_cnt.p, (size_t)NT * 4, hipMemcpyDeviceToDevice, s));
@@ -535,9 +585,9 @@ int engine_fetch(otm_engine* E, otm_results* out, std::string* err) {
     scan_i32(so, NT, E->scan_tmp.p, E->scan_tmp.cap, s);
     scan_i32(wo, NT, E->scan_tmp.p, E->scan_tmp.cap, s);
     scan_i32(ro, NT, E->scan_tmp.p, E->scan_tmp.cap, s);
-    HIPCHK(hipMemcpyAsync(&tot[0], so + NT, 4, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(&tot[1], wo + NT, 4, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(&tot[2], ro + NT, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(tot, so + NT, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(tot + 1, wo + NT, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(tot + 2, ro + NT, 4, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
   }
   const int32_t NS = tot[0], NW = tot[1], NR = tot[2];
@@ -558,26 +608,25 @@ int engine_fetch(otm_engine* E, otm_results* out, std::string* err) {
   }
   E->last_S = NS;
   E->last_W = NW;
-  E->h_traces.resize((size_t)NT + 1);
-  E->h_segs.resize((size_t)NS + 1);
-  E->h_reps_dense.resize((size_t)NR + 1);
-  E->h_ways.resize((size_t)NW + 1);
-  if (NT) HIPCHK(hipMemcpyAsync(E->h_traces.data(), E->o_traces.p, (size_t)NT * sizeof(otm_trace_result),
+  if ((rc = ensure_pinned(E->h_traces, ((size_t)NT + 1) * sizeof(otm_trace_result), err))) return rc;
+  if ((rc = ensure_pinned(E->h_segs, ((size_t)NS + 1) * sizeof(otm_segment), err))) return rc;
+  if ((rc = ensure_pinned(E->h_reps_dense, ((size_t)NR + 1) * sizeof(otm_report_rec), err))) return rc;
+  if ((rc = ensure_pinned(E->h_ways, ((size_t)NW + 1) * 8, err))) return rc;
+  if (NT) HIPCHK(hipMemcpyAsync(E->h_traces.p, E->o_traces.p, (size_t)NT * sizeof(otm_trace_result),
                                 hipMemcpyDeviceToHost, s));
-  if (NS) HIPCHK(hipMemcpyAsync(E->h_segs.data(), E->f_segs.p, (size_t)NS * sizeof(otm_segment), hipMemcpyDeviceToHost,
-                                s));
-  if (NR) HIPCHK(hipMemcpyAsync(E->h_reps_dense.data(), E->f_reps.p, (size_t)NR * sizeof(otm_report_rec),
+  if (NS) HIPCHK(hipMemcpyAsync(E->h_segs.p, E->f_segs.p, (size_t)NS * sizeof(otm_segment), hipMemcpyDeviceToHost, s));
+  if (NR) HIPCHK(hipMemcpyAsync(E->h_reps_dense.p, E->f_reps.p, (size_t)NR * sizeof(otm_report_rec),
                                 hipMemcpyDeviceToHost, s));
-  if (NW) HIPCHK(hipMemcpyAsync(E->h_ways.data(), E->f_ways.p, (size_t)NW * 8, hipMemcpyDeviceToHost, s));
+  if (NW) HIPCHK(hipMemcpyAsync(E->h_ways.p, E->f_ways.p, (size_t)NW * 8, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
   out->n_traces = NT;
   out->n_segments = NS;
   out->n_reports = NR;
   out->n_way_ids = NW;
-  out->traces = E->h_traces.data();
-  out->segments = E->h_segs.data();
-  out->reports = E->h_reps_dense.data();
-  out->way_ids = E->h_ways.data();
+  out->traces = (const otm_trace_result*)E->h_traces.p;
+  out->segments = (const otm_segment*)E->h_segs.p;
+  out->reports = (const otm_report_rec*)E->h_reps_dense.p;
+  out->way_ids = (const int64_t*)E->h_ways.p;
   return OTM_OK;
 }
 

@@ -42,7 +42,7 @@ struct otm_engine {
     size_t cap = 0;
   };
   // batch inputs (host batches are staged here)
-  Buf in_off, in_lat, in_lon, in_time, in_acc;
+  Buf in_off, in_lat, in_lon, in_time, in_acc, in_blob;
   // work
   Buf pt_trace, is_col, prevc, gc, ncand, cand_edge /* interleaved records */, col_prev, trans_off, trans, bp, state,
       chain_start, route_dist, path_off, path_len, path_pool, trace_err, overflow_list0, overflow_list, overflow_list2,
@@ -69,10 +69,8 @@ struct otm_engine {
   int64_t last_trans = 0;
   int32_t pool_cap = 0;
   // host copies of the last fetched results
-  std::vector<otm_trace_result> h_traces;
-  std::vector<otm_segment> h_segs;
-  std::vector<otm_report_rec> h_reps_dense;
-  std::vector<int64_t> h_ways;
+  // (pinned: the D2H copies run at PCIe speed without a staging hop)
+  Buf h_traces, h_segs, h_reps_dense, h_ways, h_tot, h_in;
   // timing
   bool timing = false;
   hipEvent_t kev[2 * otm::KN_COUNT] = {};

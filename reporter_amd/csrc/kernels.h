@@ -255,6 +255,11 @@ void launch_row_sizes(const int32_t* row_cnt, int64_t* row_sizes, int32_t n, hip
 void launch_row_pack(const int32_t* row_cnt, const int64_t* row_off, IdxRow* rows, int32_t n, hipStream_t s);
 // exclusive scan helpers (in place over n+1 elements: out[n] = total)
 void scan_i64(int64_t* d, int64_t n, void* tmp, size_t tmp_bytes, hipStream_t s);
+// exclusive scans of three per-trace counts (n <= FETCH_SCAN_MAX) in one
+// single-block launch, totals at o*[n]
+constexpr int FETCH_SCAN_MAX = 1 << 16;
+void launch_fetch_scan(int32_t n, const int32_t* c0, const int32_t* c1, const int32_t* c2, int32_t* o0, int32_t* o1,
+                       int32_t* o2, hipStream_t s);
 void scan_i32(int32_t* d, int64_t n, void* tmp, size_t tmp_bytes, hipStream_t s);
 size_t scan_tmp_bytes(int64_t n);
 

@@ -2882,6 +2882,65 @@ __global__ __launch_bounds__(TB) void k_compact(int32_t n_traces, DevOut o, cons
   }
 }
 
+// One block of 1024 threads: each thread sums a contiguous chunk of the
+// three count arrays, a block scan gives its chunk's bases, then the chunk's
+// exclusive offsets are written; totals at o*[n].
+__global__ __launch_bounds__(1024) void k_fetch_scan(int32_t n, const int32_t* c0, const int32_t* c1,
+                                                     const int32_t* c2, int32_t* o0, int32_t* o1, int32_t* o2) {
+  __shared__ int32_t ws[3][16];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int per = (n + 1023) / 1024;
+  const int a = min(n, t * per), e = min(n, a + per);
+  int s0 = 0, s1 = 0, s2 = 0;
+  for (int i = a; i < e; ++i) {
+    s0 += c0[i];
+    s1 += c1[i];
+    s2 += c2[i];
+  }
+  // inclusive scans within the wave, then across the 16 waves
+  int i0 = s0, i1 = s1, i2 = s2;
+  for (int o = 1; o < 64; o <<= 1) {
+    const int x0 = __shfl_up(i0, o, 64), x1 = __shfl_up(i1, o, 64), x2 = __shfl_up(i2, o, 64);
+    if (lane >= o) {
+      i0 += x0;
+      i1 += x1;
+      i2 += x2;
+    }
+  }
+  if (lane == 63) {
+    ws[0][wv] = i0;
+    ws[1][wv] = i1;
+    ws[2][wv] = i2;
+  }
+  __syncthreads();
+  int b0 = 0, b1 = 0, b2 = 0;
+  for (int k = 0; k < wv; ++k) {
+    b0 += ws[0][k];
+    b1 += ws[1][k];
+    b2 += ws[2][k];
+  }
+  int r0 = b0 + i0 - s0, r1 = b1 + i1 - s1, r2 = b2 + i2 - s2;  // this chunk's exclusive bases
+  for (int i = a; i < e; ++i) {
+    o0[i] = r0;
+    o1[i] = r1;
+    o2[i] = r2;
+    r0 += c0[i];
+    r1 += c1[i];
+    r2 += c2[i];
+  }
+  if (t == 1023) {
+    int z0 = 0, z1 = 0, z2 = 0;
+    for (int k = 0; k < 16; ++k) {
+      z0 += ws[0][k];
+      z1 += ws[1][k];
+      z2 += ws[2][k];
+    }
+    o0[n] = z0;
+    o1[n] = z1;
+    o2[n] = z2;
+  }
+}
+
 int grid_for(int64_t n, int per_block, int cap) {
   int64_t g = (n + per_block - 1) / per_block;
   if (g < 1) g = 1;
@@ -2893,6 +2952,12 @@ constexpr int WAVE_GRID_CAP = 256 * 64;  // grid-stride cap for wave kernels
 constexpr int TRANS_GRID_CAP = 65536;  // k_trans_index waves (one per column, grid-striding beyond)
 
 }  // namespace
+
+void launch_fetch_scan(int32_t n, const int32_t* c0, const int32_t* c1, const int32_t* c2, int32_t* o0, int32_t* o1,
+                       int32_t* o2, hipStream_t s) {
+  hipLaunchKernelGGL(k_fetch_scan, dim3(1), dim3(1024), 0, s, n, c0, c1, c2, o0, o1, o2);
+}
+
 
 const char* const kKernelNames[KN_COUNT] = {
     "k_columns",       "spatial_order",  "k_cand_lane",    "k_candidates",     "k_links",         "scan_trans_off",  "k_trans_index",

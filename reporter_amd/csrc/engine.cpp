@@ -242,7 +242,7 @@ void engine_free(otm_engine* E) {
       &E->in_off,        &E->in_lat,       &E->in_lon,         &E->in_time,        &E->in_acc,     &E->in_blob,
       &E->pt_trace,
       &E->is_col,        &E->prevc,        &E->gc,             &E->ncand,          &E->cand_edge,
-      &E->col_prev,     &E->trans_off,      &E->trans,          &E->bp,         &E->state,
+      &E->probe,         &E->col_prev,     &E->trans_off,      &E->trans,          &E->bp,         &E->state,
       &E->chain_start,   &E->route_dist,   &E->path_off,       &E->path_len,       &E->path_pool,  &E->trace_err,
       &E->overflow_list0, &E->overflow_list, &E->overflow_list2, &E->counters_i32, &E->scan_tmp, &E->snap,   &E->big_key,
       &E->big_lab,       &E->big_inq,      &E->big_fr,         &E->o_traces,       &E->o_seg_cnt,  &E->o_way_cnt,
@@ -295,6 +295,7 @@ static int engine_match_once(otm_engine* E, const DevBatch& b, hipStream_t s, st
   ENS(gc, Pn * 4);
   ENS(ncand, Pn * 4);
   ENS(cand_edge, Pn * KMAX * 4 * CSTRIDE);  // the interleaved {edge, offset, emission} records
+  ENS(probe, Pn * 16);
   ENS(col_prev, Pn * 4);
   ENS(trans_off, Pn * 8);
   ENS(bp, Pn * KMAX);
@@ -335,6 +336,7 @@ static int engine_match_once(otm_engine* E, const DevBatch& b, hipStream_t s, st
   w.prevc = P<int32_t>(E->prevc);
   w.gc = P<float>(E->gc);
   w.ncand = P<int32_t>(E->ncand);
+  w.probe = P<float4>(E->probe);
   w.cand_edge = P<int32_t>(E->cand_edge);
   w.cand_off = P<float>(E->cand_edge) + 1;
   w.cand_emis = P<float>(E->cand_edge) + 2;

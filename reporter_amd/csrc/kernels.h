@@ -127,6 +127,7 @@ struct DevWork {
   int32_t* prevc;        // [P] previous column (unlinked), -1
   float* gc;             // [P]
   int32_t* ncand;        // [P]
+  float4* probe;         // [P] {lat, lon, accuracy, 0}: a probe's inputs in one line (K1)
   // one interleaved record per candidate slot, {edge, offset, emission}
   // (12 B): slot j of point p is element CSTRIDE * (p * KMAX + j) of each
   // view, so a point's candidates share cache lines across the three

@@ -270,6 +270,7 @@ __global__ __launch_bounds__(TB) void k_columns(DevGraph g, DevBatch b, DevParam
         }
       }
       for (int64_t p = a + lane; p < e; p += TB) {
+        w.probe[p] = make_float4(b.lat[p], b.lon[p], b.acc[p], 0.0f);
         w.pt_trace[p] = t;
         w.ncand[p] = 0;
         w.route_dist[p] = 0.0f;
@@ -319,6 +320,7 @@ __global__ __launch_bounds__(TB) void k_columns(DevGraph g, DevBatch b, DevParam
         const bool col = in && sCol[pl];
         if (in) {
           const int64_t p = a + pl;
+          w.probe[p] = make_float4(sLat[pl], sLon[pl], b.acc[p], 0.0f);
           w.pt_trace[p] = t;
           w.is_col[p] = sCol[pl];
           w.gc[p] = sGc[pl];
@@ -417,8 +419,9 @@ __global__ __launch_bounds__(CAND_TB) void k_cand_lane(DevGraph g, DevBatch b, D
       w.overflow_list0[slot] = (int32_t)p;
       continue;
     }
-    const float lat = b.lat[p], lon = b.lon[p];
-    const float r = probe_radius(P, b.acc[p]);
+    const float4 pr = w.probe[p];  // {lat, lon, accuracy} of the column (K1), one line
+    const float lat = pr.x, lon = pr.y;
+    const float r = probe_radius(P, pr.z);
     const float r2 = r * r;
     const float ls = MPD_F * cos_deg(lat);
     const float dlat = r / MPD_F;
@@ -558,8 +561,9 @@ __global__ __launch_bounds__(TB) void k_candidates(DevGraph g, DevBatch b, DevPa
   const int64_t nwork = w.counters_i32[5];
   for (int64_t it = blockIdx.x; it < nwork; it += gridDim.x) {
     const int64_t p = w.overflow_list0[it];
-    const float lat = b.lat[p], lon = b.lon[p];
-    const float r = probe_radius(P, b.acc[p]);
+    const float4 pr = w.probe[p];  // {lat, lon, accuracy} of the column (K1), one line
+    const float lat = pr.x, lon = pr.y;
+    const float r = probe_radius(P, pr.z);
     const float r2 = r * r;
     const float ls = MPD_F * cos_deg(lat);
     const float dlat = r / MPD_F;

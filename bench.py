@@ -17,6 +17,10 @@ oracle's work counters on the same batch (independent of
 the GPU implementation); kernel times from HIP events around each launch on
 the launch stream.  The line's `roofline` object is the dominant kernel's.
 
+`--config 4` measures BASELINE's config 4 the same way instead (state-scale
+highway graph, 100k vehicles x 100 probes, 30 s sampling, sigma 50 m,
+radius 100 m): a secondary line, not the headline.
+
 Prints ONE JSON line (rank 0).  Run:
   python bench.py                      # N=1, defaults
   python -m torch.distributed.run --nproc-per-node N bench.py --gpus N
@@ -36,6 +40,15 @@ METRIC = "GPS points matched/sec (whole node) at 1/2/4/8 MI355X; % segment-ID ag
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 DEFAULT_TRAFFIC = os.path.join(ROOT, "profiles", "pmc_traffic_latest.json")
 
+# config -> (graph, workload); config 2 is the headline line, config 4 a
+# secondary one (BASELINE.json configs[3]: wide radius, long transitions)
+WORKLOAD = {
+    2: ("20x20 km city", "config2-city: %d vehicles x %d GPS points per GPU (%d points), 5 s, sigma 15 m, "
+                         "accuracy 15 m, radius 50 m, uuid-sharded"),
+    4: ("500x500 km highway-heavy state", "config4-state: %d vehicles x %d GPS points per GPU (%d points), 30 s, "
+                                          "sigma 50 m, accuracy 50 m, radius 100 m, uuid-sharded"),
+}
+
 # kernel -> (stage, main tier of the stage?)
 KERNEL_STAGE = {
     "k_columns": "columns", "spatial_order": "candidates", "k_cand_lane": "candidates", "k_candidates": "candidates", "k_links": "links_scan",
@@ -52,7 +65,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--vehicles", type=int, default=10000, help="per GPU")
+    ap.add_argument("--config", type=int, default=2, choices=(2, 4),
+                    help="BASELINE config: 2 = the headline city batch (default), 4 = state-scale high-noise batch")
+    ap.add_argument("--vehicles", type=int, default=0, help="per GPU (0: the config's own count)")
     ap.add_argument("--points", type=int, default=100, help="per vehicle")
     ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (0: min(16, cores))")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -118,10 +133,12 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
-    cfg = synth.CONFIGS[2]
-    graph = synth.cached_graph(2)
+    cfg = synth.CONFIGS[args.config]
+    graph = synth.cached_graph(args.config)
+    meili = dict(cfg.get("meili", {}))
     tr = dict(cfg["traces"])
-    tr["n_vehicles"] = args.vehicles
+    if args.vehicles <= 0:
+        args.vehicles = tr["n_vehicles"]
     tr["points_per_vehicle"] = args.points
     t0 = time.time()
     ids = synth.shard_vehicle_ids(args.vehicles, rank, world)
@@ -131,7 +148,7 @@ def main():
     log(rank, "[bench] graph %s, %d vehicles x %d pts = %d points/GPU, generated in %.1fs" %
         (os.path.basename(graph), len(ids), args.points, P, time.time() - t0))
 
-    eng = Engine(graph_path=graph, device=local)
+    eng = Engine(graph_path=graph, device=local, **meili)
     ginfo = eng.graph_info()
     nbins, bin_kph = 16, 10.0
     nseg = ginfo["segments"]
@@ -221,8 +238,8 @@ def main():
     if rank == 0 and not args.no_check:
         from oracle import pyoracle
         torc = time.perf_counter()
-        orc = pyoracle.match_batch(pyoracle.Graph(graph), batch, nthreads=min(16, os.cpu_count() or 1),
-                                   keep_stages=True)
+        orc = pyoracle.match_batch(pyoracle.Graph(graph), batch, p=pyoracle.params(**meili),
+                                   nthreads=min(16, os.cpu_count() or 1), keep_stages=True)
         log(rank, "[bench] oracle pass over %d points: %.1fs" % (P, time.perf_counter() - torc))
         nt = len(res.traces)
         seq_eq = 0
@@ -257,7 +274,8 @@ def main():
         # few (spill stats); attribute the stage's bytes to the main kernel
         achieved = b / (kern_avg[dom] * 1e-3) / 1e9 if b else None
         traffic = None
-        tj = load_traffic(args.traffic_json)
+        # the committed PMC summary is config 2's; other configs need their own
+        tj = load_traffic(args.traffic_json) if (args.config == 2 or args.traffic_json != DEFAULT_TRAFFIC) else None
         if tj and dom in tj.get("kernels", {}):
             traffic = tj["kernels"][dom].get("hbm_bytes_per_launch")
         roof = {"bound": "hbm", "kernel": dom, "stage": st, "achieved": achieved, "peak": HBM_PEAK_GBS,
@@ -275,21 +293,22 @@ def main():
             nsamp = min(len(ids), 2000)  # 200k points: a bounded sample of the same workload
             sb = synth.slice_batch(batch, 0, nsamp)
             ps = int(sb["trace_off"][-1])
-            pyoracle.match_batch(g, synth.slice_batch(batch, 0, 50), nthreads=threads)  # warm
+            op = pyoracle.params(**meili)
+            pyoracle.match_batch(g, synth.slice_batch(batch, 0, 50), p=op, nthreads=threads)  # warm
             reps, best = 0, None
             tcpu = time.perf_counter()
             while reps < 3 or time.perf_counter() - tcpu < 10.0:
                 ts = time.perf_counter()
-                pyoracle.match_batch(g, sb, nthreads=threads)
+                pyoracle.match_batch(g, sb, p=op, nthreads=threads)
                 dt = time.perf_counter() - ts
                 best = dt if best is None else min(best, dt)
                 reps += 1
                 if time.perf_counter() - tcpu > 30.0:
                     break
             cpu = {"value": ps / best, "unit": "points/s", "cores": threads, "kind": "port",
-                   "sample": "%d vehicles x %d pts (%d points) of the same config-2 batch, CPU oracle "
+                   "sample": "%d vehicles x %d pts (%d points) of the same config-%d batch, CPU oracle "
                              "(meili restatement, C -O3), best of %d runs, %d host threads" %
-                             (nsamp, args.points, ps, reps, threads)}
+                             (nsamp, args.points, ps, args.config, reps, threads)}
         except Exception as e:
             cpu = {"error": str(e)}
 
@@ -306,9 +325,9 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (seeded 20x20 km city graph + seeded probe traces; no real tiles exist here)",
-            "config": {"workload": "config2-city: 10k vehicles x 100 GPS points per GPU (1M points), 5 s, "
-                                   "sigma 15 m, accuracy 15 m, radius 50 m, uuid-sharded",
+            "data": "synthetic (seeded %s graph + seeded probe traces; no real tiles exist here)" % WORKLOAD[
+                args.config][0],
+            "config": {"workload": WORKLOAD[args.config][1] % (len(ids), args.points, P),
                        "points_per_gpu": P, "vehicles_per_gpu": len(ids), "graph": ginfo,
                        "batches_in_flight": inflight,
                        "parallelism": "uuid shards x%d, %d batches in flight per GPU (HIP streams), RCCL "

@@ -6,6 +6,7 @@
 #include "engine.h"
 
 #include <algorithm>
+#include <cmath>
 
 #include <cstring>
 
@@ -170,6 +171,27 @@ int engine_clone(const otm_engine* P, otm_engine* C, std::string* err) {
   return OTM_OK;
 }
 
+// Index radius when the config names none: the road distance within which a
+// row holds about INDEX_ROW_NODES nodes, from the graph's mean node density
+// (a street grid holds ~2 rho R^2 nodes within road distance R), capped at
+// the longest bound a transition can ask, max_route_distance_factor x
+// breakage_distance.  The config-2 city (150 m blocks) gets 1.25 km, which
+// covers every config-2 bound (5 x gc <= 952 m); the config-4 state graph
+// (1.2 km blocks, 30 s sampling: bounds to ~5 km) gets the 10 km cap, with
+// rows the same size as the city's.
+static float auto_index_radius(const otm_engine* E) {
+  constexpr double INDEX_ROW_NODES = 140.0;
+  const auto& h = E->host.h;
+  const double lat_mid = 0.5 * (h.bbox[0] + h.bbox[2]) * 3.14159265358979323846 / 180.0;
+  const double h_m = (h.bbox[2] - h.bbox[0]) * 111195.0;
+  const double w_m = (h.bbox[3] - h.bbox[1]) * 111195.0 * std::cos(lat_mid);
+  const double area = std::max(h_m * w_m, 1.0);
+  const double rho = std::max((double)h.n_nodes, 1.0) / area;
+  double r = std::sqrt(INDEX_ROW_NODES / (2.0 * rho));
+  r = std::min(r, (double)E->dp.factor * (double)E->dp.breakage);
+  return (float)(std::ceil(r / 50.0) * 50.0);
+}
+
 // Bounded distance index: part of flattening the graph into HBM, like the
 // tile preprocessing behind valhalla.Configure (py/reporter_service.py:279).
 // Row u = every node within rmax road metres of u, with D and predecessor
@@ -178,6 +200,7 @@ int engine_clone(const otm_engine* P, otm_engine* C, std::string* err) {
 int build_index(otm_engine* E, std::string* err) {
   E->idx = DevIndex{};
   E->idx.rmax = 0.0f;
+  if (E->index_rmax < 0.0f) E->index_rmax = auto_index_radius(E);
   if (!(E->index_rmax > 0.0f)) return OTM_OK;
   const int32_t N = E->g.n_nodes;
   hipStream_t s = E->stream;

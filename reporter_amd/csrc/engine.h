@@ -24,7 +24,7 @@ struct otm_engine {
   // 1250 m answers every transition with gc <= 250 m (bound 5 x gc): probes up to
   // 50 m/s at 5 s sampling; measured on config 2, 1000 m left one column in 1M to
   // the online tiers at a cost of 0.13 ms per batch
-  float index_rmax = 1250.0f;
+  float index_rmax = -1.0f;  // < 0: sized from the graph's node density (auto_index_radius)
   int64_t small_points = 0;  // batches below this many points: natural order, wave-tier candidates
   otm::DevIndex idx{};
   int64_t index_entries = 0;

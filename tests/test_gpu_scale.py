@@ -74,3 +74,8 @@ def test_config4_state_graph(oracle, results_equal):
         res = eng.match(b)
         _check_vs_oracle(oracle, results_equal, graph, b, res, meili)
         assert (res.traces["code"] == 200).mean() > 0.95
+        # the index radius sized from the graph covers config 4's long
+        # transitions (30 s sampling): no column falls to the online tiers
+        assert eng.index_info()["radius_m"] >= 5000.0
+        sp = eng.spill_stats()
+        assert sp["trans_online"] == 0 and sp["route_online"] == 0, sp

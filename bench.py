@@ -19,7 +19,9 @@ the launch stream.  The line's `roofline` object is the dominant kernel's.
 
 `--config 4` measures BASELINE's config 4 the same way instead (state-scale
 highway graph, 100k vehicles x 100 probes, 30 s sampling, sigma 50 m,
-radius 100 m): a secondary line, not the headline.
+radius 100 m), and `--config 3` one GPU's uuid shard of config 3 (100 x 100 km
+metro graph, 125k vehicles x 100 probes = 12.5M points per GPU): secondary
+lines, not the headline.
 
 Prints ONE JSON line (rank 0).  Run:
   python bench.py                      # N=1, defaults
@@ -45,6 +47,8 @@ DEFAULT_TRAFFIC = os.path.join(ROOT, "profiles", "pmc_traffic_latest.json")
 WORKLOAD = {
     2: ("20x20 km city", "config2-city: %d vehicles x %d GPS points per GPU (%d points), 5 s, sigma 15 m, "
                          "accuracy 15 m, radius 50 m, uuid-sharded"),
+    3: ("100x100 km metro", "config3-metro shard: %d vehicles x %d GPS points per GPU (%d points; 1M vehicles over "
+                            "8 GPUs), 5 s, sigma 15 m, accuracy 15 m, radius 50 m, uuid-sharded"),
     4: ("500x500 km highway-heavy state", "config4-state: %d vehicles x %d GPS points per GPU (%d points), 30 s, "
                                           "sigma 50 m, accuracy 50 m, radius 100 m, uuid-sharded"),
 }
@@ -65,8 +69,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", type=int, default=2, choices=(2, 4),
-                    help="BASELINE config: 2 = the headline city batch (default), 4 = state-scale high-noise batch")
+    ap.add_argument("--config", type=int, default=2, choices=(2, 3, 4),
+                    help="BASELINE config: 2 = the headline city batch (default), 3 = one GPU's uuid shard of the "
+                         "metro run (1M vehicles / 8 GPUs), 4 = state-scale high-noise batch")
     ap.add_argument("--vehicles", type=int, default=0, help="per GPU (0: the config's own count)")
     ap.add_argument("--points", type=int, default=100, help="per vehicle")
     ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (0: min(16, cores))")
@@ -138,7 +143,8 @@ def main():
     meili = dict(cfg.get("meili", {}))
     tr = dict(cfg["traces"])
     if args.vehicles <= 0:
-        args.vehicles = tr["n_vehicles"]
+        # config 3 is quoted over 8 GPUs: a rank's batch is one eighth of it
+        args.vehicles = tr["n_vehicles"] // 8 if args.config == 3 else tr["n_vehicles"]
     tr["points_per_vehicle"] = args.points
     t0 = time.time()
     ids = synth.shard_vehicle_ids(args.vehicles, rank, world)

@@ -93,9 +93,26 @@ int engine_init(otm_engine* E, const char* graph_path, int device, std::string* 
   UP(OTMG_SHAPE_CUM, s_cum, float);
   UP(OTMG_SEG_ID, g_id, uint64_t);
   UP(OTMG_SEG_LEN, g_len, float);
-  UP(OTMG_CELL_OFF, cell_off, int64_t);
   UP(OTMG_CELL_ENT, cell_ent, uint32_t);
 #undef UP
+  {
+    // cell offsets as 32-bit words in HBM: a sparse state-scale grid is
+    // ~100M mostly-empty cells, and a probe's row range (2 offsets) then
+    // usually sits in one cache line
+    const size_t nc = (size_t)h.grid_rows * (size_t)h.grid_cols + 1;
+    if ((uint64_t)h.n_cell_entries >= (1ull << 32)) {
+      *err = "graph: more than 2^32 cell entries (32-bit cell offsets)";
+      return OTM_EINVAL;
+    }
+    const int64_t* co = (const int64_t*)E->host.section(OTMG_CELL_OFF);
+    std::vector<uint32_t> c32(nc);
+    for (size_t c = 0; c < nc; ++c) c32[c] = (uint32_t)co[c];
+    void* d = nullptr;
+    HIPCHK(hipMalloc(&d, nc * 4));
+    HIPCHK(hipMemcpy(d, c32.data(), nc * 4, hipMemcpyHostToDevice));
+    E->graph_allocs.push_back(d);
+    g.cell_off = (const uint32_t*)d;
+  }
   {
     // per cell entry: the shape segment's endpoints (lat_a, lon_a, lat_b,
     // lon_b), laid out in cell order so a probe's scan of one grid row is

@@ -40,7 +40,7 @@ struct DevGraph {
   const float *s_lat, *s_lon, *s_cum;
   const uint64_t* g_id;
   const float* g_len;
-  const int64_t* cell_off;
+  const uint32_t* cell_off;  // 32-bit in HBM (engine_init checks the entry count)
   const uint32_t* cell_ent;
   const float4* ent_geo;  // per cell entry: shape segment endpoints (lat_a, lon_a, lat_b, lon_b)
   int32_t n_nodes, n_edges, n_segments, grid_rows, grid_cols;

@@ -86,12 +86,30 @@ def test_city_sample_sigma15(small_graph, oracle, results_equal, batch_path, rad
     assert len(res.segments) > 1000 and len(res.reports) > 50
 
 
+def _auto_index_radius(graph_path, factor=5.0, breakage=2000.0):
+    """engine.cpp:auto_index_radius restated: ~140 nodes per row at the
+    graph's mean node density, capped at factor x breakage, in 50 m steps."""
+    import math
+    import struct
+    with open(graph_path, "rb") as f:
+        hd = f.read(256)
+    n = struct.unpack_from("<i", hd, 16)[0]
+    bb = struct.unpack_from("<4d", hd, 72)  # min_lat, min_lon, max_lat, max_lon
+    lat_mid = 0.5 * (bb[0] + bb[2]) * math.pi / 180.0
+    area = max((bb[2] - bb[0]) * 111195.0 * (bb[3] - bb[1]) * 111195.0 * math.cos(lat_mid), 1.0)
+    r = min(math.sqrt(140.0 / (2.0 * max(n, 1) / area)), factor * breakage)
+    return math.ceil(r / 50.0) * 50.0
+
+
 def test_index_info(small_graph):
     with Engine(graph_path=small_graph) as eng:
         info = eng.index_info()
         n = eng.graph_info()["nodes"]
-        assert info["radius_m"] == 1250.0 and info["incomplete_rows"] == 0
+        assert info["radius_m"] == pytest.approx(_auto_index_radius(small_graph), abs=50.0)
+        assert info["incomplete_rows"] == 0
         assert info["entries"] > 10 * n
+    with Engine(graph_path=small_graph, index_radius_m=1250.0) as eng:
+        assert eng.index_info()["radius_m"] == 1250.0
     with Engine(graph_path=small_graph, index_radius_m=0) as eng:
         assert eng.index_info()["entries"] == 0
 

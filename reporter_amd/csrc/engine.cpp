@@ -269,6 +269,15 @@ int build_index(otm_engine* E, std::string* err) {
   E->index_slots = total;
   E->idx.rmax = E->index_rmax;
   E->idx.row = rows;
+  {
+    IdxRow* erow = nullptr;
+    HIPCHK(hipMalloc(&erow, ((size_t)E->g.n_edges + 1) * sizeof(IdxRow)));
+    E->graph_allocs.push_back(erow);
+    launch_edge_rows(E->g, rows, erow, s);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(s));
+    E->idx.erow = erow;
+  }
   E->idx.slot = (const uint2*)slot;
   E->idx.pred = (const int32_t*)pred;
   return OTM_OK;

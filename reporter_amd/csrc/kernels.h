@@ -76,11 +76,12 @@ struct DevOrder {
 struct IdxRow {
   int64_t off;    // first slot of the row's table
   int32_t cnt;    // entries, -1 incomplete
-  uint32_t mask;  // capacity - 1
+  uint32_t cap;   // table slots (0 for an empty or incomplete row)
 };
 struct DevIndex {
   float rmax;  // 0: no index
   const IdxRow* row;
+  const IdxRow* erow;    // per edge: the row of its end node (one round trip less from a candidate)
   const uint2* slot;     // {node (0xFFFFFFFF empty), D bits}
   const int32_t* pred;   // per slot
 };
@@ -254,6 +255,7 @@ void launch_index_build(const DevGraph& g, float rmax, int32_t* row_cnt, const I
                         int32_t* pred, bool write, hipStream_t s);
 void launch_row_sizes(const int32_t* row_cnt, int64_t* row_sizes, int32_t n, hipStream_t s);
 void launch_row_pack(const int32_t* row_cnt, const int64_t* row_off, IdxRow* rows, int32_t n, hipStream_t s);
+void launch_edge_rows(const DevGraph& g, const IdxRow* rows, IdxRow* erow, hipStream_t s);
 // exclusive scan helpers (in place over n+1 elements: out[n] = total)
 void scan_i64(int64_t* d, int64_t n, void* tmp, size_t tmp_bytes, hipStream_t s);
 // exclusive scans of three per-trace counts (n <= FETCH_SCAN_MAX) in one

@@ -1142,12 +1142,44 @@ __device__ __forceinline__ uint32_t idx_hash(uint32_t v) {
   return v;
 }
 
+// A row's table: OTM_IDX_LOAD_PCT = 0 sizes it to the power of two >= 2 x
+// entries and takes the hash's low bits; otherwise to entries x 100 / pct
+// slots, the hash mapped onto them by a multiply-high (no power-of-two
+// rounding: ~12 B per entry at 67 % instead of ~22 B).
+#ifndef OTM_IDX_LOAD_PCT
+#define OTM_IDX_LOAD_PCT 20
+#endif
+#ifndef OTM_IDX_EROW
+#define OTM_IDX_EROW 1
+#endif
+__host__ __device__ __forceinline__ int64_t idx_row_cap(int32_t c) {
+  if (c <= 0) return 0;
+#if OTM_IDX_LOAD_PCT
+  const int64_t cap = ((int64_t)c * 100 + OTM_IDX_LOAD_PCT - 1) / OTM_IDX_LOAD_PCT;
+  return cap > c ? cap : (int64_t)c + 1;
+#else
+  int64_t cap = 2;
+  while (cap < 2 * (int64_t)c) cap <<= 1;
+  return cap;
+#endif
+}
+__device__ __forceinline__ uint32_t idx_slot0(uint32_t v, const IdxRow& R) {
+#if OTM_IDX_LOAD_PCT
+  return (uint32_t)(((uint64_t)idx_hash(v) * (uint64_t)R.cap) >> 32);
+#else
+  return idx_hash(v) & (R.cap - 1u);
+#endif
+}
+__device__ __forceinline__ uint32_t idx_next(uint32_t h, const IdxRow& R) {
+  return h + 1u == R.cap ? 0u : h + 1u;
+}
+
 // Row lookup: linear probing in u's table.  Returns the slot (D set) when v is
 // in the row, -1 when absent (D(u,v) > rmax), -2 when the row is incomplete.
 __device__ __forceinline__ int64_t idx_find(const DevIndex& X, const IdxRow& R, uint32_t v, float& D) {
   if (R.cnt < 0) return -2;
   if (R.cnt == 0) return -1;
-  uint32_t h = idx_hash(v) & R.mask;
+  uint32_t h = idx_slot0(v, R);
   while (true) {
     const uint2 sl = X.slot[R.off + h];
     if (sl.x == v) {
@@ -1155,7 +1187,7 @@ __device__ __forceinline__ int64_t idx_find(const DevIndex& X, const IdxRow& R, 
       return R.off + h;
     }
     if (sl.x == EMPTY) return -1;
-    h = (h + 1) & R.mask;
+    h = idx_next(h, R);
   }
 }
 
@@ -1187,8 +1219,8 @@ __global__ __launch_bounds__(TB) void k_index_build(DevGraph g, float rmax, int3
       const uint32_t k = lkey[i];
       if (k == EMPTY) continue;
       const unsigned long long lab = llab[i];
-      uint32_t h = idx_hash(k) & R.mask;
-      while (atomicCAS(&slot[R.off + h].x, EMPTY, k) != EMPTY) h = (h + 1) & R.mask;
+      uint32_t h = idx_slot0(k, R);
+      while (atomicCAS(&slot[R.off + h].x, EMPTY, k) != EMPTY) h = idx_next(h, R);
       slot[R.off + h].y = (uint32_t)(lab >> 32);
       pred[R.off + h] = (int32_t)(uint32_t)(lab & 0xFFFFFFFFull);
     }
@@ -1196,18 +1228,10 @@ __global__ __launch_bounds__(TB) void k_index_build(DevGraph g, float rmax, int3
   }
 }
 
-// table capacity of a row: the power of two >= 2 x entries
+// table capacity of a row (idx_row_cap)
 __global__ void k_row_sizes(const int32_t* row_cnt, int64_t* sizes, int32_t n) {
   const int32_t u = blockIdx.x * blockDim.x + threadIdx.x;
-  if (u < n) {
-    const int32_t c = row_cnt[u];
-    int64_t cap = 0;
-    if (c > 0) {
-      cap = 2;
-      while (cap < 2 * (int64_t)c) cap <<= 1;
-    }
-    sizes[u] = cap;
-  }
+  if (u < n) sizes[u] = idx_row_cap(row_cnt[u]);
   if (u == n) sizes[n] = 0;
 }
 
@@ -1215,7 +1239,7 @@ __global__ void k_row_pack(const int32_t* row_cnt, const int64_t* row_off, IdxRo
   const int32_t u = blockIdx.x * blockDim.x + threadIdx.x;
   if (u >= n) return;
   const int64_t cap = row_off[u + 1] - row_off[u];
-  rows[u] = IdxRow{row_off[u], row_cnt[u], (uint32_t)(cap > 0 ? cap - 1 : 0)};
+  rows[u] = IdxRow{row_off[u], row_cnt[u], (uint32_t)cap};
 }
 
 // K4 index tier: one wavefront per column pair, lanes over the Kq x Kp
@@ -1322,7 +1346,7 @@ __global__ __launch_bounds__(TB, 8) void k_trans_index(DevGraph g, DevBatch b, D
         if (!first) continue;
         const IdxRow R = rq[i];
         unsigned long long st = 0, rl = 0;
-        for (int64_t k = lane; k <= (int64_t)R.mask && R.cnt > 0; k += TB) {
+        for (int64_t k = lane; k < (int64_t)R.cap; k += TB) {
           const uint2 sl = X.slot[R.off + k];
           if (sl.x != EMPTY && bitsf(sl.y) <= bound) {
             ++st;
@@ -1430,7 +1454,11 @@ __global__ __launch_bounds__(TB, 8) void k_trans_sub(DevGraph g, DevBatch b, Dev
         sq[sg][k] = g.e_len[e] - o;
 #endif
         if (idx_ok) {
+#if OTM_IDX_EROW
+          const IdxRow R = X.erow[e];
+#else
           const IdxRow R = X.row[g.e_to[e]];
+#endif
           rq[sg][k] = R;
           bad = bad || R.cnt < 0;
         }
@@ -1486,7 +1514,7 @@ __global__ __launch_bounds__(TB, 8) void k_trans_sub(DevGraph g, DevBatch b, Dev
           for (int k = 0; k < i; ++k) first = first && rq[sg][k].off != rq[sg][i].off;
           if (!first) continue;
           const IdxRow R = rq[sg][i];
-          for (int64_t k = sl; k <= (int64_t)R.mask && R.cnt > 0; k += S) {
+          for (int64_t k = sl; k < (int64_t)R.cap; k += S) {
             const uint2 slt = X.slot[R.off + k];
             if (slt.x != EMPTY && bitsf(slt.y) <= bound) {
               ++c_settled;
@@ -1589,7 +1617,7 @@ __global__ __launch_bounds__(256) void k_route_index(DevGraph g, DevBatch b, Dev
     w.route_dist[p] = sd + oj;
     if (w.ctr) {
       unsigned long long st = 0, rl = 0;
-      for (int64_t k = 0; k <= (int64_t)R.mask; ++k) {
+      for (int64_t k = 0; k < (int64_t)R.cap; ++k) {
         const uint2 sl = X.slot[R.off + k];
         if (sl.x != EMPTY && bitsf(sl.y) <= bound) {
           ++st;
@@ -3110,6 +3138,13 @@ void launch_index_build(const DevGraph& g, float rmax, int32_t* row_cnt, const I
 void launch_row_sizes(const int32_t* row_cnt, int64_t* row_sizes, int32_t n, hipStream_t s) {
   hipLaunchKernelGGL(k_row_sizes, dim3(grid_for((int64_t)n + 1, 256, 1 << 30)), dim3(256), 0, s, row_cnt, row_sizes,
                      n);
+}
+__global__ void k_edge_rows(DevGraph g, const IdxRow* rows, IdxRow* erow) {
+  const int32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < g.n_edges) erow[e] = rows[g.e_to[e]];
+}
+void launch_edge_rows(const DevGraph& g, const IdxRow* rows, IdxRow* erow, hipStream_t s) {
+  hipLaunchKernelGGL(k_edge_rows, dim3(grid_for((int64_t)g.n_edges, 256, 1 << 30)), dim3(256), 0, s, g, rows, erow);
 }
 void launch_row_pack(const int32_t* row_cnt, const int64_t* row_off, IdxRow* rows, int32_t n, hipStream_t s) {
   hipLaunchKernelGGL(k_row_pack, dim3(grid_for((int64_t)n, 256, 1 << 30)), dim3(256), 0, s, row_cnt, row_off, rows, n);

@@ -303,7 +303,7 @@ void engine_free(otm_engine* E) {
     b->p = nullptr;
     b->cap = 0;
   }
-  for (auto* b : {&E->h_traces, &E->h_segs, &E->h_reps_dense, &E->h_ways, &E->h_tot, &E->h_in}) {
+  for (auto* b : {&E->h_traces, &E->h_segs, &E->h_reps_dense, &E->h_ways, &E->h_tot, &E->h_in, &E->h_status}) {
     if (b->p) (void)hipHostFree(b->p);
     b->p = nullptr;
     b->cap = 0;
@@ -358,7 +358,7 @@ static int engine_match_once(otm_engine* E, const DevBatch& b, hipStream_t s, st
   ENS(overflow_list, Pn * 4);
   ENS(overflow_list2, Pn * 4);
   ENS(counters_i32, 64);
-  ENS(snap, 192);
+  ENS(snap, 192 + sizeof(BatchStatus));
   ENS(abort_flag, 16);
   if (E->trans_cap == 0) E->trans_cap = (int64_t)Pn * 48 + 4096;
   ENS(o_traces, ((size_t)NT + 1) * sizeof(otm_trace_result));
@@ -407,9 +407,8 @@ static int engine_match_once(otm_engine* E, const DevBatch& b, hipStream_t s, st
   w.counters_i32 = P<int32_t>(E->counters_i32);
   w.ctr = E->counting ? E->ctr : nullptr;
   if (E->counting) HIPCHK(hipMemsetAsync(E->ctr, 0, sizeof(DevCounters), s));
-  HIPCHK(hipMemsetAsync(w.counters_i32, 0, 64, s));  // [5] = candidate spill count
   w.abort = P<int32_t>(E->abort_flag);
-  HIPCHK(hipMemsetAsync(w.abort, 0, 4, s));
+  launch_batch_init(w.counters_i32, w.abort, s);  // [5] = candidate spill count
   Marks mk;
   mk.ev = E->timing ? E->kev : nullptr;
   ENS(ord_tile, Pn * 2);
@@ -430,8 +429,10 @@ static int engine_match_once(otm_engine* E, const DevBatch& b, hipStream_t s, st
     mk.end(KN_ORDER, s);
   }
   launch_candidates(E->g, b, dp, w, s, mk);
-  // spill snapshot A: candidate probes the lane tier handed to the wave tier
-  HIPCHK(hipMemcpyAsync(E->snap.p, w.counters_i32, 64, hipMemcpyDeviceToDevice, s));
+  // spill snapshot A: candidate probes the lane tier handed to the wave tier;
+  // the counters start over for the transition tiers (links, scan and the
+  // capacity check do not touch them)
+  launch_snap(w.counters_i32, P<int32_t>(E->snap), true, s);
   launch_links(b, dp, w, s, mk);
   mk.begin(KN_SCAN_TRANS, s);
   scan_i64(w.trans_off, NP, E->scan_tmp.p, E->scan_tmp.cap, s);
@@ -440,20 +441,19 @@ static int engine_match_once(otm_engine* E, const DevBatch& b, hipStream_t s, st
   w.trans = P<float>(E->trans);
   w.trans_cap = E->trans_cap;
   launch_cap_check(b, w, s);
-  HIPCHK(hipMemsetAsync(w.counters_i32, 0, 64, s));
   if ((rc = ensure_big(E, err))) return rc;
   w.big_key = P<uint32_t>(E->big_key);
   w.big_lab = P<unsigned long long>(E->big_lab);
   w.big_inq = P<uint32_t>(E->big_inq);
   w.big_fr = P<uint32_t>(E->big_fr);
   launch_transitions(E->g, b, dp, w, s, mk);
-  // spill snapshot B: columns per transition tier
-  HIPCHK(hipMemcpyAsync(P<char>(E->snap) + 64, w.counters_i32, 64, hipMemcpyDeviceToDevice, s));
+  // spill snapshot B: columns per transition tier (Viterbi does not touch
+  // the counters; they start over for the route tiers)
+  launch_snap(w.counters_i32, P<int32_t>(E->snap) + 16, true, s);
   launch_viterbi(b, w, s, mk);
-  HIPCHK(hipMemsetAsync(w.counters_i32, 0, 64, s));
   launch_route(E->g, b, dp, w, s, mk);
   // spill snapshot C: steps per route tier
-  HIPCHK(hipMemcpyAsync(P<char>(E->snap) + 128, w.counters_i32, 64, hipMemcpyDeviceToDevice, s));
+  launch_snap(w.counters_i32, P<int32_t>(E->snap) + 32, false, s);
 
   // Segments, way ids and reports in ONE walk per trace, each trace writing
   // into a region sized by an upper bound (DevOut): every matched point adds
@@ -504,12 +504,16 @@ int engine_match(otm_engine* E, const DevBatch& b, hipStream_t s, std::string* e
   for (int attempt = 0;; ++attempt) {
     if ((rc = engine_match_once(E, b, s, err))) return rc;
     // the one synchronisation of a batch: did every capacity hold?
-    int32_t ab = 0, cnt[3] = {0, 0, 0};
-    int64_t ttotal = 0;
-    HIPCHK(hipMemcpyAsync(&ab, E->abort_flag.p, 4, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(&ttotal, P<int64_t>(E->trans_off) + NP, 8, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(cnt, E->counters_i32.p, 12, hipMemcpyDeviceToHost, s));
+    // (gathered on the device, one copy into pinned memory)
+    if ((rc = ensure_pinned(E->h_status, sizeof(BatchStatus), err))) return rc;
+    BatchStatus* dst = (BatchStatus*)(P<char>(E->snap) + 192);
+    launch_status(P<int32_t>(E->abort_flag), P<int64_t>(E->trans_off) + NP, P<int32_t>(E->counters_i32), dst, s);
+    HIPCHK(hipMemcpyAsync(E->h_status.p, dst, sizeof(BatchStatus), hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
+    const BatchStatus st = *(const BatchStatus*)E->h_status.p;
+    const int32_t ab = st.abort;
+    const int64_t ttotal = st.ttotal;
+    const int32_t cnt[3] = {st.cnt[0], st.cnt[1], st.cnt[2]};
     E->last_trans = ttotal;
     if (!ab) break;
     if (attempt == 3) {

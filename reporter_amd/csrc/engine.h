@@ -70,7 +70,7 @@ struct otm_engine {
   int32_t pool_cap = 0;
   // host copies of the last fetched results
   // (pinned: the D2H copies run at PCIe speed without a staging hop)
-  Buf h_traces, h_segs, h_reps_dense, h_ways, h_tot, h_in;
+  Buf h_traces, h_segs, h_reps_dense, h_ways, h_tot, h_in, h_status;
   // timing
   bool timing = false;
   hipEvent_t kev[2 * otm::KN_COUNT] = {};

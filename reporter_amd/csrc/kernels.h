@@ -254,6 +254,15 @@ void launch_compact(int32_t n_traces, const DevOut& o, const int32_t* seg_off, c
 void launch_index_build(const DevGraph& g, float rmax, int32_t* row_cnt, const IdxRow* rows, uint2* slot,
                         int32_t* pred, bool write, hipStream_t s);
 void launch_row_sizes(const int32_t* row_cnt, int64_t* row_sizes, int32_t n, hipStream_t s);
+struct BatchStatus {
+  int32_t abort, pad;
+  int64_t ttotal;
+  int32_t cnt[3], pad2;
+};
+void launch_batch_init(int32_t* counters, int32_t* abort, hipStream_t s);
+void launch_snap(int32_t* counters, int32_t* snap, bool reset, hipStream_t s);
+void launch_status(const int32_t* abort, const int64_t* ttotal, const int32_t* counters, BatchStatus* out,
+                   hipStream_t s);
 void launch_row_pack(const int32_t* row_cnt, const int64_t* row_off, IdxRow* rows, int32_t n, hipStream_t s);
 void launch_edge_rows(const DevGraph& g, const IdxRow* rows, IdxRow* erow, hipStream_t s);
 // exclusive scan helpers (in place over n+1 elements: out[n] = total)

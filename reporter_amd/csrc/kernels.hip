@@ -731,6 +731,35 @@ __global__ __launch_bounds__(256) void k_links(DevBatch b, DevParams P, DevWork 
   w.trans_off[p] = cnt;
 }
 
+// Batch bookkeeping in single-wave kernels rather than memset / memcpy
+// commands: each runtime copy or fill is its own blit dispatch (3.5-8 us
+// each on the stream, ~60 us per batch before).
+__global__ void k_batch_init(int32_t* counters, int32_t* abort) {
+  const int t = threadIdx.x;
+  if (t < 16) counters[t] = 0;
+  if (t == 0) *abort = 0;
+}
+// spill snapshot: copy the 16 tier counters, optionally zeroing them for the
+// next stage's tiers
+__global__ void k_snap(int32_t* counters, int32_t* snap, int reset) {
+  const int t = threadIdx.x;
+  if (t < 16) {
+    snap[t] = counters[t];
+    if (reset) counters[t] = 0;
+  }
+}
+// the batch's status for the host's one synchronisation: abort flag,
+// transition total, path-pool counters
+__global__ void k_status(const int32_t* abort, const int64_t* ttotal, const int32_t* counters, BatchStatus* out) {
+  if (threadIdx.x == 0) {
+    out->abort = *abort;
+    out->ttotal = *ttotal;
+    out->cnt[0] = counters[0];
+    out->cnt[1] = counters[1];
+    out->cnt[2] = counters[2];
+  }
+}
+
 // the transition matrices' total (scan of K3's sizes) against the buffer
 __global__ void k_cap_check(DevBatch b, DevWork w) {
   if (w.trans_off[b.n_points] > w.trans_cap) *w.abort = 1;
@@ -3048,6 +3077,16 @@ void launch_candidates(const DevGraph& g, const DevBatch& b, const DevParams& p,
 void launch_links(const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s, const Marks& mk) {
   TIMED(KN_LINKS, hipLaunchKernelGGL(k_links, dim3(grid_for(b.n_points + 1, 256, 1 << 30)), dim3(256), 0, s, b, p,
                                      w));
+}
+void launch_batch_init(int32_t* counters, int32_t* abort, hipStream_t s) {
+  hipLaunchKernelGGL(k_batch_init, dim3(1), dim3(64), 0, s, counters, abort);
+}
+void launch_snap(int32_t* counters, int32_t* snap, bool reset, hipStream_t s) {
+  hipLaunchKernelGGL(k_snap, dim3(1), dim3(64), 0, s, counters, snap, reset ? 1 : 0);
+}
+void launch_status(const int32_t* abort, const int64_t* ttotal, const int32_t* counters, BatchStatus* out,
+                   hipStream_t s) {
+  hipLaunchKernelGGL(k_status, dim3(1), dim3(64), 0, s, abort, ttotal, counters, out);
 }
 void launch_cap_check(const DevBatch& b, DevWork& w, hipStream_t s) {
   hipLaunchKernelGGL(k_cap_check, dim3(1), dim3(1), 0, s, b, w);

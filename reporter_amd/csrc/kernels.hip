@@ -1887,15 +1887,17 @@ __device__ void viterbi_trace_global(int64_t a, int64_t e, DevWork& w) {
 // runs out of LDS with the previous column's scores broadcast by readlane;
 // the backtrack walks LDS; state / chain_start go out coalesced.  Same
 // recurrence, tie rules and chain breaks as viterbi_trace_global.
-// LDS per trace (~5.5 KB at these sizes) sets how many traces a CU holds
-// (128 points of metadata: 0.218 -> 0.207 ms on config 2 against 256); a
+// LDS per trace (~5 KB at these sizes) and 64 VGPRs give 8 waves per SIMD
+// (128 points of metadata: 0.218 -> 0.207 ms on config 2 against 256; 8
+// waves instead of 7 with a 448-float window and 768 backpointers: 2.20 ->
+// 1.96 ms on a config-3 shard, 0.201 -> 0.198 on config 2); a
 // trace longer than VIT_PTS, whose candidates exceed VIT_BP, or with one
 // column pair's block beyond VIT_TW, takes the global-memory form.
 #ifndef OTM_VIT_TW
-#define OTM_VIT_TW 512
+#define OTM_VIT_TW 448
 #endif
 #ifndef OTM_VIT_BP
-#define OTM_VIT_BP 1024
+#define OTM_VIT_BP 768
 #endif
 #ifndef OTM_VIT_PTS
 #define OTM_VIT_PTS 128
@@ -1905,7 +1907,10 @@ constexpr int VIT_BP = OTM_VIT_BP;   // candidates per trace (backpointers)
 constexpr int VIT_TW = OTM_VIT_TW;   // transition floats per window (>= one column pair's block)
 constexpr int VIT_EW = 256;          // emission floats per window (>= KMAX)
 
-__global__ __launch_bounds__(TB) void k_viterbi(DevBatch b, DevWork w) {
+#ifndef OTM_VIT_WAVES
+#define OTM_VIT_WAVES 8
+#endif
+__global__ __launch_bounds__(TB, OTM_VIT_WAVES) void k_viterbi(DevBatch b, DevWork w) {
   if (*w.abort) return;  // a capacity was exceeded: the host redoes the batch
   __shared__ float sT[VIT_TW];
   __shared__ float sEm[VIT_EW];

@@ -2492,7 +2492,13 @@ struct SegParT {
   int16_t g_first[TR], g_last[TR], g_w0[TR + 1];
   int32_t nt;
 };
-constexpr int SEGP_PTS_S = 128, SEGP_TRAV_S = 256;
+// small plan: 128 states / 160 traversals (~9.5 KB of LDS, 4 waves per SIMD);
+// measured against 256 traversals (13.3 KB, 3 waves): 0.082 -> 0.075 ms on
+// config 2, 1.04 -> 0.88 ms on a config-3 shard; 128-192 are within noise
+#ifndef OTM_SEGP_TRAV_S
+#define OTM_SEGP_TRAV_S 160
+#endif
+constexpr int SEGP_PTS_S = 128, SEGP_TRAV_S = OTM_SEGP_TRAV_S;
 constexpr int SEGP_PTS = 256, SEGP_TRAV = 512;
 
 __device__ __forceinline__ int wave_incl_max(int v, int lane) {

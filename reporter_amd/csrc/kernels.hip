@@ -237,7 +237,13 @@ __global__ __launch_bounds__(256) void k_order_scatter(DevBatch b, DevWork w, co
 // then runs the interpolation filter (a point is a column iff it lies at least
 // interpolation_distance from the last column) out of LDS, recomputing the
 // distance only where the last column is not the immediate predecessor.
-constexpr int COL_PTS = 512;
+// points staged in LDS (longer traces take the serial form): 256 leaves room
+// for 8 waves per SIMD (512: ~4.6), 0.050 -> 0.046 ms on config 2, 0.42 ->
+// 0.37 ms on a config-3 shard
+#ifndef OTM_COL_PTS
+#define OTM_COL_PTS 256
+#endif
+constexpr int COL_PTS = OTM_COL_PTS;
 __global__ __launch_bounds__(TB) void k_columns(DevGraph g, DevBatch b, DevParams P, DevWork w) {
   __shared__ float sLat[COL_PTS], sLon[COL_PTS], sGc[COL_PTS];
   __shared__ int32_t sPrev[COL_PTS];

@@ -7,6 +7,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 
 #include <cstring>
 
@@ -234,16 +235,45 @@ int build_index(otm_engine* E, std::string* err) {
   E->graph_allocs.push_back(row_off);
   HIPCHK(hipMalloc(&rows, ((size_t)N + 1) * sizeof(IdxRow)));
   E->graph_allocs.push_back(rows);
-  launch_index_build(E->g, E->index_rmax, row_cnt, nullptr, nullptr, nullptr, false, s);
-  launch_row_sizes(row_cnt, row_off, N, s);
   size_t tmpb = scan_tmp_bytes(N) + 256;
   void* tmp = nullptr;
   HIPCHK(hipMalloc(&tmp, tmpb));
-  scan_i64(row_off, N, tmp, tmpb, s);
-  launch_row_pack(row_cnt, row_off, rows, N, s);
+  // HBM budget for the slot tables (12 B per slot): half of what is free
+  // after the graph, or OTM_INDEX_BUDGET_MB.  A graph whose rows at this
+  // radius exceed it gets a smaller radius (rows shrink as R^2), counted
+  // again; below 100 m the index is left off and the online tiers answer
+  // everything (same results, slower).
+  size_t budget = 0;
+  if (const char* bm = std::getenv("OTM_INDEX_BUDGET_MB")) {
+    budget = (size_t)std::strtoull(bm, nullptr, 0) << 20;
+  } else {
+    size_t fr = 0, tot = 0;
+    HIPCHK(hipMemGetInfo(&fr, &tot));
+    budget = fr / 2;
+  }
   int64_t total = 0;
-  HIPCHK(hipMemcpyAsync(&total, row_off + N, 8, hipMemcpyDeviceToHost, s));
-  HIPCHK(hipStreamSynchronize(s));
+  for (int attempt = 0;; ++attempt) {
+    launch_index_build(E->g, E->index_rmax, row_cnt, nullptr, nullptr, nullptr, false, s);
+    launch_row_sizes(row_cnt, row_off, N, s);
+    scan_i64(row_off, N, tmp, tmpb, s);
+    launch_row_pack(row_cnt, row_off, rows, N, s);
+    HIPCHK(hipMemcpyAsync(&total, row_off + N, 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    const double need = ((double)total + 1.0) * 12.0;
+    if (need <= (double)budget) break;
+    const float r = (float)(std::floor(E->index_rmax * std::sqrt((double)budget / need) * 0.9 / 50.0) * 50.0);
+    if (attempt == 4 || r < 100.0f) {
+      (void)hipFree(tmp);
+      E->index_rmax = 0.0f;  // index off
+      E->index_entries = 0;
+      E->index_slots = 0;
+      E->index_incomplete_rows = 0;
+      HIPCHK(hipEventDestroy(a));
+      HIPCHK(hipEventDestroy(z));
+      return OTM_OK;
+    }
+    E->index_rmax = r;
+  }
   (void)hipFree(tmp);
   void *slot = nullptr, *pred = nullptr;
   HIPCHK(hipMalloc(&slot, ((size_t)total + 1) * 8));

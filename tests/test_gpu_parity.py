@@ -114,6 +114,24 @@ def test_index_info(small_graph):
         assert eng.index_info()["entries"] == 0
 
 
+@pytest.mark.parametrize("budget_mb,expect", [("2", "shrunk"), ("0", "off")])
+def test_index_hbm_budget(small_graph, oracle, results_equal, batch_path, monkeypatch, budget_mb, expect):
+    """An index whose slot tables exceed the HBM budget is rebuilt at a
+    smaller radius, or left off; results stay identical to the oracle."""
+    with Engine(graph_path=small_graph) as eng:
+        full = eng.index_info()
+    monkeypatch.setenv("OTM_INDEX_BUDGET_MB", budget_mb)
+    with Engine(graph_path=small_graph) as eng:
+        info = eng.index_info()
+    if expect == "shrunk":
+        assert 100.0 <= info["radius_m"] < full["radius_m"]
+        assert 0 < info["entries"] < full["entries"]
+    else:
+        assert info["radius_m"] == 0.0 and info["entries"] == 0
+    b = synth.make_traces(small_graph, 200, 60, interval_s=5.0, noise_sigma_m=15.0, accuracy=15.0, seed=11)
+    _run_both(small_graph, b, oracle, results_equal, stages=False, counters=False)
+
+
 def test_noise_free_traces(small_graph, oracle, results_equal, batch_path):
     b = synth.make_traces(small_graph, 100, 60, interval_s=5.0, noise_sigma_m=0.0, accuracy=0.0, seed=3)
     _run_both(small_graph, b, oracle, results_equal)

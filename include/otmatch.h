@@ -231,7 +231,9 @@ int otm_graph_info(const otm_engine* eng, int64_t* n_nodes, int64_t* n_edges,
                    int64_t* n_segments);
 
 /* The bounded distance index built at engine creation (config
- * "otm":{"index_radius_m": R}, default 1250, 0 = none): for every node, all
+ * "otm":{"index_radius_m": R}, 0 = none; absent: sized from the graph's node
+ * density, ~140 nodes per row, capped at max_route_distance_factor x
+ * breakage_distance, and shrunk to fit half the free HBM): for every node, all
  * nodes within R road metres with their distance and predecessor edge.
  * Transition and route queries whose bound 5 x gc exceeds R, or whose row
  * overflowed the builder, run the online bounded search instead; the results

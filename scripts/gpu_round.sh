@@ -13,4 +13,4 @@ timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 > gpurun_out/bench.js
 # the same bench with one batch in flight: kernel averages without overlap
 # (the bench's roofline times its kernels one batch at a time)
 (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof1 -o run -- python3 $R/bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-check --inflight 1 > $R/gpurun_out/prof1.log 2>&1)
-if [ "${OTM_PMC:-1}" = "1" ]; then bash scripts/pmc.sh gpurun_out/pmc $TAG; fi
+if [ "${OTM_PMC:-1}" = "1" ]; then PMC_STATS_CSV=$R/gpurun_out/prof1/run_kernel_stats.csv bash scripts/pmc.sh gpurun_out/pmc $TAG; fi

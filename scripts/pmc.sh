@@ -19,4 +19,4 @@ pass tcc TCC_HIT_sum TCC_MISS_sum
 pass sq SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS
 pass lds SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE
 cd $R
-python3 scripts/pmc_summary.py $OUT $TAG > $OUT/pmc_traffic_$TAG.json
+python3 scripts/pmc_summary.py $OUT $TAG ${PMC_STATS_CSV:-} > $OUT/pmc_traffic_$TAG.json

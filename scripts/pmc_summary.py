@@ -1,6 +1,11 @@
 #!/usr/bin/env python3
 """Summarise rocprofv3 --pmc CSVs (scripts/pmc.sh) into per-kernel averages.
 
+Usage: pmc_summary.py <pmc_dir> [tag] [kernel_stats.csv]
+With a kernel-trace stats CSV of the same command, each kernel also gets its
+achieved HBM GB/s (PMC bytes / average duration) and fraction of 8 TB/s.
+LDS bank-conflict rate = SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE.
+
 hbm_bytes_per_launch follows MI355X_MICROARCH.md §HBM: FETCH_SIZE and
 WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports half the bytes of a wide
 streaming read, so the read side is doubled (an upper bound for narrower
@@ -16,7 +21,11 @@ from collections import defaultdict
 
 def short(name):
     n = name.replace("otm::(anonymous namespace)::", "").split("(")[0]
-    n = n.replace("void ", "")
+    n = n.replace("void ", "").strip()
+    if n.startswith("k_segments<128"):
+        return "k_segments"  # the small LDS plan (its traversal count is a build knob)
+    if n.startswith("k_segments<256"):
+        return "k_segments_large"
     alias = {"k_trans_lane<32>": "k_trans_lane", "k_transitions<false>": "k_transitions",
              "k_transitions<true>": "k_transitions_big", "k_route_lane<24>": "k_route_lane",
              "k_route<false>": "k_route", "k_route<true>": "k_route_big", "k_segments<true>": "k_segments",
@@ -26,8 +35,17 @@ def short(name):
     return alias.get(n, n)
 
 
+def durations(stats_csv):
+    """Average kernel durations (ns) from a rocprofv3 --stats kernel_stats.csv."""
+    out = {}
+    for r in csv.DictReader(open(stats_csv)):
+        out[short(r["Name"])] = float(r["AverageNs"])
+    return out
+
+
 def main():
     root, tag = sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else "latest"
+    dur = durations(sys.argv[3]) if len(sys.argv) > 3 and os.path.exists(sys.argv[3]) else {}
     vals = defaultdict(lambda: defaultdict(list))
     for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
         per = defaultdict(float)
@@ -46,6 +64,13 @@ def main():
             d["hbm_bytes_per_launch"] = (2.0 * d["FETCH_SIZE"] + d["WRITE_SIZE"]) * 1024.0
         if "TCC_HIT_sum" in d and "TCC_MISS_sum" in d and d["TCC_HIT_sum"] + d["TCC_MISS_sum"] > 0:
             d["l2_hit_rate"] = d["TCC_HIT_sum"] / (d["TCC_HIT_sum"] + d["TCC_MISS_sum"])
+        if d.get("SQ_LDS_IDX_ACTIVE"):
+            # share of LDS-active cycles lost to bank conflicts
+            d["lds_bank_conflict_rate"] = d.get("SQ_LDS_BANK_CONFLICT", 0.0) / d["SQ_LDS_IDX_ACTIVE"]
+        if k in dur and "hbm_bytes_per_launch" in d and dur[k] > 0:
+            d["avg_duration_ns"] = dur[k]
+            d["hbm_GB_per_s"] = d["hbm_bytes_per_launch"] / dur[k]
+            d["hbm_frac_of_8TBps"] = d["hbm_GB_per_s"] / 8000.0
         out["kernels"][k] = d
     print(json.dumps(out, indent=1, sort_keys=True))
 

@@ -321,7 +321,7 @@ void engine_free(otm_engine* E) {
       &E->in_off,        &E->in_lat,       &E->in_lon,         &E->in_time,        &E->in_acc,     &E->in_blob,
       &E->pt_trace,
       &E->is_col,        &E->prevc,        &E->gc,             &E->ncand,          &E->cand_edge,
-      &E->probe,         &E->col_prev,     &E->trans_off,      &E->trans,          &E->bp,         &E->state,
+      &E->probe,         &E->col_prev,     &E->trans_off,      &E->trans,          &E->bp,         &E->state,      &E->chosen,
       &E->chain_start,   &E->route_dist,   &E->path_off,       &E->path_len,       &E->path_pool,  &E->trace_err,
       &E->overflow_list0, &E->overflow_list, &E->overflow_list2, &E->counters_i32, &E->scan_tmp, &E->snap,   &E->big_key,
       &E->big_lab,       &E->big_inq,      &E->big_fr,         &E->o_traces,       &E->o_seg_cnt,  &E->o_way_cnt,
@@ -379,6 +379,7 @@ static int engine_match_once(otm_engine* E, const DevBatch& b, hipStream_t s, st
   ENS(trans_off, Pn * 8);
   ENS(bp, Pn * KMAX);
   ENS(state, Pn * 4);
+  ENS(chosen, Pn * 8);
   ENS(chain_start, Pn);
   ENS(route_dist, Pn * 4);
   ENS(path_off, Pn * 4);
@@ -423,6 +424,7 @@ static int engine_match_once(otm_engine* E, const DevBatch& b, hipStream_t s, st
   w.trans_off = P<int64_t>(E->trans_off);
   w.bp = P<uint8_t>(E->bp);
   w.state = P<int32_t>(E->state);
+  w.chosen = P<int2>(E->chosen);
   w.chain_start = P<uint8_t>(E->chain_start);
   w.route_dist = P<float>(E->route_dist);
   w.path_off = P<int32_t>(E->path_off);

@@ -140,6 +140,7 @@ struct DevWork {
   float* trans;          // [total]
   uint8_t* bp;           // [P*KMAX]
   int32_t* state;        // [P]
+  int2* chosen;          // [P] the chosen candidate {edge, offset bits} where state >= 0 (K5)
   uint8_t* chain_start;  // [P]
   float* route_dist;     // [P]
   int32_t* path_off;     // [P]

@@ -1596,9 +1596,9 @@ __global__ __launch_bounds__(256) void k_route_index(DevGraph g, DevBatch b, Dev
     w.path_off[p] = 0;
     if (w.state[p] < 0 || w.chain_start[p]) continue;
     const int32_t q = w.col_prev[p];
-    const int i = w.state[q], j = w.state[p];
-    const int32_t ei = w.cand_edge[CSTRIDE * ((int64_t)q * KMAX + i)], ej = w.cand_edge[CSTRIDE * (p * KMAX + j)];
-    const float oi = w.cand_off[CSTRIDE * ((int64_t)q * KMAX + i)], oj = w.cand_off[CSTRIDE * (p * KMAX + j)];
+    const int2 ci = w.chosen[q], cj = w.chosen[p];
+    const int32_t ei = ci.x, ej = cj.x;
+    const float oi = __int_as_float(ci.y), oj = __int_as_float(cj.y);
     if (ei == ej && oj >= oi) {
       w.route_dist[p] = oj - oi;
       continue;
@@ -1829,6 +1829,8 @@ __device__ void viterbi_trace_global(int64_t a, int64_t e, DevWork& w) {
         int jj = bi;
         while (true) {
           w.state[pp] = jj;
+          w.chosen[pp] = make_int2(w.cand_edge[CSTRIDE * (pp * KMAX + jj)],
+                                   __float_as_int(w.cand_off[CSTRIDE * (pp * KMAX + jj)]));
           if (w.chain_start[pp]) break;
           jj = w.bp[pp * KMAX + jj];
           pp = w.col_prev[pp];
@@ -2145,8 +2147,14 @@ __global__ __launch_bounds__(TB, OTM_VIT_WAVES) void k_viterbi(DevBatch b, DevWo
     if (open) backtrack(last, lastK);
     __syncthreads();
     for (int pl = lane; pl < n; pl += TB) {
-      w.state[a + pl] = sState[pl];
+      const int st = sState[pl];
+      w.state[a + pl] = st;
       w.chain_start[a + pl] = sCs[pl];
+      // the chosen candidate, compact for the route and segment stages
+      if (st >= 0) {
+        const int64_t r = CSTRIDE * ((a + pl) * KMAX + st);
+        w.chosen[a + pl] = make_int2(w.cand_edge[r], __float_as_int(w.cand_off[r]));
+      }
     }
     __syncthreads();
   }
@@ -2534,13 +2542,13 @@ __device__ __forceinline__ StateStep state_step(const DevWork& w, int64_t a, con
   r.last = k == ns - 1 || w.chain_start[a + S.sidx[k + 1]] != 0;
   r.step = !r.cs && k > 0;
   r.lp = r.step ? S.sidx[k - 1] : r.pl;
-  const int sj = w.state[p];
-  r.ej = w.cand_edge[CSTRIDE * (p * KMAX + sj)];
-  r.oj = w.cand_off[CSTRIDE * (p * KMAX + sj)];
+  const int2 cj = w.chosen[p];
+  r.ej = cj.x;
+  r.oj = __int_as_float(cj.y);
   const int64_t q = a + r.lp;
-  const int si = w.state[q];
-  r.ei = w.cand_edge[CSTRIDE * (q * KMAX + si)];
-  r.oi = w.cand_off[CSTRIDE * (q * KMAX + si)];
+  const int2 ci = w.chosen[q];
+  r.ei = ci.x;
+  r.oi = __int_as_float(ci.y);
   r.same = r.step && r.ei == r.ej && r.oj >= r.oi;
   r.plen = 0;
   r.poff = 0;

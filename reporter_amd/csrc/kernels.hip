@@ -388,7 +388,15 @@ constexpr int HCAP = 512;  // edge hash slots (>= 2 * MAX_HITS)
 // (0.39 ms with the wave tier vs 0.40 at 12, 0.45 at 16): a smaller LDS list
 // buys occupancy; the ~1 % of probes with more edges in range spill.
 constexpr int CAND_LANE_CAP = OTM_CAND_LANE_CAP;
-constexpr int CAND_TB = 128;
+#ifndef OTM_CAND_TB
+#define OTM_CAND_TB 128
+#endif
+// min waves per SIMD for the lane tier: 8 caps it at 64 VGPRs (0.276 ->
+// 0.255 ms on config 2, 3.86 -> 3.76 ms on config 4; 6 measured no change)
+#ifndef OTM_CAND_WAVES
+#define OTM_CAND_WAVES 8
+#endif
+constexpr int CAND_TB = OTM_CAND_TB;
 #ifndef OTM_TRANS_PACK
 #define OTM_TRANS_PACK 1
 #endif
@@ -409,7 +417,7 @@ __device__ __forceinline__ void wave_cadd(unsigned long long* c, unsigned long l
 // selection-sorts the first max_candidates by (sqdist, edge).  Probes with
 // more distinct edges in range spill to the wave kernel, which also applies
 // the MAX_HITS spec limit.
-__global__ __launch_bounds__(CAND_TB) void k_cand_lane(DevGraph g, DevBatch b, DevParams P, DevWork w) {
+__global__ __launch_bounds__(CAND_TB, OTM_CAND_WAVES) void k_cand_lane(DevGraph g, DevBatch b, DevParams P, DevWork w) {
   __shared__ uint32_t sE[CAND_LANE_CAP * CAND_TB];  // edge << 4 | shape segment
   __shared__ float sQ[CAND_LANE_CAP * CAND_TB];     // best squared distance
   uint32_t* E = sE + threadIdx.x;
@@ -1581,7 +1589,11 @@ __global__ __launch_bounds__(TB, 8) void k_trans_sub(DevGraph g, DevBatch b, Dev
 
 // K6 index tier: one lane per matched step; the path is read back from the
 // index row of the source node (predecessor edges), one table probe per edge.
-__global__ __launch_bounds__(256) void k_route_index(DevGraph g, DevBatch b, DevParams P, DevWork w) {
+// route / report waves-per-SIMD hints: 4 or 8 measured within noise (kept at 1)
+#ifndef OTM_ROUTE_WAVES
+#define OTM_ROUTE_WAVES 1
+#endif
+__global__ __launch_bounds__(256, OTM_ROUTE_WAVES) void k_route_index(DevGraph g, DevBatch b, DevParams P, DevWork w) {
   if (*w.abort) return;  // a capacity was exceeded: the host redoes the batch
   const DevIndex& X = w.idx;
   unsigned long long c_search = 0, c_settled = 0, c_relaxed = 0, c_edges = 0;
@@ -2820,7 +2832,10 @@ __device__ __forceinline__ bool in_lv(const int64_t* lv, int n, int64_t x) {
   return false;
 }
 
-__global__ __launch_bounds__(256) void k_report(DevBatch b, DevReportCfg rc, DevWork w, DevOut o, int32_t n_seg_total) {
+#ifndef OTM_REPORT_WAVES
+#define OTM_REPORT_WAVES 1
+#endif
+__global__ __launch_bounds__(256, OTM_REPORT_WAVES) void k_report(DevBatch b, DevReportCfg rc, DevWork w, DevOut o, int32_t n_seg_total) {
   if (*w.abort) return;  // a capacity was exceeded: the host redoes the batch
   const int32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= b.n_traces) return;

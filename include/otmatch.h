@@ -99,6 +99,20 @@ int otm_report_batch(otm_engine* eng, int n, const char* const* reqs,
 int otm_match_json(otm_engine* eng, const char* req, size_t len, char** resp,
                    size_t* resp_len);
 
+/* report() of reporter_service.py:110-215 on the GPU (the k_report kernel)
+ * over caller-supplied Match outputs: n requests and their
+ * SegmentMatcher.Match JSON.  The segments are converted to typed records and
+ * the kernel's stats, shape_used and reports are written around the Match
+ * output passed through, as the reference does.  codes[i] / resps[i] as
+ * otm_report_segments; codes[i] = 0 with an explanation in resps[i] where a
+ * Match output does not fit the typed records (a field of another JSON type
+ * than the matcher emits: the host otm_report_segments reproduces Python's
+ * exception for those).  Returns 0 or a negative engine error. */
+int otm_report_segments_device(otm_engine* eng, int n, const char* const* reqs,
+                               const size_t* lens, const char* const* match_jsons,
+                               const size_t* match_lens, char** resps,
+                               size_t* resp_lens, int* codes);
+
 /* report() with a caller-supplied matcher output: runs
  * reporter_service.py:110-215 over `match_json` (what SegmentMatcher.Match
  * returned) for the request `req`.  Lets a host keep any matcher and use the
@@ -163,19 +177,28 @@ typedef struct otm_segment {
 #define OTM_SEG_START_VALID 1u
 #define OTM_SEG_END_VALID 2u
 #define OTM_SEG_INTERNAL 4u
+/* start_time / end_time came from a JSON int literal (segments handed to
+ * otm_report_segments_device; the matcher itself emits floats, and the int -1
+ * of an invalid time is "not VALID") */
+#define OTM_SEG_START_INT 8u
+#define OTM_SEG_END_INT 16u
 
 /* One datastore report (reporter_service.py:160-166). */
 typedef struct otm_report_rec {
   int64_t id;
   int64_t next_id; /* -1: key absent */
   double t0;
-  double t1; /* if (flags & OTM_REP_T1_INT_MINUS1) the JSON value is -1 */
+  double t1; /* the JSON value is an int when (flags & OTM_REP_T1_INT): for
+                the matcher's own segments that is the -1 of a partial next
+                segment (reporter_service.py:160) */
   int32_t length;
   int32_t queue_length;
   uint32_t flags;
   uint32_t pad;
 } otm_report_rec;
-#define OTM_REP_T1_INT_MINUS1 1u
+#define OTM_REP_T1_INT 1u
+#define OTM_REP_T1_INT_MINUS1 OTM_REP_T1_INT /* the name of round 1 */
+#define OTM_REP_T0_INT 2u
 
 /* Per-trace outcome: the stats block (reporter_service.py:201-213),
  * shape_used (:125-127) and where the trace's segments/reports live. */
@@ -197,6 +220,7 @@ typedef struct otm_trace_result {
 #define OTM_TERR_ZERODIV 1         /* "float division by zero" */
 #define OTM_TERR_CAND_OVERFLOW 2   /* > OTM_MAX_HITS edges within radius */
 #define OTM_TERR_SEARCH_OVERFLOW 3 /* bounded search settled too many nodes */
+#define OTM_TERR_ZERODIV_INT 4     /* "division by zero" (int / int in report()) */
 
 /* Host-side result arrays of one batch (owned by the engine until the next
  * call on the same thread's engine, or copy them). */
@@ -227,6 +251,13 @@ int otm_fetch_results(otm_engine* eng, otm_results* out);
  * memory (e.g. a torch tensor) so the host can reduce it across GPUs with
  * RCCL.  Pass NULL to stop accumulating. */
 int otm_hist_bind(otm_engine* eng, void* dev_counts, int nbins, float bin_kph);
+/* The same, with a second channel beside the counts: the sum
+ * of the reports' speeds per segment, u64[n_segments] in units of 1/1000
+ * km/h (fixed point, so sums are exact and independent of the order the
+ * GPU adds them in), also caller-owned device memory.  A binding reaches the
+ * engine's clones at their next batch. */
+int otm_hist_bind_ex(otm_engine* eng, void* dev_counts, int nbins, float bin_kph,
+                     void* dev_speed_sum);
 int otm_graph_info(const otm_engine* eng, int64_t* n_nodes, int64_t* n_edges,
                    int64_t* n_segments);
 
@@ -357,6 +388,9 @@ typedef struct otm_batcher_stats {
   /* otm_batcher_process_raw: messages in, messages the formatter dropped,
    * host time (us) formatting */
   int64_t raw_messages, raw_dropped, us_format;
+  /* requests answered null because the handler failed (HttpClient.POST's
+   * transport failure: the batch is cleared, nothing forwarded) */
+  int64_t null_responses;
 } otm_batcher_stats;
 int otm_batcher_get_stats(const otm_batcher* b, otm_batcher_stats* out);
 /* A key's stored batch (points in order, max_separation); returns its size

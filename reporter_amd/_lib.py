@@ -60,7 +60,7 @@ class Forward(C.Structure):
 
 BATCHER_STATS = ("records", "clean_ops", "close_ops", "requests", "request_points", "match_batches", "forwarded",
                  "null_batch_in_clean", "keys", "stored_batches", "stored_points", "us_enqueue", "us_run",
-                 "us_prepare", "us_match", "us_apply", "raw_messages", "raw_dropped", "us_format")
+                 "us_prepare", "us_match", "us_apply", "raw_messages", "raw_dropped", "us_format", "null_responses")
 
 
 class BatcherStats(C.Structure):
@@ -103,8 +103,9 @@ TRACE_DTYPE = np.dtype([(n, "<i4") for n in (
     "unreported_count", "discontinuities", "invalid_speeds", "unassociated", "successful_length",
     "unreported_length")])
 
-SEG_START_VALID, SEG_END_VALID, SEG_INTERNAL = 1, 2, 4
-REP_T1_INT_MINUS1 = 1
+SEG_START_VALID, SEG_END_VALID, SEG_INTERNAL, SEG_START_INT, SEG_END_INT = 1, 2, 4, 8, 16
+REP_T1_INT, REP_T0_INT = 1, 2
+REP_T1_INT_MINUS1 = REP_T1_INT
 
 _lib = None
 
@@ -129,6 +130,9 @@ def _declare(L):
         "otm_match_device": (C.c_int, [vp, C.POINTER(Batch), vp]),
         "otm_fetch_results": (C.c_int, [vp, C.POINTER(Results)]),
         "otm_hist_bind": (C.c_int, [vp, vp, C.c_int, C.c_float]),
+        "otm_hist_bind_ex": (C.c_int, [vp, vp, C.c_int, C.c_float, vp]),
+        "otm_report_segments_device": (C.c_int, [vp, C.c_int, C.POINTER(C.c_char_p), psz, C.POINTER(C.c_char_p), psz,
+                                                 pp, psz, C.POINTER(C.c_int)]),
         "otm_graph_info": (C.c_int, [vp, C.POINTER(i64), C.POINTER(i64), C.POINTER(i64)]),
         "otm_index_info": (C.c_int, [vp, C.POINTER(C.c_float), C.POINTER(i64), C.POINTER(i32),
                                      C.POINTER(C.c_float)]),

@@ -8,7 +8,8 @@ it forwards downstream (context.forward(key, response), :70-71).
 
 The matcher is the engine (GPU batches of every key that is ready), or any
 /report handler: a callable taking a list of request bodies and returning
-(code, body) pairs -- the HttpClient.POST of Batch.java:63.
+(code, body) pairs -- the HttpClient.POST of Batch.java:63 -- or None when the
+call failed as a whole (every request then gets HttpClient's null response).
 """
 import ctypes as C
 
@@ -52,6 +53,8 @@ class Batcher(object):
     def _call(self, ctx, n, reqs, lens, resps, resp_lens, codes):
         bodies = [C.string_at(reqs[i], lens[i]) for i in range(n)]
         out = self._handler(bodies)
+        if out is None:
+            return 1  # the whole call failed (a transport failure: null responses)
         for i, (code, body) in enumerate(out):
             b = body.encode("utf-8") if isinstance(body, str) else body
             resps[i] = _lib.malloc_bytes(b)

@@ -43,7 +43,26 @@ bool read_file(const char* path, std::string* out) {
   return true;
 }
 
-void fill_device_params(otm_engine* E) {
+// The level sets of make_thread_locals (py/reporter_service.py:55-56) for
+// k_report: Python sets, so duplicates collapse; the device config holds at
+// most 16 distinct levels of each (a level is segment_id & 7, so only 8 can
+// ever match -- more distinct entries are rejected rather than cut).
+bool device_levels(const std::vector<int64_t>& in, int64_t* out, int* n, const char* name, std::string* err) {
+  *n = 0;
+  for (int64_t v : in) {
+    bool dup = false;
+    for (int k = 0; k < *n; ++k) dup = dup || out[k] == v;
+    if (dup) continue;
+    if (*n == 16) {
+      *err = std::string(name) + ": more than 16 distinct levels";
+      return false;
+    }
+    out[(*n)++] = v;
+  }
+  return true;
+}
+
+bool fill_device_params(otm_engine* E, std::string* err) {
   const otm::MatchConfig& m = E->mc;
   E->dp.sigma_z = m.sigma_z;
   E->dp.beta = m.beta;
@@ -65,11 +84,11 @@ void fill_device_params(otm_engine* E) {
   E->small_points = sp ? (int64_t)std::strtoll(sp, nullptr, 0) : 65536;
   const otm::ReportConfig& r = E->rc;
   std::memset(&E->drc, 0, sizeof E->drc);
-  E->drc.n_report = (int)std::min<size_t>(r.report_levels.size(), 16);
-  E->drc.n_transition = (int)std::min<size_t>(r.transition_levels.size(), 16);
-  for (int k = 0; k < E->drc.n_report; ++k) E->drc.report_levels[k] = r.report_levels[(size_t)k];
-  for (int k = 0; k < E->drc.n_transition; ++k) E->drc.transition_levels[k] = r.transition_levels[(size_t)k];
+  if (!device_levels(r.report_levels, E->drc.report_levels, &E->drc.n_report, "REPORT_LEVELS", err)) return false;
+  if (!device_levels(r.transition_levels, E->drc.transition_levels, &E->drc.n_transition, "TRANSITION_LEVELS", err))
+    return false;
   E->drc.threshold_sec = r.threshold_sec;
+  return true;
 }
 
 // One GPU batch over parsed requests: results[k] -> (code, body)
@@ -263,7 +282,10 @@ int otm_engine_create(const char* cfg_path, const int* devices, int ndev, otm_en
     delete E;
     return fail(OTM_ECONFIG, err);
   }
-  fill_device_params(E);
+  if (!fill_device_params(E, &err)) {
+    delete E;
+    return fail(OTM_ECONFIG, err);
+  }
   int rc = otm::engine_init(E, graph.c_str(), devices[0], &err);
   if (rc) {
     otm::engine_free(E);
@@ -372,6 +394,87 @@ int otm_report_segments(otm_engine* E, const char* req, size_t len, const char* 
   return 200;
 }
 
+int otm_report_segments_device(otm_engine* E, int n, const char* const* reqs, const size_t* lens,
+                               const char* const* match_jsons, const size_t* match_lens, char** resps,
+                               size_t* resp_lens, int* codes) {
+  if (!E || n < 0) return fail(OTM_EINVAL, "bad arguments");
+  std::vector<std::string> bodies((size_t)n), matcher((size_t)n);
+  std::vector<int> c((size_t)n, 0);
+  // the typed traces: one point each (the request's last time), their segments
+  std::vector<int64_t> toff(1, 0);
+  std::vector<double> tend;
+  std::vector<int32_t> soff(1, 0);
+  std::vector<otm_segment> segs;
+  std::vector<int> which;
+  for (int k = 0; k < n; ++k) {
+    Value trace;
+    int code = otm::parse_request("/report", std::string_view(reqs[k], lens[k]), &trace, &bodies[(size_t)k]);
+    if (code) {
+      c[(size_t)k] = code;
+      continue;
+    }
+    Value m;
+    std::string perr;
+    if (!otm::json::parse(std::string_view(match_jsons[k], match_lens[k]), &m, &perr)) {
+      c[(size_t)k] = 500;
+      bodies[(size_t)k] = otm::error_body(perr);
+      continue;
+    }
+    std::vector<otm_segment> ts;
+    double et = 0.0;
+    std::string why;
+    if (!otm::typed_segments(trace, m, &ts, &et, &why)) {
+      bodies[(size_t)k] = "not typed: " + why;  // code 0
+      continue;
+    }
+    if (m.kind == Kind::Obj) {
+      Value mode;
+      mode.kind = Kind::Str;
+      mode.s = "auto";
+      m.set("mode", std::move(mode));  // segments['mode'] = 'auto' (reporter_service.py:131)
+    }
+    otm::json::dump(m, &matcher[(size_t)k]);
+    segs.insert(segs.end(), ts.begin(), ts.end());
+    soff.push_back((int32_t)segs.size());
+    tend.push_back(et);
+    toff.push_back((int64_t)tend.size());
+    which.push_back(k);
+  }
+  if (!which.empty()) {
+    const int32_t T = (int32_t)which.size();
+    std::vector<otm_trace_result> tr((size_t)T);
+    std::vector<otm_report_rec> rep(segs.size() + 1);
+    std::string err;
+    int rc;
+    {
+      std::lock_guard<std::mutex> lk(E->mu);
+      (void)hipSetDevice(E->device);
+      rc = otm::engine_report_segments(E, T, toff.data(), tend.data(), soff.data(), segs.data(), tr.data(),
+                                       rep.data(), &err);
+    }
+    if (rc) return fail(rc, err);
+    otm_results r{};
+    r.n_traces = T;
+    r.n_segments = (int32_t)segs.size();
+    r.traces = tr.data();
+    r.segments = segs.data();
+    r.reports = rep.data();
+    for (int32_t t = 0; t < T; ++t) {
+      const int k = which[(size_t)t];
+      std::string out;
+      c[(size_t)k] = otm::write_report_response(r, t, &out, &matcher[(size_t)k]);
+      bodies[(size_t)k] = std::move(out);
+      const int inv = tr[(size_t)t].code == 200 ? tr[(size_t)t].invalid_speeds : 0;
+      for (int q = 0; q < inv; ++q) std::fputs("Speed exceeds 200kph\n", stderr);
+    }
+  }
+  for (int k = 0; k < n; ++k) {
+    codes[k] = c[(size_t)k];
+    resps[k] = dup_out(bodies[(size_t)k], &resp_lens[k]);
+  }
+  return OTM_OK;
+}
+
 int otm_submit(otm_engine* E, const char* req, size_t len, uint64_t tag) {
   if (!E) return fail(OTM_EINVAL, "engine is NULL");
   std::lock_guard<std::mutex> lk(E->qmu);
@@ -460,14 +563,22 @@ int otm_fetch_results(otm_engine* E, otm_results* out) {
   return rc ? fail(rc, err) : OTM_OK;
 }
 
-int otm_hist_bind(otm_engine* E, void* dev_counts, int nbins, float bin_kph) {
+int otm_hist_bind_ex(otm_engine* E, void* dev_counts, int nbins, float bin_kph, void* dev_speed_sum) {
   if (!E) return fail(OTM_EINVAL, "engine is NULL");
+  if (E->parent) return fail(OTM_EINVAL, "bind the histogram on the parent engine (clones share it)");
   if (dev_counts && (nbins < 1 || !(bin_kph > 0.0f))) return fail(OTM_EINVAL, "nbins >= 1 and bin_kph > 0");
-  std::lock_guard<std::mutex> lk(E->mu);
+  if (dev_speed_sum && !dev_counts) return fail(OTM_EINVAL, "a speed-sum channel needs the counts");
+  // a batch in flight on this engine or a clone keeps the binding it started with
+  std::lock_guard<std::mutex> lk(E->hist_mu);
   E->hist = (uint32_t*)dev_counts;
+  E->speed_sum = dev_counts ? (unsigned long long*)dev_speed_sum : nullptr;
   E->nbins = dev_counts ? nbins : 0;
   E->bin_kph = bin_kph;
   return OTM_OK;
+}
+
+int otm_hist_bind(otm_engine* E, void* dev_counts, int nbins, float bin_kph) {
+  return otm_hist_bind_ex(E, dev_counts, nbins, bin_kph, nullptr);
 }
 
 int otm_graph_info(const otm_engine* E, int64_t* n_nodes, int64_t* n_edges, int64_t* n_segments) {

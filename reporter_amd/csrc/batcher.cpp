@@ -372,7 +372,11 @@ void complete(otm_batcher* B, uint32_t k, int trim, int code, char* body, size_t
     japply(ks.batch, trim);
   }
   (void)code;
-  if (ks.wop.kind == OP_PROCESS) {
+  if (ks.wop.kind == OP_PROCESS && body == nullptr) {
+    // a null response (transport failure): nothing forwarded (:70-71), and the
+    // cleared batch is not put back
+    ks.in_store = !ks.batch.pts.empty();
+  } else if (ks.wop.kind == OP_PROCESS) {
     // context.forward(key, response); store.put only if non-empty
     otm_forward f;
     f.key = (char*)std::malloc(ks.key.size() + 1);
@@ -575,8 +579,20 @@ int issue_json(otm_batcher* B, size_t r0, size_t r1) {
   const int64_t t2 = now_us();
   B->st.us_match += t2 - t1;
   if (rc != OTM_OK) {
+    // The handler failed as a whole: HttpClient.POST's transport failure,
+    // which returns null (HttpClient.java:37-39).  Batch.report then fails to
+    // parse the null response and clears the batch (Batch.java:77-81), and
+    // process() forwards nothing (BatchingProcessor.java:70-71).  Every key
+    // of this chunk completes that way; the drain goes on with the next.
     B->err = "matcher callback failed";
-    return rc;
+    B->st.null_responses += n;
+    for (int i = 0; i < n; ++i) std::free(outs[(size_t)i]);
+    par(B, (size_t)n, [&](Sink& sk, size_t a, size_t e) {
+      for (size_t i = a; i < e; ++i) complete(B, B->reqs[r0 + i].key, -2, 0, nullptr, 0, sk);
+    });
+    merge_sinks(B);
+    B->st.us_apply += now_us() - t2;
+    return OTM_OK;
   }
   // a callback must hand back malloc'd bodies (otm_free releases them)
   par(B, (size_t)n, [&](Sink& sk, size_t a, size_t e) {

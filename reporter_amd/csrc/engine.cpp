@@ -178,9 +178,6 @@ int engine_clone(const otm_engine* P, otm_engine* C, std::string* err) {
   C->rc = P->rc;
   C->dp = P->dp;
   C->drc = P->drc;
-  C->hist = P->hist;
-  C->nbins = P->nbins;
-  C->bin_kph = P->bin_kph;
   HIPCHK(hipMalloc((void**)&C->ctr, sizeof(DevCounters)));
   HIPCHK(hipMalloc((void**)&C->ctr_save, sizeof(DevCounters)));
   HIPCHK(hipMemset(C->ctr, 0, sizeof(DevCounters)));
@@ -327,7 +324,7 @@ void engine_free(otm_engine* E) {
       &E->big_lab,       &E->big_inq,      &E->big_fr,         &E->o_traces,       &E->o_seg_cnt,  &E->o_way_cnt,
       &E->o_segments,    &E->o_seg_gidx,   &E->o_way_ids,      &E->o_reports,  &E->o_rep_cnt,  &E->seg_ub,
       &E->f_seg_off,     &E->f_way_off,    &E->f_rep_off,      &E->f_segs,     &E->f_ways,     &E->f_reps,
-      &E->abort_flag,    &E->ord_tile,      &E->ord_cnt,      &E->ord_cursor,     &E->ord_grp,    &E->ord_item};
+      &E->abort_flag,    &E->rs_blob,      &E->ord_tile,      &E->ord_cnt,      &E->ord_cursor,     &E->ord_grp,    &E->ord_item};
   for (auto* b : bufs) {
     if (b->p) (void)hipFree(b->p);
     b->p = nullptr;
@@ -391,14 +388,23 @@ static int engine_match_once(otm_engine* E, const DevBatch& b, hipStream_t s, st
   ENS(counters_i32, 64);
   ENS(snap, 192 + sizeof(BatchStatus));
   ENS(abort_flag, 16);
-  if (E->trans_cap == 0) E->trans_cap = (int64_t)Pn * 48 + 4096;
+  // Capacities of the transition matrices and the path pool: sized from the
+  // batch (kept at the largest seen), so the abort -> regrow -> redo loop of
+  // engine_match is the exception.  OTM_TRANS_CAP / OTM_POOL_CAP pin the
+  // starting capacities instead (tests force the redo path with tiny ones).
+  if (!E->caps_read) {
+    E->caps_read = true;
+    if (const char* v = std::getenv("OTM_TRANS_CAP")) E->trans_cap = std::max<int64_t>(1, std::atoll(v)), E->caps_pinned = true;
+    if (const char* v = std::getenv("OTM_POOL_CAP")) E->pool_cap = (int32_t)std::max(1, std::atoi(v)), E->caps_pinned = true;
+  }
+  if (!E->caps_pinned) {
+    E->trans_cap = std::max<int64_t>(E->trans_cap, (int64_t)Pn * 48 + 4096);
+    E->pool_cap = std::max<int32_t>(E->pool_cap, (int32_t)std::min<size_t>(Pn * 8, (size_t)1 << 30));
+  }
   ENS(o_traces, ((size_t)NT + 1) * sizeof(otm_trace_result));
   ENS(o_seg_cnt, ((size_t)NT + 1) * 4);
   ENS(o_way_cnt, ((size_t)NT + 1) * 4);
   ENS(scan_tmp, scan_tmp_bytes(NP > NT ? NP : NT) + 256);
-  if (E->pool_cap == 0) {
-    E->pool_cap = (int32_t)(Pn * 8 < (1u << 30) ? Pn * 8 : (1u << 30));
-  }
   ENS(path_pool, (size_t)E->pool_cap * 4);
 
   // Small batches (the batcher's rounds) are latency bound: too few probes
@@ -511,9 +517,15 @@ static int engine_match_once(otm_engine* E, const DevBatch& b, hipStream_t s, st
   o.seg_gidx = P<int32_t>(E->o_seg_gidx);
   o.reports = E->o_reports.p;
   o.way_ids = P<int64_t>(E->o_way_ids);
-  o.hist = E->hist;
-  o.nbins = E->nbins;
-  o.bin_kph = E->bin_kph;
+  {
+    // the histogram binding lives on the parent; a clone reads it here
+    otm_engine* H = E->parent ? const_cast<otm_engine*>(E->parent) : E;
+    std::lock_guard<std::mutex> lk(H->hist_mu);
+    o.hist = H->hist;
+    o.speed_sum = H->speed_sum;
+    o.nbins = H->nbins;
+    o.bin_kph = H->bin_kph;
+  }
   launch_seg_bound(b, w, P<int64_t>(E->seg_ub), s, mk);
   mk.begin(KN_SEG_SCAN, s);
   scan_i64(P<int64_t>(E->seg_ub), NP, E->scan_tmp.p, E->scan_tmp.cap, s);
@@ -714,6 +726,78 @@ int engine_fetch(otm_engine* E, otm_results* out, std::string* err) {
   out->segments = (const otm_segment*)E->h_segs.p;
   out->reports = (const otm_report_rec*)E->h_reps_dense.p;
   out->way_ids = (const int64_t*)E->h_ways.p;
+  return OTM_OK;
+}
+
+// report() on the GPU over caller-supplied segments: the k_report kernel
+// alone, with the per-trace segment regions laid out as the matcher's
+// pipeline leaves them (DevOut: trace t's segments start at
+// seg_base[trace_off[t]]).
+int engine_report_segments(otm_engine* E, int32_t T, const int64_t* trace_off, const double* time,
+                           const int32_t* seg_off, const otm_segment* segs, otm_trace_result* traces,
+                           otm_report_rec* reports, std::string* err) {
+  const int64_t NP = trace_off[T];
+  const int32_t NS = seg_off[T];
+  for (int32_t t = 0; t < T; ++t)
+    if (trace_off[t + 1] <= trace_off[t]) {
+      *err = "every trace needs at least one point (its end time)";
+      return OTM_EINVAL;
+    }
+  int rc;
+  // one device blob: trace_off, seg_base (per point), time, segments,
+  // seg_cnt, seg_gidx, trace_err, abort; outputs: traces, reports, rep_cnt
+  const size_t b_off = ((size_t)T + 1) * 8, b_sb = ((size_t)NP + 1) * 8, b_tm = (size_t)NP * 8;
+  const size_t b_seg = ((size_t)NS + 1) * sizeof(otm_segment), b_cnt = ((size_t)T + 1) * 4;
+  const size_t b_gidx = ((size_t)NS + 1) * 4, b_err = b_cnt, b_ab = 16;
+  const size_t b_tr = ((size_t)T + 1) * sizeof(otm_trace_result), b_rep = ((size_t)NS + 1) * sizeof(otm_report_rec);
+  size_t off[12];
+  size_t tot = 0;
+  const size_t sz[11] = {b_off, b_sb, b_tm, b_seg, b_cnt, b_gidx, b_err, b_ab, b_tr, b_rep, b_cnt};
+  for (int k = 0; k < 11; ++k) {
+    off[k] = tot;
+    tot += (sz[k] + 255) & ~(size_t)255;
+  }
+  off[11] = tot;
+  if ((rc = ensure(E->rs_blob, tot, err))) return rc;
+  std::vector<char> h(off[8], 0);
+  std::memcpy(h.data() + off[0], trace_off, b_off);
+  int64_t* sb = (int64_t*)(h.data() + off[1]);
+  int32_t* cnt = (int32_t*)(h.data() + off[4]);
+  for (int32_t t = 0; t < T; ++t) {
+    sb[trace_off[t]] = seg_off[t];
+    cnt[t] = seg_off[t + 1] - seg_off[t];
+  }
+  if (NP) std::memcpy(h.data() + off[2], time, b_tm);
+  if (NS) std::memcpy(h.data() + off[3], segs, (size_t)NS * sizeof(otm_segment));
+  int32_t* gidx = (int32_t*)(h.data() + off[5]);
+  for (int32_t k = 0; k < NS; ++k) gidx[k] = -1;  // no histogram for handed-in segments
+  hipStream_t s = E->stream;
+  char* d = (char*)E->rs_blob.p;
+  HIPCHK(hipMemcpyAsync(d, h.data(), off[8], hipMemcpyHostToDevice, s));
+  DevBatch b{};
+  b.n_traces = T;
+  b.n_points = NP;
+  b.trace_off = (const int64_t*)(d + off[0]);
+  b.time = (const double*)(d + off[2]);
+  DevWork w{};
+  w.trace_err = (int32_t*)(d + off[6]);
+  w.abort = (int32_t*)(d + off[7]);
+  w.ctr = nullptr;
+  DevOut o{};
+  o.traces = d + off[8];
+  o.seg_cnt = (int32_t*)(d + off[4]);
+  o.rep_cnt = (int32_t*)(d + off[10]);
+  o.seg_base = (const int64_t*)(d + off[1]);
+  o.segments = d + off[3];
+  o.seg_gidx = (int32_t*)(d + off[5]);
+  o.reports = d + off[9];
+  o.hist = nullptr;
+  o.speed_sum = nullptr;
+  launch_report(b, E->drc, w, o, s, Marks{});
+  HIPCHK(hipGetLastError());
+  if (T) HIPCHK(hipMemcpyAsync(traces, d + off[8], (size_t)T * sizeof(otm_trace_result), hipMemcpyDeviceToHost, s));
+  if (NS) HIPCHK(hipMemcpyAsync(reports, d + off[9], (size_t)NS * sizeof(otm_report_rec), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
   return OTM_OK;
 }
 

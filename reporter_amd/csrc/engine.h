@@ -50,7 +50,9 @@ struct otm_engine {
   Buf big_key, big_lab, big_inq, big_fr;
   Buf ord_tile, ord_cnt, ord_cursor, ord_grp, ord_item;  // spatial work order
   Buf abort_flag;                                       // capacity overflow of the batch in flight
+  Buf rs_blob;                                          // otm_report_segments_device in/out
   int64_t trans_cap = 0;                                // floats in `trans` (grown on overflow)
+  bool caps_read = false, caps_pinned = false;          // OTM_TRANS_CAP / OTM_POOL_CAP
   // outputs
   Buf o_traces, o_seg_cnt, o_way_cnt, o_rep_cnt, seg_ub, o_segments, o_seg_gidx, o_way_ids, o_reports;
   // dense copies made by engine_fetch
@@ -58,8 +60,11 @@ struct otm_engine {
   otm::DevCounters* ctr = nullptr;
   otm::DevCounters* ctr_save = nullptr;
   bool counting = false;
-  // histogram (caller-owned device memory)
+  // histogram (caller-owned device memory).  Clones read their parent's
+  // binding at each batch (under the parent's hist_mu), so a rebind reaches them.
+  std::mutex hist_mu;
   uint32_t* hist = nullptr;
+  unsigned long long* speed_sum = nullptr;
   int nbins = 0;
   float bin_kph = 5.0f;
   // last batch
@@ -105,6 +110,13 @@ int engine_match_host(otm_engine* E, const otm_batch* in, std::string* err);
 int engine_fetch(otm_engine* E, otm_results* out, std::string* err);
 int engine_debug_fetch(otm_engine* E, int what, void* dst, size_t bytes, size_t* needed, std::string* err);
 int engine_counters(otm_engine* E, otm_work_counters* out);
+// report() on the GPU over caller-supplied typed segments (otm_report_segments_device):
+// per trace t its points' times [trace_off[t], trace_off[t+1]) and segments
+// [seg_off[t], seg_off[t+1]); fills traces[T] and the reports (trace t's at
+// reports + seg_off[t], traces[t].rep_cnt of them)
+int engine_report_segments(otm_engine* E, int32_t T, const int64_t* trace_off, const double* time,
+                           const int32_t* seg_off, const otm_segment* segs, otm_trace_result* traces,
+                           otm_report_rec* reports, std::string* err);
 int engine_spill_stats(otm_engine* E, otm_spill_stats* out);
 
 }  // namespace otm

@@ -183,6 +183,7 @@ struct DevOut {
   int64_t* way_ids;      // []
   void* reports;         // otm_report_rec[]
   uint32_t* hist;        // [n_segments * nbins] or nullptr
+  unsigned long long* speed_sum;  // [n_segments] sum of report speeds, 1/1000 km/h, or nullptr
   int nbins;
   float bin_kph;
 };

@@ -2840,6 +2840,15 @@ __device__ __forceinline__ bool in_lv(const int64_t* lv, int n, int64_t x) {
 #ifndef OTM_REPORT_WAVES
 #define OTM_REPORT_WAVES 1
 #endif
+// report() (py/reporter_service.py:110-215) over one trace's segments, one
+// thread per trace.  Segment times are Python values: a segment without
+// START_VALID / END_VALID carries the int -1 (what the matcher emits), one
+// with it the stored double, an int literal when START_INT / END_INT is set
+// (segments handed in by otm_report_segments_device).  A report's t0 / t1
+// inherit that int-ness for the JSON writer, and a zero duration raises
+// Python's int or float ZeroDivisionError.  The histogram is added in a
+// second pass, only for a trace that ends without an error: the reference
+// posts nothing for a trace whose report() raised.
 __global__ __launch_bounds__(256, OTM_REPORT_WAVES) void k_report(DevBatch b, DevReportCfg rc, DevWork w, DevOut o, int32_t n_seg_total) {
   if (*w.abort) return;  // a capacity was exceeded: the host redoes the batch
   const int32_t t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -2865,6 +2874,10 @@ __global__ __launch_bounds__(256, OTM_REPORT_WAVES) void k_report(DevBatch b, De
   const double end_time = b.time[b.trace_off[t + 1] - 1];
   auto ST = [&](const otm_segment& s) { return (s.flags & OTM_SEG_START_VALID) ? s.start_time : -1.0; };
   auto ET = [&](const otm_segment& s) { return (s.flags & OTM_SEG_END_VALID) ? s.end_time : -1.0; };
+  auto ST_INT = [&](const otm_segment& s) {
+    return !(s.flags & OTM_SEG_START_VALID) || (s.flags & OTM_SEG_START_INT) != 0u;
+  };
+  auto ET_INT = [&](const otm_segment& s) { return !(s.flags & OTM_SEG_END_VALID) || (s.flags & OTM_SEG_END_INT) != 0u; };
   int last_idx = r.seg_cnt - 1;
   while (last_idx >= 0 && end_time - ST(S[last_idx]) < rc.threshold_sec) --last_idx;
   r.shape_used = last_idx >= 0 ? S[last_idx].begin_shape_index : -1;
@@ -2872,7 +2885,7 @@ __global__ __launch_bounds__(256, OTM_REPORT_WAVES) void k_report(DevBatch b, De
   int prior = -1;
   int64_t prior_level = -1;
   int nrep = 0;
-  bool zerodiv = false;
+  int zerodiv = 0;
   for (int idx = 0; idx <= last_idx; ++idx) {
     const otm_segment& s = S[idx];
     const bool internal = (s.flags & OTM_SEG_INTERNAL) != 0;
@@ -2884,9 +2897,12 @@ __global__ __launch_bounds__(256, OTM_REPORT_WAVES) void k_report(DevBatch b, De
         const bool trans = in_lv(rc.transition_levels, rc.n_transition, level);
         const double t0 = ST(ps);
         const double t1 = trans ? ST(s) : ET(ps);
+        const bool t0_int = ST_INT(ps);
+        const bool t1_int = trans ? ST_INT(s) : ET_INT(ps);
         const double den = t1 - t0;
         if (den == 0.0) {
-          zerodiv = true;
+          // int / int raises "division by zero", anything else "float division by zero"
+          zerodiv = t0_int && t1_int ? OTM_TERR_ZERODIV_INT : OTM_TERR_ZERODIV;
           break;
         }
         const double speed = ((double)ps.length / den) * 3.6;
@@ -2896,21 +2912,13 @@ __global__ __launch_bounds__(256, OTM_REPORT_WAVES) void k_report(DevBatch b, De
           rep.next_id = (trans && s.segment_id >= 0) ? s.segment_id : -1;
           rep.t0 = t0;
           rep.t1 = t1;
-          rep.flags = (trans && !(s.flags & OTM_SEG_START_VALID)) ? OTM_REP_T1_INT_MINUS1 : 0u;
+          rep.flags = (t1_int ? OTM_REP_T1_INT : 0u) | (t0_int ? OTM_REP_T0_INT : 0u);
           rep.length = ps.length;
           rep.queue_length = ps.queue_length;
-          rep.pad = 0u;
+          rep.pad = (uint32_t)prior;  // the reported segment, for the histogram pass (cleared there)
           REP[nrep++] = rep;
           r.successful_count++;
           r.successful_length = ps.length;
-          if (o.hist && !(rep.flags & OTM_REP_T1_INT_MINUS1) && speed >= 0.0) {
-            const int32_t gi = o.seg_gidx[r.seg_off + prior];
-            if (gi >= 0) {
-              int bin = (int)(speed / (double)o.bin_kph);
-              bin = bin < 0 ? 0 : (bin >= o.nbins ? o.nbins - 1 : bin);
-              atomicAdd(&o.hist[(size_t)gi * o.nbins + bin], 1u);
-            }
-          }
         } else {
           r.invalid_speeds++;
         }
@@ -2929,12 +2937,31 @@ __global__ __launch_bounds__(256, OTM_REPORT_WAVES) void k_report(DevBatch b, De
   }
   if (zerodiv) {
     r.code = 500;
-    r.error_kind = OTM_TERR_ZERODIV;
+    r.error_kind = zerodiv;
     r.rep_cnt = 0;
     r.shape_used = -1;
     r.successful_count = r.unreported_count = r.discontinuities = r.invalid_speeds = r.unassociated = 0;
     r.successful_length = r.unreported_length = -1;
   } else {
+    // second pass: the speed histogram of the reports the trace returns
+    // (a t1 that is the int -1 of a partial next segment gives no speed)
+    for (int k = 0; k < nrep; ++k) {
+      otm_report_rec& rep = REP[k];
+      const int32_t ps = (int32_t)rep.pad;
+      rep.pad = 0u;
+      if (!o.hist) continue;
+      const double speed = ((double)rep.length / (rep.t1 - rep.t0)) * 3.6;
+      const bool t1_minus1 = (rep.flags & OTM_REP_T1_INT) && rep.t1 == -1.0;
+      const int32_t gi = o.seg_gidx[r.seg_off + ps];
+      if (t1_minus1 || !(speed >= 0.0) || gi < 0) continue;
+      int bin = (int)(speed / (double)o.bin_kph);
+      bin = bin < 0 ? 0 : (bin >= o.nbins ? o.nbins - 1 : bin);
+      atomicAdd(&o.hist[(size_t)gi * o.nbins + bin], 1u);
+      if (o.speed_sum) {
+        // fixed point (1/1000 km/h) so the sums are exact and order-independent
+        atomicAdd(&o.speed_sum[gi], (unsigned long long)(speed * 1000.0 + 0.5));
+      }
+    }
     r.rep_cnt = nrep;
     if (w.ctr) {
       cadd(&w.ctr->segments_out, (unsigned long long)r.seg_cnt);

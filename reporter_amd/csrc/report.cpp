@@ -66,6 +66,7 @@ std::string error_body(const std::string& msg) { return "{\"error\":\"" + msg + 
 const char* trace_error_text(int kind) {
   switch (kind) {
     case OTM_TERR_ZERODIV: return "float division by zero";
+    case OTM_TERR_ZERODIV_INT: return "division by zero";
     case OTM_TERR_CAND_OVERFLOW: return "too many candidate edges within search radius";
     case OTM_TERR_SEARCH_OVERFLOW: return "route search exceeded node limit";
   }
@@ -516,6 +517,96 @@ bool extract_points(const Value& trace, TracePoints* out, std::string* err) {
   return true;
 }
 
+// ------------------------------------------------------------ typed segments
+namespace {
+constexpr double kExactInt = 9007199254740992.0;  // 2^53: ints below it are exact doubles
+bool int_in(const Value* v, int64_t lo, int64_t hi, int64_t* out) {
+  if (!v || v->kind != Kind::Int || v->bigint || v->i < lo || v->i > hi) return false;
+  *out = v->i;
+  return true;
+}
+// a time: int literal (exact) or finite float; *is_int says which
+bool time_of(const Value* v, double* out, bool* is_int) {
+  if (!v) return false;
+  if (v->kind == Kind::Int && !v->bigint && std::fabs((double)v->i) < kExactInt) {
+    *out = (double)v->i;
+    *is_int = true;
+    return true;
+  }
+  if (v->kind == Kind::Float && std::isfinite(v->f)) {
+    *out = v->f;
+    *is_int = false;
+    return true;
+  }
+  return false;
+}
+}  // namespace
+
+bool typed_segments(const Value& trace, const Value& match, std::vector<otm_segment>* out, double* end_time,
+                    std::string* why) {
+  out->clear();
+  const Value* tr = trace.get("trace");
+  bool et_int;
+  if (!tr || tr->kind != Kind::Arr || tr->items.empty() || tr->items.back().kind != Kind::Obj ||
+      !time_of(tr->items.back().get("time"), end_time, &et_int)) {
+    *why = "the trace's last time is not a number";
+    return false;
+  }
+  const Value* segs = match.kind == Kind::Obj ? match.get("segments") : nullptr;
+  if (!segs || segs->kind != Kind::Arr) {
+    *why = "Match output has no segments array";
+    return false;
+  }
+  for (size_t k = 0; k < segs->items.size(); ++k) {
+    const Value& sv = segs->items[k];
+    otm_segment s;
+    std::memset(&s, 0, sizeof s);
+    const std::string at = "segment " + std::to_string(k) + ": ";
+    if (sv.kind != Kind::Obj) {
+      *why = at + "not an object";
+      return false;
+    }
+    const Value* id = sv.get("segment_id");
+    if (!id || id->kind == Kind::Null) {
+      s.segment_id = -1;
+    } else if (!int_in(id, 0, INT64_MAX, &s.segment_id)) {
+      *why = at + "segment_id is not a non-negative int";
+      return false;
+    }
+    bool si, ei;
+    if (!time_of(sv.get("start_time"), &s.start_time, &si) || !time_of(sv.get("end_time"), &s.end_time, &ei)) {
+      *why = at + "start_time / end_time are not numbers";
+      return false;
+    }
+    s.flags = OTM_SEG_START_VALID | OTM_SEG_END_VALID | (si ? OTM_SEG_START_INT : 0u) | (ei ? OTM_SEG_END_INT : 0u);
+    const Value* in = sv.get("internal");
+    if (in && in->kind != Kind::Bool) {
+      *why = at + "internal is not a bool";
+      return false;
+    }
+    if (in && in->b) s.flags |= OTM_SEG_INTERNAL;
+    int64_t v;
+    if (!int_in(sv.get("length"), INT32_MIN, INT32_MAX, &v)) {
+      *why = at + "length is not an int";
+      return false;
+    }
+    s.length = (int32_t)v;
+    if (!int_in(sv.get("queue_length"), INT32_MIN, INT32_MAX, &v)) {
+      *why = at + "queue_length is not an int";
+      return false;
+    }
+    s.queue_length = (int32_t)v;
+    if (!int_in(sv.get("begin_shape_index"), 0, INT32_MAX, &v)) {
+      *why = at + "begin_shape_index is not a non-negative int";
+      return false;
+    }
+    s.begin_shape_index = (int32_t)v;
+    s.end_shape_index = -1;
+    out->push_back(s);
+  }
+  return true;
+}
+
 // ------------------------------------------------------------ typed writers
 static void put_time(bool valid, double t, std::string* o) {
   if (valid) json::put_float(t, o);
@@ -562,7 +653,7 @@ void write_match_json(const otm_results& r, int32_t t, std::string* o) {
   o->push_back('}');
 }
 
-int write_report_response(const otm_results& r, int32_t t, std::string* o) {
+int write_report_response(const otm_results& r, int32_t t, std::string* o, const std::string* matcher_json) {
   const otm_trace_result& tr = r.traces[t];
   if (tr.code != 200) {
     *o = error_body(trace_error_text(tr.error_kind));
@@ -589,9 +680,15 @@ int write_report_response(const otm_results& r, int32_t t, std::string* o) {
     o->append(",\"shape_used\":");
     json::put_int(tr.shape_used, o);
   }
-  o->append(",\"segment_matcher\":{\"segments\":");
-  write_segments_array(r, tr, o);
-  o->append(",\"mode\":\"auto\"},\"datastore\":{\"mode\":\"auto\"");
+  if (matcher_json) {
+    o->append(",\"segment_matcher\":");
+    o->append(*matcher_json);
+    o->append(",\"datastore\":{\"mode\":\"auto\"");
+  } else {
+    o->append(",\"segment_matcher\":{\"segments\":");
+    write_segments_array(r, tr, o);
+    o->append(",\"mode\":\"auto\"},\"datastore\":{\"mode\":\"auto\"");
+  }
   if (tr.rep_cnt > 0) {
     o->append(",\"reports\":[");
     for (int32_t k = 0; k < tr.rep_cnt; ++k) {
@@ -600,9 +697,10 @@ int write_report_response(const otm_results& r, int32_t t, std::string* o) {
       o->append("{\"id\":");
       json::put_int(p.id, o);
       o->append(",\"t0\":");
-      json::put_float(p.t0, o);
+      if (p.flags & OTM_REP_T0_INT) json::put_int((int64_t)p.t0, o);
+      else json::put_float(p.t0, o);
       o->append(",\"t1\":");
-      if (p.flags & OTM_REP_T1_INT_MINUS1) o->append("-1");
+      if (p.flags & OTM_REP_T1_INT) json::put_int((int64_t)p.t1, o);
       else json::put_float(p.t1, o);
       o->append(",\"length\":");
       json::put_int(p.length, o);

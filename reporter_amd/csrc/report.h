@@ -28,8 +28,16 @@ bool extract_points(const json::Value& trace, TracePoints* out, std::string* err
 
 // Typed writers over one trace of a results set.
 void write_match_json(const otm_results& r, int32_t t, std::string* out);
-// Full /report response for trace t; returns the HTTP code.
-int write_report_response(const otm_results& r, int32_t t, std::string* out);
+// Full /report response for trace t; returns the HTTP code.  matcher_json:
+// the "segment_matcher" value to write verbatim (the Match output passed
+// through, mode added), or null for the typed segments of r.
+int write_report_response(const otm_results& r, int32_t t, std::string* out,
+                          const std::string* matcher_json = nullptr);
+// A Match output (and the request's last time) as typed segment records for
+// k_report: false with *why when a field has a JSON type the matcher never
+// emits (Python's exceptions for those are the host report_dom's).
+bool typed_segments(const json::Value& trace, const json::Value& match, std::vector<otm_segment>* out,
+                    double* end_time, std::string* why);
 const char* trace_error_text(int kind);
 
 std::string error_body(const std::string& msg);

@@ -131,6 +131,22 @@ class Engine(object):
     def report_segments(self, body, match_output):
         return report_segments(body, match_output, self)
 
+    def report_segments_device(self, pairs):
+        """report() on the GPU (k_report) over [(request body, Match output)]
+        -> [(code, body)]; code 0 where a Match output does not fit the typed
+        records (otm_report_segments_device)."""
+        enc = lambda x: x.encode("utf-8") if isinstance(x, str) else x  # noqa: E731
+        rq = [enc(a) for a, _ in pairs]
+        mo = [enc(b) for _, b in pairs]
+        n = len(pairs)
+        outs = (C.c_void_p * n)()
+        olens = (C.c_size_t * n)()
+        codes = (C.c_int * n)()
+        _check(lib().otm_report_segments_device(self.h, n, (C.c_char_p * n)(*rq), (C.c_size_t * n)(*map(len, rq)),
+                                                (C.c_char_p * n)(*mo), (C.c_size_t * n)(*map(len, mo)), outs, olens,
+                                                codes))
+        return [(codes[i], take(outs[i], olens[i]).decode("utf-8")) for i in range(n)]
+
     def submit(self, body, tag):
         b = body.encode("utf-8") if isinstance(body, str) else body
         _check(lib().otm_submit(self.h, b, len(b), tag))
@@ -169,9 +185,13 @@ class Engine(object):
         _check(lib().otm_fetch_results(self.h, C.byref(r)))
         return Results(r)
 
-    def hist_bind(self, tensor, nbins, bin_kph):
+    def hist_bind(self, tensor, nbins, bin_kph, speed_sum=None):
+        """Per-segment speed histogram (u32 counts [n_segments * nbins]) and,
+        optionally, the per-segment speed sums (int64 [n_segments], 1/1000
+        km/h), both caller-owned device tensors (otm_hist_bind_ex)."""
         ptr = None if tensor is None else tensor.data_ptr()
-        _check(lib().otm_hist_bind(self.h, ptr, nbins, bin_kph))
+        sp = None if speed_sum is None or tensor is None else speed_sum.data_ptr()
+        _check(lib().otm_hist_bind_ex(self.h, ptr, nbins, bin_kph, sp))
 
     def graph_info(self):
         a, b, c = C.c_int64(), C.c_int64(), C.c_int64()

@@ -88,6 +88,17 @@ def cached_graph(config, cache_dir=None):
     return path
 
 
+def segment_ids(graph_path):
+    """The graph's OSMLR segment ids (u64[n_segments], section OTMG_SEG_ID of
+    include/otm_graph_format.h), in segment-index order: row i of a
+    histogram is segment_ids(...)[i]."""
+    import struct
+    raw = np.fromfile(graph_path, dtype=np.uint8)
+    hs = struct.calcsize("<8sII4i2iq3d4dQ")
+    o, n = struct.unpack_from("<QQ", raw, hs + 16 * 17)  # OTMG_SEG_ID
+    return np.frombuffer(raw, dtype=np.uint64, count=n // 8, offset=o).copy()
+
+
 def slice_batch(b, t0, t1):
     """Traces [t0, t1) of a batch as a new batch (offsets rebased)."""
     a, e = int(b["trace_off"][t0]), int(b["trace_off"][t1])

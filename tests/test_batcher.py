@@ -171,3 +171,30 @@ def test_threaded_batcher_large_calls(small_graph, oracle):
     nb = run_native(recs, Batcher(handler=lambda bodies: [oracle.handle_request(g, x) for x in bodies], threads=4,
                                   max_pending=50000), chunk=20000)
     compare(bp, nb, recs)
+
+
+@pytest.mark.parametrize("threads", [0, 3])
+def test_handler_failure_is_a_null_response(small_graph, oracle, threads):
+    """A /report handler that fails as a whole (HttpClient.POST's transport
+    failure, HttpClient.java:37-39) answers every request of that call with
+    null: Batch.report clears the batch (Batch.java:77-81) and process()
+    forwards nothing (BatchingProcessor.java:70-71).  The drain goes on with
+    the next calls.  The serial restatement gets None for exactly the requests
+    the failing call carried."""
+    g = oracle.Graph(small_graph)
+    recs = make_stream(small_graph, n_veh=16, n_pts=60, seed=47)
+    calls = {"n": 0}
+    failed = set()
+
+    def handler(bodies):
+        calls["n"] += 1
+        if calls["n"] in (2, 5):
+            failed.update(bodies)
+            return None
+        return [oracle.handle_request(g, x) for x in bodies]
+
+    nb = run_native(recs, Batcher(handler=handler, max_batch=7, threads=threads), chunk=31)
+    assert failed, "the stream never reached a second matcher call"
+    bp = run_python(recs, lambda body: None if body in failed else oracle.handle_request(g, body)[1])
+    st = compare(bp, nb, recs)
+    assert st["null_responses"] == len(failed)

@@ -478,6 +478,19 @@ int otm_synth_traces(const char* graph_path, const otm_synth_trace_params* p,
                      int64_t* trace_off, float* lat, float* lon, double* time,
                      float* accuracy, int32_t* true_edge, float* true_off);
 
+/* Valhalla's tile hierarchy as py/get_tiles.py computes it (:30-172): levels
+ * 0 / 1 / 2 = 4 / 1 / 0.25 degree tiles over the world bbox.  otm_tile_id:
+ * Row(lat) * ncolumns + Col(lon), -1 outside.  otm_tile_file: GetFile
+ * (:82-102), e.g. "2/000/603/124.gph"; returns 0, or the buffer size needed
+ * when cap is too small.  otm_tile_files_bbox: the files the script lists for
+ * a bbox (split at the antimeridian), newline-separated, levels ascending;
+ * *out released with otm_free.  The real-tile flattener
+ * names its inputs with these; the synthetic one its OSMLR tile bits. */
+int64_t otm_tile_id(int level, double lat, double lon);
+int otm_tile_file(int64_t tile_id, int level, const char* suffix, char* out, size_t cap);
+int otm_tile_files_bbox(double minx, double miny, double maxx, double maxy, const char* suffix,
+                        char** out, size_t* out_len);
+
 /* Kafka's default key partitioner (murmur2, seed 0x9747b28c) -- the shard of
  * a uuid: (murmur2(key) & 0x7fffffff) % n. */
 int32_t otm_murmur2(const char* key, size_t len);

@@ -36,6 +36,12 @@ struct Rng {
 
 int synth_graph_write(const otm_synth_graph_params* p, const char* out_path, std::string* err);
 
+// ------------------------------------------------------------ tile hierarchy (tiles.cpp, py/get_tiles.py:30-102)
+int64_t tile_row(int level, double lat);
+int64_t tile_col(int level, double lon);
+int64_t tile_id(int level, double lat, double lon);  // -1 outside the world bbox
+std::string tile_file(int64_t id, int level, const char* suffix);
+
 // ------------------------------------------------------------ host graph view
 // A read-only view over a mapped .otmg file (sections point into the map).
 struct HostGraph {

@@ -60,16 +60,6 @@ int line_level(int idx, int art, int hwy) {
 
 float level_speed(int level) { return level == 0 ? 90.f : (level == 1 ? 50.f : 30.f); }
 
-// get_tiles.py:51-72 tile math over the world bbox, per level size.
-int64_t tile_id(int level, double lat, double lon) {
-  const double size = level == 0 ? 4.0 : (level == 1 ? 1.0 : 0.25);
-  const int64_t ncols = (int64_t)std::ceil(360.0 / size);
-  int64_t row = (int64_t)((lat + 90.0) / size);
-  double c = (lon + 180.0) / size;
-  int64_t col = c >= 0.0 ? (int64_t)c : (int64_t)(c - 1);
-  return row * ncols + col;
-}
-
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 }  // namespace
@@ -281,7 +271,7 @@ int synth_graph_write(const otm_synth_graph_params* p, const char* out_path, std
   for (size_t g = 0; g < segs.size(); ++g) {
     auto& s = segs[g];
     const auto& e0 = E[s.edges[0]];
-    int64_t t = tile_id(s.level, e0.lat[0], e0.lon[0]);
+    int64_t t = otm::tile_id(s.level, e0.lat[0], e0.lon[0]);  // tiles.cpp (py/get_tiles.py:51-72)
     int64_t idx = tile_count[{s.level, t}]++;
     seg_id[g] = (uint64_t)s.level | ((uint64_t)t << 3) | ((uint64_t)idx << 25);
     float acc = 0.f;

@@ -2,15 +2,17 @@
 
 Each rank takes its uuid shard (murmur2 partitioner), matches it (here with
 the CPU oracle: there is no GPU in this container), bins its datastore
-reports per segment and joins the histogram reduction of
-reporter_amd.flush.  The reduced shards must equal the histogram of the whole
-fleet computed by one process, and the uuid shards must partition the fleet.
+reports per segment (counts and speed sums) and joins the reduction of
+reporter_amd.flush: the same dist.reduce_scatter_tensor that RCCL runs on the
+GPUs, here over gloo.  Rank r must end up with rows [r*S/W, (r+1)*S/W) of the
+whole fleet's histogram computed by one process, the uuid shards must
+partition the fleet, and each rank's datastore flush body must describe
+exactly its rows.
 """
+import json
 import os
-import struct
 
 import numpy as np
-import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
@@ -19,22 +21,14 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 NV, NPTS, NBINS, BIN_KPH = 120, 60, 16, 10.0
 
 
-def seg_ids(graph):
-    raw = np.fromfile(graph, dtype=np.uint8)
-    fmt = "<8sII4i2iq3d4dQ"
-    hs = struct.calcsize(fmt)
-    o, n = struct.unpack_from("<QQ", raw, hs + 16 * 17)  # OTMG_SEG_ID
-    return np.frombuffer(raw, dtype=np.uint64, count=n // 8, offset=o)
-
-
-def _fleet_hist(graph, vehicle_ids, index_of):
+def _fleet_hist(graph, vehicle_ids, index_of, n_rows):
     import sys
     sys.path.insert(0, ROOT)
     from oracle import pyoracle
     from reporter_amd import flush, synth
     b = synth.make_traces(graph, len(vehicle_ids), NPTS, vehicle_ids=vehicle_ids, seed=31)
     r = pyoracle.match_batch(pyoracle.Graph(graph), b, nthreads=2)
-    return flush.histogram_from_reports(r["reports"], index_of, len(seg_ids(graph)), NBINS, BIN_KPH)
+    return flush.histograms_from_reports(r["reports"], index_of, n_rows, NBINS, BIN_KPH)
 
 
 def _worker(rank, world, graph, port, out_dir):
@@ -42,17 +36,23 @@ def _worker(rank, world, graph, port, out_dir):
     sys.path.insert(0, ROOT)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    from reporter_amd import flush, synth
-    ids = seg_ids(graph)
+    from reporter_amd import datastore, flush, synth
+    ids = synth.segment_ids(graph)
     index_of = {int(v): i for i, v in enumerate(ids)}
     mine = synth.shard_vehicle_ids(NV // world, rank, world)
-    h = _fleet_hist(graph, mine, index_of)
     rows = flush.padded_segments(len(ids), world)
-    full = torch.zeros(rows * NBINS, dtype=torch.int32)
-    full[:len(ids) * NBINS] = torch.from_numpy(h.reshape(-1).astype(np.int32))
-    part = flush.reduce_histograms(full)
+    h, s = _fleet_hist(graph, mine, index_of, rows)
+    counts = torch.from_numpy(h.reshape(-1).astype(np.int32))
+    sums = torch.from_numpy(s)
+    part, spart = flush.reduce_histograms(counts, speed_sum=sums)
+    assert part.numel() == rows * NBINS // world and spart.numel() == rows // world
     np.save(os.path.join(out_dir, "part%d.npy" % rank), part.numpy())
+    np.save(os.path.join(out_dir, "sums%d.npy" % rank), spart.numpy())
     np.save(os.path.join(out_dir, "ids%d.npy" % rank), mine)
+    body = datastore.serialize(datastore.flush_records(part.numpy(), spart.numpy(), ids, rank, world, NBINS,
+                                                       BIN_KPH))
+    with open(os.path.join(out_dir, "flush%d.json" % rank), "wb") as f:
+        f.write(body)
     dist.barrier()
     dist.destroy_process_group()
 
@@ -61,16 +61,62 @@ def test_two_rank_histogram_reduction(small_graph, tmp_path):
     world = 2
     port = 29500 + os.getpid() % 1000
     mp.start_processes(_worker, args=(world, small_graph, port, str(tmp_path)), nprocs=world, start_method="spawn")
-    from reporter_amd import flush
+    from reporter_amd import flush, synth
     ids0, ids1 = np.load(tmp_path / "ids0.npy"), np.load(tmp_path / "ids1.npy")
     assert not set(ids0.tolist()) & set(ids1.tolist())
     allv = np.concatenate([ids0, ids1])
-    sids = seg_ids(small_graph)
+    sids = synth.segment_ids(small_graph)
     index_of = {int(v): i for i, v in enumerate(sids)}
-    ref = _fleet_hist(small_graph, allv, index_of).reshape(-1)
     rows = flush.padded_segments(len(sids), world)
-    ref_p = np.zeros(rows * NBINS, np.int64)
-    ref_p[:ref.size] = ref
+    ref_h, ref_s = _fleet_hist(small_graph, allv, index_of, rows)
     got = np.concatenate([np.load(tmp_path / "part0.npy"), np.load(tmp_path / "part1.npy")])
+    got_s = np.concatenate([np.load(tmp_path / "sums0.npy"), np.load(tmp_path / "sums1.npy")])
     assert got.sum() > 0
-    assert np.array_equal(got, ref_p)
+    assert np.array_equal(got, ref_h.reshape(-1))
+    assert np.array_equal(got_s, ref_s)
+    # the flush bodies: each rank names only its own rows, together all of them
+    seen = {}
+    for r in range(world):
+        body = json.loads((tmp_path / ("flush%d.json" % r)).read_bytes())
+        lo, hi = r * rows // world, (r + 1) * rows // world
+        for rec in body["segments"]:
+            row = index_of[rec["id"]]
+            assert lo <= row < hi
+            assert rec["bins"] == ref_h[row].tolist() and rec["count"] == int(ref_h[row].sum())
+            assert rec["speed_sum_kph"] == ref_s[row] / 1000.0
+            seen[row] = True
+    assert len(seen) == int((ref_h.sum(axis=1) > 0).sum())
+
+
+def test_datastore_post_keeps_the_secret_key(tmp_path):
+    """The flush POSTs to DATASTORE_URL as configured, secret_key query
+    parameter included (README.md:196-198); a local HTTP server receives it."""
+    import threading
+    from http.server import BaseHTTPRequestHandler, HTTPServer
+
+    from reporter_amd import datastore
+    got = {}
+
+    class H(BaseHTTPRequestHandler):
+        def do_POST(self):  # noqa: N802
+            n = int(self.headers["Content-Length"])
+            got["path"] = self.path
+            got["type"] = self.headers["Content-type"]
+            got["body"] = self.rfile.read(n)
+            self.send_response(200)
+            self.end_headers()
+
+        def log_message(self, *a):
+            pass
+
+    srv = HTTPServer(("127.0.0.1", 0), H)
+    th = threading.Thread(target=srv.handle_request)
+    th.start()
+    body = datastore.serialize({"mode": "auto", "segments": [{"id": 8, "count": 1, "bins": [1]}]})
+    status = datastore.post(body, url="http://127.0.0.1:%d/store?secret_key=abc" % srv.server_port)
+    th.join()
+    srv.server_close()
+    assert status == 200
+    assert got["path"] == "/store?secret_key=abc"
+    assert got["body"] == body and got["type"].startswith("application/json")
+    assert datastore.post(body, url="") is None or os.environ.get("DATASTORE_URL")

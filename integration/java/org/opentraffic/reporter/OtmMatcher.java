@@ -1,0 +1,145 @@
+package org.opentraffic.reporter;
+
+import java.lang.foreign.*;
+import java.lang.invoke.MethodHandle;
+import java.nio.charset.StandardCharsets;
+import java.util.ArrayList;
+import java.util.List;
+import org.apache.log4j.Logger;
+
+/**
+ * In-process replacement of HttpClient.POST (HttpClient.java:18-45) -> libotmatch.so, through Panama FFM
+ * (JDK 22+, no native glue to build).
+ *
+ * The one-line change in the reference is Batch.java:63:
+ *   String response = HttpClient.POST(url, post_body);
+ * becomes
+ *   String response = OtmMatcher.POST(url, post_body);
+ * `url` is ignored; it stays in the signature so the call-site diff is one identifier.
+ *
+ * Contract (include/otmatch.h, otm_report): same request bytes in, the exact body reporter_service.py
+ * would answer out (200 / 400 / 500 bodies alike), null only on a failure of the call itself -- as
+ * HttpClient.POST returns null on a transport exception (HttpClient.java:37-39).
+ *
+ * The async pair (submit / poll) lets a host that can defer context.forward hand many records to one
+ * GPU batch: results of one uuid come back in submit order.
+ *
+ * Not compiled in this repository (the build image has no JDK); the C side it binds is built and tested
+ * (tests/test_host.py checks every symbol used here is exported).
+ */
+public final class OtmMatcher {
+  private final static Logger logger = Logger.getLogger(OtmMatcher.class);
+  private static final Linker LINKER = Linker.nativeLinker();
+  private static final SymbolLookup LIB =
+      SymbolLookup.libraryLookup(System.getProperty("otm.lib", "libotmatch.so"), Arena.global());
+
+  private static MethodHandle fn(String name, FunctionDescriptor d) {
+    return LINKER.downcallHandle(LIB.find(name).orElseThrow(), d);
+  }
+
+  // int otm_engine_create(const char* cfg, const int* devices, int ndev, otm_engine** out)
+  private static final MethodHandle CREATE = fn("otm_engine_create",
+      FunctionDescriptor.of(ValueLayout.JAVA_INT, ValueLayout.ADDRESS, ValueLayout.ADDRESS, ValueLayout.JAVA_INT,
+                            ValueLayout.ADDRESS));
+  // int otm_report(otm_engine*, const char* req, size_t len, char** resp, size_t* resp_len)
+  private static final MethodHandle REPORT = fn("otm_report",
+      FunctionDescriptor.of(ValueLayout.JAVA_INT, ValueLayout.ADDRESS, ValueLayout.ADDRESS, ValueLayout.JAVA_LONG,
+                            ValueLayout.ADDRESS, ValueLayout.ADDRESS));
+  // int otm_submit(otm_engine*, const char* req, size_t len, uint64_t tag)
+  private static final MethodHandle SUBMIT = fn("otm_submit",
+      FunctionDescriptor.of(ValueLayout.JAVA_INT, ValueLayout.ADDRESS, ValueLayout.ADDRESS, ValueLayout.JAVA_LONG,
+                            ValueLayout.JAVA_LONG));
+  // int otm_poll(otm_engine*, otm_result* out, int max, int timeout_us)
+  private static final MethodHandle POLL = fn("otm_poll",
+      FunctionDescriptor.of(ValueLayout.JAVA_INT, ValueLayout.ADDRESS, ValueLayout.ADDRESS, ValueLayout.JAVA_INT,
+                            ValueLayout.JAVA_INT));
+  // void otm_free(void*)
+  private static final MethodHandle FREE = fn("otm_free", FunctionDescriptor.ofVoid(ValueLayout.ADDRESS));
+  // const char* otm_last_error(const otm_engine*)
+  private static final MethodHandle LAST_ERROR = fn("otm_last_error",
+      FunctionDescriptor.of(ValueLayout.ADDRESS, ValueLayout.ADDRESS));
+
+  // otm_result: {uint64_t tag; int code; (4 bytes padding) char* body; size_t body_len} = 32 bytes
+  private static final MemoryLayout RESULT = MemoryLayout.structLayout(ValueLayout.JAVA_LONG.withName("tag"),
+      ValueLayout.JAVA_INT.withName("code"), MemoryLayout.paddingLayout(4), ValueLayout.ADDRESS.withName("body"),
+      ValueLayout.JAVA_LONG.withName("body_len"));
+
+  private static final MemorySegment ENGINE = create();
+
+  private static MemorySegment create() {
+    // one engine per process; the GPU is the one this process owns (LOCAL_RANK / HIP_VISIBLE_DEVICES).
+    // Replaces valhalla.Configure (py/reporter_service.py:279) + SegmentMatcher() per worker (:52).
+    try (Arena a = Arena.ofConfined()) {
+      MemorySegment cfg = a.allocateFrom(System.getProperty("otm.config", "/etc/otmatch.json"));
+      MemorySegment dev = a.allocateFrom(ValueLayout.JAVA_INT, Integer.getInteger("otm.device", 0));
+      MemorySegment out = a.allocate(ValueLayout.ADDRESS);
+      int rc = (int) CREATE.invokeExact(cfg, dev, 1, out);
+      if (rc != 0) {
+        MemorySegment msg = (MemorySegment) LAST_ERROR.invokeExact(MemorySegment.NULL);
+        throw new IllegalStateException("otm_engine_create: " + msg.reinterpret(4096).getString(0));
+      }
+      return out.get(ValueLayout.ADDRESS, 0);
+    } catch (Throwable t) {
+      throw new ExceptionInInitializerError(t);
+    }
+  }
+
+  private static String takeBody(MemorySegment p, long n) throws Throwable {
+    String v = new String(p.reinterpret(n).toArray(ValueLayout.JAVA_BYTE), StandardCharsets.UTF_8);
+    FREE.invokeExact(p);
+    return v;
+  }
+
+  /** Same contract as HttpClient.POST: the response body, or null on a failure of the call. */
+  public static String POST(String url, String body) {
+    try (Arena a = Arena.ofConfined()) {
+      byte[] b = body.getBytes(StandardCharsets.UTF_8);
+      MemorySegment req = a.allocate(b.length);
+      MemorySegment.copy(b, 0, req, ValueLayout.JAVA_BYTE, 0, b.length);
+      MemorySegment resp = a.allocate(ValueLayout.ADDRESS);
+      MemorySegment len = a.allocate(ValueLayout.JAVA_LONG);
+      int code = (int) REPORT.invokeExact(ENGINE, req, (long) b.length, resp, len);
+      // HttpClient.POST hands back the body whatever the status (the 4xx/5xx bodies are JSON too)
+      return takeBody(resp.get(ValueLayout.ADDRESS, 0), len.get(ValueLayout.JAVA_LONG, 0));
+    } catch (Throwable t) {
+      logger.error("otm_report failed for body " + body);
+      return null;  // as HttpClient.POST on an exception (HttpClient.java:37-39)
+    }
+  }
+
+  /** Queue one /report request; its result comes back from poll() with this tag. */
+  public static boolean submit(String body, long tag) {
+    try (Arena a = Arena.ofConfined()) {
+      byte[] b = body.getBytes(StandardCharsets.UTF_8);
+      MemorySegment req = a.allocate(b.length);
+      MemorySegment.copy(b, 0, req, ValueLayout.JAVA_BYTE, 0, b.length);
+      return (int) SUBMIT.invokeExact(ENGINE, req, (long) b.length, tag) == 0;
+    } catch (Throwable t) {
+      logger.error("otm_submit failed");
+      return false;
+    }
+  }
+
+  /** A finished request: the tag given to submit(), the HTTP status and body. */
+  public record Result(long tag, int code, String body) {}
+
+  /** Up to max finished requests, waiting at most timeoutUs for the first. */
+  public static List<Result> poll(int max, int timeoutUs) {
+    List<Result> out = new ArrayList<>();
+    try (Arena a = Arena.ofConfined()) {
+      MemorySegment res = a.allocate(RESULT, max);
+      int n = (int) POLL.invokeExact(ENGINE, res, max, timeoutUs);
+      for (int i = 0; i < n; ++i) {
+        MemorySegment r = res.asSlice(i * RESULT.byteSize(), RESULT.byteSize());
+        long tag = r.get(ValueLayout.JAVA_LONG, 0);
+        int code = r.get(ValueLayout.JAVA_INT, 8);
+        MemorySegment body = r.get(ValueLayout.ADDRESS, 16);
+        long blen = r.get(ValueLayout.JAVA_LONG, 24);
+        out.add(new Result(tag, code, takeBody(body, blen)));
+      }
+    } catch (Throwable t) {
+      logger.error("otm_poll failed");
+    }
+    return out;
+  }
+}

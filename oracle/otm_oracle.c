@@ -1022,8 +1022,9 @@ int orc_match_batch(const orc_graph* g, const orc_params* p, const orc_report_cf
       out->segments[ns + k] = R->segs[k];
       out->segments[ns + k].way_off += (int32_t)nw;
     }
-    memcpy(out->way_ids + nw, R->ways, sizeof(int64_t) * (size_t)R->nway);
-    memcpy(out->reports + nr, R->reps, sizeof(orc_report_rec) * (size_t)R->nrep);
+    /* (count 0 leaves the source NULL: memcpy's arguments must not be) */
+    if (R->nway) memcpy(out->way_ids + nw, R->ways, sizeof(int64_t) * (size_t)R->nway);
+    if (R->nrep) memcpy(out->reports + nr, R->reps, sizeof(orc_report_rec) * (size_t)R->nrep);
     ns += R->nseg;
     nw += R->nway;
     nr += R->nrep;

@@ -9,7 +9,8 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "build", "libotm_oracle.so")
+# OTM_ORACLE_LIB: another build of the same oracle (the ASan/UBSan one, tests/test_sanitizers.py)
+LIB_PATH = os.environ.get("OTM_ORACLE_LIB") or os.path.join(_HERE, "build", "libotm_oracle.so")
 KMAX = 32
 
 SEGMENT_DTYPE = np.dtype([("segment_id", "<i8"), ("start_time", "<f8"), ("end_time", "<f8"), ("length", "<i4"),

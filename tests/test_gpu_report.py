@@ -264,3 +264,22 @@ def test_one_engine_from_many_threads(small_graph):
     for u in range(12):
         tags = [1000 + i for i in range(u, 48, 12)]
         assert [pos[t] for t in tags] == sorted(pos[t] for t in tags), u
+
+
+def test_valhalla_module_shim(small_graph, oracle, tmp_path):
+    """reporter_amd.valhalla stands in for the binding reporter_service.py
+    imports: Configure (:279), SegmentMatcher() (:52), Match (:112) returns
+    the oracle's Match JSON; a matcher error raises (report() -> 500)."""
+    from reporter_amd import encode_request, valhalla, write_config
+    b = synth.make_traces(small_graph, 6, 40, seed=97)
+    g = oracle.Graph(small_graph)
+    valhalla.Configure(write_config(str(tmp_path / "cfg.json"), small_graph))
+    m = valhalla.SegmentMatcher()
+    for t in range(6):
+        a, e = b["trace_off"][t], b["trace_off"][t + 1]
+        body = encode_request("v%d" % t, b["lat"][a:e], b["lon"][a:e], b["time"][a:e].astype(np.int64),
+                              b["accuracy"][a:e].astype(np.int32))
+        code, want = oracle.match_json(g, body)
+        assert code == 200 and m.Match(body.decode()) == want
+    with pytest.raises(RuntimeError):
+        m.Match('{"uuid":"x","trace":[{"lat":1}]}')

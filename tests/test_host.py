@@ -30,6 +30,22 @@ def test_library_exports_every_declared_symbol():
     assert set(header_functions()) == set(_lib.EXPORTED)
 
 
+def test_integration_sources_bind_exported_symbols():
+    """The Java FFM / JNI sources under integration/ (not compiled here: no
+    JDK) bind only functions include/otmatch.h declares and the library
+    exports."""
+    import glob
+    import re
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    declared = set(header_functions())
+    used = set()
+    for f in glob.glob(os.path.join(root, "integration", "**", "*.*"), recursive=True):
+        used |= set(re.findall(r"\b(otm_[a-z0-9_]+)\s*\(", open(f).read()))
+        used |= set(re.findall(r'"(otm_[a-z0-9_]+)"', open(f).read()))
+    assert {"otm_engine_create", "otm_report", "otm_submit", "otm_poll", "otm_free"} <= used
+    assert used <= declared, used - declared
+
+
 def test_library_is_gfx950_code():
     data = open(_lib.LIB_PATH, "rb").read()
     assert b"hipv4-amdgcn-amd-amdhsa--gfx950" in data  # the offload bundle's code object entry

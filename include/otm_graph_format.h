@@ -29,6 +29,12 @@
  *              meaning shape segment k (points k,k+1) of edge overlaps the
  *              cell's lat/lon box.  Cell (r,c) covers
  *              [lat0 + r*cell, lat0 + (r+1)*cell) x [lon0 + c*cell, ...).
+ *   headings   (version 2) head_out u16[E], head_in u16[E]: the edge's
+ *              bearing in whole degrees [0, 360), clockwise from north, at its
+ *              start (first shape segment) and at its end (last shape
+ *              segment), in the direction of travel -- what Valhalla keeps
+ *              per node and edge for turn costs (the turn at a node is
+ *              head_out(next) - head_in(prev)).
  */
 #ifndef OTM_GRAPH_FORMAT_H
 #define OTM_GRAPH_FORMAT_H
@@ -36,7 +42,7 @@
 #include <stdint.h>
 
 #define OTMG_MAGIC "OTMGRAPH"
-#define OTMG_VERSION 1u
+#define OTMG_VERSION 2u
 
 /* edge flags */
 #define OTM_EDGE_INTERNAL 0x01u  /* intersection-internal / turn channel */
@@ -70,6 +76,8 @@ enum otmg_section {
   OTMG_SEG_N_EDGES,
   OTMG_CELL_OFF,
   OTMG_CELL_ENT,
+  OTMG_EDGE_HEAD_OUT, /* version 2: turn costs */
+  OTMG_EDGE_HEAD_IN,
   OTMG_NUM_SECTIONS
 };
 

@@ -491,6 +491,13 @@ int otm_tile_file(int64_t tile_id, int level, const char* suffix, char* out, siz
 int otm_tile_files_bbox(double minx, double miny, double maxx, double maxy, const char* suffix,
                         char** out, size_t* out_len);
 
+/* The ground truth behind otm_synth_traces (same generator and seeds): the
+ * edges each vehicle drives from its first probe to its last, in order.
+ * path_off[n_vehicles + 1]; at most cap edges are written; returns the total
+ * edge count (cap 0 sizes the call) or a negative error. */
+int64_t otm_synth_true_paths(const char* graph_path, const otm_synth_trace_params* p,
+                             int64_t* path_off, int32_t* path_edges, int64_t cap);
+
 /* Kafka's default key partitioner (murmur2, seed 0x9747b28c) -- the shard of
  * a uuid: (murmur2(key) & 0x7fffffff) % n. */
 int32_t otm_murmur2(const char* key, size_t len);

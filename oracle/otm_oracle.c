@@ -15,7 +15,8 @@
  *                   -> sort (sqdist, edge) -> first max_candidates
  *   S3 emission     sqdist / (2 sigma_z^2)
  *   S4 transitions  bounded Dijkstra per distinct source node, route distance
- *                   r, cost |r - gc| / beta when r <= factor * gc
+ *                   r, cost (turn_cost + |r - gc|) / beta when r <= factor * gc,
+ *                   turn_cost summed over the turns of the shortest route
  *   S5 viterbi      min-sum, ties -> lowest index, dead column -> chain break
  *   S6 route        re-run the winning searches, predecessor edges
  *   S7 segments     traversals -> OSMLR groups, times linear in distance
@@ -72,6 +73,7 @@ struct orc_graph {
   const float* glen;
   const int64_t* cell_off;
   const uint32_t* cell_ent;
+  const uint16_t *ehead_out, *ehead_in;
 };
 
 orc_graph* orc_graph_load(const char* path) {
@@ -112,6 +114,8 @@ orc_graph* orc_graph_load(const char* path) {
   g->glen = SEC(OTMG_SEG_LEN);
   g->cell_off = SEC(OTMG_CELL_OFF);
   g->cell_ent = SEC(OTMG_CELL_ENT);
+  g->ehead_out = SEC(OTMG_EDGE_HEAD_OUT);
+  g->ehead_in = SEC(OTMG_EDGE_HEAD_IN);
 #undef SEC
   return g;
 }
@@ -133,6 +137,7 @@ void orc_params_default(orc_params* p) {
   p->max_search_radius = 100.0f;
   p->gps_accuracy = 5.0f;
   p->max_candidates = ORC_KMAX;
+  p->turn_penalty_factor = 200.0f;
 }
 void orc_report_cfg_default(orc_report_cfg* c) {
   memset(c, 0, sizeof *c);
@@ -162,6 +167,29 @@ float orc_cos_deg(float deg) {
   c = c * x2 + 1.0f;
   return c;
 }
+/* exp(x), 0 <= x <= 4: Taylor series in double, fixed term order (no libm:
+ * the engine computes the same table with the same operations) */
+static double orc_exp_series(double x) {
+  double term = 1.0, sum = 1.0;
+  for (int n = 1; n <= 40; ++n) {
+    term = term * x / (double)n;
+    sum = sum + term;
+  }
+  return sum;
+}
+uint32_t orc_turn_units(float factor, int d) {
+  if (!(factor > 0.0f)) return 0u;
+  const double x = (double)(180 - d) / 45.0;
+  return (uint32_t)floor((double)factor * 64.0 / orc_exp_series(x) + 0.5);
+}
+/* deviation from straight on (0..180 degrees) of the turn from edge a's end
+ * heading into edge b's start heading */
+static int orc_turn_deg(unsigned hin, unsigned hout) {
+  const int d = ((int)hout - (int)hin + 360) % 360;
+  return d <= 180 ? d : 360 - d;
+}
+#define TURN_UNITS_MAX 0xFFFFFFu /* 2^24 - 1: a float holds the sum exactly */
+
 /* equirectangular distance at the mean latitude (meters) */
 static float orc_gc(float la, float lo, float lb, float lob) {
   const float ls = MPD_F * orc_cos_deg((la + lb) * 0.5f);
@@ -418,6 +446,7 @@ typedef struct batch {
   atomic_int next;
   int phase;
   orc_counters* ctr; /* per thread */
+  uint32_t turn_units[181]; /* orc_turn_units per deviation 0..180 */
 } batch;
 
 #define GROW(arr, n, cap, T)                                   \
@@ -498,8 +527,24 @@ static int transitions(batch* B, ws* w, int64_t p, orc_counters* C) {
           r = sd + op[j];
         }
         if (r <= bound) {
+          /* turn cost of the route: the turns from e_i into the
+             path, between its edges and into e_j, in integer 1/64 m units
+             (order-free, exact in a float below 2^24) */
+          uint32_t units = 0;
+          if (!(ep[j] == eq[i] && op[j] >= oq[i])) {
+            int32_t next = ep[j];
+            for (int32_t x = g->efrom[ep[j]]; x != u;) {
+              const int32_t e = w->pred[x];
+              units += B->turn_units[orc_turn_deg(g->ehead_in[e], g->ehead_out[next])];
+              next = e;
+              x = g->efrom[e];
+            }
+            units += B->turn_units[orc_turn_deg(g->ehead_in[eq[i]], g->ehead_out[next])];
+            if (units > TURN_UNITS_MAX) units = TURN_UNITS_MAX;
+          }
+          const float tc = (float)units * 0.015625f;
           const float diff = fabsf(r - gcv);
-          T[i * Kp + j] = diff / B->P->beta;
+          T[i * Kp + j] = (tc + diff) / B->P->beta;
           C->transitions++;
         }
       }
@@ -973,6 +1018,7 @@ int orc_match_batch(const orc_graph* g, const orc_params* p, const orc_report_cf
   B.lon = lon;
   B.time = time;
   B.acc = accuracy;
+  for (int d = 0; d <= 180; ++d) B.turn_units[d] = orc_turn_units(p->turn_penalty_factor, d);
   const size_t PP = (size_t)P + 1;
   B.is_col = (uint8_t*)calloc(PP, 1);
   B.chain_start = (uint8_t*)calloc(PP, 1);

@@ -34,6 +34,7 @@ typedef struct orc_params {
   float sigma_z, beta, max_route_distance_factor, breakage_distance;
   float interpolation_distance, search_radius, max_search_radius, gps_accuracy;
   int max_candidates;
+  float turn_penalty_factor; /* meili auto costing: 200 (0 = no turn costs) */
 } orc_params;
 
 typedef struct orc_report_cfg {
@@ -98,6 +99,9 @@ int64_t orc_graph_count(const orc_graph* g, int what); /* 0 nodes 1 edges 2 segm
 void orc_params_default(orc_params* p);
 void orc_report_cfg_default(orc_report_cfg* c);
 float orc_cos_deg(float deg);
+/* turn-cost units (1/64 m) of a turn that deviates d degrees from straight
+ * on, d = 0..180: round(factor * exp(-(180 - d) / 45) * 64) */
+uint32_t orc_turn_units(float factor, int d);
 
 /* Match a batch (host arrays).  nthreads >= 1 worker threads, one trace per
  * task.  keep_stages != 0 also fills the stage arrays. */

@@ -165,6 +165,7 @@ def _declare(L):
         "otm_synth_graph": (C.c_int, [C.POINTER(SynthGraphParams), C.c_char_p]),
         "otm_synth_traces": (C.c_int, [C.c_char_p, C.POINTER(SynthTraceParams), vp, vp, vp, vp, vp, vp, vp]),
         "otm_murmur2": (i32, [C.c_char_p, sz]),
+        "otm_synth_true_paths": (i64, [C.c_char_p, C.POINTER(SynthTraceParams), vp, vp, i64]),
         "otm_tile_id": (i64, [C.c_int, C.c_double, C.c_double]),
         "otm_tile_file": (C.c_int, [i64, C.c_int, C.c_char_p, C.c_char_p, sz]),
         "otm_tile_files_bbox": (C.c_int, [C.c_double, C.c_double, C.c_double, C.c_double, C.c_char_p, pp, psz]),

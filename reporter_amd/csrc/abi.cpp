@@ -270,8 +270,13 @@ int otm_engine_create(const char* cfg_path, const int* devices, int ndev, otm_en
     getf("search_radius", &E->mc.search_radius);
     getf("max_search_radius", &E->mc.max_search_radius);
     getf("gps_accuracy", &E->mc.gps_accuracy);
+    getf("turn_penalty_factor", &E->mc.turn_penalty_factor);
     const Value* mk = dflt->get("max_candidates");
     if (mk && mk->kind == Kind::Int) E->mc.max_candidates = (int)mk->i;
+  }
+  if (!(E->mc.turn_penalty_factor >= 0.0f && E->mc.turn_penalty_factor <= 10000.0f)) {
+    delete E;
+    return fail(OTM_EINVAL, "turn_penalty_factor must be in [0, 10000]");
   }
   if (E->mc.max_candidates < 1 || E->mc.max_candidates > otm::KMAX) {
     delete E;

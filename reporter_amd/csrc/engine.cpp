@@ -57,6 +57,27 @@ static T* P(otm_engine::Buf& b) {
 
 int build_index(otm_engine* E, std::string* err);
 
+// exp(x), 0 <= x <= 4: Taylor series in double with a fixed term order, so the
+// table is the same wherever it is computed (the CPU oracle's
+// orc_turn_units does the same operations); no libm involved
+static double exp_series(double x) {
+  double term = 1.0, sum = 1.0;
+  for (int n = 1; n <= 40; ++n) {
+    term = term * x / (double)n;
+    sum = sum + term;
+  }
+  return sum;
+}
+// turn cost of a turn deviating d degrees from straight on, in 1/64 m:
+// round(factor * exp(-(180 - d) / 45) * 64) -- meili's turn table
+// turn_penalty_factor * exp(-theta / 45) with theta the angle between the
+// reversed incoming and the outgoing edge (theta = 180 - d)
+uint32_t turn_units(float factor, int d) {
+  if (!(factor > 0.0f)) return 0u;
+  const double x = (double)(180 - d) / 45.0;
+  return (uint32_t)std::floor((double)factor * 64.0 / exp_series(x) + 0.5);
+}
+
 int engine_init(otm_engine* E, const char* graph_path, int device, std::string* err) {
   int rc = load_graph(graph_path, &E->host, err);
   if (rc) return rc;
@@ -95,7 +116,20 @@ int engine_init(otm_engine* E, const char* graph_path, int device, std::string* 
   UP(OTMG_SEG_ID, g_id, uint64_t);
   UP(OTMG_SEG_LEN, g_len, float);
   UP(OTMG_CELL_ENT, cell_ent, uint32_t);
+  UP(OTMG_EDGE_HEAD_OUT, e_head_out, uint16_t);
+  UP(OTMG_EDGE_HEAD_IN, e_head_in, uint16_t);
 #undef UP
+  {
+    // turn units per deviation 0..180 degrees for the configured
+    // turn_penalty_factor, one small device table
+    uint32_t tu[TURN_TABLE];
+    for (int d = 0; d < TURN_TABLE; ++d) tu[d] = turn_units(E->mc.turn_penalty_factor, d);
+    void* d = nullptr;
+    HIPCHK(hipMalloc(&d, sizeof tu));
+    HIPCHK(hipMemcpy(d, tu, sizeof tu, hipMemcpyHostToDevice));
+    E->graph_allocs.push_back(d);
+    E->dp.turn_units = (const uint32_t*)d;
+  }
   {
     // cell offsets as 32-bit words in HBM: a sparse state-scale grid is
     // ~100M mostly-empty cells, and a probe's row range (2 offsets) then
@@ -235,7 +269,7 @@ int build_index(otm_engine* E, std::string* err) {
   size_t tmpb = scan_tmp_bytes(N) + 256;
   void* tmp = nullptr;
   HIPCHK(hipMalloc(&tmp, tmpb));
-  // HBM budget for the slot tables (12 B per slot): half of what is free
+  // HBM budget for the slot tables (20 B per slot: 16 B slot + 4 B predecessor): half of what is free
   // after the graph, or OTM_INDEX_BUDGET_MB.  A graph whose rows at this
   // radius exceed it gets a smaller radius (rows shrink as R^2), counted
   // again; below 100 m the index is left off and the online tiers answer
@@ -250,13 +284,13 @@ int build_index(otm_engine* E, std::string* err) {
   }
   int64_t total = 0;
   for (int attempt = 0;; ++attempt) {
-    launch_index_build(E->g, E->index_rmax, row_cnt, nullptr, nullptr, nullptr, false, s);
+    launch_index_build(E->g, E->dp.turn_units, E->index_rmax, row_cnt, nullptr, nullptr, nullptr, false, s);
     launch_row_sizes(row_cnt, row_off, N, s);
     scan_i64(row_off, N, tmp, tmpb, s);
     launch_row_pack(row_cnt, row_off, rows, N, s);
     HIPCHK(hipMemcpyAsync(&total, row_off + N, 8, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
-    const double need = ((double)total + 1.0) * 12.0;
+    const double need = ((double)total + 1.0) * 20.0;
     if (need <= (double)budget) break;
     const float r = (float)(std::floor(E->index_rmax * std::sqrt((double)budget / need) * 0.9 / 50.0) * 50.0);
     if (attempt == 4 || r < 100.0f) {
@@ -273,12 +307,12 @@ int build_index(otm_engine* E, std::string* err) {
   }
   (void)hipFree(tmp);
   void *slot = nullptr, *pred = nullptr;
-  HIPCHK(hipMalloc(&slot, ((size_t)total + 1) * 8));
+  HIPCHK(hipMalloc(&slot, ((size_t)total + 1) * 16));
   E->graph_allocs.push_back(slot);
-  HIPCHK(hipMemsetAsync(slot, 0xFF, ((size_t)total + 1) * 8, s));
+  HIPCHK(hipMemsetAsync(slot, 0xFF, ((size_t)total + 1) * 16, s));
   HIPCHK(hipMalloc(&pred, ((size_t)total + 1) * 4));
   E->graph_allocs.push_back(pred);
-  launch_index_build(E->g, E->index_rmax, row_cnt, rows, (uint2*)slot, (int32_t*)pred, true, s);
+  launch_index_build(E->g, E->dp.turn_units, E->index_rmax, row_cnt, rows, (uint4*)slot, (int32_t*)pred, true, s);
   HIPCHK(hipEventRecord(z, s));
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventSynchronize(z));
@@ -305,7 +339,7 @@ int build_index(otm_engine* E, std::string* err) {
     HIPCHK(hipStreamSynchronize(s));
     E->idx.erow = erow;
   }
-  E->idx.slot = (const uint2*)slot;
+  E->idx.slot = (const uint4*)slot;
   E->idx.pred = (const int32_t*)pred;
   return OTM_OK;
 }

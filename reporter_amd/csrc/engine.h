@@ -28,7 +28,7 @@ struct otm_engine {
   int64_t small_points = 0;  // batches below this many points: natural order, wave-tier candidates
   otm::DevIndex idx{};
   int64_t index_entries = 0;
-  int64_t index_slots = 0;  // hash-table slots (8 B each + 4 B predecessor)
+  int64_t index_slots = 0;  // hash-table slots (16 B each + 4 B predecessor)
   int32_t index_incomplete_rows = 0;
   float index_build_ms = 0.0f;
   otm::MatchConfig mc;
@@ -98,6 +98,8 @@ struct otm_engine {
 namespace otm {
 
 int engine_init(otm_engine* E, const char* graph_path, int device, std::string* err);
+// turn cost units (1/64 m) of a turn deviating d = 0..180 degrees from straight on
+uint32_t turn_units(float factor, int d);
 // a second batch context on the same GPU: own stream and buffers, the
 // parent's HBM graph, index and configuration
 int engine_clone(const otm_engine* parent, otm_engine* C, std::string* err);

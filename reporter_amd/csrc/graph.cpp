@@ -52,7 +52,8 @@ int load_graph(const char* path, HostGraph* g, std::string* err) {
       4ull * h.n_edges, 4ull * (h.n_edges + 1), 8ull * h.n_edges, 4ull * h.n_edges, 4ull * h.n_edges,
       1ull * h.n_edges, 1ull * h.n_edges, 4ull * h.n_edges, 4ull * h.n_edges, 4ull * h.n_shape,
       4ull * h.n_shape, 4ull * h.n_shape, 8ull * h.n_segments, 4ull * h.n_segments, 4ull * h.n_segments,
-      4ull * h.n_segments, 8ull * ((uint64_t)h.grid_rows * h.grid_cols + 1), 4ull * h.n_cell_entries};
+      4ull * h.n_segments, 8ull * ((uint64_t)h.grid_rows * h.grid_cols + 1), 4ull * h.n_cell_entries,
+      2ull * h.n_edges, 2ull * h.n_edges};
   for (int s = 0; s < OTMG_NUM_SECTIONS; ++s) {
     if (h.sec[s].bytes != expect[s] || h.sec[s].offset + h.sec[s].bytes > (uint64_t)st.st_size ||
         (h.sec[s].offset & 255)) {
@@ -83,6 +84,13 @@ int load_graph(const char* path, HostGraph* g, std::string* err) {
   g->g_nedges = (const int32_t*)g->section(OTMG_SEG_N_EDGES);
   g->cell_off = (const int64_t*)g->section(OTMG_CELL_OFF);
   g->cell_ent = (const uint32_t*)g->section(OTMG_CELL_ENT);
+  g->e_head_out = (const uint16_t*)g->section(OTMG_EDGE_HEAD_OUT);
+  g->e_head_in = (const uint16_t*)g->section(OTMG_EDGE_HEAD_IN);
+  for (int32_t e = 0; e < h.n_edges; ++e)
+    if (g->e_head_out[e] >= 360 || g->e_head_in[e] >= 360) {
+      *err = "graph file: edge heading out of [0, 360)";
+      return OTM_EIO;
+    }
   // structural checks the kernels rely on (no bounds checks on device)
   if (g->out_off[0] != 0 || g->out_off[h.n_nodes] != h.n_edges || g->e_shape_off[0] != 0 ||
       g->e_shape_off[h.n_edges] != h.n_shape || g->cell_off[(size_t)h.grid_rows * h.grid_cols] != h.n_cell_entries) {

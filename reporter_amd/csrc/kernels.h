@@ -43,6 +43,7 @@ struct DevGraph {
   const uint32_t* cell_off;  // 32-bit in HBM (engine_init checks the entry count)
   const uint32_t* cell_ent;
   const float4* ent_geo;  // per cell entry: shape segment endpoints (lat_a, lon_a, lat_b, lon_b)
+  const uint16_t *e_head_out, *e_head_in;  // edge bearing at start / end, whole degrees (turn costs)
   int32_t n_nodes, n_edges, n_segments, grid_rows, grid_cols;
   double lat0, lon0, cell;
   // spatial work order tiles: the node bbox cut into ORDER_SIDE^2 tiles
@@ -70,9 +71,11 @@ struct DevOrder {
 // Bounded distance index (built once per engine): for every
 // node u the nodes v with D(u,v) <= rmax, with D and the predecessor edge of
 // the search fixed point, held as one open-addressing hash table per row
-// (capacity a power of two >= 2 x entries, linear probing) so a lookup is
-// about one 8-byte read.  cnt < 0 marks a row whose search exceeded the build
-// table (queries on it use the online tiers).
+// (linear probing) so a lookup is about one 16-byte read.  A slot also
+// carries what the turn cost of the route u -> v needs: the turn units
+// between its own edges and the headings of its first and last edge.  cnt < 0
+// marks a row whose search exceeded the build table (queries on it use the
+// online tiers).
 struct IdxRow {
   int64_t off;    // first slot of the row's table
   int32_t cnt;    // entries, -1 incomplete
@@ -82,7 +85,9 @@ struct DevIndex {
   float rmax;  // 0: no index
   const IdxRow* row;
   const IdxRow* erow;    // per edge: the row of its end node (one round trip less from a candidate)
-  const uint2* slot;     // {node (0xFFFFFFFF empty), D bits}
+  // {node (0xFFFFFFFF empty), D bits, turn units between the route's edges,
+  //  head_out(first edge) | head_in(last edge) << 16 (0xFFFFFFFF: v == u)}
+  const uint4* slot;
   const int32_t* pred;   // per slot
 };
 constexpr int INDEX_BUILD_CAP = 2048;   // LDS table of the index builder
@@ -90,8 +95,12 @@ constexpr int INDEX_BUILD_LIMIT = 1536; // nodes per row before the row is left 
 
 // which kernels walk the spatial work order (env OTM_ORDER_MASK)
 constexpr int ORDER_CAND = 1, ORDER_TRANS = 2, ORDER_ROUTE = 4;
+constexpr int TURN_TABLE = 181;                 // turn units per deviation 0..180 degrees
+constexpr uint32_t TURN_UNITS_MAX = 0xFFFFFFu;   // 2^24 - 1: a route's units sum exact in a float
+constexpr uint32_t NO_TURNS = 0xFFFFFFFFu;       // index slot heads of the empty route (v == u)
 struct DevParams {
   float sigma_z, beta, factor, breakage, interp, search_radius, max_search_radius, gps_accuracy;
+  const uint32_t* turn_units;  // [TURN_TABLE] (device)
   int max_candidates;
   int order_mask;
   int cand_wave_all;  // small batch: every probe to the wave tier (latency, not throughput, bound)
@@ -253,8 +262,8 @@ void launch_compact(int32_t n_traces, const DevOut& o, const int32_t* seg_off, c
                     const int32_t* rep_off, void* segs_out, int64_t* ways_out, void* reps_out, hipStream_t s);
 // index build: pass 0 counts rows (row_cnt), pass 1 inserts them into the
 // row tables (slot array pre-filled with 0xFF)
-void launch_index_build(const DevGraph& g, float rmax, int32_t* row_cnt, const IdxRow* rows, uint2* slot,
-                        int32_t* pred, bool write, hipStream_t s);
+void launch_index_build(const DevGraph& g, const uint32_t* turn_units, float rmax, int32_t* row_cnt,
+                        const IdxRow* rows, uint4* slot, int32_t* pred, bool write, hipStream_t s);
 void launch_row_sizes(const int32_t* row_cnt, int64_t* row_sizes, int32_t n, hipStream_t s);
 struct BatchStatus {
   int32_t abort, pad;

@@ -113,6 +113,24 @@ __device__ __forceinline__ void cadd(unsigned long long* c, unsigned long long v
   if (c && v) atomicAdd(c, v);
 }
 
+// ============================================================== turn costs
+// deviation from straight on (0..180 degrees) of the turn from an edge whose
+// end heading is hin into an edge whose start heading is hout
+__device__ __forceinline__ uint32_t turn_deg(uint32_t hin, uint32_t hout) {
+  int d = (int)hout - (int)hin;
+  d += d < 0 ? 360 : 0;
+  return (uint32_t)(d <= 180 ? d : 360 - d);
+}
+// transition cost (turn_cost + |r - gc|) / beta of DESIGN.md §3; the turn
+// cost is integer 1/64 m units summed over the route's turns (order-free),
+// exact in a float below 2^24
+__device__ __forceinline__ float trans_cost(uint32_t units, float r, float gcv, float beta) {
+  units = units > TURN_UNITS_MAX ? TURN_UNITS_MAX : units;
+  const float tc = (float)units * 0.015625f;
+  const float diff = fabsf(r - gcv);
+  return (tc + diff) / beta;
+}
+
 // wave-wide inclusive scan of an int (64 lanes)
 __device__ __forceinline__ int wave_incl_scan(int v, int lane) {
 #pragma unroll
@@ -401,9 +419,6 @@ constexpr int CAND_TB = OTM_CAND_TB;
 #define OTM_CAND_INFL 2
 #endif
 constexpr int CAND_INFL = OTM_CAND_INFL;
-#ifndef OTM_TRANS_PACK
-#define OTM_TRANS_PACK 1
-#endif
 #ifndef OTM_CAND_FIND
 #define OTM_CAND_FIND 1
 #endif
@@ -1023,8 +1038,10 @@ __global__ __launch_bounds__(LANE_TB) void k_trans_lane(DevGraph g, DevBatch b, 
   if (*w.abort) return;  // a capacity was exceeded: the host redoes the batch
   __shared__ uint32_t sK[CAP * LANE_TB];
   __shared__ float sD[CAP * LANE_TB];
+  __shared__ int32_t sP[CAP * LANE_TB];  // predecessor edges: the routes' turns
   uint32_t* K = sK + threadIdx.x;
   float* D = sD + threadIdx.x;
+  int32_t* Pd = sP + threadIdx.x;
   unsigned long long c_search = 0, c_settled = 0, c_relaxed = 0, c_trans = 0;
   const int64_t nwork = w.counters_i32[4];  // columns the index could not answer
   if (nwork < LANE_TIER_MIN) {
@@ -1058,7 +1075,7 @@ __global__ __launch_bounds__(LANE_TB) void k_trans_lane(DevGraph g, DevBatch b, 
         }
       if (!first) continue;
       unsigned long long rel = 0;
-      const int n = lane_search<CAP, false>(g, K, D, nullptr, u, bound, rel);
+      const int n = lane_search<CAP, true>(g, K, D, Pd, u, bound, rel);
       if (n < 0) {
         failed = true;
         break;
@@ -1068,14 +1085,18 @@ __global__ __launch_bounds__(LANE_TB) void k_trans_lane(DevGraph g, DevBatch b, 
       s_relaxed += rel;
       for (int ii = i; ii < Kq; ++ii) {
         if (g.e_to[eq[CSTRIDE * (ii)]] != u) continue;
-        const float start = g.e_len[eq[CSTRIDE * (ii)]] - oq[CSTRIDE * (ii)];
+        const int32_t ei = eq[CSTRIDE * (ii)];
+        const float start = g.e_len[ei] - oq[CSTRIDE * (ii)];
         for (int j = 0; j < Kp; ++j) {
+          const int32_t ej = ep[CSTRIDE * (j)];
           float r;
           bool ok = true;
-          if (ep[CSTRIDE * (j)] == eq[CSTRIDE * (ii)] && op[CSTRIDE * (j)] >= oq[CSTRIDE * (ii)]) {
+          int f = -1;
+          const bool same = ej == ei && op[CSTRIDE * (j)] >= oq[CSTRIDE * (ii)];
+          if (same) {
             r = op[CSTRIDE * (j)] - oq[CSTRIDE * (ii)];
           } else {
-            const int f = lane_find<CAP>(K, n, (uint32_t)g.e_from[ep[CSTRIDE * (j)]]);
+            f = lane_find<CAP>(K, n, (uint32_t)g.e_from[ej]);
             if (f < 0) {
               ok = false;
               r = 0.0f;
@@ -1086,8 +1107,19 @@ __global__ __launch_bounds__(LANE_TB) void k_trans_lane(DevGraph g, DevBatch b, 
           }
           float cost = INFINITY;
           if (ok && r <= bound) {
-            const float diff = fabsf(r - gcv);
-            cost = diff / P.beta;
+            // the route's turns, walked back from e_j's start node to u
+            uint32_t units = 0;
+            if (!same) {
+              int32_t next = ej;
+              while ((K[f * LANE_TB] & ~DONE) != (uint32_t)u) {
+                const int32_t e = Pd[f * LANE_TB];
+                units += P.turn_units[turn_deg(g.e_head_in[e], g.e_head_out[next])];
+                next = e;
+                f = lane_find<CAP>(K, n, (uint32_t)g.e_from[e]);
+              }
+              units += P.turn_units[turn_deg(g.e_head_in[ei], g.e_head_out[next])];
+            }
+            cost = trans_cost(units, r, gcv, P.beta);
             ++s_trans;
           }
           Tm[ii * Kp + j] = cost;
@@ -1222,29 +1254,44 @@ __device__ __forceinline__ uint32_t idx_next(uint32_t h, const IdxRow& R) {
   return h + 1u == R.cap ? 0u : h + 1u;
 }
 
-// Row lookup: linear probing in u's table.  Returns the slot (D set) when v is
-// in the row, -1 when absent (D(u,v) > rmax), -2 when the row is incomplete.
-__device__ __forceinline__ int64_t idx_find(const DevIndex& X, const IdxRow& R, uint32_t v, float& D) {
+// Row lookup: linear probing in u's table.  Returns the slot (its contents in
+// *out) when v is in the row, -1 when absent (D(u,v) > rmax), -2 when the row
+// is incomplete.
+__device__ __forceinline__ int64_t idx_find(const DevIndex& X, const IdxRow& R, uint32_t v, uint4& out) {
   if (R.cnt < 0) return -2;
   if (R.cnt == 0) return -1;
   uint32_t h = idx_slot0(v, R);
   while (true) {
-    const uint2 sl = X.slot[R.off + h];
+    const uint4 sl = X.slot[R.off + h];
     if (sl.x == v) {
-      D = bitsf(sl.y);
+      out = sl;
       return R.off + h;
     }
     if (sl.x == EMPTY) return -1;
     h = idx_next(h, R);
   }
 }
+__device__ __forceinline__ int64_t idx_find(const DevIndex& X, const IdxRow& R, uint32_t v, float& D) {
+  uint4 sl;
+  const int64_t k = idx_find(X, R, v, sl);
+  if (k >= 0) D = bitsf(sl.y);
+  return k;
+}
+// turn units of the route e_i -> (index route u -> v) -> e_j from v's slot
+__device__ __forceinline__ uint32_t idx_turn_units(const uint32_t* TU, const uint4& sl, uint32_t hin_i,
+                                                   uint32_t hout_j) {
+  if (sl.w == NO_TURNS) return TU[turn_deg(hin_i, hout_j)];
+  return TU[turn_deg(hin_i, sl.w & 0xFFFFu)] + sl.z + TU[turn_deg(sl.w >> 16, hout_j)];
+}
 
 // Index build: one wavefront per source node u runs the bounded search with
 // bound rmax in an LDS table of INDEX_BUILD_CAP slots (same fixed point as the
-// online tiers), then writes the settled nodes sorted by id.
+// online tiers), then inserts every settled node v into the row's table with
+// its distance, predecessor edge and the turns of the route u -> v (each lane
+// walks its entry's predecessor chain back to u in the LDS table).
 template <bool WRITE>
-__global__ __launch_bounds__(TB) void k_index_build(DevGraph g, float rmax, int32_t* row_cnt, const IdxRow* rows,
-                                                    uint2* slot, int32_t* pred) {
+__global__ __launch_bounds__(TB) void k_index_build(DevGraph g, const uint32_t* TU, float rmax, int32_t* row_cnt,
+                                                    const IdxRow* rows, uint4* slot, int32_t* pred) {
   __shared__ uint32_t lkey[INDEX_BUILD_CAP];
   __shared__ unsigned long long llab[INDEX_BUILD_CAP];
   __shared__ uint32_t linq[INDEX_BUILD_CAP];
@@ -1267,10 +1314,26 @@ __global__ __launch_bounds__(TB) void k_index_build(DevGraph g, float rmax, int3
       const uint32_t k = lkey[i];
       if (k == EMPTY) continue;
       const unsigned long long lab = llab[i];
+      const int32_t pk = (int32_t)(uint32_t)(lab & 0xFFFFFFFFull);
+      // the route u -> k: turns between its edges, first / last edge headings
+      uint32_t inner = 0, heads = NO_TURNS;
+      if (k != (uint32_t)u) {
+        int32_t next = pk;
+        for (int32_t x = g.e_from[pk]; x != u;) {
+          const int sx = table_find<false>(T, (uint32_t)x);
+          const int32_t e = (int32_t)(uint32_t)(llab[sx] & 0xFFFFFFFFull);
+          inner += TU[turn_deg(g.e_head_in[e], g.e_head_out[next])];
+          next = e;
+          x = g.e_from[e];
+        }
+        heads = (uint32_t)g.e_head_out[next] | ((uint32_t)g.e_head_in[pk] << 16);
+      }
       uint32_t h = idx_slot0(k, R);
       while (atomicCAS(&slot[R.off + h].x, EMPTY, k) != EMPTY) h = idx_next(h, R);
       slot[R.off + h].y = (uint32_t)(lab >> 32);
-      pred[R.off + h] = (int32_t)(uint32_t)(lab & 0xFFFFFFFFull);
+      slot[R.off + h].z = inner;
+      slot[R.off + h].w = heads;
+      pred[R.off + h] = pk;
     }
     __syncthreads();
   }
@@ -1290,162 +1353,28 @@ __global__ void k_row_pack(const int32_t* row_cnt, const int64_t* row_off, IdxRo
   rows[u] = IdxRow{row_off[u], row_cnt[u], (uint32_t)cap};
 }
 
-// K4 index tier: one wavefront per column pair, lanes over the Kq x Kp
-// (source candidate, target candidate) pairs; each pair is one probe of the
-// source node's index row.  Loads are grouped by what they depend on (point p,
-// then column q, then edges, then rows) so a column costs ~5 memory round
-// trips.  Columns the index cannot answer (bound > rmax, or a source row
-// incomplete) go to the search tiers.
-__global__ __launch_bounds__(TB, 8) void k_trans_index(DevGraph g, DevBatch b, DevParams P, DevWork w) {
-  if (*w.abort) return;  // a capacity was exceeded: the host redoes the batch
-  __shared__ int32_t ep[KMAX], vp[KMAX], eq[KMAX];
-  __shared__ float op[KMAX], oq[KMAX], sq[KMAX];
-  __shared__ IdxRow rq[KMAX];
-  const int lane = threadIdx.x;
-  const DevIndex& X = w.idx;
-  unsigned long long c_search = 0, c_settled = 0, c_relaxed = 0, c_trans = 0;
-  const ItemRange IR = item_range(w, b, (P.order_mask & ORDER_TRANS) != 0, 1);
-  for (int64_t it = IR.i0; it < IR.i1; it += IR.stride) {
-    // wave-uniform: keep p (and every load indexed by it) scalar
-    const int64_t p = IR.ordered ? (int64_t)__builtin_amdgcn_readfirstlane(w.ord.item[it]) : it;
-    // by p
-    const int32_t q = w.col_prev[p];
-    const int Kp = w.ncand[p];
-    const float gcv = w.gc[p];
-    const int64_t toff = w.trans_off[p];
-    int32_t e_p = 0;
-    float o_p = 0.0f;
-    if (lane < KMAX) {
-      e_p = w.cand_edge[CSTRIDE * (p * KMAX + lane)];
-      o_p = w.cand_off[CSTRIDE * (p * KMAX + lane)];
-    }
-    if (q < 0) continue;
-    // by q
-    const int Kq = w.ncand[q];
-    int32_t e_q = 0;
-    float o_q = 0.0f;
-    if (lane < KMAX) {
-      e_q = w.cand_edge[CSTRIDE * ((int64_t)q * KMAX + lane)];
-      o_q = w.cand_off[CSTRIDE * ((int64_t)q * KMAX + lane)];
-    }
-    // by edge
-    int32_t u = 0;
-    float len_q = 0.0f;
-    if (lane < Kq) {
-      u = g.e_to[e_q];
-      len_q = g.e_len[e_q];
-    }
-    if (lane < Kp) {
-      ep[lane] = e_p;
-      op[lane] = o_p;
-      vp[lane] = g.e_from[e_p];
-    }
-    // by row
-    const float bound = P.factor * gcv;
-    bool usable = X.rmax > 0.0f && bound <= X.rmax;
-    if (lane < Kq && usable) {  // (no rows at all when the index is off)
-      const IdxRow R = X.row[u];
-      usable = R.cnt >= 0;
-      eq[lane] = e_q;
-      oq[lane] = o_q;
-      sq[lane] = len_q - o_q;
-      rq[lane] = R;
-    }
-    if (__ballot(!usable) != 0ull) {
-      if (lane == 0) {
-        const int slot = atomicAdd(&w.counters_i32[4], 1);
-        w.overflow_list0[slot] = (int32_t)p;
-      }
-      __syncthreads();
-      continue;
-    }
-    __syncthreads();
-    float* Tm = w.trans + toff;
-    unsigned long long ntr = 0;
-    for (int idx = lane; idx < Kq * Kp; idx += TB) {
-      const int i = idx / Kp, j = idx - (idx / Kp) * Kp;
-      float r = 0.0f;
-      bool ok = true;
-      if (ep[j] == eq[i] && op[j] >= oq[i]) {
-        r = op[j] - oq[i];
-      } else {
-        float D;
-        if (idx_find(X, rq[i], (uint32_t)vp[j], D) >= 0) {
-          const float sd = sq[i] + D;
-          r = sd + op[j];
-        } else {
-          ok = false;
-        }
-      }
-      float cost = INFINITY;
-      if (ok && r <= bound) {
-        const float diff = fabsf(r - gcv);
-        cost = diff / P.beta;
-        ++ntr;
-      }
-      Tm[i * Kp + j] = cost;
-    }
-    if (w.ctr) {
-      // algorithmic counts of the equivalent searches: per distinct source,
-      // the row entries with D <= bound and their out-degrees
-      for (int i = 0; i < Kq; ++i) {
-        bool first = true;
-        for (int k = 0; k < i; ++k) first = first && rq[k].off != rq[i].off;
-        if (!first) continue;
-        const IdxRow R = rq[i];
-        unsigned long long st = 0, rl = 0;
-        for (int64_t k = lane; k < (int64_t)R.cap; k += TB) {
-          const uint2 sl = X.slot[R.off + k];
-          if (sl.x != EMPTY && bitsf(sl.y) <= bound) {
-            ++st;
-            rl += (unsigned long long)(g.out_off[sl.x + 1] - g.out_off[sl.x]);
-          }
-        }
-        for (int sh = 32; sh > 0; sh >>= 1) {
-          st += __shfl_xor(st, sh, 64);
-          rl += __shfl_xor(rl, sh, 64);
-        }
-        c_search += 1;
-        c_settled += st;
-        c_relaxed += rl;
-      }
-      for (int sh = 32; sh > 0; sh >>= 1) ntr += __shfl_xor(ntr, sh, 64);
-      c_trans += ntr;
-    }
-    __syncthreads();
-  }
-  if (w.ctr && lane == 0) {
-    cadd(&w.ctr->searches, c_search);
-    cadd(&w.ctr->nodes_settled, c_settled);
-    cadd(&w.ctr->edges_relaxed, c_relaxed);
-    cadd(&w.ctr->transitions, c_trans);
-  }
-}
-
-// K4 index tier, sub-wave form: S lanes per column, TB / S columns in flight
-// per wave.  Same per-pair work as k_trans_index; a column is a chain of ~5
-// dependent round trips (point -> previous column -> edges -> rows ->
-// slots), so several columns per wave multiply the misses in flight at the
-// same occupancy.  Columns with more pairs than S loop within their group.
+// K4 index tier: S lanes per column, TB / S columns in flight per wave,
+// lanes over the column's Kq x Kp (source candidate, target candidate) pairs;
+// each pair is one probe of the source node's index row, whose 16-byte slot
+// holds the route distance and its turns.  A column is a chain of ~5
+// dependent round trips (point -> previous column -> edges -> rows -> slots),
+// so several columns per wave multiply the misses in flight at the same
+// occupancy.  Columns with more pairs than S loop within their group; columns
+// the index cannot answer (bound > rmax, a source row incomplete, more than
+// KC candidates) go to the search tiers.
 template <int S>
 __global__ __launch_bounds__(TB, 8) void k_trans_sub(DevGraph g, DevBatch b, DevParams P, DevWork w) {
   if (*w.abort) return;  // a capacity was exceeded: the host redoes the batch
   constexpr int NS = TB / S;
-#if OTM_TRANS_PACK
-  // a pair reads its target and source as one 16-byte LDS word each;
-  // columns with more than KC candidates go to the online tiers
+  // a pair reads its target and source as one 16-byte LDS word each
   constexpr int KC = 16;
-  __shared__ int4 tg[NS][KC];  // target: edge, offset bits, from-node
-  __shared__ int4 sr[NS][KC];  // source: edge, offset bits, remaining-length bits
+  __shared__ int4 tg[NS][KC];  // target: edge, offset bits, from-node, start heading
+  __shared__ int4 sr[NS][KC];  // source: edge, offset bits, remaining-length bits, end heading
   __shared__ IdxRow rq[NS][KC];
-#else
-  constexpr int KC = KMAX;
-  __shared__ int32_t ep[NS][KMAX], vp[NS][KMAX], eq[NS][KMAX];
-  __shared__ float op[NS][KMAX], oq[NS][KMAX], sq[NS][KMAX];
-  __shared__ IdxRow rq[NS][KMAX];
-#endif
+  __shared__ uint32_t TU[TURN_TABLE];  // turn units per deviation
   const int lane = threadIdx.x, sg = lane / S, sl = lane % S;
   const unsigned long long smask = (S == 64 ? ~0ull : ((1ull << S) - 1ull)) << (sg * S);
+  for (int k = lane; k < TURN_TABLE; k += TB) TU[k] = P.turn_units[k];
   const DevIndex& X = w.idx;
   unsigned long long c_search = 0, c_settled = 0, c_relaxed = 0, c_trans = 0;
   const bool ordered = (P.order_mask & ORDER_TRANS) != 0;
@@ -1483,24 +1412,13 @@ __global__ __launch_bounds__(TB, 8) void k_trans_sub(DevGraph g, DevBatch b, Dev
     for (int k = sl; k < KC; k += S) {
       if (act && k < Kp) {
         const int32_t e = w.cand_edge[CSTRIDE * (p * KMAX + k)];
-#if OTM_TRANS_PACK
-        tg[sg][k] = make_int4(e, __float_as_int(w.cand_off[CSTRIDE * (p * KMAX + k)]), g.e_from[e], 0);
-#else
-        ep[sg][k] = e;
-        op[sg][k] = w.cand_off[CSTRIDE * (p * KMAX + k)];
-        vp[sg][k] = g.e_from[e];
-#endif
+        tg[sg][k] = make_int4(e, __float_as_int(w.cand_off[CSTRIDE * (p * KMAX + k)]), g.e_from[e],
+                              (int)g.e_head_out[e]);
       }
       if (act && k < Kq) {
         const int32_t e = w.cand_edge[CSTRIDE * ((int64_t)q * KMAX + k)];
         const float o = w.cand_off[CSTRIDE * ((int64_t)q * KMAX + k)];
-#if OTM_TRANS_PACK
-        sr[sg][k] = make_int4(e, __float_as_int(o), __float_as_int(g.e_len[e] - o), 0);
-#else
-        eq[sg][k] = e;
-        oq[sg][k] = o;
-        sq[sg][k] = g.e_len[e] - o;
-#endif
+        sr[sg][k] = make_int4(e, __float_as_int(o), __float_as_int(g.e_len[e] - o), (int)g.e_head_in[e]);
         if (idx_ok) {
 #if OTM_IDX_EROW
           const IdxRow R = X.erow[e];
@@ -1526,29 +1444,25 @@ __global__ __launch_bounds__(TB, 8) void k_trans_sub(DevGraph g, DevBatch b, Dev
         const int i = idx / Kp, j = idx - (idx / Kp) * Kp;
         float r = 0.0f;
         bool ok = true;
-#if OTM_TRANS_PACK
+        uint32_t units = 0;
         const int4 T = tg[sg][j], Sx = sr[sg][i];
         const int32_t ej = T.x, vj = T.z, ei = Sx.x;
         const float oj = __int_as_float(T.y), oi = __int_as_float(Sx.y), si = __int_as_float(Sx.z);
-#else
-        const int32_t ej = ep[sg][j], vj = vp[sg][j], ei = eq[sg][i];
-        const float oj = op[sg][j], oi = oq[sg][i], si = sq[sg][i];
-#endif
         if (ej == ei && oj >= oi) {
           r = oj - oi;
         } else {
-          float D;
-          if (idx_find(X, rq[sg][i], (uint32_t)vj, D) >= 0) {
-            const float sd = si + D;
+          uint4 slv;
+          if (idx_find(X, rq[sg][i], (uint32_t)vj, slv) >= 0) {
+            const float sd = si + bitsf(slv.y);
             r = sd + oj;
+            units = idx_turn_units(TU, slv, (uint32_t)Sx.w, (uint32_t)T.w);
           } else {
             ok = false;
           }
         }
         float cost = INFINITY;
         if (ok && r <= bound) {
-          const float diff = fabsf(r - gcv);
-          cost = diff / P.beta;
+          cost = trans_cost(units, r, gcv, P.beta);
           ++ntr;
         }
         Tm[i * Kp + j] = cost;
@@ -1563,7 +1477,7 @@ __global__ __launch_bounds__(TB, 8) void k_trans_sub(DevGraph g, DevBatch b, Dev
           if (!first) continue;
           const IdxRow R = rq[sg][i];
           for (int64_t k = sl; k < (int64_t)R.cap; k += S) {
-            const uint2 slt = X.slot[R.off + k];
+            const uint4 slt = X.slot[R.off + k];
             if (slt.x != EMPTY && bitsf(slt.y) <= bound) {
               ++c_settled;
               c_relaxed += (unsigned long long)(g.out_off[slt.x + 1] - g.out_off[slt.x]);
@@ -1670,7 +1584,7 @@ __global__ __launch_bounds__(256, OTM_ROUTE_WAVES) void k_route_index(DevGraph g
     if (w.ctr) {
       unsigned long long st = 0, rl = 0;
       for (int64_t k = 0; k < (int64_t)R.cap; ++k) {
-        const uint2 sl = X.slot[R.off + k];
+        const uint4 sl = X.slot[R.off + k];
         if (sl.x != EMPTY && bitsf(sl.y) <= bound) {
           ++st;
           rl += (unsigned long long)(g.out_off[sl.x + 1] - g.out_off[sl.x]);
@@ -1761,13 +1675,15 @@ __global__ __launch_bounds__(TB) void k_transitions(DevGraph g, DevBatch b, DevP
       for (int idx = lane; idx < Kq * Kp; idx += TB) {
         const int i = idx / Kp, j = idx - (idx / Kp) * Kp;
         if (g.e_to[eq[i]] != u) continue;
-        const float start = g.e_len[eq[i]] - oq[i];
+        const int32_t ei = eq[i], ej = ep[j];
+        const float start = g.e_len[ei] - oq[i];
         float r;
         bool ok = true;
-        if (ep[j] == eq[i] && op[j] >= oq[i]) {
+        const bool same = ej == ei && op[j] >= oq[i];
+        if (same) {
           r = op[j] - oq[i];
         } else {
-          const int slot = table_find<BIG>(T, (uint32_t)g.e_from[ep[j]]);
+          const int slot = table_find<BIG>(T, (uint32_t)g.e_from[ej]);
           if (slot < 0) {
             ok = false;
             r = 0.0f;
@@ -1779,8 +1695,20 @@ __global__ __launch_bounds__(TB) void k_transitions(DevGraph g, DevBatch b, DevP
         }
         float cost = INFINITY;
         if (ok && r <= bound) {
-          const float diff = fabsf(r - gcv);
-          cost = diff / P.beta;
+          // the route's turns, walked back over the converged labels
+          uint32_t units = 0;
+          if (!same) {
+            int32_t next = ej;
+            for (int32_t x = g.e_from[ej]; x != u;) {
+              const int sx = table_find<BIG>(T, (uint32_t)x);
+              const int32_t e = (int32_t)(uint32_t)(Mem<BIG>::ld(&T.lab[sx]) & 0xFFFFFFFFull);
+              units += P.turn_units[turn_deg(g.e_head_in[e], g.e_head_out[next])];
+              next = e;
+              x = g.e_from[e];
+            }
+            units += P.turn_units[turn_deg(g.e_head_in[ei], g.e_head_out[next])];
+          }
+          cost = trans_cost(units, r, gcv, P.beta);
           ++ntr;
         }
         Tm[i * Kp + j] = cost;
@@ -3102,7 +3030,7 @@ namespace {
 // read the list length themselves (fixed grids, no host round trip) and exit
 // at once when the list is empty.
 constexpr int LANE_CAP = 24;        // route stage: 12 B per slot
-constexpr int LANE_CAP_TRANS = 32;  // transitions: 8 B per slot (no predecessors)
+constexpr int LANE_CAP_TRANS = 24;  // transitions: 12 B per slot (predecessors give the route's turns)
 constexpr int SPILL_GRID = 4096;
 constexpr int LANE_GRID = 2048;
 }  // namespace
@@ -3182,7 +3110,7 @@ void launch_transitions(const DevGraph& g, const DevBatch& b, const DevParams& p
   else if (sub == 16)
     TIMED(KN_TRANS_INDEX, hipLaunchKernelGGL(k_trans_sub<16>, dim3(grid), dim3(TB), 0, s, g, b, p, w));
   else
-    TIMED(KN_TRANS_INDEX, hipLaunchKernelGGL(k_trans_index, dim3(grid), dim3(TB), 0, s, g, b, p, w));
+    TIMED(KN_TRANS_INDEX, hipLaunchKernelGGL(k_trans_sub<64>, dim3(grid), dim3(TB), 0, s, g, b, p, w));
   TIMED(KN_TRANS_LANE, hipLaunchKernelGGL(k_trans_lane<LANE_CAP_TRANS>, dim3(LANE_GRID), dim3(LANE_TB), 0, s, g, b,
                                           p, w));
   TIMED(KN_TRANS_WAVE, hipLaunchKernelGGL(k_transitions<false>, dim3(SPILL_GRID), dim3(TB), 0, s, g, b, p, w, 0));
@@ -3238,13 +3166,15 @@ void launch_report(const DevBatch& b, const DevReportCfg& rc, DevWork& w, DevOut
 }
 #undef TIMED
 
-void launch_index_build(const DevGraph& g, float rmax, int32_t* row_cnt, const IdxRow* rows, uint2* slot,
-                        int32_t* pred, bool write, hipStream_t s) {
+void launch_index_build(const DevGraph& g, const uint32_t* turn_units, float rmax, int32_t* row_cnt,
+                        const IdxRow* rows, uint4* slot, int32_t* pred, bool write, hipStream_t s) {
   const int grid = grid_for(g.n_nodes, 1, 256 * 16);
   if (write)
-    hipLaunchKernelGGL(k_index_build<true>, dim3(grid), dim3(TB), 0, s, g, rmax, row_cnt, rows, slot, pred);
+    hipLaunchKernelGGL(k_index_build<true>, dim3(grid), dim3(TB), 0, s, g, turn_units, rmax, row_cnt, rows, slot,
+                       pred);
   else
-    hipLaunchKernelGGL(k_index_build<false>, dim3(grid), dim3(TB), 0, s, g, rmax, row_cnt, rows, slot, pred);
+    hipLaunchKernelGGL(k_index_build<false>, dim3(grid), dim3(TB), 0, s, g, turn_units, rmax, row_cnt, rows, slot,
+                       pred);
 }
 void launch_row_sizes(const int32_t* row_cnt, int64_t* row_sizes, int32_t n, hipStream_t s) {
   hipLaunchKernelGGL(k_row_sizes, dim3(grid_for((int64_t)n + 1, 256, 1 << 30)), dim3(256), 0, s, row_cnt, row_sizes,

@@ -64,6 +64,7 @@ struct HostGraph {
   const int32_t *g_first = nullptr, *g_nedges = nullptr;
   const int64_t* cell_off = nullptr;
   const uint32_t* cell_ent = nullptr;
+  const uint16_t *e_head_out = nullptr, *e_head_in = nullptr;
 
   const void* section(int s) const { return (const char*)map + h.sec[s].offset; }
   ~HostGraph();
@@ -82,6 +83,9 @@ struct MatchConfig {
   float max_search_radius = 100.0f;
   float gps_accuracy = 5.0f;
   int max_candidates = 32;
+  // meili's turn penalty (auto costing: 200; the default costing's is 0):
+  // the transition cost is (turn_cost + |route - gc|) / beta
+  float turn_penalty_factor = 200.0f;
 };
 
 // reporter_service.py make_thread_locals (:51-62) state

@@ -308,6 +308,16 @@ int synth_graph_write(const otm_synth_graph_params* p, const char* out_path, std
   std::vector<float> elen(NE), espeed(NE);
   std::vector<int64_t> eway(NE);
   std::vector<uint8_t> eflags(NE), elevel(NE);
+  std::vector<uint16_t> ehead_out(NE), ehead_in(NE);
+  // bearing (whole degrees, clockwise from north) of shape segment a -> b
+  auto bearing = [&](float la0, float lo0, float la1, float lo1) {
+    const double mid = 0.5 * ((double)la0 + (double)la1) * kPi / 180.0;
+    const double dx = ((double)lo1 - (double)lo0) * kMpd * std::cos(mid);
+    const double dy = ((double)la1 - (double)la0) * kMpd;
+    double b = std::atan2(dx, dy) * 180.0 / kPi;
+    long r = std::lround(b < 0.0 ? b + 360.0 : b);
+    return (uint16_t)(r % 360);
+  };
   std::vector<float> slat, slon, scum;
   for (int k = 0; k < NE; ++k) {
     const auto& e = E[order[k]];
@@ -327,6 +337,9 @@ int synth_graph_write(const otm_synth_graph_params* p, const char* out_path, std
     elevel[k] = (uint8_t)e.level;
     espeed[k] = e.speed;
     eopp[k] = rank[e.opp];
+    const size_t ns = e.lat.size();
+    ehead_out[k] = bearing(e.lat[0], e.lon[0], e.lat[1], e.lon[1]);
+    ehead_in[k] = bearing(e.lat[ns - 2], e.lon[ns - 2], e.lat[ns - 1], e.lon[ns - 1]);
     out_off[e.from + 1]++;
   }
   eshape_off[NE] = (int32_t)slat.size();
@@ -417,6 +430,7 @@ int synth_graph_write(const otm_synth_graph_params* p, const char* out_path, std
       {slon.data(), slon.size() * 4}, {scum.data(), scum.size() * 4}, {seg_id.data(), (size_t)NG * 8},
       {seg_len.data(), (size_t)NG * 4},       {gfirst.data(), (size_t)NG * 4},        {gnedges.data(), (size_t)NG * 4},
       {cell_off.data(), cell_off.size() * 8}, {cell_ent.data(), cell_ent.size() * 4},
+      {ehead_out.data(), (size_t)NE * 2},     {ehead_in.data(), (size_t)NE * 2},
   };
   size_t off = align256(sizeof(h));
   for (int s = 0; s < OTMG_NUM_SECTIONS; ++s) {

@@ -8,7 +8,9 @@
 // on each axis.  lat/lon are float32 and time integral, as the Java host
 // would send them (Point.java:19-21).  Vehicle v's stream depends only on
 // (seed, vehicle_offset + v), so uuid shards generate identical vehicles.
+#include <algorithm>
 #include <cmath>
+#include <cstring>
 #include <string>
 #include <vector>
 
@@ -28,8 +30,11 @@ double heading(const HostGraph& g, int e, bool at_end) {
 }
 }  // namespace
 
+// path (optional): the edges each vehicle drives from its first to its last
+// probe, in order, appended per vehicle; path_off[v] = where vehicle v's start
 int synth_traces(const HostGraph& g, const otm_synth_trace_params* p, int64_t* trace_off, float* lat, float* lon,
-                 double* time, float* accuracy, int32_t* true_edge, float* true_off) {
+                 double* time, float* accuracy, int32_t* true_edge, float* true_off,
+                 std::vector<int32_t>* path = nullptr, int64_t* path_off = nullptr) {
   const int NE = g.h.n_edges;
   std::vector<int> starts;
   for (int e = 0; e < NE; ++e)
@@ -43,6 +48,10 @@ int synth_traces(const HostGraph& g, const otm_synth_trace_params* p, int64_t* t
     rng.next();
     int e = starts[rng.next() % starts.size()];
     double off = rng.uni() * g.e_len[e];
+    if (path) {
+      path_off[v] = (int64_t)path->size();
+      path->push_back(e);
+    }
     double f = rng.uni();
     int internal_run = 0;
     auto speed_of = [&](int edge) {
@@ -73,7 +82,8 @@ int synth_traces(const HostGraph& g, const otm_synth_trace_params* p, int64_t* t
       if (true_edge) true_edge[P] = e;
       if (true_off) true_off[P] = (float)off;
       ++P;
-      // advance
+      // advance (not past the last probe: the true path ends on its edge)
+      if (s + 1 == p->points_per_vehicle) break;
       double dt = p->interval_s;
       int guard = 0;
       while (dt > 0 && guard++ < 10000) {
@@ -112,10 +122,12 @@ int synth_traces(const HostGraph& g, const otm_synth_trace_params* p, int64_t* t
         internal_run = (g.e_flags[next] & OTM_EDGE_INTERNAL) ? internal_run + 1 : 0;
         e = next;
         off = 0;
+        if (path) path->push_back(e);
       }
     }
   }
   trace_off[p->n_vehicles] = P;
+  if (path) path_off[p->n_vehicles] = (int64_t)path->size();
   return OTM_OK;
 }
 
@@ -132,6 +144,34 @@ extern "C" int otm_synth_traces(const char* graph_path, const otm_synth_trace_pa
     return rc;
   }
   return otm::synth_traces(g, p, trace_off, lat, lon, time, accuracy, true_edge, true_off);
+}
+
+// The ground truth of otm_synth_traces: each vehicle's driven edge sequence
+// (same generator, same seeds), for implementation-independent accuracy
+// figures.  Fills path_off[n_vehicles + 1] and up to `cap` edges; returns the
+// total edge count (call with cap 0 to size), or a negative error.
+extern "C" int64_t otm_synth_true_paths(const char* graph_path, const otm_synth_trace_params* p, int64_t* path_off,
+                                        int32_t* path_edges, int64_t cap) {
+  otm::HostGraph g;
+  std::string err;
+  int rc = otm::load_graph(graph_path, &g, &err);
+  if (rc) {
+    otm::set_thread_error(err);
+    return rc;
+  }
+  const size_t P = (size_t)p->n_vehicles * (size_t)p->points_per_vehicle;
+  std::vector<int64_t> toff((size_t)p->n_vehicles + 1);
+  std::vector<float> la(P), lo(P), acc(P);
+  std::vector<double> tm(P);
+  std::vector<int32_t> path;
+  std::vector<int64_t> poff((size_t)p->n_vehicles + 1);
+  rc = otm::synth_traces(g, p, toff.data(), la.data(), lo.data(), tm.data(), acc.data(), nullptr, nullptr, &path,
+                         poff.data());
+  if (rc) return rc;
+  if (path_off) std::memcpy(path_off, poff.data(), poff.size() * 8);
+  if (path_edges && cap > 0)
+    std::memcpy(path_edges, path.data(), (size_t)std::min<int64_t>(cap, (int64_t)path.size()) * 4);
+  return (int64_t)path.size();
 }
 
 // Kafka DefaultPartitioner: murmur2 (seed 0x9747b28c) over the key bytes.

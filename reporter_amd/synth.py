@@ -17,6 +17,8 @@ import numpy as np
 from . import _lib
 from ._lib import lib
 
+GRAPH_VERSION = 2  # OTMG_VERSION (include/otm_graph_format.h): cached graphs of another format are rebuilt
+
 CONFIGS = {
     1: dict(graph=dict(width_m=5000, height_m=5000), traces=dict(n_vehicles=100, points_per_vehicle=60,
                                                                  interval_s=5.0, noise_sigma_m=0.0, accuracy=0.0)),
@@ -80,7 +82,7 @@ def cached_graph(config, cache_dir=None):
     os.makedirs(cache_dir, exist_ok=True)
     g = CONFIGS[config]["graph"]
     tag = "_".join("%s%s" % (k, v) for k, v in sorted(g.items()))
-    path = os.path.join(cache_dir, "cfg%d_%s.otmg" % (config, tag))
+    path = os.path.join(cache_dir, "cfg%d_v%d_%s.otmg" % (config, GRAPH_VERSION, tag))
     if not os.path.exists(path):
         tmp = path + ".%d.tmp" % os.getpid()
         make_graph(tmp, **g)
@@ -97,6 +99,80 @@ def segment_ids(graph_path):
     hs = struct.calcsize("<8sII4i2iq3d4dQ")
     o, n = struct.unpack_from("<QQ", raw, hs + 16 * 17)  # OTMG_SEG_ID
     return np.frombuffer(raw, dtype=np.uint64, count=n // 8, offset=o).copy()
+
+
+def edge_segments(graph_path):
+    """Per edge: its OSMLR segment index (-1 none), section OTMG_EDGE_SEG."""
+    import struct
+    raw = np.fromfile(graph_path, dtype=np.uint8)
+    hs = struct.calcsize("<8sII4i2iq3d4dQ")
+    o, n = struct.unpack_from("<QQ", raw, hs + 16 * 8)  # OTMG_EDGE_SEG
+    return np.frombuffer(raw, dtype=np.int32, count=n // 4, offset=o).copy()
+
+
+def true_paths(graph_path, n_vehicles, points_per_vehicle, interval_s=5.0, noise_sigma_m=15.0, accuracy=15.0,
+               t0=1500000000.0, seed=7, vehicle_offset=0, vehicle_ids=None):
+    """Ground truth of make_traces (same arguments): (path_off [V+1], edges) --
+    the edges each vehicle drove from its first probe to its last."""
+    ids = None
+    if vehicle_ids is not None:
+        ids = np.ascontiguousarray(vehicle_ids, dtype=np.int32)
+        n_vehicles = len(ids)
+    tp = _lib.SynthTraceParams(n_vehicles, points_per_vehicle, interval_s, noise_sigma_m, accuracy, t0, seed,
+                               vehicle_offset, ids.ctypes.data if ids is not None else None)
+    off = np.zeros(n_vehicles + 1, np.int64)
+    n = lib().otm_synth_true_paths(graph_path.encode(), C.byref(tp), off.ctypes.data, None, 0)
+    if n < 0:
+        raise RuntimeError("otm_synth_true_paths failed: %s" % _lib.last_error())
+    edges = np.zeros(max(n, 1), np.int32)
+    lib().otm_synth_true_paths(graph_path.encode(), C.byref(tp), off.ctypes.data, edges.ctypes.data, n)
+    return off, edges[:n]
+
+
+def _dedup(seq):
+    out = []
+    for x in seq:
+        if not out or out[-1] != x:
+            out.append(x)
+    return out
+
+
+def _lcs(a, b):
+    if not a or not b:
+        return 0
+    prev = [0] * (len(b) + 1)
+    for x in a:
+        cur = [0]
+        for j, y in enumerate(b):
+            cur.append(prev[j] + 1 if x == y else max(prev[j + 1], cur[j]))
+        prev = cur
+    return prev[-1]
+
+
+def segment_agreement(graph_path, path_off, path_edges, results):
+    """Implementation-independent accuracy of a matched batch against the
+    generator's ground truth: per trace the OSMLR segment-id sequence the
+    vehicle drove (segments of its true edges, consecutive repeats merged)
+    against the matched one (segments with an id, in order).  Returns
+    {"segment_id_agreement": sum LCS / sum max(len), "sequences_exact":
+    fraction of traces whose sequences are equal, "traces": n}."""
+    ids = segment_ids(graph_path)
+    eseg = edge_segments(graph_path)
+    tr = results.traces if hasattr(results, "traces") else results["traces"]
+    segs = results.segments if hasattr(results, "segments") else results["segments"]
+    lcs = den = exact = 0
+    for t in range(len(tr)):
+        e = path_edges[path_off[t]:path_off[t + 1]]
+        sg = eseg[e]
+        truth = _dedup(ids[sg[sg >= 0]].tolist())
+        a, n = int(tr["seg_off"][t]), int(tr["seg_cnt"][t])
+        m = segs["segment_id"][a:a + n]
+        got = _dedup(m[m >= 0].astype(np.uint64).tolist())
+        lcs += _lcs(truth, got)
+        den += max(len(truth), len(got))
+        exact += truth == got
+    return {"segment_id_agreement": lcs / float(max(den, 1)), "sequences_exact": exact / float(max(len(tr), 1)),
+            "traces": len(tr)}
 
 
 def slice_batch(b, t0, t1):

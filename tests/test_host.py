@@ -124,3 +124,21 @@ def test_oracle_json_path_config1(small_graph, oracle):
 def test_cos_deg_accuracy(oracle):
     for d in np.linspace(-89.9, 89.9, 41):
         assert abs(oracle.cos_deg(float(d)) - np.cos(np.radians(d))) < 2e-7
+
+
+def test_turn_cost_table():
+    """meili's turn penalty table (turn_penalty_factor * exp(-theta / 45),
+    theta the angle between the reversed incoming and the outgoing edge) in
+    the oracle's 1/64 m units: straight on (deviation 0, theta 180) is the
+    smallest penalty, a U-turn (deviation 180, theta 0) the whole factor."""
+    import math
+    from oracle import pyoracle
+    L = pyoracle.lib()
+    L.orc_turn_units.restype = C.c_uint32
+    L.orc_turn_units.argtypes = [C.c_float, C.c_int]
+    t = [L.orc_turn_units(200.0, d) for d in range(181)]
+    assert t[180] == 200 * 64 and t[0] == round(200 * math.exp(-4) * 64)
+    assert all(t[d] <= t[d + 1] for d in range(180))
+    for d in (0, 45, 90, 135, 180):
+        assert abs(t[d] - 200 * 64 * math.exp(-(180 - d) / 45.0)) <= 0.5
+    assert all(L.orc_turn_units(0.0, d) == 0 for d in range(181))

@@ -74,7 +74,10 @@ def parse():
                          "metro run (1M vehicles / 8 GPUs), 4 = state-scale high-noise batch")
     ap.add_argument("--vehicles", type=int, default=0, help="per GPU (0: the config's own count)")
     ap.add_argument("--points", type=int, default=100, help="per vehicle")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (0: min(16, cores))")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU baseline threads (0: every host core this process may run on, os.sched_getaffinity)")
+    ap.add_argument("--host-steps", type=int, default=-1,
+                    help="steps of the host-inclusive leg (otm_match_soa from host arrays; -1: --steps, 0: skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-check", action="store_true", help="skip the untimed oracle pass (agreement, bytes)")
     ap.add_argument("--traffic-json", default=DEFAULT_TRAFFIC, help="PMC traffic summary (scripts/pmc_summary.py)")
@@ -113,6 +116,62 @@ def stage_bytes(c, ncand, col_prev, n_points):
         "route": 8 * c["route_nodes_settled"] + 12 * c["route_edges_relaxed"] + 4 * c["route_edges"],
         "segments": 16 * c["segments_out"],
     }
+
+
+def index_probe_bytes(ncand, col_prev, cand_edge, cand_off, kmax=32):
+    """Algorithmic bytes of the transition stage in the form the GPU runs it
+    (the distance-index probe of k_trans_sub), per linked
+    column q -> p of the oracle's stage outputs:
+      24 B column metadata (col_prev, 2 x ncand, gc, trans_off)
+      12 B x (Kq + Kp) candidate records {edge, offset, emission}
+      22 B x Kq source edges: row descriptor (16) + length (4) + end heading (2)
+       6 B x Kp target edges: from-node (4) + start heading (2)
+      16 B per pair that needs a route: one index slot {v, D, turns, headings}
+       4 B x Kq x Kp costs written
+    Pairs on the same edge, forward (the route is along the edge), read no slot."""
+    linked = np.nonzero(col_prev >= 0)[0]
+    if len(linked) == 0:
+        return 0
+    kq = ncand[col_prev[linked]].astype(np.int64)
+    kp = ncand[linked].astype(np.int64)
+    E = cand_edge.reshape(-1, kmax)
+    O = cand_off.reshape(-1, kmax)
+    same = 0
+    ar = np.arange(kmax)
+    for c0 in range(0, len(linked), 20000):
+        pl = linked[c0:c0 + 20000]
+        ql = col_prev[pl]
+        vq = ar[None, :] < ncand[ql][:, None]
+        vp = ar[None, :] < ncand[pl][:, None]
+        m = (E[ql][:, :, None] == E[pl][:, None, :]) & (O[pl][:, None, :] >= O[ql][:, :, None])
+        m &= vq[:, :, None] & vp[:, None, :]
+        same += int(m.sum())
+    pairs = int((kq * kp).sum())
+    return (24 * len(linked) + int(12 * (kq + kp).sum()) + int(22 * kq.sum()) + int(6 * kp.sum())
+            + 16 * (pairs - same) + 4 * pairs)
+
+
+def host_info():
+    """The GPU box's host: logical CPUs this process may run on, all of the
+    machine's, and the CPU model (lscpu)."""
+    import subprocess
+    model = None
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=20).stdout
+        for line in out.splitlines():
+            if line.startswith("Model name:"):
+                model = line.split(":", 1)[1].strip()
+    except Exception:
+        pass
+    quota = None
+    try:  # cgroup v2 CPU quota ("max" or "<quota> <period>")
+        q = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q and q[0] != "max":
+            quota = float(q[0]) / float(q[1])
+    except Exception:
+        pass
+    return {"usable_cpus": len(os.sched_getaffinity(0)), "machine_cpus": os.cpu_count(), "cgroup_cpu_quota": quota,
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS"), "model": model}
 
 
 def load_traffic(path):
@@ -161,7 +220,9 @@ def main():
     nseg_pad = flush.padded_segments(nseg, world)
     hist = torch.zeros(nseg_pad * nbins, dtype=torch.int32, device=dev)
     hist_shard = torch.zeros(nseg_pad * nbins // world, dtype=torch.int32, device=dev)
-    eng.hist_bind(hist, nbins, bin_kph)
+    speed_sum = torch.zeros(nseg_pad, dtype=torch.int64, device=dev)
+    speed_shard = torch.zeros(nseg_pad // world, dtype=torch.int64, device=dev)
+    eng.hist_bind(hist, nbins, bin_kph, speed_sum=speed_sum)
     # batches in flight: clones share the graph, index and histogram binding
     inflight = max(1, args.inflight)
     engines = [eng] + [eng.clone() for _ in range(inflight - 1)]
@@ -183,6 +244,7 @@ def main():
             step(i)
     torch.cuda.synchronize(dev)
     hist.zero_()
+    speed_sum.zero_()
     torch.cuda.synchronize(dev)
 
     # timed region: K steps spread over the in-flight contexts (one host
@@ -211,7 +273,7 @@ def main():
         t.join()
     torch.cuda.synchronize(dev)
     if world > 1:
-        flush.reduce_histograms(hist, out=hist_shard)
+        flush.reduce_histograms(hist, out=hist_shard, speed_sum=speed_sum, speed_out=speed_shard)
         torch.cuda.synchronize(dev)
         dist.barrier()
     elapsed = time.perf_counter() - t_start
@@ -236,11 +298,57 @@ def main():
     value = total_points / elapsed
     ms_per_step = elapsed * 1e3 / args.steps
     spill = eng.spill_stats()
+    index = eng.index_info()
+
+    # ---- host-inclusive leg (config 2 "via Java FFM host"): the binary C-ABI
+    # call the host makes, otm_match_soa, from host arrays to host results --
+    # H2D of the inputs, every kernel, the compaction and the D2H copies --
+    # with the same batches in flight; not `value`
+    host_leg = None
+    host_steps = args.steps if args.host_steps < 0 else args.host_steps
+    if host_steps > 0:
+        import ctypes as C
+        hb = _lib.Batch(len(batch["trace_off"]) - 1, P, batch["trace_off"].ctypes.data, batch["lat"].ctypes.data,
+                        batch["lon"].ctypes.data, batch["time"].ctypes.data, batch["accuracy"].ctypes.data)
+        outs = [_lib.Results() for _ in engines]
+
+        def host_step(i):
+            rc = _lib.lib().otm_match_soa(engines[i].h, C.byref(hb), C.byref(outs[i]))
+            if rc != 0:
+                raise RuntimeError("otm_match_soa: %s" % _lib.last_error())
+
+        for i in range(inflight):
+            host_step(i)
+        hticket = itertools.count()
+        hgate = threading.Barrier(inflight + 1)
+
+        def hworker(i):
+            hgate.wait()
+            while next(hticket) < host_steps:
+                host_step(i)
+
+        hthreads = [threading.Thread(target=hworker, args=(i,)) for i in range(inflight)]
+        for t in hthreads:
+            t.start()
+        torch.cuda.synchronize(dev)
+        th0 = time.perf_counter()
+        hgate.wait()
+        for t in hthreads:
+            t.join()
+        torch.cuda.synchronize(dev)
+        hel = time.perf_counter() - th0
+        host_leg = {"value": P * host_steps / hel, "unit": "points/s", "ms_per_step": hel * 1e3 / host_steps,
+                    "steps": host_steps, "batches_in_flight": inflight,
+                    "includes": "otm_match_soa from pageable host arrays: H2D of the inputs (24 B/point), all "
+                                "kernels, result compaction, D2H of traces / segments / reports / way ids into "
+                                "pinned host buffers; JSON not included"}
+        hist.zero_()
+        speed_sum.zero_()
 
     # ---- untimed: the CPU oracle over this rank's whole batch -> agreement
     # with the GPU result and the algorithmic bytes of every stage
     res = eng.fetch()
-    agreement, sbytes, stages = None, None, None
+    agreement, sbytes, stages, probe_bytes = None, None, None, None
     if rank == 0 and not args.no_check:
         from oracle import pyoracle
         torc = time.perf_counter()
@@ -256,10 +364,21 @@ def main():
                                          orc["segments"]["segment_id"][oa:oa + on]))
         same = all(getattr(res, k).tobytes() == orc[k].tobytes() for k in ("traces", "segments", "reports",
                                                                             "way_ids"))
+        # implementation-independent: both against the generator's ground truth
+        tr_args = dict(cfg["traces"])
+        tr_args["points_per_vehicle"] = args.points
+        tr_args.pop("n_vehicles", None)
+        poff, pedges = synth.true_paths(graph, len(ids), vehicle_ids=ids, **tr_args)
+        truth_gpu = synth.segment_agreement(graph, poff, pedges, res)
         agreement = {"segment_id_sequences_equal_vs_oracle": seq_eq / float(max(nt, 1)), "traces": nt,
                      "all_outputs_bit_identical": bool(same),
+                     "vs_ground_truth": {"segment_id_agreement": truth_gpu["segment_id_agreement"],
+                                         "sequences_exact": truth_gpu["sequences_exact"],
+                                         "what": "per trace, the OSMLR segment-id sequence the synthetic vehicle "
+                                                 "drove vs the matched one: sum of LCS / sum of max length"},
                      "meili": "unavailable (parity vs meili unpinned)"}
         sbytes = stage_bytes(orc["counters"], orc["ncand"], orc["col_prev"], P)
+        probe_bytes = index_probe_bytes(orc["ncand"], orc["col_prev"], orc["cand_edge"], orc["cand_off"])
         stage_ms = {}
         for k, v in kern_avg.items():
             st = KERNEL_STAGE[k]
@@ -284,37 +403,62 @@ def main():
         tj = load_traffic(args.traffic_json) if (args.config == 2 or args.traffic_json != DEFAULT_TRAFFIC) else None
         if tj and dom in tj.get("kernels", {}):
             traffic = tj["kernels"][dom].get("hbm_bytes_per_launch")
+        sec = kern_avg[dom] * 1e-3
         roof = {"bound": "hbm", "kernel": dom, "stage": st, "achieved": achieved, "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
                 "algorithmic_bytes_per_launch": b, "launch_ms": kern_avg[dom],
+                "algorithmic_bytes_basis": "SURVEY.md §8(d): the bounded searches the oracle runs for the stage",
                 "traffic_source": os.path.relpath(args.traffic_json, ROOT) if traffic is not None else None}
+        if st == "transitions" and probe_bytes:
+            # the index-probe algorithm's own bytes (what k_trans_sub must move)
+            roof["index_probe_bytes_per_launch"] = probe_bytes
+            roof["frac_index_probe"] = probe_bytes / sec / 1e9 / HBM_PEAK_GBS
+        if traffic is not None:
+            # measured HBM bytes (PMC, corrected per the traffic file) over the same launch time
+            roof["frac_counter"] = traffic / sec / 1e9 / HBM_PEAK_GBS
+            roof["traffic_correction"] = (tj or {}).get("correction")
+        roof["index_build_ms"] = index["build_ms"]
+        roof["index_radius_m"] = index["radius_m"]
 
     # ---- CPU baseline: the oracle on this GPU's batch, host threads
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             from oracle import pyoracle
-            threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+            hinfo = host_info()
             g = pyoracle.Graph(graph)
             nsamp = min(len(ids), 2000)  # 200k points: a bounded sample of the same workload
             sb = synth.slice_batch(batch, 0, nsamp)
             ps = int(sb["trace_off"][-1])
             op = pyoracle.params(**meili)
-            pyoracle.match_batch(g, synth.slice_batch(batch, 0, 50), p=op, nthreads=threads)  # warm
-            reps, best = 0, None
-            tcpu = time.perf_counter()
-            while reps < 3 or time.perf_counter() - tcpu < 10.0:
-                ts = time.perf_counter()
-                pyoracle.match_batch(g, sb, p=op, nthreads=threads)
-                dt = time.perf_counter() - ts
-                best = dt if best is None else min(best, dt)
-                reps += 1
-                if time.perf_counter() - tcpu > 30.0:
-                    break
+            # The host's capacity: every CPU this process may run on, and (when a
+            # cgroup quota or OMP_NUM_THREADS caps it below that) the capped
+            # count too; the faster of the two is the baseline
+            cands = [args.cpu_threads] if args.cpu_threads else sorted({
+                hinfo["usable_cpus"], int(hinfo["cgroup_cpu_quota"] or hinfo["usable_cpus"]),
+                int(hinfo["omp_num_threads"] or hinfo["usable_cpus"])})
+            best, threads, reps = None, None, 0
+            for nth in cands:
+                pyoracle.match_batch(g, synth.slice_batch(batch, 0, 50), p=op, nthreads=nth)  # warm
+                tcpu = time.perf_counter()
+                k = 0
+                while k < 3 or time.perf_counter() - tcpu < 10.0:
+                    ts = time.perf_counter()
+                    pyoracle.match_batch(g, sb, p=op, nthreads=nth)
+                    dt = time.perf_counter() - ts
+                    if best is None or dt < best:
+                        best, threads = dt, nth
+                    k += 1
+                    if time.perf_counter() - tcpu > 20.0:
+                        break
+                reps += k
             cpu = {"value": ps / best, "unit": "points/s", "cores": threads, "kind": "port",
+                   "host": hinfo,
                    "sample": "%d vehicles x %d pts (%d points) of the same config-%d batch, CPU oracle "
-                             "(meili restatement, C -O3), best of %d runs, %d host threads" %
-                             (nsamp, args.points, ps, args.config, reps, threads)}
+                             "(meili restatement, C -O3, bounded Dijkstra per transition: no distance index), "
+                             "best of %d runs over %s host threads (best: %d; %s)" %
+                             (nsamp, args.points, ps, args.config, reps, "/".join(map(str, cands)), threads,
+                              hinfo["model"])}
         except Exception as e:
             cpu = {"error": str(e)}
 
@@ -344,6 +488,7 @@ def main():
             "stages": stages,
             "spill": spill,
             "cpu_baseline": cpu,
+            "host_inclusive": host_leg,
             "agreement": agreement,
             "hip_runtime": _lib.runtime_info(),
         }

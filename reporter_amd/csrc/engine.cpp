@@ -358,6 +358,7 @@ void engine_free(otm_engine* E) {
       &E->big_lab,       &E->big_inq,      &E->big_fr,         &E->o_traces,       &E->o_seg_cnt,  &E->o_way_cnt,
       &E->o_segments,    &E->o_seg_gidx,   &E->o_way_ids,      &E->o_reports,  &E->o_rep_cnt,  &E->seg_ub,
       &E->f_seg_off,     &E->f_way_off,    &E->f_rep_off,      &E->f_segs,     &E->f_ways,     &E->f_reps,
+      &E->f_traces,
       &E->abort_flag,    &E->rs_blob,      &E->ord_tile,      &E->ord_cnt,      &E->ord_cursor,     &E->ord_grp,    &E->ord_item};
   for (auto* b : bufs) {
     if (b->p) (void)hipFree(b->p);
@@ -727,6 +728,7 @@ int engine_fetch(otm_engine* E, otm_results* out, std::string* err) {
   ENS_F(f_segs, ((size_t)NS + 1) * sizeof(otm_segment));
   ENS_F(f_ways, ((size_t)NW + 1) * 8);
   ENS_F(f_reps, ((size_t)NR + 1) * sizeof(otm_report_rec));
+  ENS_F(f_traces, ((size_t)NT + 1) * sizeof(otm_trace_result));
   if (NT) {
     DevOut o{};
     o.traces = E->o_traces.p;
@@ -736,7 +738,7 @@ int engine_fetch(otm_engine* E, otm_results* out, std::string* err) {
     o.segments = E->o_segments.p;
     o.way_ids = P<int64_t>(E->o_way_ids);
     o.reports = E->o_reports.p;
-    launch_compact(NT, o, so, wo, ro, E->f_segs.p, P<int64_t>(E->f_ways), E->f_reps.p, s);
+    launch_compact(NT, o, so, wo, ro, E->f_segs.p, P<int64_t>(E->f_ways), E->f_reps.p, E->f_traces.p, s);
     HIPCHK(hipGetLastError());
   }
   E->last_S = NS;
@@ -745,7 +747,7 @@ int engine_fetch(otm_engine* E, otm_results* out, std::string* err) {
   if ((rc = ensure_pinned(E->h_segs, ((size_t)NS + 1) * sizeof(otm_segment), err))) return rc;
   if ((rc = ensure_pinned(E->h_reps_dense, ((size_t)NR + 1) * sizeof(otm_report_rec), err))) return rc;
   if ((rc = ensure_pinned(E->h_ways, ((size_t)NW + 1) * 8, err))) return rc;
-  if (NT) HIPCHK(hipMemcpyAsync(E->h_traces.p, E->o_traces.p, (size_t)NT * sizeof(otm_trace_result),
+  if (NT) HIPCHK(hipMemcpyAsync(E->h_traces.p, E->f_traces.p, (size_t)NT * sizeof(otm_trace_result),
                                 hipMemcpyDeviceToHost, s));
   if (NS) HIPCHK(hipMemcpyAsync(E->h_segs.p, E->f_segs.p, (size_t)NS * sizeof(otm_segment), hipMemcpyDeviceToHost, s));
   if (NR) HIPCHK(hipMemcpyAsync(E->h_reps_dense.p, E->f_reps.p, (size_t)NR * sizeof(otm_report_rec),

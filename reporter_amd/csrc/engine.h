@@ -56,7 +56,7 @@ struct otm_engine {
   // outputs
   Buf o_traces, o_seg_cnt, o_way_cnt, o_rep_cnt, seg_ub, o_segments, o_seg_gidx, o_way_ids, o_reports;
   // dense copies made by engine_fetch
-  Buf f_seg_off, f_way_off, f_rep_off, f_segs, f_ways, f_reps;
+  Buf f_seg_off, f_way_off, f_rep_off, f_segs, f_ways, f_reps, f_traces;
   otm::DevCounters* ctr = nullptr;
   otm::DevCounters* ctr_save = nullptr;
   bool counting = false;

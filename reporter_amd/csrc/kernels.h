@@ -259,7 +259,8 @@ void launch_seg_bound(const DevBatch& b, DevWork& w, int64_t* ub, hipStream_t s,
 // fetch-time compaction of the per-trace regions into dense arrays; offsets
 // are the exclusive scans of seg_cnt / way_cnt / rep_cnt
 void launch_compact(int32_t n_traces, const DevOut& o, const int32_t* seg_off, const int32_t* way_off,
-                    const int32_t* rep_off, void* segs_out, int64_t* ways_out, void* reps_out, hipStream_t s);
+                    const int32_t* rep_off, void* segs_out, int64_t* ways_out, void* reps_out, void* traces_out,
+                    hipStream_t s);
 // index build: pass 0 counts rows (row_cnt), pass 1 inserts them into the
 // row tables (slot array pre-filled with 0xFF)
 void launch_index_build(const DevGraph& g, const uint32_t* turn_units, float rmax, int32_t* row_cnt,

@@ -2916,13 +2916,14 @@ __global__ __launch_bounds__(256) void k_seg_bound(DevBatch b, DevWork w, int64_
 }
 
 // One wavefront per trace: copy its segments (way offsets rebased), way ids
-// and reports from the trace's region to the dense arrays; rewrite the
-// trace's offsets.
+// and reports from the trace's region to the dense arrays, and its result
+// record with the dense offsets to `to` (the regions' records stay as they
+// are, so fetching a batch twice gives the same arrays).
 __global__ __launch_bounds__(TB) void k_compact(int32_t n_traces, DevOut o, const int32_t* seg_off, const int32_t* way_off,
                                                 const int32_t* rep_off, otm_segment* so, int64_t* wo,
-                                                otm_report_rec* ro) {
+                                                otm_report_rec* ro, otm_trace_result* to) {
   const int lane = threadIdx.x;
-  otm_trace_result* TR = (otm_trace_result*)o.traces;
+  const otm_trace_result* TR = (const otm_trace_result*)o.traces;
   const otm_segment* SI = (const otm_segment*)o.segments;
   const otm_report_rec* RI = (const otm_report_rec*)o.reports;
   for (int32_t t = blockIdx.x; t < n_traces; t += gridDim.x) {
@@ -2937,8 +2938,10 @@ __global__ __launch_bounds__(TB) void k_compact(int32_t n_traces, DevOut o, cons
     for (int k = lane; k < nw; k += TB) wo[dw + k] = o.way_ids[base + k];
     for (int k = lane; k < nr; k += TB) ro[dr + k] = RI[base + k];
     if (lane == 0) {
-      TR[t].seg_off = ds;
-      TR[t].rep_off = dr;
+      otm_trace_result x = TR[t];
+      x.seg_off = ds;
+      x.rep_off = dr;
+      to[t] = x;
     }
   }
 }
@@ -3148,9 +3151,11 @@ void launch_seg_bound(const DevBatch& b, DevWork& w, int64_t* ub, hipStream_t s,
                                          b, w, ub));
 }
 void launch_compact(int32_t n_traces, const DevOut& o, const int32_t* seg_off, const int32_t* way_off,
-                    const int32_t* rep_off, void* segs_out, int64_t* ways_out, void* reps_out, hipStream_t s) {
+                    const int32_t* rep_off, void* segs_out, int64_t* ways_out, void* reps_out, void* traces_out,
+                    hipStream_t s) {
   hipLaunchKernelGGL(k_compact, dim3(grid_for(n_traces, 1, WAVE_GRID_CAP)), dim3(TB), 0, s, n_traces, o, seg_off, way_off,
-                     rep_off, (otm_segment*)segs_out, ways_out, (otm_report_rec*)reps_out);
+                     rep_off, (otm_segment*)segs_out, ways_out, (otm_report_rec*)reps_out,
+                     (otm_trace_result*)traces_out);
 }
 void launch_report(const DevBatch& b, const DevReportCfg& rc, DevWork& w, DevOut& o, hipStream_t s,
                    const Marks& mk) {

@@ -6,10 +6,16 @@ With a kernel-trace stats CSV of the same command, each kernel also gets its
 achieved HBM GB/s (PMC bytes / average duration) and fraction of 8 TB/s.
 LDS bank-conflict rate = SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE.
 
-hbm_bytes_per_launch follows MI355X_MICROARCH.md §HBM: FETCH_SIZE and
-WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports half the bytes of a wide
-streaming read, so the read side is doubled (an upper bound for narrower
-access shapes, which the guide leaves uncalibrated).
+hbm_bytes_per_launch = 32 x (TCC_EA0_RDREQ_DRAM_32B + TCC_EA0_WRREQ_WRITE_DRAM_32B
++ TCC_EA0_WRREQ_ATOMIC_DRAM_32B): the DRAM-destined requests in 32-byte units
+(rocprofv3 -L on gfx950: "1 64-byte request will be counted to 2, 128-byte as
+4"), so every access width is weighted by its real request size -- the
+calibration MI355X_MICROARCH.md §HBM asks for instead of its x2 for wide
+streaming reads.  (Like FETCH_SIZE, these are memory-side requests;
+Infinity-Cache hits are not excluded.)  The FETCH_SIZE x 2 + WRITE_SIZE figure
+of round 1 is kept as fetch_x2_write_bytes, and the request-size mix
+(TCC_EA0_RDREQ_32B / 64B / 128B of TCC_EA0_RDREQ) shows what the kernel's
+gathers cost.
 """
 import csv
 import glob
@@ -56,12 +62,24 @@ def main():
             names[r["Dispatch_Id"]] = short(r["Kernel_Name"])
         for (disp, cn), v in per.items():
             vals[names[disp]][cn].append(v)
-    out = {"tag": tag, "note": "per-launch means over the profiled dispatches; FETCH_SIZE doubled (gfx950)",
+    out = {"tag": tag, "note": "per-launch means over the profiled dispatches",
+           "correction": "hbm_bytes = 32 B x size-weighted DRAM read + write + atomic requests (no FETCH_SIZE factor)",
            "kernels": {}}
     for k, cs in sorted(vals.items()):
         d = {cn: sum(v) / len(v) for cn, v in cs.items()}
         if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
-            d["hbm_bytes_per_launch"] = (2.0 * d["FETCH_SIZE"] + d["WRITE_SIZE"]) * 1024.0
+            d["fetch_x2_write_bytes"] = (2.0 * d["FETCH_SIZE"] + d["WRITE_SIZE"]) * 1024.0
+        dram = [d.get(c) for c in ("TCC_EA0_RDREQ_DRAM_32B_sum", "TCC_EA0_WRREQ_WRITE_DRAM_32B_sum",
+                                   "TCC_EA0_WRREQ_ATOMIC_DRAM_32B_sum")]
+        if all(v is not None for v in dram):
+            d["hbm_read_bytes"] = 32.0 * dram[0]
+            d["hbm_write_bytes"] = 32.0 * (dram[1] + dram[2])
+            d["hbm_bytes_per_launch"] = d["hbm_read_bytes"] + d["hbm_write_bytes"]
+        if d.get("TCC_EA0_RDREQ_sum"):
+            n = d["TCC_EA0_RDREQ_sum"]
+            d["read_request_mix"] = {"32B": d.get("TCC_EA0_RDREQ_32B_sum", 0.0) / n,
+                                     "64B": d.get("TCC_EA0_RDREQ_64B_sum", 0.0) / n,
+                                     "128B": d.get("TCC_EA0_RDREQ_128B_sum", 0.0) / n}
         if "TCC_HIT_sum" in d and "TCC_MISS_sum" in d and d["TCC_HIT_sum"] + d["TCC_MISS_sum"] > 0:
             d["l2_hit_rate"] = d["TCC_HIT_sum"] / (d["TCC_HIT_sum"] + d["TCC_MISS_sum"])
         if d.get("SQ_LDS_IDX_ACTIVE"):

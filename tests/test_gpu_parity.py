@@ -287,3 +287,15 @@ def test_clone_concurrent_batches_identical(small_graph):
             assert got["a"] == want_a and got["b"] == want_b
         finally:
             cl.close()
+
+
+def test_fetch_is_idempotent(small_graph):
+    """otm_fetch_results may be called again for the same batch (a host that
+    re-reads, the bench's checks after its timed legs): same arrays."""
+    b = synth.make_traces(small_graph, 120, 60, seed=57)
+    with Engine(graph_path=small_graph) as eng:
+        r1 = eng.match(b)
+        r2 = eng.fetch()
+        r3 = eng.fetch()
+    for k in ("traces", "segments", "reports", "way_ids"):
+        assert getattr(r1, k).tobytes() == getattr(r2, k).tobytes() == getattr(r3, k).tobytes(), k

@@ -272,6 +272,14 @@ int otm_graph_info(const otm_engine* eng, int64_t* n_nodes, int64_t* n_edges,
 int otm_index_info(const otm_engine* eng, float* rmax, int64_t* entries,
                    int32_t* incomplete_rows, float* build_ms);
 
+/* The candidate search's grid index on the device: the graph file's cells
+ * (meili's 500 per 0.25 deg tile) merged mult x mult (config
+ * "otm":{"grid_mult": m} or env OTM_GRID_MULT; absent or 0: chosen from the
+ * graph's entry density and the search radius).  Coarser cells change how
+ * many cells and entries a probe visits, never the candidates. */
+int otm_grid_info(const otm_engine* eng, double* cell_deg, int32_t* rows, int32_t* cols,
+                  int64_t* entries, int32_t* mult);
+
 /* Work counters of the last batch (for the roofline's algorithmic bytes). */
 typedef struct otm_work_counters {
   int64_t points, columns, cells_visited, cell_entries_scanned, candidates;

@@ -255,6 +255,13 @@ int otm_engine_create(const char* cfg_path, const int* devices, int ndev, otm_en
   const Value* ir = o->get("index_radius_m");
   if (ir && ir->is_num()) E->index_rmax = (float)ir->num();
   if (const char* er = std::getenv("OTM_INDEX_RADIUS")) E->index_rmax = (float)std::atof(er);  // A/B override
+  const Value* gm = o->get("grid_mult");
+  if (gm && gm->kind == Kind::Int) E->grid_mult = (int)gm->i;
+  if (const char* v = std::getenv("OTM_GRID_MULT")) E->grid_mult = std::atoi(v);
+  if (E->grid_mult < 0 || E->grid_mult > 64) {
+    delete E;
+    return fail(OTM_EINVAL, "grid_mult must be in [0 (auto), 64]");
+  }
   const Value* meili = cfg.get("meili");
   const Value* dflt = meili ? meili->get("default") : nullptr;
   if (dflt && dflt->kind == Kind::Obj) {
@@ -600,6 +607,17 @@ int otm_index_info(const otm_engine* E, float* rmax, int64_t* entries, int32_t* 
   if (entries) *entries = E->index_entries;
   if (incomplete_rows) *incomplete_rows = E->index_incomplete_rows;
   if (build_ms) *build_ms = E->index_build_ms;
+  return OTM_OK;
+}
+
+int otm_grid_info(const otm_engine* E, double* cell_deg, int32_t* rows, int32_t* cols, int64_t* entries,
+                  int32_t* mult) {
+  if (!E) return fail(OTM_EINVAL, "engine is NULL");
+  if (cell_deg) *cell_deg = E->g.cell;
+  if (rows) *rows = E->grid_rows;
+  if (cols) *cols = E->grid_cols;
+  if (entries) *entries = E->grid_entries;
+  if (mult) *mult = E->grid_mult;
   return OTM_OK;
 }
 

@@ -78,9 +78,34 @@ uint32_t turn_units(float factor, int d) {
   return (uint32_t)std::floor((double)factor * 64.0 / exp_series(x) + 0.5);
 }
 
+// Grid multiplier when the config names none: the m that minimises the
+// modelled cost of a probe's cell walk, ROW_COST x rows + entries scanned,
+// with rows = box / (m cell) + 1 for a radius box of 2 x search_radius and
+// entries = (entries per file cell) x m^2 x rows^2.  ROW_COST = 32 entries is
+// fitted to the candidate kernel's times at m = 1..4 on configs 2 and 4
+// (DESIGN.md §5): the city (2.9 entries per 56 m cell, 50 m radius) gets 2,
+// the state graph (0.35 per cell, 100 m) 4.
+static int auto_grid_mult(const otm_engine* E) {
+  constexpr double ROW_COST = 32.0;
+  const auto& h = E->host.h;
+  const double cells = std::max(1.0, (double)h.grid_rows * (double)h.grid_cols);
+  const double dens = (double)h.n_cell_entries / cells;
+  const double cell_m = h.grid_cell_deg * 111195.0;
+  const double box = 2.0 * std::max(1.0, (double)E->mc.search_radius);
+  int best = 1;
+  double best_cost = 1e300;
+  for (int m = 1; m <= 16; ++m) {
+    const double rows = box / (m * cell_m) + 1.0;
+    const double cost = ROW_COST * rows + dens * (double)m * m * rows * rows;
+    if (cost < best_cost) best_cost = cost, best = m;
+  }
+  return best;
+}
+
 int engine_init(otm_engine* E, const char* graph_path, int device, std::string* err) {
   int rc = load_graph(graph_path, &E->host, err);
   if (rc) return rc;
+  if (E->grid_mult == 0) E->grid_mult = auto_grid_mult(E);
   E->device = device;
   HIPCHK(hipSetDevice(device));
   HIPCHK(hipStreamCreateWithFlags(&E->stream, hipStreamNonBlocking));
@@ -115,7 +140,6 @@ int engine_init(otm_engine* E, const char* graph_path, int device, std::string* 
   UP(OTMG_SHAPE_CUM, s_cum, float);
   UP(OTMG_SEG_ID, g_id, uint64_t);
   UP(OTMG_SEG_LEN, g_len, float);
-  UP(OTMG_CELL_ENT, cell_ent, uint32_t);
   UP(OTMG_EDGE_HEAD_OUT, e_head_out, uint16_t);
   UP(OTMG_EDGE_HEAD_IN, e_head_in, uint16_t);
 #undef UP
@@ -131,29 +155,71 @@ int engine_init(otm_engine* E, const char* graph_path, int device, std::string* 
     E->dp.turn_units = (const uint32_t*)d;
   }
   {
+    // The grid index of the candidate search.  The file's cells (meili's
+    // 500 per 0.25 deg tile, ~55 m) may be merged m x m into coarser ones
+    // (OTM_GRID_MULT, or grid_mult in the config): a probe's radius box then
+    // spans fewer grid rows -- fewer dependent row loads -- at the price of
+    // more entries scanned.  The candidates do not change: a shape segment is
+    // listed in every cell its bbox touches, at either size, so every segment
+    // within the radius is found and the per-edge best (sqdist, segment) is
+    // the same minimum.  Only the cells / entries visited counts differ.
+    const int m = E->grid_mult < 1 ? 1 : E->grid_mult;
+    const int64_t* fo = (const int64_t*)E->host.section(OTMG_CELL_OFF);
+    const uint32_t* fe = (const uint32_t*)E->host.section(OTMG_CELL_ENT);
+    const int32_t R = (h.grid_rows + m - 1) / m, Cn = (h.grid_cols + m - 1) / m;
+    std::vector<uint64_t> co_ent;  // (coarse cell << 32 | entry), coarse grids only
+    const size_t nc = (size_t)R * (size_t)Cn + 1;
+    std::vector<uint32_t> c32(nc, 0);
+    std::vector<uint32_t> ent;
+    if (m == 1) {
+      if ((uint64_t)h.n_cell_entries >= (1ull << 32)) {
+        *err = "graph: more than 2^32 cell entries (32-bit cell offsets)";
+        return OTM_EINVAL;
+      }
+      for (size_t c = 0; c < nc; ++c) c32[c] = (uint32_t)fo[c];
+      ent.assign(fe, fe + h.n_cell_entries);
+    } else {
+      co_ent.reserve((size_t)h.n_cell_entries);
+      for (int32_t r = 0; r < h.grid_rows; ++r)
+        for (int32_t c = 0; c < h.grid_cols; ++c) {
+          const size_t f = (size_t)r * h.grid_cols + c;
+          const uint64_t cc = (uint64_t)(r / m) * (uint64_t)Cn + (uint64_t)(c / m);
+          for (int64_t q = fo[f]; q < fo[f + 1]; ++q) co_ent.push_back(cc << 32 | fe[q]);
+        }
+      std::sort(co_ent.begin(), co_ent.end());
+      co_ent.erase(std::unique(co_ent.begin(), co_ent.end()), co_ent.end());
+      if (co_ent.size() >= (1ull << 32)) {
+        *err = "graph: more than 2^32 cell entries (32-bit cell offsets)";
+        return OTM_EINVAL;
+      }
+      ent.resize(co_ent.size());
+      for (size_t k = 0; k < co_ent.size(); ++k) {
+        ent[k] = (uint32_t)co_ent[k];
+        c32[(co_ent[k] >> 32) + 1]++;
+      }
+      for (size_t c = 0; c + 1 < nc; ++c) c32[c + 1] += c32[c];
+      std::vector<uint64_t>().swap(co_ent);
+    }
+    E->grid_rows = R;
+    E->grid_cols = Cn;
+    E->grid_entries = (int64_t)ent.size();
     // cell offsets as 32-bit words in HBM: a sparse state-scale grid is
     // ~100M mostly-empty cells, and a probe's row range (2 offsets) then
     // usually sits in one cache line
-    const size_t nc = (size_t)h.grid_rows * (size_t)h.grid_cols + 1;
-    if ((uint64_t)h.n_cell_entries >= (1ull << 32)) {
-      *err = "graph: more than 2^32 cell entries (32-bit cell offsets)";
-      return OTM_EINVAL;
-    }
-    const int64_t* co = (const int64_t*)E->host.section(OTMG_CELL_OFF);
-    std::vector<uint32_t> c32(nc);
-    for (size_t c = 0; c < nc; ++c) c32[c] = (uint32_t)co[c];
     void* d = nullptr;
     HIPCHK(hipMalloc(&d, nc * 4));
     HIPCHK(hipMemcpy(d, c32.data(), nc * 4, hipMemcpyHostToDevice));
     E->graph_allocs.push_back(d);
     g.cell_off = (const uint32_t*)d;
-  }
-  {
+    d = nullptr;
+    HIPCHK(hipMalloc(&d, ent.size() * 4 + 16));
+    if (!ent.empty()) HIPCHK(hipMemcpy(d, ent.data(), ent.size() * 4, hipMemcpyHostToDevice));
+    E->graph_allocs.push_back(d);
+    g.cell_ent = (const uint32_t*)d;
     // per cell entry: the shape segment's endpoints (lat_a, lon_a, lat_b,
     // lon_b), laid out in cell order so a probe's scan of one grid row is
     // one contiguous float4 stream (no edge -> shape indirection)
-    const size_t ne = h.sec[OTMG_CELL_ENT].bytes / 4;
-    const uint32_t* ent = (const uint32_t*)E->host.section(OTMG_CELL_ENT);
+    const size_t ne = ent.size();
     const int32_t* soff = (const int32_t*)E->host.section(OTMG_EDGE_SHAPE_OFF);
     const float* slat = (const float*)E->host.section(OTMG_SHAPE_LAT);
     const float* slon = (const float*)E->host.section(OTMG_SHAPE_LON);
@@ -165,17 +231,18 @@ int engine_init(otm_engine* E, const char* graph_path, int device, std::string* 
       geo[q * 4 + 2] = slat[a + 1];
       geo[q * 4 + 3] = slon[a + 1];
     }
-    void* d = nullptr;
+    d = nullptr;
     HIPCHK(hipMalloc(&d, geo.size() * 4));
     HIPCHK(hipMemcpy(d, geo.data(), geo.size() * 4, hipMemcpyHostToDevice));
     E->graph_allocs.push_back(d);
     g.ent_geo = (const float4*)d;
+    g.grid_rows = R;
+    g.grid_cols = Cn;
+    g.cell = h.grid_cell_deg * (double)m;
   }
   g.n_nodes = h.n_nodes;
   g.n_edges = h.n_edges;
   g.n_segments = h.n_segments;
-  g.grid_rows = h.grid_rows;
-  g.grid_cols = h.grid_cols;
   {
     // spatial-order tiles over the node bbox (a hair wider so max lands inside)
     const double h_deg = (h.bbox[2] - h.bbox[0]) * 1.0001 + 1e-9, w_deg = (h.bbox[3] - h.bbox[1]) * 1.0001 + 1e-9;
@@ -186,7 +253,6 @@ int engine_init(otm_engine* E, const char* graph_path, int device, std::string* 
   }
   g.lat0 = h.grid_lat0;
   g.lon0 = h.grid_lon0;
-  g.cell = h.grid_cell_deg;
   HIPCHK(hipMalloc((void**)&E->ctr, sizeof(DevCounters)));
   HIPCHK(hipMalloc((void**)&E->ctr_save, sizeof(DevCounters)));
   HIPCHK(hipMemset(E->ctr, 0, sizeof(DevCounters)));

@@ -26,6 +26,9 @@ struct otm_engine {
   // the online tiers at a cost of 0.13 ms per batch
   float index_rmax = -1.0f;  // < 0: sized from the graph's node density (auto_index_radius)
   int64_t small_points = 0;  // batches below this many points: natural order, wave-tier candidates
+  int grid_mult = 0;         // candidate grid cells = grid_mult x grid_mult of the file's (0: auto_grid_mult)
+  int32_t grid_rows = 0, grid_cols = 0;
+  int64_t grid_entries = 0;
   otm::DevIndex idx{};
   int64_t index_entries = 0;
   int64_t index_slots = 0;  // hash-table slots (16 B each + 4 B predecessor)

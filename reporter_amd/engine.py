@@ -26,11 +26,13 @@ def _check(rc):
         raise OtmError("libotmatch error %d: %s" % (rc, _lib.last_error()))
 
 
-def write_config(path, graph_path, index_radius_m=None, **meili):
+def write_config(path, graph_path, index_radius_m=None, grid_mult=None, **meili):
     """Write an engine config: {"otm":{"graph":...,"index_radius_m":R},"meili":{"default":{...}}}."""
     otm = {"graph": os.path.abspath(graph_path)}
     if index_radius_m is not None:
         otm["index_radius_m"] = index_radius_m
+    if grid_mult is not None:
+        otm["grid_mult"] = grid_mult
     cfg = {"otm": otm, "meili": {"default": meili}}
     with open(path, "w") as f:
         json.dump(cfg, f)
@@ -48,7 +50,7 @@ class Results(object):
 
 
 class Engine(object):
-    def __init__(self, config_path=None, graph_path=None, device=0, index_radius_m=None, **meili):
+    def __init__(self, config_path=None, graph_path=None, device=0, index_radius_m=None, grid_mult=None, **meili):
         """Either a config file (valhalla.Configure-style) or a graph path."""
         L = lib()
         self._tmp = None
@@ -57,7 +59,8 @@ class Engine(object):
                 raise ValueError("config_path or graph_path required")
             fd, self._tmp = tempfile.mkstemp(suffix=".json", prefix="otm_cfg_")
             os.close(fd)
-            config_path = write_config(self._tmp, graph_path, index_radius_m=index_radius_m, **meili)
+            config_path = write_config(self._tmp, graph_path, index_radius_m=index_radius_m, grid_mult=grid_mult,
+                                       **meili)
         h = C.c_void_p()
         dev = (C.c_int * 1)(device)
         rc = L.otm_engine_create(config_path.encode(), dev, 1, C.byref(h))
@@ -202,6 +205,11 @@ class Engine(object):
         r, e, i, ms = C.c_float(), C.c_int64(), C.c_int32(), C.c_float()
         _check(lib().otm_index_info(self.h, C.byref(r), C.byref(e), C.byref(i), C.byref(ms)))
         return {"radius_m": r.value, "entries": e.value, "incomplete_rows": i.value, "build_ms": ms.value}
+
+    def grid_info(self):
+        cd, r, c, n, m = C.c_double(), C.c_int32(), C.c_int32(), C.c_int64(), C.c_int32()
+        _check(lib().otm_grid_info(self.h, C.byref(cd), C.byref(r), C.byref(c), C.byref(n), C.byref(m)))
+        return {"cell_deg": cd.value, "rows": r.value, "cols": c.value, "entries": n.value, "mult": m.value}
 
     def set_counting(self, on):
         _check(lib().otm_set_counting(self.h, 1 if on else 0))

@@ -76,6 +76,8 @@ def parse():
     ap.add_argument("--points", type=int, default=100, help="per vehicle")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="CPU baseline threads (0: every host core this process may run on, os.sched_getaffinity)")
+    ap.add_argument("--host-pageable", action="store_true",
+                    help="host-inclusive leg from pageable numpy arrays instead of otm_host_alloc buffers")
     ap.add_argument("--host-steps", type=int, default=-1,
                     help="steps of the host-inclusive leg (otm_match_soa from host arrays; -1: --steps, 0: skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -308,8 +310,23 @@ def main():
     host_steps = args.steps if args.host_steps < 0 else args.host_steps
     if host_steps > 0:
         import ctypes as C
-        hb = _lib.Batch(len(batch["trace_off"]) - 1, P, batch["trace_off"].ctypes.data, batch["lat"].ctypes.data,
-                        batch["lon"].ctypes.data, batch["time"].ctypes.data, batch["accuracy"].ctypes.data)
+        # the host's SoA buffers in page-locked memory (otm_host_alloc), as a
+        # Java FFM host would allocate them, filled outside the timed region
+        L = _lib.lib()
+        pinned, hptr = [], {}
+        for k in ("trace_off", "lat", "lon", "time", "accuracy"):
+            a = np.ascontiguousarray(batch[k])
+            if args.host_pageable:
+                hptr[k] = a.ctypes.data
+                continue
+            p_ = L.otm_host_alloc(a.nbytes)
+            if not p_:
+                raise RuntimeError("otm_host_alloc failed")
+            C.memmove(p_, a.ctypes.data, a.nbytes)
+            pinned.append(p_)
+            hptr[k] = p_
+        hb = _lib.Batch(len(batch["trace_off"]) - 1, P, hptr["trace_off"], hptr["lat"], hptr["lon"], hptr["time"],
+                        hptr["accuracy"])
         outs = [_lib.Results() for _ in engines]
 
         def host_step(i):
@@ -337,11 +354,14 @@ def main():
             t.join()
         torch.cuda.synchronize(dev)
         hel = time.perf_counter() - th0
+        for p_ in pinned:
+            L.otm_host_free(p_)
         host_leg = {"value": P * host_steps / hel, "unit": "points/s", "ms_per_step": hel * 1e3 / host_steps,
                     "steps": host_steps, "batches_in_flight": inflight,
-                    "includes": "otm_match_soa from pageable host arrays: H2D of the inputs (24 B/point), all "
-                                "kernels, result compaction, D2H of traces / segments / reports / way ids into "
-                                "pinned host buffers; JSON not included"}
+                    "host_buffers": "pageable" if args.host_pageable else "page-locked (otm_host_alloc)",
+                    "includes": "otm_match_soa from the host arrays: H2D of the inputs "
+                                "(24 B/point), all kernels, result compaction, D2H of traces / segments / reports "
+                                "/ way ids into pinned host buffers; JSON not included"}
         hist.zero_()
         speed_sum.zero_()
 

@@ -235,8 +235,15 @@ typedef struct otm_results {
   const int64_t* way_ids;
 } otm_results;
 
-/* Match a host-resident batch; results copied back to host. */
+/* Match a host-resident batch; results copied back to host.  Inputs in
+ * pinned memory (otm_host_alloc) go to the device by DMA at full PCIe speed;
+ * pageable inputs are staged by the HIP runtime. */
 int otm_match_soa(otm_engine* eng, const otm_batch* in, otm_results* out);
+/* Page-locked host memory for a host's batch buffers (hipHostMalloc): a Java
+ * host maps it as a MemorySegment and fills its SoA arrays in place.
+ * NULL on failure; release with otm_host_free (not otm_free). */
+void* otm_host_alloc(size_t bytes);
+void otm_host_free(void* p);
 
 /* Match a batch whose arrays are already in this engine's device memory.
  * Results stay on the device (fetch with otm_fetch_results).  `stream` is a

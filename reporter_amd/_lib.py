@@ -127,6 +127,8 @@ def _declare(L):
         "otm_poll": (C.c_int, [vp, C.POINTER(Result), C.c_int, C.c_int]),
         "otm_encode_request": (C.c_int, [C.c_char_p, C.c_int, vp, vp, vp, vp, pp, psz]),
         "otm_match_soa": (C.c_int, [vp, C.POINTER(Batch), C.POINTER(Results)]),
+        "otm_host_alloc": (vp, [sz]),
+        "otm_host_free": (None, [vp]),
         "otm_match_device": (C.c_int, [vp, C.POINTER(Batch), vp]),
         "otm_fetch_results": (C.c_int, [vp, C.POINTER(Results)]),
         "otm_hist_bind": (C.c_int, [vp, vp, C.c_int, C.c_float]),

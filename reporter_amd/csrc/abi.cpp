@@ -540,6 +540,19 @@ int otm_encode_request(const char* uuid, int n, const float* lat, const float* l
   return OTM_OK;
 }
 
+void* otm_host_alloc(size_t bytes) {
+  void* p = nullptr;
+  if (hipHostMalloc(&p, bytes ? bytes : 16, hipHostMallocDefault) != hipSuccess) {
+    fail(OTM_ENOMEM, "hipHostMalloc failed");
+    return nullptr;
+  }
+  return p;
+}
+
+void otm_host_free(void* p) {
+  if (p) (void)hipHostFree(p);
+}
+
 int otm_match_soa(otm_engine* E, const otm_batch* in, otm_results* out) {
   if (!E || !in || !out) return fail(OTM_EINVAL, "bad arguments");
   std::lock_guard<std::mutex> lk(E->mu);

@@ -422,6 +422,12 @@ constexpr int CAND_INFL = OTM_CAND_INFL;
 #ifndef OTM_CAND_FIND
 #define OTM_CAND_FIND 1
 #endif
+// transition index tier: pairs per lane whose first slot loads are issued
+// together: 2 measured 0.337 -> 0.302 ms on config 2, 1.956 -> 1.888 ms on
+// config 4; 3 and 4 slower (0.365 / 0.436 ms: registers, 4 spills)
+#ifndef OTM_TRANS_BATCH
+#define OTM_TRANS_BATCH 2
+#endif
 
 // wave-reduce a per-lane count and add it to a device counter (all 64 lanes active)
 __device__ __forceinline__ void wave_cadd(unsigned long long* c, unsigned long long v) {
@@ -1440,6 +1446,70 @@ __global__ __launch_bounds__(TB, 8) void k_trans_sub(DevGraph g, DevBatch b, Dev
     if (act) {
       float* Tm = w.trans + toff;
       unsigned long long ntr = 0;
+#if OTM_TRANS_BATCH > 1
+      // OTM_TRANS_BATCH pairs per lane per step: every pair's first slot is
+      // loaded before any is resolved, so their probes are in flight together
+      constexpr int NB = OTM_TRANS_BATCH;
+      const int npair = Kq * Kp;
+      for (int idx0 = sl; idx0 < npair; idx0 += S * NB) {
+        uint4 s0[NB];
+        uint32_t h0[NB];
+#pragma unroll
+        for (int u = 0; u < NB; ++u) {
+          const int idx = idx0 + u * S;
+          s0[u] = make_uint4(EMPTY, 0u, 0u, 0u);
+          h0[u] = 0u;
+          if (idx < npair) {
+            const int i = idx / Kp, j = idx - (idx / Kp) * Kp;
+            const int4 T = tg[sg][j], Sx = sr[sg][i];
+            const IdxRow R = rq[sg][i];
+            const bool same = T.x == Sx.x && __int_as_float(T.y) >= __int_as_float(Sx.y);
+            if (!same && R.cnt > 0) {
+              h0[u] = idx_slot0((uint32_t)T.z, R);
+              s0[u] = X.slot[R.off + h0[u]];
+            }
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < NB; ++u) {
+          const int idx = idx0 + u * S;
+          if (idx >= npair) continue;
+          const int i = idx / Kp, j = idx - (idx / Kp) * Kp;
+          const int4 T = tg[sg][j], Sx = sr[sg][i];
+          const int32_t ej = T.x, vj = T.z, ei = Sx.x;
+          const float oj = __int_as_float(T.y), oi = __int_as_float(Sx.y), si = __int_as_float(Sx.z);
+          float r = 0.0f;
+          bool ok = true;
+          uint32_t units = 0;
+          if (ej == ei && oj >= oi) {
+            r = oj - oi;
+          } else {
+            const IdxRow R = rq[sg][i];
+            uint4 sv = s0[u];
+            uint32_t h = h0[u];
+            if (R.cnt > 0) {
+              while (sv.x != (uint32_t)vj && sv.x != EMPTY) {  // the rest of the linear probe (rare)
+                h = idx_next(h, R);
+                sv = X.slot[R.off + h];
+              }
+            }
+            if (R.cnt > 0 && sv.x == (uint32_t)vj) {
+              const float sd = si + bitsf(sv.y);
+              r = sd + oj;
+              units = idx_turn_units(TU, sv, (uint32_t)Sx.w, (uint32_t)T.w);
+            } else {
+              ok = false;
+            }
+          }
+          float cost = INFINITY;
+          if (ok && r <= bound) {
+            cost = trans_cost(units, r, gcv, P.beta);
+            ++ntr;
+          }
+          Tm[i * Kp + j] = cost;
+        }
+      }
+#else
       for (int idx = sl; idx < Kq * Kp; idx += S) {
         const int i = idx / Kp, j = idx - (idx / Kp) * Kp;
         float r = 0.0f;
@@ -1467,6 +1537,7 @@ __global__ __launch_bounds__(TB, 8) void k_trans_sub(DevGraph g, DevBatch b, Dev
         }
         Tm[i * Kp + j] = cost;
       }
+#endif
       if (w.ctr) {
         // algorithmic counts of the equivalent searches (per-lane partials,
         // summed over the wave at the end): per distinct source, the row

@@ -41,6 +41,8 @@ sys.path.insert(0, ROOT)
 METRIC = "GPS points matched/sec (whole node) at 1/2/4/8 MI355X; % segment-ID agreement vs meili"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 DEFAULT_TRAFFIC = os.path.join(ROOT, "profiles", "pmc_traffic_latest.json")
+# committed PMC summaries per config (scripts/pmc.sh); --traffic-json overrides
+CONFIG_TRAFFIC = {2: DEFAULT_TRAFFIC, 4: os.path.join(ROOT, "profiles", "pmc_traffic_config4_latest.json")}
 
 # config -> (graph, workload); config 2 is the headline line, config 4 a
 # secondary one (BASELINE.json configs[3]: wide radius, long transitions)
@@ -56,7 +58,7 @@ WORKLOAD = {
 # kernel -> (stage, main tier of the stage?)
 KERNEL_STAGE = {
     "k_columns": "columns", "spatial_order": "candidates", "k_cand_lane": "candidates", "k_candidates": "candidates", "k_links": "links_scan",
-    "scan_trans_off": "links_scan", "k_trans_index": "transitions", "k_trans_lane": "transitions",
+    "scan_trans_off": "links_scan", "k_trans_sub": "transitions", "k_trans_lane": "transitions",
     "k_transitions": "transitions", "k_transitions_big": "transitions", "k_viterbi": "viterbi",
     "k_route_index": "route", "k_route_lane": "route", "k_route": "route", "k_route_big": "route",
     "k_seg_bound": "segments", "scan_seg_bound": "segments", "k_segments": "segments",
@@ -82,7 +84,8 @@ def parse():
                     help="steps of the host-inclusive leg (otm_match_soa from host arrays; -1: --steps, 0: skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-check", action="store_true", help="skip the untimed oracle pass (agreement, bytes)")
-    ap.add_argument("--traffic-json", default=DEFAULT_TRAFFIC, help="PMC traffic summary (scripts/pmc_summary.py)")
+    ap.add_argument("--traffic-json", default=None,
+                    help="PMC traffic summary (scripts/pmc_summary.py); default: the committed one for --config")
     ap.add_argument("--inflight", type=int, default=3,
                     help="batches in flight per GPU: engine clones on their own HIP streams, one host thread each")
     return ap.parse_args()
@@ -419,8 +422,8 @@ def main():
         # few (spill stats); attribute the stage's bytes to the main kernel
         achieved = b / (kern_avg[dom] * 1e-3) / 1e9 if b else None
         traffic = None
-        # the committed PMC summary is config 2's; other configs need their own
-        tj = load_traffic(args.traffic_json) if (args.config == 2 or args.traffic_json != DEFAULT_TRAFFIC) else None
+        tpath = args.traffic_json or CONFIG_TRAFFIC.get(args.config)
+        tj = load_traffic(tpath) if tpath else None
         if tj and dom in tj.get("kernels", {}):
             traffic = tj["kernels"][dom].get("hbm_bytes_per_launch")
         sec = kern_avg[dom] * 1e-3
@@ -428,7 +431,7 @@ def main():
                 "unit": "GB/s", "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
                 "algorithmic_bytes_per_launch": b, "launch_ms": kern_avg[dom],
                 "algorithmic_bytes_basis": "SURVEY.md §8(d): the bounded searches the oracle runs for the stage",
-                "traffic_source": os.path.relpath(args.traffic_json, ROOT) if traffic is not None else None}
+                "traffic_source": os.path.relpath(tpath, ROOT) if traffic is not None else None}
         if st == "transitions" and probe_bytes:
             # the index-probe algorithm's own bytes (what k_trans_sub must move)
             roof["index_probe_bytes_per_launch"] = probe_bytes

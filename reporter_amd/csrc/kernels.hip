@@ -3084,7 +3084,7 @@ int grid_for(int64_t n, int per_block, int cap) {
 
 // ============================================================== launchers
 constexpr int WAVE_GRID_CAP = 256 * 64;  // grid-stride cap for wave kernels
-constexpr int TRANS_GRID_CAP = 65536;  // k_trans_index waves (one per column, grid-striding beyond)
+constexpr int TRANS_GRID_CAP = 65536;  // k_trans_sub waves (one per column, grid-striding beyond)
 
 }  // namespace
 
@@ -3095,7 +3095,7 @@ void launch_fetch_scan(int32_t n, const int32_t* c0, const int32_t* c1, const in
 
 
 const char* const kKernelNames[KN_COUNT] = {
-    "k_columns",       "spatial_order",  "k_cand_lane",    "k_candidates",     "k_links",         "scan_trans_off",  "k_trans_index",
+    "k_columns",       "spatial_order",  "k_cand_lane",    "k_candidates",     "k_links",         "scan_trans_off",  "k_trans_sub",
     "k_trans_lane",    "k_transitions",  "k_transitions_big", "k_viterbi",      "k_route_index",   "k_route_lane",
     "k_route",         "k_route_big",    "k_seg_bound",      "scan_seg_bound",  "k_segments",       "k_report"};
 

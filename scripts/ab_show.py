@@ -1,5 +1,5 @@
 import glob, json, sys
-names = sys.argv[1:] or ["k_cand_lane", "k_trans_index", "k_route_index"]
+names = sys.argv[1:] or ["k_cand_lane", "k_trans_sub", "k_route_index"]
 for f in sorted(glob.glob("gpurun_out/ab/run*.json")):
     try:
         b = json.loads(open(f).read())

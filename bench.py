@@ -58,7 +58,7 @@ WORKLOAD = {
 # kernel -> (stage, main tier of the stage?)
 KERNEL_STAGE = {
     "k_columns": "columns", "spatial_order": "candidates", "k_cand_lane": "candidates", "k_candidates": "candidates", "k_links": "links_scan",
-    "scan_trans_off": "links_scan", "k_trans_sub": "transitions", "k_trans_lane": "transitions",
+    "scan_trans_off": "links_scan", "k_trans_sub": "transitions", "k_trans_wide": "transitions", "k_trans_lane": "transitions",
     "k_transitions": "transitions", "k_transitions_big": "transitions", "k_viterbi": "viterbi",
     "k_route_index": "route", "k_route_lane": "route", "k_route": "route", "k_route_big": "route",
     "k_seg_bound": "segments", "scan_seg_bound": "segments", "k_segments": "segments",

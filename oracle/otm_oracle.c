@@ -205,17 +205,20 @@ typedef struct {
   int32_t k;
 } hit;
 
+/* (sqdist, edge, offset): a node candidate (offset 0) sorts before an
+ * interior candidate of its representative edge at the same distance */
 static int hit_cmp(const void* a, const void* b) {
   const hit* x = (const hit*)a;
   const hit* y = (const hit*)b;
   if (x->sqd < y->sqd) return -1;
   if (x->sqd > y->sqd) return 1;
-  return (x->edge > y->edge) - (x->edge < y->edge);
+  if (x->edge != y->edge) return (x->edge > y->edge) - (x->edge < y->edge);
+  return (x->off > y->off) - (x->off < y->off);
 }
 
 /* projection of the probe (lat,lon) onto shape segment k of edge e */
 static void project(const orc_graph* g, int32_t e, int32_t k, float lat, float lon, float ls, float* sqd_out,
-                    float* off_out) {
+                    float* off_out, int* at_end) {
   const int32_t a = g->eshape[e] + k, b = a + 1;
   const float ax = (g->slon[a] - lon) * ls;
   const float ay = (g->slat[a] - lat) * MPD_F;
@@ -237,6 +240,8 @@ static void project(const orc_graph* g, int32_t e, int32_t k, float lat, float l
   const float len = g->elen[e];
   off = off > len ? len : off;
   *off_out = off;
+  /* clamped to the edge's last shape point: the projection is its end node */
+  *at_end = t == 1.0f && b == g->eshape[e + 1] - 1;
 }
 
 /* radius rule: max(search_radius, accuracy or gps_accuracy), capped */
@@ -274,7 +279,8 @@ static int candidates(const orc_graph* g, const orc_params* P, float lat, float 
           const uint32_t ent = g->cell_ent[q];
           const int32_t e = (int32_t)(ent >> 4), k = (int32_t)(ent & 15u);
           float sqd, off;
-          project(g, e, k, lat, lon, ls, &sqd, &off);
+          int at_end;
+          project(g, e, k, lat, lon, ls, &sqd, &off, &at_end);
           C->cell_entries_scanned++;
           if (!(sqd <= r2)) continue;
           int f = -1;
@@ -299,6 +305,36 @@ static int candidates(const orc_graph* g, const orc_params* P, float lat, float 
       }
     }
   }
+  /* node snap: an edge's best projection
+   * at its start node v (offset 0), or at its end node v when v has an
+   * outgoing edge, becomes the node candidate of v -- one per node, shared by
+   * all its edges, carried as (v's first outgoing edge, offset 0) at the
+   * smallest distance of the projections that snapped to it */
+  int nk = 0;
+  for (int h = 0; h < nh; ++h) {
+    const int32_t e = hits[h].edge;
+    float sqd, off;
+    int at_end;
+    project(g, e, hits[h].k, lat, lon, ls, &sqd, &off, &at_end);
+    hit x = hits[h];
+    x.off = off;
+    int32_t v = -1;
+    if (off == 0.0f) v = g->efrom[e];
+    else if (at_end && g->out_off[g->eto[e] + 1] > g->out_off[g->eto[e]]) v = g->eto[e];
+    if (v >= 0) {
+      x.edge = g->out_off[v];
+      x.off = 0.0f;
+      int f = -1;
+      for (int m = 0; m < nk; ++m)
+        if (hits[m].edge == x.edge && hits[m].off == 0.0f) f = m;
+      if (f >= 0) {
+        if (x.sqd < hits[f].sqd) hits[f].sqd = x.sqd;
+        continue;
+      }
+    }
+    hits[nk++] = x;
+  }
+  nh = nk;
   qsort(hits, (size_t)nh, sizeof(hit), hit_cmp);
   const int K = nh < P->max_candidates ? nh : P->max_candidates;
   const float ds = (2.0f * P->sigma_z) * P->sigma_z;
@@ -490,6 +526,16 @@ static void phase_a(batch* B, ws* w, int32_t t, orc_counters* C) {
 }
 
 /* ------------------------------------------------------------ S4 */
+/* A candidate at offset 0 is a node candidate (S2's node snap): its routes
+ * start at that node with nothing left to drive; an edge candidate's start at
+ * its edge's end node after the rest of the edge. */
+static int32_t src_node(const orc_graph* g, int32_t e, float off) { return off == 0.0f ? g->efrom[e] : g->eto[e]; }
+static float src_start(const orc_graph* g, int32_t e, float off) { return off == 0.0f ? 0.0f : g->elen[e] - off; }
+#define NO_HEAD 0xFFFFu /* a node candidate's side of a route: no turn */
+static uint32_t turn_cost_units(const batch* B, unsigned hin, unsigned hout) {
+  return (hin == NO_HEAD || hout == NO_HEAD) ? 0u : B->turn_units[orc_turn_deg(hin, hout)];
+}
+
 static int transitions(batch* B, ws* w, int64_t p, orc_counters* C) {
   const orc_graph* g = B->g;
   const int64_t q = B->col_prev[p];
@@ -505,7 +551,7 @@ static int transitions(batch* B, ws* w, int64_t p, orc_counters* C) {
   int32_t srcs[ORC_KMAX];
   int ns = 0;
   for (int i = 0; i < Kq; ++i) {
-    int32_t u = g->eto[eq[i]];
+    int32_t u = src_node(g, eq[i], oq[i]);
     int seen = 0;
     for (int s = 0; s < ns; ++s) seen |= srcs[s] == u;
     if (!seen) srcs[ns++] = u;
@@ -514,8 +560,8 @@ static int transitions(batch* B, ws* w, int64_t p, orc_counters* C) {
     const int32_t u = srcs[s];
     if (dijkstra(g, w, u, bound, C, 0) < 0) return -1;
     for (int i = 0; i < Kq; ++i) {
-      if (g->eto[eq[i]] != u) continue;
-      const float start = g->elen[eq[i]] - oq[i];
+      if (src_node(g, eq[i], oq[i]) != u) continue;
+      const float start = src_start(g, eq[i], oq[i]);
       for (int j = 0; j < Kp; ++j) {
         float r;
         if (ep[j] == eq[i] && op[j] >= oq[i]) {
@@ -529,17 +575,18 @@ static int transitions(batch* B, ws* w, int64_t p, orc_counters* C) {
         if (r <= bound) {
           /* turn cost of the route: the turns from e_i into the
              path, between its edges and into e_j, in integer 1/64 m units
-             (order-free, exact in a float below 2^24) */
+             (order-free, exact in a float below 2^24); a node candidate has
+             no heading, so no turn on its side */
           uint32_t units = 0;
           if (!(ep[j] == eq[i] && op[j] >= oq[i])) {
-            int32_t next = ep[j];
+            unsigned hn = op[j] == 0.0f ? NO_HEAD : g->ehead_out[ep[j]];
             for (int32_t x = g->efrom[ep[j]]; x != u;) {
               const int32_t e = w->pred[x];
-              units += B->turn_units[orc_turn_deg(g->ehead_in[e], g->ehead_out[next])];
-              next = e;
+              units += turn_cost_units(B, g->ehead_in[e], hn);
+              hn = g->ehead_out[e];
               x = g->efrom[e];
             }
-            units += B->turn_units[orc_turn_deg(g->ehead_in[eq[i]], g->ehead_out[next])];
+            units += turn_cost_units(B, oq[i] == 0.0f ? NO_HEAD : g->ehead_in[eq[i]], hn);
             if (units > TURN_UNITS_MAX) units = TURN_UNITS_MAX;
           }
           const float tc = (float)units * 0.015625f;
@@ -728,7 +775,7 @@ static int route_step(batch* B, ws* w, int64_t p, int32_t* path, int* plen, int*
   }
   *same = 0;
   const float bound = B->P->max_route_distance_factor * B->gc[p];
-  const int32_t u = g->eto[ei], v = g->efrom[ej];
+  const int32_t u = src_node(g, ei, oi), v = g->efrom[ej];
   if (dijkstra(g, w, u, bound, C, 1) < 0) return -1;
   int n = 0;
   for (int32_t x = v; x != u;) {
@@ -743,7 +790,7 @@ static int route_step(batch* B, ws* w, int64_t p, int32_t* path, int* plen, int*
   }
   *plen = n;
   C->route_edges += n;
-  const float start = g->elen[ei] - oi;
+  const float start = src_start(g, ei, oi);
   const float sd = start + w->dist[v];
   *R = sd + oj;
   return 0;
@@ -770,12 +817,13 @@ static int segments_of_trace(batch* B, ws* w, int32_t t, tres* R, orc_counters* 
     if (p < b && !is_state) continue;
     const int new_chain = p == b || B->chain_start[p];
     if (open && new_chain) {
-      /* close the open chain */
+      /* close the open chain; a chain ending on a node candidate ends at the
+         node: the traversal opened there never left it */
       const int32_t sl = B->state[lastp];
       cur.off1 = B->cand_off[lastp * ORC_KMAX + sl];
       cur.t1 = B->time[lastp];
       cur.sh1 = (int32_t)(lastp - a);
-      tpush(&T, cur);
+      if (cur.off1 != 0.0f) tpush(&T, cur);
       if (nstate >= 2) group_chain(B, R, &T);
       T.n = 0;
       open = 0;
@@ -809,13 +857,16 @@ static int segments_of_trace(batch* B, ws* w, int32_t t, tres* R, orc_counters* 
     const double ta = B->time[lastp], tb = B->time[p];
     const int32_t ca = (int32_t)(lastp - a), cb = (int32_t)(p - a);
     if (!same) {
+      /* close the traversal on the state's edge, unless the state is a node
+         candidate: its route starts at the node */
       const int32_t ei = cur.edge;
-      const float start = g->elen[ei] - B->cand_off[lastp * ORC_KMAX + B->state[lastp]];
+      const float oi = B->cand_off[lastp * ORC_KMAX + B->state[lastp]];
+      const float start = src_start(g, ei, oi);
       float x = start;
       cur.off1 = g->elen[ei];
       cur.t1 = time_at(ta, tb, x, Rd);
       cur.sh1 = x >= Rd ? cb : ca;
-      tpush(&T, cur);
+      if (oi != 0.0f) tpush(&T, cur);
       float dd = 0.0f;
       for (int k = 0; k < plen; ++k) {
         const int32_t pe = path[k];

@@ -105,6 +105,10 @@ static int auto_grid_mult(const otm_engine* E) {
 int engine_init(otm_engine* E, const char* graph_path, int device, std::string* err) {
   int rc = load_graph(graph_path, &E->host, err);
   if (rc) return rc;
+  if (E->host.h.n_edges >= (1 << 27)) {  // K2's lane-tier entries: edge << 4 below the node flag bit
+    *err = "graph: 2^27 or more edges";
+    return OTM_EINVAL;
+  }
   if (E->grid_mult == 0) E->grid_mult = auto_grid_mult(E);
   E->device = device;
   HIPCHK(hipSetDevice(device));
@@ -398,7 +402,7 @@ int build_index(otm_engine* E, std::string* err) {
   E->idx.row = rows;
   {
     IdxRow* erow = nullptr;
-    HIPCHK(hipMalloc(&erow, ((size_t)E->g.n_edges + 1) * sizeof(IdxRow)));
+    HIPCHK(hipMalloc(&erow, (2 * (size_t)E->g.n_edges + 1) * sizeof(IdxRow)));
     E->graph_allocs.push_back(erow);
     launch_edge_rows(E->g, rows, erow, s);
     HIPCHK(hipGetLastError());

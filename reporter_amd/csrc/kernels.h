@@ -84,7 +84,7 @@ struct IdxRow {
 struct DevIndex {
   float rmax;  // 0: no index
   const IdxRow* row;
-  const IdxRow* erow;    // per edge: the row of its end node (one round trip less from a candidate)
+  const IdxRow* erow;    // [2E]: per edge the row of its end node, then of its start node (node candidates)
   // {node (0xFFFFFFFF empty), D bits, turn units between the route's edges,
   //  head_out(first edge) | head_in(last edge) << 16 (0xFFFFFFFF: v == u)}
   const uint4* slot;
@@ -208,6 +208,7 @@ enum KernelId {
   KN_LINKS,
   KN_SCAN_TRANS,
   KN_TRANS_INDEX,
+  KN_TRANS_WIDE,
   KN_TRANS_LANE,
   KN_TRANS_WAVE,
   KN_TRANS_GLOBAL,

@@ -76,7 +76,7 @@ __device__ __forceinline__ float seg_sqdist(float alat, float alon, float blat, 
 }
 
 __device__ __forceinline__ void project(const DevGraph& g, int32_t e, int32_t k, float lat, float lon, float ls,
-                                        float& sqd, float& off_out) {
+                                        float& sqd, float& off_out, bool& at_end) {
   const int32_t a = g.e_shape_off[e] + k, b = a + 1;
   const float ax = (g.s_lon[a] - lon) * ls;
   const float ay = (g.s_lat[a] - lat) * MPD_F;
@@ -97,6 +97,25 @@ __device__ __forceinline__ void project(const DevGraph& g, int32_t e, int32_t k,
   float off = g.s_cum[a] + t * (g.s_cum[b] - g.s_cum[a]);
   const float len = g.e_len[e];
   off_out = off > len ? len : off;
+  // clamped to the edge's last shape point: the projection is its end node
+  at_end = t == 1.0f && b == g.e_shape_off[e + 1] - 1;
+}
+__device__ __forceinline__ void project(const DevGraph& g, int32_t e, int32_t k, float lat, float lon, float ls,
+                                        float& sqd, float& off_out) {
+  bool at_end;
+  project(g, e, k, lat, lon, ls, sqd, off_out, at_end);
+}
+// node snap: the node an edge's best projection snaps to -- its
+// start node at offset 0, its end node when clamped there and the node has an
+// outgoing edge -- or -1.  The node candidate is carried as (the node's first
+// outgoing edge, offset 0).
+__device__ __forceinline__ int32_t snap_node(const DevGraph& g, int32_t e, float off, bool at_end) {
+  if (off == 0.0f) return g.e_from[e];
+  if (at_end) {
+    const int32_t v = g.e_to[e];
+    if (g.out_off[v + 1] > g.out_off[v]) return v;
+  }
+  return -1;
 }
 
 __device__ __forceinline__ float probe_radius(const DevParams& P, float acc) {
@@ -129,6 +148,30 @@ __device__ __forceinline__ float trans_cost(uint32_t units, float r, float gcv, 
   const float tc = (float)units * 0.015625f;
   const float diff = fabsf(r - gcv);
   return (tc + diff) / beta;
+}
+
+// ============================================================== node candidates
+// DESIGN.md §3 node snap: a candidate at offset 0 is the node candidate of its
+// edge's start node (K2 snaps every end-of-edge projection to the node, so
+// an edge candidate never sits at offset 0).  Its routes start at the node
+// with nothing left to drive, and it has no heading on its side of a route.
+constexpr uint32_t NO_HEAD = 0xFFFFu;
+__device__ __forceinline__ bool cand_node(float off) { return off == 0.0f; }
+__device__ __forceinline__ int32_t src_node(const DevGraph& g, int32_t e, float off) {
+  return cand_node(off) ? g.e_from[e] : g.e_to[e];
+}
+__device__ __forceinline__ float src_start(const DevGraph& g, int32_t e, float off) {
+  return cand_node(off) ? 0.0f : g.e_len[e] - off;
+}
+__device__ __forceinline__ uint32_t src_head(const DevGraph& g, int32_t e, float off) {
+  return cand_node(off) ? NO_HEAD : (uint32_t)g.e_head_in[e];
+}
+__device__ __forceinline__ uint32_t dst_head(const DevGraph& g, int32_t e, float off) {
+  return cand_node(off) ? NO_HEAD : (uint32_t)g.e_head_out[e];
+}
+// turn units of one turn (none when either side is a node candidate)
+__device__ __forceinline__ uint32_t turn_units(const uint32_t* TU, uint32_t hin, uint32_t hout) {
+  return (hin == NO_HEAD || hout == NO_HEAD) ? 0u : TU[turn_deg(hin, hout)];
 }
 
 // wave-wide inclusive scan of an int (64 lanes)
@@ -399,6 +442,9 @@ __device__ __forceinline__ ItemRange item_range(const DevWork& w, const DevBatch
 
 // ============================================================== K2 candidates
 constexpr int HCAP = 512;  // edge hash slots (>= 2 * MAX_HITS)
+// a lane-tier entry that is a node candidate (edge << 4 keeps bits 4..30:
+// graphs up to 2^27 edges, checked at engine load)
+constexpr uint32_t NODE_ENT = 0x80000000u;
 #ifndef OTM_CAND_LANE_CAP
 #define OTM_CAND_LANE_CAP 8
 #endif
@@ -549,16 +595,44 @@ __global__ __launch_bounds__(CAND_TB, OTM_CAND_WAVES) void k_cand_lane(DevGraph 
       w.overflow_list0[slot] = (int32_t)p;
       continue;
     }
+    // node snap: an entry whose projection snaps to a node becomes that
+    // node's candidate (NODE_ENT | first outgoing edge << 4), one per node
+    // at the smallest distance
+    for (int m = 0; m < n; ++m) {
+      const uint32_t em = E[m * S];
+      const int32_t e = (int32_t)(em >> 4);
+      float sqd, off;
+      bool at_end;
+      project(g, e, (int32_t)(em & 15u), lat, lon, ls, sqd, off, at_end);
+      const int32_t v = snap_node(g, e, off, at_end);
+      if (v < 0) continue;
+      const uint32_t key = NODE_ENT | ((uint32_t)g.out_off[v] << 4);
+      int f = -1;
+      for (int t = 0; t < m; ++t)
+        if (E[t * S] == key) f = t;
+      if (f >= 0) {
+        const float qm = Q[m * S];
+        if (qm < Q[f * S]) Q[f * S] = qm;
+        --n;  // drop entry m: the last entry moves here and is examined next
+        E[m * S] = E[n * S];
+        Q[m * S] = Q[n * S];
+        --m;
+        continue;
+      }
+      E[m * S] = key;
+    }
     const int K = n < P.max_candidates ? n : P.max_candidates;
     const float ds = (2.0f * P.sigma_z) * P.sigma_z;
     for (int j = 0; j < K; ++j) {
+      // selection by (sqdist, edge, node before edge candidate)
       int m = j;
       float qm = Q[j * S];
       uint32_t em = E[j * S];
       for (int t = j + 1; t < n; ++t) {
         const float qt = Q[t * S];
         const uint32_t et = E[t * S];
-        if (qt < qm || (qt == qm && (et >> 4) < (em >> 4))) {
+        const uint32_t xt = (et & ~NODE_ENT) >> 4, xm = (em & ~NODE_ENT) >> 4;
+        if (qt < qm || (qt == qm && (xt < xm || (xt == xm && et > em)))) {
           m = t;
           qm = qt;
           em = et;
@@ -570,9 +644,9 @@ __global__ __launch_bounds__(CAND_TB, OTM_CAND_WAVES) void k_cand_lane(DevGraph 
         Q[j * S] = qm;
         E[j * S] = em;
       }
-      const int32_t e = (int32_t)(em >> 4);
-      float sqd, off;
-      project(g, e, (int32_t)(em & 15u), lat, lon, ls, sqd, off);
+      const int32_t e = (int32_t)((em & ~NODE_ENT) >> 4);
+      float sqd = qm, off = 0.0f;
+      if (!(em & NODE_ENT)) project(g, e, (int32_t)(em & 15u), lat, lon, ls, sqd, off);
       w.cand_edge[CSTRIDE * (p * KMAX + j)] = e;
       w.cand_off[CSTRIDE * (p * KMAX + j)] = off;
       w.cand_emis[CSTRIDE * (p * KMAX + j)] = sqd / ds;
@@ -694,18 +768,65 @@ __global__ __launch_bounds__(TB) void k_candidates(DevGraph g, DevBatch b, DevPa
       __syncthreads();
       continue;
     }
-    // compact the distinct edges: key = sqdist bits << 32 | edge
+    // compact the distinct edges as sqdist bits << 32 | edge << 5 | shape
+    // segment << 1; the edge table is then reused as the node table.  Each
+    // edge is projected once, lane-parallel over the compacted list: an edge
+    // candidate gets flag bit 1; one whose projection snaps to a node leaves
+    // LAB_NONE (sorts last) and meets the other edges at that node in the node
+    // table (key: the node's first outgoing edge; value: the smallest sqdist
+    // bits << 32 | a slot of the group), which writes the node candidate
+    // sqdist bits << 32 | first outgoing edge << 5 into that slot -- so a node
+    // sorts before an edge candidate of the same edge at the same distance.
     for (int i = lane; i < HCAP; i += TB) {
       if (hkey[i] != EMPTY) {
         const int idx = atomicAdd(&s_n, 1);
-        skey[idx] = (hval[i] & 0xFFFFFFFF00000000ull) | (unsigned long long)hkey[i];
+        skey[idx] = (hval[i] & 0xFFFFFFFF00000000ull) | ((unsigned long long)hkey[i] << 5) | ((hval[i] & 15ull) << 1);
       }
     }
     __syncthreads();
-    const int n = s_n;
+    for (int i = lane; i < HCAP; i += TB) {
+      hkey[i] = EMPTY;
+      hval[i] = LAB_NONE;
+    }
+    if (lane == 0) s_count = 0;  // from here: distinct candidates
+    __syncthreads();
+    const int n0 = s_n;
+    for (int idx = lane; idx < n0; idx += TB) {
+      const unsigned long long key = skey[idx];
+      const int32_t e = (int32_t)(((uint32_t)key) >> 5);
+      float sqd, off;
+      bool at_end;
+      project(g, e, (int32_t)((key >> 1) & 15ull), lat, lon, ls, sqd, off, at_end);
+      const int32_t v = snap_node(g, e, off, at_end);
+      if (v < 0) {
+        skey[idx] = key | 1ull;
+        atomicAdd(&s_count, 1);
+      } else {
+        skey[idx] = LAB_NONE;
+        const uint32_t rep = (uint32_t)g.out_off[v];
+        uint32_t slot = hash32(rep) >> (32 - 9);
+        while (true) {
+          const uint32_t old = atomicCAS(&hkey[slot], EMPTY, rep);
+          if (old == EMPTY || old == rep) break;
+          slot = (slot + 1) & (HCAP - 1);
+        }
+        atomicMin(&hval[slot], (key & 0xFFFFFFFF00000000ull) | (unsigned long long)idx);
+      }
+    }
+    __syncthreads();
+    for (int i = lane; i < HCAP; i += TB) {
+      if (hkey[i] != EMPTY) {
+        const unsigned long long hv = hval[i];
+        skey[(int)(hv & 0xFFFFull)] = (hv & 0xFFFFFFFF00000000ull) | ((unsigned long long)hkey[i] << 5);
+        atomicAdd(&s_count, 1);
+      }
+    }
+    __syncthreads();
+    const int ns = n0;  // entries in skey (snapped edges past their node's slot: LAB_NONE)
+    const int n = s_count;  // distinct candidates
     int N = 1;
-    while (N < n) N <<= 1;
-    for (int i = n + lane; i < N; i += TB) skey[i] = LAB_NONE;
+    while (N < ns) N <<= 1;
+    for (int i = ns + lane; i < N; i += TB) skey[i] = LAB_NONE;
     __syncthreads();
     // bitonic sort ascending
     for (int kk = 2; kk <= N; kk <<= 1) {
@@ -727,12 +848,9 @@ __global__ __launch_bounds__(TB) void k_candidates(DevGraph g, DevBatch b, DevPa
     const int K = n < P.max_candidates ? n : P.max_candidates;
     if (lane < K) {
       const unsigned long long key = skey[lane];
-      const int32_t e = (int32_t)(key & 0xFFFFFFFFull);
-      uint32_t slot = hash32((uint32_t)e) >> (32 - 9);
-      while (hkey[slot] != (uint32_t)e) slot = (slot + 1) & (HCAP - 1);
-      const int32_t kseg = (int32_t)(hval[slot] & 15ull);
-      float sqd, off;
-      project(g, e, kseg, lat, lon, ls, sqd, off);
+      const int32_t e = (int32_t)(((uint32_t)key) >> 5);
+      float sqd = bitsf((uint32_t)(key >> 32)), off = 0.0f;
+      if (key & 1ull) project(g, e, (int32_t)((key >> 1) & 15ull), lat, lon, ls, sqd, off);
       const float ds = (2.0f * P.sigma_z) * P.sigma_z;
       w.cand_edge[CSTRIDE * (p * KMAX + lane)] = e;
       w.cand_off[CSTRIDE * (p * KMAX + lane)] = off;
@@ -1072,10 +1190,10 @@ __global__ __launch_bounds__(LANE_TB) void k_trans_lane(DevGraph g, DevBatch b, 
     unsigned long long s_search = 0, s_settled = 0, s_relaxed = 0, s_trans = 0;
     bool failed = false;
     for (int i = 0; i < Kq && !failed; ++i) {
-      const int32_t u = g.e_to[eq[CSTRIDE * (i)]];
+      const int32_t u = src_node(g, eq[CSTRIDE * (i)], oq[CSTRIDE * (i)]);
       bool first = true;
       for (int k = 0; k < i; ++k)
-        if (g.e_to[eq[CSTRIDE * (k)]] == u) {
+        if (src_node(g, eq[CSTRIDE * (k)], oq[CSTRIDE * (k)]) == u) {
           first = false;
           break;
         }
@@ -1090,9 +1208,9 @@ __global__ __launch_bounds__(LANE_TB) void k_trans_lane(DevGraph g, DevBatch b, 
       s_settled += (unsigned long long)n;
       s_relaxed += rel;
       for (int ii = i; ii < Kq; ++ii) {
-        if (g.e_to[eq[CSTRIDE * (ii)]] != u) continue;
+        if (src_node(g, eq[CSTRIDE * (ii)], oq[CSTRIDE * (ii)]) != u) continue;
         const int32_t ei = eq[CSTRIDE * (ii)];
-        const float start = g.e_len[ei] - oq[CSTRIDE * (ii)];
+        const float start = src_start(g, ei, oq[CSTRIDE * (ii)]);
         for (int j = 0; j < Kp; ++j) {
           const int32_t ej = ep[CSTRIDE * (j)];
           float r;
@@ -1116,14 +1234,14 @@ __global__ __launch_bounds__(LANE_TB) void k_trans_lane(DevGraph g, DevBatch b, 
             // the route's turns, walked back from e_j's start node to u
             uint32_t units = 0;
             if (!same) {
-              int32_t next = ej;
+              uint32_t hn = dst_head(g, ej, op[CSTRIDE * (j)]);
               while ((K[f * LANE_TB] & ~DONE) != (uint32_t)u) {
                 const int32_t e = Pd[f * LANE_TB];
-                units += P.turn_units[turn_deg(g.e_head_in[e], g.e_head_out[next])];
-                next = e;
+                units += turn_units(P.turn_units, g.e_head_in[e], hn);
+                hn = g.e_head_out[e];
                 f = lane_find<CAP>(K, n, (uint32_t)g.e_from[e]);
               }
-              units += P.turn_units[turn_deg(g.e_head_in[ei], g.e_head_out[next])];
+              units += turn_units(P.turn_units, src_head(g, ei, oq[CSTRIDE * (ii)]), hn);
             }
             cost = trans_cost(units, r, gcv, P.beta);
             ++s_trans;
@@ -1173,7 +1291,7 @@ __global__ __launch_bounds__(LANE_TB) void k_route_lane(DevGraph g, DevBatch b, 
     const int32_t ei = w.cand_edge[CSTRIDE * ((int64_t)q * KMAX + i)], ej = w.cand_edge[CSTRIDE * (p * KMAX + j)];
     const float oi = w.cand_off[CSTRIDE * ((int64_t)q * KMAX + i)], oj = w.cand_off[CSTRIDE * (p * KMAX + j)];
     const float bound = P.factor * w.gc[p];
-    const int32_t u = g.e_to[ei], v = g.e_from[ej];
+    const int32_t u = src_node(g, ei, oi), v = g.e_from[ej];
     unsigned long long rel = 0;
     const int n = lane_search<CAP, true>(g, K, D, Pd, u, bound, rel);
     if (n < 0) {
@@ -1202,7 +1320,7 @@ __global__ __launch_bounds__(LANE_TB) void k_route_lane(DevGraph g, DevBatch b, 
       w.path_off[p] = off;
       w.path_len[p] = len;
     }
-    const float start = g.e_len[ei] - oi;
+    const float start = src_start(g, ei, oi);
     const float sd = start + D[fv * LANE_TB];
     w.route_dist[p] = sd + oj;
     ++c_search;
@@ -1237,6 +1355,9 @@ __device__ __forceinline__ uint32_t idx_hash(uint32_t v) {
 #endif
 #ifndef OTM_IDX_EROW
 #define OTM_IDX_EROW 1
+#endif
+#ifndef OTM_IDX_EROW_SRC
+#define OTM_IDX_EROW_SRC 1
 #endif
 __host__ __device__ __forceinline__ int64_t idx_row_cap(int32_t c) {
   if (c <= 0) return 0;
@@ -1286,8 +1407,8 @@ __device__ __forceinline__ int64_t idx_find(const DevIndex& X, const IdxRow& R, 
 // turn units of the route e_i -> (index route u -> v) -> e_j from v's slot
 __device__ __forceinline__ uint32_t idx_turn_units(const uint32_t* TU, const uint4& sl, uint32_t hin_i,
                                                    uint32_t hout_j) {
-  if (sl.w == NO_TURNS) return TU[turn_deg(hin_i, hout_j)];
-  return TU[turn_deg(hin_i, sl.w & 0xFFFFu)] + sl.z + TU[turn_deg(sl.w >> 16, hout_j)];
+  if (sl.w == NO_TURNS) return turn_units(TU, hin_i, hout_j);
+  return turn_units(TU, hin_i, sl.w & 0xFFFFu) + sl.z + turn_units(TU, sl.w >> 16, hout_j);
 }
 
 // Index build: one wavefront per source node u runs the bounded search with
@@ -1368,12 +1489,20 @@ __global__ void k_row_pack(const int32_t* row_cnt, const int64_t* row_off, IdxRo
 // occupancy.  Columns with more pairs than S loop within their group; columns
 // the index cannot answer (bound > rmax, a source row incomplete, more than
 // KC candidates) go to the search tiers.
-template <int S>
+// At 8 lanes per column (8 columns per wave) a column with more than
+// OTM_TRANS_KC8 candidates on either side goes to the wide list
+// (w.overflow_list2, count w.counters_i32[6]), which a 16-lane pass (LIST)
+// then answers from the index; KC8 keeps the LDS words within 8 waves per SIMD.
+#ifndef OTM_TRANS_KC8
+#define OTM_TRANS_KC8 8
+#endif
+template <int S, bool LIST>
 __global__ __launch_bounds__(TB, 8) void k_trans_sub(DevGraph g, DevBatch b, DevParams P, DevWork w) {
   if (*w.abort) return;  // a capacity was exceeded: the host redoes the batch
   constexpr int NS = TB / S;
   // a pair reads its target and source as one 16-byte LDS word each
-  constexpr int KC = 16;
+  constexpr int KC = S >= 16 ? 16 : OTM_TRANS_KC8;
+  constexpr bool WIDE = KC < 16;
   __shared__ int4 tg[NS][KC];  // target: edge, offset bits, from-node, start heading
   __shared__ int4 sr[NS][KC];  // source: edge, offset bits, remaining-length bits, end heading
   __shared__ IdxRow rq[NS][KC];
@@ -1383,9 +1512,13 @@ __global__ __launch_bounds__(TB, 8) void k_trans_sub(DevGraph g, DevBatch b, Dev
   for (int k = lane; k < TURN_TABLE; k += TB) TU[k] = P.turn_units[k];
   const DevIndex& X = w.idx;
   unsigned long long c_search = 0, c_settled = 0, c_relaxed = 0, c_trans = 0;
-  const bool ordered = (P.order_mask & ORDER_TRANS) != 0;
+  const bool ordered = !LIST && (P.order_mask & ORDER_TRANS) != 0;
   int64_t base, end, stride;
-  if (ordered) {
+  if (LIST) {
+    base = (int64_t)blockIdx.x * NS;
+    end = w.counters_i32[6];
+    stride = (int64_t)gridDim.x * NS;
+  } else if (ordered) {
     const int grp = blockIdx.x % ORDER_GROUPS;
     base = w.ord.grp[grp] + (int64_t)(blockIdx.x / ORDER_GROUPS) * NS;
     end = w.ord.grp[grp + 1];
@@ -1399,7 +1532,7 @@ __global__ __launch_bounds__(TB, 8) void k_trans_sub(DevGraph g, DevBatch b, Dev
     const int64_t it = base + sg;
     bool act = it < end;
     int64_t p = 0;
-    if (act) p = ordered ? (int64_t)w.ord.item[it] : it;
+    if (act) p = LIST ? (int64_t)w.overflow_list2[it] : (ordered ? (int64_t)w.ord.item[it] : it);
     const int32_t q = act ? w.col_prev[p] : -1;
     act = act && q >= 0;
     int Kp = 0, Kq = 0;
@@ -1413,23 +1546,31 @@ __global__ __launch_bounds__(TB, 8) void k_trans_sub(DevGraph g, DevBatch b, Dev
     }
     const float bound = P.factor * gcv;
     const bool idx_ok = X.rmax > 0.0f && bound <= X.rmax;
+    const bool wide = WIDE && act && idx_ok && (Kp > KC || Kq > KC);
+    if (wide && sl == 0) w.overflow_list2[atomicAdd(&w.counters_i32[6], 1)] = (int32_t)p;
+    act = act && !wide;
     bool bad = act && (!idx_ok || Kp > KC || Kq > KC);
     // candidates of p (targets) and of q (sources), then edges, then rows
     for (int k = sl; k < KC; k += S) {
       if (act && k < Kp) {
         const int32_t e = w.cand_edge[CSTRIDE * (p * KMAX + k)];
-        tg[sg][k] = make_int4(e, __float_as_int(w.cand_off[CSTRIDE * (p * KMAX + k)]), g.e_from[e],
-                              (int)g.e_head_out[e]);
+        const float o = w.cand_off[CSTRIDE * (p * KMAX + k)];
+        tg[sg][k] = make_int4(e, __float_as_int(o), g.e_from[e], (int)dst_head(g, e, o));
       }
       if (act && k < Kq) {
         const int32_t e = w.cand_edge[CSTRIDE * ((int64_t)q * KMAX + k)];
         const float o = w.cand_off[CSTRIDE * ((int64_t)q * KMAX + k)];
-        sr[sg][k] = make_int4(e, __float_as_int(o), __float_as_int(g.e_len[e] - o), (int)g.e_head_in[e]);
+        sr[sg][k] = make_int4(e, __float_as_int(o), __float_as_int(src_start(g, e, o)), (int)src_head(g, e, o));
         if (idx_ok) {
 #if OTM_IDX_EROW
-          const IdxRow R = X.erow[e];
+#if OTM_IDX_EROW_SRC
+          // erow[e]: the row of e's end node; erow[E + e]: of its start node
+          const IdxRow R = X.erow[cand_node(o) ? (int64_t)g.n_edges + e : (int64_t)e];
 #else
-          const IdxRow R = X.row[g.e_to[e]];
+          const IdxRow R = cand_node(o) ? X.row[g.e_from[e]] : X.erow[e];
+#endif
+#else
+          const IdxRow R = X.row[src_node(g, e, o)];
 #endif
           rq[sg][k] = R;
           bad = bad || R.cnt < 0;
@@ -1606,8 +1747,7 @@ __global__ __launch_bounds__(256, OTM_ROUTE_WAVES) void k_route_index(DevGraph g
       continue;
     }
     const float bound = P.factor * w.gc[p];
-    const int32_t u = g.e_to[ei], v = g.e_from[ej];
-    const float len_i = g.e_len[ei];
+    const int32_t u = src_node(g, ei, oi), v = g.e_from[ej];
     float Dv = 0.0f;
     IdxRow R{};
     int64_t sv = -1;
@@ -1649,7 +1789,7 @@ __global__ __launch_bounds__(256, OTM_ROUTE_WAVES) void k_route_index(DevGraph g
       w.path_off[p] = off;
       w.path_len[p] = len;
     }
-    const float start = len_i - oi;
+    const float start = src_start(g, ei, oi);
     const float sd = start + Dv;
     w.route_dist[p] = sd + oj;
     if (w.ctr) {
@@ -1721,7 +1861,7 @@ __global__ __launch_bounds__(TB) void k_transitions(DevGraph g, DevBatch b, DevP
     }
     __syncthreads();
     // distinct source nodes (first occurrence order)
-    const int32_t u_l = lane < Kq ? g.e_to[eq[lane]] : -1;
+    const int32_t u_l = lane < Kq ? src_node(g, eq[lane], oq[lane]) : -1;
     bool first = lane < Kq;
     for (int k = 0; k < Kq; ++k) {
       const int32_t uk = __shfl(u_l, k, 64);
@@ -1745,9 +1885,9 @@ __global__ __launch_bounds__(TB) void k_transitions(DevGraph g, DevBatch b, DevP
       unsigned long long ntr = 0;
       for (int idx = lane; idx < Kq * Kp; idx += TB) {
         const int i = idx / Kp, j = idx - (idx / Kp) * Kp;
-        if (g.e_to[eq[i]] != u) continue;
+        if (src_node(g, eq[i], oq[i]) != u) continue;
         const int32_t ei = eq[i], ej = ep[j];
-        const float start = g.e_len[ei] - oq[i];
+        const float start = src_start(g, ei, oq[i]);
         float r;
         bool ok = true;
         const bool same = ej == ei && op[j] >= oq[i];
@@ -1769,15 +1909,15 @@ __global__ __launch_bounds__(TB) void k_transitions(DevGraph g, DevBatch b, DevP
           // the route's turns, walked back over the converged labels
           uint32_t units = 0;
           if (!same) {
-            int32_t next = ej;
+            uint32_t hn = dst_head(g, ej, op[j]);
             for (int32_t x = g.e_from[ej]; x != u;) {
               const int sx = table_find<BIG>(T, (uint32_t)x);
               const int32_t e = (int32_t)(uint32_t)(Mem<BIG>::ld(&T.lab[sx]) & 0xFFFFFFFFull);
-              units += P.turn_units[turn_deg(g.e_head_in[e], g.e_head_out[next])];
-              next = e;
+              units += turn_units(P.turn_units, g.e_head_in[e], hn);
+              hn = g.e_head_out[e];
               x = g.e_from[e];
             }
-            units += P.turn_units[turn_deg(g.e_head_in[ei], g.e_head_out[next])];
+            units += turn_units(P.turn_units, src_head(g, ei, oq[i]), hn);
           }
           cost = trans_cost(units, r, gcv, P.beta);
           ++ntr;
@@ -2209,7 +2349,7 @@ __global__ __launch_bounds__(TB) void k_route(DevGraph g, DevBatch b, DevParams 
       continue;
     }
     const float bound = P.factor * w.gc[p];
-    const int32_t u = g.e_to[ei], v = g.e_from[ej];
+    const int32_t u = src_node(g, ei, oi), v = g.e_from[ej];
     const int settled = wave_search<BIG>(g, T, S, u, bound, lane);
     if (settled < 0) {
       if (lane == 0) {
@@ -2251,7 +2391,7 @@ __global__ __launch_bounds__(TB) void k_route(DevGraph g, DevBatch b, DevParams 
         w.path_off[p] = off;
         w.path_len[p] = n;
       }
-      const float start = g.e_len[ei] - oi;
+      const float start = src_start(g, ei, oi);
       const float sd = start + D;
       w.route_dist[p] = sd + oj;
       if (w.ctr) {
@@ -2423,7 +2563,9 @@ __device__ void segments_trace(const DevGraph& g, const DevWork& w, DevOut& o, i
       cur.t1 = S.time(lastp);
       cur.sh1 = lastp;
       if (nstate >= 2) {
-        em.push(cur);
+        // a chain ending on a node candidate ends at the node: the traversal
+        // opened there never left it
+        if (!cand_node(cur.off1)) em.push(cur);
         em.flush();
       }
       open = false;
@@ -2449,13 +2591,15 @@ __device__ void segments_trace(const DevGraph& g, const DevWork& w, DevOut& o, i
     const float oi = S.off(lastp);
     const bool same = ei == ej && oj >= oi;
     if (!same) {
+      // close the traversal on the state's edge, unless the state is a node
+      // candidate: its route starts at the node
       const float elen = cur.at.len;  // == e_len[ei]
-      const float start = elen - oi;
+      const float start = cand_node(oi) ? 0.0f : elen - oi;
       float x = start;
       cur.off1 = elen;
       cur.t1 = time_at(ta, tb, x, Rd);
       cur.sh1 = x >= Rd ? cb : ca;
-      em.push(cur);
+      if (!cand_node(oi)) em.push(cur);
       float dd = 0.0f;
       const int32_t po = S.poff(p), pl = S.plen(p);
       for (int k = 0; k < pl; ++k) {
@@ -2632,7 +2776,7 @@ __global__ __launch_bounds__(TB) void k_segments(DevGraph g, DevBatch b, DevWork
           } else {
             const float Rd = w.route_dist[a + r.pl];
             const double ta = b.time[a + r.lp], tb = b.time[a + r.pl];
-            const float start = g.e_len[r.ei] - r.oi;
+            const float start = src_start(g, r.ei, r.oi);
             float dd = 0.0f;
             for (int i = 0; i < r.plen; ++i) dd = dd + g.e_len[w.path_pool[r.poff + i]];
             const float x = start + dd;
@@ -2641,7 +2785,10 @@ __global__ __launch_bounds__(TB) void k_segments(DevGraph g, DevBatch b, DevWork
             S.o_sh0[k] = (int16_t)(x >= Rd ? r.pl : r.lp);
           }
         }
-        nem = (r.step && !r.same ? 1 + r.plen : 0) + (r.last && !r.cs ? 1 : 0);
+        // the close of the open traversal (none from a node candidate), the
+        // route's edges, the chain's final close (none at a node candidate)
+        nem = (r.step && !r.same ? (cand_node(r.oi) ? 0 : 1) + r.plen : 0) +
+              (r.last && !r.cs && !cand_node(r.oj) ? 1 : 0);
       }
       const int ch = c_chain + wave_incl_scan(cs, lane);
       int lo = wave_incl_max(opener, lane);
@@ -2677,17 +2824,19 @@ __global__ __launch_bounds__(TB) void k_segments(DevGraph g, DevBatch b, DevWork
         const float Rd = w.route_dist[a + r.pl];
         const double ta = b.time[a + r.lp], tb = b.time[a + r.pl];
         const float elen = g.e_len[r.ei];
-        const float start = elen - r.oi;
-        const int jo = S.lopen[k - 1];
-        S.t_edge[slot] = r.ei;
-        S.t_off0[slot] = S.o_off0[jo];
-        S.t_t0[slot] = S.o_t0[jo];
-        S.t_sh0[slot] = S.o_sh0[jo];
-        S.t_off1[slot] = elen;
-        S.t_t1[slot] = time_at(ta, tb, start, Rd);
-        S.t_sh1[slot] = (int16_t)(start >= Rd ? r.pl : r.lp);
-        S.t_chain[slot] = chk;
-        ++slot;
+        const float start = src_start(g, r.ei, r.oi);
+        if (!cand_node(r.oi)) {
+          const int jo = S.lopen[k - 1];
+          S.t_edge[slot] = r.ei;
+          S.t_off0[slot] = S.o_off0[jo];
+          S.t_t0[slot] = S.o_t0[jo];
+          S.t_sh0[slot] = S.o_sh0[jo];
+          S.t_off1[slot] = elen;
+          S.t_t1[slot] = time_at(ta, tb, start, Rd);
+          S.t_sh1[slot] = (int16_t)(start >= Rd ? r.pl : r.lp);
+          S.t_chain[slot] = chk;
+          ++slot;
+        }
         float dd = 0.0f;
         for (int i = 0; i < r.plen; ++i) {
           const int32_t pe = w.path_pool[r.poff + i];
@@ -2706,7 +2855,7 @@ __global__ __launch_bounds__(TB) void k_segments(DevGraph g, DevBatch b, DevWork
           ++slot;
         }
       }
-      if (r.last && !r.cs) {
+      if (r.last && !r.cs && !cand_node(r.oj)) {
         const int jo = S.lopen[k];
         S.t_edge[slot] = r.ej;
         S.t_off0[slot] = S.o_off0[jo];
@@ -3096,7 +3245,7 @@ void launch_fetch_scan(int32_t n, const int32_t* c0, const int32_t* c1, const in
 
 const char* const kKernelNames[KN_COUNT] = {
     "k_columns",       "spatial_order",  "k_cand_lane",    "k_candidates",     "k_links",         "scan_trans_off",  "k_trans_sub",
-    "k_trans_lane",    "k_transitions",  "k_transitions_big", "k_viterbi",      "k_route_index",   "k_route_lane",
+    "k_trans_wide",    "k_trans_lane",    "k_transitions",  "k_transitions_big", "k_viterbi",      "k_route_index",   "k_route_lane",
     "k_route",         "k_route_big",    "k_seg_bound",      "scan_seg_bound",  "k_segments",       "k_report"};
 
 namespace {
@@ -3107,6 +3256,7 @@ constexpr int LANE_CAP = 24;        // route stage: 12 B per slot
 constexpr int LANE_CAP_TRANS = 24;  // transitions: 12 B per slot (predecessors give the route's turns)
 constexpr int SPILL_GRID = 4096;
 constexpr int LANE_GRID = 2048;
+constexpr int WIDE_GRID = 2048;  // k_trans_sub's wide-column pass (grid-strides over its list)
 }  // namespace
 
 #define TIMED(k, launch) \
@@ -3173,18 +3323,27 @@ void launch_transitions(const DevGraph& g, const DevBatch& b, const DevParams& p
   static const char* genv = std::getenv("OTM_TRANS_GRID");
   static const int sub = [] {
     const char* e = std::getenv("OTM_TRANS_SUB");
-    const int v = e ? std::atoi(e) : 16;
-    return v == 16 || v == 32 ? v : 64;
+    const int v = e ? std::atoi(e) : 8;
+    return v == 8 || v == 16 || v == 32 ? v : 64;
   }();
   const int per = TB / sub;  // columns per wave step
   const int grid = genv ? std::max(ORDER_GROUPS, std::atoi(genv) / ORDER_GROUPS * ORDER_GROUPS)
                         : order_grid((b.n_points + per - 1) / per, 1, TRANS_GRID_CAP);
-  if (sub == 32)
-    TIMED(KN_TRANS_INDEX, hipLaunchKernelGGL(k_trans_sub<32>, dim3(grid), dim3(TB), 0, s, g, b, p, w));
-  else if (sub == 16)
-    TIMED(KN_TRANS_INDEX, hipLaunchKernelGGL(k_trans_sub<16>, dim3(grid), dim3(TB), 0, s, g, b, p, w));
-  else
-    TIMED(KN_TRANS_INDEX, hipLaunchKernelGGL(k_trans_sub<64>, dim3(grid), dim3(TB), 0, s, g, b, p, w));
+  if (sub == 8) {
+    // 8 lanes per column over the columns of <= OTM_TRANS_KC8 candidates a
+    // side, then 16 lanes over the wide rest (a list filled on the device)
+    TIMED(KN_TRANS_INDEX, hipLaunchKernelGGL((k_trans_sub<8, false>), dim3(grid), dim3(TB), 0, s, g, b, p, w));
+    TIMED(KN_TRANS_WIDE, hipLaunchKernelGGL((k_trans_sub<16, true>), dim3(WIDE_GRID), dim3(TB), 0, s, g, b, p, w));
+  } else {
+    if (sub == 32)
+      TIMED(KN_TRANS_INDEX, hipLaunchKernelGGL((k_trans_sub<32, false>), dim3(grid), dim3(TB), 0, s, g, b, p, w));
+    else if (sub == 16)
+      TIMED(KN_TRANS_INDEX, hipLaunchKernelGGL((k_trans_sub<16, false>), dim3(grid), dim3(TB), 0, s, g, b, p, w));
+    else
+      TIMED(KN_TRANS_INDEX, hipLaunchKernelGGL((k_trans_sub<64, false>), dim3(grid), dim3(TB), 0, s, g, b, p, w));
+    mk.begin(KN_TRANS_WIDE, s);
+    mk.end(KN_TRANS_WIDE, s);
+  }
   TIMED(KN_TRANS_LANE, hipLaunchKernelGGL(k_trans_lane<LANE_CAP_TRANS>, dim3(LANE_GRID), dim3(LANE_TB), 0, s, g, b,
                                           p, w));
   TIMED(KN_TRANS_WAVE, hipLaunchKernelGGL(k_transitions<false>, dim3(SPILL_GRID), dim3(TB), 0, s, g, b, p, w, 0));
@@ -3234,7 +3393,7 @@ void launch_report(const DevBatch& b, const DevReportCfg& rc, DevWork& w, DevOut
   // blocks spread the traces over more waves (env OTM_REPORT_TB)
   static const int tb = [] {
     const char* e = std::getenv("OTM_REPORT_TB");
-    const int v = e ? std::atoi(e) : 16;  // 0.053 -> 0.050 ms against 64 on config 2
+    const int v = e ? std::atoi(e) : 8;  // 0.053 -> 0.050 ms against 64 on config 2
     return v == 16 || v == 32 || v == 64 || v == 128 ? v : 16;
   }();
   TIMED(KN_REPORT, hipLaunchKernelGGL(k_report, dim3(grid_for(b.n_traces, tb, 1 << 30)), dim3(tb), 0, s, b, rc, w,
@@ -3258,7 +3417,10 @@ void launch_row_sizes(const int32_t* row_cnt, int64_t* row_sizes, int32_t n, hip
 }
 __global__ void k_edge_rows(DevGraph g, const IdxRow* rows, IdxRow* erow) {
   const int32_t e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e < g.n_edges) erow[e] = rows[g.e_to[e]];
+  if (e < g.n_edges) {
+    erow[e] = rows[g.e_to[e]];
+    erow[(int64_t)g.n_edges + e] = rows[g.e_from[e]];  // node candidates' source rows
+  }
 }
 void launch_edge_rows(const DevGraph& g, const IdxRow* rows, IdxRow* erow, hipStream_t s) {
   hipLaunchKernelGGL(k_edge_rows, dim3(grid_for((int64_t)g.n_edges, 256, 1 << 30)), dim3(256), 0, s, g, rows, erow);

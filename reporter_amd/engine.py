@@ -232,7 +232,9 @@ class Engine(object):
 
     def kernel_ms(self):
         """Per-kernel times (ms) of the last timed match_device call, by kernel name."""
-        n = 19
+        n = 0
+        while lib().otm_kernel_name(n):
+            n += 1
         ms = (C.c_float * n)()
         _check(lib().otm_get_kernel_ms(self.h, ms, n))
         return {lib().otm_kernel_name(k).decode(): ms[k] for k in range(n)}

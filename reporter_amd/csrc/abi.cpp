@@ -262,6 +262,14 @@ int otm_engine_create(const char* cfg_path, const int* devices, int ndev, otm_en
     delete E;
     return fail(OTM_EINVAL, "grid_mult must be in [0 (auto), 64]");
   }
+  const Value* tl = o->get("trans_lanes");
+  if (tl && tl->kind == Kind::Int) E->trans_lanes = (int)tl->i;
+  if (const char* v = std::getenv("OTM_TRANS_SUB")) E->trans_lanes = std::atoi(v);  // A/B override
+  if (E->trans_lanes != 4 && E->trans_lanes != 8 && E->trans_lanes != 16 && E->trans_lanes != 32 &&
+      E->trans_lanes != 64) {
+    delete E;
+    return fail(OTM_EINVAL, "trans_lanes must be 4, 8, 16, 32 or 64");
+  }
   const Value* meili = cfg.get("meili");
   const Value* dflt = meili ? meili->get("default") : nullptr;
   if (dflt && dflt->kind == Kind::Obj) {

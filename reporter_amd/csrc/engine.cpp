@@ -278,6 +278,7 @@ int engine_clone(const otm_engine* P, otm_engine* C, std::string* err) {
   C->index_incomplete_rows = P->index_incomplete_rows;
   C->index_build_ms = P->index_build_ms;
   C->small_points = P->small_points;
+  C->trans_lanes = P->trans_lanes;
   C->mc = P->mc;
   C->rc = P->rc;
   C->dp = P->dp;
@@ -589,7 +590,7 @@ static int engine_match_once(otm_engine* E, const DevBatch& b, hipStream_t s, st
   w.big_lab = P<unsigned long long>(E->big_lab);
   w.big_inq = P<uint32_t>(E->big_inq);
   w.big_fr = P<uint32_t>(E->big_fr);
-  launch_transitions(E->g, b, dp, w, s, mk);
+  launch_transitions(E->g, b, dp, w, s, mk, E->trans_lanes);
   // spill snapshot B: columns per transition tier (Viterbi does not touch
   // the counters; they start over for the route tiers)
   launch_snap(w.counters_i32, P<int32_t>(E->snap) + 16, true, s);

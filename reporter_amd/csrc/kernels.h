@@ -245,7 +245,7 @@ void launch_cap_check(const DevBatch& b, DevWork& w, hipStream_t s);
 // lane tier -> wave LDS tier -> global tier, spill lists on the device
 // (counters_i32[0] / [3] must be zero on entry)
 void launch_transitions(const DevGraph& g, const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s,
-                        const Marks& mk);
+                        const Marks& mk, int sub);
 void launch_viterbi(const DevBatch& b, DevWork& w, hipStream_t s, const Marks& mk);
 void launch_route(const DevGraph& g, const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s,
                   const Marks& mk);

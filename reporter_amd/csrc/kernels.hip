@@ -1496,12 +1496,15 @@ __global__ void k_row_pack(const int32_t* row_cnt, const int64_t* row_off, IdxRo
 #ifndef OTM_TRANS_KC8
 #define OTM_TRANS_KC8 8
 #endif
+#ifndef OTM_TRANS_KC4
+#define OTM_TRANS_KC4 6
+#endif
 template <int S, bool LIST>
 __global__ __launch_bounds__(TB, 8) void k_trans_sub(DevGraph g, DevBatch b, DevParams P, DevWork w) {
   if (*w.abort) return;  // a capacity was exceeded: the host redoes the batch
   constexpr int NS = TB / S;
   // a pair reads its target and source as one 16-byte LDS word each
-  constexpr int KC = S >= 16 ? 16 : OTM_TRANS_KC8;
+  constexpr int KC = S >= 16 ? 16 : (S == 8 ? OTM_TRANS_KC8 : OTM_TRANS_KC4);
   constexpr bool WIDE = KC < 16;
   __shared__ int4 tg[NS][KC];  // target: edge, offset bits, from-node, start heading
   __shared__ int4 sr[NS][KC];  // source: edge, offset bits, remaining-length bits, end heading
@@ -3316,23 +3319,23 @@ void launch_cap_check(const DevBatch& b, DevWork& w, hipStream_t s) {
   hipLaunchKernelGGL(k_cap_check, dim3(1), dim3(1), 0, s, b, w);
 }
 void launch_transitions(const DevGraph& g, const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s,
-                        const Marks& mk) {
+                        const Marks& mk, int sub) {
   // many more waves than fit at once (each column is a few dependent
   // round trips): measured 0.78 ms at 16K waves, 0.67 ms at 64K; a grid of
   // one resident round was slowest (0.92 ms, partial rounds at 7 waves/SIMD)
   static const char* genv = std::getenv("OTM_TRANS_GRID");
-  static const int sub = [] {
-    const char* e = std::getenv("OTM_TRANS_SUB");
-    const int v = e ? std::atoi(e) : 8;
-    return v == 8 || v == 16 || v == 32 ? v : 64;
-  }();
+  // sub: lanes per column (engine trans_lanes)
   const int per = TB / sub;  // columns per wave step
   const int grid = genv ? std::max(ORDER_GROUPS, std::atoi(genv) / ORDER_GROUPS * ORDER_GROUPS)
                         : order_grid((b.n_points + per - 1) / per, 1, TRANS_GRID_CAP);
-  if (sub == 8) {
-    // 8 lanes per column over the columns of <= OTM_TRANS_KC8 candidates a
-    // side, then 16 lanes over the wide rest (a list filled on the device)
-    TIMED(KN_TRANS_INDEX, hipLaunchKernelGGL((k_trans_sub<8, false>), dim3(grid), dim3(TB), 0, s, g, b, p, w));
+  if (sub <= 8) {
+    // 8 (4) lanes per column over the columns of <= OTM_TRANS_KC8 (KC4)
+    // candidates a side, then 16 lanes over the wide rest (a list filled on
+    // the device)
+    if (sub == 4)
+      TIMED(KN_TRANS_INDEX, hipLaunchKernelGGL((k_trans_sub<4, false>), dim3(grid), dim3(TB), 0, s, g, b, p, w));
+    else
+      TIMED(KN_TRANS_INDEX, hipLaunchKernelGGL((k_trans_sub<8, false>), dim3(grid), dim3(TB), 0, s, g, b, p, w));
     TIMED(KN_TRANS_WIDE, hipLaunchKernelGGL((k_trans_sub<16, true>), dim3(WIDE_GRID), dim3(TB), 0, s, g, b, p, w));
   } else {
     if (sub == 32)

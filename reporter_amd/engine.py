@@ -26,13 +26,15 @@ def _check(rc):
         raise OtmError("libotmatch error %d: %s" % (rc, _lib.last_error()))
 
 
-def write_config(path, graph_path, index_radius_m=None, grid_mult=None, **meili):
+def write_config(path, graph_path, index_radius_m=None, grid_mult=None, trans_lanes=None, **meili):
     """Write an engine config: {"otm":{"graph":...,"index_radius_m":R},"meili":{"default":{...}}}."""
     otm = {"graph": os.path.abspath(graph_path)}
     if index_radius_m is not None:
         otm["index_radius_m"] = index_radius_m
     if grid_mult is not None:
         otm["grid_mult"] = grid_mult
+    if trans_lanes is not None:
+        otm["trans_lanes"] = trans_lanes
     cfg = {"otm": otm, "meili": {"default": meili}}
     with open(path, "w") as f:
         json.dump(cfg, f)
@@ -50,7 +52,8 @@ class Results(object):
 
 
 class Engine(object):
-    def __init__(self, config_path=None, graph_path=None, device=0, index_radius_m=None, grid_mult=None, **meili):
+    def __init__(self, config_path=None, graph_path=None, device=0, index_radius_m=None, grid_mult=None,
+                 trans_lanes=None, **meili):
         """Either a config file (valhalla.Configure-style) or a graph path."""
         L = lib()
         self._tmp = None
@@ -60,7 +63,7 @@ class Engine(object):
             fd, self._tmp = tempfile.mkstemp(suffix=".json", prefix="otm_cfg_")
             os.close(fd)
             config_path = write_config(self._tmp, graph_path, index_radius_m=index_radius_m, grid_mult=grid_mult,
-                                       **meili)
+                                       trans_lanes=trans_lanes, **meili)
         h = C.c_void_p()
         dev = (C.c_int * 1)(device)
         rc = L.otm_engine_create(config_path.encode(), dev, 1, C.byref(h))

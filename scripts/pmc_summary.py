@@ -37,7 +37,7 @@ def short(name):
              "k_route<false>": "k_route", "k_route<true>": "k_route_big", "k_segments<true>": "k_segments",
              "k_segments<128, 256>": "k_segments", "k_segments<256, 512>": "k_segments_large",
              # the transition index tier's launch slot (otm_kernel_name) runs one of these forms
-             "k_trans_sub<8, false>": "k_trans_sub", "k_trans_sub<16, false>": "k_trans_sub",
+             "k_trans_sub<4, false>": "k_trans_sub", "k_trans_sub<8, false>": "k_trans_sub", "k_trans_sub<16, false>": "k_trans_sub",
              "k_trans_sub<32, false>": "k_trans_sub", "k_trans_sub<64, false>": "k_trans_sub",
              "k_trans_sub<16, true>": "k_trans_wide"}
     return alias.get(n, n)

@@ -59,9 +59,10 @@ def _stage_compare(eng, orc, batch):
 
 
 def _run_both(graph, batch, oracle, results_equal, meili=None, stages=True, counters=True, index_radius_m=None,
-              grid_mult=None):
+              grid_mult=None, trans_lanes=None):
     meili = meili or {}
-    with Engine(graph_path=graph, index_radius_m=index_radius_m, grid_mult=grid_mult, **meili) as eng:
+    with Engine(graph_path=graph, index_radius_m=index_radius_m, grid_mult=grid_mult, trans_lanes=trans_lanes,
+                **meili) as eng:
         eng.set_counting(counters)
         res = eng.match(batch)
         p = oracle.params(**meili)
@@ -93,6 +94,40 @@ def test_city_sample_sigma15(small_graph, oracle, results_equal, batch_path, rad
     res, orc = _run_both(small_graph, b, oracle, results_equal, index_radius_m=radius, grid_mult=grid_mult)
     assert (res.traces["code"] == 200).mean() > 0.95
     assert len(res.segments) > 1000 and len(res.reports) > 50
+
+
+@pytest.mark.parametrize("lanes", [4, 8, 16, 32, 64])
+def test_transition_lanes(small_graph, oracle, results_equal, lanes):
+    # k_trans_sub at 8 lanes per column runs two passes (columns of more than
+    # OTM_TRANS_KC8 candidates a side go to a 16-lane pass over a device list);
+    # 16 / 32 / 64 lanes run one.  Node candidates merge edges, so K varies
+    # per column and both passes see work here.
+    b = synth.make_traces(small_graph, 200, 100, interval_s=5.0, noise_sigma_m=15.0, accuracy=15.0, seed=23)
+    res, orc = _run_both(small_graph, b, oracle, results_equal, trans_lanes=lanes)
+    k = orc["ncand"]
+    assert k.max() > 8 and (k > 0).mean() > 0.9
+
+
+def test_node_candidates(small_graph, oracle, results_equal):
+    # SURVEY Appendix B's node snap: end-of-edge projections merge into one
+    # candidate per node, carried at offset 0 on the node's first outgoing
+    # edge; routes start there with no turn on its side, and a chain never
+    # emits a traversal for the edge that only carries a node candidate
+    b = synth.make_traces(small_graph, 100, 100, interval_s=5.0, noise_sigma_m=15.0, accuracy=15.0, seed=29)
+    res, orc = _run_both(small_graph, b, oracle, results_equal)
+    P = len(b["lat"])
+    k = orc["ncand"]
+    off = orc["cand_off"].reshape(P, -1)
+    edge = orc["cand_edge"].reshape(P, -1)
+    node = np.zeros(off.shape, bool)
+    for p in range(P):
+        node[p, :k[p]] = off[p, :k[p]] == 0.0
+        nodes = edge[p, :k[p]][node[p, :k[p]]]
+        assert len(np.unique(nodes)) == len(nodes)  # one candidate per node
+    assert node.sum() > 0.05 * k.sum()
+    st = orc["state"]
+    m = st >= 0
+    assert (off[np.nonzero(m)[0], st[m]] == 0.0).mean() > 0.02  # matched node states occur
 
 
 def _auto_index_radius(graph_path, factor=5.0, breakage=2000.0):

@@ -111,6 +111,36 @@ def test_oracle_loads_graph_and_matches(small_graph, oracle):
     assert c["points"] == len(b["lat"]) and c["searches"] > 0 and c["nodes_settled"] >= c["searches"]
 
 
+def test_oracle_node_candidates(small_graph, oracle):
+    # node snap: a node candidate sits at offset 0 on its node's
+    # first outgoing edge, one per node per point; candidates come in
+    # distance order
+    import struct
+    raw = np.fromfile(small_graph, dtype=np.uint8)
+    hs = struct.calcsize("<8sII4i2iq3d4dQ")
+
+    def sec(i, dt):
+        o, n = struct.unpack_from("<QQ", raw, hs + 16 * i)
+        return np.frombuffer(raw, dtype=dt, count=n // np.dtype(dt).itemsize, offset=o)
+    out_off, efrom = sec(2, np.int32), sec(3, np.int32)
+    b = synth.make_traces(small_graph, 40, 80, seed=5)
+    r = oracle.match_batch(oracle.Graph(small_graph), b, keep_stages=True)
+    P = len(b["lat"])
+    k = r["ncand"]
+    e = r["cand_edge"].reshape(P, 32)
+    o = r["cand_off"].reshape(P, 32)
+    q = r["cand_emis"].reshape(P, 32)
+    n_node = 0
+    for p in range(P):
+        ee, oo, qq = e[p, :k[p]], o[p, :k[p]], q[p, :k[p]]
+        nd = ee[oo == 0.0]
+        n_node += len(nd)
+        assert len(np.unique(nd)) == len(nd)
+        assert np.array_equal(nd, out_off[efrom[nd]])
+        assert np.all(np.diff(qq) >= 0)  # (sqdist order; emission = sqdist / 2 sigma^2 can merge ulps)
+    assert n_node > 0.05 * k.sum()
+
+
 def test_oracle_json_path_config1(small_graph, oracle):
     """Config 1 plumbing: synthesize_gps traces -> handle_request -> 200s."""
     g = oracle.Graph(small_graph)

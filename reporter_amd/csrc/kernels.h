@@ -56,7 +56,10 @@ struct DevGraph {
 // which the dispatcher deals to one XCD, so each XCD's L2 holds one region's
 // grid cells and index rows; inside a group, neighbouring lanes and waves get
 // neighbouring probes.
-constexpr int ORDER_BITS = 6;
+#ifndef OTM_ORDER_BITS
+#define OTM_ORDER_BITS 6
+#endif
+constexpr int ORDER_BITS = OTM_ORDER_BITS;  // <= 8: tile ids are u16
 constexpr int ORDER_SIDE = 1 << ORDER_BITS;  // 64 x 64 tiles
 constexpr int ORDER_TILES = ORDER_SIDE * ORDER_SIDE;
 constexpr int ORDER_GROUPS = 8;

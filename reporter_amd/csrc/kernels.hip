@@ -75,6 +75,37 @@ __device__ __forceinline__ float seg_sqdist(float alat, float alon, float blat, 
   return px * px + py * py;
 }
 
+// seg_sqdist for the scan of K2's lane tier: INFINITY when the segment's
+// line is already farther than the radius (|cross| / |v| > r, with a 1 %
+// margin that rounding cannot cross), so most entries skip the division and
+// clamp; the rest get seg_sqdist's value, bit for bit.
+#ifndef OTM_CAND_PREFILTER
+#define OTM_CAND_PREFILTER 0
+#endif
+__device__ __forceinline__ float seg_sqdist_r2(float alat, float alon, float blat, float blon, float lat, float lon,
+                                               float ls, float r2) {
+  const float ax = (alon - lon) * ls;
+  const float ay = (alat - lat) * MPD_F;
+  const float bx = (blon - lon) * ls;
+  const float by = (blat - lat) * MPD_F;
+  const float vx = bx - ax;
+  const float vy = by - ay;
+  const float l2 = vx * vx + vy * vy;
+#if OTM_CAND_PREFILTER
+  const float cr = ax * vy - ay * vx;
+  if (cr * cr > 1.01f * r2 * l2) return INFINITY;
+#endif
+  float t = 0.0f;
+  if (l2 > 0.0f) {
+    const float dot = ax * vx + ay * vy;
+    t = -dot / l2;
+    t = t < 0.0f ? 0.0f : (t > 1.0f ? 1.0f : t);
+  }
+  const float px = ax + t * vx;
+  const float py = ay + t * vy;
+  return px * px + py * py;
+}
+
 __device__ __forceinline__ void project(const DevGraph& g, int32_t e, int32_t k, float lat, float lon, float ls,
                                         float& sqd, float& off_out, bool& at_end) {
   const int32_t a = g.e_shape_off[e] + k, b = a + 1;
@@ -546,7 +577,7 @@ __global__ __launch_bounds__(CAND_TB, OTM_CAND_WAVES) void k_cand_lane(DevGraph 
             if (q + u < q1) {
               const float4 G = g.ent_geo[q + u];
               en[u] = g.cell_ent[q + u];
-              sq[u] = seg_sqdist(G.x, G.y, G.z, G.w, lat, lon, ls);
+              sq[u] = seg_sqdist_r2(G.x, G.y, G.z, G.w, lat, lon, ls, r2);
             }
           }
 #pragma unroll

@@ -262,6 +262,13 @@ int otm_engine_create(const char* cfg_path, const int* devices, int ndev, otm_en
     delete E;
     return fail(OTM_EINVAL, "grid_mult must be in [0 (auto), 64]");
   }
+  const Value* cl = o->get("cand_lanes");
+  if (cl && cl->kind == Kind::Int) E->cand_lanes = (int)cl->i;
+  if (const char* v = std::getenv("OTM_CAND_LANES")) E->cand_lanes = std::atoi(v);  // A/B override
+  if (E->cand_lanes != 1 && E->cand_lanes != 4 && E->cand_lanes != 8 && E->cand_lanes != 16) {
+    delete E;
+    return fail(OTM_EINVAL, "cand_lanes must be 1, 4, 8 or 16");
+  }
   const Value* tl = o->get("trans_lanes");
   if (tl && tl->kind == Kind::Int) E->trans_lanes = (int)tl->i;
   if (const char* v = std::getenv("OTM_TRANS_SUB")) E->trans_lanes = std::atoi(v);  // A/B override

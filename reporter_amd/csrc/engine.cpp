@@ -279,6 +279,7 @@ int engine_clone(const otm_engine* P, otm_engine* C, std::string* err) {
   C->index_build_ms = P->index_build_ms;
   C->small_points = P->small_points;
   C->trans_lanes = P->trans_lanes;
+  C->cand_lanes = P->cand_lanes;
   C->mc = P->mc;
   C->rc = P->rc;
   C->dp = P->dp;
@@ -572,7 +573,7 @@ static int engine_match_once(otm_engine* E, const DevBatch& b, hipStream_t s, st
     mk.begin(KN_ORDER, s);
     mk.end(KN_ORDER, s);
   }
-  launch_candidates(E->g, b, dp, w, s, mk);
+  launch_candidates(E->g, b, dp, w, s, mk, E->cand_lanes);
   // spill snapshot A: candidate probes the lane tier handed to the wave tier;
   // the counters start over for the transition tiers (links, scan and the
   // capacity check do not touch them)

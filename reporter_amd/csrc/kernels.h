@@ -241,7 +241,7 @@ struct Marks {
 void launch_columns(const DevGraph& g, const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s,
                     const Marks& mk);
 void launch_candidates(const DevGraph& g, const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s,
-                       const Marks& mk);
+                       const Marks& mk, int lanes);
 void launch_links(const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s, const Marks& mk);
 // sets *w.abort when the scanned transition total exceeds w.trans_cap
 void launch_cap_check(const DevBatch& b, DevWork& w, hipStream_t s);

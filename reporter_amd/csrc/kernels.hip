@@ -694,6 +694,211 @@ __global__ __launch_bounds__(CAND_TB, OTM_CAND_WAVES) void k_cand_lane(DevGraph 
   }
 }
 
+// Sub-group tier: G lanes per probe, CAND_TB / G probes per block.  A probe's
+// lanes take interleaved entries of each grid row (G consecutive 16-byte
+// geometry words per step: a line or two per probe per load instead of a
+// line per lane -- the lane tier is bound by its divergent gathers in the
+// texture addresser), and keep each edge's best (sqdist, shape segment) in the
+// probe's LDS hash table with 64-bit atomicMin.  Then each lane projects its
+// slots once: edge candidates and node candidates (the node snap) get the
+// wave tier's sort keys, duplicate nodes keep their smallest key, and every
+// surviving key's rank among the probe's keys is its candidate slot.  A probe
+// with more than CAND_SUB_CAP distinct edges goes to the wave tier.
+constexpr int CAND_SUB_HS = 16;   // table slots per probe
+constexpr int CAND_SUB_CAP = 12;  // distinct edges before the wave tier
+template <int G>
+__global__ __launch_bounds__(CAND_TB, OTM_CAND_WAVES) void k_cand_sub(DevGraph g, DevBatch b, DevParams P, DevWork w) {
+  constexpr int NPB = CAND_TB / G;
+  constexpr int HS = CAND_SUB_HS;
+  constexpr int SPL = HS / G;  // slots per lane
+  __shared__ uint32_t tK[NPB][HS];
+  __shared__ unsigned long long tV[NPB][HS];
+  __shared__ unsigned long long tS[NPB][HS];  // sort keys (~0: none)
+  __shared__ int tN[NPB];                     // distinct edges; > HS: table overflow
+  const int sg = threadIdx.x / G, sl = threadIdx.x % G;
+  unsigned long long c_cells = 0, c_ent = 0, c_cand = 0;
+  const bool ordered = (P.order_mask & ORDER_CAND) != 0;
+  int64_t base, end, stride;
+  if (ordered) {
+    const int grp = blockIdx.x % ORDER_GROUPS;
+    base = w.ord.grp[grp] + (int64_t)(blockIdx.x / ORDER_GROUPS) * NPB;
+    end = w.ord.grp[grp + 1];
+    stride = (int64_t)(gridDim.x / ORDER_GROUPS) * NPB;
+  } else {
+    base = (int64_t)blockIdx.x * NPB;
+    end = b.n_points;
+    stride = (int64_t)gridDim.x * NPB;
+  }
+  const float ds = (2.0f * P.sigma_z) * P.sigma_z;
+  for (; base < end; base += stride) {
+    const int64_t it = base + sg;
+    bool act = it < end;
+    int64_t p = 0;
+    if (act) p = ordered ? (int64_t)w.ord.item[it] : it;
+    if (act && !ordered) act = w.is_col[p] != 0;
+    if (act && P.cand_wave_all) {
+      if (sl == 0) w.overflow_list0[atomicAdd(&w.counters_i32[5], 1)] = (int32_t)p;
+      act = false;
+    }
+#pragma unroll
+    for (int u = 0; u < SPL; ++u) {
+      tK[sg][sl + u * G] = EMPTY;
+      tV[sg][sl + u * G] = LAB_NONE;
+    }
+    if (sl == 0) tN[sg] = 0;
+    __syncthreads();
+    float lat = 0.0f, lon = 0.0f, ls = 1.0f;
+    unsigned long long my_cells = 0, my_ents = 0;
+    if (act) {
+      const float4 pr = w.probe[p];  // {lat, lon, accuracy} of the column (K1)
+      lat = pr.x;
+      lon = pr.y;
+      const float r = probe_radius(P, pr.z);
+      const float r2 = r * r;
+      ls = MPD_F * cos_deg(lat);
+      const float dlat = r / MPD_F;
+      const float dlon = r / ls;
+      const double la_lo = ((double)lat - (double)dlat - g.lat0) / g.cell;
+      const double la_hi = ((double)lat + (double)dlat - g.lat0) / g.cell;
+      const double lo_lo = ((double)lon - (double)dlon - g.lon0) / g.cell;
+      const double lo_hi = ((double)lon + (double)dlon - g.lon0) / g.cell;
+      const double R = g.grid_rows, Cn = g.grid_cols;
+      int r0 = 0, r1 = -1, c0 = 0, c1 = -1;
+      if (!(la_hi < 0.0 || lo_hi < 0.0 || la_lo >= R || lo_lo >= Cn)) {
+        r0 = la_lo < 0.0 ? 0 : (int)floor(la_lo);
+        r1 = la_hi >= R ? (int)R - 1 : (int)floor(la_hi);
+        c0 = lo_lo < 0.0 ? 0 : (int)floor(lo_lo);
+        c1 = lo_hi >= Cn ? (int)Cn - 1 : (int)floor(lo_hi);
+      }
+      unsigned long long ents = 0;
+      for (int rr = r0; rr <= r1; ++rr) {
+        const size_t rbase = (size_t)rr * (size_t)g.grid_cols;
+        const int64_t q0 = g.cell_off[rbase + c0], q1 = g.cell_off[rbase + c1 + 1];
+        ents += (unsigned long long)(q1 - q0);
+        for (int64_t q = q0 + sl; q < q1; q += 2 * G) {
+          // two entries per lane in flight: q and q + G
+          float sq[2];
+          uint32_t en[2];
+#pragma unroll
+          for (int u = 0; u < 2; ++u) {
+            sq[u] = INFINITY;
+            en[u] = 0;
+            if (q + u * G < q1) {
+              const float4 Gm = g.ent_geo[q + u * G];
+              en[u] = g.cell_ent[q + u * G];
+              sq[u] = seg_sqdist(Gm.x, Gm.y, Gm.z, Gm.w, lat, lon, ls);
+            }
+          }
+#pragma unroll
+          for (int u = 0; u < 2; ++u) {
+            if (!(sq[u] <= r2)) continue;
+            const uint32_t e = en[u] >> 4;
+            uint32_t h = hash32(e) >> 28;  // HS = 16
+            int probe = 0;
+            for (; probe < HS; ++probe) {
+              const uint32_t old = atomicCAS(&tK[sg][h], EMPTY, e);
+              if (old == EMPTY) atomicAdd(&tN[sg], 1);
+              if (old == EMPTY || old == e) break;
+              h = (h + 1) & (HS - 1);
+            }
+            if (probe == HS) {
+              atomicOr(&tN[sg], 0x10000);  // full table: the wave tier takes the probe
+              continue;
+            }
+            atomicMin(&tV[sg][h], ((unsigned long long)fbits(sq[u]) << 32) | (unsigned long long)(en[u] & 15u));
+          }
+        }
+      }
+      my_cells = (unsigned long long)(r1 - r0 + 1) * (unsigned long long)(c1 - c0 + 1);
+      my_ents = ents;
+    }
+    __syncthreads();
+    const int nd = act ? tN[sg] : 0;
+    if (act && nd > CAND_SUB_CAP) {  // (the wave tier counts its probes' work)
+      if (sl == 0) w.overflow_list0[atomicAdd(&w.counters_i32[5], 1)] = (int32_t)p;
+      act = false;
+    }
+    if (act && sl == 0) {
+      c_cells += my_cells;
+      c_ent += my_ents;
+    }
+    // each lane: project its slots once; sort keys as the wave tier's
+    unsigned long long key[SPL];
+    float offv[SPL];
+#pragma unroll
+    for (int u = 0; u < SPL; ++u) {
+      key[u] = LAB_NONE;
+      offv[u] = 0.0f;
+      const int s = sl + u * G;
+      const uint32_t e = tK[sg][s];
+      if (act && e != EMPTY) {
+        const unsigned long long v = tV[sg][s];
+        float sqd, off;
+        bool at_end;
+        project(g, (int32_t)e, (int32_t)(v & 15ull), lat, lon, ls, sqd, off, at_end);
+        const int32_t nv = snap_node(g, (int32_t)e, off, at_end);
+        const unsigned long long qb = v & 0xFFFFFFFF00000000ull;
+        if (nv < 0) {
+          key[u] = qb | ((unsigned long long)e << 5) | ((v & 15ull) << 1) | 1ull;
+          offv[u] = off;
+        } else {
+          key[u] = qb | ((unsigned long long)(uint32_t)g.out_off[nv] << 5);
+        }
+      }
+      tS[sg][s] = key[u];
+    }
+    __syncthreads();
+    // duplicate nodes (same first outgoing edge): the smallest key, then the lowest slot, stays
+    bool alive[SPL];
+#pragma unroll
+    for (int u = 0; u < SPL; ++u) {
+      const int s = sl + u * G;
+      alive[u] = key[u] != LAB_NONE;
+      if (alive[u] && !(key[u] & 1ull)) {
+        const unsigned long long rep = key[u] & 0xFFFFFFFFull;
+        for (int t2 = 0; t2 < HS; ++t2) {
+          const unsigned long long o = tS[sg][t2];
+          if (t2 != s && o != LAB_NONE && (o & 0xFFFFFFFFull) == rep && (o < key[u] || (o == key[u] && t2 < s)))
+            alive[u] = false;
+        }
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < SPL; ++u)
+      if (!alive[u]) tS[sg][sl + u * G] = LAB_NONE;
+    __syncthreads();
+    // rank among the probe's surviving keys = candidate slot
+    int nal = 0;
+#pragma unroll
+    for (int u = 0; u < SPL; ++u) nal += alive[u] ? 1 : 0;
+#pragma unroll
+    for (int o = 1; o < G; o <<= 1) nal += __shfl_xor(nal, o, 64);
+    const int K = nal < P.max_candidates ? nal : P.max_candidates;
+#pragma unroll
+    for (int u = 0; u < SPL; ++u) {
+      if (!alive[u]) continue;
+      int rank = 0;
+      for (int t2 = 0; t2 < HS; ++t2) rank += tS[sg][t2] < key[u] ? 1 : 0;
+      if (rank >= K) continue;
+      const int32_t e = (int32_t)(((uint32_t)key[u]) >> 5);
+      w.cand_edge[CSTRIDE * (p * KMAX + rank)] = e;
+      w.cand_off[CSTRIDE * (p * KMAX + rank)] = offv[u];
+      w.cand_emis[CSTRIDE * (p * KMAX + rank)] = bitsf((uint32_t)(key[u] >> 32)) / ds;
+    }
+    if (act && sl == 0) {
+      w.ncand[p] = K;
+      c_cand += (unsigned long long)K;
+    }
+    __syncthreads();
+  }
+  if (w.ctr) {
+    wave_cadd(&w.ctr->cells_visited, c_cells);
+    wave_cadd(&w.ctr->cell_entries_scanned, c_ent);
+    wave_cadd(&w.ctr->candidates, c_cand);
+  }
+}
+
 // Wave tier: one wavefront per spilled probe (list from the lane tier).
 __global__ __launch_bounds__(TB) void k_candidates(DevGraph g, DevBatch b, DevParams P, DevWork w) {
   __shared__ uint32_t hkey[HCAP];
@@ -3327,9 +3532,20 @@ void launch_order(const DevBatch& b, DevWork& w, hipStream_t s, const Marks& mk)
 }
 
 void launch_candidates(const DevGraph& g, const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s,
-                       const Marks& mk) {
-  TIMED(KN_CAND_LANE, hipLaunchKernelGGL(k_cand_lane, dim3(order_grid(b.n_points, CAND_TB, 1 << 30)), dim3(CAND_TB),
-                                         0, s, g, b, p, w));
+                       const Marks& mk, int lanes) {
+  // lanes per probe: 1 = the lane tier, 4 / 8 / 16 = the sub-group tier
+  if (lanes == 4)
+    TIMED(KN_CAND_LANE, hipLaunchKernelGGL(k_cand_sub<4>, dim3(order_grid(b.n_points, CAND_TB / 4, 1 << 30)),
+                                           dim3(CAND_TB), 0, s, g, b, p, w));
+  else if (lanes == 8)
+    TIMED(KN_CAND_LANE, hipLaunchKernelGGL(k_cand_sub<8>, dim3(order_grid(b.n_points, CAND_TB / 8, 1 << 30)),
+                                           dim3(CAND_TB), 0, s, g, b, p, w));
+  else if (lanes == 16)
+    TIMED(KN_CAND_LANE, hipLaunchKernelGGL(k_cand_sub<16>, dim3(order_grid(b.n_points, CAND_TB / 16, 1 << 30)),
+                                           dim3(CAND_TB), 0, s, g, b, p, w));
+  else
+    TIMED(KN_CAND_LANE, hipLaunchKernelGGL(k_cand_lane, dim3(order_grid(b.n_points, CAND_TB, 1 << 30)),
+                                           dim3(CAND_TB), 0, s, g, b, p, w));
   TIMED(KN_CAND_WAVE, hipLaunchKernelGGL(k_candidates, dim3(4096), dim3(TB), 0, s, g, b, p, w));
 }
 void launch_links(const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s, const Marks& mk) {

@@ -59,10 +59,10 @@ def _stage_compare(eng, orc, batch):
 
 
 def _run_both(graph, batch, oracle, results_equal, meili=None, stages=True, counters=True, index_radius_m=None,
-              grid_mult=None, trans_lanes=None):
+              grid_mult=None, trans_lanes=None, cand_lanes=None):
     meili = meili or {}
     with Engine(graph_path=graph, index_radius_m=index_radius_m, grid_mult=grid_mult, trans_lanes=trans_lanes,
-                **meili) as eng:
+                cand_lanes=cand_lanes, **meili) as eng:
         eng.set_counting(counters)
         res = eng.match(batch)
         p = oracle.params(**meili)
@@ -106,6 +106,20 @@ def test_transition_lanes(small_graph, oracle, results_equal, lanes):
     res, orc = _run_both(small_graph, b, oracle, results_equal, trans_lanes=lanes)
     k = orc["ncand"]
     assert k.max() > 8 and (k > 0).mean() > 0.9
+
+
+@pytest.mark.parametrize("lanes", [1, 4, 8, 16])
+@pytest.mark.parametrize("grid_mult", [1, None], ids=["grid1", "grid_auto"])
+def test_candidate_lanes(small_graph, rural_graph, oracle, results_equal, lanes, grid_mult):
+    # K2's lane tier (1 lane per probe) and sub-group tier (4 / 8 / 16 lanes
+    # per probe, an LDS hash table per probe); probes beyond either's edge cap
+    # go to the wave tier -- candidates, counters and everything after
+    # identical to the oracle.  The rural graph at 100 m has many edges per probe.
+    b = synth.make_traces(small_graph, 150, 100, interval_s=5.0, noise_sigma_m=15.0, accuracy=15.0, seed=31)
+    _run_both(small_graph, b, oracle, results_equal, grid_mult=grid_mult, cand_lanes=lanes)
+    b = synth.make_traces(rural_graph, 100, 60, interval_s=30.0, noise_sigma_m=50.0, accuracy=50.0, seed=37)
+    _run_both(rural_graph, b, oracle, results_equal, meili={"search_radius": 100.0, "max_search_radius": 100.0},
+              grid_mult=grid_mult, cand_lanes=lanes)
 
 
 def test_node_candidates(small_graph, oracle, results_equal):

@@ -58,10 +58,27 @@ typedef struct otm_engine otm_engine;
  *   such as "15" is rejected with OTM_ECONFIG ("invalid truth value '15'"),
  *   where the reference's worker threads would die.
  * Replaces valhalla.Configure (py/reporter_service.py:279) + per-thread
- * SegmentMatcher() construction (:52).  ndev must be 1 in this release;
- * multi-GPU runs one engine per process/GPU. */
+ * SegmentMatcher() construction (:52).
+ *   ndev == 1: one GPU.  ndev > 1: a multi-device engine for a host that
+ *   drives several GPUs from one process (the Java host is one JVM): one
+ *   member engine per entry of devices (a full graph + index replica each;
+ *   a device may repeat).  Request-level calls (otm_report, otm_report_batch,
+ *   otm_submit/otm_poll, otm_match_json) and the batcher send each trace to
+ *   member (murmur2(uuid) & 0x7fffffff) % ndev -- Kafka's partition of the
+ *   key, SURVEY.md §8(e) -- run the members concurrently and merge the
+ *   results in request order; otm_match_soa splits its traces into
+ *   point-balanced contiguous ranges (the binary batch carries no uuid).
+ *   Device-side calls (otm_match_device, otm_hist_bind*) go to a member
+ *   (otm_engine_member); info getters answer for member 0.  Multi-process
+ *   runs (one engine per GPU process, RCCL reduce of the histograms) are
+ *   DESIGN.md §8. */
 int otm_engine_create(const char* cfg_path, const int* devices, int ndev,
                       otm_engine** out);
+/* Members of an engine: ndev of a multi-device engine, 1 otherwise. */
+int otm_engine_members(const otm_engine* eng);
+/* Member i of a multi-device engine (NULL when out of range); a one-device
+ * engine is its own member 0.  Owned by eng. */
+otm_engine* otm_engine_member(otm_engine* eng, int i);
 /* A second batch context on the same GPU (extension): its own HIP stream and
  * work buffers over the parent's HBM-resident graph, distance index and
  * configuration.  Batches on a parent and its clones run concurrently when

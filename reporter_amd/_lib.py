@@ -116,6 +116,8 @@ def _declare(L):
     psz = C.POINTER(C.c_size_t)
     sig = {
         "otm_engine_create": (C.c_int, [C.c_char_p, C.POINTER(C.c_int), C.c_int, pp]),
+        "otm_engine_members": (C.c_int, [vp]),
+        "otm_engine_member": (vp, [vp, C.c_int]),
         "otm_engine_destroy": (None, [vp]),
         "otm_last_error": (C.c_char_p, [vp]),
         "otm_free": (None, [vp]),

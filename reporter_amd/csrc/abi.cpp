@@ -126,11 +126,19 @@ void run_requests(otm_engine* E, std::vector<Value>& traces, std::vector<int>& c
   std::string err;
   otm_results r;
   int rc;
+  // a multi-device engine: each trace to its uuid's member (Kafka's partition);
+  // a uuid that is not a string (the reference accepts any non-null) to member 0
+  std::vector<int32_t> shard;
+  if (!E->members.empty()) {
+    shard.resize(which.size(), 0);
+    for (size_t n = 0; n < which.size(); ++n) {
+      const Value* u = traces[(size_t)which[n]].get("uuid");
+      if (u && u->kind == Kind::Str) shard[n] = otm::shard_of(u->s.data(), u->s.size(), (int)E->members.size());
+    }
+  }
   {
     std::lock_guard<std::mutex> lk(E->mu);
-    (void)hipSetDevice(E->device);
-    rc = otm::engine_match_host(E, &b, &err);
-    if (!rc) rc = otm::engine_fetch(E, &r, &err);
+    rc = otm::match_host_fetch(E, &b, shard.empty() ? nullptr : shard.data(), &r, &err);
     if (!rc) {
       for (size_t n = 0; n < which.size(); ++n) {
         const int k = which[n];
@@ -236,7 +244,28 @@ const char* otm_runtime_info(void) {
 int otm_engine_create(const char* cfg_path, const int* devices, int ndev, otm_engine** out) {
   if (!out) return fail(OTM_EINVAL, "out is NULL");
   *out = nullptr;
-  if (ndev != 1 || !devices) return fail(OTM_EINVAL, "exactly one device per engine (one engine per GPU process)");
+  if (ndev < 1 || !devices) return fail(OTM_EINVAL, "devices must name at least one device");
+  if (ndev > 1) {
+    // a multi-device engine: one member per device, each a full replica
+    auto* G = new otm_engine();
+    for (int i = 0; i < ndev; ++i) {
+      otm_engine* M = nullptr;
+      int rc = otm_engine_create(cfg_path, devices + i, 1, &M);
+      if (rc) {
+        const std::string msg = std::string("device ") + std::to_string(devices[i]) + ": " + otm_last_error(nullptr);
+        for (otm_engine* m : G->members) otm_engine_destroy(m);
+        delete G;
+        return fail(rc, msg);
+      }
+      G->members.push_back(M);
+    }
+    const otm_engine* L = G->members[0];
+    G->device = L->device;
+    G->mc = L->mc;
+    G->rc = L->rc;
+    *out = G;
+    return OTM_OK;
+  }
   std::string text;
   if (!cfg_path || !read_file(cfg_path, &text)) return fail(OTM_EINVAL, std::string("cannot read config ") + (cfg_path ? cfg_path : "(null)"));
   Value cfg;
@@ -327,6 +356,7 @@ int otm_engine_clone(otm_engine* P, otm_engine** out) {
   if (!P || !out) return fail(OTM_EINVAL, "engine or out is NULL");
   *out = nullptr;
   if (P->parent) return fail(OTM_EINVAL, "clone the parent engine, not a clone");
+  if (!P->members.empty()) return fail(OTM_EINVAL, "clone a member engine (otm_engine_member), not a multi-device engine");
   auto* C = new otm_engine();
   std::string err;
   int rc = otm::engine_clone(P, C, &err);
@@ -350,8 +380,21 @@ void otm_engine_destroy(otm_engine* E) {
     E->worker.join();
     for (auto& r : E->done) std::free(r.body);
   }
+  if (!E->members.empty()) {
+    for (otm_engine* m : E->members) otm_engine_destroy(m);
+    delete E;
+    return;
+  }
   otm::engine_free(E);
   delete E;
+}
+
+int otm_engine_members(const otm_engine* E) { return !E ? 0 : E->members.empty() ? 1 : (int)E->members.size(); }
+
+otm_engine* otm_engine_member(otm_engine* E, int i) {
+  if (!E || i < 0) return nullptr;
+  if (E->members.empty()) return i == 0 ? E : nullptr;
+  return i < (int)E->members.size() ? E->members[(size_t)i] : nullptr;
 }
 
 int otm_report(otm_engine* E, const char* req, size_t len, char** resp, size_t* resp_len) {
@@ -425,6 +468,7 @@ int otm_report_segments_device(otm_engine* E, int n, const char* const* reqs, co
                                const char* const* match_jsons, const size_t* match_lens, char** resps,
                                size_t* resp_lens, int* codes) {
   if (!E || n < 0) return fail(OTM_EINVAL, "bad arguments");
+  if (!E->members.empty()) E = E->members[0];  // no per-uuid state: the first member's GPU
   std::vector<std::string> bodies((size_t)n), matcher((size_t)n);
   std::vector<int> c((size_t)n, 0);
   // the typed traces: one point each (the request's last time), their segments
@@ -571,15 +615,14 @@ void otm_host_free(void* p) {
 int otm_match_soa(otm_engine* E, const otm_batch* in, otm_results* out) {
   if (!E || !in || !out) return fail(OTM_EINVAL, "bad arguments");
   std::lock_guard<std::mutex> lk(E->mu);
-  (void)hipSetDevice(E->device);
   std::string err;
-  int rc = otm::engine_match_host(E, in, &err);
-  if (!rc) rc = otm::engine_fetch(E, out, &err);
+  int rc = otm::match_host_fetch(E, in, nullptr, out, &err);
   return rc ? fail(rc, err) : OTM_OK;
 }
 
 int otm_match_device(otm_engine* E, const otm_batch* in, void* stream) {
   if (!E || !in) return fail(OTM_EINVAL, "bad arguments");
+  if (!E->members.empty()) return fail(OTM_EINVAL, "device batches go to a member engine (otm_engine_member)");
   std::lock_guard<std::mutex> lk(E->mu);
   (void)hipSetDevice(E->device);
   otm::DevBatch b;
@@ -598,6 +641,18 @@ int otm_match_device(otm_engine* E, const otm_batch* in, void* stream) {
 int otm_fetch_results(otm_engine* E, otm_results* out) {
   if (!E || !out) return fail(OTM_EINVAL, "bad arguments");
   std::lock_guard<std::mutex> lk(E->mu);
+  if (!E->members.empty()) {
+    // the merged results of the group's last batch
+    out->n_traces = (int32_t)E->g_traces.size();
+    out->n_segments = (int32_t)E->g_segs.size();
+    out->n_reports = (int32_t)E->g_reps.size();
+    out->n_way_ids = (int32_t)E->g_ways.size();
+    out->traces = E->g_traces.data();
+    out->segments = E->g_segs.data();
+    out->reports = E->g_reps.data();
+    out->way_ids = E->g_ways.data();
+    return OTM_OK;
+  }
   std::string err;
   int rc = otm::engine_fetch(E, out, &err);
   return rc ? fail(rc, err) : OTM_OK;
@@ -606,6 +661,7 @@ int otm_fetch_results(otm_engine* E, otm_results* out) {
 int otm_hist_bind_ex(otm_engine* E, void* dev_counts, int nbins, float bin_kph, void* dev_speed_sum) {
   if (!E) return fail(OTM_EINVAL, "engine is NULL");
   if (E->parent) return fail(OTM_EINVAL, "bind the histogram on the parent engine (clones share it)");
+  if (!E->members.empty()) return fail(OTM_EINVAL, "bind one histogram per member engine (otm_engine_member)");
   if (dev_counts && (nbins < 1 || !(bin_kph > 0.0f))) return fail(OTM_EINVAL, "nbins >= 1 and bin_kph > 0");
   if (dev_speed_sum && !dev_counts) return fail(OTM_EINVAL, "a speed-sum channel needs the counts");
   // a batch in flight on this engine or a clone keeps the binding it started with
@@ -623,6 +679,7 @@ int otm_hist_bind(otm_engine* E, void* dev_counts, int nbins, float bin_kph) {
 
 int otm_graph_info(const otm_engine* E, int64_t* n_nodes, int64_t* n_edges, int64_t* n_segments) {
   if (!E) return fail(OTM_EINVAL, "engine is NULL");
+  if (!E->members.empty()) E = E->members[0];  // every member holds the same graph
   if (n_nodes) *n_nodes = E->host.h.n_nodes;
   if (n_edges) *n_edges = E->host.h.n_edges;
   if (n_segments) *n_segments = E->host.h.n_segments;
@@ -631,6 +688,7 @@ int otm_graph_info(const otm_engine* E, int64_t* n_nodes, int64_t* n_edges, int6
 
 int otm_index_info(const otm_engine* E, float* rmax, int64_t* entries, int32_t* incomplete_rows, float* build_ms) {
   if (!E) return fail(OTM_EINVAL, "engine is NULL");
+  if (!E->members.empty()) E = E->members[0];  // every member holds the same graph
   if (rmax) *rmax = E->idx.rmax;
   if (entries) *entries = E->index_entries;
   if (incomplete_rows) *incomplete_rows = E->index_incomplete_rows;
@@ -641,6 +699,7 @@ int otm_index_info(const otm_engine* E, float* rmax, int64_t* entries, int32_t* 
 int otm_grid_info(const otm_engine* E, double* cell_deg, int32_t* rows, int32_t* cols, int64_t* entries,
                   int32_t* mult) {
   if (!E) return fail(OTM_EINVAL, "engine is NULL");
+  if (!E->members.empty()) E = E->members[0];  // every member holds the same graph
   if (cell_deg) *cell_deg = E->g.cell;
   if (rows) *rows = E->grid_rows;
   if (cols) *cols = E->grid_cols;
@@ -651,30 +710,35 @@ int otm_grid_info(const otm_engine* E, double* cell_deg, int32_t* rows, int32_t*
 
 int otm_set_counting(otm_engine* E, int on) {
   if (!E) return fail(OTM_EINVAL, "engine is NULL");
+  for (otm_engine* m : E->members) m->counting = on != 0;
   E->counting = on != 0;
   return OTM_OK;
 }
 
 int otm_get_counters(otm_engine* E, otm_work_counters* out) {
   if (!E || !out) return fail(OTM_EINVAL, "bad arguments");
+  if (!E->members.empty()) E = E->members[0];  // the first member (others: otm_engine_member)
   std::lock_guard<std::mutex> lk(E->mu);
   return otm::engine_counters(E, out) ? fail(OTM_EDEVICE, "counter copy failed") : OTM_OK;
 }
 
 int otm_set_timing(otm_engine* E, int on) {
   if (!E) return fail(OTM_EINVAL, "engine is NULL");
+  for (otm_engine* m : E->members) m->timing = on != 0;
   E->timing = on != 0;
   return OTM_OK;
 }
 
 int otm_get_stage_ms(otm_engine* E, float* ms, int n) {
   if (!E || !ms) return fail(OTM_EINVAL, "bad arguments");
+  if (!E->members.empty()) E = E->members[0];  // the first member (others: otm_engine_member)
   for (int k = 0; k < n && k < 8; ++k) ms[k] = E->stage_ms[k];
   return OTM_OK;
 }
 
 int otm_get_kernel_ms(otm_engine* E, float* ms, int n) {
   if (!E || !ms) return fail(OTM_EINVAL, "bad arguments");
+  if (!E->members.empty()) E = E->members[0];  // the first member (others: otm_engine_member)
   for (int k = 0; k < n && k < otm::KN_COUNT; ++k) ms[k] = E->kernel_ms[k];
   return OTM_OK;
 }
@@ -684,12 +748,14 @@ const char* otm_kernel_name(int k) { return k >= 0 && k < otm::KN_COUNT ? otm::k
 
 int otm_get_spill_stats(otm_engine* E, otm_spill_stats* out) {
   if (!E || !out) return fail(OTM_EINVAL, "bad arguments");
+  if (!E->members.empty()) E = E->members[0];  // the first member (others: otm_engine_member)
   std::lock_guard<std::mutex> lk(E->mu);
   return otm::engine_spill_stats(E, out) ? fail(OTM_EDEVICE, "spill stats copy failed") : OTM_OK;
 }
 
 int otm_debug_fetch(otm_engine* E, int what, void* dst, size_t bytes, size_t* needed) {
   if (!E) return fail(OTM_EINVAL, "engine is NULL");
+  if (!E->members.empty()) E = E->members[0];  // the first member (others: otm_engine_member)
   std::lock_guard<std::mutex> lk(E->mu);
   std::string err;
   int rc = otm::engine_debug_fetch(E, what, dst, bytes, needed, &err);

@@ -481,13 +481,20 @@ int issue_binary(otm_batcher* B, size_t r0, size_t r1) {
   std::string err;
   otm_results res;
   int rc;
+  // a multi-device engine: each request to its key's member (Kafka's partition)
+  std::vector<int32_t> shard;
+  if (!E->members.empty()) {
+    shard.resize(n);
+    for (size_t i = 0; i < n; ++i) {
+      const std::string& key = B->keys[B->reqs[r0 + i].key].key;
+      shard[i] = otm::shard_of(key.data(), key.size(), (int)E->members.size());
+    }
+  }
   {
     std::lock_guard<std::mutex> lk(E->mu);
-    (void)hipSetDevice(E->device);
     const int64_t t1 = now_us();
     B->st.us_prepare += t1 - t0;
-    rc = otm::engine_match_host(E, &b, &err);
-    if (!rc) rc = otm::engine_fetch(E, &res, &err);
+    rc = otm::match_host_fetch(E, &b, shard.empty() ? nullptr : shard.data(), &res, &err);
     const int64_t t2 = now_us();
     B->st.us_match += t2 - t1;
     if (!rc) {

@@ -15,6 +15,15 @@
 
 struct otm_engine {
   const otm_engine* parent = nullptr;  // a clone shares its parent's graph and index (otm_engine_clone)
+  // a multi-device engine (otm_engine_create with ndev > 1, group.cpp): one
+  // member engine per device and no GPU state of its own; host batches are split
+  // across the members by uuid and merged back (the g_* arrays hold the merged
+  // results of its last batch)
+  std::vector<otm_engine*> members;
+  std::vector<otm_trace_result> g_traces;
+  std::vector<otm_segment> g_segs;
+  std::vector<otm_report_rec> g_reps;
+  std::vector<int64_t> g_ways;
   int device = 0;
   hipStream_t stream = nullptr;
   otm::HostGraph host;
@@ -125,5 +134,12 @@ int engine_report_segments(otm_engine* E, int32_t T, const int64_t* trace_off, c
                            const int32_t* seg_off, const otm_segment* segs, otm_trace_result* traces,
                            otm_report_rec* reports, std::string* err);
 int engine_spill_stats(otm_engine* E, otm_spill_stats* out);
+// host batch -> host results on any engine (group.cpp): one device
+// (engine_match_host + engine_fetch), or a multi-device engine, whose traces go
+// to member shard[t] (point-balanced contiguous ranges when shard is NULL), run
+// concurrently and are merged in trace order.  The caller holds E->mu.
+int match_host_fetch(otm_engine* E, const otm_batch* b, const int32_t* shard, otm_results* out, std::string* err);
+// a uuid's member among n: Kafka's partition of the key, (murmur2 & 0x7fffffff) % n
+int shard_of(const char* key, size_t len, int n);
 
 }  // namespace otm

@@ -2308,22 +2308,55 @@ __device__ void viterbi_trace_global(int64_t a, int64_t e, DevWork& w) {
 constexpr int VIT_PTS = OTM_VIT_PTS; // points per trace (metadata held for the whole trace)
 constexpr int VIT_BP = OTM_VIT_BP;   // candidates per trace (backpointers)
 constexpr int VIT_TW = OTM_VIT_TW;   // transition floats per window (>= one column pair's block)
-constexpr int VIT_EW = 256;          // emission floats per window (>= KMAX)
+// emission floats per window (>= KMAX); the walk form (OTM_VIT_WALK) needs 144
+// to stay within 8 waves per SIMD of LDS
+#ifndef OTM_VIT_EW
+#define OTM_VIT_EW 256
+#endif
+constexpr int VIT_EW = OTM_VIT_EW;
+static_assert(VIT_EW >= KMAX, "one column's emissions fit a window");
 
 #ifndef OTM_VIT_WAVES
 #define OTM_VIT_WAVES 8
+#endif
+// Backtrack form.  1: a backpointer is the trace-wide index of the
+// predecessor candidate (eoff of the previous column + its state), so lane 0's
+// walk is one dependent LDS read per column, marking the visited entries; the
+// states and chain starts are then read back point-parallel.  0: the round-1
+// walk (state, backpointer, eoff and previous column: three dependent reads).
+// 1 measured 0.159 vs 0.157 ms (config 2) at 8 waves per SIMD, but its 16-bit
+// backpointers need the emission window cut to 144 floats to stay there (with
+// 256: 7 waves, 0.180 ms): 0 kept.
+#ifndef OTM_VIT_WALK
+#define OTM_VIT_WALK 0
+#endif
+// Window staging.  1: the transition block and the first emissions are loaded
+// before any is stored (one global round trip per window); 0: transitions,
+// then emissions.  Measured equal (k_viterbi 0.159 vs 0.158 ms config 2, 1.090
+// vs 1.077 config 4; profiles/r02_ab_viterbi.txt): 0 kept.
+#ifndef OTM_VIT_STAGE1
+#define OTM_VIT_STAGE1 0
+#endif
+#if OTM_VIT_WALK
+constexpr int16_t VIT_BP_START = 0x7FFF;  // chain start: the walk ends here
+constexpr int16_t VIT_BP_DEAD = 0x7FFE;   // unreachable state: never walked
+constexpr int VIT_BP_MARK = 0x8000;       // set on the entries the walk visits
 #endif
 __global__ __launch_bounds__(TB, OTM_VIT_WAVES) void k_viterbi(DevBatch b, DevWork w) {
   if (*w.abort) return;  // a capacity was exceeded: the host redoes the batch
   __shared__ float sT[VIT_TW];
   __shared__ float sEm[VIT_EW];
+#if OTM_VIT_WALK
+  __shared__ uint16_t sBp[VIT_BP];
+#else
   __shared__ uint8_t sBp[VIT_BP];
+  __shared__ int8_t sState[VIT_PTS];
+  __shared__ uint8_t sCs[VIT_PTS];
+#endif
   __shared__ int32_t sToff[VIT_PTS + 1];
   __shared__ int16_t sEoff[VIT_PTS + 1];
   __shared__ int16_t sCprev[VIT_PTS];
   __shared__ int8_t sKc[VIT_PTS];  // ncand of a column, -1 for a non-column point
-  __shared__ int8_t sState[VIT_PTS];
-  __shared__ uint8_t sCs[VIT_PTS];
   const int lane = threadIdx.x;
   for (int32_t t = blockIdx.x; t < b.n_traces; t += gridDim.x) {
     const int64_t a = b.trace_off[t], e = b.trace_off[t + 1];
@@ -2366,8 +2399,10 @@ __global__ __launch_bounds__(TB, OTM_VIT_WAVES) void k_viterbi(DevBatch b, DevWo
           sCprev[pl] = (int16_t)cp;
           sToff[pl] = to;
           sEoff[pl] = (int16_t)min(etot + incl - k, 32767);
+#if !OTM_VIT_WALK
           sState[pl] = -1;
           sCs[pl] = 0;
+#endif
         }
         etot += __shfl(incl, 63, 64);
       }
@@ -2392,6 +2427,25 @@ __global__ __launch_bounds__(TB, OTM_VIT_WAVES) void k_viterbi(DevBatch b, DevWo
     bool open = false;
     int last = -1;
     int win_end = 0, wt0 = 0, we0 = 0;
+#if OTM_VIT_WALK
+    int lastEo = 0;  // eoff of column `last`
+    auto backtrack = [&](int endl, int Ke) {
+      (void)endl;
+      float bv;
+      int bi;
+      wave_argmin(lane < Ke ? prev : INFINITY, lane, bv, bi);
+      __syncthreads();  // backpointers written by other lanes
+      if (lane == 0) {
+        int ix = lastEo + bi;
+        while (true) {
+          const int v = sBp[ix];
+          sBp[ix] = (uint16_t)(v | VIT_BP_MARK);
+          if (v == VIT_BP_START) break;
+          ix = v;
+        }
+      }
+    };
+#else
     auto backtrack = [&](int endl, int Ke) {
       float bv;
       int bi;
@@ -2408,6 +2462,7 @@ __global__ __launch_bounds__(TB, OTM_VIT_WAVES) void k_viterbi(DevBatch b, DevWo
         }
       }
     };
+#endif
     // The forward pass walks the points in chunks of 64 whose metadata sits
     // in registers (lane k holds point c0 + k) and is read with readlane: the
     // per-column chain keeps one LDS round trip (emission + transition reads,
@@ -2447,6 +2502,63 @@ __global__ __launch_bounds__(TB, OTM_VIT_WAVES) void k_viterbi(DevBatch b, DevWo
           }
           win_end = we;
           const int nt = sToff[win_end] - wt0;
+#if OTM_VIT_STAGE1
+          // one round trip for the window: the transition block (nt <= VIT_TW
+          // <= 8 x 64 floats) and the first four emissions of the first 64
+          // points are all loaded before any of them is stored
+          static_assert(VIT_TW <= 8 * TB, "one pass of transition loads");
+          {
+            float v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+              const int f = u * TB + lane;
+              v[u] = f < nt ? w.trans[t0 + wt0 + f] : 0.0f;
+            }
+            const int q = pl + lane;
+            int kq = 0, eq = 0;
+            if (q < win_end) {
+              kq = sKc[q];
+              eq = sEoff[q] - we0;
+            }
+            float ev[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) ev[u] = u < kq ? w.cand_emis[CSTRIDE * ((a + q) * KMAX + u)] : 0.0f;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+              const int f = u * TB + lane;
+              if (f < nt) sT[f] = v[u];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+              if (u < kq) sEm[eq + u] = ev[u];
+            // the rest: candidates beyond four, points beyond 64 (rare)
+            for (int j0 = 4; __ballot(j0 < kq) != 0ull; j0 += 4) {
+#pragma unroll
+              for (int u = 0; u < 4; ++u)
+                ev[u] = j0 + u < kq ? w.cand_emis[CSTRIDE * ((a + q) * KMAX + j0 + u)] : 0.0f;
+#pragma unroll
+              for (int u = 0; u < 4; ++u)
+                if (j0 + u < kq) sEm[eq + j0 + u] = ev[u];
+            }
+          }
+          for (int q0 = pl + TB; q0 < win_end; q0 += TB) {
+            const int q = q0 + lane;
+            int kq = 0, eq = 0;
+            if (q < win_end) {
+              kq = sKc[q];
+              eq = sEoff[q] - we0;
+            }
+            for (int j0 = 0; __ballot(j0 < kq) != 0ull; j0 += 4) {
+              float v[4];
+#pragma unroll
+              for (int u = 0; u < 4; ++u)
+                v[u] = j0 + u < kq ? w.cand_emis[CSTRIDE * ((a + q) * KMAX + j0 + u)] : 0.0f;
+#pragma unroll
+              for (int u = 0; u < 4; ++u)
+                if (j0 + u < kq) sEm[eq + j0 + u] = v[u];
+            }
+          }
+#else
           for (int f0 = 0; f0 < nt; f0 += 8 * TB) {
             float v[8];
 #pragma unroll
@@ -2479,6 +2591,7 @@ __global__ __launch_bounds__(TB, OTM_VIT_WAVES) void k_viterbi(DevBatch b, DevWo
                 if (j0 + u < kq) sEm[eq + j0 + u] = v[u];
             }
           }
+#endif
           __syncthreads();
         }
         const int eo = __builtin_amdgcn_readlane(r_eo, k);
@@ -2519,7 +2632,11 @@ __global__ __launch_bounds__(TB, OTM_VIT_WAVES) void k_viterbi(DevBatch b, DevWo
           const bool alive = lane < Kp && bi >= 0;
           if (lane < Kp) {
             cur = alive ? best + em : INFINITY;
+#if OTM_VIT_WALK
+            sBp[eo + lane] = alive ? (uint16_t)(lastEo + bi) : (uint16_t)VIT_BP_DEAD;
+#else
             sBp[eo + lane] = alive ? (uint8_t)bi : (uint8_t)0xFF;
+#endif
           }
           if (__ballot(alive) == 0ull) {
             backtrack(last, lastK);
@@ -2531,20 +2648,41 @@ __global__ __launch_bounds__(TB, OTM_VIT_WAVES) void k_viterbi(DevBatch b, DevWo
         }
         if (!started) {
           cur = lane < Kp ? em : INFINITY;
+#if OTM_VIT_WALK
+          if (lane < Kp) sBp[eo + lane] = (uint16_t)VIT_BP_START;
+#else
           if (lane == 0) sCs[pl] = 1;
+#endif
         }
         prev = cur;
         open = true;
         last = pl;
         lastK = Kp;
+#if OTM_VIT_WALK
+        lastEo = eo;
+#endif
       }
     }
     if (open) backtrack(last, lastK);
     __syncthreads();
     for (int pl = lane; pl < n; pl += TB) {
+#if OTM_VIT_WALK
+      // every column with candidates lies on a walked chain: its state is the
+      // marked entry, and a chain start's entries all hold VIT_BP_START
+      const int kc = sKc[pl];
+      const int eo = sEoff[pl];
+      int st = -1, cs = 0;
+      for (int j = 0; j < kc; ++j) {
+        const int v = sBp[eo + j];
+        if (v & VIT_BP_MARK) st = j;
+        if (j == 0) cs = (v & ~VIT_BP_MARK) == VIT_BP_START;
+      }
+#else
       const int st = sState[pl];
+      const int cs = sCs[pl];
+#endif
       w.state[a + pl] = st;
-      w.chain_start[a + pl] = sCs[pl];
+      w.chain_start[a + pl] = (uint8_t)cs;
       // the chosen candidate, compact for the route and segment stages
       if (st >= 0) {
         const int64_t r = CSTRIDE * ((a + pl) * KMAX + st);

@@ -55,8 +55,10 @@ class Results(object):
 
 class Engine(object):
     def __init__(self, config_path=None, graph_path=None, device=0, index_radius_m=None, grid_mult=None,
-                 trans_lanes=None, cand_lanes=None, **meili):
-        """Either a config file (valhalla.Configure-style) or a graph path."""
+                 trans_lanes=None, cand_lanes=None, devices=None, **meili):
+        """Either a config file (valhalla.Configure-style) or a graph path.
+        devices=[d0, d1, ...] makes a multi-device engine (otm_engine_create
+        with ndev > 1): traces go to member murmur2(uuid) % ndev."""
         L = lib()
         self._tmp = None
         if config_path is None:
@@ -67,12 +69,32 @@ class Engine(object):
             config_path = write_config(self._tmp, graph_path, index_radius_m=index_radius_m, grid_mult=grid_mult,
                                        trans_lanes=trans_lanes, cand_lanes=cand_lanes, **meili)
         h = C.c_void_p()
-        dev = (C.c_int * 1)(device)
-        rc = L.otm_engine_create(config_path.encode(), dev, 1, C.byref(h))
+        devs = list(devices) if devices is not None else [device]
+        dev = (C.c_int * len(devs))(*devs)
+        rc = L.otm_engine_create(config_path.encode(), dev, len(devs), C.byref(h))
         if rc != _lib.OTM_OK:
             raise OtmError("otm_engine_create failed (%d): %s" % (rc, _lib.last_error()))
         self.h = h
-        self.device = device
+        self.device = devs[0]
+        self.devices = devs
+
+    def members(self):
+        """Member count: ndev of a multi-device engine, else 1."""
+        return lib().otm_engine_members(self.h)
+
+    def member(self, i):
+        """Member i of a multi-device engine as an Engine view (owned by self:
+        do not close it; it lives as long as self)."""
+        h = lib().otm_engine_member(self.h, i)
+        if not h:
+            raise OtmError("no member %d" % i)
+        e = Engine.__new__(Engine)
+        e._tmp = None
+        e.h = C.c_void_p(h)
+        e.device = self.devices[i] if len(self.devices) > 1 else self.device
+        e.parent = self
+        e._view = True
+        return e
 
     def clone(self):
         """A second batch context on this GPU sharing the graph and index
@@ -90,6 +112,8 @@ class Engine(object):
         return e
 
     def close(self):
+        if getattr(self, "_view", False):
+            self.h = None  # a member view: its group owns it
         if getattr(self, "h", None):
             lib().otm_engine_destroy(self.h)
             self.h = None

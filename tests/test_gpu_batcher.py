@@ -21,3 +21,16 @@ def test_gpu_batcher_matches_serial_restatement(small_graph, json_path, threads)
         nb = run_native(recs, Batcher(engine=eng, json_path=json_path, threads=threads))
         st = compare(bp, nb, recs)
         assert st["forwarded"] > 10 and st["match_batches"] < st["requests"]
+
+
+@pytest.mark.parametrize("json_path", [False, True], ids=["binary", "json"])
+def test_gpu_batcher_on_multi_device_engine(small_graph, json_path):
+    """The batcher over a multi-device engine (two members, repeated device 0):
+    each key's requests go to its murmur2 member; forwarded records, counts
+    and stored batches equal the serial restatement's."""
+    recs = make_stream(small_graph, n_veh=30, n_pts=80, seed=53)
+    with Engine(graph_path=small_graph) as one, Engine(graph_path=small_graph, devices=[0, 0]) as grp:
+        bp = run_python(recs, lambda body: one.report(body)[1])
+        nb = run_native(recs, Batcher(engine=grp, json_path=json_path, threads=4))
+        st = compare(bp, nb, recs)
+        assert st["forwarded"] > 10

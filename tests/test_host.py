@@ -172,3 +172,20 @@ def test_turn_cost_table():
     for d in (0, 45, 90, 135, 180):
         assert abs(t[d] - 200 * 64 * math.exp(-(180 - d) / 45.0)) <= 0.5
     assert all(L.orc_turn_units(0.0, d) == 0 for d in range(181))
+
+
+def test_engine_create_device_arguments():
+    """otm_engine_create's device list (no GPU needed: rejected before any
+    device call): ndev < 1 or a NULL list is OTM_EINVAL; a NULL engine has
+    no members."""
+    L = _lib.lib()
+    h = C.c_void_p()
+    devs = (C.c_int * 2)(0, 0)
+    assert L.otm_engine_create(b"/nonexistent.json", devs, 0, C.byref(h)) == -1  # OTM_EINVAL
+    assert L.otm_engine_create(b"/nonexistent.json", None, 2, C.byref(h)) == -1  # OTM_EINVAL
+    assert not h.value
+    assert L.otm_engine_members(None) == 0
+    assert not L.otm_engine_member(None, 0)
+    # a group whose members cannot be created fails as the member does
+    assert L.otm_engine_create(b"/nonexistent.json", devs, 2, C.byref(h)) == -1  # OTM_EINVAL
+    assert "cannot read config" in _lib.last_error()

@@ -86,6 +86,8 @@ def parse():
     ap.add_argument("--no-check", action="store_true", help="skip the untimed oracle pass (agreement, bytes)")
     ap.add_argument("--traffic-json", default=None,
                     help="PMC traffic summary (scripts/pmc_summary.py); default: the committed one for --config")
+    ap.add_argument("--host-stagger-ms", type=float, default=0.0,
+                    help="host-inclusive leg: in-flight worker i starts i x this many ms late (A/B of phase drift)")
     ap.add_argument("--inflight", type=int, default=3,
                     help="batches in flight per GPU: engine clones on their own HIP streams, one host thread each")
     return ap.parse_args()
@@ -344,6 +346,8 @@ def main():
 
         def hworker(i):
             hgate.wait()
+            if args.host_stagger_ms > 0:
+                time.sleep(i * args.host_stagger_ms / 1e3)
             while next(hticket) < host_steps:
                 host_step(i)
 

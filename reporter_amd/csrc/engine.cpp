@@ -102,6 +102,8 @@ static int auto_grid_mult(const otm_engine* E) {
   return best;
 }
 
+int create_stream(int slot, hipStream_t* s);
+
 int engine_init(otm_engine* E, const char* graph_path, int device, std::string* err) {
   int rc = load_graph(graph_path, &E->host, err);
   if (rc) return rc;
@@ -112,7 +114,10 @@ int engine_init(otm_engine* E, const char* graph_path, int device, std::string* 
   if (E->grid_mult == 0) E->grid_mult = auto_grid_mult(E);
   E->device = device;
   HIPCHK(hipSetDevice(device));
-  HIPCHK(hipStreamCreateWithFlags(&E->stream, hipStreamNonBlocking));
+  if (create_stream(0, &E->stream)) {
+    *err = "stream creation failed";
+    return OTM_EDEVICE;
+  }
   const otmg_header& h = E->host.h;
   auto up = [&](int sec, const void** dst) -> int {
     void* d = nullptr;
@@ -264,11 +269,40 @@ int engine_init(otm_engine* E, const char* graph_path, int device, std::string* 
   return build_index(E, err);
 }
 
+// The stream of batch context `slot` (0: the engine, k: its k-th clone).
+// OTM_STREAM_PRIO="hi,lo,..." gives the contexts HIP stream priorities (hi =
+// greatest, lo = least, or an integer), so that batches in flight drift out of
+// phase: the prioritised one finishes its kernels first and copies while the
+// others compute (an A/B knob; default: every stream at normal priority).
+int create_stream(int slot, hipStream_t* s) {
+  const char* v = std::getenv("OTM_STREAM_PRIO");
+  if (v && *v) {
+    std::string list(v);
+    std::string item;
+    for (int k = 0; k <= slot; ++k) {
+      const size_t c = list.find(',');
+      item = list.substr(0, c);
+      list = c == std::string::npos ? std::string() : list.substr(c + 1);
+    }
+    if (!item.empty()) {
+      int least = 0, greatest = 0;
+      if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) return 1;
+      const int pr = item == "hi" ? greatest : item == "lo" ? least : std::atoi(item.c_str());
+      return hipStreamCreateWithPriority(s, hipStreamNonBlocking, pr) != hipSuccess;
+    }
+  }
+  return hipStreamCreateWithFlags(s, hipStreamNonBlocking) != hipSuccess;
+}
+
 int engine_clone(const otm_engine* P, otm_engine* C, std::string* err) {
   C->parent = P;
   C->device = P->device;
   HIPCHK(hipSetDevice(C->device));
-  HIPCHK(hipStreamCreateWithFlags(&C->stream, hipStreamNonBlocking));
+  const int slot = ++const_cast<otm_engine*>(P)->n_clones;
+  if (create_stream(slot, &C->stream)) {
+    *err = "stream creation failed";
+    return OTM_EDEVICE;
+  }
   C->host.h = P->host.h;  // the header only: a clone reads no host graph sections
   C->g = P->g;
   C->idx = P->idx;
@@ -695,6 +729,18 @@ int engine_match(otm_engine* E, const DevBatch& b, hipStream_t s, std::string* e
   return OTM_OK;
 }
 
+// The kind of the large host<->device copies.  OTM_COPY_NOCU=1 asks for
+// hipMemcpyDeviceToDeviceNoCU on the (pinned, device-mapped) host buffers: a
+// copy engine instead of the runtime's blit kernels, which otherwise occupy
+// every CU while they wait on PCIe (an A/B knob).
+hipMemcpyKind big_copy_kind(hipMemcpyKind k) {
+  static const int nocu = [] {
+    const char* v = std::getenv("OTM_COPY_NOCU");
+    return v && *v == '1' ? 1 : 0;
+  }();
+  return nocu ? hipMemcpyDeviceToDeviceNoCU : k;
+}
+
 int engine_match_host(otm_engine* E, const otm_batch* in, std::string* err) {
   const int32_t NT = in->n_traces;
   if (NT < 0 || !in->trace_off) {
@@ -746,11 +792,12 @@ int engine_match_host(otm_engine* E, const otm_batch* in, std::string* err) {
     b.acc = (const float*)(d + b_off + b_tm + 2 * b_pt);
     return engine_match(E, b, s, err);
   }
+  const hipMemcpyKind h2d = big_copy_kind(hipMemcpyHostToDevice);
   HIPCHK(hipMemcpyAsync(E->in_off.p, in->trace_off, b_off, hipMemcpyHostToDevice, s));
-  HIPCHK(hipMemcpyAsync(E->in_lat.p, in->lat, b_pt, hipMemcpyHostToDevice, s));
-  HIPCHK(hipMemcpyAsync(E->in_lon.p, in->lon, b_pt, hipMemcpyHostToDevice, s));
-  HIPCHK(hipMemcpyAsync(E->in_time.p, in->time, b_tm, hipMemcpyHostToDevice, s));
-  HIPCHK(hipMemcpyAsync(E->in_acc.p, in->accuracy, b_pt, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(E->in_lat.p, in->lat, b_pt, h2d, s));
+  HIPCHK(hipMemcpyAsync(E->in_lon.p, in->lon, b_pt, h2d, s));
+  HIPCHK(hipMemcpyAsync(E->in_time.p, in->time, b_tm, h2d, s));
+  HIPCHK(hipMemcpyAsync(E->in_acc.p, in->accuracy, b_pt, h2d, s));
   b.trace_off = (const int64_t*)E->in_off.p;
   b.lat = (const float*)E->in_lat.p;
   b.lon = (const float*)E->in_lon.p;
@@ -819,12 +866,11 @@ int engine_fetch(otm_engine* E, otm_results* out, std::string* err) {
   if ((rc = ensure_pinned(E->h_segs, ((size_t)NS + 1) * sizeof(otm_segment), err))) return rc;
   if ((rc = ensure_pinned(E->h_reps_dense, ((size_t)NR + 1) * sizeof(otm_report_rec), err))) return rc;
   if ((rc = ensure_pinned(E->h_ways, ((size_t)NW + 1) * 8, err))) return rc;
-  if (NT) HIPCHK(hipMemcpyAsync(E->h_traces.p, E->f_traces.p, (size_t)NT * sizeof(otm_trace_result),
-                                hipMemcpyDeviceToHost, s));
-  if (NS) HIPCHK(hipMemcpyAsync(E->h_segs.p, E->f_segs.p, (size_t)NS * sizeof(otm_segment), hipMemcpyDeviceToHost, s));
-  if (NR) HIPCHK(hipMemcpyAsync(E->h_reps_dense.p, E->f_reps.p, (size_t)NR * sizeof(otm_report_rec),
-                                hipMemcpyDeviceToHost, s));
-  if (NW) HIPCHK(hipMemcpyAsync(E->h_ways.p, E->f_ways.p, (size_t)NW * 8, hipMemcpyDeviceToHost, s));
+  const hipMemcpyKind d2h = NT > FETCH_SCAN_MAX ? big_copy_kind(hipMemcpyDeviceToHost) : hipMemcpyDeviceToHost;
+  if (NT) HIPCHK(hipMemcpyAsync(E->h_traces.p, E->f_traces.p, (size_t)NT * sizeof(otm_trace_result), d2h, s));
+  if (NS) HIPCHK(hipMemcpyAsync(E->h_segs.p, E->f_segs.p, (size_t)NS * sizeof(otm_segment), d2h, s));
+  if (NR) HIPCHK(hipMemcpyAsync(E->h_reps_dense.p, E->f_reps.p, (size_t)NR * sizeof(otm_report_rec), d2h, s));
+  if (NW) HIPCHK(hipMemcpyAsync(E->h_ways.p, E->f_ways.p, (size_t)NW * 8, d2h, s));
   HIPCHK(hipStreamSynchronize(s));
   out->n_traces = NT;
   out->n_segments = NS;

@@ -25,6 +25,7 @@ struct otm_engine {
   std::vector<otm_report_rec> g_reps;
   std::vector<int64_t> g_ways;
   int device = 0;
+  int n_clones = 0;  // clones made of this engine (their stream slots)
   hipStream_t stream = nullptr;
   otm::HostGraph host;
   otm::DevGraph g{};

@@ -67,13 +67,17 @@ public final class OtmMatcher {
   private static final MemorySegment ENGINE = create();
 
   private static MemorySegment create() {
-    // one engine per process; the GPU is the one this process owns (LOCAL_RANK / HIP_VISIBLE_DEVICES).
+    // one engine per process.  -Dotm.devices=0,1,...,7 gives this one JVM every listed GPU behind the one
+    // handle (traces go to murmur2(uuid) % ndev, INTEGRATION.md §5); default: the one GPU this process owns
+    // (-Dotm.device, LOCAL_RANK / HIP_VISIBLE_DEVICES).
     // Replaces valhalla.Configure (py/reporter_service.py:279) + SegmentMatcher() per worker (:52).
     try (Arena a = Arena.ofConfined()) {
       MemorySegment cfg = a.allocateFrom(System.getProperty("otm.config", "/etc/otmatch.json"));
-      MemorySegment dev = a.allocateFrom(ValueLayout.JAVA_INT, Integer.getInteger("otm.device", 0));
+      String list = System.getProperty("otm.devices", Integer.toString(Integer.getInteger("otm.device", 0)));
+      int[] ids = java.util.Arrays.stream(list.split(",")).map(String::trim).mapToInt(Integer::parseInt).toArray();
+      MemorySegment dev = a.allocateFrom(ValueLayout.JAVA_INT, ids);
       MemorySegment out = a.allocate(ValueLayout.ADDRESS);
-      int rc = (int) CREATE.invokeExact(cfg, dev, 1, out);
+      int rc = (int) CREATE.invokeExact(cfg, dev, ids.length, out);
       if (rc != 0) {
         MemorySegment msg = (MemorySegment) LAST_ERROR.invokeExact(MemorySegment.NULL);
         throw new IllegalStateException("otm_engine_create: " + msg.reinterpret(4096).getString(0));

@@ -629,7 +629,10 @@ __global__ __launch_bounds__(CAND_TB, OTM_CAND_WAVES) void k_cand_lane(DevGraph 
     // node snap: an entry whose projection snaps to a node becomes that
     // node's candidate (NODE_ENT | first outgoing edge << 4), one per node
     // at the smallest distance
-    for (int m = 0; m < n; ++m) {
+#ifndef OTM_CAND_DIAG
+#define OTM_CAND_DIAG 0  // A/B diagnostics only (wrong results): 1 skips the node snap, 2 also the output projection
+#endif
+    for (int m = 0; m < (OTM_CAND_DIAG ? 0 : n); ++m) {
       const uint32_t em = E[m * S];
       const int32_t e = (int32_t)(em >> 4);
       float sqd, off;
@@ -677,7 +680,7 @@ __global__ __launch_bounds__(CAND_TB, OTM_CAND_WAVES) void k_cand_lane(DevGraph 
       }
       const int32_t e = (int32_t)((em & ~NODE_ENT) >> 4);
       float sqd = qm, off = 0.0f;
-      if (!(em & NODE_ENT)) project(g, e, (int32_t)(em & 15u), lat, lon, ls, sqd, off);
+      if (!(em & NODE_ENT) && OTM_CAND_DIAG < 2) project(g, e, (int32_t)(em & 15u), lat, lon, ls, sqd, off);
       w.cand_edge[CSTRIDE * (p * KMAX + j)] = e;
       w.cand_off[CSTRIDE * (p * KMAX + j)] = off;
       w.cand_emis[CSTRIDE * (p * KMAX + j)] = sqd / ds;

@@ -685,6 +685,7 @@ __global__ __launch_bounds__(CAND_TB, OTM_CAND_WAVES) void k_cand_lane(DevGraph 
       w.cand_off[CSTRIDE * (p * KMAX + j)] = off;
       w.cand_emis[CSTRIDE * (p * KMAX + j)] = sqd / ds;
     }
+
     w.ncand[p] = K;
     c_cells += cells;
     c_ent += ents;
@@ -3368,6 +3369,15 @@ __device__ __forceinline__ bool in_lv(const int64_t* lv, int n, int64_t x) {
 #ifndef OTM_REPORT_WAVES
 #define OTM_REPORT_WAVES 1
 #endif
+// report() launch: 1 = a wave per trace over an LDS copy of its segments
+// (k_report_wave), 0 = a thread per trace (k_report), 2 = the wave form up to
+// REPW_MAX_TRACES traces (two rounds of 8 waves per SIMD), else the thread
+// form.  Measured: config 2 (10k traces) 0.0445 -> 0.0392 ms with the wave
+// form; config 4 (100k traces) 0.106 -> 0.290 ms, so it is not used there.
+#ifndef OTM_REPORT_FORM
+#define OTM_REPORT_FORM 2
+#endif
+constexpr int32_t REPW_MAX_TRACES = 2 * 8 * 4 * 256;
 // report() (py/reporter_service.py:110-215) over one trace's segments, one
 // thread per trace.  Segment times are Python values: a segment without
 // START_VALID / END_VALID carries the int -1 (what the matcher emits), one
@@ -3377,27 +3387,21 @@ __device__ __forceinline__ bool in_lv(const int64_t* lv, int n, int64_t x) {
 // Python's int or float ZeroDivisionError.  The histogram is added in a
 // second pass, only for a trace that ends without an error: the reference
 // posts nothing for a trace whose report() raised.
-__global__ __launch_bounds__(256, OTM_REPORT_WAVES) void k_report(DevBatch b, DevReportCfg rc, DevWork w, DevOut o, int32_t n_seg_total) {
-  if (*w.abort) return;  // a capacity was exceeded: the host redoes the batch
-  const int32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= b.n_traces) return;
-  otm_trace_result r;
+// The serial part of report() for trace t over its segments S (global memory,
+// or the wave's LDS copy in k_report_wave): the trace result r and the reports
+// written to REP, each carrying its reported segment's index in `pad` for the
+// histogram pass (which clears it).  Returns the report count; an error trace
+// (matcher error or ZeroDivisionError) gets code 500 and no reports.
+__device__ int report_walk(int32_t t, const DevBatch& b, const DevReportCfg& rc, const DevWork& w,
+                           const otm_segment* S, otm_trace_result& r, otm_report_rec* REP) {
   r.code = 200;
-  r.error_kind = w.trace_err[t];
-  r.seg_off = (int32_t)o.seg_base[b.trace_off[t]];
-  r.seg_cnt = o.seg_cnt[t];
-  r.rep_off = r.seg_off;
   r.rep_cnt = 0;
   r.shape_used = -1;
   r.successful_count = r.unreported_count = r.discontinuities = r.invalid_speeds = r.unassociated = 0;
   r.successful_length = r.unreported_length = -1;
-  const otm_segment* S = (const otm_segment*)o.segments + r.seg_off;
-  otm_report_rec* REP = (otm_report_rec*)o.reports + r.rep_off;
   if (r.error_kind != 0) {
     r.code = 500;
-    ((otm_trace_result*)o.traces)[t] = r;
-    o.rep_cnt[t] = 0;
-    return;
+    return 0;
   }
   const double end_time = b.time[b.trace_off[t + 1] - 1];
   auto ST = [&](const otm_segment& s) { return (s.flags & OTM_SEG_START_VALID) ? s.start_time : -1.0; };
@@ -3466,38 +3470,102 @@ __global__ __launch_bounds__(256, OTM_REPORT_WAVES) void k_report(DevBatch b, De
   if (zerodiv) {
     r.code = 500;
     r.error_kind = zerodiv;
-    r.rep_cnt = 0;
     r.shape_used = -1;
     r.successful_count = r.unreported_count = r.discontinuities = r.invalid_speeds = r.unassociated = 0;
     r.successful_length = r.unreported_length = -1;
-  } else {
-    // second pass: the speed histogram of the reports the trace returns
-    // (a t1 that is the int -1 of a partial next segment gives no speed)
-    for (int k = 0; k < nrep; ++k) {
-      otm_report_rec& rep = REP[k];
-      const int32_t ps = (int32_t)rep.pad;
-      rep.pad = 0u;
-      if (!o.hist) continue;
-      const double speed = ((double)rep.length / (rep.t1 - rep.t0)) * 3.6;
-      const bool t1_minus1 = (rep.flags & OTM_REP_T1_INT) && rep.t1 == -1.0;
-      const int32_t gi = o.seg_gidx[r.seg_off + ps];
-      if (t1_minus1 || !(speed >= 0.0) || gi < 0) continue;
-      int bin = (int)(speed / (double)o.bin_kph);
-      bin = bin < 0 ? 0 : (bin >= o.nbins ? o.nbins - 1 : bin);
-      atomicAdd(&o.hist[(size_t)gi * o.nbins + bin], 1u);
-      if (o.speed_sum) {
-        // fixed point (1/1000 km/h) so the sums are exact and order-independent
-        atomicAdd(&o.speed_sum[gi], (unsigned long long)(speed * 1000.0 + 0.5));
-      }
-    }
-    r.rep_cnt = nrep;
-    if (w.ctr) {
-      cadd(&w.ctr->segments_out, (unsigned long long)r.seg_cnt);
-      cadd(&w.ctr->reports_out, (unsigned long long)nrep);
-    }
+    return 0;
+  }
+  return nrep;
+}
+
+// The histogram pass over one report: its speed bin and speed sum, for a
+// trace that ended without an error (the reference posts nothing for a trace
+// whose report() raised); a t1 that is the int -1 of a partial next segment
+// gives no speed.  Clears the report's `pad`.
+__device__ __forceinline__ void report_hist(const DevOut& o, int32_t seg_off, otm_report_rec& rep) {
+  const int32_t ps = (int32_t)rep.pad;
+  rep.pad = 0u;
+  if (!o.hist) return;
+  const double speed = ((double)rep.length / (rep.t1 - rep.t0)) * 3.6;
+  const bool t1_minus1 = (rep.flags & OTM_REP_T1_INT) && rep.t1 == -1.0;
+  const int32_t gi = o.seg_gidx[seg_off + ps];
+  if (t1_minus1 || !(speed >= 0.0) || gi < 0) return;
+  int bin = (int)(speed / (double)o.bin_kph);
+  bin = bin < 0 ? 0 : (bin >= o.nbins ? o.nbins - 1 : bin);
+  atomicAdd(&o.hist[(size_t)gi * o.nbins + bin], 1u);
+  if (o.speed_sum) {
+    // fixed point (1/1000 km/h) so the sums are exact and order-independent
+    atomicAdd(&o.speed_sum[gi], (unsigned long long)(speed * 1000.0 + 0.5));
+  }
+}
+
+// report() (py/reporter_service.py:110-215), one thread per trace (the
+// OTM_REPORT_FORM 0 launch).
+__global__ __launch_bounds__(256, OTM_REPORT_WAVES) void k_report(DevBatch b, DevReportCfg rc, DevWork w, DevOut o, int32_t n_seg_total) {
+  if (*w.abort) return;  // a capacity was exceeded: the host redoes the batch
+  const int32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= b.n_traces) return;
+  otm_trace_result r;
+  r.error_kind = w.trace_err[t];
+  r.seg_off = (int32_t)o.seg_base[b.trace_off[t]];
+  r.seg_cnt = o.seg_cnt[t];
+  r.rep_off = r.seg_off;
+  otm_report_rec* REP = (otm_report_rec*)o.reports + r.rep_off;
+  const int nrep = report_walk(t, b, rc, w, (const otm_segment*)o.segments + r.seg_off, r, REP);
+  for (int k = 0; k < nrep; ++k) report_hist(o, r.seg_off, REP[k]);
+  r.rep_cnt = nrep;
+  if (w.ctr && r.code == 200) {
+    cadd(&w.ctr->segments_out, (unsigned long long)r.seg_cnt);
+    cadd(&w.ctr->reports_out, (unsigned long long)nrep);
   }
   ((otm_trace_result*)o.traces)[t] = r;
   o.rep_cnt[t] = r.rep_cnt;
+}
+
+// report(), one wavefront per trace: the lanes copy the trace's segments into
+// LDS with coalesced loads, lane 0 walks them there (the walk is serial: each
+// step's global round trip becomes an LDS read), and the lanes run the
+// histogram pass over the reports in parallel.  A trace with more segments
+// than REPW_CAP is walked out of global memory.
+constexpr int REPW_CAP = 64;
+__global__ __launch_bounds__(TB) void k_report_wave(DevBatch b, DevReportCfg rc, DevWork w, DevOut o, int32_t n_seg_total) {
+  if (*w.abort) return;  // a capacity was exceeded: the host redoes the batch
+  __shared__ unsigned long long sSeg[REPW_CAP * sizeof(otm_segment) / 8];
+  __shared__ int32_t sN;
+  static_assert(sizeof(otm_segment) % 8 == 0, "segment words");
+  constexpr int SW = (int)(sizeof(otm_segment) / 8);  // 8-byte words per segment
+  const int lane = threadIdx.x;
+  for (int32_t t = blockIdx.x; t < b.n_traces; t += gridDim.x) {
+    otm_trace_result r;
+    r.error_kind = w.trace_err[t];
+    r.seg_off = (int32_t)o.seg_base[b.trace_off[t]];
+    r.seg_cnt = o.seg_cnt[t];
+    r.rep_off = r.seg_off;
+    const otm_segment* G = (const otm_segment*)o.segments + r.seg_off;
+    otm_report_rec* REP = (otm_report_rec*)o.reports + r.rep_off;
+    const bool fits = r.seg_cnt <= REPW_CAP;
+    if (fits && r.error_kind == 0) {
+      const unsigned long long* gw = (const unsigned long long*)G;
+      for (int k = lane; k < r.seg_cnt * SW; k += TB) sSeg[k] = gw[k];
+    }
+    __syncthreads();
+    if (lane == 0) {
+      const int nrep = report_walk(t, b, rc, w, fits ? (const otm_segment*)sSeg : G, r, REP);
+      r.rep_cnt = nrep;
+      sN = nrep;
+      if (w.ctr && r.code == 200) {
+        cadd(&w.ctr->segments_out, (unsigned long long)r.seg_cnt);
+        cadd(&w.ctr->reports_out, (unsigned long long)nrep);
+      }
+      ((otm_trace_result*)o.traces)[t] = r;
+      o.rep_cnt[t] = nrep;
+      __threadfence_block();  // the reports, for the other lanes' histogram pass
+    }
+    __syncthreads();
+    const int nrep = sN;
+    for (int k = lane; k < nrep; k += TB) report_hist(o, r.seg_off, REP[k]);
+    __syncthreads();
+  }
 }
 
 // ============================================================== segment bound / compaction
@@ -3787,8 +3855,12 @@ void launch_report(const DevBatch& b, const DevReportCfg& rc, DevWork& w, DevOut
     const int v = e ? std::atoi(e) : 8;  // 0.053 -> 0.050 ms against 64 on config 2
     return v == 16 || v == 32 || v == 64 || v == 128 ? v : 16;
   }();
-  TIMED(KN_REPORT, hipLaunchKernelGGL(k_report, dim3(grid_for(b.n_traces, tb, 1 << 30)), dim3(tb), 0, s, b, rc, w,
-                                      o, 0));
+  if (OTM_REPORT_FORM == 1 || (OTM_REPORT_FORM == 2 && b.n_traces <= REPW_MAX_TRACES))
+    TIMED(KN_REPORT, hipLaunchKernelGGL(k_report_wave, dim3(grid_for(b.n_traces, 1, WAVE_GRID_CAP)), dim3(TB), 0, s,
+                                        b, rc, w, o, 0));
+  else
+    TIMED(KN_REPORT, hipLaunchKernelGGL(k_report, dim3(grid_for(b.n_traces, tb, 1 << 30)), dim3(tb), 0, s, b, rc, w,
+                                        o, 0));
 }
 #undef TIMED
 

@@ -458,7 +458,7 @@ void engine_free(otm_engine* E) {
       &E->in_off,        &E->in_lat,       &E->in_lon,         &E->in_time,        &E->in_acc,     &E->in_blob,
       &E->pt_trace,
       &E->is_col,        &E->prevc,        &E->gc,             &E->ncand,          &E->cand_edge,
-      &E->probe,         &E->col_prev,     &E->trans_off,      &E->trans,          &E->bp,         &E->state,      &E->chosen,
+      &E->probe,         &E->col_prev,     &E->kq_prev,        &E->trans_off,      &E->trans,          &E->bp,         &E->state,      &E->chosen,
       &E->chain_start,   &E->route_dist,   &E->path_off,       &E->path_len,       &E->path_pool,  &E->trace_err,
       &E->overflow_list0, &E->overflow_list, &E->overflow_list2, &E->counters_i32, &E->scan_tmp, &E->snap,   &E->big_key,
       &E->big_lab,       &E->big_inq,      &E->big_fr,         &E->o_traces,       &E->o_seg_cnt,  &E->o_way_cnt,
@@ -514,6 +514,7 @@ static int engine_match_once(otm_engine* E, const DevBatch& b, hipStream_t s, st
   ENS(cand_edge, Pn * KMAX * 4 * CSTRIDE);  // the interleaved {edge, offset, emission} records
   ENS(probe, Pn * 16);
   ENS(col_prev, Pn * 4);
+  ENS(kq_prev, Pn * 4);
   ENS(trans_off, Pn * 8);
   ENS(bp, Pn * KMAX);
   ENS(state, Pn * 4);
@@ -568,6 +569,7 @@ static int engine_match_once(otm_engine* E, const DevBatch& b, hipStream_t s, st
   w.cand_off = P<float>(E->cand_edge) + 1;
   w.cand_emis = P<float>(E->cand_edge) + 2;
   w.col_prev = P<int32_t>(E->col_prev);
+  w.kq_prev = P<int32_t>(E->kq_prev);
   w.trans_off = P<int64_t>(E->trans_off);
   w.bp = P<uint8_t>(E->bp);
   w.state = P<int32_t>(E->state);

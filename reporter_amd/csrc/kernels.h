@@ -148,6 +148,7 @@ struct DevWork {
   float* cand_off;       // view at word 1
   float* cand_emis;      // view at word 2
   int32_t* col_prev;     // [P] linked previous column, -1
+  int32_t* kq_prev;      // [P] candidates of the linked previous column (K3), so K4 reads them with p's own words
   int64_t* trans_off;    // [P+1]
   float* trans;          // [total]
   uint8_t* bp;           // [P*KMAX]

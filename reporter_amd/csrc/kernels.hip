@@ -1116,16 +1116,18 @@ __global__ __launch_bounds__(256) void k_links(DevBatch b, DevParams P, DevWork 
     w.trans_off[p] = 0;
     return;
   }
-  int32_t cp = -1;
+  int32_t cp = -1, kq = 0;
   int64_t cnt = 0;
   if (w.is_col[p]) {
     const int32_t q = w.prevc[p];
     if (q >= 0 && w.ncand[p] > 0 && w.ncand[q] > 0 && w.gc[p] <= P.breakage) {
       cp = q;
-      cnt = (int64_t)w.ncand[q] * (int64_t)w.ncand[p];
+      kq = w.ncand[q];
+      cnt = (int64_t)kq * (int64_t)w.ncand[p];
     }
   }
   w.col_prev[p] = cp;
+  w.kq_prev[p] = kq;
   w.trans_off[p] = cnt;
 }
 
@@ -1776,17 +1778,20 @@ __global__ __launch_bounds__(TB, 8) void k_trans_sub(DevGraph g, DevBatch b, Dev
     bool act = it < end;
     int64_t p = 0;
     if (act) p = LIST ? (int64_t)w.overflow_list2[it] : (ordered ? (int64_t)w.ord.item[it] : it);
-    const int32_t q = act ? w.col_prev[p] : -1;
-    act = act && q >= 0;
+    // the column's words in one round trip (K3 wrote the previous column's
+    // candidate count beside the link)
+    int32_t q = -1;
     int Kp = 0, Kq = 0;
     float gcv = 0.0f;
     int64_t toff = 0;
     if (act) {
+      q = w.col_prev[p];
+      Kq = w.kq_prev[p];
       Kp = w.ncand[p];
       gcv = w.gc[p];
       toff = w.trans_off[p];
-      Kq = w.ncand[q];
     }
+    act = act && q >= 0;
     const float bound = P.factor * gcv;
     const bool idx_ok = X.rmax > 0.0f && bound <= X.rmax;
     const bool wide = WIDE && act && idx_ok && (Kp > KC || Kq > KC);

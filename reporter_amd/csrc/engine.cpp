@@ -586,10 +586,13 @@ static int engine_match_once(otm_engine* E, const DevBatch& b, hipStream_t s, st
   w.overflow_list2 = P<int32_t>(E->overflow_list2);
   w.idx = E->idx;
   w.counters_i32 = P<int32_t>(E->counters_i32);
+  w.snap = P<int32_t>(E->snap);
   w.ctr = E->counting ? E->ctr : nullptr;
   if (E->counting) HIPCHK(hipMemsetAsync(E->ctr, 0, sizeof(DevCounters), s));
   w.abort = P<int32_t>(E->abort_flag);
-  launch_batch_init(w.counters_i32, w.abort, s);  // [5] = candidate spill count
+  // the counters' and abort flag's reset, the spill snapshots and the
+  // transition capacity check ride in K1, K3, K4, K5 and K7 (OTM_FOLD_BOOKKEEPING)
+  if (!fold_bookkeeping()) launch_batch_init(w.counters_i32, w.abort, s);  // [5] = candidate spill count
   Marks mk;
   mk.ev = E->timing ? E->kev : nullptr;
   ENS(ord_tile, Pn * 2);
@@ -613,7 +616,7 @@ static int engine_match_once(otm_engine* E, const DevBatch& b, hipStream_t s, st
   // spill snapshot A: candidate probes the lane tier handed to the wave tier;
   // the counters start over for the transition tiers (links, scan and the
   // capacity check do not touch them)
-  launch_snap(w.counters_i32, P<int32_t>(E->snap), true, s);
+  if (!fold_bookkeeping()) launch_snap(w.counters_i32, P<int32_t>(E->snap), true, s);
   launch_links(b, dp, w, s, mk);
   mk.begin(KN_SCAN_TRANS, s);
   scan_i64(w.trans_off, NP, E->scan_tmp.p, E->scan_tmp.cap, s);
@@ -621,7 +624,7 @@ static int engine_match_once(otm_engine* E, const DevBatch& b, hipStream_t s, st
   ENS(trans, ((size_t)E->trans_cap + 1) * 4);
   w.trans = P<float>(E->trans);
   w.trans_cap = E->trans_cap;
-  launch_cap_check(b, w, s);
+  if (!fold_bookkeeping()) launch_cap_check(b, w, s);
   if ((rc = ensure_big(E, err))) return rc;
   w.big_key = P<uint32_t>(E->big_key);
   w.big_lab = P<unsigned long long>(E->big_lab);
@@ -630,11 +633,11 @@ static int engine_match_once(otm_engine* E, const DevBatch& b, hipStream_t s, st
   launch_transitions(E->g, b, dp, w, s, mk, E->trans_lanes);
   // spill snapshot B: columns per transition tier (Viterbi does not touch
   // the counters; they start over for the route tiers)
-  launch_snap(w.counters_i32, P<int32_t>(E->snap) + 16, true, s);
+  if (!fold_bookkeeping()) launch_snap(w.counters_i32, P<int32_t>(E->snap) + 16, true, s);
   launch_viterbi(b, w, s, mk);
   launch_route(E->g, b, dp, w, s, mk);
   // spill snapshot C: steps per route tier
-  launch_snap(w.counters_i32, P<int32_t>(E->snap) + 32, false, s);
+  if (!fold_bookkeeping()) launch_snap(w.counters_i32, P<int32_t>(E->snap) + 32, false, s);
 
   // Segments, way ids and reports in ONE walk per trace, each trace writing
   // into a region sized by an upper bound (DevOut): every matched point adds

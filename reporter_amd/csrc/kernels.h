@@ -164,6 +164,7 @@ struct DevWork {
   int32_t* overflow_list0; // [P] columns/steps the index could not answer
   int32_t* overflow_list;  // [P] columns/steps the lane tier spilled
   int32_t* overflow_list2; // [P] ... the LDS wave tier spilled
+  int32_t* snap;           // [48] spill snapshots A (after K2), B (after K4), C (after K6)
   int32_t* counters_i32;   // [0] list 1 count, [1] pool used, [2] pool overflow flag, [3] list 2 count,
                            // [4] list 0 count
   int32_t* abort;          // [1] set when a capacity (transition matrices, path pool) was exceeded:
@@ -278,6 +279,8 @@ struct BatchStatus {
 };
 void launch_batch_init(int32_t* counters, int32_t* abort, hipStream_t s);
 void launch_snap(int32_t* counters, int32_t* snap, bool reset, hipStream_t s);
+// batch bookkeeping folded into the stage kernels (no launches of their own)
+bool fold_bookkeeping();
 void launch_status(const int32_t* abort, const int64_t* ttotal, const int32_t* counters, BatchStatus* out,
                    hipStream_t s);
 void launch_row_pack(const int32_t* row_cnt, const int64_t* row_off, IdxRow* rows, int32_t n, hipStream_t s);

@@ -215,6 +215,27 @@ __device__ __forceinline__ int wave_incl_scan(int v, int lane) {
   return v;
 }
 
+// The same bookkeeping folded into the stage kernels: each kernel boundary in
+// a stream costs ~5-10 us, and these ran as five one-wave launches per batch.
+#ifndef OTM_FOLD_BOOKKEEPING
+#define OTM_FOLD_BOOKKEEPING 1
+#endif
+// one thread: spill snapshot k (16 counters), optionally resetting them
+__device__ __forceinline__ void fold_snap(DevWork& w, int k, bool reset) {
+  for (int t = 0; t < 16; ++t) {
+    w.snap[16 * k + t] = w.counters_i32[t];
+    if (reset) w.counters_i32[t] = 0;
+  }
+}
+// every transition kernel's first test: the matrices' total against the
+// buffer (the first kernel to run sets the abort flag for the rest)
+__device__ __forceinline__ bool trans_over_cap(const DevBatch& b, const DevWork& w) {
+  if (!OTM_FOLD_BOOKKEEPING) return false;
+  if (w.trans_off[b.n_points] <= w.trans_cap) return false;
+  *w.abort = 1;
+  return true;
+}
+
 // ============================================================== spatial work order
 __device__ __forceinline__ int hilbert_d(int x, int y) {
   int d = 0;
@@ -341,6 +362,11 @@ __global__ __launch_bounds__(TB) void k_columns(DevGraph g, DevBatch b, DevParam
   __shared__ int32_t sPrev[COL_PTS];
   __shared__ uint8_t sCol[COL_PTS];
   const int lane = threadIdx.x;
+  if (OTM_FOLD_BOOKKEEPING && blockIdx.x == 0) {
+    // the batch's tier counters and abort flag start at zero (k_batch_init)
+    if (lane < 16) w.counters_i32[lane] = 0;
+    if (lane == 0) *w.abort = 0;
+  }
   for (int32_t t = blockIdx.x; t < b.n_traces; t += gridDim.x) {
     const int64_t a = b.trace_off[t], e = b.trace_off[t + 1];
     const int n = (int)(e - a);
@@ -1114,6 +1140,9 @@ __global__ __launch_bounds__(256) void k_links(DevBatch b, DevParams P, DevWork 
   if (p > b.n_points) return;
   if (p == b.n_points) {
     w.trans_off[p] = 0;
+    // spill snapshot A: candidate probes the lane tier handed to the wave
+    // tier; the counters start over for the transition tiers
+    if (OTM_FOLD_BOOKKEEPING) fold_snap(w, 0, true);
     return;
   }
   int32_t cp = -1, kq = 0;
@@ -1164,6 +1193,8 @@ __global__ void k_status(const int32_t* abort, const int64_t* ttotal, const int3
 __global__ void k_cap_check(DevBatch b, DevWork w) {
   if (w.trans_off[b.n_points] > w.trans_cap) *w.abort = 1;
 }
+
+
 
 // ============================================================== bounded search
 // Label-correcting single-source search in one wavefront.  Labels are 64-bit
@@ -1401,7 +1432,7 @@ __device__ __forceinline__ int lane_find(const uint32_t* K, int n, uint32_t v) {
 
 template <int CAP>
 __global__ __launch_bounds__(LANE_TB) void k_trans_lane(DevGraph g, DevBatch b, DevParams P, DevWork w) {
-  if (*w.abort) return;  // a capacity was exceeded: the host redoes the batch
+  if (*w.abort || trans_over_cap(b, w)) return;  // a capacity was exceeded: the host redoes the batch
   __shared__ uint32_t sK[CAP * LANE_TB];
   __shared__ float sD[CAP * LANE_TB];
   __shared__ int32_t sP[CAP * LANE_TB];  // predecessor edges: the routes' turns
@@ -1743,7 +1774,7 @@ __global__ void k_row_pack(const int32_t* row_cnt, const int64_t* row_off, IdxRo
 #endif
 template <int S, bool LIST>
 __global__ __launch_bounds__(TB, 8) void k_trans_sub(DevGraph g, DevBatch b, DevParams P, DevWork w) {
-  if (*w.abort) return;  // a capacity was exceeded: the host redoes the batch
+  if (*w.abort || trans_over_cap(b, w)) return;  // a capacity was exceeded: the host redoes the batch
   constexpr int NS = TB / S;
   // a pair reads its target and source as one 16-byte LDS word each
   constexpr int KC = S >= 16 ? 16 : (S == 8 ? OTM_TRANS_KC8 : OTM_TRANS_KC4);
@@ -2071,7 +2102,7 @@ __global__ __launch_bounds__(256, OTM_ROUTE_WAVES) void k_route_index(DevGraph g
 template <bool BIG>
 __global__ __launch_bounds__(TB) void k_transitions(DevGraph g, DevBatch b, DevParams P, DevWork w,
                                                      int32_t n_overflow) {
-  if (*w.abort) return;
+  if (*w.abort || trans_over_cap(b, w)) return;
   __shared__ uint32_t lkey[BIG ? 1 : LDS_TABLE_CAP];
   __shared__ unsigned long long llab[BIG ? 1 : LDS_TABLE_CAP];
   __shared__ uint32_t linq[BIG ? 1 : LDS_TABLE_CAP];
@@ -2352,6 +2383,9 @@ constexpr int16_t VIT_BP_DEAD = 0x7FFE;   // unreachable state: never walked
 constexpr int VIT_BP_MARK = 0x8000;       // set on the entries the walk visits
 #endif
 __global__ __launch_bounds__(TB, OTM_VIT_WAVES) void k_viterbi(DevBatch b, DevWork w) {
+  // spill snapshot B: columns per transition tier (Viterbi does not touch the
+  // counters; they start over for the route tiers)
+  if (OTM_FOLD_BOOKKEEPING && blockIdx.x == 0 && threadIdx.x == 0) fold_snap(w, 1, true);
   if (*w.abort) return;  // a capacity was exceeded: the host redoes the batch
   __shared__ float sT[VIT_TW];
   __shared__ float sEm[VIT_EW];
@@ -3577,8 +3611,10 @@ __global__ __launch_bounds__(TB) void k_report_wave(DevBatch b, DevReportCfg rc,
 // Traversals a matched point can add: the close of the open traversal, its
 // route's path edges, the re-open (+ the chain's final close): <= 2 + path.
 __global__ __launch_bounds__(256) void k_seg_bound(DevBatch b, DevWork w, int64_t* ub) {
-  if (*w.abort) return;  // a capacity was exceeded: the host redoes the batch
   const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  // spill snapshot C: steps per route tier (kept for the status read)
+  if (OTM_FOLD_BOOKKEEPING && p == b.n_points) fold_snap(w, 2, false);
+  if (*w.abort) return;  // a capacity was exceeded: the host redoes the batch
   if (p > b.n_points) return;
   int64_t v = 0;
   if (p < b.n_points && w.is_col[p] && w.state[p] >= 0) {
@@ -3776,6 +3812,7 @@ void launch_status(const int32_t* abort, const int64_t* ttotal, const int32_t* c
                    hipStream_t s) {
   hipLaunchKernelGGL(k_status, dim3(1), dim3(64), 0, s, abort, ttotal, counters, out);
 }
+bool fold_bookkeeping() { return OTM_FOLD_BOOKKEEPING != 0; }
 void launch_cap_check(const DevBatch& b, DevWork& w, hipStream_t s) {
   hipLaunchKernelGGL(k_cap_check, dim3(1), dim3(1), 0, s, b, w);
 }

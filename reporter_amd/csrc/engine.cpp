@@ -746,6 +746,19 @@ hipMemcpyKind big_copy_kind(hipMemcpyKind k) {
   return nocu ? hipMemcpyDeviceToDeviceNoCU : k;
 }
 
+// OTM_COPY_SERIAL=1: the large host<->device copies of all batch contexts in
+// the process take turns (issued and completed under one lock), so that each
+// runs alone on a copy engine instead of as blit kernels beside the others'
+// (an A/B knob for the host-inclusive leg).
+static std::mutex g_copy_mu;
+static bool copy_serial() {
+  static const bool on = [] {
+    const char* v = std::getenv("OTM_COPY_SERIAL");
+    return v && *v == '1';
+  }();
+  return on;
+}
+
 int engine_match_host(otm_engine* E, const otm_batch* in, std::string* err) {
   const int32_t NT = in->n_traces;
   if (NT < 0 || !in->trace_off) {
@@ -798,11 +811,16 @@ int engine_match_host(otm_engine* E, const otm_batch* in, std::string* err) {
     return engine_match(E, b, s, err);
   }
   const hipMemcpyKind h2d = big_copy_kind(hipMemcpyHostToDevice);
-  HIPCHK(hipMemcpyAsync(E->in_off.p, in->trace_off, b_off, hipMemcpyHostToDevice, s));
-  HIPCHK(hipMemcpyAsync(E->in_lat.p, in->lat, b_pt, h2d, s));
-  HIPCHK(hipMemcpyAsync(E->in_lon.p, in->lon, b_pt, h2d, s));
-  HIPCHK(hipMemcpyAsync(E->in_time.p, in->time, b_tm, h2d, s));
-  HIPCHK(hipMemcpyAsync(E->in_acc.p, in->accuracy, b_pt, h2d, s));
+  {
+    std::unique_lock<std::mutex> lk(g_copy_mu, std::defer_lock);
+    if (copy_serial()) lk.lock();
+    HIPCHK(hipMemcpyAsync(E->in_off.p, in->trace_off, b_off, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(E->in_lat.p, in->lat, b_pt, h2d, s));
+    HIPCHK(hipMemcpyAsync(E->in_lon.p, in->lon, b_pt, h2d, s));
+    HIPCHK(hipMemcpyAsync(E->in_time.p, in->time, b_tm, h2d, s));
+    HIPCHK(hipMemcpyAsync(E->in_acc.p, in->accuracy, b_pt, h2d, s));
+    if (copy_serial()) HIPCHK(hipStreamSynchronize(s));
+  }
   b.trace_off = (const int64_t*)E->in_off.p;
   b.lat = (const float*)E->in_lat.p;
   b.lon = (const float*)E->in_lon.p;
@@ -872,6 +890,11 @@ int engine_fetch(otm_engine* E, otm_results* out, std::string* err) {
   if ((rc = ensure_pinned(E->h_reps_dense, ((size_t)NR + 1) * sizeof(otm_report_rec), err))) return rc;
   if ((rc = ensure_pinned(E->h_ways, ((size_t)NW + 1) * 8, err))) return rc;
   const hipMemcpyKind d2h = NT > FETCH_SCAN_MAX ? big_copy_kind(hipMemcpyDeviceToHost) : hipMemcpyDeviceToHost;
+  std::unique_lock<std::mutex> lk(g_copy_mu, std::defer_lock);
+  if (copy_serial() && NT > FETCH_SCAN_MAX) {
+    HIPCHK(hipStreamSynchronize(s));  // the compaction first: the lock covers only the copies
+    lk.lock();
+  }
   if (NT) HIPCHK(hipMemcpyAsync(E->h_traces.p, E->f_traces.p, (size_t)NT * sizeof(otm_trace_result), d2h, s));
   if (NS) HIPCHK(hipMemcpyAsync(E->h_segs.p, E->f_segs.p, (size_t)NS * sizeof(otm_segment), d2h, s));
   if (NR) HIPCHK(hipMemcpyAsync(E->h_reps_dense.p, E->f_reps.p, (size_t)NR * sizeof(otm_report_rec), d2h, s));

@@ -34,4 +34,10 @@ nocu)
   BENCH_EXTRA="--inflight 2" run nocu_2 OTM_COPY_NOCU=1
   BENCH_EXTRA="--inflight 4" run nocu_4 OTM_COPY_NOCU=1
   ;;
+serial)
+  run base OTM_NOP=1
+  run serial OTM_COPY_SERIAL=1
+  BENCH_EXTRA="--inflight 4" run serial_4 OTM_COPY_SERIAL=1
+  BENCH_EXTRA="--inflight 2" run serial_2 OTM_COPY_SERIAL=1
+  ;;
 esac

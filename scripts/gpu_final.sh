@@ -16,3 +16,5 @@ PMC_STATS_CSV=$R/$O/prof1/run_kernel_stats.csv bash scripts/pmc.sh $O/pmc $TAG
 PMC_BENCH_ARGS="--config 4" PMC_STATS_CSV=$R/$O/prof1c4/run_kernel_stats.csv bash scripts/pmc.sh $O/pmc4 ${TAG}_c4
 timeout -k 10 400 python -u bench.py --traffic-json $O/pmc/pmc_traffic_$TAG.json > $O/bench.json 2> $O/bench.err
 timeout -k 10 500 python -u bench.py --config 4 --steps 10 --warmup 2 --traffic-json $O/pmc4/pmc_traffic_${TAG}_c4.json > $O/bench_c4.json 2> $O/bench_c4.err
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
+timeout -k 10 600 python -u bench.py --config 3 --steps 5 --warmup 2 --no-cpu-baseline > $O/bench_c3.json 2> $O/bench_c3.err

@@ -162,6 +162,17 @@ int otm_encode_request(const char* uuid, int n, const float* lat,
                        const float* lon, const int64_t* time,
                        const int32_t* accuracy, char** out, size_t* out_len);
 
+/* The points of one /report request body, as the matcher reads them
+ * (parse_trace + handle_request validation, py/reporter_service.py:85-106,
+ * 218-234, then each point's lat, lon, time and accuracy).  fast = 1 takes
+ * the DOM-free reader of the Java batcher's own bytes and returns -2 for a
+ * body outside its grammar (a request batch then takes the DOM path); fast =
+ * 0 always parses the DOM.  Returns the point count (at most max_points are
+ * written) with the uuid copied when it is a JSON string (NUL-terminated,
+ * truncated to uuid_cap), -1 for a request the DOM path rejects. */
+int otm_request_points(const char* req, size_t len, int fast, float* lat, float* lon, double* time, float* acc,
+                       int max_points, char* uuid, size_t uuid_cap);
+
 /* ----------------------------------------------------------- binary level */
 
 /* A batch of traces, structure of arrays.  Points of trace t are

@@ -117,6 +117,7 @@ def _declare(L):
     sig = {
         "otm_engine_create": (C.c_int, [C.c_char_p, C.POINTER(C.c_int), C.c_int, pp]),
         "otm_engine_members": (C.c_int, [vp]),
+        "otm_request_points": (C.c_int, [C.c_char_p, sz, C.c_int, vp, vp, vp, vp, C.c_int, C.c_char_p, sz]),
         "otm_engine_member": (vp, [vp, C.c_int]),
         "otm_engine_destroy": (None, [vp]),
         "otm_last_error": (C.c_char_p, [vp]),

@@ -8,6 +8,7 @@
 #include <cstring>
 #include <fstream>
 #include <sstream>
+#include <thread>
 
 #include "engine.h"
 #include "json.h"
@@ -24,6 +25,46 @@ int fail(int code, const std::string& msg) {
   t_err = msg;
   otm::set_thread_error(msg);
   return code;
+}
+
+// Host threads for the per-request work of a large request batch (JSON
+// parse, point extraction, response writing): the machine's cores, at most 16,
+// and at least 256 requests per thread (OTM_HOST_THREADS / OTM_HOST_CHUNK
+// override both, read per call).
+size_t host_threads(size_t n) {
+  size_t cap, chunk = 256;
+  if (const char* v = std::getenv("OTM_HOST_THREADS")) {
+    cap = (size_t)std::max(1, std::atoi(v));
+  } else {
+    const unsigned hw = std::thread::hardware_concurrency();
+    cap = (size_t)std::min(16u, hw ? hw : 1u);
+  }
+  if (const char* v = std::getenv("OTM_HOST_CHUNK")) chunk = (size_t)std::max(1, std::atoi(v));
+  return std::max<size_t>(1, std::min(cap, (n + chunk - 1) / chunk));
+}
+// fn(a, e) over [0, n) in contiguous chunks, one per thread (the caller's the first)
+template <class F>
+void par_for(size_t n, F fn) {
+  const size_t T = host_threads(n);
+  if (T <= 1) {
+    fn((size_t)0, n);
+    return;
+  }
+  const size_t per = (n + T - 1) / T;
+  std::vector<std::thread> th;
+  for (size_t i = 1; i < T; ++i) {
+    const size_t a = i * per, e = std::min(n, a + per);
+    if (a < e) th.emplace_back([&fn, a, e] { fn(a, e); });
+  }
+  fn((size_t)0, std::min(n, per));
+  for (auto& t : th) t.join();
+}
+
+// the Java request bytes read without a DOM (otm::fast_request); OTM_FAST_JSON=0
+// sends every body through the DOM (A/B and the parity tests)
+bool fast_requests() {
+  const char* v = std::getenv("OTM_FAST_JSON");
+  return !(v && *v == '0');
 }
 
 char* dup_out(const std::string& s, size_t* n) {
@@ -91,30 +132,55 @@ bool fill_device_params(otm_engine* E, std::string* err) {
   return true;
 }
 
+// One request of a batch: its DOM (parse_request), or -- for the Java
+// batcher's own bytes -- its points and uuid read directly (fast_request).
+struct Req {
+  Value dom;
+  otm::TracePoints tp;
+  std::string uuid;
+  bool fast = false;
+};
+
 // One GPU batch over parsed requests: results[k] -> (code, body)
-void run_requests(otm_engine* E, std::vector<Value>& traces, std::vector<int>& codes, std::vector<std::string>& bodies,
+void run_requests(otm_engine* E, std::vector<Req>& rq, std::vector<int>& codes, std::vector<std::string>& bodies,
                   const std::vector<int>& todo, bool match_only) {
-  // points of every request that passed validation
-  std::vector<int64_t> off(1, 0);
-  std::vector<float> lat, lon, acc;
-  std::vector<double> tm;
-  std::vector<int> which;  // request index of each batch trace
-  for (int k : todo) {
-    otm::TracePoints tp;
-    std::string perr;
-    if (!otm::extract_points(traces[(size_t)k], &tp, &perr)) {
-      codes[(size_t)k] = 500;
-      bodies[(size_t)k] = otm::error_body(perr);
-      continue;
+  // points of every request that passed validation (extracted in parallel,
+  // then laid out in request order)
+  std::vector<uint8_t> ok(todo.size(), 0);
+  par_for(todo.size(), [&](size_t a, size_t e) {
+    for (size_t i = a; i < e; ++i) {
+      const int k = todo[i];
+      std::string perr;
+      if (rq[(size_t)k].fast || otm::extract_points(rq[(size_t)k].dom, &rq[(size_t)k].tp, &perr)) {
+        ok[i] = 1;
+      } else {
+        codes[(size_t)k] = 500;
+        bodies[(size_t)k] = otm::error_body(perr);
+      }
     }
-    lat.insert(lat.end(), tp.lat.begin(), tp.lat.end());
-    lon.insert(lon.end(), tp.lon.begin(), tp.lon.end());
-    acc.insert(acc.end(), tp.acc.begin(), tp.acc.end());
-    tm.insert(tm.end(), tp.time.begin(), tp.time.end());
-    off.push_back((int64_t)lat.size());
-    which.push_back(k);
-  }
+  });
+  std::vector<int64_t> off(1, 0);
+  std::vector<int> which;  // request index of each batch trace
+  for (size_t i = 0; i < todo.size(); ++i)
+    if (ok[i]) {
+      off.push_back(off.back() + (int64_t)rq[(size_t)todo[i]].tp.lat.size());
+      which.push_back(todo[i]);
+    }
   if (which.empty()) return;
+  const size_t np = (size_t)off.back();
+  std::vector<float> lat(np), lon(np), acc(np);
+  std::vector<double> tm(np);
+  par_for(which.size(), [&](size_t a, size_t e) {
+    for (size_t n = a; n < e; ++n) {
+      otm::TracePoints& tp = rq[(size_t)which[n]].tp;
+      const size_t o = (size_t)off[n];
+      std::copy(tp.lat.begin(), tp.lat.end(), lat.begin() + o);
+      std::copy(tp.lon.begin(), tp.lon.end(), lon.begin() + o);
+      std::copy(tp.acc.begin(), tp.acc.end(), acc.begin() + o);
+      std::copy(tp.time.begin(), tp.time.end(), tm.begin() + o);
+      tp = otm::TracePoints();
+    }
+  });
   otm_batch b;
   b.n_traces = (int32_t)which.size();
   b.n_points = off.back();
@@ -132,34 +198,43 @@ void run_requests(otm_engine* E, std::vector<Value>& traces, std::vector<int>& c
   if (!E->members.empty()) {
     shard.resize(which.size(), 0);
     for (size_t n = 0; n < which.size(); ++n) {
-      const Value* u = traces[(size_t)which[n]].get("uuid");
-      if (u && u->kind == Kind::Str) shard[n] = otm::shard_of(u->s.data(), u->s.size(), (int)E->members.size());
+      const Req& q = rq[(size_t)which[n]];
+      const Value* u = q.fast ? nullptr : q.dom.get("uuid");
+      if (q.fast) shard[n] = otm::shard_of(q.uuid.data(), q.uuid.size(), (int)E->members.size());
+      else if (u && u->kind == Kind::Str) shard[n] = otm::shard_of(u->s.data(), u->s.size(), (int)E->members.size());
     }
   }
   {
     std::lock_guard<std::mutex> lk(E->mu);
     rc = otm::match_host_fetch(E, &b, shard.empty() ? nullptr : shard.data(), &r, &err);
     if (!rc) {
-      for (size_t n = 0; n < which.size(); ++n) {
-        const int k = which[n];
-        std::string out;
-        if (match_only) {
-          const otm_trace_result& tr = r.traces[n];
-          if (tr.code != 200 && tr.error_kind != OTM_TERR_ZERODIV) {
-            codes[(size_t)k] = 500;
-            bodies[(size_t)k] = otm::error_body(otm::trace_error_text(tr.error_kind));
+      // the responses in parallel (each writes its own slot), the reference's
+      // stderr lines after, in request order
+      par_for(which.size(), [&](size_t a, size_t e) {
+        for (size_t n = a; n < e; ++n) {
+          const int k = which[n];
+          std::string out;
+          if (match_only) {
+            const otm_trace_result& tr = r.traces[n];
+            if (tr.code != 200 && tr.error_kind != OTM_TERR_ZERODIV) {
+              codes[(size_t)k] = 500;
+              bodies[(size_t)k] = otm::error_body(otm::trace_error_text(tr.error_kind));
+            } else {
+              otm::write_match_json(r, (int32_t)n, &out);
+              codes[(size_t)k] = 200;
+              bodies[(size_t)k] = std::move(out);
+            }
           } else {
-            otm::write_match_json(r, (int32_t)n, &out);
-            codes[(size_t)k] = 200;
+            codes[(size_t)k] = otm::write_report_response(r, (int32_t)n, &out);
             bodies[(size_t)k] = std::move(out);
           }
-        } else {
-          codes[(size_t)k] = otm::write_report_response(r, (int32_t)n, &out);
-          bodies[(size_t)k] = std::move(out);
+        }
+      });
+      if (!match_only)
+        for (size_t n = 0; n < which.size(); ++n) {
           const int inv = r.traces[n].code == 200 ? r.traces[n].invalid_speeds : 0;
           for (int q = 0; q < inv; ++q) std::fputs("Speed exceeds 200kph\n", stderr);
         }
-      }
     }
   }
   if (rc) {
@@ -173,21 +248,30 @@ void run_requests(otm_engine* E, std::vector<Value>& traces, std::vector<int>& c
 
 void report_many(otm_engine* E, int n, const char* const* reqs, const size_t* lens, int* codes, char** resps,
                  size_t* resp_lens) {
-  std::vector<Value> traces((size_t)n);
+  std::vector<Req> rq((size_t)n);
   std::vector<int> c((size_t)n, 0);
   std::vector<std::string> bodies((size_t)n);
   std::vector<int> todo;
-  for (int k = 0; k < n; ++k) {
-    int code = otm::parse_request("/report", std::string_view(reqs[k], lens[k]), &traces[(size_t)k],
-                                  &bodies[(size_t)k]);
-    if (code) c[(size_t)k] = code;
-    else todo.push_back(k);
-  }
-  run_requests(E, traces, c, bodies, todo, false);
-  for (int k = 0; k < n; ++k) {
-    codes[k] = c[(size_t)k];
-    resps[k] = dup_out(bodies[(size_t)k], &resp_lens[k]);
-  }
+  par_for((size_t)n, [&](size_t a, size_t e) {
+    for (size_t k = a; k < e; ++k) {
+      const std::string_view body(reqs[k], lens[k]);
+      if (fast_requests() && otm::fast_request(body, &rq[k].tp, &rq[k].uuid)) {
+        rq[k].fast = true;
+        continue;
+      }
+      const int code = otm::parse_request("/report", body, &rq[k].dom, &bodies[k]);
+      if (code) c[k] = code;
+    }
+  });
+  for (int k = 0; k < n; ++k)
+    if (!c[(size_t)k]) todo.push_back(k);
+  run_requests(E, rq, c, bodies, todo, false);
+  par_for((size_t)n, [&](size_t a, size_t e) {
+    for (size_t k = a; k < e; ++k) {
+      codes[k] = c[k];
+      resps[k] = dup_out(bodies[k], &resp_lens[k]);
+    }
+  });
 }
 
 void worker_loop(otm_engine* E) {
@@ -411,20 +495,55 @@ int otm_report_batch(otm_engine* E, int n, const char* const* reqs, const size_t
   return OTM_OK;
 }
 
+int otm_request_points(const char* req, size_t len, int fast, float* lat, float* lon, double* time, float* acc,
+                       int max_points, char* uuid, size_t uuid_cap) {
+  if (!req) return fail(OTM_EINVAL, "req is NULL");
+  otm::TracePoints tp;
+  std::string u;
+  bool have_uuid = false;
+  if (fast) {
+    if (!otm::fast_request(std::string_view(req, len), &tp, &u)) return -2;
+    have_uuid = true;
+  } else {
+    Value dom;
+    std::string resp, err;
+    if (otm::parse_request("/report", std::string_view(req, len), &dom, &resp)) return -1;
+    if (!otm::extract_points(dom, &tp, &err)) return -1;
+    const Value* uv = dom.get("uuid");
+    if (uv && uv->kind == Kind::Str) {
+      u = uv->s;
+      have_uuid = true;
+    }
+  }
+  const int n = (int)tp.lat.size();
+  for (int k = 0; k < n && k < max_points; ++k) {
+    if (lat) lat[k] = tp.lat[(size_t)k];
+    if (lon) lon[k] = tp.lon[(size_t)k];
+    if (time) time[k] = tp.time[(size_t)k];
+    if (acc) acc[k] = tp.acc[(size_t)k];
+  }
+  if (uuid && uuid_cap) {
+    const size_t m = have_uuid ? std::min(u.size(), uuid_cap - 1) : 0;
+    std::memcpy(uuid, u.data(), m);
+    uuid[m] = 0;
+  }
+  return n;
+}
+
 int otm_match_json(otm_engine* E, const char* req, size_t len, char** resp, size_t* resp_len) {
-  std::vector<Value> traces(1);
+  std::vector<Req> rq(1);
   std::vector<int> codes(1, 0);
   std::vector<std::string> bodies(1);
   std::string perr;
-  if (!otm::json::parse(std::string_view(req, len), &traces[0], &perr)) {
+  if (!otm::json::parse(std::string_view(req, len), &rq[0].dom, &perr)) {
     *resp = dup_out(otm::error_body(perr), resp_len);
     return 500;
   }
-  if (traces[0].kind != Kind::Obj) {
+  if (rq[0].dom.kind != Kind::Obj) {
     *resp = dup_out(otm::error_body("request must be a JSON object"), resp_len);
     return 500;
   }
-  run_requests(E, traces, codes, bodies, {0}, true);
+  run_requests(E, rq, codes, bodies, {0}, true);
   *resp = dup_out(bodies[0], resp_len);
   return codes[0];
 }

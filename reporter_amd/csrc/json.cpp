@@ -209,8 +209,13 @@ struct Parser {
     const char* e = t.data() + k;
     if (flt) {
       v->kind = Kind::Float;
-      std::string tmp(b, e);
-      v->f = std::strtod(tmp.c_str(), nullptr);
+      // correctly rounded like strtod (float('...')), without a temporary
+      // string; overflow / underflow (inf, subnormal) go through strtod
+      auto r = std::from_chars(b, e, v->f);
+      if (r.ec != std::errc()) {
+        std::string tmp(b, e);
+        v->f = std::strtod(tmp.c_str(), nullptr);
+      }
     } else {
       v->kind = Kind::Int;
       auto r = std::from_chars(b, e, v->i);
@@ -235,6 +240,9 @@ struct Parser {
     }
     if (c == '{') {
       v->kind = Kind::Obj;
+      // a trace point has 3-4 keys: one allocation each for keys and values
+      v->keys.reserve(4);
+      v->items.reserve(4);
       ++i;
       ws();
       if (i < t.size() && t[i] == '}') {

@@ -1,6 +1,8 @@
 // report.cpp -- see report.h.
 #include "report.h"
 
+#include <charconv>
+
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -515,6 +517,114 @@ bool extract_points(const Value& trace, TracePoints* out, std::string* err) {
     out->acc[k] = num(pt.get("accuracy"), &ac) ? (float)ac : 0.0f;
   }
   return true;
+}
+
+bool fast_request(std::string_view b, TracePoints* out, std::string* uuid) {
+  const size_t n = b.size();
+  size_t i = 0;
+  auto lit = [&](std::string_view w) {
+    if (b.compare(i, w.size(), w) != 0) return false;
+    i += w.size();
+    return true;
+  };
+  auto digit = [&](size_t k) { return k < n && b[k] >= '0' && b[k] <= '9'; };
+  // a JSON number as json.loads + float() read it (int -> exact double,
+  // float -> correctly rounded)
+  auto num = [&](double* d) {
+    const size_t a = i;
+    if (i < n && b[i] == '-') ++i;
+    if (!digit(i)) return false;
+    if (b[i] == '0') {
+      ++i;
+    } else {
+      while (digit(i)) ++i;
+    }
+    bool flt = false;
+    if (i < n && b[i] == '.') {
+      if (!digit(i + 1)) return false;
+      flt = true;
+      ++i;
+      while (digit(i)) ++i;
+    }
+    if (i < n && (b[i] == 'e' || b[i] == 'E')) return false;
+    const char* s = b.data() + a;
+    const char* e = b.data() + i;
+    if (flt) {
+      const auto r = std::from_chars(s, e, *d);
+      return r.ec == std::errc() && r.ptr == e;
+    }
+    if (i - a > 18) return false;
+    int64_t v = 0;
+    const auto r = std::from_chars(s, e, v);
+    if (r.ec != std::errc() || r.ptr != e) return false;
+    *d = (double)v;
+    return true;
+  };
+  out->lat.clear();
+  out->lon.clear();
+  out->time.clear();
+  out->acc.clear();
+  if (!lit("{")) return false;
+  bool have_uuid = false, have_trace = false;
+  while (true) {
+    if (lit("\"uuid\":\"")) {
+      if (have_uuid) return false;
+      have_uuid = true;
+      const size_t a = i;
+      while (i < n && b[i] != '"') {
+        const unsigned char c = (unsigned char)b[i];
+        if (c < 0x20 || c > 0x7e || c == '\\') return false;
+        ++i;
+      }
+      if (i >= n) return false;
+      uuid->assign(b.data() + a, i - a);
+      ++i;
+    } else if (lit("\"trace\":[")) {
+      if (have_trace) return false;
+      have_trace = true;
+      while (true) {
+        if (!lit("{")) return false;
+        bool hl = false, ho = false, ht = false, ha = false;
+        double la = 0.0, lo = 0.0, ti = 0.0, ac = 0.0;
+        while (true) {
+          if (lit("\"lat\":")) {
+            if (hl || !num(&la)) return false;
+            hl = true;
+          } else if (lit("\"lon\":")) {
+            if (ho || !num(&lo)) return false;
+            ho = true;
+          } else if (lit("\"time\":")) {
+            if (ht || !num(&ti)) return false;
+            ht = true;
+          } else if (lit("\"accuracy\":")) {
+            if (ha || !num(&ac)) return false;
+            ha = true;
+          } else {
+            return false;
+          }
+          if (lit(",")) continue;
+          if (lit("}")) break;
+          return false;
+        }
+        if (!hl || !ho || !ht) return false;
+        // extract_points' conversions
+        out->lat.push_back((float)la);
+        out->lon.push_back((float)lo);
+        out->time.push_back(ti);
+        out->acc.push_back(ha ? (float)ac : 0.0f);
+        if (lit(",")) continue;
+        if (lit("]")) break;
+        return false;
+      }
+      if (out->lat.size() < 2) return false;
+    } else {
+      return false;
+    }
+    if (lit(",")) continue;
+    if (lit("}")) break;
+    return false;
+  }
+  return have_uuid && have_trace && i == n;
 }
 
 // ------------------------------------------------------------ typed segments

@@ -25,6 +25,14 @@ struct TracePoints {
   std::vector<double> time;
 };
 bool extract_points(const json::Value& trace, TracePoints* out, std::string* err);
+// The Java batcher's request bytes (Batch.java:52-61, Point.java:39-45) read
+// straight into points, without a DOM: {"uuid":"<printable ASCII>","trace":[
+// {"lat":n,"lon":n,"time":n[,"accuracy":n]}, ... >= 2 points]} with the keys
+// in any order, each once, no whitespace, plain numbers (no exponent, ints of
+// at most 18 digits).  Returns false (and the caller takes parse_request +
+// extract_points) on anything else, so every accepted body gives exactly the
+// points, uuid and outcome of the DOM path.
+bool fast_request(std::string_view body, TracePoints* out, std::string* uuid);
 
 // Typed writers over one trace of a results set.
 void write_match_json(const otm_results& r, int32_t t, std::string* out);

@@ -363,3 +363,28 @@ def test_fetch_is_idempotent(small_graph):
         r3 = eng.fetch()
     for k in ("traces", "segments", "reports", "way_ids"):
         assert getattr(r1, k).tobytes() == getattr(r2, k).tobytes() == getattr(r3, k).tobytes(), k
+
+
+def test_json_report_path_host_threads(small_graph, oracle, monkeypatch):
+    """otm_report_batch's parse / point extraction / response writing split over
+    host threads (forced here with tiny chunks): byte-equal to the oracle, in
+    request order, malformed bodies included."""
+    b = synth.make_traces(small_graph, 120, 40, seed=19)
+    bodies = []
+    for t in range(120):
+        a, e = b["trace_off"][t], b["trace_off"][t + 1]
+        bodies.append(encode_request("car%d" % t, b["lat"][a:e], b["lon"][a:e], b["time"][a:e].astype(np.int64),
+                                     b["accuracy"][a:e].astype(np.int32)))
+        if t % 17 == 3:
+            bodies.append(b'{"uuid":"x","trace":[{"lat":1}]}')
+        if t % 23 == 5:
+            bodies.append(b"[]")
+    g = oracle.Graph(small_graph)
+    monkeypatch.setenv("OTM_HOST_THREADS", "7")
+    monkeypatch.setenv("OTM_HOST_CHUNK", "5")
+    with Engine(graph_path=small_graph) as eng:
+        got = eng.report_batch(bodies)
+        for body, (code, resp) in zip(bodies, got):
+            assert (code, resp) == oracle.handle_request(g, body), body[:80]
+        monkeypatch.setenv("OTM_HOST_THREADS", "1")
+        assert eng.report_batch(bodies) == got

@@ -86,6 +86,8 @@ def parse():
     ap.add_argument("--no-check", action="store_true", help="skip the untimed oracle pass (agreement, bytes)")
     ap.add_argument("--traffic-json", default=None,
                     help="PMC traffic summary (scripts/pmc_summary.py); default: the committed one for --config")
+    ap.add_argument("--json-calls", type=int, default=5,
+                    help="calls of the JSON leg (otm_report_batch over the batch's request bodies; 0: skip)")
     ap.add_argument("--host-stagger-ms", type=float, default=0.0,
                     help="host-inclusive leg: in-flight worker i starts i x this many ms late (A/B of phase drift)")
     ap.add_argument("--inflight", type=int, default=3,
@@ -372,6 +374,49 @@ def main():
         hist.zero_()
         speed_sum.zero_()
 
+    # ---- JSON leg: the literal drop-in call, otm_report_batch over the Java
+    # batcher's request bytes (one body per vehicle, Batch.java:52-61) to the
+    # exact /report response bodies; host parse / write on the library's host
+    # threads, one call at a time; not `value`
+    json_leg = None
+    if args.json_calls > 0:
+        import ctypes as C
+        from reporter_amd import encode_request
+        L = _lib.lib()
+        off = batch["trace_off"]
+        bodies = [encode_request(str(int(v)), batch["lat"][off[t]:off[t + 1]], batch["lon"][off[t]:off[t + 1]],
+                                 batch["time"][off[t]:off[t + 1]].astype(np.int64),
+                                 batch["accuracy"][off[t]:off[t + 1]].astype(np.int32))
+                  for t, v in enumerate(ids)]
+        nb = len(bodies)
+        arr = (C.c_char_p * nb)(*bodies)
+        lens = (C.c_size_t * nb)(*[len(x) for x in bodies])
+        outs = (C.c_void_p * nb)()
+        olens = (C.c_size_t * nb)()
+        codes = (C.c_int * nb)()
+
+        def json_call():
+            if L.otm_report_batch(eng.h, nb, arr, lens, outs, olens, codes) != 0:
+                raise RuntimeError("otm_report_batch: %s" % _lib.last_error())
+            nbytes = 0
+            for i in range(nb):
+                nbytes += olens[i]
+                L.otm_free(outs[i])
+            return nbytes
+
+        json_call()
+        tj = time.perf_counter()
+        for _ in range(args.json_calls):
+            resp_bytes = json_call()
+        jel = (time.perf_counter() - tj) / args.json_calls
+        json_leg = {"value": P / jel, "unit": "points/s", "ms_per_call": jel * 1e3, "calls": args.json_calls,
+                    "requests_per_call": nb, "request_bytes": int(sum(len(x) for x in bodies)),
+                    "response_bytes": int(resp_bytes), "status_200": int(sum(1 for i in range(nb) if codes[i] == 200)),
+                    "includes": "otm_report_batch: request JSON parse (the Java bytes without a DOM), H2D, all "
+                                "kernels, compaction, D2H, response JSON writing; one call at a time"}
+        hist.zero_()
+        speed_sum.zero_()
+
     # ---- untimed: the CPU oracle over this rank's whole batch -> agreement
     # with the GPU result and the algorithmic bytes of every stage
     res = eng.fetch()
@@ -516,6 +561,7 @@ def main():
             "spill": spill,
             "cpu_baseline": cpu,
             "host_inclusive": host_leg,
+            "json_report": json_leg,
             "agreement": agreement,
             "hip_runtime": _lib.runtime_info(),
         }

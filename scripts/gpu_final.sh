@@ -10,8 +10,8 @@ O=gpurun_out/$TAG
 mkdir -p $R/$O
 cd $R
 timeout -k 10 700 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1
-(cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$O/prof1 -o run -- python3 $R/bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-check --host-steps 0 --inflight 1 > $R/$O/prof1.log 2>&1)
-(cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$O/prof1c4 -o run -- python3 $R/bench.py --config 4 --steps 5 --warmup 2 --no-cpu-baseline --no-check --host-steps 0 --inflight 1 > $R/$O/prof1c4.log 2>&1)
+(cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$O/prof1 -o run -- python3 $R/bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-check --host-steps 0 --json-calls 0 --inflight 1 > $R/$O/prof1.log 2>&1)
+(cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$O/prof1c4 -o run -- python3 $R/bench.py --config 4 --steps 5 --warmup 2 --no-cpu-baseline --no-check --host-steps 0 --json-calls 0 --inflight 1 > $R/$O/prof1c4.log 2>&1)
 PMC_STATS_CSV=$R/$O/prof1/run_kernel_stats.csv bash scripts/pmc.sh $O/pmc $TAG
 PMC_BENCH_ARGS="--config 4" PMC_STATS_CSV=$R/$O/prof1c4/run_kernel_stats.csv bash scripts/pmc.sh $O/pmc4 ${TAG}_c4
 timeout -k 10 400 python -u bench.py --traffic-json $O/pmc/pmc_traffic_$TAG.json > $O/bench.json 2> $O/bench.err

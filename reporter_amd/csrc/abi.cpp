@@ -2,6 +2,7 @@
 #include <dlfcn.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -132,6 +133,16 @@ bool fill_device_params(otm_engine* E, std::string* err) {
   return true;
 }
 
+// OTM_JSON_PROFILE=1: one stderr line per request batch with its phases (ms)
+double now_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+bool json_profile() {
+  const char* v = std::getenv("OTM_JSON_PROFILE");
+  return v && *v == '1';
+}
+thread_local double t_gpu_ms = 0.0, t_pack_ms = 0.0, t_write_ms = 0.0;
+
 // One request of a batch: its DOM (parse_request), or -- for the Java
 // batcher's own bytes -- its points and uuid read directly (fast_request).
 struct Req {
@@ -159,6 +170,8 @@ void run_requests(otm_engine* E, std::vector<Req>& rq, std::vector<int>& codes, 
       }
     }
   });
+  const double tp0 = now_ms();
+  t_gpu_ms = t_write_ms = 0.0;
   std::vector<int64_t> off(1, 0);
   std::vector<int> which;  // request index of each batch trace
   for (size_t i = 0; i < todo.size(); ++i)
@@ -206,7 +219,11 @@ void run_requests(otm_engine* E, std::vector<Req>& rq, std::vector<int>& codes, 
   }
   {
     std::lock_guard<std::mutex> lk(E->mu);
+    const double tg0 = now_ms();
+    t_pack_ms = tg0 - tp0;
     rc = otm::match_host_fetch(E, &b, shard.empty() ? nullptr : shard.data(), &r, &err);
+    const double tg1 = now_ms();
+    t_gpu_ms = tg1 - tg0;
     if (!rc) {
       // the responses in parallel (each writes its own slot), the reference's
       // stderr lines after, in request order
@@ -235,6 +252,7 @@ void run_requests(otm_engine* E, std::vector<Req>& rq, std::vector<int>& codes, 
           const int inv = r.traces[n].code == 200 ? r.traces[n].invalid_speeds : 0;
           for (int q = 0; q < inv; ++q) std::fputs("Speed exceeds 200kph\n", stderr);
         }
+      t_write_ms = now_ms() - tg1;
     }
   }
   if (rc) {
@@ -248,6 +266,7 @@ void run_requests(otm_engine* E, std::vector<Req>& rq, std::vector<int>& codes, 
 
 void report_many(otm_engine* E, int n, const char* const* reqs, const size_t* lens, int* codes, char** resps,
                  size_t* resp_lens) {
+  const double t0 = now_ms();
   std::vector<Req> rq((size_t)n);
   std::vector<int> c((size_t)n, 0);
   std::vector<std::string> bodies((size_t)n);
@@ -265,13 +284,21 @@ void report_many(otm_engine* E, int n, const char* const* reqs, const size_t* le
   });
   for (int k = 0; k < n; ++k)
     if (!c[(size_t)k]) todo.push_back(k);
+  const double t1 = now_ms();
   run_requests(E, rq, c, bodies, todo, false);
+  const double t2 = now_ms();
   par_for((size_t)n, [&](size_t a, size_t e) {
     for (size_t k = a; k < e; ++k) {
       codes[k] = c[k];
       resps[k] = dup_out(bodies[k], &resp_lens[k]);
     }
   });
+  const double t3 = now_ms();
+  std::vector<Req>().swap(rq);
+  const double t4 = now_ms();
+  if (json_profile())
+    std::fprintf(stderr, "[otm json] %d requests: parse %.2f, pack %.2f, gpu %.2f, write %.2f, copy out %.2f, free %.2f ms\n",
+                 n, t1 - t0, t_pack_ms, t_gpu_ms, t_write_ms, t3 - t2, t4 - t3);
 }
 
 void worker_loop(otm_engine* E) {

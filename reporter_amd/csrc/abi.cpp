@@ -8,6 +8,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
+#include <new>
 #include <sstream>
 #include <thread>
 
@@ -55,7 +56,12 @@ void par_for(size_t n, F fn) {
   std::vector<std::thread> th;
   for (size_t i = 1; i < T; ++i) {
     const size_t a = i * per, e = std::min(n, a + per);
-    if (a < e) th.emplace_back([&fn, a, e] { fn(a, e); });
+    if (a >= e) continue;
+    try {
+      th.emplace_back([&fn, a, e] { fn(a, e); });
+    } catch (...) {
+      fn(a, e);  // no thread to be had: this chunk on the caller (nothing throws across the ABI)
+    }
   }
   fn((size_t)0, std::min(n, per));
   for (auto& t : th) t.join();
@@ -352,7 +358,7 @@ const char* otm_runtime_info(void) {
   return info.c_str();
 }
 
-int otm_engine_create(const char* cfg_path, const int* devices, int ndev, otm_engine** out) {
+static int otm_engine_create_impl(const char* cfg_path, const int* devices, int ndev, otm_engine** out) {
   if (!out) return fail(OTM_EINVAL, "out is NULL");
   *out = nullptr;
   if (ndev < 1 || !devices) return fail(OTM_EINVAL, "devices must name at least one device");
@@ -508,14 +514,14 @@ otm_engine* otm_engine_member(otm_engine* E, int i) {
   return i < (int)E->members.size() ? E->members[(size_t)i] : nullptr;
 }
 
-int otm_report(otm_engine* E, const char* req, size_t len, char** resp, size_t* resp_len) {
+static int otm_report_impl(otm_engine* E, const char* req, size_t len, char** resp, size_t* resp_len) {
   int code = 0;
   const char* reqs[1] = {req};
   report_many(E, 1, reqs, &len, &code, resp, resp_len);
   return code;
 }
 
-int otm_report_batch(otm_engine* E, int n, const char* const* reqs, const size_t* lens, char** resps,
+static int otm_report_batch_impl(otm_engine* E, int n, const char* const* reqs, const size_t* lens, char** resps,
                      size_t* resp_lens, int* codes) {
   if (!E || n < 0) return fail(OTM_EINVAL, "bad arguments");
   report_many(E, n, reqs, lens, codes, resps, resp_lens);
@@ -557,7 +563,7 @@ int otm_request_points(const char* req, size_t len, int fast, float* lat, float*
   return n;
 }
 
-int otm_match_json(otm_engine* E, const char* req, size_t len, char** resp, size_t* resp_len) {
+static int otm_match_json_impl(otm_engine* E, const char* req, size_t len, char** resp, size_t* resp_len) {
   std::vector<Req> rq(1);
   std::vector<int> codes(1, 0);
   std::vector<std::string> bodies(1);
@@ -610,7 +616,7 @@ int otm_report_segments(otm_engine* E, const char* req, size_t len, const char* 
   return 200;
 }
 
-int otm_report_segments_device(otm_engine* E, int n, const char* const* reqs, const size_t* lens,
+static int otm_report_segments_device_impl(otm_engine* E, int n, const char* const* reqs, const size_t* lens,
                                const char* const* match_jsons, const size_t* match_lens, char** resps,
                                size_t* resp_lens, int* codes) {
   if (!E || n < 0) return fail(OTM_EINVAL, "bad arguments");
@@ -692,7 +698,7 @@ int otm_report_segments_device(otm_engine* E, int n, const char* const* reqs, co
   return OTM_OK;
 }
 
-int otm_submit(otm_engine* E, const char* req, size_t len, uint64_t tag) {
+static int otm_submit_impl(otm_engine* E, const char* req, size_t len, uint64_t tag) {
   if (!E) return fail(OTM_EINVAL, "engine is NULL");
   std::lock_guard<std::mutex> lk(E->qmu);
   if (!E->worker_started) {
@@ -758,7 +764,7 @@ void otm_host_free(void* p) {
   if (p) (void)hipHostFree(p);
 }
 
-int otm_match_soa(otm_engine* E, const otm_batch* in, otm_results* out) {
+static int otm_match_soa_impl(otm_engine* E, const otm_batch* in, otm_results* out) {
   if (!E || !in || !out) return fail(OTM_EINVAL, "bad arguments");
   std::lock_guard<std::mutex> lk(E->mu);
   std::string err;
@@ -766,7 +772,7 @@ int otm_match_soa(otm_engine* E, const otm_batch* in, otm_results* out) {
   return rc ? fail(rc, err) : OTM_OK;
 }
 
-int otm_match_device(otm_engine* E, const otm_batch* in, void* stream) {
+static int otm_match_device_impl(otm_engine* E, const otm_batch* in, void* stream) {
   if (!E || !in) return fail(OTM_EINVAL, "bad arguments");
   if (!E->members.empty()) return fail(OTM_EINVAL, "device batches go to a member engine (otm_engine_member)");
   std::lock_guard<std::mutex> lk(E->mu);
@@ -784,7 +790,7 @@ int otm_match_device(otm_engine* E, const otm_batch* in, void* stream) {
   return rc ? fail(rc, err) : OTM_OK;
 }
 
-int otm_fetch_results(otm_engine* E, otm_results* out) {
+static int otm_fetch_results_impl(otm_engine* E, otm_results* out) {
   if (!E || !out) return fail(OTM_EINVAL, "bad arguments");
   std::lock_guard<std::mutex> lk(E->mu);
   if (!E->members.empty()) {
@@ -906,6 +912,109 @@ int otm_debug_fetch(otm_engine* E, int what, void* dst, size_t bytes, size_t* ne
   std::string err;
   int rc = otm::engine_debug_fetch(E, what, dst, bytes, needed, &err);
   return rc ? fail(rc, err) : OTM_OK;
+}
+
+// Entry points: nothing throws across the C ABI (an allocation failure or an
+// internal exception becomes an error code, or a 500 body).
+int otm_engine_create(const char* cfg_path, const int* devices, int ndev, otm_engine** out) {
+  try {
+    return otm_engine_create_impl(cfg_path, devices, ndev, out);
+  } catch (const std::bad_alloc&) {
+    return fail(OTM_ENOMEM, "out of host memory");
+  } catch (const std::exception& e) {
+    return fail(OTM_EINVAL, std::string("internal error: ") + e.what());
+  }
+}
+
+int otm_report_batch(otm_engine* E, int n, const char* const* reqs, const size_t* lens, char** resps,
+                     size_t* resp_lens, int* codes) {
+  try {
+    return otm_report_batch_impl(E, n, reqs, lens, resps, resp_lens, codes);
+  } catch (const std::bad_alloc&) {
+    return fail(OTM_ENOMEM, "out of host memory");
+  } catch (const std::exception& e) {
+    return fail(OTM_EINVAL, std::string("internal error: ") + e.what());
+  }
+}
+
+int otm_report_segments_device(otm_engine* E, int n, const char* const* reqs, const size_t* lens,
+                               const char* const* match_jsons, const size_t* match_lens, char** resps,
+                               size_t* resp_lens, int* codes) {
+  try {
+    return otm_report_segments_device_impl(E, n, reqs, lens, match_jsons, match_lens, resps, resp_lens, codes);
+  } catch (const std::bad_alloc&) {
+    return fail(OTM_ENOMEM, "out of host memory");
+  } catch (const std::exception& e) {
+    return fail(OTM_EINVAL, std::string("internal error: ") + e.what());
+  }
+}
+
+int otm_submit(otm_engine* E, const char* req, size_t len, uint64_t tag) {
+  try {
+    return otm_submit_impl(E, req, len, tag);
+  } catch (const std::bad_alloc&) {
+    return fail(OTM_ENOMEM, "out of host memory");
+  } catch (const std::exception& e) {
+    return fail(OTM_EINVAL, std::string("internal error: ") + e.what());
+  }
+}
+
+int otm_match_soa(otm_engine* E, const otm_batch* in, otm_results* out) {
+  try {
+    return otm_match_soa_impl(E, in, out);
+  } catch (const std::bad_alloc&) {
+    return fail(OTM_ENOMEM, "out of host memory");
+  } catch (const std::exception& e) {
+    return fail(OTM_EINVAL, std::string("internal error: ") + e.what());
+  }
+}
+
+int otm_match_device(otm_engine* E, const otm_batch* in, void* stream) {
+  try {
+    return otm_match_device_impl(E, in, stream);
+  } catch (const std::bad_alloc&) {
+    return fail(OTM_ENOMEM, "out of host memory");
+  } catch (const std::exception& e) {
+    return fail(OTM_EINVAL, std::string("internal error: ") + e.what());
+  }
+}
+
+int otm_fetch_results(otm_engine* E, otm_results* out) {
+  try {
+    return otm_fetch_results_impl(E, out);
+  } catch (const std::bad_alloc&) {
+    return fail(OTM_ENOMEM, "out of host memory");
+  } catch (const std::exception& e) {
+    return fail(OTM_EINVAL, std::string("internal error: ") + e.what());
+  }
+}
+
+int otm_report(otm_engine* E, const char* req, size_t len, char** resp, size_t* resp_len) {
+  try {
+    return otm_report_impl(E, req, len, resp, resp_len);
+  } catch (...) {
+    // a 500 like :239-240, its body allocated without anything that throws
+    static const char kBody[] = "{\"error\":\"internal error\"}";
+    char* b = (char*)std::malloc(sizeof kBody);
+    if (b) std::memcpy(b, kBody, sizeof kBody);
+    if (resp) *resp = b;
+    if (resp_len) *resp_len = b ? sizeof kBody - 1 : 0;
+    return 500;
+  }
+}
+
+int otm_match_json(otm_engine* E, const char* req, size_t len, char** resp, size_t* resp_len) {
+  try {
+    return otm_match_json_impl(E, req, len, resp, resp_len);
+  } catch (...) {
+    // a 500 like :239-240, its body allocated without anything that throws
+    static const char kBody[] = "{\"error\":\"internal error\"}";
+    char* b = (char*)std::malloc(sizeof kBody);
+    if (b) std::memcpy(b, kBody, sizeof kBody);
+    if (resp) *resp = b;
+    if (resp_len) *resp_len = b ? sizeof kBody - 1 : 0;
+    return 500;
+  }
 }
 
 }  // extern "C"

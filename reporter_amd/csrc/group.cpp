@@ -104,7 +104,13 @@ int group_match(otm_engine* G, const otm_batch* b, const int32_t* shard, otm_res
   }
   std::vector<std::thread> th;
   for (int m = 0; m < nd; ++m)
-    if (!mo[(size_t)m].traces.empty()) th.emplace_back(run_member, G->members[(size_t)m], std::ref(mo[(size_t)m]));
+    if (!mo[(size_t)m].traces.empty()) {
+      try {
+        th.emplace_back(run_member, G->members[(size_t)m], std::ref(mo[(size_t)m]));
+      } catch (...) {
+        run_member(G->members[(size_t)m], mo[(size_t)m]);  // no thread: this member on the caller
+      }
+    }
   for (auto& t : th) t.join();
   for (const MemberOut& o : mo)
     if (o.rc) {

@@ -1,7 +1,7 @@
 """Host code under AddressSanitizer + UndefinedBehaviorSanitizer.
 
 The CPU oracle (oracle/, C) and libotmatch's host C++ (the C ABI, JSON,
-report(), batcher, formatter, tile math, synthetic inputs) are rebuilt with
+report(), the request reader, batcher, formatter, tile math, synthetic inputs) are rebuilt with
 -fsanitize=address,undefined (`make asan` in oracle/ and reporter_amd/csrc/,
 clang for both so one ASan runtime serves the process; GPU sanitizers are not
 available on this pool, so device code is not instrumented).  The CPU test
@@ -21,7 +21,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ASAN_LIB = os.path.join(ROOT, "reporter_amd", "lib", "asan", "libotmatch.so")
 ASAN_ORACLE = os.path.join(ROOT, "oracle", "build", "asan", "libotm_oracle.so")
 MODULES = ["tests/test_golden.py", "tests/test_host.py", "tests/test_formatter.py", "tests/test_batcher.py",
-           "tests/test_tiles.py"]
+           "tests/test_tiles.py", "tests/test_fast_request.py"]
 
 
 def _runtime():

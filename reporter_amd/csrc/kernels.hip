@@ -1769,6 +1769,9 @@ __global__ void k_row_pack(const int32_t* row_cnt, const int64_t* row_off, IdxRo
 #ifndef OTM_TRANS_KC8
 #define OTM_TRANS_KC8 8
 #endif
+#ifndef OTM_TRANS_PAD
+#define OTM_TRANS_PAD 0
+#endif
 #ifndef OTM_TRANS_KC4
 #define OTM_TRANS_KC4 6
 #endif
@@ -1779,9 +1782,11 @@ __global__ __launch_bounds__(TB, 8) void k_trans_sub(DevGraph g, DevBatch b, Dev
   // a pair reads its target and source as one 16-byte LDS word each
   constexpr int KC = S >= 16 ? 16 : (S == 8 ? OTM_TRANS_KC8 : OTM_TRANS_KC4);
   constexpr bool WIDE = KC < 16;
-  __shared__ int4 tg[NS][KC];  // target: edge, offset bits, from-node, start heading
-  __shared__ int4 sr[NS][KC];  // source: edge, offset bits, remaining-length bits, end heading
-  __shared__ IdxRow rq[NS][KC];
+  // (OTM_TRANS_PAD: one spare 16-byte word per column group, spreading the
+  // groups' rows over the LDS banks)
+  __shared__ int4 tg[NS][KC + OTM_TRANS_PAD];  // target: edge, offset bits, from-node, start heading
+  __shared__ int4 sr[NS][KC + OTM_TRANS_PAD];  // source: edge, offset bits, remaining-length bits, end heading
+  __shared__ IdxRow rq[NS][KC + OTM_TRANS_PAD];
   __shared__ uint32_t TU[TURN_TABLE];  // turn units per deviation
   const int lane = threadIdx.x, sg = lane / S, sl = lane % S;
   const unsigned long long smask = (S == 64 ? ~0ull : ((1ull << S) - 1ull)) << (sg * S);

@@ -498,6 +498,7 @@ void otm_engine_destroy(otm_engine* E) {
     for (auto& r : E->done) std::free(r.body);
   }
   if (!E->members.empty()) {
+    otm::member_pool_free(E);
     for (otm_engine* m : E->members) otm_engine_destroy(m);
     delete E;
     return;

@@ -20,6 +20,9 @@ struct otm_engine {
   // across the members by uuid and merged back (the g_* arrays hold the merged
   // results of its last batch)
   std::vector<otm_engine*> members;
+  // one persistent host thread per member (group.cpp): a HIP host thread keeps
+  // runtime state that a thread spawned per batch would leak
+  struct MemberPool* member_pool = nullptr;
   std::vector<otm_trace_result> g_traces;
   std::vector<otm_segment> g_segs;
   std::vector<otm_report_rec> g_reps;
@@ -142,5 +145,7 @@ int engine_spill_stats(otm_engine* E, otm_spill_stats* out);
 int match_host_fetch(otm_engine* E, const otm_batch* b, const int32_t* shard, otm_results* out, std::string* err);
 // a uuid's member among n: Kafka's partition of the key, (murmur2 & 0x7fffffff) % n
 int shard_of(const char* key, size_t len, int n);
+// stop and join a multi-device engine's member threads (before its members go)
+void member_pool_free(otm_engine* G);
 
 }  // namespace otm

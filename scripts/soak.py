@@ -1,0 +1,67 @@
+#!/usr/bin/env python3
+"""Soak test on the GPU box: many request batches through one engine and one
+multi-device engine (members on repeated device 0), checking every call's
+responses are byte-identical to the first and that host RSS and free device
+memory do not drift.  One JSON line out."""
+import ctypes as C
+import hashlib
+import json
+import os
+import resource
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    import torch
+    from reporter_amd import Engine, _lib, encode_request, synth
+    L = _lib.lib()
+    graph = synth.cached_graph(2)
+    tr = dict(synth.CONFIGS[2]["traces"])
+    tr["n_vehicles"] = 2000
+    b = synth.make_traces(graph, **tr)
+    bodies = []
+    for t in range(2000):
+        a, e = b["trace_off"][t], b["trace_off"][t + 1]
+        bodies.append(encode_request("veh%d" % t, b["lat"][a:e], b["lon"][a:e], b["time"][a:e].astype(np.int64),
+                                     b["accuracy"][a:e].astype(np.int32)))
+    n = len(bodies)
+    arr = (C.c_char_p * n)(*bodies)
+    lens = (C.c_size_t * n)(*[len(x) for x in bodies])
+    outs = (C.c_void_p * n)()
+    olens = (C.c_size_t * n)()
+    codes = (C.c_int * n)()
+    iters = int(os.environ.get("OTM_SOAK_ITERS", "300"))
+    out = {"requests_per_call": n, "iterations": iters}
+    for name, devs in (("one", [0]), ("group", [0, 0])):
+        with Engine(graph_path=graph, devices=devs) as eng:
+            ref = None
+            rss0 = free0 = None
+            t0 = time.perf_counter()
+            for it in range(iters):
+                assert L.otm_report_batch(eng.h, n, arr, lens, outs, olens, codes) == 0
+                h = hashlib.sha256()
+                for i in range(n):
+                    h.update(C.string_at(outs[i], olens[i]))
+                    L.otm_free(outs[i])
+                d = h.hexdigest()
+                if ref is None:
+                    ref = d
+                assert d == ref, "responses changed at iteration %d" % it
+                if it == 10:
+                    rss0 = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss
+                    free0 = torch.cuda.mem_get_info(0)[0]
+            out[name] = {"seconds": time.perf_counter() - t0,
+                         "rss_growth_kb_after_warmup": resource.getrusage(resource.RUSAGE_SELF).ru_maxrss - rss0,
+                         "device_free_drop_mb_after_warmup": (free0 - torch.cuda.mem_get_info(0)[0]) / 2**20,
+                         "identical": True}
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -60,6 +60,32 @@ def main():
                          "rss_growth_kb_after_warmup": resource.getrusage(resource.RUSAGE_SELF).ru_maxrss - rss0,
                          "device_free_drop_mb_after_warmup": (free0 - torch.cuda.mem_get_info(0)[0]) / 2**20,
                          "identical": True}
+    # async submit/poll: every body submitted, polled back by tag, byte-equal
+    # to the batch call's response
+    with Engine(graph_path=graph) as eng:
+        want = [x for x in eng.report_batch(bodies)]
+        t0 = time.perf_counter()
+        rss_a = None
+        for rnd in range(max(1, iters // 30)):
+            for k, body in enumerate(bodies):
+                eng.submit(body, k)
+            seen = {}
+            while len(seen) < n:
+                for tag, code, resp in eng.poll(4096, 2000000):
+                    seen[tag] = (code, resp)
+            assert [seen[k] for k in range(n)] == want
+            if rnd == 2:
+                rss_a = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss
+        out["submit_poll"] = {"rounds": max(1, iters // 30), "seconds": time.perf_counter() - t0,
+                              "rss_growth_kb_after_warmup": resource.getrusage(resource.RUSAGE_SELF).ru_maxrss - (rss_a or 0)
+                              if rss_a else None, "identical": True}
+    # engine create / destroy cycles give their device memory back
+    free_a = torch.cuda.mem_get_info(0)[0]
+    for _ in range(20):
+        with Engine(graph_path=graph, devices=[0, 0]) as eng:
+            eng.report_batch(bodies[:50])
+    torch.cuda.synchronize()
+    out["create_destroy"] = {"cycles": 20, "device_free_drop_mb": (free_a - torch.cuda.mem_get_info(0)[0]) / 2**20}
     print(json.dumps(out), flush=True)
 
 

@@ -8,6 +8,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
+#include <exception>
 #include <new>
 #include <sstream>
 #include <thread>
@@ -54,17 +55,31 @@ void par_for(size_t n, F fn) {
   }
   const size_t per = (n + T - 1) / T;
   std::vector<std::thread> th;
+  std::vector<std::exception_ptr> errs(T);
   for (size_t i = 1; i < T; ++i) {
     const size_t a = i * per, e = std::min(n, a + per);
     if (a >= e) continue;
     try {
-      th.emplace_back([&fn, a, e] { fn(a, e); });
+      // an exception in a worker is carried back to the caller, not terminate()
+      th.emplace_back([&fn, &errs, i, a, e] {
+        try {
+          fn(a, e);
+        } catch (...) {
+          errs[i] = std::current_exception();
+        }
+      });
     } catch (...) {
-      fn(a, e);  // no thread to be had: this chunk on the caller (nothing throws across the ABI)
+      fn(a, e);  // no thread to be had: this chunk on the caller
     }
   }
-  fn((size_t)0, std::min(n, per));
+  try {
+    fn((size_t)0, std::min(n, per));
+  } catch (...) {
+    errs[0] = std::current_exception();
+  }
   for (auto& t : th) t.join();
+  for (auto& x : errs)
+    if (x) std::rethrow_exception(x);  // to the entry point's guard
 }
 
 // the Java request bytes read without a DOM (otm::fast_request); OTM_FAST_JSON=0

@@ -27,6 +27,7 @@
 // known when its records arrive.  Requests of all runnable keys go to the
 // matcher together: one GPU batch per round.
 #include <algorithm>
+#include <exception>
 #include <chrono>
 #include <cmath>
 #include <condition_variable>
@@ -185,10 +186,21 @@ class Pool {
       ++gen_;
     }
     cv_.notify_all();
-    chunk(0, n, fn);
+    try {
+      chunk(0, n, fn);
+    } catch (...) {
+      std::lock_guard<std::mutex> lk(mu_);
+      if (!err_) err_ = std::current_exception();
+    }
     std::unique_lock<std::mutex> lk(mu_);
     done_.wait(lk, [this] { return pending_ == 0; });
     fn_ = nullptr;
+    if (err_) {  // a member's exception, to the entry point's guard
+      std::exception_ptr e = err_;
+      err_ = nullptr;
+      lk.unlock();
+      std::rethrow_exception(e);
+    }
   }
 
  private:
@@ -210,7 +222,12 @@ class Pool {
         fn = fn_;
         n = n_items_;
       }
-      chunk(t, n, *fn);
+      try {
+        chunk(t, n, *fn);
+      } catch (...) {
+        std::lock_guard<std::mutex> lk(mu_);
+        if (!err_) err_ = std::current_exception();
+      }
       {
         std::lock_guard<std::mutex> lk(mu_);
         if (--pending_ == 0) done_.notify_one();
@@ -219,6 +236,7 @@ class Pool {
   }
   int n_;
   std::vector<std::thread> th_;
+  std::exception_ptr err_;
   std::mutex mu_;
   std::condition_variable cv_, done_;
   uint64_t gen_ = 0;
@@ -711,7 +729,7 @@ void otm_batcher_defaults(otm_batcher_cfg* c) {
   c->reserved = 0;
 }
 
-int otm_batcher_create(otm_engine* eng, const otm_batcher_cfg* cfg, otm_report_fn fn, void* ctx,
+static int otm_batcher_create_impl(otm_engine* eng, const otm_batcher_cfg* cfg, otm_report_fn fn, void* ctx,
                        otm_batcher** out) {
   if (!out || (!eng && !fn)) return OTM_EINVAL;
   auto* B = new otm_batcher();
@@ -736,7 +754,7 @@ void otm_batcher_destroy(otm_batcher* B) {
   delete B;
 }
 
-int otm_batcher_process(otm_batcher* B, int n, const char* const* keys, const size_t* key_lens, const float* lat,
+static int otm_batcher_process_impl(otm_batcher* B, int n, const char* const* keys, const size_t* key_lens, const float* lat,
                         const float* lon, const int32_t* accuracy, const int64_t* time, const int64_t* ts_ms) {
   if (!B || n < 0) return OTM_EINVAL;
   const int64_t t0 = now_us();
@@ -748,7 +766,7 @@ int otm_batcher_process(otm_batcher* B, int n, const char* const* keys, const si
   return OTM_OK;
 }
 
-int otm_batcher_process_raw(otm_batcher* B, const otm_formatter* f, int32_t n, const char* msgs, const int64_t* off,
+static int otm_batcher_process_raw_impl(otm_batcher* B, const otm_formatter* f, int32_t n, const char* msgs, const int64_t* off,
                             const int64_t* ts_ms, int nthreads) {
   if (!B || !f || n < 0 || (n > 0 && !ts_ms)) return OTM_EINVAL;
   const int64_t t0 = now_us();
@@ -780,12 +798,12 @@ int otm_batcher_process_raw(otm_batcher* B, const otm_formatter* f, int32_t n, c
   return OTM_OK;
 }
 
-int otm_batcher_flush(otm_batcher* B) {
+static int otm_batcher_flush_impl(otm_batcher* B) {
   if (!B) return OTM_EINVAL;
   return drain(B);
 }
 
-int otm_batcher_close(otm_batcher* B) {
+static int otm_batcher_close_impl(otm_batcher* B) {
   if (!B) return OTM_EINVAL;
   int rc = drain(B);
   if (rc) return rc;
@@ -848,6 +866,50 @@ int otm_batcher_batch(const otm_batcher* B, const char* key, size_t key_len, int
   }
   if (max_separation) *max_separation = b.max_sep;
   return n;
+}
+
+// nothing throws across the C ABI
+int otm_batcher_create(otm_engine* eng, const otm_batcher_cfg* cfg, otm_report_fn fn, void* ctx,
+                       otm_batcher** out) {
+  try {
+    return otm_batcher_create_impl(eng, cfg, fn, ctx, out);
+  } catch (...) {
+    return OTM_ENOMEM;  // (a host allocation failure; the batcher should then be destroyed)
+  }
+}
+
+int otm_batcher_process(otm_batcher* B, int n, const char* const* keys, const size_t* key_lens, const float* lat,
+                        const float* lon, const int32_t* accuracy, const int64_t* time, const int64_t* ts_ms) {
+  try {
+    return otm_batcher_process_impl(B, n, keys, key_lens, lat, lon, accuracy, time, ts_ms);
+  } catch (...) {
+    return OTM_ENOMEM;  // (a host allocation failure; the batcher should then be destroyed)
+  }
+}
+
+int otm_batcher_process_raw(otm_batcher* B, const otm_formatter* f, int32_t n, const char* msgs, const int64_t* off,
+                            const int64_t* ts_ms, int nthreads) {
+  try {
+    return otm_batcher_process_raw_impl(B, f, n, msgs, off, ts_ms, nthreads);
+  } catch (...) {
+    return OTM_ENOMEM;  // (a host allocation failure; the batcher should then be destroyed)
+  }
+}
+
+int otm_batcher_flush(otm_batcher* B) {
+  try {
+    return otm_batcher_flush_impl(B);
+  } catch (...) {
+    return OTM_ENOMEM;  // (a host allocation failure; the batcher should then be destroyed)
+  }
+}
+
+int otm_batcher_close(otm_batcher* B) {
+  try {
+    return otm_batcher_close_impl(B);
+  } catch (...) {
+    return OTM_ENOMEM;  // (a host allocation failure; the batcher should then be destroyed)
+  }
 }
 
 }  // extern "C"

@@ -178,7 +178,14 @@ int group_match(otm_engine* G, const otm_batch* b, const int32_t* shard, otm_res
     if (!mo[(size_t)m].traces.empty()) {
       otm_engine* M = G->members[(size_t)m];
       MemberOut* o = &mo[(size_t)m];
-      tasks[(size_t)m] = [M, o] { run_member(M, *o); };
+      tasks[(size_t)m] = [M, o] {
+        try {
+          run_member(M, *o);
+        } catch (...) {  // (a host allocation failure) -> the batch's error, not terminate()
+          o->rc = OTM_ENOMEM;
+          o->err = "out of host memory";
+        }
+      };
     }
   G->member_pool->run(tasks);
   for (const MemberOut& o : mo)

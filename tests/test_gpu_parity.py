@@ -365,10 +365,13 @@ def test_fetch_is_idempotent(small_graph):
         assert getattr(r1, k).tobytes() == getattr(r2, k).tobytes() == getattr(r3, k).tobytes(), k
 
 
-def test_json_report_path_host_threads(small_graph, oracle, monkeypatch):
+@pytest.mark.parametrize("fast", ["1", "0"], ids=["dom_free_reader", "dom"])
+def test_json_report_path_host_threads(small_graph, oracle, monkeypatch, fast):
     """otm_report_batch's parse / point extraction / response writing split over
-    host threads (forced here with tiny chunks): byte-equal to the oracle, in
-    request order, malformed bodies included."""
+    host threads (forced here with tiny chunks), with the Java bodies read by
+    the DOM-free reader or by the DOM path (OTM_FAST_JSON=0): byte-equal to the
+    oracle, in request order, malformed bodies included."""
+    monkeypatch.setenv("OTM_FAST_JSON", fast)
     b = synth.make_traces(small_graph, 120, 40, seed=19)
     bodies = []
     for t in range(120):

@@ -759,6 +759,20 @@ static bool copy_serial() {
   return on;
 }
 
+// OTM_COPY_SYNC=1: the large host<->device copies as hipMemcpyWithStream (the
+// call torch makes for pinned copies; it returns when the copy is done) --
+// an A/B of the runtime's engine choice for the host-inclusive leg
+static bool copy_sync() {
+  static const bool on = [] {
+    const char* v = std::getenv("OTM_COPY_SYNC");
+    return v && *v == '1';
+  }();
+  return on;
+}
+static hipError_t big_copy(void* dst, const void* src, size_t n, hipMemcpyKind k, hipStream_t s) {
+  return copy_sync() ? hipMemcpyWithStream(dst, src, n, k, s) : hipMemcpyAsync(dst, src, n, k, s);
+}
+
 int engine_match_host(otm_engine* E, const otm_batch* in, std::string* err) {
   const int32_t NT = in->n_traces;
   if (NT < 0 || !in->trace_off) {
@@ -815,10 +829,10 @@ int engine_match_host(otm_engine* E, const otm_batch* in, std::string* err) {
     std::unique_lock<std::mutex> lk(g_copy_mu, std::defer_lock);
     if (copy_serial()) lk.lock();
     HIPCHK(hipMemcpyAsync(E->in_off.p, in->trace_off, b_off, hipMemcpyHostToDevice, s));
-    HIPCHK(hipMemcpyAsync(E->in_lat.p, in->lat, b_pt, h2d, s));
-    HIPCHK(hipMemcpyAsync(E->in_lon.p, in->lon, b_pt, h2d, s));
-    HIPCHK(hipMemcpyAsync(E->in_time.p, in->time, b_tm, h2d, s));
-    HIPCHK(hipMemcpyAsync(E->in_acc.p, in->accuracy, b_pt, h2d, s));
+    HIPCHK(big_copy(E->in_lat.p, in->lat, b_pt, h2d, s));
+    HIPCHK(big_copy(E->in_lon.p, in->lon, b_pt, h2d, s));
+    HIPCHK(big_copy(E->in_time.p, in->time, b_tm, h2d, s));
+    HIPCHK(big_copy(E->in_acc.p, in->accuracy, b_pt, h2d, s));
     if (copy_serial()) HIPCHK(hipStreamSynchronize(s));
   }
   b.trace_off = (const int64_t*)E->in_off.p;
@@ -895,10 +909,10 @@ int engine_fetch(otm_engine* E, otm_results* out, std::string* err) {
     HIPCHK(hipStreamSynchronize(s));  // the compaction first: the lock covers only the copies
     lk.lock();
   }
-  if (NT) HIPCHK(hipMemcpyAsync(E->h_traces.p, E->f_traces.p, (size_t)NT * sizeof(otm_trace_result), d2h, s));
-  if (NS) HIPCHK(hipMemcpyAsync(E->h_segs.p, E->f_segs.p, (size_t)NS * sizeof(otm_segment), d2h, s));
-  if (NR) HIPCHK(hipMemcpyAsync(E->h_reps_dense.p, E->f_reps.p, (size_t)NR * sizeof(otm_report_rec), d2h, s));
-  if (NW) HIPCHK(hipMemcpyAsync(E->h_ways.p, E->f_ways.p, (size_t)NW * 8, d2h, s));
+  if (NT) HIPCHK(big_copy(E->h_traces.p, E->f_traces.p, (size_t)NT * sizeof(otm_trace_result), d2h, s));
+  if (NS) HIPCHK(big_copy(E->h_segs.p, E->f_segs.p, (size_t)NS * sizeof(otm_segment), d2h, s));
+  if (NR) HIPCHK(big_copy(E->h_reps_dense.p, E->f_reps.p, (size_t)NR * sizeof(otm_report_rec), d2h, s));
+  if (NW) HIPCHK(big_copy(E->h_ways.p, E->f_ways.p, (size_t)NW * 8, d2h, s));
   HIPCHK(hipStreamSynchronize(s));
   out->n_traces = NT;
   out->n_segments = NS;

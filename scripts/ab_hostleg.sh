@@ -40,4 +40,9 @@ serial)
   BENCH_EXTRA="--inflight 4" run serial_4 OTM_COPY_SERIAL=1
   BENCH_EXTRA="--inflight 2" run serial_2 OTM_COPY_SERIAL=1
   ;;
+sync)
+  run base OTM_NOP=1
+  run sync OTM_COPY_SYNC=1
+  run sync_serial OTM_COPY_SYNC=1 OTM_COPY_SERIAL=1
+  ;;
 esac

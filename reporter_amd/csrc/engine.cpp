@@ -769,7 +769,36 @@ static bool copy_sync() {
   }();
   return on;
 }
+// OTM_COPY_KERNEL=<blocks>: the large copies by the library's own k_copy with
+// that many workgroups when the host side is pinned (device-mapped), instead of
+// the runtime's copy -- an A/B knob for the host-inclusive leg
+static int copy_kernel_blocks() {
+  const char* v = std::getenv("OTM_COPY_KERNEL");  // (read per copy: tests switch it)
+  return v ? std::max(0, std::min(1024, std::atoi(v))) : 0;
+}
+// p .. p + n lies in one pinned, device-mapped host allocation
+static bool host_mapped(const void* p, size_t n) {
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  if (a.type != hipMemoryTypeHost || a.devicePointer != p) return false;
+  hipDeviceptr_t base = nullptr;
+  size_t size = 0;
+  if (hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return (const char*)p + n <= (const char*)base + size;
+}
 static hipError_t big_copy(void* dst, const void* src, size_t n, hipMemcpyKind k, hipStream_t s) {
+  const int blocks = copy_kernel_blocks();
+  if (blocks > 0 && n >= (1u << 16) && ((uintptr_t)dst % 16) == 0 && ((uintptr_t)src % 16) == 0 &&
+      host_mapped(k == hipMemcpyHostToDevice ? src : dst, n)) {
+    launch_copy(dst, src, n, blocks, s);
+    return hipGetLastError();
+  }
   return copy_sync() ? hipMemcpyWithStream(dst, src, n, k, s) : hipMemcpyAsync(dst, src, n, k, s);
 }
 

@@ -3731,6 +3731,23 @@ constexpr int TRANS_GRID_CAP = 65536;  // k_trans_sub waves (one per column, gri
 
 }  // namespace
 
+// A host<->device copy by a few workgroups of this library's own (the pinned
+// host buffer is device-mapped): the runtime's blit copies put a 512-thread
+// workgroup on every CU, whose waves then sit on PCIe latency beside the other
+// batches' kernels.  16-byte words, grid-strided; the tail byte by byte.
+__global__ __launch_bounds__(256) void k_copy(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, size_t n) {
+  const size_t nw = n / 16;
+  const uint4* s4 = (const uint4*)src;
+  uint4* d4 = (uint4*)dst;
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < nw; i += stride) d4[i] = s4[i];
+  const size_t t = nw * 16 + (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < n && (size_t)blockIdx.x * blockDim.x + threadIdx.x < 16) dst[t] = src[t];
+}
+void launch_copy(void* dst, const void* src, size_t n, int blocks, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_copy, dim3(blocks), dim3(256), 0, s, (const uint8_t*)src, (uint8_t*)dst, n);
+}
+
 void launch_fetch_scan(int32_t n, const int32_t* c0, const int32_t* c1, const int32_t* c2, int32_t* o0, int32_t* o1,
                        int32_t* o2, hipStream_t s) {
   hipLaunchKernelGGL(k_fetch_scan, dim3(1), dim3(1024), 0, s, n, c0, c1, c2, o0, o1, o2);

@@ -45,4 +45,11 @@ sync)
   run sync OTM_COPY_SYNC=1
   run sync_serial OTM_COPY_SYNC=1 OTM_COPY_SERIAL=1
   ;;
+kern)
+  run base OTM_NOP=1
+  run k32 OTM_COPY_KERNEL=32
+  run k64 OTM_COPY_KERNEL=64
+  run k16 OTM_COPY_KERNEL=16
+  run k128 OTM_COPY_KERNEL=128
+  ;;
 esac

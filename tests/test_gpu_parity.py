@@ -391,3 +391,37 @@ def test_json_report_path_host_threads(small_graph, oracle, monkeypatch, fast):
             assert (code, resp) == oracle.handle_request(g, body), body[:80]
         monkeypatch.setenv("OTM_HOST_THREADS", "1")
         assert eng.report_batch(bodies) == got
+
+
+@pytest.mark.parametrize("blocks", ["0", "32"])
+def test_pinned_host_batch_copy_paths(small_graph, monkeypatch, blocks):
+    """otm_match_soa from pinned host buffers (otm_host_alloc) through the
+    runtime's copies and through the library's own copy kernel
+    (OTM_COPY_KERNEL): the same results as from pageable numpy arrays."""
+    import ctypes as C
+    from reporter_amd import _lib
+    L = _lib.lib()
+    from reporter_amd.engine import Results
+    b = synth.make_traces(small_graph, 5000, 60, seed=29)  # 300k points (> 2^18): the large-batch copy path
+    with Engine(graph_path=small_graph) as eng:
+        want = eng.match(b)
+        want = [getattr(want, k).tobytes() for k in ("traces", "segments", "reports", "way_ids")]
+        monkeypatch.setenv("OTM_COPY_KERNEL", blocks)
+        ptrs, keep = {}, []
+        for k in ("trace_off", "lat", "lon", "time", "accuracy"):
+            a = np.ascontiguousarray(b[k])
+            p = L.otm_host_alloc(a.nbytes)
+            assert p
+            C.memmove(p, a.ctypes.data, a.nbytes)
+            ptrs[k] = p
+            keep.append(p)
+        try:
+            hb = _lib.Batch(len(b["trace_off"]) - 1, int(b["trace_off"][-1]), ptrs["trace_off"], ptrs["lat"],
+                            ptrs["lon"], ptrs["time"], ptrs["accuracy"])
+            r = _lib.Results()
+            assert L.otm_match_soa(eng.h, C.byref(hb), C.byref(r)) == 0
+            got = Results(r)
+            assert [getattr(got, k).tobytes() for k in ("traces", "segments", "reports", "way_ids")] == want
+        finally:
+            for p in keep:
+                L.otm_host_free(p)

@@ -88,6 +88,8 @@ def parse():
                     help="PMC traffic summary (scripts/pmc_summary.py); default: the committed one for --config")
     ap.add_argument("--json-calls", type=int, default=5,
                     help="calls of the JSON leg (otm_report_batch over the batch's request bodies; 0: skip)")
+    ap.add_argument("--stagger-ms", type=float, default=0.0,
+                    help="device leg: in-flight worker i starts i x this many ms late (A/B of phase drift)")
     ap.add_argument("--host-stagger-ms", type=float, default=0.0,
                     help="host-inclusive leg: in-flight worker i starts i x this many ms late (A/B of phase drift)")
     ap.add_argument("--inflight", type=int, default=3,
@@ -267,6 +269,8 @@ def main():
 
     def worker(i):
         gate.wait()
+        if args.stagger_ms > 0:
+            time.sleep(i * args.stagger_ms / 1e3)
         while next(ticket) < args.steps:
             step(i)
 

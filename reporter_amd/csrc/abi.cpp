@@ -82,6 +82,9 @@ void par_for(size_t n, F fn) {
     if (x) std::rethrow_exception(x);  // to the entry point's guard
 }
 
+#ifndef OTM_JSON_SCRATCH
+#define OTM_JSON_SCRATCH 1
+#endif
 // the Java request bytes read without a DOM (otm::fast_request); OTM_FAST_JSON=0
 // sends every body through the DOM (A/B and the parity tests)
 bool fast_requests() {
@@ -263,8 +266,17 @@ void run_requests(otm_engine* E, std::vector<Req>& rq, std::vector<int>& codes, 
               bodies[(size_t)k] = std::move(out);
             }
           } else {
+#if OTM_JSON_SCRATCH
+            // written into a per-thread buffer that keeps its capacity, then
+            // copied once at its final size (no growth reallocations per body)
+            thread_local std::string scratch;
+            scratch.clear();
+            codes[(size_t)k] = otm::write_report_response(r, (int32_t)n, &scratch);
+            bodies[(size_t)k].assign(scratch);
+#else
             codes[(size_t)k] = otm::write_report_response(r, (int32_t)n, &out);
             bodies[(size_t)k] = std::move(out);
+#endif
           }
         }
       });

@@ -2,13 +2,19 @@
 #include <dlfcn.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <fstream>
 #include <exception>
+#include <functional>
+#include <memory>
+#include <mutex>
 #include <new>
 #include <sstream>
 #include <thread>
@@ -45,12 +51,118 @@ size_t host_threads(size_t n) {
   if (const char* v = std::getenv("OTM_HOST_CHUNK")) chunk = (size_t)std::max(1, std::atoi(v));
   return std::max<size_t>(1, std::min(cap, (n + chunk - 1) / chunk));
 }
-// fn(a, e) over [0, n) in contiguous chunks, one per thread (the caller's the first)
+// Persistent host workers for par_for: threads spawned per call cost ~75 thread
+// creations per 10k-request batch and dropped each thread's response scratch
+// buffer (below) with the thread.  A par_for posts its chunks as one job; the
+// workers and the caller take chunks until none is left, so a caller always
+// finishes its own job even when every worker is busy with another caller's.
+// The pool never calls HIP.  It is leaked at exit on purpose (its workers sit
+// in a wait; nothing to join).
+class HostPool {
+ public:
+  static HostPool& get() {
+    static HostPool* p = new HostPool();
+    return *p;
+  }
+  void run(size_t n, size_t T, const std::function<void(size_t, size_t)>& fn) {
+    auto job = std::make_shared<Job>();
+    job->fn = &fn;
+    job->n = n;
+    job->per = (n + T - 1) / T;
+    job->chunks = (n + job->per - 1) / job->per;
+    job->errs.resize(job->chunks);
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      grow(T - 1);
+      jobs_.push_back(job);
+    }
+    cv_.notify_all();
+    work(*job);
+    {
+      std::unique_lock<std::mutex> lk(job->m);
+      job->cv.wait(lk, [&] { return job->done == job->chunks; });
+    }
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      auto it = std::find(jobs_.begin(), jobs_.end(), job);
+      if (it != jobs_.end()) jobs_.erase(it);
+    }
+    for (auto& x : job->errs)
+      if (x) std::rethrow_exception(x);  // to the entry point's guard
+  }
+
+ private:
+  struct Job {
+    const std::function<void(size_t, size_t)>* fn = nullptr;
+    size_t n = 0, per = 0, chunks = 0;
+    std::atomic<size_t> next{0};
+    size_t done = 0;  // under m
+    std::vector<std::exception_ptr> errs;
+    std::mutex m;
+    std::condition_variable cv;
+  };
+  // chunks of job until none is left to take
+  static void work(Job& j) {
+    while (true) {
+      const size_t c = j.next.fetch_add(1);
+      if (c >= j.chunks) return;
+      const size_t a = c * j.per, e = std::min(j.n, a + j.per);
+      try {
+        (*j.fn)(a, e);
+      } catch (...) {
+        j.errs[c] = std::current_exception();
+      }
+      std::lock_guard<std::mutex> lk(j.m);
+      if (++j.done == j.chunks) j.cv.notify_all();
+    }
+  }
+  void grow(size_t want) {  // under mu_
+    while (nthreads_ < want) {
+      try {
+        std::thread([this] { loop(); }).detach();
+      } catch (...) {
+        return;  // no thread to be had: the callers take the chunks
+      }
+      ++nthreads_;
+    }
+  }
+  void loop() {
+    while (true) {
+      std::shared_ptr<Job> j;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] {
+          while (!jobs_.empty() && jobs_.front()->next.load() >= jobs_.front()->chunks) jobs_.pop_front();
+          return !jobs_.empty();
+        });
+        j = jobs_.front();
+      }
+      work(*j);
+    }
+  }
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<std::shared_ptr<Job>> jobs_;
+  size_t nthreads_ = 0;
+};
+
+bool host_pool() {
+  const char* v = std::getenv("OTM_HOST_POOL");
+  return !(v && *v == '0');
+}
+
+// fn(a, e) over [0, n) in contiguous chunks, one per thread (the caller's the
+// first); on the persistent pool unless OTM_HOST_POOL=0 (threads per call)
 template <class F>
 void par_for(size_t n, F fn) {
   const size_t T = host_threads(n);
   if (T <= 1) {
     fn((size_t)0, n);
+    return;
+  }
+  if (host_pool()) {
+    const std::function<void(size_t, size_t)> f = std::ref(fn);
+    HostPool::get().run(n, T, f);
     return;
   }
   const size_t per = (n + T - 1) / T;
@@ -89,6 +201,11 @@ void par_for(size_t n, F fn) {
 // sends every body through the DOM (A/B and the parity tests)
 bool fast_requests() {
   const char* v = std::getenv("OTM_FAST_JSON");
+  return !(v && *v == '0');
+}
+
+bool pack_reuse() {
+  const char* v = std::getenv("OTM_PACK_REUSE");
   return !(v && *v == '0');
 }
 
@@ -165,7 +282,7 @@ bool json_profile() {
   const char* v = std::getenv("OTM_JSON_PROFILE");
   return v && *v == '1';
 }
-thread_local double t_gpu_ms = 0.0, t_pack_ms = 0.0, t_write_ms = 0.0;
+thread_local double t_gpu_ms = 0.0, t_pack_ms = 0.0, t_write_ms = 0.0, t_extract_ms = 0.0;
 
 // One request of a batch: its DOM (parse_request), or -- for the Java
 // batcher's own bytes -- its points and uuid read directly (fast_request).
@@ -181,6 +298,7 @@ void run_requests(otm_engine* E, std::vector<Req>& rq, std::vector<int>& codes, 
                   const std::vector<int>& todo, bool match_only) {
   // points of every request that passed validation (extracted in parallel,
   // then laid out in request order)
+  const double te0 = now_ms();
   std::vector<uint8_t> ok(todo.size(), 0);
   par_for(todo.size(), [&](size_t a, size_t e) {
     for (size_t i = a; i < e; ++i) {
@@ -195,7 +313,8 @@ void run_requests(otm_engine* E, std::vector<Req>& rq, std::vector<int>& codes, 
     }
   });
   const double tp0 = now_ms();
-  t_gpu_ms = t_write_ms = 0.0;
+  t_extract_ms = tp0 - te0;
+  t_gpu_ms = t_write_ms = t_pack_ms = 0.0;
   std::vector<int64_t> off(1, 0);
   std::vector<int> which;  // request index of each batch trace
   for (size_t i = 0; i < todo.size(); ++i)
@@ -205,8 +324,24 @@ void run_requests(otm_engine* E, std::vector<Req>& rq, std::vector<int>& codes, 
     }
   if (which.empty()) return;
   const size_t np = (size_t)off.back();
-  std::vector<float> lat(np), lon(np), acc(np);
-  std::vector<double> tm(np);
+  // the batch arrays: per calling thread, kept between calls (grown, never
+  // shrunk) -- fresh ones cost ~3 ms of page faults to fill and ~2.5 ms to
+  // unmap per 1M points; OTM_PACK_REUSE=0 allocates them per call
+  thread_local std::vector<float> keep_lat, keep_lon, keep_acc;
+  thread_local std::vector<double> keep_tm;
+  std::vector<float> own_lat, own_lon, own_acc;
+  std::vector<double> own_tm;
+  const bool reuse = pack_reuse();
+  std::vector<float>& lat = reuse ? keep_lat : own_lat;
+  std::vector<float>& lon = reuse ? keep_lon : own_lon;
+  std::vector<float>& acc = reuse ? keep_acc : own_acc;
+  std::vector<double>& tm = reuse ? keep_tm : own_tm;
+  if (lat.size() < np) {
+    lat.resize(np);
+    lon.resize(np);
+    acc.resize(np);
+    tm.resize(np);
+  }
   par_for(which.size(), [&](size_t a, size_t e) {
     for (size_t n = a; n < e; ++n) {
       otm::TracePoints& tp = rq[(size_t)which[n]].tp;
@@ -330,8 +465,10 @@ void report_many(otm_engine* E, int n, const char* const* reqs, const size_t* le
   std::vector<Req>().swap(rq);
   const double t4 = now_ms();
   if (json_profile())
-    std::fprintf(stderr, "[otm json] %d requests: parse %.2f, pack %.2f, gpu %.2f, write %.2f, copy out %.2f, free %.2f ms\n",
-                 n, t1 - t0, t_pack_ms, t_gpu_ms, t_write_ms, t3 - t2, t4 - t3);
+    std::fprintf(stderr, "[otm json] %d requests: parse %.2f, extract %.2f, pack %.2f, gpu %.2f, write %.2f, "
+                 "tail %.2f, copy out %.2f, free %.2f ms\n",
+                 n, t1 - t0, t_extract_ms, t_pack_ms, t_gpu_ms, t_write_ms,
+                 (t2 - t1) - t_extract_ms - t_pack_ms - t_gpu_ms - t_write_ms, t3 - t2, t4 - t3);
 }
 
 void worker_loop(otm_engine* E) {

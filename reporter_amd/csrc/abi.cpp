@@ -462,6 +462,14 @@ void report_many(otm_engine* E, int n, const char* const* reqs, const size_t* le
     }
   });
   const double t3 = now_ms();
+  // the response strings released by the pool threads that wrote them (their
+  // allocator arenas), the requests with them
+  par_for((size_t)n, [&](size_t a, size_t e) {
+    for (size_t k = a; k < e; ++k) {
+      std::string().swap(bodies[k]);
+      rq[k] = Req();
+    }
+  });
   std::vector<Req>().swap(rq);
   const double t4 = now_ms();
   if (json_profile())

@@ -211,6 +211,10 @@ struct Parser {
       v->kind = Kind::Float;
       // correctly rounded like strtod (float('...')), without a temporary
       // string; overflow / underflow (inf, subnormal) go through strtod
+      if (decimal_fast(b, e, &v->f)) {
+        i = k;
+        return true;
+      }
       auto r = std::from_chars(b, e, v->f);
       if (r.ec != std::errc()) {
         std::string tmp(b, e);
@@ -350,6 +354,32 @@ struct Parser {
 };
 
 }  // namespace
+
+bool decimal_fast(const char* s, const char* e, double* out) {
+  static const double p10[16] = {1e0, 1e1, 1e2,  1e3,  1e4,  1e5,  1e6,  1e7,
+                                 1e8, 1e9, 1e10, 1e11, 1e12, 1e13, 1e14, 1e15};
+  const bool neg = s < e && *s == '-';
+  if (neg) ++s;
+  uint64_t m = 0;
+  int digits = 0, frac = -1;
+  for (; s < e; ++s) {
+    const char c = *s;
+    if (c >= '0' && c <= '9') {
+      m = m * 10 + (uint64_t)(c - '0');
+      if (++digits > 15) return false;
+      if (frac >= 0) ++frac;
+    } else if (c == '.' && frac < 0) {
+      frac = 0;
+    } else {
+      return false;
+    }
+  }
+  if (!digits || frac == 0) return false;
+  double d = (double)m;
+  if (frac > 0) d /= p10[frac];
+  *out = neg ? -d : d;
+  return true;
+}
 
 bool parse(std::string_view text, Value* out, std::string* err) {
   Parser p;

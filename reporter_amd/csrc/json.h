@@ -45,6 +45,12 @@ bool parse_jackson(std::string_view text, Value* out);
 // bytes.decode('utf-8') check: empty string when valid, else str(UnicodeDecodeError)
 std::string utf8_error(std::string_view bytes);
 
+// float('...') of a plain decimal [-]digits[.digits] with at most 15 digits in
+// all: the digits are an exact double below 2^53 and 10^k (k <= 15) is exact,
+// so one IEEE division is the correctly rounded value strtod returns (Clinger's
+// fast path).  false for anything else (exponents, more digits): use strtod.
+bool decimal_fast(const char* s, const char* e, double* out);
+
 // json.dumps(v, separators=(',', ':'))
 void dump(const Value& v, std::string* out);
 // float.__repr__ as json.dumps writes it (NaN / Infinity / -Infinity for non-finite)

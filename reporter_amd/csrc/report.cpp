@@ -550,6 +550,7 @@ bool fast_request(std::string_view b, TracePoints* out, std::string* uuid) {
     const char* s = b.data() + a;
     const char* e = b.data() + i;
     if (flt) {
+      if (json::decimal_fast(s, e, d)) return true;
       const auto r = std::from_chars(s, e, *d);
       return r.ec == std::errc() && r.ptr == e;
     }

@@ -93,3 +93,31 @@ def test_fast_reader_rejects_or_agrees_on_variants():
                                   b'{"uuid":"a","trace":[{"lat":1,"lon":2,"time":3},{"lat":1,"lon":2}]}'])
 def test_fast_reader_hands_back_invalid_requests(body):
     assert points(body, True)[0] == -2
+
+
+def test_decimal_reading_is_correctly_rounded():
+    """Float literals as float('...') reads them (json.loads), on both readers:
+    the short-decimal fast path (<= 15 digits, one exact division) and the
+    from_chars / strtod fallback for longer ones.  `time` keeps the double."""
+    rng = random.Random(9)
+    lits = ["0.1", "-0.0", "0.3", "1462826734.5", "123456789012345.6", "0.000000000000001",
+            "9007199254740993.0", "1.7976931348623157", "2.2250738585072014", "1234567.000000001",
+            "0.12345678901234567890123", "4.35", "100000000000000.0", "999999999999999.9"]
+    for _ in range(3000):
+        nd = rng.randint(1, 19)
+        digits = "".join(rng.choice("0123456789") for _ in range(nd))
+        cut = rng.randint(1, nd)
+        ip = digits[:cut].lstrip("0") or "0"
+        fp = digits[cut:] or "0"
+        lits.append(("-" if rng.random() < 0.3 else "") + ip + "." + fp)
+    for k in range(0, len(lits), 100):
+        chunk = lits[k:k + 100]
+        if len(chunk) < 2:
+            chunk = chunk + ["0.5"]
+        body = ('{"uuid":"u","trace":[' + ",".join('{"lat":37.5,"lon":-122.25,"time":%s}' % t for t in chunk)
+                + "]}").encode()
+        want = np.asarray([float(t) for t in chunk], np.float64).tobytes()
+        for fast in (True, False):
+            n, got = points(body, fast)
+            assert n == len(chunk)
+            assert got[2] == want, (fast, chunk)

@@ -521,43 +521,59 @@ bool extract_points(const Value& trace, TracePoints* out, std::string* err) {
 
 bool fast_request(std::string_view b, TracePoints* out, std::string* uuid) {
   const size_t n = b.size();
+  const char* const p = b.data();
   size_t i = 0;
   auto lit = [&](std::string_view w) {
-    if (b.compare(i, w.size(), w) != 0) return false;
+    if (i + w.size() > n || std::memcmp(p + i, w.data(), w.size()) != 0) return false;
     i += w.size();
     return true;
   };
-  auto digit = [&](size_t k) { return k < n && b[k] >= '0' && b[k] <= '9'; };
+  auto digit = [&](size_t k) { return k < n && (unsigned)(p[k] - '0') < 10u; };
   // a JSON number as json.loads + float() read it (int -> exact double,
-  // float -> correctly rounded)
+  // float -> correctly rounded), in one pass: up to 15 significant digits the
+  // digits are exact and one division by an exact power of ten is the correctly
+  // rounded value (json::decimal_fast); longer floats go through from_chars
+  static const double p10[16] = {1e0, 1e1, 1e2,  1e3,  1e4,  1e5,  1e6,  1e7,
+                                 1e8, 1e9, 1e10, 1e11, 1e12, 1e13, 1e14, 1e15};
   auto num = [&](double* d) {
     const size_t a = i;
-    if (i < n && b[i] == '-') ++i;
+    const bool neg = i < n && p[i] == '-';
+    if (neg) ++i;
     if (!digit(i)) return false;
-    if (b[i] == '0') {
+    uint64_t m = 0;
+    int nd = 0;
+    if (p[i] == '0') {
       ++i;
+      nd = 1;
     } else {
-      while (digit(i)) ++i;
+      while (digit(i)) {
+        m = m * 10 + (uint64_t)(p[i] - '0');
+        ++nd;
+        ++i;
+      }
     }
-    bool flt = false;
-    if (i < n && b[i] == '.') {
+    int frac = 0;
+    if (i < n && p[i] == '.') {
       if (!digit(i + 1)) return false;
-      flt = true;
       ++i;
-      while (digit(i)) ++i;
+      while (digit(i)) {
+        m = m * 10 + (uint64_t)(p[i] - '0');
+        ++nd;
+        ++frac;
+        ++i;
+      }
+      if (i < n && (p[i] == 'e' || p[i] == 'E')) return false;
+      if (nd <= 15) {
+        const double v = (double)m / p10[frac];
+        *d = neg ? -v : v;
+        return true;
+      }
+      const auto r = std::from_chars(p + a, p + i, *d);
+      return r.ec == std::errc() && r.ptr == p + i;
     }
-    if (i < n && (b[i] == 'e' || b[i] == 'E')) return false;
-    const char* s = b.data() + a;
-    const char* e = b.data() + i;
-    if (flt) {
-      if (json::decimal_fast(s, e, d)) return true;
-      const auto r = std::from_chars(s, e, *d);
-      return r.ec == std::errc() && r.ptr == e;
-    }
-    if (i - a > 18) return false;
-    int64_t v = 0;
-    const auto r = std::from_chars(s, e, v);
-    if (r.ec != std::errc() || r.ptr != e) return false;
+    if (i < n && (p[i] == 'e' || p[i] == 'E')) return false;
+    if (i - a > 18) return false;  // (m cannot have wrapped: at most 18 digits)
+    const int64_t v = neg ? -(int64_t)m : (int64_t)m;
     *d = (double)v;
     return true;
   };
@@ -594,16 +610,19 @@ bool fast_request(std::string_view b, TracePoints* out, std::string* uuid) {
         bool hl = false, ho = false, ht = false, ha = false;
         double la = 0.0, lo = 0.0, ti = 0.0, ac = 0.0;
         while (true) {
-          if (lit("\"lat\":")) {
+          // the key by its first letters, then checked whole (trying each key's
+          // literal in turn measured ~40% slower)
+          const char k1 = i + 2 < n ? p[i + 1] : 0, k2 = i + 2 < n ? p[i + 2] : 0;
+          if (k1 == 'l' && k2 == 'a' && lit("\"lat\":")) {
             if (hl || !num(&la)) return false;
             hl = true;
-          } else if (lit("\"lon\":")) {
+          } else if (k1 == 'l' && k2 == 'o' && lit("\"lon\":")) {
             if (ho || !num(&lo)) return false;
             ho = true;
-          } else if (lit("\"time\":")) {
+          } else if (k1 == 't' && lit("\"time\":")) {
             if (ht || !num(&ti)) return false;
             ht = true;
-          } else if (lit("\"accuracy\":")) {
+          } else if (k1 == 'a' && lit("\"accuracy\":")) {
             if (ha || !num(&ac)) return false;
             ha = true;
           } else {

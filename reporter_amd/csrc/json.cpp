@@ -488,7 +488,13 @@ void put_float(double d, std::string* out) {
     if (*p != '.') digits[nd++] = *p;
     ++p;
   }
-  const int e10 = std::atoi(std::string(p + 1, (size_t)(r.ptr - (p + 1))).c_str());
+  // the exponent to_chars wrote after the 'e': [+-]DD[D]
+  int e10 = 0;
+  const char* q = p + 1;
+  const bool eneg = q < r.ptr && *q == '-';
+  if (q < r.ptr && (*q == '-' || *q == '+')) ++q;
+  for (; q < r.ptr; ++q) e10 = e10 * 10 + (*q - '0');
+  if (eneg) e10 = -e10;
   const int decpt = e10 + 1;  // value = 0.DIGITS x 10^decpt
   if (neg) out->push_back('-');
   if (decpt > -4 && decpt <= 16) {  // float_repr_style 'short', repr rules

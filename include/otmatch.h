@@ -75,6 +75,16 @@ typedef struct otm_engine otm_engine;
 int otm_engine_create(const char* cfg_path, const int* devices, int ndev,
                       otm_engine** out);
 /* Members of an engine: ndev of a multi-device engine, 1 otherwise. */
+/* The matcher parameters a config file gives, without a device: meili's
+ * "default" section with the mode's section ("meili.mode", default "auto")
+ * on top, as valhalla.Configure (py/reporter_service.py:279) reads the meili
+ * config.  otm_engine_create uses exactly these. */
+typedef struct otm_meili_params {
+  float sigma_z, beta, max_route_distance_factor, breakage_distance, interpolation_distance;
+  float search_radius, max_search_radius, gps_accuracy, turn_penalty_factor;
+  int32_t max_candidates;
+} otm_meili_params;
+int otm_config_meili(const char* cfg_path, otm_meili_params* out);
 int otm_engine_members(const otm_engine* eng);
 /* Member i of a multi-device engine (NULL when out of range); a one-device
  * engine is its own member 0.  Owned by eng. */

@@ -475,6 +475,7 @@ typedef struct batch {
   uint8_t* chain_start;
   int32_t *ncand, *cand_edge, *state, *col_prev;
   float *cand_off, *cand_emis, *route_dist, *gc;
+  float* ipos;   /* interpolated points: position along their step's route, -1 none (S7) */
   int32_t* terr; /* per trace error kind */
   int64_t* trans_off;
   float* trans;
@@ -796,9 +797,122 @@ static int route_step(batch* B, ws* w, int64_t p, int32_t* path, int* plen, int*
   return 0;
 }
 
-static double time_at(double ta, double tb, float x, float R) {
-  if (R > 0.0f) return ta + (tb - ta) * ((double)x / (double)R);
-  return ta;
+/* ------------------------------------------------------------ S7a interpolated points
+ * a point within interpolation_distance of the previous
+ * column gets no HMM state and is "projected onto the final route
+ * afterwards"; README.md:162-163 defines begin/end_shape_index as the trace
+ * index "before/at" a segment's start/end.  So the interpolated points of a
+ * step q -> p (q < k < p; a step that stays on one edge has no boundary inside
+ * it and needs none) are placed on the step's route:
+ *   pieces, in route order: the rest of q's edge [off_q, len] (none for a node
+ *   candidate), the path's edges [0, len], p's edge [0, off_p] (none for a node
+ *   candidate); piece m starts at route distance xs_m;
+ *   on each piece, the point's best projection onto that edge's polyline
+ *   (lowest sqdist, ties the lowest shape segment) is admissible iff its
+ *   offset lies inside the piece; its position is xs_m + (off - o0_m) and its
+ *   cost sqdist / (2 sigma_z^2) + |position - gc(q, k)| / beta -- meili's
+ *   emission plus a transition from q (no turns), the lowest cost winning
+ *   (ties: the earliest piece);
+ *   a point with no admissible piece, or placed behind an earlier point of the
+ *   step (position below the running maximum, starting at q's 0), stays
+ *   unplaced (-1).
+ * The placed points and the two states are the step's anchors (positions
+ * nondecreasing in trace order).  A boundary at route distance x gets
+ *   shape index = the last anchor (trace order) at position <= x;
+ *   time = linear between the last anchor L before p with position <= x and
+ *   the anchor N after it: t_L + (t_N - t_L) * ((x - x_L) / (x_N - x_L)),
+ *   t_L when x_N == x_L.
+ * A step without placed points is the two-state rule: t_q + (t_p - t_q) * x /
+ * R, and q's index unless x reaches R. */
+typedef struct {
+  int32_t edge;
+  float o0, o1, xs;
+} piece;
+
+static float interp_pos(const batch* B, const piece* pc, int npc, int64_t q, int64_t k) {
+  const orc_graph* g = B->g;
+  const float lat = B->lat[k], lon = B->lon[k];
+  const float ls = MPD_F * orc_cos_deg(lat);
+  const float gcd = orc_gc(B->lat[q], B->lon[q], lat, lon);
+  const float ds = (2.0f * B->P->sigma_z) * B->P->sigma_z;
+  float best = INF_F, bpos = -1.0f;
+  for (int m = 0; m < npc; ++m) {
+    const int32_t e = pc[m].edge;
+    const int nsh = g->eshape[e + 1] - g->eshape[e] - 1;
+    float bsq = INF_F, boff = 0.0f;
+    for (int s = 0; s < nsh; ++s) {
+      float sqd, off;
+      int at_end;
+      project(g, e, s, lat, lon, ls, &sqd, &off, &at_end);
+      if (sqd < bsq) {
+        bsq = sqd;
+        boff = off;
+      }
+    }
+    if (!(boff >= pc[m].o0 && boff <= pc[m].o1)) continue;
+    const float pos = pc[m].xs + (boff - pc[m].o0);
+    const float cost = bsq / ds + fabsf(pos - gcd) / B->P->beta;
+    if (cost < best) {
+      best = cost;
+      bpos = pos;
+    }
+  }
+  return bpos;
+}
+
+/* places the interpolated points of step q -> p (route: the rest of e_i from
+   o_i, path[0..plen), e_j up to o_j) */
+static void interp_step(batch* B, int64_t q, int64_t p, int32_t ei, float oi, int32_t ej, float oj,
+                        const int32_t* path, int plen) {
+  if (p - q < 2) return;
+  const orc_graph* g = B->g;
+  piece* pc = (piece*)malloc(sizeof(piece) * (size_t)(plen + 2));
+  int n = 0;
+  const float start = src_start(g, ei, oi);
+  if (oi != 0.0f) pc[n++] = (piece){ei, oi, g->elen[ei], 0.0f};
+  float dd = 0.0f;
+  for (int k = 0; k < plen; ++k) {
+    const float len = g->elen[path[k]];
+    pc[n++] = (piece){path[k], 0.0f, len, start + dd};
+    dd = dd + len;
+  }
+  if (oj != 0.0f) pc[n++] = (piece){ej, 0.0f, oj, start + dd};
+  float run = 0.0f;
+  for (int64_t k = q + 1; k < p; ++k) {
+    const float v = interp_pos(B, pc, n, q, k);
+    if (v >= 0.0f && v >= run) {
+      B->ipos[k] = v;
+      run = v;
+    } else {
+      B->ipos[k] = -1.0f;
+    }
+  }
+  free(pc);
+}
+
+/* time and shape index (relative to trace start a) of the boundary at route
+   distance x of step q -> p */
+static void step_bound(const batch* B, int64_t a, int64_t q, int64_t p, float R, float x, double* t, int32_t* sh) {
+  int64_t iL = q, k = q + 1;
+  float xL = 0.0f, xN = R;
+  double tL = B->time[q], tN = B->time[p];
+  for (; k < p; ++k) {
+    const float v = B->ipos[k];
+    if (!(v >= 0.0f)) continue;
+    if (!(v <= x)) break;
+    iL = k;
+    xL = v;
+    tL = B->time[k];
+  }
+  for (; k < p; ++k)
+    if (B->ipos[k] >= 0.0f) {
+      xN = B->ipos[k];
+      tN = B->time[k];
+      break;
+    }
+  *sh = (int32_t)((R <= x ? p : iL) - a);
+  const float den = xN - xL;
+  *t = den > 0.0f ? tL + (tN - tL) * ((double)(x - xL) / (double)den) : tL;
 }
 
 static int segments_of_trace(batch* B, ws* w, int32_t t, tres* R, orc_counters* C) {
@@ -854,18 +968,16 @@ static int segments_of_trace(batch* B, ws* w, int32_t t, tres* R, orc_counters* 
       break;
     }
     B->route_dist[p] = Rd;
-    const double ta = B->time[lastp], tb = B->time[p];
-    const int32_t ca = (int32_t)(lastp - a), cb = (int32_t)(p - a);
     if (!same) {
       /* close the traversal on the state's edge, unless the state is a node
          candidate: its route starts at the node */
       const int32_t ei = cur.edge;
       const float oi = B->cand_off[lastp * ORC_KMAX + B->state[lastp]];
+      interp_step(B, lastp, p, ei, oi, ej, oj, path, plen);
       const float start = src_start(g, ei, oi);
       float x = start;
       cur.off1 = g->elen[ei];
-      cur.t1 = time_at(ta, tb, x, Rd);
-      cur.sh1 = x >= Rd ? cb : ca;
+      step_bound(B, a, lastp, p, Rd, x, &cur.t1, &cur.sh1);
       if (oi != 0.0f) tpush(&T, cur);
       float dd = 0.0f;
       for (int k = 0; k < plen; ++k) {
@@ -877,17 +989,14 @@ static int segments_of_trace(batch* B, ws* w, int32_t t, tres* R, orc_counters* 
         const float xb = start + dd;
         dd = dd + g->elen[pe];
         const float xe = start + dd;
-        m.t0 = time_at(ta, tb, xb, Rd);
-        m.t1 = time_at(ta, tb, xe, Rd);
-        m.sh0 = xb >= Rd ? cb : ca;
-        m.sh1 = xe >= Rd ? cb : ca;
+        step_bound(B, a, lastp, p, Rd, xb, &m.t0, &m.sh0);
+        step_bound(B, a, lastp, p, Rd, xe, &m.t1, &m.sh1);
         tpush(&T, m);
       }
       x = start + dd;
       cur.edge = ej;
       cur.off0 = 0.0f;
-      cur.t0 = time_at(ta, tb, x, Rd);
-      cur.sh0 = x >= Rd ? cb : ca;
+      step_bound(B, a, lastp, p, Rd, x, &cur.t0, &cur.sh0);
     }
     nstate++;
     lastp = p;
@@ -970,7 +1079,10 @@ static void phase_b(batch* B, ws* w, int32_t t, orc_counters* C) {
   R->tr.shape_used = -1;
   R->tr.successful_length = R->tr.unreported_length = -1;
   int err = B->terr[t];
-  for (int64_t p = a; p < b; ++p) B->route_dist[p] = 0.0f;
+  for (int64_t p = a; p < b; ++p) {
+    B->route_dist[p] = 0.0f;
+    B->ipos[p] = -1.0f;
+  }
   if (!err) {
     for (int64_t p = a; p < b && !err; ++p)
       if (B->is_col[p] && B->col_prev[p] >= 0)
@@ -1081,6 +1193,7 @@ int orc_match_batch(const orc_graph* g, const orc_params* p, const orc_report_cf
   B.col_prev = (int32_t*)calloc(PP, 4);
   B.route_dist = (float*)calloc(PP, 4);
   B.gc = (float*)calloc(PP, 4);
+  B.ipos = (float*)calloc(PP, 4);
   B.terr = (int32_t*)calloc((size_t)n_traces + 1, 4);
   B.trans_off = (int64_t*)calloc(PP, 8);
   B.res = (tres*)calloc((size_t)n_traces + 1, sizeof(tres));
@@ -1149,6 +1262,7 @@ int orc_match_batch(const orc_graph* g, const orc_params* p, const orc_report_cf
     out->col_prev = B.col_prev;
     out->route_dist = B.route_dist;
     out->gc = B.gc;
+    out->ipos = B.ipos;
   } else {
     free(B.ncand);
     free(B.cand_edge);
@@ -1160,6 +1274,7 @@ int orc_match_batch(const orc_graph* g, const orc_params* p, const orc_report_cf
     free(B.col_prev);
     free(B.route_dist);
     free(B.gc);
+    free(B.ipos);
   }
   free(B.is_col);
   free(B.chain_start);
@@ -1184,6 +1299,7 @@ void orc_results_free(orc_results* r) {
   free(r->col_prev);
   free(r->route_dist);
   free(r->gc);
+  free(r->ipos);
   memset(r, 0, sizeof *r);
 }
 

@@ -91,6 +91,7 @@ typedef struct orc_results {
   float* route_dist;   /* [P]        */
   float* gc;           /* [P]        */
   orc_counters counters;
+  float* ipos;         /* [P] interpolated points: route position in their step, -1 none */
 } orc_results;
 
 orc_graph* orc_graph_load(const char* path);

@@ -50,7 +50,7 @@ class Results(C.Structure):
                 ("ncand", C.c_void_p), ("cand_edge", C.c_void_p), ("cand_off", C.c_void_p),
                 ("cand_emis", C.c_void_p), ("trans_off", C.c_void_p), ("trans", C.c_void_p),
                 ("state", C.c_void_p), ("col_prev", C.c_void_p), ("route_dist", C.c_void_p),
-                ("gc", C.c_void_p), ("counters", Counters)]
+                ("gc", C.c_void_p), ("counters", Counters), ("ipos", C.c_void_p)]
 
 
 _lib = None
@@ -193,6 +193,7 @@ def match_batch(graph, batch, p=None, rc=None, nthreads=1, keep_stages=False):
         out["col_prev"] = _arr(r.col_prev, np.int32, P)
         out["route_dist"] = _arr(r.route_dist, np.float32, P)
         out["gc"] = _arr(r.gc, np.float32, P)
+        out["ipos"] = _arr(r.ipos, np.float32, P)
     lib().orc_results_free(C.byref(r))
     return out
 

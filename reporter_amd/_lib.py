@@ -87,6 +87,13 @@ class SynthGraphParams(C.Structure):
                 ("seed", C.c_uint64)]
 
 
+class MeiliParams(C.Structure):
+    """otm_meili_params (include/otmatch.h)"""
+    _fields_ = [(n, C.c_float) for n in ("sigma_z", "beta", "max_route_distance_factor", "breakage_distance",
+                                         "interpolation_distance", "search_radius", "max_search_radius",
+                                         "gps_accuracy", "turn_penalty_factor")] + [("max_candidates", C.c_int32)]
+
+
 class SynthTraceParams(C.Structure):
     _fields_ = [("n_vehicles", C.c_int32), ("points_per_vehicle", C.c_int32), ("interval_s", C.c_double),
                 ("noise_sigma_m", C.c_double), ("accuracy", C.c_float), ("t0", C.c_double), ("seed", C.c_uint64),
@@ -117,6 +124,7 @@ def _declare(L):
     sig = {
         "otm_engine_create": (C.c_int, [C.c_char_p, C.POINTER(C.c_int), C.c_int, pp]),
         "otm_engine_members": (C.c_int, [vp]),
+        "otm_config_meili": (C.c_int, [C.c_char_p, vp]),
         "otm_request_points": (C.c_int, [C.c_char_p, sz, C.c_int, vp, vp, vp, vp, C.c_int, C.c_char_p, sz]),
         "otm_engine_member": (vp, [vp, C.c_int]),
         "otm_engine_destroy": (None, [vp]),

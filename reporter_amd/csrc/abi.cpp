@@ -211,6 +211,7 @@ bool pack_reuse() {
 
 char* dup_out(const std::string& s, size_t* n) {
   char* p = (char*)std::malloc(s.size() + 1);
+  if (!p) throw std::bad_alloc();
   std::memcpy(p, s.data(), s.size());
   p[s.size()] = 0;
   if (n) *n = s.size();
@@ -227,20 +228,19 @@ bool read_file(const char* path, std::string* out) {
 }
 
 // The level sets of make_thread_locals (py/reporter_service.py:55-56) for
-// k_report: Python sets, so duplicates collapse; the device config holds at
-// most 16 distinct levels of each (a level is segment_id & 7, so only 8 can
-// ever match -- more distinct entries are rejected rather than cut).
+// k_report: Python sets, so duplicates collapse.  A level tested against them
+// is segment_id & 7 (:154) or -1 (no segment id), so only -1..7 can ever
+// match: other values are dropped here (the reference accepts any int and
+// they never match), leaving at most 9 distinct levels for the device config.
 bool device_levels(const std::vector<int64_t>& in, int64_t* out, int* n, const char* name, std::string* err) {
+  (void)name;
+  (void)err;
   *n = 0;
   for (int64_t v : in) {
+    if (v < -1 || v > 7) continue;
     bool dup = false;
     for (int k = 0; k < *n; ++k) dup = dup || out[k] == v;
-    if (dup) continue;
-    if (*n == 16) {
-      *err = std::string(name) + ": more than 16 distinct levels";
-      return false;
-    }
-    out[(*n)++] = v;
+    if (!dup) out[(*n)++] = v;
   }
   return true;
 }
@@ -455,12 +455,29 @@ void report_many(otm_engine* E, int n, const char* const* reqs, const size_t* le
   const double t1 = now_ms();
   run_requests(E, rq, c, bodies, todo, false);
   const double t2 = now_ms();
+  // every response body or none: a failed allocation frees the ones already
+  // made (the caller gets only the error, nothing to otm_free)
+  std::atomic<bool> oom{false};
   par_for((size_t)n, [&](size_t a, size_t e) {
     for (size_t k = a; k < e; ++k) {
       codes[k] = c[k];
-      resps[k] = dup_out(bodies[k], &resp_lens[k]);
+      resps[k] = (char*)std::malloc(bodies[k].size() + 1);
+      if (!resps[k]) {
+        oom = true;
+        continue;
+      }
+      std::memcpy(resps[k], bodies[k].data(), bodies[k].size());
+      resps[k][bodies[k].size()] = 0;
+      resp_lens[k] = bodies[k].size();
     }
   });
+  if (oom) {
+    for (int k = 0; k < n; ++k) {
+      std::free(resps[k]);
+      resps[k] = nullptr;
+    }
+    throw std::bad_alloc();
+  }
   const double t3 = now_ms();
   // the response strings released by the pool threads that wrote them (their
   // allocator arenas), the requests with them
@@ -530,6 +547,74 @@ const char* otm_runtime_info(void) {
   return info.c_str();
 }
 
+// The matcher parameters of a config, as meili builds them: the
+// "meili.default" section with the travel mode's own section on top
+// ("meili.<mode>", mode = "meili.mode" or "auto", the mode reporter_service.py's
+// matches run in: README.md:136).  A stock valhalla_build_config file has
+// default.turn_penalty_factor 0 and auto.turn_penalty_factor 200 (SURVEY
+// Appendix B), so an auto match runs with 200.
+static bool read_meili(const Value& cfg, otm::MatchConfig* mc, std::string* err) {
+  const Value* meili = cfg.get("meili");
+  std::string mode = "auto";
+  if (meili) {
+    const Value* m = meili->get("mode");
+    if (m && m->kind == Kind::Str) mode = m->s;
+  }
+  for (const char* sec : {"default", mode.c_str()}) {
+    const Value* d = meili ? meili->get(sec) : nullptr;
+    if (!d || d->kind != Kind::Obj) continue;
+    auto getf = [&](const char* k, float* dst) {
+      const Value* v = d->get(k);
+      if (v && v->is_num()) *dst = (float)v->num();
+    };
+    getf("sigma_z", &mc->sigma_z);
+    getf("beta", &mc->beta);
+    getf("max_route_distance_factor", &mc->max_route_distance_factor);
+    getf("breakage_distance", &mc->breakage_distance);
+    getf("interpolation_distance", &mc->interpolation_distance);
+    getf("search_radius", &mc->search_radius);
+    getf("max_search_radius", &mc->max_search_radius);
+    getf("gps_accuracy", &mc->gps_accuracy);
+    getf("turn_penalty_factor", &mc->turn_penalty_factor);
+    const Value* mk = d->get("max_candidates");
+    if (mk && mk->kind == Kind::Int) mc->max_candidates = (int)mk->i;
+  }
+  if (!(mc->turn_penalty_factor >= 0.0f && mc->turn_penalty_factor <= 10000.0f)) {
+    *err = "turn_penalty_factor must be in [0, 10000]";
+    return false;
+  }
+  if (mc->max_candidates < 1 || mc->max_candidates > otm::KMAX) {
+    *err = "max_candidates must be in [1, 32]";
+    return false;
+  }
+  return true;
+}
+
+int otm_config_meili(const char* cfg_path, otm_meili_params* out) {
+  if (!cfg_path || !out) return fail(OTM_EINVAL, "bad arguments");
+  try {
+    std::string text, perr;
+    if (!read_file(cfg_path, &text)) return fail(OTM_EINVAL, std::string("cannot read config ") + cfg_path);
+    Value cfg;
+    if (!otm::json::parse(text, &cfg, &perr)) return fail(OTM_EINVAL, "config: " + perr);
+    otm::MatchConfig mc;
+    if (!read_meili(cfg, &mc, &perr)) return fail(OTM_EINVAL, perr);
+    out->sigma_z = mc.sigma_z;
+    out->beta = mc.beta;
+    out->max_route_distance_factor = mc.max_route_distance_factor;
+    out->breakage_distance = mc.breakage_distance;
+    out->interpolation_distance = mc.interpolation_distance;
+    out->search_radius = mc.search_radius;
+    out->max_search_radius = mc.max_search_radius;
+    out->gps_accuracy = mc.gps_accuracy;
+    out->turn_penalty_factor = mc.turn_penalty_factor;
+    out->max_candidates = mc.max_candidates;
+    return OTM_OK;
+  } catch (const std::bad_alloc&) {
+    return fail(OTM_ENOMEM, "out of host memory");
+  }
+}
+
 static int otm_engine_create_impl(const char* cfg_path, const int* devices, int ndev, otm_engine** out) {
   if (!out) return fail(OTM_EINVAL, "out is NULL");
   *out = nullptr;
@@ -595,34 +680,11 @@ static int otm_engine_create_impl(const char* cfg_path, const int* devices, int 
     delete E;
     return fail(OTM_EINVAL, "trans_lanes must be 4, 8, 16, 32 or 64");
   }
-  const Value* meili = cfg.get("meili");
-  const Value* dflt = meili ? meili->get("default") : nullptr;
-  if (dflt && dflt->kind == Kind::Obj) {
-    auto getf = [&](const char* k, float* dst) {
-      const Value* v = dflt->get(k);
-      if (v && v->is_num()) *dst = (float)v->num();
-    };
-    getf("sigma_z", &E->mc.sigma_z);
-    getf("beta", &E->mc.beta);
-    getf("max_route_distance_factor", &E->mc.max_route_distance_factor);
-    getf("breakage_distance", &E->mc.breakage_distance);
-    getf("interpolation_distance", &E->mc.interpolation_distance);
-    getf("search_radius", &E->mc.search_radius);
-    getf("max_search_radius", &E->mc.max_search_radius);
-    getf("gps_accuracy", &E->mc.gps_accuracy);
-    getf("turn_penalty_factor", &E->mc.turn_penalty_factor);
-    const Value* mk = dflt->get("max_candidates");
-    if (mk && mk->kind == Kind::Int) E->mc.max_candidates = (int)mk->i;
-  }
-  if (!(E->mc.turn_penalty_factor >= 0.0f && E->mc.turn_penalty_factor <= 10000.0f)) {
-    delete E;
-    return fail(OTM_EINVAL, "turn_penalty_factor must be in [0, 10000]");
-  }
-  if (E->mc.max_candidates < 1 || E->mc.max_candidates > otm::KMAX) {
-    delete E;
-    return fail(OTM_EINVAL, "max_candidates must be in [1, 32]");
-  }
   std::string err;
+  if (!read_meili(cfg, &E->mc, &err)) {
+    delete E;
+    return fail(OTM_EINVAL, err);
+  }
   if (!otm::read_report_env(&E->rc, &err)) {
     delete E;
     return fail(OTM_ECONFIG, err);
@@ -688,6 +750,7 @@ otm_engine* otm_engine_member(otm_engine* E, int i) {
 }
 
 static int otm_report_impl(otm_engine* E, const char* req, size_t len, char** resp, size_t* resp_len) {
+  if (!E || !resp || (!req && len)) return fail(OTM_EINVAL, "bad arguments");
   int code = 0;
   const char* reqs[1] = {req};
   report_many(E, 1, reqs, &len, &code, resp, resp_len);
@@ -737,6 +800,7 @@ int otm_request_points(const char* req, size_t len, int fast, float* lat, float*
 }
 
 static int otm_match_json_impl(otm_engine* E, const char* req, size_t len, char** resp, size_t* resp_len) {
+  if (!E || !resp || (!req && len)) return fail(OTM_EINVAL, "bad arguments");
   std::vector<Req> rq(1);
   std::vector<int> codes(1, 0);
   std::vector<std::string> bodies(1);

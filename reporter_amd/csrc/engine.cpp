@@ -459,7 +459,7 @@ void engine_free(otm_engine* E) {
       &E->pt_trace,
       &E->is_col,        &E->prevc,        &E->gc,             &E->ncand,          &E->cand_edge,
       &E->probe,         &E->col_prev,     &E->kq_prev,        &E->trans_off,      &E->trans,          &E->bp,         &E->state,      &E->chosen,
-      &E->chain_start,   &E->route_dist,   &E->path_off,       &E->path_len,       &E->path_pool,  &E->trace_err,
+      &E->chain_start,   &E->route_dist,   &E->ipos,   &E->path_off,       &E->path_len,       &E->path_pool,  &E->trace_err,
       &E->overflow_list0, &E->overflow_list, &E->overflow_list2, &E->counters_i32, &E->scan_tmp, &E->snap,   &E->big_key,
       &E->big_lab,       &E->big_inq,      &E->big_fr,         &E->o_traces,       &E->o_seg_cnt,  &E->o_way_cnt,
       &E->o_segments,    &E->o_seg_gidx,   &E->o_way_ids,      &E->o_reports,  &E->o_rep_cnt,  &E->seg_ub,
@@ -521,6 +521,7 @@ static int engine_match_once(otm_engine* E, const DevBatch& b, hipStream_t s, st
   ENS(chosen, Pn * 8);
   ENS(chain_start, Pn);
   ENS(route_dist, Pn * 4);
+  ENS(ipos, Pn * 4);
   ENS(path_off, Pn * 4);
   ENS(path_len, Pn * 4);
   ENS(trace_err, ((size_t)NT + 1) * 4);
@@ -576,6 +577,7 @@ static int engine_match_once(otm_engine* E, const DevBatch& b, hipStream_t s, st
   w.chosen = P<int2>(E->chosen);
   w.chain_start = P<uint8_t>(E->chain_start);
   w.route_dist = P<float>(E->route_dist);
+  w.ipos = P<float>(E->ipos);
   w.path_off = P<int32_t>(E->path_off);
   w.path_len = P<int32_t>(E->path_len);
   w.path_pool = P<int32_t>(E->path_pool);
@@ -672,7 +674,7 @@ static int engine_match_once(otm_engine* E, const DevBatch& b, hipStream_t s, st
     o.nbins = H->nbins;
     o.bin_kph = H->bin_kph;
   }
-  launch_seg_bound(b, w, P<int64_t>(E->seg_ub), s, mk);
+  launch_seg_bound(E->g, b, dp, w, P<int64_t>(E->seg_ub), s, mk);
   mk.begin(KN_SEG_SCAN, s);
   scan_i64(P<int64_t>(E->seg_ub), NP, E->scan_tmp.p, E->scan_tmp.cap, s);
   mk.end(KN_SEG_SCAN, s);
@@ -1054,6 +1056,7 @@ int engine_debug_fetch(otm_engine* E, int what, void* dst, size_t bytes, size_t*
     case 7: src = E->col_prev.p; n = Pn * 4; break;
     case 8: src = E->route_dist.p; n = Pn * 4; break;
     case 9: src = E->gc.p; n = Pn * 4; break;
+    case 10: src = E->ipos.p; n = Pn * 4; break;
     default: *err = "unknown debug buffer"; return OTM_EINVAL;
   }
   if (needed) *needed = n;

@@ -32,16 +32,16 @@ int shard_of(const char* key, size_t len, int n) {
 // of host memory each that the HIP runtime keeps after the thread exits.)
 struct MemberPool {
   explicit MemberPool(size_t n) : slots_(n) {
-    for (size_t i = 0; i < n; ++i) th_.emplace_back([this, i] { loop(i); });
-  }
-  ~MemberPool() {
-    {
-      std::lock_guard<std::mutex> lk(mu_);
-      stop_ = true;
+    try {
+      for (size_t i = 0; i < n; ++i) th_.emplace_back([this, i] { loop(i); });
+    } catch (...) {
+      // a thread that failed to start: stop and join the ones that did, so
+      // no joinable std::thread is destroyed (std::terminate), then report it
+      stop_all();
+      throw;
     }
-    cv_.notify_all();
-    for (auto& t : th_) t.join();
   }
+  ~MemberPool() { stop_all(); }
   void run(std::vector<std::function<void()>>& tasks) {
     std::unique_lock<std::mutex> lk(mu_);
     pending_ = 0;
@@ -56,6 +56,15 @@ struct MemberPool {
   }
 
  private:
+  void stop_all() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : th_)
+      if (t.joinable()) t.join();
+  }
   void loop(size_t i) {
     uint64_t seen = 0;
     while (true) {

@@ -156,6 +156,7 @@ struct DevWork {
   int2* chosen;          // [P] the chosen candidate {edge, offset bits} where state >= 0 (K5)
   uint8_t* chain_start;  // [P]
   float* route_dist;     // [P]
+  float* ipos;           // [P] interpolated point: position along its step's route (K7a), -1 none
   int32_t* path_off;     // [P]
   int32_t* path_len;     // [P]
   int32_t* path_pool;    // [pool_cap]
@@ -261,7 +262,8 @@ void launch_report(const DevBatch& b, const DevReportCfg& rc, DevWork& w, DevOut
 void launch_order(const DevBatch& b, DevWork& w, hipStream_t s, const Marks& mk);
 // per-point bound of the segments / way ids a matched point can emit (scanned
 // into DevOut::seg_base)
-void launch_seg_bound(const DevBatch& b, DevWork& w, int64_t* ub, hipStream_t s, const Marks& mk);
+void launch_seg_bound(const DevGraph& g, const DevBatch& b, const DevParams& p, DevWork& w, int64_t* ub, hipStream_t s,
+                      const Marks& mk);
 // fetch-time compaction of the per-trace regions into dense arrays; offsets
 // are the exclusive scans of seg_cnt / way_cnt / rep_cnt
 void launch_compact(int32_t n_traces, const DevOut& o, const int32_t* seg_off, const int32_t* way_off,

@@ -398,6 +398,7 @@ __global__ __launch_bounds__(TB) void k_columns(DevGraph g, DevBatch b, DevParam
         w.pt_trace[p] = t;
         w.ncand[p] = 0;
         w.route_dist[p] = 0.0f;
+        w.ipos[p] = -1.0f;
         w.path_len[p] = 0;
         w.path_off[p] = 0;
       }
@@ -452,6 +453,7 @@ __global__ __launch_bounds__(TB) void k_columns(DevGraph g, DevBatch b, DevParam
           // later stages write these for columns only (spatial work order)
           w.ncand[p] = 0;
           w.route_dist[p] = 0.0f;
+          w.ipos[p] = -1.0f;
           w.path_len[p] = 0;
           w.path_off[p] = 0;
         }
@@ -2945,6 +2947,43 @@ __device__ __forceinline__ double time_at(double ta, double tb, float x, float R
   return ta;
 }
 
+// The boundary of step lp -> pl (trace-local points of the trace at a) at
+// route distance x (DESIGN.md §3 rule 7, oracle step_bound): the step's
+// anchors are lp (position 0), its placed interpolated points (K7a) and pl (R);
+// the time is linear between the last anchor before pl at position <= x and
+// the anchor after it, the shape index is the last anchor at position <= x.
+// Without interpolated points: the two-state rule, bit for bit.
+__device__ __forceinline__ void step_bound(const DevBatch& b, const DevWork& w, int64_t a, int lp, int pl, float R,
+                                           double ta, double tb, float x, double& t, int& sh) {
+  if (pl - lp < 2) {
+    t = time_at(ta, tb, x, R);
+    sh = x >= R ? pl : lp;
+    return;
+  }
+  int iL = lp, k = lp + 1;
+  float xL = 0.0f, xN = R;
+  double tL = ta, tN = tb;
+  for (; k < pl; ++k) {
+    const float v = w.ipos[a + k];
+    if (!(v >= 0.0f)) continue;
+    if (!(v <= x)) break;
+    iL = k;
+    xL = v;
+    tL = b.time[a + k];
+  }
+  for (; k < pl; ++k) {
+    const float v = w.ipos[a + k];
+    if (v >= 0.0f) {
+      xN = v;
+      tN = b.time[a + k];
+      break;
+    }
+  }
+  sh = R <= x ? pl : iL;
+  const float den = xN - xL;
+  t = den > 0.0f ? tL + (tN - tL) * ((double)(x - xL) / (double)den) : tL;
+}
+
 // Point data of one trace as the emitter reads it: straight from HBM ...
 struct SegSrcGlobal {
   const DevGraph* g;
@@ -3022,8 +3061,9 @@ __device__ void segments_trace(const DevGraph& g, const DevWork& w, DevOut& o, i
       const float start = cand_node(oi) ? 0.0f : elen - oi;
       float x = start;
       cur.off1 = elen;
-      cur.t1 = time_at(ta, tb, x, Rd);
-      cur.sh1 = x >= Rd ? cb : ca;
+      int sh;
+      step_bound(*S.b, w, S.a, ca, cb, Rd, ta, tb, x, cur.t1, sh);
+      cur.sh1 = sh;
       if (!cand_node(oi)) em.push(cur);
       float dd = 0.0f;
       const int32_t po = S.poff(p), pl = S.plen(p);
@@ -3037,18 +3077,18 @@ __device__ void segments_trace(const DevGraph& g, const DevWork& w, DevOut& o, i
         const float xb = start + dd;
         dd = dd + m.at.len;
         const float xe = start + dd;
-        m.t0 = time_at(ta, tb, xb, Rd);
-        m.t1 = time_at(ta, tb, xe, Rd);
-        m.sh0 = xb >= Rd ? cb : ca;
-        m.sh1 = xe >= Rd ? cb : ca;
+        step_bound(*S.b, w, S.a, ca, cb, Rd, ta, tb, xb, m.t0, sh);
+        m.sh0 = sh;
+        step_bound(*S.b, w, S.a, ca, cb, Rd, ta, tb, xe, m.t1, sh);
+        m.sh1 = sh;
         em.push(m);
       }
       x = start + dd;
       cur.edge = ej;
       cur.at = S.attr(p);
       cur.off0 = 0.0f;
-      cur.t0 = time_at(ta, tb, x, Rd);
-      cur.sh0 = x >= Rd ? cb : ca;
+      step_bound(*S.b, w, S.a, ca, cb, Rd, ta, tb, x, cur.t0, sh);
+      cur.sh0 = sh;
     }
     ++nstate;
     lastp = p;
@@ -3205,9 +3245,12 @@ __global__ __launch_bounds__(TB) void k_segments(DevGraph g, DevBatch b, DevWork
             float dd = 0.0f;
             for (int i = 0; i < r.plen; ++i) dd = dd + g.e_len[w.path_pool[r.poff + i]];
             const float x = start + dd;
-            S.o_t0[k] = time_at(ta, tb, x, Rd);
+            double t0;
+            int sh;
+            step_bound(b, w, a, r.lp, r.pl, Rd, ta, tb, x, t0, sh);
+            S.o_t0[k] = t0;
             S.o_off0[k] = 0.0f;
-            S.o_sh0[k] = (int16_t)(x >= Rd ? r.pl : r.lp);
+            S.o_sh0[k] = (int16_t)sh;
           }
         }
         // the close of the open traversal (none from a node candidate), the
@@ -3257,8 +3300,11 @@ __global__ __launch_bounds__(TB) void k_segments(DevGraph g, DevBatch b, DevWork
           S.t_t0[slot] = S.o_t0[jo];
           S.t_sh0[slot] = S.o_sh0[jo];
           S.t_off1[slot] = elen;
-          S.t_t1[slot] = time_at(ta, tb, start, Rd);
-          S.t_sh1[slot] = (int16_t)(start >= Rd ? r.pl : r.lp);
+          double t1;
+          int sh;
+          step_bound(b, w, a, r.lp, r.pl, Rd, ta, tb, start, t1, sh);
+          S.t_t1[slot] = t1;
+          S.t_sh1[slot] = (int16_t)sh;
           S.t_chain[slot] = chk;
           ++slot;
         }
@@ -3272,10 +3318,14 @@ __global__ __launch_bounds__(TB) void k_segments(DevGraph g, DevBatch b, DevWork
           S.t_edge[slot] = pe;
           S.t_off0[slot] = 0.0f;
           S.t_off1[slot] = len;
-          S.t_t0[slot] = time_at(ta, tb, xb, Rd);
-          S.t_t1[slot] = time_at(ta, tb, xe, Rd);
-          S.t_sh0[slot] = (int16_t)(xb >= Rd ? r.pl : r.lp);
-          S.t_sh1[slot] = (int16_t)(xe >= Rd ? r.pl : r.lp);
+          double tt;
+          int sh;
+          step_bound(b, w, a, r.lp, r.pl, Rd, ta, tb, xb, tt, sh);
+          S.t_t0[slot] = tt;
+          S.t_sh0[slot] = (int16_t)sh;
+          step_bound(b, w, a, r.lp, r.pl, Rd, ta, tb, xe, tt, sh);
+          S.t_t1[slot] = tt;
+          S.t_sh1[slot] = (int16_t)sh;
           S.t_chain[slot] = chk;
           ++slot;
         }
@@ -3613,9 +3663,95 @@ __global__ __launch_bounds__(TB) void k_report_wave(DevBatch b, DevReportCfg rc,
 }
 
 // ============================================================== segment bound / compaction
+// K7a, interpolated points (DESIGN.md §3 rule 7, oracle interp_step): the
+// points between the two states of a step that leaves its edge are placed on
+// the step's route -- on each route piece (the rest of q's edge, the path's
+// edges, p's edge up to p) the point's best projection onto the piece's edge,
+// admissible inside the piece, costed sqdist / (2 sigma_z^2) + |pos - gc(q, k)|
+// / beta; the cheapest wins, and a point behind the step's running maximum
+// stays unplaced (-1).  One thread per step, serial over its points: steps
+// with interpolated points are rare at the benchmark configs (5 s and 30 s
+// sampling) and short at any.
+struct RoutePiece {
+  int32_t edge;
+  float o0, o1, xs;
+};
+__device__ __forceinline__ RoutePiece route_piece(const DevGraph& g, const DevWork& w, int m, bool has0, int32_t ei,
+                                                  float oi, int32_t ej, float oj, int32_t poff, int32_t plen,
+                                                  float start, float& dd) {
+  RoutePiece r;
+  if (has0 && m == 0) {
+    r.edge = ei;
+    r.o0 = oi;
+    r.o1 = g.e_len[ei];
+    r.xs = 0.0f;
+    return r;
+  }
+  const int k = m - (has0 ? 1 : 0);
+  if (k < plen) {
+    r.edge = w.path_pool[poff + k];
+    r.o0 = 0.0f;
+    r.o1 = g.e_len[r.edge];
+    r.xs = start + dd;
+    dd = dd + r.o1;
+    return r;
+  }
+  r.edge = ej;
+  r.o0 = 0.0f;
+  r.o1 = oj;
+  r.xs = start + dd;
+  return r;
+}
+__device__ void interp_step(const DevGraph& g, const DevBatch& b, const DevParams& P, DevWork& w, int64_t q,
+                            int64_t p) {
+  const int2 ci = w.chosen[q], cj = w.chosen[p];
+  const int32_t ei = ci.x, ej = cj.x;
+  const float oi = __int_as_float(ci.y), oj = __int_as_float(cj.y);
+  const int32_t poff = w.path_off[p], plen = w.path_len[p];
+  const bool has0 = !cand_node(oi);
+  const int npc = (has0 ? 1 : 0) + plen + (cand_node(oj) ? 0 : 1);
+  const float start = src_start(g, ei, oi);
+  const float ds = (2.0f * P.sigma_z) * P.sigma_z;
+  const float qlat = b.lat[q], qlon = b.lon[q];
+  float run = 0.0f;
+  for (int64_t k = q + 1; k < p; ++k) {
+    const float lat = b.lat[k], lon = b.lon[k];
+    const float ls = MPD_F * cos_deg(lat);
+    const float gcd = gc_dist(qlat, qlon, lat, lon);
+    float best = INFINITY, bpos = -1.0f, dd = 0.0f;
+    for (int m = 0; m < npc; ++m) {
+      const RoutePiece pc = route_piece(g, w, m, has0, ei, oi, ej, oj, poff, plen, start, dd);
+      const int nsh = g.e_shape_off[pc.edge + 1] - g.e_shape_off[pc.edge] - 1;
+      float bsq = INFINITY, boff = 0.0f;
+      for (int sg = 0; sg < nsh; ++sg) {
+        float sqd, off;
+        project(g, pc.edge, sg, lat, lon, ls, sqd, off);
+        if (sqd < bsq) {
+          bsq = sqd;
+          boff = off;
+        }
+      }
+      if (!(boff >= pc.o0 && boff <= pc.o1)) continue;
+      const float pos = pc.xs + (boff - pc.o0);
+      const float cost = bsq / ds + fabsf(pos - gcd) / P.beta;
+      if (cost < best) {
+        best = cost;
+        bpos = pos;
+      }
+    }
+    if (bpos >= 0.0f && bpos >= run) {
+      w.ipos[k] = bpos;
+      run = bpos;
+    } else {
+      w.ipos[k] = -1.0f;
+    }
+  }
+}
+
 // Traversals a matched point can add: the close of the open traversal, its
 // route's path edges, the re-open (+ the chain's final close): <= 2 + path.
-__global__ __launch_bounds__(256) void k_seg_bound(DevBatch b, DevWork w, int64_t* ub) {
+// The same thread places the interpolated points of its step (K7a).
+__global__ __launch_bounds__(256) void k_seg_bound(DevGraph g, DevBatch b, DevParams P, DevWork w, int64_t* ub) {
   const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   // spill snapshot C: steps per route tier (kept for the status read)
   if (OTM_FOLD_BOOKKEEPING && p == b.n_points) fold_snap(w, 2, false);
@@ -3625,6 +3761,12 @@ __global__ __launch_bounds__(256) void k_seg_bound(DevBatch b, DevWork w, int64_
   if (p < b.n_points && w.is_col[p] && w.state[p] >= 0) {
     const int32_t pl = w.path_len[p];
     v = 2 + (pl > 0 ? pl : 0);
+    const int32_t q = w.col_prev[p];
+    if (q >= 0 && p - q > 1 && !w.chain_start[p] && pl >= 0 && w.trace_err[w.pt_trace[p]] == 0) {
+      const int2 ci = w.chosen[q], cj = w.chosen[p];
+      // a step that stays on its edge has no boundary inside it
+      if (!(ci.x == cj.x && __int_as_float(cj.y) >= __int_as_float(ci.y))) interp_step(g, b, P, w, q, p);
+    }
   }
   ub[p] = v;
 }
@@ -3899,9 +4041,10 @@ void launch_segments(const DevGraph& g, const DevBatch& b, DevWork& w, DevOut& o
                      o, (const int32_t*)lst, (const int32_t*)cnt, (int32_t*)nullptr, (int32_t*)nullptr);
   mk.end(KN_SEG_WRITE, s);
 }
-void launch_seg_bound(const DevBatch& b, DevWork& w, int64_t* ub, hipStream_t s, const Marks& mk) {
+void launch_seg_bound(const DevGraph& g, const DevBatch& b, const DevParams& p, DevWork& w, int64_t* ub, hipStream_t s,
+                      const Marks& mk) {
   TIMED(KN_SEG_BOUND, hipLaunchKernelGGL(k_seg_bound, dim3(grid_for(b.n_points + 1, 256, 1 << 30)), dim3(256), 0, s,
-                                         b, w, ub));
+                                         g, b, p, w, ub));
 }
 void launch_compact(int32_t n_traces, const DevOut& o, const int32_t* seg_off, const int32_t* way_off,
                     const int32_t* rep_off, void* segs_out, int64_t* ways_out, void* reps_out, void* traces_out,

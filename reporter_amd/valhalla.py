@@ -22,10 +22,11 @@ _engine = None
 
 
 def Configure(path):  # noqa: N802 -- the binding's name (py/reporter_service.py:279)
+    # A second Configure does not close the engine earlier SegmentMatchers
+    # hold (a Match may be running on it): each matcher keeps its engine
+    # alive, and the old engine is freed when the last of them goes away.
     global _engine
     with _lock:
-        if _engine is not None:
-            _engine.close()
         _engine = Engine(config_path=path)
 
 

@@ -56,6 +56,8 @@ def _stage_compare(eng, orc, batch):
     npt.assert_array_equal(tg[:len(sel)][sel], orc["trans"][sel], err_msg="trans")
     npt.assert_array_equal(eng.debug("state")[:P], orc["state"], err_msg="state")
     npt.assert_array_equal(eng.debug("route_dist")[:P], orc["route_dist"], err_msg="route_dist")
+    # interpolated points' positions on their step's route (K7a)
+    npt.assert_array_equal(eng.debug("ipos")[:P][ok_pts], orc["ipos"][ok_pts], err_msg="ipos")
 
 
 def _run_both(graph, batch, oracle, results_equal, meili=None, stages=True, counters=True, index_radius_m=None,
@@ -259,6 +261,90 @@ def test_edge_cases(small_graph, oracle, results_equal, batch_path):
     b = dict(trace_off=np.array(off, np.int64), lat=np.array(lat, np.float32), lon=np.array(lon, np.float32),
              time=np.array(tm, np.float64), accuracy=np.array(acc, np.float32))
     _run_both(small_graph, b, oracle, results_equal)
+
+
+MPD = 20037581.187 / 180.0
+
+
+def stop_and_go(b, seed, stops_per_trace=3, max_stop=20, jitter_m=2.0):
+    """Stops inserted into a batch: at a few points of each trace the vehicle
+    stands for 2..max_stop one-second samples jittered by jitter_m (every
+    later time shifted), so most of them fall within interpolation_distance
+    of the stop's column."""
+    rng = np.random.default_rng(seed)
+    lat, lon, tm, acc, off = [], [], [], [], [0]
+    for t in range(len(b["trace_off"]) - 1):
+        a, e = int(b["trace_off"][t]), int(b["trace_off"][t + 1])
+        stops = set(rng.choice(e - a, size=min(stops_per_trace, e - a), replace=False).tolist())
+        shift = 0.0
+        for i in range(a, e):
+            lat.append(b["lat"][i])
+            lon.append(b["lon"][i])
+            tm.append(b["time"][i] + shift)
+            acc.append(b["accuracy"][i])
+            if i - a in stops:
+                for _ in range(int(rng.integers(2, max_stop))):
+                    shift += 1.0
+                    dy, dx = rng.normal(0.0, jitter_m, 2)
+                    la = float(b["lat"][i])
+                    lat.append(la + dy / MPD)
+                    lon.append(float(b["lon"][i]) + dx / (MPD * np.cos(np.radians(la))))
+                    tm.append(b["time"][i] + shift)
+                    acc.append(b["accuracy"][i])
+        off.append(len(lat))
+    return dict(trace_off=np.array(off, np.int64), lat=np.array(lat, np.float32), lon=np.array(lon, np.float32),
+                time=np.array(tm, np.float64), accuracy=np.array(acc, np.float32))
+
+
+@pytest.mark.parametrize("kind", ["dense", "stop_and_go", "long_stop_and_go"])
+def test_interpolated_points(small_graph, oracle, results_equal, batch_path, kind):
+    # SURVEY Appendix B / README.md:162-163: interpolated points are placed on
+    # the matched route and the segment shape indices are the last point
+    # before/at each boundary (DESIGN.md §3 rule 7) -- bit-identical to the
+    # oracle, with the indices landing on interpolated points
+    if kind == "dense":
+        # one-second sampling: a local street's 8-11 m per step with 5 m noise
+        b = synth.make_traces(small_graph, 150, 100, interval_s=1.0, noise_sigma_m=5.0, accuracy=10.0, seed=41)
+    elif kind == "stop_and_go":
+        b = stop_and_go(synth.make_traces(small_graph, 150, 60, interval_s=5.0, noise_sigma_m=15.0, accuracy=15.0,
+                                          seed=43), seed=44)
+    else:
+        # traces beyond the segment kernel's LDS plans (the serial walk)
+        b = stop_and_go(synth.make_traces(small_graph, 12, 240, interval_s=2.0, noise_sigma_m=5.0, accuracy=10.0,
+                                          seed=45), seed=46, stops_per_trace=8)
+        assert np.diff(b["trace_off"]).max() > 256
+    res, orc = _run_both(small_graph, b, oracle, results_equal)
+    ip = orc["ipos"]
+    P = len(b["lat"])
+    assert (ip >= 0).sum() > P // 50
+    # shape indices are trace-relative: map them to batch points
+    tr, segs = orc["traces"], orc["segments"]
+    landed = 0
+    for t in range(len(tr)):
+        a, c = int(tr["seg_off"][t]), int(tr["seg_cnt"][t])
+        base = int(b["trace_off"][t])
+        for f in ("begin_shape_index", "end_shape_index"):
+            landed += int((ip[base + segs[f][a:a + c]] >= 0).sum())
+    assert landed > 20
+
+
+def test_interpolated_points_hand_road(tmp_path, oracle, results_equal):
+    # the hand-built road of tests/test_interp.py, on the GPU
+    import handgraph
+    path, _ = handgraph.straight_road(str(tmp_path / "road.otmg"), lat=40.0, n_nodes=5)
+    traces = [[(0.0002, 0.0), (0.00025, 1.0), (0.00022, 2.0), (0.0003, 3.0), (0.0011, 10.0), (0.0021, 20.0)],
+              [(0.0005, 0.0), (0.0005, 5.0), (0.0005, 10.0), (0.0005, 15.0), (0.0015, 25.0)],
+              [(0.0002, 0.0), (0.00028, 1.0), (0.0012, 30.0), (0.0022, 40.0), (0.0032, 50.0)]]
+    lon = np.concatenate([np.array([p[0] for p in t], np.float32) for t in traces])
+    tm = np.concatenate([np.array([p[1] for p in t], np.float64) for t in traces])
+    off = np.concatenate([[0], np.cumsum([len(t) for t in traces])]).astype(np.int64)
+    b = dict(trace_off=off, lat=np.full(len(lon), 40.0, np.float32), lon=lon, time=tm,
+             accuracy=np.full(len(lon), 5.0, np.float32))
+    res, orc = _run_both(path, b, oracle, results_equal)
+    s = res.segments
+    assert list(s["begin_shape_index"][:3]) == [0, 3, 4]
+    assert list(s["end_shape_index"][:3]) == [3, 4, 5]
+    assert res.traces["shape_used"][2] == 1
 
 
 def test_empty_batch(small_graph):

@@ -189,3 +189,51 @@ def test_engine_create_device_arguments():
     # a group whose members cannot be created fails as the member does
     assert L.otm_engine_create(b"/nonexistent.json", devs, 2, C.byref(h)) == -1  # OTM_EINVAL
     assert "cannot read config" in _lib.last_error()
+
+
+def test_meili_config_mode_section_over_default(tmp_path):
+    """meili's config layering: "default" with the mode's section on top.  A
+    stock valhalla_build_config meili block has
+    default.turn_penalty_factor 0 and auto.turn_penalty_factor 200: an auto
+    match runs with 200 (no device needed: otm_config_meili)."""
+    import json
+    L = _lib.lib()
+    cfg = tmp_path / "valhalla.json"
+
+    def read(meili):
+        cfg.write_text(json.dumps({"otm": {"graph": "g.otmg"}, "meili": meili}))
+        p = _lib.MeiliParams()
+        assert L.otm_config_meili(str(cfg).encode(), C.byref(p)) == 0, _lib.last_error()
+        return p
+
+    stock = {"mode": "auto", "customizable": ["mode", "search_radius"],
+             "default": {"sigma_z": 4.07, "gps_accuracy": 5.0, "beta": 3, "max_route_distance_factor": 5,
+                         "breakage_distance": 2000, "interpolation_distance": 10, "search_radius": 50,
+                         "max_search_radius": 100, "turn_penalty_factor": 0},
+             "auto": {"turn_penalty_factor": 200, "search_radius": 50},
+             "pedestrian": {"turn_penalty_factor": 100, "search_radius": 25}}
+    p = read(stock)
+    assert p.turn_penalty_factor == 200.0 and p.search_radius == 50.0 and p.sigma_z == pytest.approx(4.07)
+    # another mode's section applies instead
+    p = read(dict(stock, mode="pedestrian"))
+    assert p.turn_penalty_factor == 100.0 and p.search_radius == 25.0
+    # no mode section: the default section alone
+    p = read({"default": {"turn_penalty_factor": 0, "beta": 4}})
+    assert p.turn_penalty_factor == 0.0 and p.beta == 4.0
+    # no meili block at all: the built-in defaults (the auto costing's 200)
+    p = read({})
+    assert p.turn_penalty_factor == 200.0 and p.max_candidates == 32
+    cfg.write_text(json.dumps({"meili": {"default": {"max_candidates": 99}}}))
+    assert L.otm_config_meili(str(cfg).encode(), C.byref(p)) == -1
+    assert "max_candidates" in _lib.last_error()
+
+
+def test_null_engine_request_calls_fail_cleanly():
+    """A NULL engine is a bad-arguments error on every request entry point,
+    not a crash."""
+    L = _lib.lib()
+    out = C.c_void_p()
+    n = C.c_size_t()
+    body = b'{"uuid":"a","trace":[]}'
+    assert L.otm_report(None, body, len(body), C.byref(out), C.byref(n)) < 0
+    assert L.otm_match_json(None, body, len(body), C.byref(out), C.byref(n)) < 0

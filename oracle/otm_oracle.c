@@ -251,9 +251,30 @@ static float probe_radius(const orc_params* P, float acc) {
   return r < P->max_search_radius ? r : P->max_search_radius;
 }
 
+/* distinct edges one probe's scan projects (the §8(d) unique-edge term) */
+#define SEEN_CAP 1024
+typedef struct {
+  int32_t key[SEEN_CAP];
+  uint32_t stamp[SEEN_CAP];
+  uint32_t gen;
+} seen_set;
+static void seen_add(const orc_graph* g, seen_set* S, int32_t e, orc_counters* C) {
+  uint32_t h = ((uint32_t)e * 2654435761u) >> 22;
+  for (int k = 0; k < SEEN_CAP; ++k, h = (h + 1) & (SEEN_CAP - 1)) {
+    if (S->stamp[h] != S->gen) {
+      S->stamp[h] = S->gen;
+      S->key[h] = e;
+      C->edges_projected++;
+      C->edge_shape_points += g->eshape[e + 1] - g->eshape[e];
+      return;
+    }
+    if (S->key[h] == e) return;
+  }
+}
+
 /* returns number of candidates, or -1 on overflow */
 static int candidates(const orc_graph* g, const orc_params* P, float lat, float lon, float acc, int32_t* c_edge,
-                      float* c_off, float* c_emis, hit* hits, orc_counters* C) {
+                      float* c_off, float* c_emis, hit* hits, seen_set* seen, orc_counters* C) {
   const float r = probe_radius(P, acc);
   const float r2 = r * r;
   const float ls = MPD_F * orc_cos_deg(lat);
@@ -266,6 +287,10 @@ static int candidates(const orc_graph* g, const orc_params* P, float lat, float 
   const double lo_hi = ((double)lon + (double)dlon - g->h.grid_lon0) / cell;
   const double R = g->h.grid_rows, Cn = g->h.grid_cols;
   int nh = 0;
+  if (seen && ++seen->gen == 0) {
+    memset(seen->stamp, 0, sizeof seen->stamp);
+    seen->gen = 1;
+  }
   if (!(la_hi < 0.0 || lo_hi < 0.0 || la_lo >= R || lo_lo >= Cn)) {
     const int r0 = la_lo < 0.0 ? 0 : (int)floor(la_lo);
     const int r1 = la_hi >= R ? (int)R - 1 : (int)floor(la_hi);
@@ -282,6 +307,7 @@ static int candidates(const orc_graph* g, const orc_params* P, float lat, float 
           int at_end;
           project(g, e, k, lat, lon, ls, &sqd, &off, &at_end);
           C->cell_entries_scanned++;
+          if (seen) seen_add(g, seen, e, C);
           if (!(sqd <= r2)) continue;
           int f = -1;
           for (int h = 0; h < nh; ++h)
@@ -363,6 +389,7 @@ typedef struct ws {
   size_t hn, hcap;
   int32_t nlab;
   hit hits[ORC_MAX_HITS + 1];
+  seen_set seen;
 } ws;
 
 static void hpush(ws* w, float d, int32_t n) {
@@ -483,6 +510,7 @@ typedef struct batch {
   atomic_int next;
   int phase;
   orc_counters* ctr; /* per thread */
+  int count_unique;  /* count §8(d)'s unique projected edges (keep_stages) */
   uint32_t turn_units[181]; /* orc_turn_units per deviation 0..180 */
 } batch;
 
@@ -515,7 +543,8 @@ static void phase_a(batch* B, ws* w, int32_t t, orc_counters* C) {
     C->columns++;
     B->gc[p] = gcv;
     int K = candidates(g, P, B->lat[p], B->lon[p], B->acc[p], B->cand_edge + p * ORC_KMAX,
-                       B->cand_off + p * ORC_KMAX, B->cand_emis + p * ORC_KMAX, w->hits, C);
+                       B->cand_off + p * ORC_KMAX, B->cand_emis + p * ORC_KMAX, w->hits,
+                       B->count_unique ? &w->seen : NULL, C);
     if (K < 0) {
       if (!B->terr[t]) B->terr[t] = TERR_CAND_OVERFLOW;
       K = 0;
@@ -1181,6 +1210,7 @@ int orc_match_batch(const orc_graph* g, const orc_params* p, const orc_report_cf
   B.lon = lon;
   B.time = time;
   B.acc = accuracy;
+  B.count_unique = keep_stages;
   for (int d = 0; d <= 180; ++d) B.turn_units[d] = orc_turn_units(p->turn_penalty_factor, d);
   const size_t PP = (size_t)P + 1;
   B.is_col = (uint8_t*)calloc(PP, 1);

@@ -70,6 +70,10 @@ typedef struct orc_counters {
   int64_t searches, nodes_settled, edges_relaxed, transitions;
   int64_t route_searches, route_nodes_settled, route_edges_relaxed, route_edges;
   int64_t segments_out, reports_out;
+  /* SURVEY §8(d)'s unique-edge term, per probe the distinct edges whose shape
+     segments its scan projects and their shape points (counted only when the
+     batch keeps its stages: the timed CPU baseline does not pay for it) */
+  int64_t edges_projected, edge_shape_points;
 } orc_counters;
 
 typedef struct orc_results {

@@ -24,7 +24,7 @@ TRACE_DTYPE = np.dtype([(n, "<i4") for n in (
     "unreported_length")])
 COUNTER_NAMES = ("points", "columns", "cells_visited", "cell_entries_scanned", "candidates", "searches", "nodes_settled",
                  "edges_relaxed", "transitions", "route_searches", "route_nodes_settled", "route_edges_relaxed",
-                 "route_edges", "segments_out", "reports_out")
+                 "route_edges", "segments_out", "reports_out", "edges_projected", "edge_shape_points")
 
 
 class Params(C.Structure):
@@ -53,7 +53,30 @@ class Results(C.Structure):
                 ("gc", C.c_void_p), ("counters", Counters), ("ipos", C.c_void_p)]
 
 
+# The CPU baseline's build of the same sources (oracle/Makefile `native`:
+# -O3 -march=x86-64-v4, AVX-512, for the GPU box's EPYC host); bench.py times it
+# and checks its output against the portable build's, byte for byte.
+NATIVE_LIB_PATH = os.path.join(_HERE, "build", "native", "libotm_oracle.so")
+
 _lib = None
+_native = None
+
+
+def host_has_avx512():
+    try:
+        with open("/proc/cpuinfo") as f:
+            flags = f.read()
+        return all(x in flags for x in ("avx512f", "avx512bw", "avx512cd", "avx512dq", "avx512vl"))
+    except OSError:
+        return False
+
+
+def native_lib():
+    """The baseline build when it exists and this host can run it, else None."""
+    global _native
+    if _native is None and os.path.exists(NATIVE_LIB_PATH) and host_has_avx512():
+        _native = _declare(C.CDLL(NATIVE_LIB_PATH))
+    return _native
 
 
 def lib():
@@ -61,36 +84,39 @@ def lib():
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise RuntimeError("oracle not built: run `make -C oracle` (%s missing)" % LIB_PATH)
-        L = C.CDLL(LIB_PATH)
-        L.orc_graph_load.restype = C.c_void_p
-        L.orc_graph_load.argtypes = [C.c_char_p]
-        L.orc_graph_free.argtypes = [C.c_void_p]
-        L.orc_graph_count.restype = C.c_int64
-        L.orc_graph_count.argtypes = [C.c_void_p, C.c_int]
-        L.orc_params_default.argtypes = [C.POINTER(Params)]
-        L.orc_report_cfg_default.argtypes = [C.POINTER(ReportCfg)]
-        L.orc_cos_deg.restype = C.c_float
-        L.orc_cos_deg.argtypes = [C.c_float]
-        L.orc_match_batch.argtypes = [C.c_void_p, C.POINTER(Params), C.POINTER(ReportCfg), C.c_int32,
-                                      C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,
-                                      C.c_int, C.POINTER(Results)]
-        L.orc_results_free.argtypes = [C.POINTER(Results)]
-        for fn in ("orc_handle_request",):
-            getattr(L, fn).argtypes = [C.c_void_p, C.POINTER(Params), C.POINTER(ReportCfg), C.c_char_p,
-                                       C.c_char_p, C.c_size_t, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]
-        L.orc_match_json.argtypes = [C.c_void_p, C.POINTER(Params), C.c_char_p, C.c_size_t,
-                                     C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]
-        L.orc_report_segments.argtypes = [C.POINTER(ReportCfg), C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t,
-                                          C.POINTER(C.c_void_p), C.POINTER(C.c_size_t), C.POINTER(C.c_void_p)]
-        L.orc_handle_batch.argtypes = [C.c_void_p, C.POINTER(Params), C.POINTER(ReportCfg), C.c_int,
-                                       C.POINTER(C.c_char_p), C.POINTER(C.c_size_t), C.c_int,
-                                       C.POINTER(C.c_int), C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]
-        L.orc_json_redump.argtypes = [C.c_char_p, C.c_size_t, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]
-        L.orc_decode_polyline6.restype = C.c_int64
-        L.orc_decode_polyline6.argtypes = [C.c_char_p, C.c_size_t, C.c_void_p, C.c_int64]
-        L.orc_free.argtypes = [C.c_void_p]
-        _lib = L
+        _lib = _declare(C.CDLL(LIB_PATH))
     return _lib
+
+
+def _declare(L):
+    L.orc_graph_load.restype = C.c_void_p
+    L.orc_graph_load.argtypes = [C.c_char_p]
+    L.orc_graph_free.argtypes = [C.c_void_p]
+    L.orc_graph_count.restype = C.c_int64
+    L.orc_graph_count.argtypes = [C.c_void_p, C.c_int]
+    L.orc_params_default.argtypes = [C.POINTER(Params)]
+    L.orc_report_cfg_default.argtypes = [C.POINTER(ReportCfg)]
+    L.orc_cos_deg.restype = C.c_float
+    L.orc_cos_deg.argtypes = [C.c_float]
+    L.orc_match_batch.argtypes = [C.c_void_p, C.POINTER(Params), C.POINTER(ReportCfg), C.c_int32,
+                                  C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,
+                                  C.c_int, C.POINTER(Results)]
+    L.orc_results_free.argtypes = [C.POINTER(Results)]
+    for fn in ("orc_handle_request",):
+        getattr(L, fn).argtypes = [C.c_void_p, C.POINTER(Params), C.POINTER(ReportCfg), C.c_char_p,
+                                   C.c_char_p, C.c_size_t, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]
+    L.orc_match_json.argtypes = [C.c_void_p, C.POINTER(Params), C.c_char_p, C.c_size_t,
+                                 C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]
+    L.orc_report_segments.argtypes = [C.POINTER(ReportCfg), C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t,
+                                      C.POINTER(C.c_void_p), C.POINTER(C.c_size_t), C.POINTER(C.c_void_p)]
+    L.orc_handle_batch.argtypes = [C.c_void_p, C.POINTER(Params), C.POINTER(ReportCfg), C.c_int,
+                                   C.POINTER(C.c_char_p), C.POINTER(C.c_size_t), C.c_int,
+                                   C.POINTER(C.c_int), C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]
+    L.orc_json_redump.argtypes = [C.c_char_p, C.c_size_t, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]
+    L.orc_decode_polyline6.restype = C.c_int64
+    L.orc_decode_polyline6.argtypes = [C.c_char_p, C.c_size_t, C.c_void_p, C.c_int64]
+    L.orc_free.argtypes = [C.c_void_p]
+    return L
 
 
 def _take(ptr, n):
@@ -137,15 +163,16 @@ def report_cfg_from_env(env):
 
 
 class Graph(object):
-    def __init__(self, path):
+    def __init__(self, path, L=None):
         self.path = path
-        self.h = lib().orc_graph_load(path.encode())
+        self.L = L or lib()
+        self.h = self.L.orc_graph_load(path.encode())
         if not self.h:
             raise RuntimeError("oracle cannot load graph %s" % path)
 
     def close(self):
         if self.h:
-            lib().orc_graph_free(self.h)
+            self.L.orc_graph_free(self.h)
             self.h = None
 
     def __del__(self):
@@ -159,8 +186,10 @@ def _arr(ptr, dtype, n):
     return np.frombuffer(buf, dtype=dtype, count=n).copy()
 
 
-def match_batch(graph, batch, p=None, rc=None, nthreads=1, keep_stages=False):
-    """batch: dict of numpy arrays trace_off(i64), lat(f32), lon(f32), time(f64), accuracy(f32)."""
+def match_batch(graph, batch, p=None, rc=None, nthreads=1, keep_stages=False, L=None):
+    """batch: dict of numpy arrays trace_off(i64), lat(f32), lon(f32), time(f64), accuracy(f32).
+    L: another build of the oracle (native_lib()) for the graph's handle."""
+    L = L or graph.L
     p = p or params()
     rc = rc or report_cfg()
     off = np.ascontiguousarray(batch["trace_off"], dtype=np.int64)
@@ -169,7 +198,7 @@ def match_batch(graph, batch, p=None, rc=None, nthreads=1, keep_stages=False):
     tm = np.ascontiguousarray(batch["time"], dtype=np.float64)
     acc = np.ascontiguousarray(batch["accuracy"], dtype=np.float32)
     r = Results()
-    rcode = lib().orc_match_batch(graph.h, C.byref(p), C.byref(rc), len(off) - 1, off.ctypes.data,
+    rcode = L.orc_match_batch(graph.h, C.byref(p), C.byref(rc), len(off) - 1, off.ctypes.data,
                                   lat.ctypes.data, lon.ctypes.data, tm.ctypes.data, acc.ctypes.data, nthreads,
                                   1 if keep_stages else 0, C.byref(r))
     if rcode != 0:
@@ -194,7 +223,7 @@ def match_batch(graph, batch, p=None, rc=None, nthreads=1, keep_stages=False):
         out["route_dist"] = _arr(r.route_dist, np.float32, P)
         out["gc"] = _arr(r.gc, np.float32, P)
         out["ipos"] = _arr(r.ipos, np.float32, P)
-    lib().orc_results_free(C.byref(r))
+    L.orc_results_free(C.byref(r))
     return out
 
 
@@ -237,7 +266,10 @@ def report_segments(req, match_output, rc=None):
     return code, body, e
 
 
-def handle_batch(graph, bodies, p=None, rc=None, nthreads=1):
+def handle_batch(graph, bodies, p=None, rc=None, nthreads=1, L=None):
+    """orc_handle_batch: JSON request bodies -> [(code, body bytes)] (request
+    parse, match, report(), response writing), nthreads host threads."""
+    L = L or graph.L
     p = p or params()
     rc = rc or report_cfg()
     n = len(bodies)
@@ -246,10 +278,12 @@ def handle_batch(graph, bodies, p=None, rc=None, nthreads=1):
     codes = (C.c_int * n)()
     outs = (C.c_void_p * n)()
     olens = (C.c_size_t * n)()
-    lib().orc_handle_batch(graph.h, C.byref(p), C.byref(rc), n, arr, lens, nthreads, codes, outs, olens)
+    L.orc_handle_batch(graph.h, C.byref(p), C.byref(rc), n, arr, lens, nthreads, codes, outs, olens)
     res = []
     for i in range(n):
-        res.append((codes[i], _take(outs[i], olens[i])))
+        s = C.string_at(outs[i], olens[i])
+        L.orc_free(outs[i])
+        res.append((codes[i], s))
     return res
 
 

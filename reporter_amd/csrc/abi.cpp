@@ -665,20 +665,12 @@ static int otm_engine_create_impl(const char* cfg_path, const int* devices, int 
     delete E;
     return fail(OTM_EINVAL, "grid_mult must be in [0 (auto), 64]");
   }
-  const Value* cl = o->get("cand_lanes");
-  if (cl && cl->kind == Kind::Int) E->cand_lanes = (int)cl->i;
-  if (const char* v = std::getenv("OTM_CAND_LANES")) E->cand_lanes = std::atoi(v);  // A/B override
-  if (E->cand_lanes != 1 && E->cand_lanes != 4 && E->cand_lanes != 8 && E->cand_lanes != 16) {
-    delete E;
-    return fail(OTM_EINVAL, "cand_lanes must be 1, 4, 8 or 16");
-  }
   const Value* tl = o->get("trans_lanes");
   if (tl && tl->kind == Kind::Int) E->trans_lanes = (int)tl->i;
   if (const char* v = std::getenv("OTM_TRANS_SUB")) E->trans_lanes = std::atoi(v);  // A/B override
-  if (E->trans_lanes != 4 && E->trans_lanes != 8 && E->trans_lanes != 16 && E->trans_lanes != 32 &&
-      E->trans_lanes != 64) {
+  if (E->trans_lanes != 8 && E->trans_lanes != 16) {
     delete E;
-    return fail(OTM_EINVAL, "trans_lanes must be 4, 8, 16, 32 or 64");
+    return fail(OTM_EINVAL, "trans_lanes must be 8 or 16");
   }
   std::string err;
   if (!read_meili(cfg, &E->mc, &err)) {

@@ -313,7 +313,6 @@ int engine_clone(const otm_engine* P, otm_engine* C, std::string* err) {
   C->index_build_ms = P->index_build_ms;
   C->small_points = P->small_points;
   C->trans_lanes = P->trans_lanes;
-  C->cand_lanes = P->cand_lanes;
   C->mc = P->mc;
   C->rc = P->rc;
   C->dp = P->dp;
@@ -614,7 +613,7 @@ static int engine_match_once(otm_engine* E, const DevBatch& b, hipStream_t s, st
     mk.begin(KN_ORDER, s);
     mk.end(KN_ORDER, s);
   }
-  launch_candidates(E->g, b, dp, w, s, mk, E->cand_lanes);
+  launch_candidates(E->g, b, dp, w, s, mk);
   // spill snapshot A: candidate probes the lane tier handed to the wave tier;
   // the counters start over for the transition tiers (links, scan and the
   // capacity check do not touch them)
@@ -736,72 +735,13 @@ int engine_match(otm_engine* E, const DevBatch& b, hipStream_t s, std::string* e
   return OTM_OK;
 }
 
-// The kind of the large host<->device copies.  OTM_COPY_NOCU=1 asks for
-// hipMemcpyDeviceToDeviceNoCU on the (pinned, device-mapped) host buffers: a
-// copy engine instead of the runtime's blit kernels, which otherwise occupy
-// every CU while they wait on PCIe (an A/B knob).
-hipMemcpyKind big_copy_kind(hipMemcpyKind k) {
-  static const int nocu = [] {
-    const char* v = std::getenv("OTM_COPY_NOCU");
-    return v && *v == '1' ? 1 : 0;
-  }();
-  return nocu ? hipMemcpyDeviceToDeviceNoCU : k;
-}
-
-// OTM_COPY_SERIAL=1: the large host<->device copies of all batch contexts in
-// the process take turns (issued and completed under one lock), so that each
-// runs alone on a copy engine instead of as blit kernels beside the others'
-// (an A/B knob for the host-inclusive leg).
-static std::mutex g_copy_mu;
-static bool copy_serial() {
-  static const bool on = [] {
-    const char* v = std::getenv("OTM_COPY_SERIAL");
-    return v && *v == '1';
-  }();
-  return on;
-}
-
-// OTM_COPY_SYNC=1: the large host<->device copies as hipMemcpyWithStream (the
-// call torch makes for pinned copies; it returns when the copy is done) --
-// an A/B of the runtime's engine choice for the host-inclusive leg
-static bool copy_sync() {
-  static const bool on = [] {
-    const char* v = std::getenv("OTM_COPY_SYNC");
-    return v && *v == '1';
-  }();
-  return on;
-}
-// OTM_COPY_KERNEL=<blocks>: the large copies by the library's own k_copy with
-// that many workgroups when the host side is pinned (device-mapped), instead of
-// the runtime's copy -- an A/B knob for the host-inclusive leg
-static int copy_kernel_blocks() {
-  const char* v = std::getenv("OTM_COPY_KERNEL");  // (read per copy: tests switch it)
-  return v ? std::max(0, std::min(1024, std::atoi(v))) : 0;
-}
-// p .. p + n lies in one pinned, device-mapped host allocation
-static bool host_mapped(const void* p, size_t n) {
-  hipPointerAttribute_t a;
-  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
-    (void)hipGetLastError();
-    return false;
-  }
-  if (a.type != hipMemoryTypeHost || a.devicePointer != p) return false;
-  hipDeviceptr_t base = nullptr;
-  size_t size = 0;
-  if (hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)p) != hipSuccess) {
-    (void)hipGetLastError();
-    return false;
-  }
-  return (const char*)p + n <= (const char*)base + size;
-}
+// The large host<->device copies: hipMemcpyAsync on the batch's stream.
+// Measured and not kept (profiles/r02_hostleg_ab/): a copy
+// engine through hipMemcpyDeviceToDeviceNoCU, copies taking turns across the
+// batch contexts, hipMemcpyWithStream, and the library's own copy kernel with
+// 16-128 workgroups -- the leg runs at the sum of its PCIe bytes and kernels.
 static hipError_t big_copy(void* dst, const void* src, size_t n, hipMemcpyKind k, hipStream_t s) {
-  const int blocks = copy_kernel_blocks();
-  if (blocks > 0 && n >= (1u << 16) && ((uintptr_t)dst % 16) == 0 && ((uintptr_t)src % 16) == 0 &&
-      host_mapped(k == hipMemcpyHostToDevice ? src : dst, n)) {
-    launch_copy(dst, src, n, blocks, s);
-    return hipGetLastError();
-  }
-  return copy_sync() ? hipMemcpyWithStream(dst, src, n, k, s) : hipMemcpyAsync(dst, src, n, k, s);
+  return hipMemcpyAsync(dst, src, n, k, s);
 }
 
 int engine_match_host(otm_engine* E, const otm_batch* in, std::string* err) {
@@ -855,17 +795,12 @@ int engine_match_host(otm_engine* E, const otm_batch* in, std::string* err) {
     b.acc = (const float*)(d + b_off + b_tm + 2 * b_pt);
     return engine_match(E, b, s, err);
   }
-  const hipMemcpyKind h2d = big_copy_kind(hipMemcpyHostToDevice);
-  {
-    std::unique_lock<std::mutex> lk(g_copy_mu, std::defer_lock);
-    if (copy_serial()) lk.lock();
-    HIPCHK(hipMemcpyAsync(E->in_off.p, in->trace_off, b_off, hipMemcpyHostToDevice, s));
-    HIPCHK(big_copy(E->in_lat.p, in->lat, b_pt, h2d, s));
-    HIPCHK(big_copy(E->in_lon.p, in->lon, b_pt, h2d, s));
-    HIPCHK(big_copy(E->in_time.p, in->time, b_tm, h2d, s));
-    HIPCHK(big_copy(E->in_acc.p, in->accuracy, b_pt, h2d, s));
-    if (copy_serial()) HIPCHK(hipStreamSynchronize(s));
-  }
+  const hipMemcpyKind h2d = hipMemcpyHostToDevice;
+  HIPCHK(hipMemcpyAsync(E->in_off.p, in->trace_off, b_off, hipMemcpyHostToDevice, s));
+  HIPCHK(big_copy(E->in_lat.p, in->lat, b_pt, h2d, s));
+  HIPCHK(big_copy(E->in_lon.p, in->lon, b_pt, h2d, s));
+  HIPCHK(big_copy(E->in_time.p, in->time, b_tm, h2d, s));
+  HIPCHK(big_copy(E->in_acc.p, in->accuracy, b_pt, h2d, s));
   b.trace_off = (const int64_t*)E->in_off.p;
   b.lat = (const float*)E->in_lat.p;
   b.lon = (const float*)E->in_lon.p;
@@ -934,12 +869,7 @@ int engine_fetch(otm_engine* E, otm_results* out, std::string* err) {
   if ((rc = ensure_pinned(E->h_segs, ((size_t)NS + 1) * sizeof(otm_segment), err))) return rc;
   if ((rc = ensure_pinned(E->h_reps_dense, ((size_t)NR + 1) * sizeof(otm_report_rec), err))) return rc;
   if ((rc = ensure_pinned(E->h_ways, ((size_t)NW + 1) * 8, err))) return rc;
-  const hipMemcpyKind d2h = NT > FETCH_SCAN_MAX ? big_copy_kind(hipMemcpyDeviceToHost) : hipMemcpyDeviceToHost;
-  std::unique_lock<std::mutex> lk(g_copy_mu, std::defer_lock);
-  if (copy_serial() && NT > FETCH_SCAN_MAX) {
-    HIPCHK(hipStreamSynchronize(s));  // the compaction first: the lock covers only the copies
-    lk.lock();
-  }
+  const hipMemcpyKind d2h = hipMemcpyDeviceToHost;
   if (NT) HIPCHK(big_copy(E->h_traces.p, E->f_traces.p, (size_t)NT * sizeof(otm_trace_result), d2h, s));
   if (NS) HIPCHK(big_copy(E->h_segs.p, E->f_segs.p, (size_t)NS * sizeof(otm_segment), d2h, s));
   if (NR) HIPCHK(big_copy(E->h_reps_dense.p, E->f_reps.p, (size_t)NR * sizeof(otm_report_rec), d2h, s));

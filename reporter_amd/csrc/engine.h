@@ -39,8 +39,7 @@ struct otm_engine {
   // the online tiers at a cost of 0.13 ms per batch
   float index_rmax = -1.0f;  // < 0: sized from the graph's node density (auto_index_radius)
   int64_t small_points = 0;  // batches below this many points: natural order, wave-tier candidates
-  int cand_lanes = 1;       // K2 lanes per probe: 1 (lane tier) or 4 / 8 / 16 (sub-group tier, measured slower)
-  int trans_lanes = 8;      // k_trans_sub lanes per column: 4 or 8 (two passes, wide columns at 16), 16, 32, 64
+  int trans_lanes = 8;      // k_trans_sub lanes per column: 8 (two passes, wide columns at 16) or 16 (one pass)
   int grid_mult = 0;         // candidate grid cells = grid_mult x grid_mult of the file's (0: auto_grid_mult)
   int32_t grid_rows = 0, grid_cols = 0;
   int64_t grid_entries = 0;

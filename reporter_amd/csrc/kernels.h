@@ -244,7 +244,7 @@ struct Marks {
 void launch_columns(const DevGraph& g, const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s,
                     const Marks& mk);
 void launch_candidates(const DevGraph& g, const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s,
-                       const Marks& mk, int lanes);
+                       const Marks& mk);
 void launch_links(const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s, const Marks& mk);
 // sets *w.abort when the scanned transition total exceeds w.trans_cap
 void launch_cap_check(const DevBatch& b, DevWork& w, hipStream_t s);
@@ -292,8 +292,6 @@ void scan_i64(int64_t* d, int64_t n, void* tmp, size_t tmp_bytes, hipStream_t s)
 // exclusive scans of three per-trace counts (n <= FETCH_SCAN_MAX) in one
 // single-block launch, totals at o*[n]
 constexpr int FETCH_SCAN_MAX = 1 << 16;
-// dst <- src (n bytes) by `blocks` workgroups of the library (16-byte aligned buffers; a host side must be pinned)
-void launch_copy(void* dst, const void* src, size_t n, int blocks, hipStream_t s);
 void launch_fetch_scan(int32_t n, const int32_t* c0, const int32_t* c1, const int32_t* c2, int32_t* o0, int32_t* o1,
                        int32_t* o2, hipStream_t s);
 void scan_i32(int32_t* d, int64_t n, void* tmp, size_t tmp_bytes, hipStream_t s);

@@ -75,37 +75,6 @@ __device__ __forceinline__ float seg_sqdist(float alat, float alon, float blat, 
   return px * px + py * py;
 }
 
-// seg_sqdist for the scan of K2's lane tier: INFINITY when the segment's
-// line is already farther than the radius (|cross| / |v| > r, with a 1 %
-// margin that rounding cannot cross), so most entries skip the division and
-// clamp; the rest get seg_sqdist's value, bit for bit.
-#ifndef OTM_CAND_PREFILTER
-#define OTM_CAND_PREFILTER 0
-#endif
-__device__ __forceinline__ float seg_sqdist_r2(float alat, float alon, float blat, float blon, float lat, float lon,
-                                               float ls, float r2) {
-  const float ax = (alon - lon) * ls;
-  const float ay = (alat - lat) * MPD_F;
-  const float bx = (blon - lon) * ls;
-  const float by = (blat - lat) * MPD_F;
-  const float vx = bx - ax;
-  const float vy = by - ay;
-  const float l2 = vx * vx + vy * vy;
-#if OTM_CAND_PREFILTER
-  const float cr = ax * vy - ay * vx;
-  if (cr * cr > 1.01f * r2 * l2) return INFINITY;
-#endif
-  float t = 0.0f;
-  if (l2 > 0.0f) {
-    const float dot = ax * vx + ay * vy;
-    t = -dot / l2;
-    t = t < 0.0f ? 0.0f : (t > 1.0f ? 1.0f : t);
-  }
-  const float px = ax + t * vx;
-  const float py = ay + t * vy;
-  return px * px + py * py;
-}
-
 __device__ __forceinline__ void project(const DevGraph& g, int32_t e, int32_t k, float lat, float lon, float ls,
                                         float& sqd, float& off_out, bool& at_end) {
   const int32_t a = g.e_shape_off[e] + k, b = a + 1;
@@ -524,9 +493,6 @@ constexpr int CAND_TB = OTM_CAND_TB;
 #define OTM_CAND_INFL 2
 #endif
 constexpr int CAND_INFL = OTM_CAND_INFL;
-#ifndef OTM_CAND_FIND
-#define OTM_CAND_FIND 1
-#endif
 // transition index tier: pairs per lane whose first slot loads are issued
 // together: 2 measured 0.337 -> 0.302 ms on config 2, 1.956 -> 1.888 ms on
 // config 4; 3 and 4 slower (0.365 / 0.436 ms: registers, 4 spills)
@@ -605,7 +571,7 @@ __global__ __launch_bounds__(CAND_TB, OTM_CAND_WAVES) void k_cand_lane(DevGraph 
             if (q + u < q1) {
               const float4 G = g.ent_geo[q + u];
               en[u] = g.cell_ent[q + u];
-              sq[u] = seg_sqdist_r2(G.x, G.y, G.z, G.w, lat, lon, ls, r2);
+              sq[u] = seg_sqdist(G.x, G.y, G.z, G.w, lat, lon, ls);
             }
           }
 #pragma unroll
@@ -615,7 +581,6 @@ __global__ __launch_bounds__(CAND_TB, OTM_CAND_WAVES) void k_cand_lane(DevGraph 
             const uint32_t ent = en[u];
             const uint32_t e = ent >> 4;
             int f = -1;
-#if OTM_CAND_FIND
             // every slot's edge read at once (independent LDS reads, no
             // early exit): one LDS round trip per hit instead of up to 8
 #pragma unroll
@@ -623,13 +588,6 @@ __global__ __launch_bounds__(CAND_TB, OTM_CAND_WAVES) void k_cand_lane(DevGraph 
               const uint32_t em = E[m * S];
               if (m < n && (em >> 4) == e) f = m;
             }
-#else
-            for (int m = 0; m < n; ++m)
-              if ((E[m * S] >> 4) == e) {
-                f = m;
-                break;
-              }
-#endif
             if (f < 0) {
               if (n == CAND_LANE_CAP) {
                 spill = true;
@@ -657,10 +615,7 @@ __global__ __launch_bounds__(CAND_TB, OTM_CAND_WAVES) void k_cand_lane(DevGraph 
     // node snap: an entry whose projection snaps to a node becomes that
     // node's candidate (NODE_ENT | first outgoing edge << 4), one per node
     // at the smallest distance
-#ifndef OTM_CAND_DIAG
-#define OTM_CAND_DIAG 0  // A/B diagnostics only (wrong results): 1 skips the node snap, 2 also the output projection
-#endif
-    for (int m = 0; m < (OTM_CAND_DIAG ? 0 : n); ++m) {
+    for (int m = 0; m < n; ++m) {
       const uint32_t em = E[m * S];
       const int32_t e = (int32_t)(em >> 4);
       float sqd, off;
@@ -708,7 +663,7 @@ __global__ __launch_bounds__(CAND_TB, OTM_CAND_WAVES) void k_cand_lane(DevGraph 
       }
       const int32_t e = (int32_t)((em & ~NODE_ENT) >> 4);
       float sqd = qm, off = 0.0f;
-      if (!(em & NODE_ENT) && OTM_CAND_DIAG < 2) project(g, e, (int32_t)(em & 15u), lat, lon, ls, sqd, off);
+      if (!(em & NODE_ENT)) project(g, e, (int32_t)(em & 15u), lat, lon, ls, sqd, off);
       w.cand_edge[CSTRIDE * (p * KMAX + j)] = e;
       w.cand_off[CSTRIDE * (p * KMAX + j)] = off;
       w.cand_emis[CSTRIDE * (p * KMAX + j)] = sqd / ds;
@@ -718,211 +673,6 @@ __global__ __launch_bounds__(CAND_TB, OTM_CAND_WAVES) void k_cand_lane(DevGraph 
     c_cells += cells;
     c_ent += ents;
     c_cand += (unsigned long long)K;
-  }
-  if (w.ctr) {
-    wave_cadd(&w.ctr->cells_visited, c_cells);
-    wave_cadd(&w.ctr->cell_entries_scanned, c_ent);
-    wave_cadd(&w.ctr->candidates, c_cand);
-  }
-}
-
-// Sub-group tier: G lanes per probe, CAND_TB / G probes per block.  A probe's
-// lanes take interleaved entries of each grid row (G consecutive 16-byte
-// geometry words per step: a line or two per probe per load instead of a
-// line per lane -- the lane tier is bound by its divergent gathers in the
-// texture addresser), and keep each edge's best (sqdist, shape segment) in the
-// probe's LDS hash table with 64-bit atomicMin.  Then each lane projects its
-// slots once: edge candidates and node candidates (the node snap) get the
-// wave tier's sort keys, duplicate nodes keep their smallest key, and every
-// surviving key's rank among the probe's keys is its candidate slot.  A probe
-// with more than CAND_SUB_CAP distinct edges goes to the wave tier.
-constexpr int CAND_SUB_HS = 16;   // table slots per probe
-constexpr int CAND_SUB_CAP = 12;  // distinct edges before the wave tier
-template <int G>
-__global__ __launch_bounds__(CAND_TB, OTM_CAND_WAVES) void k_cand_sub(DevGraph g, DevBatch b, DevParams P, DevWork w) {
-  constexpr int NPB = CAND_TB / G;
-  constexpr int HS = CAND_SUB_HS;
-  constexpr int SPL = HS / G;  // slots per lane
-  __shared__ uint32_t tK[NPB][HS];
-  __shared__ unsigned long long tV[NPB][HS];
-  __shared__ unsigned long long tS[NPB][HS];  // sort keys (~0: none)
-  __shared__ int tN[NPB];                     // distinct edges; > HS: table overflow
-  const int sg = threadIdx.x / G, sl = threadIdx.x % G;
-  unsigned long long c_cells = 0, c_ent = 0, c_cand = 0;
-  const bool ordered = (P.order_mask & ORDER_CAND) != 0;
-  int64_t base, end, stride;
-  if (ordered) {
-    const int grp = blockIdx.x % ORDER_GROUPS;
-    base = w.ord.grp[grp] + (int64_t)(blockIdx.x / ORDER_GROUPS) * NPB;
-    end = w.ord.grp[grp + 1];
-    stride = (int64_t)(gridDim.x / ORDER_GROUPS) * NPB;
-  } else {
-    base = (int64_t)blockIdx.x * NPB;
-    end = b.n_points;
-    stride = (int64_t)gridDim.x * NPB;
-  }
-  const float ds = (2.0f * P.sigma_z) * P.sigma_z;
-  for (; base < end; base += stride) {
-    const int64_t it = base + sg;
-    bool act = it < end;
-    int64_t p = 0;
-    if (act) p = ordered ? (int64_t)w.ord.item[it] : it;
-    if (act && !ordered) act = w.is_col[p] != 0;
-    if (act && P.cand_wave_all) {
-      if (sl == 0) w.overflow_list0[atomicAdd(&w.counters_i32[5], 1)] = (int32_t)p;
-      act = false;
-    }
-#pragma unroll
-    for (int u = 0; u < SPL; ++u) {
-      tK[sg][sl + u * G] = EMPTY;
-      tV[sg][sl + u * G] = LAB_NONE;
-    }
-    if (sl == 0) tN[sg] = 0;
-    __syncthreads();
-    float lat = 0.0f, lon = 0.0f, ls = 1.0f;
-    unsigned long long my_cells = 0, my_ents = 0;
-    if (act) {
-      const float4 pr = w.probe[p];  // {lat, lon, accuracy} of the column (K1)
-      lat = pr.x;
-      lon = pr.y;
-      const float r = probe_radius(P, pr.z);
-      const float r2 = r * r;
-      ls = MPD_F * cos_deg(lat);
-      const float dlat = r / MPD_F;
-      const float dlon = r / ls;
-      const double la_lo = ((double)lat - (double)dlat - g.lat0) / g.cell;
-      const double la_hi = ((double)lat + (double)dlat - g.lat0) / g.cell;
-      const double lo_lo = ((double)lon - (double)dlon - g.lon0) / g.cell;
-      const double lo_hi = ((double)lon + (double)dlon - g.lon0) / g.cell;
-      const double R = g.grid_rows, Cn = g.grid_cols;
-      int r0 = 0, r1 = -1, c0 = 0, c1 = -1;
-      if (!(la_hi < 0.0 || lo_hi < 0.0 || la_lo >= R || lo_lo >= Cn)) {
-        r0 = la_lo < 0.0 ? 0 : (int)floor(la_lo);
-        r1 = la_hi >= R ? (int)R - 1 : (int)floor(la_hi);
-        c0 = lo_lo < 0.0 ? 0 : (int)floor(lo_lo);
-        c1 = lo_hi >= Cn ? (int)Cn - 1 : (int)floor(lo_hi);
-      }
-      unsigned long long ents = 0;
-      for (int rr = r0; rr <= r1; ++rr) {
-        const size_t rbase = (size_t)rr * (size_t)g.grid_cols;
-        const int64_t q0 = g.cell_off[rbase + c0], q1 = g.cell_off[rbase + c1 + 1];
-        ents += (unsigned long long)(q1 - q0);
-        for (int64_t q = q0 + sl; q < q1; q += 2 * G) {
-          // two entries per lane in flight: q and q + G
-          float sq[2];
-          uint32_t en[2];
-#pragma unroll
-          for (int u = 0; u < 2; ++u) {
-            sq[u] = INFINITY;
-            en[u] = 0;
-            if (q + u * G < q1) {
-              const float4 Gm = g.ent_geo[q + u * G];
-              en[u] = g.cell_ent[q + u * G];
-              sq[u] = seg_sqdist(Gm.x, Gm.y, Gm.z, Gm.w, lat, lon, ls);
-            }
-          }
-#pragma unroll
-          for (int u = 0; u < 2; ++u) {
-            if (!(sq[u] <= r2)) continue;
-            const uint32_t e = en[u] >> 4;
-            uint32_t h = hash32(e) >> 28;  // HS = 16
-            int probe = 0;
-            for (; probe < HS; ++probe) {
-              const uint32_t old = atomicCAS(&tK[sg][h], EMPTY, e);
-              if (old == EMPTY) atomicAdd(&tN[sg], 1);
-              if (old == EMPTY || old == e) break;
-              h = (h + 1) & (HS - 1);
-            }
-            if (probe == HS) {
-              atomicOr(&tN[sg], 0x10000);  // full table: the wave tier takes the probe
-              continue;
-            }
-            atomicMin(&tV[sg][h], ((unsigned long long)fbits(sq[u]) << 32) | (unsigned long long)(en[u] & 15u));
-          }
-        }
-      }
-      my_cells = (unsigned long long)(r1 - r0 + 1) * (unsigned long long)(c1 - c0 + 1);
-      my_ents = ents;
-    }
-    __syncthreads();
-    const int nd = act ? tN[sg] : 0;
-    if (act && nd > CAND_SUB_CAP) {  // (the wave tier counts its probes' work)
-      if (sl == 0) w.overflow_list0[atomicAdd(&w.counters_i32[5], 1)] = (int32_t)p;
-      act = false;
-    }
-    if (act && sl == 0) {
-      c_cells += my_cells;
-      c_ent += my_ents;
-    }
-    // each lane: project its slots once; sort keys as the wave tier's
-    unsigned long long key[SPL];
-    float offv[SPL];
-#pragma unroll
-    for (int u = 0; u < SPL; ++u) {
-      key[u] = LAB_NONE;
-      offv[u] = 0.0f;
-      const int s = sl + u * G;
-      const uint32_t e = tK[sg][s];
-      if (act && e != EMPTY) {
-        const unsigned long long v = tV[sg][s];
-        float sqd, off;
-        bool at_end;
-        project(g, (int32_t)e, (int32_t)(v & 15ull), lat, lon, ls, sqd, off, at_end);
-        const int32_t nv = snap_node(g, (int32_t)e, off, at_end);
-        const unsigned long long qb = v & 0xFFFFFFFF00000000ull;
-        if (nv < 0) {
-          key[u] = qb | ((unsigned long long)e << 5) | ((v & 15ull) << 1) | 1ull;
-          offv[u] = off;
-        } else {
-          key[u] = qb | ((unsigned long long)(uint32_t)g.out_off[nv] << 5);
-        }
-      }
-      tS[sg][s] = key[u];
-    }
-    __syncthreads();
-    // duplicate nodes (same first outgoing edge): the smallest key, then the lowest slot, stays
-    bool alive[SPL];
-#pragma unroll
-    for (int u = 0; u < SPL; ++u) {
-      const int s = sl + u * G;
-      alive[u] = key[u] != LAB_NONE;
-      if (alive[u] && !(key[u] & 1ull)) {
-        const unsigned long long rep = key[u] & 0xFFFFFFFFull;
-        for (int t2 = 0; t2 < HS; ++t2) {
-          const unsigned long long o = tS[sg][t2];
-          if (t2 != s && o != LAB_NONE && (o & 0xFFFFFFFFull) == rep && (o < key[u] || (o == key[u] && t2 < s)))
-            alive[u] = false;
-        }
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int u = 0; u < SPL; ++u)
-      if (!alive[u]) tS[sg][sl + u * G] = LAB_NONE;
-    __syncthreads();
-    // rank among the probe's surviving keys = candidate slot
-    int nal = 0;
-#pragma unroll
-    for (int u = 0; u < SPL; ++u) nal += alive[u] ? 1 : 0;
-#pragma unroll
-    for (int o = 1; o < G; o <<= 1) nal += __shfl_xor(nal, o, 64);
-    const int K = nal < P.max_candidates ? nal : P.max_candidates;
-#pragma unroll
-    for (int u = 0; u < SPL; ++u) {
-      if (!alive[u]) continue;
-      int rank = 0;
-      for (int t2 = 0; t2 < HS; ++t2) rank += tS[sg][t2] < key[u] ? 1 : 0;
-      if (rank >= K) continue;
-      const int32_t e = (int32_t)(((uint32_t)key[u]) >> 5);
-      w.cand_edge[CSTRIDE * (p * KMAX + rank)] = e;
-      w.cand_off[CSTRIDE * (p * KMAX + rank)] = offv[u];
-      w.cand_emis[CSTRIDE * (p * KMAX + rank)] = bitsf((uint32_t)(key[u] >> 32)) / ds;
-    }
-    if (act && sl == 0) {
-      w.ncand[p] = K;
-      c_cand += (unsigned long long)K;
-    }
-    __syncthreads();
   }
   if (w.ctr) {
     wave_cadd(&w.ctr->cells_visited, c_cells);
@@ -1628,12 +1378,6 @@ __device__ __forceinline__ uint32_t idx_hash(uint32_t v) {
 #ifndef OTM_IDX_LOAD_PCT
 #define OTM_IDX_LOAD_PCT 20
 #endif
-#ifndef OTM_IDX_EROW
-#define OTM_IDX_EROW 1
-#endif
-#ifndef OTM_IDX_EROW_SRC
-#define OTM_IDX_EROW_SRC 1
-#endif
 __host__ __device__ __forceinline__ int64_t idx_row_cap(int32_t c) {
   if (c <= 0) return 0;
 #if OTM_IDX_LOAD_PCT
@@ -1771,27 +1515,20 @@ __global__ void k_row_pack(const int32_t* row_cnt, const int64_t* row_off, IdxRo
 #ifndef OTM_TRANS_KC8
 #define OTM_TRANS_KC8 8
 #endif
-#ifndef OTM_TRANS_PAD
-#define OTM_TRANS_PAD 0
-#endif
-#ifndef OTM_TRANS_KC4
-#define OTM_TRANS_KC4 6
-#endif
 template <int S, bool LIST>
 __global__ __launch_bounds__(TB, 8) void k_trans_sub(DevGraph g, DevBatch b, DevParams P, DevWork w) {
   if (*w.abort || trans_over_cap(b, w)) return;  // a capacity was exceeded: the host redoes the batch
+  static_assert(S == 8 || S == 16, "8 lanes per column (two passes) or 16 (one pass / the wide pass)");
   constexpr int NS = TB / S;
   // a pair reads its target and source as one 16-byte LDS word each
-  constexpr int KC = S >= 16 ? 16 : (S == 8 ? OTM_TRANS_KC8 : OTM_TRANS_KC4);
+  constexpr int KC = S >= 16 ? 16 : OTM_TRANS_KC8;
   constexpr bool WIDE = KC < 16;
-  // (OTM_TRANS_PAD: one spare 16-byte word per column group, spreading the
-  // groups' rows over the LDS banks)
-  __shared__ int4 tg[NS][KC + OTM_TRANS_PAD];  // target: edge, offset bits, from-node, start heading
-  __shared__ int4 sr[NS][KC + OTM_TRANS_PAD];  // source: edge, offset bits, remaining-length bits, end heading
-  __shared__ IdxRow rq[NS][KC + OTM_TRANS_PAD];
+  __shared__ int4 tg[NS][KC];  // target: edge, offset bits, from-node, start heading
+  __shared__ int4 sr[NS][KC];  // source: edge, offset bits, remaining-length bits, end heading
+  __shared__ IdxRow rq[NS][KC];
   __shared__ uint32_t TU[TURN_TABLE];  // turn units per deviation
   const int lane = threadIdx.x, sg = lane / S, sl = lane % S;
-  const unsigned long long smask = (S == 64 ? ~0ull : ((1ull << S) - 1ull)) << (sg * S);
+  const unsigned long long smask = ((1ull << S) - 1ull) << (sg * S);
   for (int k = lane; k < TURN_TABLE; k += TB) TU[k] = P.turn_units[k];
   const DevIndex& X = w.idx;
   unsigned long long c_search = 0, c_settled = 0, c_relaxed = 0, c_trans = 0;
@@ -1848,16 +1585,8 @@ __global__ __launch_bounds__(TB, 8) void k_trans_sub(DevGraph g, DevBatch b, Dev
         const float o = w.cand_off[CSTRIDE * ((int64_t)q * KMAX + k)];
         sr[sg][k] = make_int4(e, __float_as_int(o), __float_as_int(src_start(g, e, o)), (int)src_head(g, e, o));
         if (idx_ok) {
-#if OTM_IDX_EROW
-#if OTM_IDX_EROW_SRC
           // erow[e]: the row of e's end node; erow[E + e]: of its start node
           const IdxRow R = X.erow[cand_node(o) ? (int64_t)g.n_edges + e : (int64_t)e];
-#else
-          const IdxRow R = cand_node(o) ? X.row[g.e_from[e]] : X.erow[e];
-#endif
-#else
-          const IdxRow R = X.row[src_node(g, e, o)];
-#endif
           rq[sg][k] = R;
           bad = bad || R.cnt < 0;
         }
@@ -1873,7 +1602,6 @@ __global__ __launch_bounds__(TB, 8) void k_trans_sub(DevGraph g, DevBatch b, Dev
     if (act) {
       float* Tm = w.trans + toff;
       unsigned long long ntr = 0;
-#if OTM_TRANS_BATCH > 1
       // OTM_TRANS_BATCH pairs per lane per step: every pair's first slot is
       // loaded before any is resolved, so their probes are in flight together
       constexpr int NB = OTM_TRANS_BATCH;
@@ -1936,35 +1664,6 @@ __global__ __launch_bounds__(TB, 8) void k_trans_sub(DevGraph g, DevBatch b, Dev
           Tm[i * Kp + j] = cost;
         }
       }
-#else
-      for (int idx = sl; idx < Kq * Kp; idx += S) {
-        const int i = idx / Kp, j = idx - (idx / Kp) * Kp;
-        float r = 0.0f;
-        bool ok = true;
-        uint32_t units = 0;
-        const int4 T = tg[sg][j], Sx = sr[sg][i];
-        const int32_t ej = T.x, vj = T.z, ei = Sx.x;
-        const float oj = __int_as_float(T.y), oi = __int_as_float(Sx.y), si = __int_as_float(Sx.z);
-        if (ej == ei && oj >= oi) {
-          r = oj - oi;
-        } else {
-          uint4 slv;
-          if (idx_find(X, rq[sg][i], (uint32_t)vj, slv) >= 0) {
-            const float sd = si + bitsf(slv.y);
-            r = sd + oj;
-            units = idx_turn_units(TU, slv, (uint32_t)Sx.w, (uint32_t)T.w);
-          } else {
-            ok = false;
-          }
-        }
-        float cost = INFINITY;
-        if (ok && r <= bound) {
-          cost = trans_cost(units, r, gcv, P.beta);
-          ++ntr;
-        }
-        Tm[i * Kp + j] = cost;
-      }
-#endif
       if (w.ctr) {
         // algorithmic counts of the equivalent searches (per-lane partials,
         // summed over the wave at the end): per distinct source, the row
@@ -2355,8 +2054,7 @@ __device__ void viterbi_trace_global(int64_t a, int64_t e, DevWork& w) {
 constexpr int VIT_PTS = OTM_VIT_PTS; // points per trace (metadata held for the whole trace)
 constexpr int VIT_BP = OTM_VIT_BP;   // candidates per trace (backpointers)
 constexpr int VIT_TW = OTM_VIT_TW;   // transition floats per window (>= one column pair's block)
-// emission floats per window (>= KMAX); the walk form (OTM_VIT_WALK) needs 144
-// to stay within 8 waves per SIMD of LDS
+// emission floats per window (>= KMAX)
 #ifndef OTM_VIT_EW
 #define OTM_VIT_EW 256
 #endif
@@ -2366,29 +2064,9 @@ static_assert(VIT_EW >= KMAX, "one column's emissions fit a window");
 #ifndef OTM_VIT_WAVES
 #define OTM_VIT_WAVES 8
 #endif
-// Backtrack form.  1: a backpointer is the trace-wide index of the
-// predecessor candidate (eoff of the previous column + its state), so lane 0's
-// walk is one dependent LDS read per column, marking the visited entries; the
-// states and chain starts are then read back point-parallel.  0: the round-1
-// walk (state, backpointer, eoff and previous column: three dependent reads).
-// 1 measured 0.159 vs 0.157 ms (config 2) at 8 waves per SIMD, but its 16-bit
-// backpointers need the emission window cut to 144 floats to stay there (with
-// 256: 7 waves, 0.180 ms): 0 kept.
-#ifndef OTM_VIT_WALK
-#define OTM_VIT_WALK 0
-#endif
-// Window staging.  1: the transition block and the first emissions are loaded
-// before any is stored (one global round trip per window); 0: transitions,
-// then emissions.  Measured equal (k_viterbi 0.159 vs 0.158 ms config 2, 1.090
-// vs 1.077 config 4; profiles/r02_ab_viterbi.txt): 0 kept.
-#ifndef OTM_VIT_STAGE1
-#define OTM_VIT_STAGE1 0
-#endif
-#if OTM_VIT_WALK
-constexpr int16_t VIT_BP_START = 0x7FFF;  // chain start: the walk ends here
-constexpr int16_t VIT_BP_DEAD = 0x7FFE;   // unreachable state: never walked
-constexpr int VIT_BP_MARK = 0x8000;       // set on the entries the walk visits
-#endif
+// Measured and not kept (profiles/r02_ab_viterbi.txt): a one-read backtrack
+// through trace-wide backpointer indices (0.159 vs 0.157 ms, and 16-bit
+// backpointers cost occupancy), one global round trip per window (equal).
 __global__ __launch_bounds__(TB, OTM_VIT_WAVES) void k_viterbi(DevBatch b, DevWork w) {
   // spill snapshot B: columns per transition tier (Viterbi does not touch the
   // counters; they start over for the route tiers)
@@ -2396,13 +2074,9 @@ __global__ __launch_bounds__(TB, OTM_VIT_WAVES) void k_viterbi(DevBatch b, DevWo
   if (*w.abort) return;  // a capacity was exceeded: the host redoes the batch
   __shared__ float sT[VIT_TW];
   __shared__ float sEm[VIT_EW];
-#if OTM_VIT_WALK
-  __shared__ uint16_t sBp[VIT_BP];
-#else
   __shared__ uint8_t sBp[VIT_BP];
   __shared__ int8_t sState[VIT_PTS];
   __shared__ uint8_t sCs[VIT_PTS];
-#endif
   __shared__ int32_t sToff[VIT_PTS + 1];
   __shared__ int16_t sEoff[VIT_PTS + 1];
   __shared__ int16_t sCprev[VIT_PTS];
@@ -2449,10 +2123,8 @@ __global__ __launch_bounds__(TB, OTM_VIT_WAVES) void k_viterbi(DevBatch b, DevWo
           sCprev[pl] = (int16_t)cp;
           sToff[pl] = to;
           sEoff[pl] = (int16_t)min(etot + incl - k, 32767);
-#if !OTM_VIT_WALK
           sState[pl] = -1;
           sCs[pl] = 0;
-#endif
         }
         etot += __shfl(incl, 63, 64);
       }
@@ -2477,25 +2149,6 @@ __global__ __launch_bounds__(TB, OTM_VIT_WAVES) void k_viterbi(DevBatch b, DevWo
     bool open = false;
     int last = -1;
     int win_end = 0, wt0 = 0, we0 = 0;
-#if OTM_VIT_WALK
-    int lastEo = 0;  // eoff of column `last`
-    auto backtrack = [&](int endl, int Ke) {
-      (void)endl;
-      float bv;
-      int bi;
-      wave_argmin(lane < Ke ? prev : INFINITY, lane, bv, bi);
-      __syncthreads();  // backpointers written by other lanes
-      if (lane == 0) {
-        int ix = lastEo + bi;
-        while (true) {
-          const int v = sBp[ix];
-          sBp[ix] = (uint16_t)(v | VIT_BP_MARK);
-          if (v == VIT_BP_START) break;
-          ix = v;
-        }
-      }
-    };
-#else
     auto backtrack = [&](int endl, int Ke) {
       float bv;
       int bi;
@@ -2512,7 +2165,6 @@ __global__ __launch_bounds__(TB, OTM_VIT_WAVES) void k_viterbi(DevBatch b, DevWo
         }
       }
     };
-#endif
     // The forward pass walks the points in chunks of 64 whose metadata sits
     // in registers (lane k holds point c0 + k) and is read with readlane: the
     // per-column chain keeps one LDS round trip (emission + transition reads,
@@ -2552,63 +2204,6 @@ __global__ __launch_bounds__(TB, OTM_VIT_WAVES) void k_viterbi(DevBatch b, DevWo
           }
           win_end = we;
           const int nt = sToff[win_end] - wt0;
-#if OTM_VIT_STAGE1
-          // one round trip for the window: the transition block (nt <= VIT_TW
-          // <= 8 x 64 floats) and the first four emissions of the first 64
-          // points are all loaded before any of them is stored
-          static_assert(VIT_TW <= 8 * TB, "one pass of transition loads");
-          {
-            float v[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-              const int f = u * TB + lane;
-              v[u] = f < nt ? w.trans[t0 + wt0 + f] : 0.0f;
-            }
-            const int q = pl + lane;
-            int kq = 0, eq = 0;
-            if (q < win_end) {
-              kq = sKc[q];
-              eq = sEoff[q] - we0;
-            }
-            float ev[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) ev[u] = u < kq ? w.cand_emis[CSTRIDE * ((a + q) * KMAX + u)] : 0.0f;
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-              const int f = u * TB + lane;
-              if (f < nt) sT[f] = v[u];
-            }
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-              if (u < kq) sEm[eq + u] = ev[u];
-            // the rest: candidates beyond four, points beyond 64 (rare)
-            for (int j0 = 4; __ballot(j0 < kq) != 0ull; j0 += 4) {
-#pragma unroll
-              for (int u = 0; u < 4; ++u)
-                ev[u] = j0 + u < kq ? w.cand_emis[CSTRIDE * ((a + q) * KMAX + j0 + u)] : 0.0f;
-#pragma unroll
-              for (int u = 0; u < 4; ++u)
-                if (j0 + u < kq) sEm[eq + j0 + u] = ev[u];
-            }
-          }
-          for (int q0 = pl + TB; q0 < win_end; q0 += TB) {
-            const int q = q0 + lane;
-            int kq = 0, eq = 0;
-            if (q < win_end) {
-              kq = sKc[q];
-              eq = sEoff[q] - we0;
-            }
-            for (int j0 = 0; __ballot(j0 < kq) != 0ull; j0 += 4) {
-              float v[4];
-#pragma unroll
-              for (int u = 0; u < 4; ++u)
-                v[u] = j0 + u < kq ? w.cand_emis[CSTRIDE * ((a + q) * KMAX + j0 + u)] : 0.0f;
-#pragma unroll
-              for (int u = 0; u < 4; ++u)
-                if (j0 + u < kq) sEm[eq + j0 + u] = v[u];
-            }
-          }
-#else
           for (int f0 = 0; f0 < nt; f0 += 8 * TB) {
             float v[8];
 #pragma unroll
@@ -2641,7 +2236,6 @@ __global__ __launch_bounds__(TB, OTM_VIT_WAVES) void k_viterbi(DevBatch b, DevWo
                 if (j0 + u < kq) sEm[eq + j0 + u] = v[u];
             }
           }
-#endif
           __syncthreads();
         }
         const int eo = __builtin_amdgcn_readlane(r_eo, k);
@@ -2682,11 +2276,7 @@ __global__ __launch_bounds__(TB, OTM_VIT_WAVES) void k_viterbi(DevBatch b, DevWo
           const bool alive = lane < Kp && bi >= 0;
           if (lane < Kp) {
             cur = alive ? best + em : INFINITY;
-#if OTM_VIT_WALK
-            sBp[eo + lane] = alive ? (uint16_t)(lastEo + bi) : (uint16_t)VIT_BP_DEAD;
-#else
             sBp[eo + lane] = alive ? (uint8_t)bi : (uint8_t)0xFF;
-#endif
           }
           if (__ballot(alive) == 0ull) {
             backtrack(last, lastK);
@@ -2698,39 +2288,19 @@ __global__ __launch_bounds__(TB, OTM_VIT_WAVES) void k_viterbi(DevBatch b, DevWo
         }
         if (!started) {
           cur = lane < Kp ? em : INFINITY;
-#if OTM_VIT_WALK
-          if (lane < Kp) sBp[eo + lane] = (uint16_t)VIT_BP_START;
-#else
           if (lane == 0) sCs[pl] = 1;
-#endif
         }
         prev = cur;
         open = true;
         last = pl;
         lastK = Kp;
-#if OTM_VIT_WALK
-        lastEo = eo;
-#endif
       }
     }
     if (open) backtrack(last, lastK);
     __syncthreads();
     for (int pl = lane; pl < n; pl += TB) {
-#if OTM_VIT_WALK
-      // every column with candidates lies on a walked chain: its state is the
-      // marked entry, and a chain start's entries all hold VIT_BP_START
-      const int kc = sKc[pl];
-      const int eo = sEoff[pl];
-      int st = -1, cs = 0;
-      for (int j = 0; j < kc; ++j) {
-        const int v = sBp[eo + j];
-        if (v & VIT_BP_MARK) st = j;
-        if (j == 0) cs = (v & ~VIT_BP_MARK) == VIT_BP_START;
-      }
-#else
       const int st = sState[pl];
       const int cs = sCs[pl];
-#endif
       w.state[a + pl] = st;
       w.chain_start[a + pl] = (uint8_t)cs;
       // the chosen candidate, compact for the route and segment stages
@@ -3873,23 +3443,6 @@ constexpr int TRANS_GRID_CAP = 65536;  // k_trans_sub waves (one per column, gri
 
 }  // namespace
 
-// A host<->device copy by a few workgroups of this library's own (the pinned
-// host buffer is device-mapped): the runtime's blit copies put a 512-thread
-// workgroup on every CU, whose waves then sit on PCIe latency beside the other
-// batches' kernels.  16-byte words, grid-strided; the tail byte by byte.
-__global__ __launch_bounds__(256) void k_copy(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, size_t n) {
-  const size_t nw = n / 16;
-  const uint4* s4 = (const uint4*)src;
-  uint4* d4 = (uint4*)dst;
-  const size_t stride = (size_t)gridDim.x * blockDim.x;
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < nw; i += stride) d4[i] = s4[i];
-  const size_t t = nw * 16 + (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t < n && (size_t)blockIdx.x * blockDim.x + threadIdx.x < 16) dst[t] = src[t];
-}
-void launch_copy(void* dst, const void* src, size_t n, int blocks, hipStream_t s) {
-  if (n) hipLaunchKernelGGL(k_copy, dim3(blocks), dim3(256), 0, s, (const uint8_t*)src, (uint8_t*)dst, n);
-}
-
 void launch_fetch_scan(int32_t n, const int32_t* c0, const int32_t* c1, const int32_t* c2, int32_t* o0, int32_t* o1,
                        int32_t* o2, hipStream_t s) {
   hipLaunchKernelGGL(k_fetch_scan, dim3(1), dim3(1024), 0, s, n, c0, c1, c2, o0, o1, o2);
@@ -3946,20 +3499,9 @@ void launch_order(const DevBatch& b, DevWork& w, hipStream_t s, const Marks& mk)
 }
 
 void launch_candidates(const DevGraph& g, const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s,
-                       const Marks& mk, int lanes) {
-  // lanes per probe: 1 = the lane tier, 4 / 8 / 16 = the sub-group tier
-  if (lanes == 4)
-    TIMED(KN_CAND_LANE, hipLaunchKernelGGL(k_cand_sub<4>, dim3(order_grid(b.n_points, CAND_TB / 4, 1 << 30)),
-                                           dim3(CAND_TB), 0, s, g, b, p, w));
-  else if (lanes == 8)
-    TIMED(KN_CAND_LANE, hipLaunchKernelGGL(k_cand_sub<8>, dim3(order_grid(b.n_points, CAND_TB / 8, 1 << 30)),
-                                           dim3(CAND_TB), 0, s, g, b, p, w));
-  else if (lanes == 16)
-    TIMED(KN_CAND_LANE, hipLaunchKernelGGL(k_cand_sub<16>, dim3(order_grid(b.n_points, CAND_TB / 16, 1 << 30)),
-                                           dim3(CAND_TB), 0, s, g, b, p, w));
-  else
-    TIMED(KN_CAND_LANE, hipLaunchKernelGGL(k_cand_lane, dim3(order_grid(b.n_points, CAND_TB, 1 << 30)),
-                                           dim3(CAND_TB), 0, s, g, b, p, w));
+                       const Marks& mk) {
+  TIMED(KN_CAND_LANE, hipLaunchKernelGGL(k_cand_lane, dim3(order_grid(b.n_points, CAND_TB, 1 << 30)),
+                                         dim3(CAND_TB), 0, s, g, b, p, w));
   TIMED(KN_CAND_WAVE, hipLaunchKernelGGL(k_candidates, dim3(4096), dim3(TB), 0, s, g, b, p, w));
 }
 void launch_links(const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s, const Marks& mk) {
@@ -3990,22 +3532,13 @@ void launch_transitions(const DevGraph& g, const DevBatch& b, const DevParams& p
   const int per = TB / sub;  // columns per wave step
   const int grid = genv ? std::max(ORDER_GROUPS, std::atoi(genv) / ORDER_GROUPS * ORDER_GROUPS)
                         : order_grid((b.n_points + per - 1) / per, 1, TRANS_GRID_CAP);
-  if (sub <= 8) {
-    // 8 (4) lanes per column over the columns of <= OTM_TRANS_KC8 (KC4)
-    // candidates a side, then 16 lanes over the wide rest (a list filled on
-    // the device)
-    if (sub == 4)
-      TIMED(KN_TRANS_INDEX, hipLaunchKernelGGL((k_trans_sub<4, false>), dim3(grid), dim3(TB), 0, s, g, b, p, w));
-    else
-      TIMED(KN_TRANS_INDEX, hipLaunchKernelGGL((k_trans_sub<8, false>), dim3(grid), dim3(TB), 0, s, g, b, p, w));
+  if (sub == 8) {
+    // 8 lanes per column over the columns of <= OTM_TRANS_KC8 candidates a
+    // side, then 16 lanes over the wide rest (a list filled on the device)
+    TIMED(KN_TRANS_INDEX, hipLaunchKernelGGL((k_trans_sub<8, false>), dim3(grid), dim3(TB), 0, s, g, b, p, w));
     TIMED(KN_TRANS_WIDE, hipLaunchKernelGGL((k_trans_sub<16, true>), dim3(WIDE_GRID), dim3(TB), 0, s, g, b, p, w));
   } else {
-    if (sub == 32)
-      TIMED(KN_TRANS_INDEX, hipLaunchKernelGGL((k_trans_sub<32, false>), dim3(grid), dim3(TB), 0, s, g, b, p, w));
-    else if (sub == 16)
-      TIMED(KN_TRANS_INDEX, hipLaunchKernelGGL((k_trans_sub<16, false>), dim3(grid), dim3(TB), 0, s, g, b, p, w));
-    else
-      TIMED(KN_TRANS_INDEX, hipLaunchKernelGGL((k_trans_sub<64, false>), dim3(grid), dim3(TB), 0, s, g, b, p, w));
+    TIMED(KN_TRANS_INDEX, hipLaunchKernelGGL((k_trans_sub<16, false>), dim3(grid), dim3(TB), 0, s, g, b, p, w));
     mk.begin(KN_TRANS_WIDE, s);
     mk.end(KN_TRANS_WIDE, s);
   }

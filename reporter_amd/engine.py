@@ -26,7 +26,7 @@ def _check(rc):
         raise OtmError("libotmatch error %d: %s" % (rc, _lib.last_error()))
 
 
-def write_config(path, graph_path, index_radius_m=None, grid_mult=None, trans_lanes=None, cand_lanes=None, **meili):
+def write_config(path, graph_path, index_radius_m=None, grid_mult=None, trans_lanes=None, **meili):
     """Write an engine config: {"otm":{"graph":...,"index_radius_m":R},"meili":{"default":{...}}}."""
     otm = {"graph": os.path.abspath(graph_path)}
     if index_radius_m is not None:
@@ -35,8 +35,6 @@ def write_config(path, graph_path, index_radius_m=None, grid_mult=None, trans_la
         otm["grid_mult"] = grid_mult
     if trans_lanes is not None:
         otm["trans_lanes"] = trans_lanes
-    if cand_lanes is not None:
-        otm["cand_lanes"] = cand_lanes
     cfg = {"otm": otm, "meili": {"default": meili}}
     with open(path, "w") as f:
         json.dump(cfg, f)
@@ -55,7 +53,7 @@ class Results(object):
 
 class Engine(object):
     def __init__(self, config_path=None, graph_path=None, device=0, index_radius_m=None, grid_mult=None,
-                 trans_lanes=None, cand_lanes=None, devices=None, **meili):
+                 trans_lanes=None, devices=None, **meili):
         """Either a config file (valhalla.Configure-style) or a graph path.
         devices=[d0, d1, ...] makes a multi-device engine (otm_engine_create
         with ndev > 1): traces go to member murmur2(uuid) % ndev."""
@@ -67,7 +65,7 @@ class Engine(object):
             fd, self._tmp = tempfile.mkstemp(suffix=".json", prefix="otm_cfg_")
             os.close(fd)
             config_path = write_config(self._tmp, graph_path, index_radius_m=index_radius_m, grid_mult=grid_mult,
-                                       trans_lanes=trans_lanes, cand_lanes=cand_lanes, **meili)
+                                       trans_lanes=trans_lanes, **meili)
         h = C.c_void_p()
         devs = list(devices) if devices is not None else [device]
         dev = (C.c_int * len(devs))(*devs)

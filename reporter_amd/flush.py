@@ -17,6 +17,8 @@ One dist.reduce_scatter_tensor per buffer: RCCL over xGMI with backend
 segments, 16 bins) that is 0.87 MB + 0.11 MB per flush; at a 1M-segment
 metro graph 64 MB + 8 MB, one ring pass per flush window.
 """
+import time
+
 import torch
 import torch.distributed as dist
 
@@ -43,6 +45,29 @@ def reduce_histograms(hist, out=None, speed_sum=None, speed_out=None):
         speed_out = torch.empty(speed_sum.numel() // world, dtype=speed_sum.dtype, device=speed_sum.device)
     dist.reduce_scatter_tensor(speed_out, speed_sum)
     return out, speed_out
+
+
+def close_window(t_start, hist, hist_out=None, speed_sum=None, speed_out=None, sync=None):
+    """End of a timed window of the multi-GPU bench (bench.py): wait for this
+    rank's work (`sync`, e.g. torch.cuda.synchronize), then -- over more than
+    one rank -- the window's histogram flush (reduce_histograms: RCCL over
+    xGMI, or gloo) and a barrier.  Returns the window's seconds since
+    `t_start` (time.perf_counter) as the MAX over ranks: every rank gets the
+    same figure, the slowest rank's."""
+    multi = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+    if sync:
+        sync()
+    if multi:
+        reduce_histograms(hist, out=hist_out, speed_sum=speed_sum, speed_out=speed_out)
+        if sync:
+            sync()
+        dist.barrier()
+    elapsed = time.perf_counter() - t_start
+    if multi:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=hist.device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed
 
 
 def histogram_from_reports(reports, seg_index_of_id, n_rows, nbins, bin_kph):

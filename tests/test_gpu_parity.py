@@ -61,10 +61,10 @@ def _stage_compare(eng, orc, batch):
 
 
 def _run_both(graph, batch, oracle, results_equal, meili=None, stages=True, counters=True, index_radius_m=None,
-              grid_mult=None, trans_lanes=None, cand_lanes=None):
+              grid_mult=None, trans_lanes=None):
     meili = meili or {}
     with Engine(graph_path=graph, index_radius_m=index_radius_m, grid_mult=grid_mult, trans_lanes=trans_lanes,
-                cand_lanes=cand_lanes, **meili) as eng:
+                **meili) as eng:
         eng.set_counting(counters)
         res = eng.match(batch)
         p = oracle.params(**meili)
@@ -79,7 +79,7 @@ def _run_both(graph, batch, oracle, results_equal, meili=None, stages=True, coun
             grid_keys = ("cells_visited", "cell_entries_scanned")
             same_grid = eng.grid_info()["mult"] == 1
             for k, v in orc["counters"].items():
-                if k in grid_keys and not same_grid:
+                if (k in grid_keys and not same_grid) or k not in c:  # (oracle-only: §8(d)'s unique-edge term)
                     continue
                 assert c[k] == v, "counter %s gpu %d oracle %d" % (k, c[k], v)
         return res, orc
@@ -98,30 +98,28 @@ def test_city_sample_sigma15(small_graph, oracle, results_equal, batch_path, rad
     assert len(res.segments) > 1000 and len(res.reports) > 50
 
 
-@pytest.mark.parametrize("lanes", [4, 8, 16, 32, 64])
+@pytest.mark.parametrize("lanes", [8, 16])
 def test_transition_lanes(small_graph, oracle, results_equal, lanes):
     # k_trans_sub at 8 lanes per column runs two passes (columns of more than
     # OTM_TRANS_KC8 candidates a side go to a 16-lane pass over a device list);
-    # 16 / 32 / 64 lanes run one.  Node candidates merge edges, so K varies
-    # per column and both passes see work here.
+    # 16 lanes run one.  Node candidates merge edges, so K varies per column
+    # and both passes see work here.
     b = synth.make_traces(small_graph, 200, 100, interval_s=5.0, noise_sigma_m=15.0, accuracy=15.0, seed=23)
     res, orc = _run_both(small_graph, b, oracle, results_equal, trans_lanes=lanes)
     k = orc["ncand"]
     assert k.max() > 8 and (k > 0).mean() > 0.9
 
 
-@pytest.mark.parametrize("lanes", [1, 4, 8, 16])
 @pytest.mark.parametrize("grid_mult", [1, None], ids=["grid1", "grid_auto"])
-def test_candidate_lanes(small_graph, rural_graph, oracle, results_equal, lanes, grid_mult):
-    # K2's lane tier (1 lane per probe) and sub-group tier (4 / 8 / 16 lanes
-    # per probe, an LDS hash table per probe); probes beyond either's edge cap
-    # go to the wave tier -- candidates, counters and everything after
-    # identical to the oracle.  The rural graph at 100 m has many edges per probe.
+def test_candidate_tiers(small_graph, rural_graph, oracle, results_equal, grid_mult):
+    # K2's lane tier (1 lane per probe); probes beyond its edge cap go to the
+    # wave tier -- candidates, counters and everything after identical to the
+    # oracle.  The rural graph at 100 m has many edges per probe.
     b = synth.make_traces(small_graph, 150, 100, interval_s=5.0, noise_sigma_m=15.0, accuracy=15.0, seed=31)
-    _run_both(small_graph, b, oracle, results_equal, grid_mult=grid_mult, cand_lanes=lanes)
+    _run_both(small_graph, b, oracle, results_equal, grid_mult=grid_mult)
     b = synth.make_traces(rural_graph, 100, 60, interval_s=30.0, noise_sigma_m=50.0, accuracy=50.0, seed=37)
     _run_both(rural_graph, b, oracle, results_equal, meili={"search_radius": 100.0, "max_search_radius": 100.0},
-              grid_mult=grid_mult, cand_lanes=lanes)
+              grid_mult=grid_mult)
 
 
 def test_node_candidates(small_graph, oracle, results_equal):
@@ -479,11 +477,9 @@ def test_json_report_path_host_threads(small_graph, oracle, monkeypatch, fast):
         assert eng.report_batch(bodies) == got
 
 
-@pytest.mark.parametrize("blocks", ["0", "32"])
-def test_pinned_host_batch_copy_paths(small_graph, monkeypatch, blocks):
-    """otm_match_soa from pinned host buffers (otm_host_alloc) through the
-    runtime's copies and through the library's own copy kernel
-    (OTM_COPY_KERNEL): the same results as from pageable numpy arrays."""
+def test_pinned_host_batch_copy_path(small_graph):
+    """otm_match_soa from pinned host buffers (otm_host_alloc): the same
+    results as from pageable numpy arrays."""
     import ctypes as C
     from reporter_amd import _lib
     L = _lib.lib()
@@ -492,7 +488,6 @@ def test_pinned_host_batch_copy_paths(small_graph, monkeypatch, blocks):
     with Engine(graph_path=small_graph) as eng:
         want = eng.match(b)
         want = [getattr(want, k).tobytes() for k in ("traces", "segments", "reports", "way_ids")]
-        monkeypatch.setenv("OTM_COPY_KERNEL", blocks)
         ptrs, keep = {}, []
         for k in ("trace_off", "lat", "lon", "time", "accuracy"):
             a = np.ascontiguousarray(b[k])

@@ -120,3 +120,49 @@ def test_datastore_post_keeps_the_secret_key(tmp_path):
     assert got["path"] == "/store?secret_key=abc"
     assert got["body"] == body and got["type"].startswith("application/json")
     assert datastore.post(body, url="") is None or os.environ.get("DATASTORE_URL")
+
+
+def _window_worker(rank, world, port, out_dir):
+    import sys
+    import time
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from reporter_amd import flush
+    rows, nb = flush.padded_segments(37, world), 4
+    hist = torch.arange(rows * nb, dtype=torch.int32) * (rank + 1)
+    sums = torch.arange(rows, dtype=torch.int64) * 1000 * (rank + 1)
+    out = torch.empty(rows * nb // world, dtype=torch.int32)
+    sout = torch.empty(rows // world, dtype=torch.int64)
+    dist.barrier()
+    t0 = time.perf_counter()
+    time.sleep(0.05 + 0.25 * rank)  # rank 1 is the slow one
+    el = flush.close_window(t0, hist, hist_out=out, speed_sum=sums, speed_out=sout)
+    np.save(os.path.join(out_dir, "w%d.npy" % rank), np.array([el]))
+    np.save(os.path.join(out_dir, "h%d.npy" % rank), out.numpy())
+    np.save(os.path.join(out_dir, "s%d.npy" % rank), sout.numpy())
+    dist.destroy_process_group()
+
+
+def test_bench_window_helper_max_over_ranks_and_flush(tmp_path):
+    """bench.py's N > 1 timed window (flush.close_window): the histogram
+    reduce-scatter runs inside it and every rank reports the slowest rank's
+    time."""
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    world = 2
+    mp.start_processes(_window_worker, args=(world, port, str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    el = [float(np.load(str(tmp_path / ("w%d.npy" % r)))[0]) for r in range(world)]
+    assert el[0] == el[1] and el[0] >= 0.3
+    from reporter_amd import flush
+    rows, nb = flush.padded_segments(37, world), 4
+    full = np.arange(rows * nb, dtype=np.int64) * 3  # (1 + 2) x
+    fs = np.arange(rows, dtype=np.int64) * 1000 * 3
+    for r in range(world):
+        h = np.load(str(tmp_path / ("h%d.npy" % r)))
+        sm = np.load(str(tmp_path / ("s%d.npy" % r)))
+        np.testing.assert_array_equal(h, full[r * rows * nb // world:(r + 1) * rows * nb // world])
+        np.testing.assert_array_equal(sm, fs[r * rows // world:(r + 1) * rows // world])

@@ -842,11 +842,10 @@ static int route_step(batch* B, ws* w, int64_t p, int32_t* path, int* plen, int*
  *   cost sqdist / (2 sigma_z^2) + |position - gc(q, k)| / beta -- meili's
  *   emission plus a transition from q (no turns), the lowest cost winning
  *   (ties: the earliest piece);
- *   a point with no admissible piece, or placed behind an earlier point of the
- *   step (position below the running maximum, starting at q's 0), stays
- *   unplaced (-1).
- * The placed points and the two states are the step's anchors (positions
- * nondecreasing in trace order).  A boundary at route distance x gets
+ *   a point with no admissible piece stays unplaced (-1).
+ * The step's anchors are its two states and the placed points that are not
+ * behind an earlier anchor (position >= the running maximum, starting at q's
+ * 0): their positions are nondecreasing in trace order.  A boundary at route distance x gets
  *   shape index = the last anchor (trace order) at position <= x;
  *   time = linear between the last anchor L before p with position <= x and
  *   the anchor N after it: t_L + (t_N - t_L) * ((x - x_L) / (x_N - x_L)),
@@ -906,16 +905,7 @@ static void interp_step(batch* B, int64_t q, int64_t p, int32_t ei, float oi, in
     dd = dd + len;
   }
   if (oj != 0.0f) pc[n++] = (piece){ej, 0.0f, oj, start + dd};
-  float run = 0.0f;
-  for (int64_t k = q + 1; k < p; ++k) {
-    const float v = interp_pos(B, pc, n, q, k);
-    if (v >= 0.0f && v >= run) {
-      B->ipos[k] = v;
-      run = v;
-    } else {
-      B->ipos[k] = -1.0f;
-    }
-  }
+  for (int64_t k = q + 1; k < p; ++k) B->ipos[k] = interp_pos(B, pc, n, q, k);
   free(pc);
 }
 
@@ -923,18 +913,19 @@ static void interp_step(batch* B, int64_t q, int64_t p, int32_t ei, float oi, in
    distance x of step q -> p */
 static void step_bound(const batch* B, int64_t a, int64_t q, int64_t p, float R, float x, double* t, int32_t* sh) {
   int64_t iL = q, k = q + 1;
-  float xL = 0.0f, xN = R;
+  float xL = 0.0f, xN = R, run = 0.0f;
   double tL = B->time[q], tN = B->time[p];
   for (; k < p; ++k) {
     const float v = B->ipos[k];
-    if (!(v >= 0.0f)) continue;
+    if (!(v >= run)) continue; /* unplaced, or behind an earlier anchor: no anchor */
     if (!(v <= x)) break;
     iL = k;
     xL = v;
     tL = B->time[k];
+    run = v;
   }
   for (; k < p; ++k)
-    if (B->ipos[k] >= 0.0f) {
+    if (B->ipos[k] >= run) {
       xN = B->ipos[k];
       tN = B->time[k];
       break;

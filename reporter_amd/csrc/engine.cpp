@@ -456,7 +456,8 @@ void engine_free(otm_engine* E) {
   otm_engine::Buf* bufs[] = {
       &E->in_off,        &E->in_lat,       &E->in_lon,         &E->in_time,        &E->in_acc,     &E->in_blob,
       &E->pt_trace,
-      &E->is_col,        &E->prevc,        &E->gc,             &E->ncand,          &E->cand_edge,
+      &E->is_col,        &E->prevc,        &E->nextc,        &E->gc,             &E->ncand,          &E->cand_eo,      &E->cand_em,
+      &E->cand_xeo,      &E->cand_xem,
       &E->probe,         &E->col_prev,     &E->kq_prev,        &E->trans_off,      &E->trans,          &E->bp,         &E->state,      &E->chosen,
       &E->chain_start,   &E->route_dist,   &E->ipos,   &E->path_off,       &E->path_len,       &E->path_pool,  &E->trace_err,
       &E->overflow_list0, &E->overflow_list, &E->overflow_list2, &E->counters_i32, &E->scan_tmp, &E->snap,   &E->big_key,
@@ -508,9 +509,13 @@ static int engine_match_once(otm_engine* E, const DevBatch& b, hipStream_t s, st
   ENS(pt_trace, Pn * 4);
   ENS(is_col, Pn);
   ENS(prevc, Pn * 4);
+  ENS(nextc, Pn * 4);
   ENS(gc, Pn * 4);
   ENS(ncand, Pn * 4);
-  ENS(cand_edge, Pn * KMAX * 4 * CSTRIDE);  // the interleaved {edge, offset, emission} records
+  ENS(cand_eo, Pn * KIN * 8);  // inline candidate slots {edge, offset bits}
+  ENS(cand_em, Pn * KIN * 4);  //   ... and their emissions
+  ENS(cand_xeo, Pn * KX * 8);  // slots KIN.. (only the wider points touch them)
+  ENS(cand_xem, Pn * KX * 4);
   ENS(probe, Pn * 16);
   ENS(col_prev, Pn * 4);
   ENS(kq_prev, Pn * 4);
@@ -562,12 +567,14 @@ static int engine_match_once(otm_engine* E, const DevBatch& b, hipStream_t s, st
   w.pt_trace = P<int32_t>(E->pt_trace);
   w.is_col = P<uint8_t>(E->is_col);
   w.prevc = P<int32_t>(E->prevc);
+  w.nextc = P<int32_t>(E->nextc);
   w.gc = P<float>(E->gc);
   w.ncand = P<int32_t>(E->ncand);
   w.probe = P<float4>(E->probe);
-  w.cand_edge = P<int32_t>(E->cand_edge);
-  w.cand_off = P<float>(E->cand_edge) + 1;
-  w.cand_emis = P<float>(E->cand_edge) + 2;
+  w.cand_eo = P<int2>(E->cand_eo);
+  w.cand_em = P<float>(E->cand_em);
+  w.cand_xeo = P<int2>(E->cand_xeo);
+  w.cand_xem = P<float>(E->cand_xem);
   w.col_prev = P<int32_t>(E->col_prev);
   w.kq_prev = P<int32_t>(E->kq_prev);
   w.trans_off = P<int64_t>(E->trans_off);
@@ -967,7 +974,8 @@ int engine_debug_fetch(otm_engine* E, int what, void* dst, size_t bytes, size_t*
     case 1:
     case 2:
     case 3: {
-      // word (what - 1) of each interleaved candidate record, as [P*KMAX]
+      // candidate edges (1), offsets (2) or emissions (3) as [P*KMAX], slot
+      // j of point p at p * KMAX + j (inline and overflow slots joined)
       n = Pn * KMAX * 4;
       if (needed) *needed = n;
       if (!dst) return OTM_OK;
@@ -975,9 +983,21 @@ int engine_debug_fetch(otm_engine* E, int what, void* dst, size_t bytes, size_t*
         *err = "debug buffer too small";
         return OTM_EINVAL;
       }
-      const char* base = (const char*)E->cand_edge.p + 4 * (what - 1);
-      if (n) HIPCHK(hipMemcpy2DAsync(dst, 4, base, 4 * CSTRIDE, 4, Pn * KMAX, hipMemcpyDeviceToHost, E->stream));
+      if (!n) return OTM_OK;
+      const bool rec = what != 3;
+      std::vector<char> in(Pn * KIN * (rec ? 8 : 4)), ov(Pn * KX * (rec ? 8 : 4));
+      HIPCHK(hipMemcpyAsync(in.data(), rec ? E->cand_eo.p : E->cand_em.p, in.size(), hipMemcpyDeviceToHost,
+                            E->stream));
+      HIPCHK(hipMemcpyAsync(ov.data(), rec ? E->cand_xeo.p : E->cand_xem.p, ov.size(), hipMemcpyDeviceToHost,
+                            E->stream));
       HIPCHK(hipStreamSynchronize(E->stream));
+      int32_t* d = (int32_t*)dst;
+      for (size_t p = 0; p < Pn; ++p)
+        for (int j = 0; j < KMAX; ++j) {
+          const int32_t* src = j < KIN ? (const int32_t*)in.data() + (rec ? 2 : 1) * (p * KIN + j)
+                                       : (const int32_t*)ov.data() + (rec ? 2 : 1) * (p * KX + (j - KIN));
+          d[p * KMAX + j] = rec ? src[what - 1] : src[0];
+        }
       return OTM_OK;
     }
     case 4: src = E->trans_off.p; n = (Pn + 1) * 8; break;

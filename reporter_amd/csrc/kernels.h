@@ -20,7 +20,8 @@
 namespace otm {
 
 constexpr int KMAX = 32;           // max candidates per column (== ORC_KMAX)
-constexpr int CSTRIDE = 3;         // words per candidate record (DevWork::cand_*)
+constexpr int KIN = 8;             // inline candidate slots per point (DevWork::cand_eo / cand_em)
+constexpr int KX = KMAX - KIN;     // overflow candidate slots per point (DevWork::cand_xeo / cand_xem)
 constexpr int MAX_HITS = 256;      // distinct edges within one radius (spec limit)
 constexpr int SEARCH_LIMIT = 24576;  // nodes settled by one search (spec limit)
 constexpr int LDS_TABLE_CAP = 256;   // K4/K6 LDS tier: table slots
@@ -137,16 +138,20 @@ struct DevCounters {
 struct DevWork {
   int32_t* pt_trace;     // [P] trace of point
   uint8_t* is_col;       // [P]
-  int32_t* prevc;        // [P] previous column (unlinked), -1
+  int32_t* prevc;        // [P] column: previous column (unlinked), -1; other points: the column before them
+  int32_t* nextc;        // [P] column q: its next column p when interpolated points lie between (K3), else -1
   float* gc;             // [P]
   int32_t* ncand;        // [P]
   float4* probe;         // [P] {lat, lon, accuracy, 0}: a probe's inputs in one line (K1)
-  // one interleaved record per candidate slot, {edge, offset, emission}
-  // (12 B): slot j of point p is element CSTRIDE * (p * KMAX + j) of each
-  // view, so a point's candidates share cache lines across the three
-  int32_t* cand_edge;    // [P*KMAX*3], view at word 0
-  float* cand_off;       // view at word 1
-  float* cand_emis;      // view at word 2
+  // Candidates of point p, slot j: the first KIN slots
+  // inline -- {edge, offset bits} at cand_eo[p * KIN + j] (two points per
+  // 128-B line) and the emission at cand_em[p * KIN + j] (four points per
+  // line); slots KIN.. of the rare wider points at cand_xeo / cand_xem[p * KX
+  // + j - KIN] (untouched lines for every other point)
+  int2* cand_eo;         // [P*KIN]
+  float* cand_em;        // [P*KIN]
+  int2* cand_xeo;        // [P*KX]
+  float* cand_xem;       // [P*KX]
   int32_t* col_prev;     // [P] linked previous column, -1
   int32_t* kq_prev;      // [P] candidates of the linked previous column (K3), so K4 reads them with p's own words
   int64_t* trans_off;    // [P+1]

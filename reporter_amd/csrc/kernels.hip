@@ -132,6 +132,23 @@ __device__ __forceinline__ void cadd(unsigned long long* c, unsigned long long v
   if (c && v) atomicAdd(c, v);
 }
 
+// candidate slot j of point p (DevWork: KIN inline slots, the rest overflow)
+__device__ __forceinline__ int2 crec(const DevWork& w, int64_t p, int j) {
+  return j < KIN ? w.cand_eo[p * KIN + j] : w.cand_xeo[p * KX + (j - KIN)];
+}
+__device__ __forceinline__ float cemis(const DevWork& w, int64_t p, int j) {
+  return j < KIN ? w.cand_em[p * KIN + j] : w.cand_xem[p * KX + (j - KIN)];
+}
+__device__ __forceinline__ void cput(const DevWork& w, int64_t p, int j, int32_t e, float off, float em) {
+  if (j < KIN) {
+    w.cand_eo[p * KIN + j] = make_int2(e, __float_as_int(off));
+    w.cand_em[p * KIN + j] = em;
+  } else {
+    w.cand_xeo[p * KX + (j - KIN)] = make_int2(e, __float_as_int(off));
+    w.cand_xem[p * KX + (j - KIN)] = em;
+  }
+}
+
 // ============================================================== turn costs
 // deviation from straight on (0..180 degrees) of the turn from an edge whose
 // end heading is hin into an edge whose start heading is hout
@@ -350,7 +367,7 @@ __global__ __launch_bounds__(TB) void k_columns(DevGraph g, DevBatch b, DevParam
           const bool col = last < 0 || gcv >= P.interp;
           w.is_col[p] = col ? 1 : 0;
           w.gc[p] = col ? gcv : 0.0f;
-          w.prevc[p] = col ? (int32_t)last : -1;
+          w.prevc[p] = (int32_t)last;  // a non-column: the column before it (K7a)
           if (col) {
             last = p;
             ++ncols;
@@ -368,6 +385,7 @@ __global__ __launch_bounds__(TB) void k_columns(DevGraph g, DevBatch b, DevParam
         w.ncand[p] = 0;
         w.route_dist[p] = 0.0f;
         w.ipos[p] = -1.0f;
+        w.nextc[p] = -1;
         w.path_len[p] = 0;
         w.path_off[p] = 0;
       }
@@ -400,7 +418,7 @@ __global__ __launch_bounds__(TB) void k_columns(DevGraph g, DevBatch b, DevParam
           const bool col = last < 0 || gcv >= P.interp;
           sCol[pl] = col ? 1 : 0;
           sGc[pl] = col ? gcv : 0.0f;
-          sPrev[pl] = col && last >= 0 ? (int32_t)(a + last) : -1;
+          sPrev[pl] = last >= 0 ? (int32_t)(a + last) : -1;  // a non-column: the column before it (K7a)
           if (col) {
             last = pl;
             ++ncols;
@@ -423,6 +441,7 @@ __global__ __launch_bounds__(TB) void k_columns(DevGraph g, DevBatch b, DevParam
           w.ncand[p] = 0;
           w.route_dist[p] = 0.0f;
           w.ipos[p] = -1.0f;
+          w.nextc[p] = -1;
           w.path_len[p] = 0;
           w.path_off[p] = 0;
         }
@@ -664,9 +683,7 @@ __global__ __launch_bounds__(CAND_TB, OTM_CAND_WAVES) void k_cand_lane(DevGraph 
       const int32_t e = (int32_t)((em & ~NODE_ENT) >> 4);
       float sqd = qm, off = 0.0f;
       if (!(em & NODE_ENT)) project(g, e, (int32_t)(em & 15u), lat, lon, ls, sqd, off);
-      w.cand_edge[CSTRIDE * (p * KMAX + j)] = e;
-      w.cand_off[CSTRIDE * (p * KMAX + j)] = off;
-      w.cand_emis[CSTRIDE * (p * KMAX + j)] = sqd / ds;
+      cput(w, p, j, e, off, sqd / ds);
     }
 
     w.ncand[p] = K;
@@ -870,9 +887,7 @@ __global__ __launch_bounds__(TB) void k_candidates(DevGraph g, DevBatch b, DevPa
       float sqd = bitsf((uint32_t)(key >> 32)), off = 0.0f;
       if (key & 1ull) project(g, e, (int32_t)((key >> 1) & 15ull), lat, lon, ls, sqd, off);
       const float ds = (2.0f * P.sigma_z) * P.sigma_z;
-      w.cand_edge[CSTRIDE * (p * KMAX + lane)] = e;
-      w.cand_off[CSTRIDE * (p * KMAX + lane)] = off;
-      w.cand_emis[CSTRIDE * (p * KMAX + lane)] = sqd / ds;
+      cput(w, p, lane, e, off, sqd / ds);
     }
     if (lane == 0) {
       w.ncand[p] = K;
@@ -901,6 +916,7 @@ __global__ __launch_bounds__(256) void k_links(DevBatch b, DevParams P, DevWork 
   int64_t cnt = 0;
   if (w.is_col[p]) {
     const int32_t q = w.prevc[p];
+    if (q >= 0 && p - q > 1) w.nextc[q] = (int32_t)p;  // interpolated points between: K7a finds p from them
     if (q >= 0 && w.ncand[p] > 0 && w.ncand[q] > 0 && w.gc[p] <= P.breakage) {
       cp = q;
       kq = w.ncand[q];
@@ -1206,19 +1222,15 @@ __global__ __launch_bounds__(LANE_TB) void k_trans_lane(DevGraph g, DevBatch b, 
     const int Kq = w.ncand[q], Kp = w.ncand[p];
     const float gcv = w.gc[p];
     const float bound = P.factor * gcv;
-    // this point's and the previous column's candidate records (CSTRIDE words apart)
-    const int32_t* eq = w.cand_edge + CSTRIDE * ((int64_t)q * KMAX);
-    const float* oq = w.cand_off + CSTRIDE * ((int64_t)q * KMAX);
-    const int32_t* ep = w.cand_edge + CSTRIDE * (p * KMAX);
-    const float* op = w.cand_off + CSTRIDE * (p * KMAX);
     float* Tm = w.trans + w.trans_off[p];
     unsigned long long s_search = 0, s_settled = 0, s_relaxed = 0, s_trans = 0;
     bool failed = false;
     for (int i = 0; i < Kq && !failed; ++i) {
-      const int32_t u = src_node(g, eq[CSTRIDE * (i)], oq[CSTRIDE * (i)]);
+      const int2 ri = crec(w, q, i);
+      const int32_t u = src_node(g, ri.x, __int_as_float(ri.y));
       bool first = true;
       for (int k = 0; k < i; ++k)
-        if (src_node(g, eq[CSTRIDE * (k)], oq[CSTRIDE * (k)]) == u) {
+        if (const int2 rk = crec(w, q, k); src_node(g, rk.x, __int_as_float(rk.y)) == u) {
           first = false;
           break;
         }
@@ -1233,17 +1245,21 @@ __global__ __launch_bounds__(LANE_TB) void k_trans_lane(DevGraph g, DevBatch b, 
       s_settled += (unsigned long long)n;
       s_relaxed += rel;
       for (int ii = i; ii < Kq; ++ii) {
-        if (src_node(g, eq[CSTRIDE * (ii)], oq[CSTRIDE * (ii)]) != u) continue;
-        const int32_t ei = eq[CSTRIDE * (ii)];
-        const float start = src_start(g, ei, oq[CSTRIDE * (ii)]);
+        const int2 rii = crec(w, q, ii);
+        const int32_t ei = rii.x;
+        const float oi = __int_as_float(rii.y);
+        if (src_node(g, ei, oi) != u) continue;
+        const float start = src_start(g, ei, oi);
         for (int j = 0; j < Kp; ++j) {
-          const int32_t ej = ep[CSTRIDE * (j)];
+          const int2 rj = crec(w, p, j);
+          const int32_t ej = rj.x;
+          const float oj = __int_as_float(rj.y);
           float r;
           bool ok = true;
           int f = -1;
-          const bool same = ej == ei && op[CSTRIDE * (j)] >= oq[CSTRIDE * (ii)];
+          const bool same = ej == ei && oj >= oi;
           if (same) {
-            r = op[CSTRIDE * (j)] - oq[CSTRIDE * (ii)];
+            r = oj - oi;
           } else {
             f = lane_find<CAP>(K, n, (uint32_t)g.e_from[ej]);
             if (f < 0) {
@@ -1251,7 +1267,7 @@ __global__ __launch_bounds__(LANE_TB) void k_trans_lane(DevGraph g, DevBatch b, 
               r = 0.0f;
             } else {
               const float sd = start + D[f * LANE_TB];
-              r = sd + op[CSTRIDE * (j)];
+              r = sd + oj;
             }
           }
           float cost = INFINITY;
@@ -1259,14 +1275,14 @@ __global__ __launch_bounds__(LANE_TB) void k_trans_lane(DevGraph g, DevBatch b, 
             // the route's turns, walked back from e_j's start node to u
             uint32_t units = 0;
             if (!same) {
-              uint32_t hn = dst_head(g, ej, op[CSTRIDE * (j)]);
+              uint32_t hn = dst_head(g, ej, oj);
               while ((K[f * LANE_TB] & ~DONE) != (uint32_t)u) {
                 const int32_t e = Pd[f * LANE_TB];
                 units += turn_units(P.turn_units, g.e_head_in[e], hn);
                 hn = g.e_head_out[e];
                 f = lane_find<CAP>(K, n, (uint32_t)g.e_from[e]);
               }
-              units += turn_units(P.turn_units, src_head(g, ei, oq[CSTRIDE * (ii)]), hn);
+              units += turn_units(P.turn_units, src_head(g, ei, oi), hn);
             }
             cost = trans_cost(units, r, gcv, P.beta);
             ++s_trans;
@@ -1312,9 +1328,9 @@ __global__ __launch_bounds__(LANE_TB) void k_route_lane(DevGraph g, DevBatch b, 
   for (int64_t it = (int64_t)blockIdx.x * LANE_TB + threadIdx.x; it < nwork; it += (int64_t)gridDim.x * LANE_TB) {
     const int64_t p = w.overflow_list0[it];
     const int32_t q = w.col_prev[p];
-    const int i = w.state[q], j = w.state[p];
-    const int32_t ei = w.cand_edge[CSTRIDE * ((int64_t)q * KMAX + i)], ej = w.cand_edge[CSTRIDE * (p * KMAX + j)];
-    const float oi = w.cand_off[CSTRIDE * ((int64_t)q * KMAX + i)], oj = w.cand_off[CSTRIDE * (p * KMAX + j)];
+    const int2 ci = w.chosen[q], cj = w.chosen[p];
+    const int32_t ei = ci.x, ej = cj.x;
+    const float oi = __int_as_float(ci.y), oj = __int_as_float(cj.y);
     const float bound = P.factor * w.gc[p];
     const int32_t u = src_node(g, ei, oi), v = g.e_from[ej];
     unsigned long long rel = 0;
@@ -1576,13 +1592,15 @@ __global__ __launch_bounds__(TB, 8) void k_trans_sub(DevGraph g, DevBatch b, Dev
     // candidates of p (targets) and of q (sources), then edges, then rows
     for (int k = sl; k < KC; k += S) {
       if (act && k < Kp) {
-        const int32_t e = w.cand_edge[CSTRIDE * (p * KMAX + k)];
-        const float o = w.cand_off[CSTRIDE * (p * KMAX + k)];
+        const int2 c = crec(w, p, k);
+        const int32_t e = c.x;
+        const float o = __int_as_float(c.y);
         tg[sg][k] = make_int4(e, __float_as_int(o), g.e_from[e], (int)dst_head(g, e, o));
       }
       if (act && k < Kq) {
-        const int32_t e = w.cand_edge[CSTRIDE * ((int64_t)q * KMAX + k)];
-        const float o = w.cand_off[CSTRIDE * ((int64_t)q * KMAX + k)];
+        const int2 c = crec(w, q, k);
+        const int32_t e = c.x;
+        const float o = __int_as_float(c.y);
         sr[sg][k] = make_int4(e, __float_as_int(o), __float_as_int(src_start(g, e, o)), (int)src_head(g, e, o));
         if (idx_ok) {
           // erow[e]: the row of e's end node; erow[E + e]: of its start node
@@ -1837,12 +1855,14 @@ __global__ __launch_bounds__(TB) void k_transitions(DevGraph g, DevBatch b, DevP
     const float gcv = w.gc[p];
     const float bound = P.factor * gcv;
     if (lane < Kq) {
-      eq[lane] = w.cand_edge[CSTRIDE * ((int64_t)q * KMAX + lane)];
-      oq[lane] = w.cand_off[CSTRIDE * ((int64_t)q * KMAX + lane)];
+      const int2 c = crec(w, q, lane);
+      eq[lane] = c.x;
+      oq[lane] = __int_as_float(c.y);
     }
     if (lane < Kp) {
-      ep[lane] = w.cand_edge[CSTRIDE * (p * KMAX + lane)];
-      op[lane] = w.cand_off[CSTRIDE * (p * KMAX + lane)];
+      const int2 c = crec(w, p, lane);
+      ep[lane] = c.x;
+      op[lane] = __int_as_float(c.y);
     }
     __syncthreads();
     // distinct source nodes (first occurrence order)
@@ -1970,8 +1990,7 @@ __device__ void viterbi_trace_global(int64_t a, int64_t e, DevWork& w) {
         int jj = bi;
         while (true) {
           w.state[pp] = jj;
-          w.chosen[pp] = make_int2(w.cand_edge[CSTRIDE * (pp * KMAX + jj)],
-                                   __float_as_int(w.cand_off[CSTRIDE * (pp * KMAX + jj)]));
+          w.chosen[pp] = crec(w, pp, jj);
           if (w.chain_start[pp]) break;
           jj = w.bp[pp * KMAX + jj];
           pp = w.col_prev[pp];
@@ -2005,7 +2024,7 @@ __device__ void viterbi_trace_global(int64_t a, int64_t e, DevWork& w) {
         }
         const bool alive = lane < Kp && bi >= 0;
         if (lane < Kp) {
-          cur = alive ? best + w.cand_emis[CSTRIDE * (p * KMAX + lane)] : INFINITY;
+          cur = alive ? best + cemis(w, p, lane) : INFINITY;
           w.bp[p * KMAX + lane] = alive ? (uint8_t)bi : (uint8_t)0xFF;
         }
         if (__ballot(alive) == 0ull) {
@@ -2017,7 +2036,7 @@ __device__ void viterbi_trace_global(int64_t a, int64_t e, DevWork& w) {
         backtrack(last);
       }
       if (!started) {
-        cur = lane < Kp ? w.cand_emis[CSTRIDE * (p * KMAX + lane)] : INFINITY;
+        cur = lane < Kp ? cemis(w, p, lane) : INFINITY;
         if (lane == 0) w.chain_start[p] = 1;
       }
       prev = cur;
@@ -2226,11 +2245,23 @@ __global__ __launch_bounds__(TB, OTM_VIT_WAVES) void k_viterbi(DevBatch b, DevWo
               kq = sKc[q];
               eq = sEoff[q] - we0;
             }
-            for (int j0 = 0; __ballot(j0 < kq) != 0ull; j0 += 4) {
+            // the inline slots as two 16-byte loads of the point's 32-byte
+            // block (consecutive lanes: consecutive blocks), the rest (points
+            // with more than KIN candidates) from the overflow slots
+            if (kq > 0) {
+              const float4* e4 = (const float4*)(w.cand_em + (a + q) * KIN);
+              const float4 x0 = e4[0];
+              const float4 x1 = kq > 4 ? e4[1] : x0;
+              const float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+#pragma unroll
+              for (int u = 0; u < 8; ++u)
+                if (u < kq) sEm[eq + u] = v[u];
+            }
+            for (int j0 = KIN; __ballot(j0 < kq) != 0ull; j0 += 4) {
               float v[4];
 #pragma unroll
               for (int u = 0; u < 4; ++u)
-                v[u] = j0 + u < kq ? w.cand_emis[CSTRIDE * ((a + q) * KMAX + j0 + u)] : 0.0f;
+                v[u] = j0 + u < kq ? w.cand_xem[(a + q) * KX + (j0 - KIN + u)] : 0.0f;
 #pragma unroll
               for (int u = 0; u < 4; ++u)
                 if (j0 + u < kq) sEm[eq + j0 + u] = v[u];
@@ -2305,8 +2336,7 @@ __global__ __launch_bounds__(TB, OTM_VIT_WAVES) void k_viterbi(DevBatch b, DevWo
       w.chain_start[a + pl] = (uint8_t)cs;
       // the chosen candidate, compact for the route and segment stages
       if (st >= 0) {
-        const int64_t r = CSTRIDE * ((a + pl) * KMAX + st);
-        w.chosen[a + pl] = make_int2(w.cand_edge[r], __float_as_int(w.cand_off[r]));
+        w.chosen[a + pl] = crec(w, a + pl, st);
       }
     }
     __syncthreads();
@@ -2339,8 +2369,9 @@ __global__ __launch_bounds__(TB) void k_route(DevGraph g, DevBatch b, DevParams 
     const int64_t p = (int64_t)list[it];
     const int32_t q = w.col_prev[p];
     const int i = w.state[q], j = w.state[p];
-    const int32_t ei = w.cand_edge[CSTRIDE * ((int64_t)q * KMAX + i)], ej = w.cand_edge[CSTRIDE * (p * KMAX + j)];
-    const float oi = w.cand_off[CSTRIDE * ((int64_t)q * KMAX + i)], oj = w.cand_off[CSTRIDE * (p * KMAX + j)];
+    const int2 ci = crec(w, q, i), cj = crec(w, p, j);
+    const int32_t ei = ci.x, ej = cj.x;
+    const float oi = __int_as_float(ci.y), oj = __int_as_float(cj.y);
     if (ei == ej && oj >= oi) {
       if (lane == 0) w.route_dist[p] = oj - oi;
       continue;
@@ -2531,19 +2562,20 @@ __device__ __forceinline__ void step_bound(const DevBatch& b, const DevWork& w, 
     return;
   }
   int iL = lp, k = lp + 1;
-  float xL = 0.0f, xN = R;
+  float xL = 0.0f, xN = R, run = 0.0f;
   double tL = ta, tN = tb;
   for (; k < pl; ++k) {
     const float v = w.ipos[a + k];
-    if (!(v >= 0.0f)) continue;
+    if (!(v >= run)) continue;  // unplaced, or behind an earlier anchor: no anchor
     if (!(v <= x)) break;
     iL = k;
     xL = v;
     tL = b.time[a + k];
+    run = v;
   }
   for (; k < pl; ++k) {
     const float v = w.ipos[a + k];
-    if (v >= 0.0f) {
+    if (v >= run) {
       xN = v;
       tN = b.time[a + k];
       break;
@@ -2569,8 +2601,8 @@ struct SegSrcGlobal {
   __device__ float rd(int pl) const { return w->route_dist[a + pl]; }
   __device__ int32_t poff(int pl) const { return w->path_off[a + pl]; }
   __device__ int32_t plen(int pl) const { return w->path_len[a + pl]; }
-  __device__ int32_t edge(int pl) const { return w->cand_edge[CSTRIDE * ((a + pl) * KMAX + w->state[a + pl])]; }
-  __device__ float off(int pl) const { return w->cand_off[CSTRIDE * ((a + pl) * KMAX + w->state[a + pl])]; }
+  __device__ int32_t edge(int pl) const { return w->chosen[a + pl].x; }
+  __device__ float off(int pl) const { return __int_as_float(w->chosen[a + pl].y); }
   __device__ EAttr attr(int pl) const { return edge_attr(*g, edge(pl)); }
 };
 
@@ -3233,47 +3265,21 @@ __global__ __launch_bounds__(TB) void k_report_wave(DevBatch b, DevReportCfg rc,
 }
 
 // ============================================================== segment bound / compaction
-// K7a, interpolated points (DESIGN.md §3 rule 7, oracle interp_step): the
-// points between the two states of a step that leaves its edge are placed on
-// the step's route -- on each route piece (the rest of q's edge, the path's
-// edges, p's edge up to p) the point's best projection onto the piece's edge,
+// K7a, interpolated points (DESIGN.md §3 rule 7, oracle interp_pos): a point
+// k between the two states q < k < p of a step that leaves its edge is placed
+// on the step's route -- on each route piece (the rest of q's edge, the path's
+// edges, p's edge up to p) its best projection onto the piece's edge,
 // admissible inside the piece, costed sqdist / (2 sigma_z^2) + |pos - gc(q, k)|
-// / beta; the cheapest wins, and a point behind the step's running maximum
-// stays unplaced (-1).  One thread per step, serial over its points: steps
-// with interpolated points are rare at the benchmark configs (5 s and 30 s
-// sampling) and short at any.
+// / beta; the cheapest wins (-1: none).  One thread per interpolated point
+// (its step from prevc / nextc); the monotone filter (a point behind the
+// step's running maximum is no anchor) is applied where the anchors are read
+// (step_bound).
 struct RoutePiece {
   int32_t edge;
   float o0, o1, xs;
 };
-__device__ __forceinline__ RoutePiece route_piece(const DevGraph& g, const DevWork& w, int m, bool has0, int32_t ei,
-                                                  float oi, int32_t ej, float oj, int32_t poff, int32_t plen,
-                                                  float start, float& dd) {
-  RoutePiece r;
-  if (has0 && m == 0) {
-    r.edge = ei;
-    r.o0 = oi;
-    r.o1 = g.e_len[ei];
-    r.xs = 0.0f;
-    return r;
-  }
-  const int k = m - (has0 ? 1 : 0);
-  if (k < plen) {
-    r.edge = w.path_pool[poff + k];
-    r.o0 = 0.0f;
-    r.o1 = g.e_len[r.edge];
-    r.xs = start + dd;
-    dd = dd + r.o1;
-    return r;
-  }
-  r.edge = ej;
-  r.o0 = 0.0f;
-  r.o1 = oj;
-  r.xs = start + dd;
-  return r;
-}
-__device__ void interp_step(const DevGraph& g, const DevBatch& b, const DevParams& P, DevWork& w, int64_t q,
-                            int64_t p) {
+__device__ float interp_pos(const DevGraph& g, const DevBatch& b, const DevParams& P, const DevWork& w, int64_t q,
+                            int64_t p, int64_t k) {
   const int2 ci = w.chosen[q], cj = w.chosen[p];
   const int32_t ei = ci.x, ej = cj.x;
   const float oi = __int_as_float(ci.y), oj = __int_as_float(cj.y);
@@ -3282,63 +3288,73 @@ __device__ void interp_step(const DevGraph& g, const DevBatch& b, const DevParam
   const int npc = (has0 ? 1 : 0) + plen + (cand_node(oj) ? 0 : 1);
   const float start = src_start(g, ei, oi);
   const float ds = (2.0f * P.sigma_z) * P.sigma_z;
-  const float qlat = b.lat[q], qlon = b.lon[q];
-  float run = 0.0f;
-  for (int64_t k = q + 1; k < p; ++k) {
-    const float lat = b.lat[k], lon = b.lon[k];
-    const float ls = MPD_F * cos_deg(lat);
-    const float gcd = gc_dist(qlat, qlon, lat, lon);
-    float best = INFINITY, bpos = -1.0f, dd = 0.0f;
-    for (int m = 0; m < npc; ++m) {
-      const RoutePiece pc = route_piece(g, w, m, has0, ei, oi, ej, oj, poff, plen, start, dd);
-      const int nsh = g.e_shape_off[pc.edge + 1] - g.e_shape_off[pc.edge] - 1;
-      float bsq = INFINITY, boff = 0.0f;
-      for (int sg = 0; sg < nsh; ++sg) {
-        float sqd, off;
-        project(g, pc.edge, sg, lat, lon, ls, sqd, off);
-        if (sqd < bsq) {
-          bsq = sqd;
-          boff = off;
-        }
-      }
-      if (!(boff >= pc.o0 && boff <= pc.o1)) continue;
-      const float pos = pc.xs + (boff - pc.o0);
-      const float cost = bsq / ds + fabsf(pos - gcd) / P.beta;
-      if (cost < best) {
-        best = cost;
-        bpos = pos;
+  const float lat = b.lat[k], lon = b.lon[k];
+  const float ls = MPD_F * cos_deg(lat);
+  const float gcd = gc_dist(b.lat[q], b.lon[q], lat, lon);
+  float best = INFINITY, bpos = -1.0f, dd = 0.0f;
+  for (int m = 0; m < npc; ++m) {
+    RoutePiece pc;
+    const int pk = m - (has0 ? 1 : 0);
+    if (has0 && m == 0) {
+      pc = RoutePiece{ei, oi, g.e_len[ei], 0.0f};
+    } else if (pk < plen) {
+      const int32_t e = w.path_pool[poff + pk];
+      const float len = g.e_len[e];
+      pc = RoutePiece{e, 0.0f, len, start + dd};
+      dd = dd + len;
+    } else {
+      pc = RoutePiece{ej, 0.0f, oj, start + dd};
+    }
+    const int32_t s0 = g.e_shape_off[pc.edge], nsh = g.e_shape_off[pc.edge + 1] - s0 - 1;
+    float bsq = INFINITY, boff = 0.0f;
+    for (int sg = 0; sg < nsh; ++sg) {
+      float sqd, off;
+      project(g, pc.edge, sg, lat, lon, ls, sqd, off);
+      if (sqd < bsq) {
+        bsq = sqd;
+        boff = off;
       }
     }
-    if (bpos >= 0.0f && bpos >= run) {
-      w.ipos[k] = bpos;
-      run = bpos;
-    } else {
-      w.ipos[k] = -1.0f;
+    if (!(boff >= pc.o0 && boff <= pc.o1)) continue;
+    const float pos = pc.xs + (boff - pc.o0);
+    const float cost = bsq / ds + fabsf(pos - gcd) / P.beta;
+    if (cost < best) {
+      best = cost;
+      bpos = pos;
     }
   }
+  return bpos;
 }
 
 // Traversals a matched point can add: the close of the open traversal, its
 // route's path edges, the re-open (+ the chain's final close): <= 2 + path.
-// The same thread places the interpolated points of its step (K7a).
+// An interpolated point's thread places it instead (K7a).
 __global__ __launch_bounds__(256) void k_seg_bound(DevGraph g, DevBatch b, DevParams P, DevWork w, int64_t* ub) {
-  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   // spill snapshot C: steps per route tier (kept for the status read)
-  if (OTM_FOLD_BOOKKEEPING && p == b.n_points) fold_snap(w, 2, false);
+  if (OTM_FOLD_BOOKKEEPING && k == b.n_points) fold_snap(w, 2, false);
   if (*w.abort) return;  // a capacity was exceeded: the host redoes the batch
-  if (p > b.n_points) return;
+  if (k > b.n_points) return;
   int64_t v = 0;
-  if (p < b.n_points && w.is_col[p] && w.state[p] >= 0) {
-    const int32_t pl = w.path_len[p];
-    v = 2 + (pl > 0 ? pl : 0);
-    const int32_t q = w.col_prev[p];
-    if (q >= 0 && p - q > 1 && !w.chain_start[p] && pl >= 0 && w.trace_err[w.pt_trace[p]] == 0) {
-      const int2 ci = w.chosen[q], cj = w.chosen[p];
-      // a step that stays on its edge has no boundary inside it
-      if (!(ci.x == cj.x && __int_as_float(cj.y) >= __int_as_float(ci.y))) interp_step(g, b, P, w, q, p);
+  if (k < b.n_points) {
+    if (w.is_col[k]) {
+      if (w.state[k] >= 0) {
+        const int32_t pl = w.path_len[k];
+        v = 2 + (pl > 0 ? pl : 0);
+      }
+    } else {
+      // the step q -> p around this point: linked, matched, leaving q's edge
+      const int32_t q = w.prevc[k];
+      const int32_t p = q >= 0 ? w.nextc[q] : -1;
+      if (p >= 0 && w.col_prev[p] == q && !w.chain_start[p] && w.state[p] >= 0 && w.path_len[p] >= 0 &&
+          w.trace_err[w.pt_trace[k]] == 0) {
+        const int2 ci = w.chosen[q], cj = w.chosen[p];
+        if (!(ci.x == cj.x && __int_as_float(cj.y) >= __int_as_float(ci.y)))
+          w.ipos[k] = interp_pos(g, b, P, w, q, p, k);
+      }
     }
   }
-  ub[p] = v;
+  ub[k] = v;
 }
 
 // One wavefront per trace: copy its segments (way offsets rebased), way ids

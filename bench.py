@@ -98,6 +98,8 @@ def parse():
                     help="PMC traffic summary (scripts/pmc_summary.py); default: the committed one for --config")
     ap.add_argument("--json-calls", type=int, default=5,
                     help="calls of the JSON leg (otm_report_batch over the batch's request bodies; 0: skip)")
+    ap.add_argument("--async-rounds", type=int, default=5,
+                    help="JSON async leg: submissions of the batch's request bodies in a row (0: skip)")
     ap.add_argument("--single-requests", type=int, default=300,
                     help="otm_report calls one at a time for the single-request latency (0: skip)")
     ap.add_argument("--stagger-ms", type=float, default=0.0,
@@ -451,7 +453,56 @@ def main():
                       "p99_ms": float(np.percentile(lat_ms, 99)), "points_per_request": P // max(nb, 1),
                       "includes": "otm_report through ctypes: parse, one GPU batch of one trace (H2D, kernels, "
                                   "one sync, D2H), report() and the response body"}
+        # async leg: the same bodies through otm_submit_batch / otm_poll,
+        # args.async_rounds submissions of the batch's 10k requests in a row
+        # (the pipeline: batches on two contexts, parse / writing of one over
+        # another's GPU work), results polled as they come; sustained rate
+        json_async = None
+        if args.async_rounds > 0:
+            rdt = np.dtype([("tag", "<u8"), ("code", "<i4"), ("pad", "<i4"), ("body", "<u8"), ("len", "<u8")])
+            assert C.sizeof(_lib.Result) == rdt.itemsize
+            cap = 1 << 16
+            rbuf = (_lib.Result * cap)()
+            tag_arrs = [(C.c_uint64 * nb)(*range(r * nb, (r + 1) * nb)) for r in range(args.async_rounds)]
+
+            def async_run():
+                total = nb * args.async_rounds
+                parts = []
+                got = 0
+                ta = time.perf_counter()
+                for r in range(args.async_rounds):
+                    if L.otm_submit_batch(eng.h, nb, arr, lens, tag_arrs[r]) != 0:
+                        raise RuntimeError("otm_submit_batch: %s" % _lib.last_error())
+                    n = L.otm_poll(eng.h, rbuf, cap, 0)
+                    if n > 0:
+                        parts.append(np.frombuffer(rbuf, dtype=rdt, count=n).copy())
+                        got += n
+                while got < total:
+                    n = L.otm_poll(eng.h, rbuf, cap, 200000)
+                    if n < 0:
+                        raise RuntimeError("otm_poll: %s" % _lib.last_error())
+                    if n > 0:
+                        parts.append(np.frombuffer(rbuf, dtype=rdt, count=n).copy())
+                        got += n
+                ta = time.perf_counter() - ta
+                return ta, np.concatenate(parts)
+
+            async_run()  # warm: the pipeline's clone and its buffers
+            ta, rr = async_run()
+            in_order = bool((np.diff(rr["tag"].astype(np.int64)) == 1).all())
+            same = all(rr["code"][i] == gpu_resp[i][0] and C.string_at(int(rr["body"][i]), int(rr["len"][i])) ==
+                       gpu_resp[i][1] for i in range(len(gpu_resp)))
+            for pb in rr["body"]:
+                L.otm_free(C.c_void_p(int(pb)))
+            json_async = {"value": P * args.async_rounds / ta, "unit": "points/s", "requests": int(len(rr)),
+                          "seconds": ta, "results_in_submit_order": in_order,
+                          "first_responses_byte_equal_to_json_report": bool(same),
+                          "includes": "otm_submit_batch of the 10k Java request bodies x %d in a row (copies into the "
+                                      "queue), otm_poll until every response is back: the async pipeline, %s "
+                                      "workers on their own batch contexts" %
+                                      (args.async_rounds, os.environ.get("OTM_ASYNC_WORKERS", "2"))}
         json_leg = {"value": P / jel, "unit": "points/s", "ms_per_call": jel * 1e3, "calls": args.json_calls,
+                    "async": json_async,
                     "single_request_latency": single,
                     "requests_per_call": nb, "request_bytes": int(sum(len(x) for x in bodies)),
                     "response_bytes": int(resp_bytes), "status_200": int(sum(1 for i in range(nb) if codes[i] == 200)),

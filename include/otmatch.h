@@ -160,6 +160,13 @@ typedef struct otm_result {
   size_t body_len;
 } otm_result;
 int otm_submit(otm_engine* eng, const char* req, size_t len, uint64_t tag);
+/* n requests at once (a Kafka poll's records): the same as n otm_submit
+ * calls in order, the bodies copied over the library's host threads.  The
+ * async path is a pipeline: each worker runs whole request batches on its
+ * own batch context (OTM_ASYNC_WORKERS, default 2; OTM_ASYNC_BATCH requests
+ * per batch, default 8192), so one batch's parse and response writing overlap
+ * another's GPU work; results are published in submit order. */
+int otm_submit_batch(otm_engine* eng, int n, const char* const* reqs, const size_t* lens, const uint64_t* tags);
 /* Fills up to max results; waits at most timeout_us for the first one.
  * Returns the number filled (>=0) or a negative engine error. */
 int otm_poll(otm_engine* eng, otm_result* out, int max, int timeout_us);

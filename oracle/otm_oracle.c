@@ -138,6 +138,7 @@ void orc_params_default(orc_params* p) {
   p->gps_accuracy = 5.0f;
   p->max_candidates = ORC_KMAX;
   p->turn_penalty_factor = 200.0f;
+  p->turn_aware = 0;
 }
 void orc_report_cfg_default(orc_report_cfg* c) {
   memset(c, 0, sizeof *c);
@@ -390,6 +391,12 @@ typedef struct ws {
   int32_t nlab;
   hit hits[ORC_MAX_HITS + 1];
   seen_set seen;
+  /* turn-aware searches (orc_params.turn_aware): labels per edge */
+  float* ed;
+  uint32_t *eu, *elab, *edone, estamp;
+  int32_t* ep;
+  struct ehn* eheap;
+  size_t ehn_n, ehcap;
 } ws;
 
 static void hpush(ws* w, float d, int32_t n) {
@@ -511,6 +518,7 @@ typedef struct batch {
   int phase;
   orc_counters* ctr; /* per thread */
   int count_unique;  /* count §8(d)'s unique projected edges (keep_stages) */
+  int32_t *in_off, *in_edge; /* in-edge CSR (turn-aware searches only) */
   uint32_t turn_units[181]; /* orc_turn_units per deviation 0..180 */
 } batch;
 
@@ -566,7 +574,173 @@ static uint32_t turn_cost_units(const batch* B, unsigned hin, unsigned hout) {
   return (hin == NO_HEAD || hout == NO_HEAD) ? 0u : B->turn_units[orc_turn_deg(hin, hout)];
 }
 
+/* ------------------------------------------------------------ turn-aware routes (experiment)
+ * SURVEY Appendix B picks a transition's route by "distance
+ * cost plus turn penalty"; the spec picks it by distance alone and adds that
+ * route's turns.  With orc_params.turn_aware the oracle instead runs an
+ * edge-labelled search -- a label per edge, i.e. per (node, incoming edge) --
+ * minimising dist + units / 64 (ties: the smaller distance, then the smaller
+ * edge), so scripts/turn_aware_rate.py can measure how often the two rules
+ * choose different routes, transitions, states and segments.  The GPU
+ * implements the spec only. */
+struct ehn {
+  double c;
+  int32_t e;
+};
+static double ecost(float d, uint32_t u) { return (double)d + (double)u * 0.015625; }
+static void ehpush(ws* w, double c, int32_t e) {
+  if (w->ehn_n == w->ehcap) {
+    w->ehcap = w->ehcap ? w->ehcap * 2 : 1024;
+    w->eheap = (struct ehn*)realloc(w->eheap, w->ehcap * sizeof(struct ehn));
+  }
+  size_t i = w->ehn_n++;
+  while (i > 0) {
+    size_t q = (i - 1) / 2;
+    if (w->eheap[q].c <= c) break;
+    w->eheap[i] = w->eheap[q];
+    i = q;
+  }
+  w->eheap[i].c = c;
+  w->eheap[i].e = e;
+}
+static struct ehn ehpop(ws* w) {
+  struct ehn top = w->eheap[0], last = w->eheap[--w->ehn_n];
+  size_t i = 0;
+  while (1) {
+    size_t c = 2 * i + 1;
+    if (c >= w->ehn_n) break;
+    if (c + 1 < w->ehn_n && w->eheap[c + 1].c < w->eheap[c].c) ++c;
+    if (w->eheap[c].c >= last.c) break;
+    w->eheap[i] = w->eheap[c];
+    i = c;
+  }
+  if (w->ehn_n) w->eheap[i] = last;
+  return top;
+}
+static uint32_t uadd(uint32_t a, uint32_t b) {
+  const uint32_t s = a + b;
+  return s > TURN_UNITS_MAX ? TURN_UNITS_MAX : s;
+}
+static void ta_relax(ws* w, int32_t f, float d, uint32_t un, int32_t pe) {
+  const uint32_t s = w->estamp;
+  const double c = ecost(d, un);
+  if (w->elab[f] != s) {
+    w->elab[f] = s;
+  } else {
+    if (w->edone[f] == s) return;
+    const double oc = ecost(w->ed[f], w->eu[f]);
+    if (!(c < oc || (c == oc && (d < w->ed[f] || (d == w->ed[f] && pe < w->ep[f]))))) return;
+  }
+  w->ed[f] = d;
+  w->eu[f] = un;
+  w->ep[f] = pe;
+  ehpush(w, c, f);
+}
+/* labels of every edge whose route from node u (arriving with heading hin,
+   NO_HEAD for a node candidate) stays within distance `bound` */
+static void ta_search(const batch* B, ws* w, int32_t u, unsigned hin, float bound) {
+  const orc_graph* g = B->g;
+  if (++w->estamp == 0) {
+    memset(w->elab, 0, sizeof(uint32_t) * (size_t)g->h.n_edges);
+    memset(w->edone, 0, sizeof(uint32_t) * (size_t)g->h.n_edges);
+    w->estamp = 1;
+  }
+  const uint32_t s = w->estamp;
+  w->ehn_n = 0;
+  for (int32_t e = g->out_off[u]; e < g->out_off[u + 1]; ++e) {
+    const float d = g->elen[e];
+    if (!(d <= bound)) continue;
+    ta_relax(w, e, d, turn_cost_units(B, hin, g->ehead_out[e]), -1);
+  }
+  while (w->ehn_n) {
+    const struct ehn h = ehpop(w);
+    const int32_t e = h.e;
+    if (w->edone[e] == s || h.c != ecost(w->ed[e], w->eu[e])) continue;
+    w->edone[e] = s;
+    const int32_t v = g->eto[e];
+    for (int32_t f = g->out_off[v]; f < g->out_off[v + 1]; ++f) {
+      const float nd = w->ed[e] + g->elen[f];
+      if (!(nd <= bound)) continue;
+      ta_relax(w, f, nd, uadd(w->eu[e], turn_cost_units(B, g->ehead_in[e], g->ehead_out[f])), e);
+    }
+  }
+}
+/* the cheapest route from the search's source into edge ej (offset oj):
+   returns 0 when none; *last = the route's last edge (-1: the empty route) */
+static int ta_target(const batch* B, const ws* w, int32_t u, unsigned hin, int32_t ej, float oj, float* dist,
+                     uint32_t* units, int32_t* last) {
+  const orc_graph* g = B->g;
+  const int32_t v = g->efrom[ej];
+  const unsigned hout = oj == 0.0f ? NO_HEAD : g->ehead_out[ej];
+  int found = 0;
+  double bc = 0.0;
+  float bd = 0.0f;
+  uint32_t bu = 0;
+  int32_t be = -1;
+  if (v == u) {
+    found = 1;
+    bu = turn_cost_units(B, hin, hout);
+    bc = ecost(0.0f, bu);
+  }
+  for (int32_t k = B->in_off[v]; k < B->in_off[v + 1]; ++k) {
+    const int32_t e = B->in_edge[k];
+    if (w->edone[e] != w->estamp) continue;
+    const uint32_t un = uadd(w->eu[e], turn_cost_units(B, g->ehead_in[e], hout));
+    const double c = ecost(w->ed[e], un);
+    if (!found || c < bc || (c == bc && (w->ed[e] < bd || (w->ed[e] == bd && e < be)))) {
+      found = 1;
+      bc = c;
+      bd = w->ed[e];
+      bu = un;
+      be = e;
+    }
+  }
+  *dist = bd;
+  *units = bu;
+  *last = be;
+  return found;
+}
+static unsigned src_hin(const orc_graph* g, int32_t e, float off) { return off == 0.0f ? NO_HEAD : g->ehead_in[e]; }
+
+static void ta_transitions(batch* B, ws* w, int64_t p) {
+  const orc_graph* g = B->g;
+  const int64_t q = B->col_prev[p];
+  const int Kq = B->ncand[q], Kp = B->ncand[p];
+  const float gcv = B->gc[p];
+  const float bound = B->P->max_route_distance_factor * gcv;
+  float* T = B->trans + B->trans_off[p];
+  const int32_t* eq = B->cand_edge + q * ORC_KMAX;
+  const float* oq = B->cand_off + q * ORC_KMAX;
+  const int32_t* ep = B->cand_edge + p * ORC_KMAX;
+  const float* op = B->cand_off + p * ORC_KMAX;
+  for (int i = 0; i < Kq; ++i) {
+    const int32_t u = src_node(g, eq[i], oq[i]);
+    const unsigned hin = src_hin(g, eq[i], oq[i]);
+    const float start = src_start(g, eq[i], oq[i]);
+    ta_search(B, w, u, hin, bound);
+    for (int j = 0; j < Kp; ++j) {
+      T[i * Kp + j] = INF_F;
+      float r;
+      uint32_t units = 0;
+      if (ep[j] == eq[i] && op[j] >= oq[i]) {
+        r = op[j] - oq[i];
+      } else {
+        float d;
+        int32_t last;
+        if (!ta_target(B, w, u, hin, ep[j], op[j], &d, &units, &last)) continue;
+        const float sd = start + d;
+        r = sd + op[j];
+      }
+      if (r <= bound) T[i * Kp + j] = ((float)units * 0.015625f + fabsf(r - gcv)) / B->P->beta;
+    }
+  }
+}
+
 static int transitions(batch* B, ws* w, int64_t p, orc_counters* C) {
+  if (B->P->turn_aware) {
+    ta_transitions(B, w, p);
+    return 0;
+  }
   const orc_graph* g = B->g;
   const int64_t q = B->col_prev[p];
   const int Kq = B->ncand[q], Kp = B->ncand[p];
@@ -805,6 +979,26 @@ static int route_step(batch* B, ws* w, int64_t p, int32_t* path, int* plen, int*
   }
   *same = 0;
   const float bound = B->P->max_route_distance_factor * B->gc[p];
+  if (B->P->turn_aware) {
+    const int32_t u = src_node(g, ei, oi);
+    const unsigned hin = src_hin(g, ei, oi);
+    ta_search(B, w, u, hin, bound);
+    float d;
+    uint32_t units;
+    int32_t last;
+    if (!ta_target(B, w, u, hin, ej, oj, &d, &units, &last)) return -1;
+    int n = 0;
+    for (int32_t e = last; e >= 0; e = w->ep[e]) path[n++] = e;
+    for (int k = 0; k < n / 2; ++k) {
+      int32_t tmp = path[k];
+      path[k] = path[n - 1 - k];
+      path[n - 1 - k] = tmp;
+    }
+    *plen = n;
+    const float sd = src_start(g, ei, oi) + d;
+    *R = sd + oj;
+    return 0;
+  }
   const int32_t u = src_node(g, ei, oi), v = g->efrom[ej];
   if (dijkstra(g, w, u, bound, C, 1) < 0) return -1;
   int n = 0;
@@ -1148,6 +1342,14 @@ static void* worker(void* arg) {
   w.pred = (int32_t*)malloc(sizeof(int32_t) * nn);
   w.lab = (uint32_t*)calloc(nn, sizeof(uint32_t));
   w.done = (uint32_t*)calloc(nn, sizeof(uint32_t));
+  if (B->P->turn_aware) {
+    const size_t ne = (size_t)B->g->h.n_edges;
+    w.ed = (float*)malloc(sizeof(float) * ne);
+    w.eu = (uint32_t*)malloc(sizeof(uint32_t) * ne);
+    w.ep = (int32_t*)malloc(sizeof(int32_t) * ne);
+    w.elab = (uint32_t*)calloc(ne, sizeof(uint32_t));
+    w.edone = (uint32_t*)calloc(ne, sizeof(uint32_t));
+  }
   orc_counters* C = &B->ctr[A->tid];
   while (1) {
     int t = atomic_fetch_add(&B->next, 1);
@@ -1160,6 +1362,12 @@ static void* worker(void* arg) {
   free(w.lab);
   free(w.done);
   free(w.heap);
+  free(w.ed);
+  free(w.eu);
+  free(w.ep);
+  free(w.elab);
+  free(w.edone);
+  free(w.eheap);
   return NULL;
 }
 
@@ -1202,6 +1410,17 @@ int orc_match_batch(const orc_graph* g, const orc_params* p, const orc_report_cf
   B.time = time;
   B.acc = accuracy;
   B.count_unique = keep_stages;
+  if (p->turn_aware) {
+    const int32_t nn = g->h.n_nodes, ne = g->h.n_edges;
+    B.in_off = (int32_t*)calloc((size_t)nn + 1, 4);
+    B.in_edge = (int32_t*)malloc(sizeof(int32_t) * ((size_t)ne + 1));
+    for (int32_t e = 0; e < ne; ++e) B.in_off[g->eto[e] + 1]++;
+    for (int32_t v = 0; v < nn; ++v) B.in_off[v + 1] += B.in_off[v];
+    int32_t* fill = (int32_t*)malloc(sizeof(int32_t) * ((size_t)nn + 1));
+    memcpy(fill, B.in_off, sizeof(int32_t) * (size_t)nn);
+    for (int32_t e = 0; e < ne; ++e) B.in_edge[fill[g->eto[e]]++] = e;
+    free(fill);
+  }
   for (int d = 0; d <= 180; ++d) B.turn_units[d] = orc_turn_units(p->turn_penalty_factor, d);
   const size_t PP = (size_t)P + 1;
   B.is_col = (uint8_t*)calloc(PP, 1);
@@ -1299,6 +1518,8 @@ int orc_match_batch(const orc_graph* g, const orc_params* p, const orc_report_cf
   }
   free(B.is_col);
   free(B.chain_start);
+  free(B.in_off);
+  free(B.in_edge);
   free(B.terr);
   free(B.res);
   free(B.ctr);

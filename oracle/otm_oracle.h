@@ -35,6 +35,10 @@ typedef struct orc_params {
   float interpolation_distance, search_radius, max_search_radius, gps_accuracy;
   int max_candidates;
   float turn_penalty_factor; /* meili auto costing: 200 (0 = no turn costs) */
+  /* experiment: routes chosen by distance + turn cost with a
+     label per (node, incoming edge) instead of by distance alone; 0 = the
+     spec (what the GPU computes) */
+  int turn_aware;
 } orc_params;
 
 typedef struct orc_report_cfg {

@@ -136,6 +136,7 @@ def _declare(L):
         "otm_report_segments": (C.c_int, [vp, C.c_char_p, sz, C.c_char_p, sz, pp, psz]),
         "otm_submit": (C.c_int, [vp, C.c_char_p, sz, C.c_uint64]),
         "otm_poll": (C.c_int, [vp, C.POINTER(Result), C.c_int, C.c_int]),
+        "otm_submit_batch": (C.c_int, [vp, C.c_int, vp, vp, vp]),
         "otm_encode_request": (C.c_int, [C.c_char_p, C.c_int, vp, vp, vp, vp, pp, psz]),
         "otm_match_soa": (C.c_int, [vp, C.POINTER(Batch), C.POINTER(Results)]),
         "otm_host_alloc": (vp, [sz]),

@@ -496,35 +496,82 @@ void report_many(otm_engine* E, int n, const char* const* reqs, const size_t* le
                  (t2 - t1) - t_extract_ms - t_pack_ms - t_gpu_ms - t_write_ms, t3 - t2, t4 - t3);
 }
 
-void worker_loop(otm_engine* E) {
+// Requests per async batch (OTM_ASYNC_BATCH): small enough that a burst of
+// submissions splits over the pipeline's workers, large enough to fill the GPU.
+size_t async_batch() {
+  const char* e = std::getenv("OTM_ASYNC_BATCH");  // (read per batch: tests switch it)
+  return e ? (size_t)std::max(1, std::atoi(e)) : (size_t)8192;
+}
+// Pipeline depth (OTM_ASYNC_WORKERS, default 2): batch contexts working at
+// once.  A multi-device engine or a clone runs one (its members / parent own
+// the other contexts).
+int async_workers(const otm_engine* E) {
+  if (!E->members.empty() || E->parent) return 1;
+  const char* e = std::getenv("OTM_ASYNC_WORKERS");
+  return e ? std::max(1, std::min(8, std::atoi(e))) : 2;
+}
+
+// Worker wi of the async pipeline: take the next batch (in submit order, a
+// ticket each), run it whole on its own context -- parse, GPU, responses --
+// then publish its results once every earlier batch has published, so each
+// uuid's results come back in submit order.
+void worker_loop(otm_engine* E, int wi) {
+  otm_engine* ctx = wi == 0 ? E : E->actx[(size_t)wi - 1];
   while (true) {
     std::vector<otm_engine::Pending> batch;
+    uint64_t seq;
     {
       std::unique_lock<std::mutex> lk(E->qmu);
       E->qcv.wait(lk, [&] { return E->stop || !E->queue.empty(); });
-      if (E->stop && E->queue.empty()) return;
-      while (!E->queue.empty() && batch.size() < 65536) {
+      if (E->queue.empty()) return;  // stopping, nothing left
+      const size_t cap = async_batch();
+      while (!E->queue.empty() && batch.size() < cap) {
         batch.push_back(std::move(E->queue.front()));
         E->queue.pop_front();
       }
+      seq = E->take_seq++;
     }
     const int n = (int)batch.size();
     std::vector<const char*> reqs((size_t)n);
-    std::vector<size_t> lens((size_t)n), rl((size_t)n);
-    std::vector<int> codes((size_t)n);
-    std::vector<char*> resps((size_t)n);
+    std::vector<size_t> lens((size_t)n), rl((size_t)n, 0);
+    std::vector<int> codes((size_t)n, 500);
+    std::vector<char*> resps((size_t)n, nullptr);
     for (int k = 0; k < n; ++k) {
       reqs[(size_t)k] = batch[(size_t)k].body.data();
       lens[(size_t)k] = batch[(size_t)k].body.size();
     }
-    report_many(E, n, reqs.data(), lens.data(), codes.data(), resps.data(), rl.data());
+    try {
+      report_many(ctx, n, reqs.data(), lens.data(), codes.data(), resps.data(), rl.data());
+    } catch (...) {
+      // out of host memory (report_many freed what it made): the batch's
+      // requests complete with a null body and code 500
+      for (int k = 0; k < n; ++k) {
+        codes[(size_t)k] = 500;
+        resps[(size_t)k] = nullptr;
+        rl[(size_t)k] = 0;
+      }
+    }
     {
-      std::lock_guard<std::mutex> lk(E->qmu);
+      std::unique_lock<std::mutex> lk(E->qmu);
+      E->qcv.wait(lk, [&] { return E->pub_seq == seq; });
       for (int k = 0; k < n; ++k)
         E->done.push_back(otm_result{batch[(size_t)k].tag, codes[(size_t)k], resps[(size_t)k], rl[(size_t)k]});
+      ++E->pub_seq;
     }
     E->qcv.notify_all();
   }
+}
+
+// the pipeline's workers and their contexts, at the first submission (under E->qmu)
+void start_workers(otm_engine* E) {
+  const int nw = async_workers(E);
+  for (int i = 1; i < nw; ++i) {
+    otm_engine* C = nullptr;
+    if (otm_engine_clone(E, &C) != OTM_OK) break;  // fewer workers, same results
+    E->actx.push_back(C);
+  }
+  for (int i = 0; i <= (int)E->actx.size(); ++i) E->workers.emplace_back(worker_loop, E, i);
+  E->worker_started = true;
 }
 
 }  // namespace
@@ -720,8 +767,9 @@ void otm_engine_destroy(otm_engine* E) {
       E->stop = true;
     }
     E->qcv.notify_all();
-    E->worker.join();
+    for (auto& t : E->workers) t.join();  // (queued requests are finished first)
     for (auto& r : E->done) std::free(r.body);
+    for (otm_engine* C : E->actx) otm_engine_destroy(C);
   }
   if (!E->members.empty()) {
     otm::member_pool_free(E);
@@ -930,12 +978,27 @@ static int otm_report_segments_device_impl(otm_engine* E, int n, const char* con
 static int otm_submit_impl(otm_engine* E, const char* req, size_t len, uint64_t tag) {
   if (!E) return fail(OTM_EINVAL, "engine is NULL");
   std::lock_guard<std::mutex> lk(E->qmu);
-  if (!E->worker_started) {
-    E->worker = std::thread(worker_loop, E);
-    E->worker_started = true;
-  }
+  if (!E->worker_started) start_workers(E);
   if (E->queue.size() >= (1u << 22)) return fail(OTM_EAGAIN, "submit queue full");
   E->queue.push_back(otm_engine::Pending{tag, std::string(req, len)});
+  E->qcv.notify_all();
+  return OTM_OK;
+}
+
+static int otm_submit_batch_impl(otm_engine* E, int n, const char* const* reqs, const size_t* lens,
+                                 const uint64_t* tags) {
+  if (!E || n < 0 || (n && (!reqs || !lens || !tags))) return fail(OTM_EINVAL, "bad arguments");
+  // the copies outside the queue lock, over the host threads
+  std::vector<otm_engine::Pending> items((size_t)n);
+  par_for((size_t)n, [&](size_t a, size_t e) {
+    for (size_t k = a; k < e; ++k) items[k] = otm_engine::Pending{tags[k], std::string(reqs[k], lens[k])};
+  });
+  {
+    std::lock_guard<std::mutex> lk(E->qmu);
+    if (!E->worker_started) start_workers(E);
+    if (E->queue.size() + (size_t)n > (1u << 22)) return fail(OTM_EAGAIN, "submit queue full");
+    for (auto& it : items) E->queue.push_back(std::move(it));
+  }
   E->qcv.notify_all();
   return OTM_OK;
 }
@@ -1181,6 +1244,16 @@ int otm_report_segments_device(otm_engine* E, int n, const char* const* reqs, co
 int otm_submit(otm_engine* E, const char* req, size_t len, uint64_t tag) {
   try {
     return otm_submit_impl(E, req, len, tag);
+  } catch (const std::bad_alloc&) {
+    return fail(OTM_ENOMEM, "out of host memory");
+  } catch (const std::exception& e) {
+    return fail(OTM_EINVAL, std::string("internal error: ") + e.what());
+  }
+}
+
+int otm_submit_batch(otm_engine* E, int n, const char* const* reqs, const size_t* lens, const uint64_t* tags) {
+  try {
+    return otm_submit_batch_impl(E, n, reqs, lens, tags);
   } catch (const std::bad_alloc&) {
     return fail(OTM_ENOMEM, "out of host memory");
   } catch (const std::exception& e) {

@@ -98,7 +98,11 @@ struct otm_engine {
   hipEvent_t kev[2 * otm::KN_COUNT] = {};
   float kernel_ms[otm::KN_COUNT] = {};
   float stage_ms[8] = {};
-  // async submit/poll
+  // async submit/poll: a pipeline of workers, each running whole request
+  // batches on its own batch context (worker 0 on this engine, the others on
+  // clones it owns), so one batch's host parse / response writing overlaps
+  // another's GPU work; batches are taken and their results published in
+  // submit order (abi.cpp worker_loop)
   struct Pending {
     uint64_t tag;
     std::string body;
@@ -107,7 +111,9 @@ struct otm_engine {
   std::condition_variable qcv;
   std::deque<Pending> queue;
   std::deque<otm_result> done;
-  std::thread worker;
+  std::vector<std::thread> workers;
+  std::vector<otm_engine*> actx;  // the workers' clones (worker i >= 1 runs on actx[i - 1])
+  uint64_t take_seq = 0, pub_seq = 0;
   bool stop = false;
   bool worker_started = false;
 };

@@ -680,10 +680,38 @@ __global__ __launch_bounds__(CAND_TB, OTM_CAND_WAVES) void k_cand_lane(DevGraph 
         Q[j * S] = qm;
         E[j * S] = em;
       }
-      const int32_t e = (int32_t)((em & ~NODE_ENT) >> 4);
-      float sqd = qm, off = 0.0f;
-      if (!(em & NODE_ENT)) project(g, e, (int32_t)(em & 15u), lat, lon, ls, sqd, off);
-      cput(w, p, j, e, off, sqd / ds);
+    }
+    // the K chosen, in order, out as whole blocks: the point's 64-B record
+    // block in four 16-B stores, its 32-B emission block in two (unused
+    // slots: edge -1, emission +inf) -- whole lines to write back, not
+    // partially written ones
+    static_assert(CAND_LANE_CAP <= KIN, "the lane tier's candidates fit the inline slots");
+    int4* eo4 = (int4*)(w.cand_eo + p * KIN);
+    float4* em4 = (float4*)(w.cand_em + p * KIN);
+    float emv[4];
+#pragma unroll
+    for (int j = 0; j < KIN; j += 2) {
+      int32_t e2[2];
+      float o2[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int jj = j + u;
+        e2[u] = -1;
+        o2[u] = 0.0f;
+        float emj = INFINITY;
+        if (jj < K) {
+          const uint32_t en = E[jj * S];
+          const int32_t e = (int32_t)((en & ~NODE_ENT) >> 4);
+          float sqd = Q[jj * S], off = 0.0f;
+          if (!(en & NODE_ENT)) project(g, e, (int32_t)(en & 15u), lat, lon, ls, sqd, off);
+          e2[u] = e;
+          o2[u] = off;
+          emj = sqd / ds;
+        }
+        emv[(j + u) & 3] = emj;
+      }
+      eo4[j >> 1] = make_int4(e2[0], __float_as_int(o2[0]), e2[1], __float_as_int(o2[1]));
+      if ((j & 3) == 2) em4[j >> 2] = make_float4(emv[0], emv[1], emv[2], emv[3]);
     }
 
     w.ncand[p] = K;
@@ -888,6 +916,8 @@ __global__ __launch_bounds__(TB) void k_candidates(DevGraph g, DevBatch b, DevPa
       if (key & 1ull) project(g, e, (int32_t)((key >> 1) & 15ull), lat, lon, ls, sqd, off);
       const float ds = (2.0f * P.sigma_z) * P.sigma_z;
       cput(w, p, lane, e, off, sqd / ds);
+    } else if (lane < KIN) {
+      cput(w, p, lane, -1, 0.0f, INFINITY);  // the rest of the inline block (whole lines written back)
     }
     if (lane == 0) {
       w.ncand[p] = K;
@@ -1440,8 +1470,12 @@ __device__ __forceinline__ int64_t idx_find(const DevIndex& X, const IdxRow& R, 
   return k;
 }
 // turn units of the route e_i -> (index route u -> v) -> e_j from v's slot
+#ifndef OTM_TRANS_TU_DIAG
+#define OTM_TRANS_TU_DIAG 0  // A/B diagnostic only (wrong results): every turn-table read at entry 0
+#endif
 __device__ __forceinline__ uint32_t idx_turn_units(const uint32_t* TU, const uint4& sl, uint32_t hin_i,
                                                    uint32_t hout_j) {
+  if (OTM_TRANS_TU_DIAG) return TU[0] + sl.z + (hin_i ^ hout_j);
   if (sl.w == NO_TURNS) return turn_units(TU, hin_i, hout_j);
   return turn_units(TU, hin_i, sl.w & 0xFFFFu) + sl.z + turn_units(TU, sl.w >> 16, hout_j);
 }
@@ -1542,9 +1576,18 @@ __global__ __launch_bounds__(TB, 8) void k_trans_sub(DevGraph g, DevBatch b, Dev
   __shared__ int4 tg[NS][KC];  // target: edge, offset bits, from-node, start heading
   __shared__ int4 sr[NS][KC];  // source: edge, offset bits, remaining-length bits, end heading
   __shared__ IdxRow rq[NS][KC];
+  // slot of candidate k in its column group's row: XOR-swizzled so that the
+  // groups a ds_read_b128 lane group spans (MI355X_MICROARCH.md §LDS: lanes
+  // {0-3,12-15,20-27}, ...) read different banks when they read the same k
+  // (a 128-B row at 8 lanes per column puts groups sg and sg + 2 on the same
+  // 64 banks; at 16 lanes, every row spans all 64)
+#ifndef OTM_TRANS_SWZ
+#define OTM_TRANS_SWZ 1
+#endif
   __shared__ uint32_t TU[TURN_TABLE];  // turn units per deviation
   const int lane = threadIdx.x, sg = lane / S, sl = lane % S;
   const unsigned long long smask = ((1ull << S) - 1ull) << (sg * S);
+  const int swz = !OTM_TRANS_SWZ ? 0 : (S == 8 ? ((sg >> 1) & 1) * 4 : (sg & 1) * 8);
   for (int k = lane; k < TURN_TABLE; k += TB) TU[k] = P.turn_units[k];
   const DevIndex& X = w.idx;
   unsigned long long c_search = 0, c_settled = 0, c_relaxed = 0, c_trans = 0;
@@ -1595,17 +1638,17 @@ __global__ __launch_bounds__(TB, 8) void k_trans_sub(DevGraph g, DevBatch b, Dev
         const int2 c = crec(w, p, k);
         const int32_t e = c.x;
         const float o = __int_as_float(c.y);
-        tg[sg][k] = make_int4(e, __float_as_int(o), g.e_from[e], (int)dst_head(g, e, o));
+        tg[sg][k ^ swz] = make_int4(e, __float_as_int(o), g.e_from[e], (int)dst_head(g, e, o));
       }
       if (act && k < Kq) {
         const int2 c = crec(w, q, k);
         const int32_t e = c.x;
         const float o = __int_as_float(c.y);
-        sr[sg][k] = make_int4(e, __float_as_int(o), __float_as_int(src_start(g, e, o)), (int)src_head(g, e, o));
+        sr[sg][k ^ swz] = make_int4(e, __float_as_int(o), __float_as_int(src_start(g, e, o)), (int)src_head(g, e, o));
         if (idx_ok) {
           // erow[e]: the row of e's end node; erow[E + e]: of its start node
           const IdxRow R = X.erow[cand_node(o) ? (int64_t)g.n_edges + e : (int64_t)e];
-          rq[sg][k] = R;
+          rq[sg][k ^ swz] = R;
           bad = bad || R.cnt < 0;
         }
       }
@@ -1634,8 +1677,8 @@ __global__ __launch_bounds__(TB, 8) void k_trans_sub(DevGraph g, DevBatch b, Dev
           h0[u] = 0u;
           if (idx < npair) {
             const int i = idx / Kp, j = idx - (idx / Kp) * Kp;
-            const int4 T = tg[sg][j], Sx = sr[sg][i];
-            const IdxRow R = rq[sg][i];
+            const int4 T = tg[sg][j ^ swz], Sx = sr[sg][i ^ swz];
+            const IdxRow R = rq[sg][i ^ swz];
             const bool same = T.x == Sx.x && __int_as_float(T.y) >= __int_as_float(Sx.y);
             if (!same && R.cnt > 0) {
               h0[u] = idx_slot0((uint32_t)T.z, R);
@@ -1648,7 +1691,7 @@ __global__ __launch_bounds__(TB, 8) void k_trans_sub(DevGraph g, DevBatch b, Dev
           const int idx = idx0 + u * S;
           if (idx >= npair) continue;
           const int i = idx / Kp, j = idx - (idx / Kp) * Kp;
-          const int4 T = tg[sg][j], Sx = sr[sg][i];
+          const int4 T = tg[sg][j ^ swz], Sx = sr[sg][i ^ swz];
           const int32_t ej = T.x, vj = T.z, ei = Sx.x;
           const float oj = __int_as_float(T.y), oi = __int_as_float(Sx.y), si = __int_as_float(Sx.z);
           float r = 0.0f;
@@ -1657,7 +1700,7 @@ __global__ __launch_bounds__(TB, 8) void k_trans_sub(DevGraph g, DevBatch b, Dev
           if (ej == ei && oj >= oi) {
             r = oj - oi;
           } else {
-            const IdxRow R = rq[sg][i];
+            const IdxRow R = rq[sg][i ^ swz];
             uint4 sv = s0[u];
             uint32_t h = h0[u];
             if (R.cnt > 0) {
@@ -1688,9 +1731,9 @@ __global__ __launch_bounds__(TB, 8) void k_trans_sub(DevGraph g, DevBatch b, Dev
         // entries with D <= bound and their out-degrees
         for (int i = 0; i < Kq; ++i) {
           bool first = true;
-          for (int k = 0; k < i; ++k) first = first && rq[sg][k].off != rq[sg][i].off;
+          for (int k = 0; k < i; ++k) first = first && rq[sg][k ^ swz].off != rq[sg][i ^ swz].off;
           if (!first) continue;
-          const IdxRow R = rq[sg][i];
+          const IdxRow R = rq[sg][i ^ swz];
           for (int64_t k = sl; k < (int64_t)R.cap; k += S) {
             const uint4 slt = X.slot[R.off + k];
             if (slt.x != EMPTY && bitsf(slt.y) <= bound) {

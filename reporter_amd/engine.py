@@ -181,6 +181,15 @@ class Engine(object):
         b = body.encode("utf-8") if isinstance(body, str) else body
         _check(lib().otm_submit(self.h, b, len(b), tag))
 
+    def submit_batch(self, bodies, tags):
+        """otm_submit_batch: many requests in one call (in order)."""
+        bs = [b.encode("utf-8") if isinstance(b, str) else b for b in bodies]
+        n = len(bs)
+        arr = (C.c_char_p * n)(*bs)
+        lens = (C.c_size_t * n)(*[len(b) for b in bs])
+        tg = (C.c_uint64 * n)(*tags)
+        _check(lib().otm_submit_batch(self.h, n, arr, lens, tg))
+
     def poll(self, max_results=1024, timeout_us=0):
         res = (_lib.Result * max_results)()
         n = lib().otm_poll(self.h, res, max_results, timeout_us)

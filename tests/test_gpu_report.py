@@ -281,6 +281,37 @@ def test_one_engine_from_many_threads(small_graph):
         assert [pos[t] for t in tags] == sorted(pos[t] for t in tags), u
 
 
+@pytest.mark.parametrize("workers,batch", [("1", "8192"), ("2", "37"), ("3", "11")])
+def test_async_pipeline_order_and_bodies(small_graph, monkeypatch, workers, batch):
+    """otm_submit_batch / otm_poll through the async pipeline (workers on
+    their own batch contexts, OTM_ASYNC_WORKERS; small OTM_ASYNC_BATCH forces
+    many batches in flight): every body byte-equal to the sequential answer,
+    each uuid's results in submit order, every tag once."""
+    from reporter_amd import encode_request
+    monkeypatch.setenv("OTM_ASYNC_WORKERS", workers)
+    monkeypatch.setenv("OTM_ASYNC_BATCH", batch)
+    b = synth.make_traces(small_graph, 120, 30, seed=93)
+    bodies = []
+    for t in range(120):
+        a, e = b["trace_off"][t], b["trace_off"][t + 1]
+        bodies.append(encode_request("veh%d" % (t % 17), b["lat"][a:e], b["lon"][a:e],
+                                     b["time"][a:e].astype(np.int64), b["accuracy"][a:e].astype(np.int32)))
+    bodies += [b"", b'{"uuid":"x","trace":[]}']
+    with Engine(graph_path=small_graph) as eng:
+        want = eng.report_batch(bodies)
+        tags = list(range(5000, 5000 + 3 * len(bodies)))
+        for r in range(3):
+            eng.submit_batch(bodies, tags[r * len(bodies):(r + 1) * len(bodies)])
+        polled = []
+        while len(polled) < len(tags):
+            polled += eng.poll(4096, 2000000)
+    assert sorted(t for t, _, _ in polled) == tags
+    for tag, code, resp in polled:
+        assert (code, resp) == want[(tag - 5000) % len(bodies)]
+    # results are published in submit order: tags come back increasing
+    assert [t for t, _, _ in polled] == tags
+
+
 def test_valhalla_module_shim(small_graph, oracle, tmp_path):
     """reporter_amd.valhalla stands in for the binding reporter_service.py
     imports: Configure (:279), SegmentMatcher() (:52), Match (:112) returns

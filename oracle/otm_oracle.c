@@ -138,7 +138,6 @@ void orc_params_default(orc_params* p) {
   p->gps_accuracy = 5.0f;
   p->max_candidates = ORC_KMAX;
   p->turn_penalty_factor = 200.0f;
-  p->turn_aware = 0;
 }
 void orc_report_cfg_default(orc_report_cfg* c) {
   memset(c, 0, sizeof *c);
@@ -374,115 +373,70 @@ static int candidates(const orc_graph* g, const orc_params* P, float lat, float 
   return K;
 }
 
-/* ================================================================== S4/S6 bounded Dijkstra */
+/* ================================================================== S4/S6 turn-aware bounded search
+ * a transition's route is the shortest by "distance cost
+ * plus turn penalty" (DESIGN.md §3 rule 4).  The search labels every directed
+ * edge g with the cheapest way to be at g's start, turned into it (its
+ * departure label), and every node v with the cheapest way to arrive at v
+ * (its arrival label).  Costs are integers in 1/64 m: an edge costs L(e) =
+ * round(len(e) x 64), a turn its turn units; a label is the 64-bit key
+ * cost << 32 | predecessor edge (0xFFFFFFFF: none), compared as one integer,
+ * so ties go to the smaller predecessor and the labels are the search's
+ * unique fixed point (every step costs > 0) -- the GPU's label-correcting
+ * searches and index builder reach the same labels in any order.  A search
+ * from source node u entered with heading hin (NO_HEAD for a node candidate):
+ *   arrival(u) = (0, none); departure(g) = (turn(hin, g), none) for g out of u;
+ *   a departure label (c, .) of g gives arrival(to(g)) <= (c + L(g), g) and
+ *   departure(h) <= (c + L(g) + turn(g, h), g) for h out of to(g);
+ * bounded: only labels with cost <= floor(B x 64), B = max_route_distance_factor
+ * x gc.  A route's distance and turn units are summed along its edges in
+ * route order (rule 4). */
+#define NONE_PRED 0xFFFFFFFFu
 typedef struct {
-  float d;
-  int32_t n;
-} hnode;
+  uint64_t k;
+  int32_t e;
+} khn;
 
 typedef struct ws {
-  float* dist;
-  int32_t* pred;
-  uint32_t* lab;
-  uint32_t* done;
+  uint64_t *ek, *nk;      /* departure labels per edge, arrival labels per node */
+  uint32_t *elab, *nlab;  /* stamps: labelled in this search */
   uint32_t stamp;
-  hnode* heap;
+  int32_t* elist;         /* the labelled edges, in labelling order */
+  int32_t ne, nn;         /* labelled edges / nodes */
+  khn* heap;
   size_t hn, hcap;
-  int32_t nlab;
   hit hits[ORC_MAX_HITS + 1];
   seen_set seen;
-  /* turn-aware searches (orc_params.turn_aware): labels per edge */
-  float* ed;
-  uint32_t *eu, *elab, *edone, estamp;
-  int32_t* ep;
-  struct ehn* eheap;
-  size_t ehn_n, ehcap;
 } ws;
 
-static void hpush(ws* w, float d, int32_t n) {
+static void hpush(ws* w, uint64_t k, int32_t e) {
   if (w->hn == w->hcap) {
     w->hcap = w->hcap ? w->hcap * 2 : 1024;
-    w->heap = (hnode*)realloc(w->heap, w->hcap * sizeof(hnode));
+    w->heap = (khn*)realloc(w->heap, w->hcap * sizeof(khn));
   }
   size_t i = w->hn++;
   while (i > 0) {
-    size_t p = (i - 1) / 2;
-    if (w->heap[p].d <= d) break;
-    w->heap[i] = w->heap[p];
-    i = p;
+    size_t q = (i - 1) / 2;
+    if (w->heap[q].k <= k) break;
+    w->heap[i] = w->heap[q];
+    i = q;
   }
-  w->heap[i].d = d;
-  w->heap[i].n = n;
+  w->heap[i].k = k;
+  w->heap[i].e = e;
 }
-static hnode hpop(ws* w) {
-  hnode top = w->heap[0];
-  hnode last = w->heap[--w->hn];
+static khn hpop(ws* w) {
+  khn top = w->heap[0], last = w->heap[--w->hn];
   size_t i = 0;
   while (1) {
     size_t c = 2 * i + 1;
     if (c >= w->hn) break;
-    if (c + 1 < w->hn && w->heap[c + 1].d < w->heap[c].d) ++c;
-    if (w->heap[c].d >= last.d) break;
+    if (c + 1 < w->hn && w->heap[c + 1].k < w->heap[c].k) ++c;
+    if (w->heap[c].k >= last.k) break;
     w->heap[i] = w->heap[c];
     i = c;
   }
   if (w->hn) w->heap[i] = last;
   return top;
-}
-
-/* Labels D(v) for every v with D(v) <= B from source node u (D(u) = 0).
- * pred(v) = the lexicographically smallest (D(w) + len(e), e) over in-edges.
- * Returns 0, or -1 when more than ORC_SEARCH_LIMIT nodes are labelled. */
-static int dijkstra(const orc_graph* g, ws* w, int32_t u, float B, orc_counters* C, int route) {
-  if (++w->stamp == 0) {
-    memset(w->lab, 0, sizeof(uint32_t) * (size_t)g->h.n_nodes);
-    memset(w->done, 0, sizeof(uint32_t) * (size_t)g->h.n_nodes);
-    w->stamp = 1;
-  }
-  const uint32_t s = w->stamp;
-  w->hn = 0;
-  w->lab[u] = s;
-  w->dist[u] = 0.0f;
-  w->pred[u] = -1;
-  w->nlab = 1;
-  hpush(w, 0.0f, u);
-  int64_t relaxed = 0;
-  while (w->hn) {
-    hnode h = hpop(w);
-    if (w->done[h.n] == s || h.d != w->dist[h.n]) continue;
-    w->done[h.n] = s;
-    const float d = h.d;
-    for (int32_t e = g->out_off[h.n]; e < g->out_off[h.n + 1]; ++e) {
-      ++relaxed;
-      const float nd = d + g->elen[e];
-      if (!(nd <= B)) continue;
-      const int32_t v = g->eto[e];
-      if (w->lab[v] != s) {
-        if (w->nlab == ORC_SEARCH_LIMIT) return -1;
-        w->lab[v] = s;
-        w->dist[v] = nd;
-        w->pred[v] = e;
-        w->nlab++;
-        hpush(w, nd, v);
-      } else if (nd < w->dist[v]) {
-        w->dist[v] = nd;
-        w->pred[v] = e;
-        hpush(w, nd, v);
-      } else if (nd == w->dist[v] && e < w->pred[v]) {
-        w->pred[v] = e;
-      }
-    }
-  }
-  if (route) {
-    C->route_searches++;
-    C->route_nodes_settled += w->nlab;
-    C->route_edges_relaxed += relaxed;
-  } else {
-    C->searches++;
-    C->nodes_settled += w->nlab;
-    C->edges_relaxed += relaxed;
-  }
-  return 0;
 }
 
 /* ================================================================== per-batch state */
@@ -518,7 +472,7 @@ typedef struct batch {
   int phase;
   orc_counters* ctr; /* per thread */
   int count_unique;  /* count §8(d)'s unique projected edges (keep_stages) */
-  int32_t *in_off, *in_edge; /* in-edge CSR (turn-aware searches only) */
+  uint32_t* elen64;  /* L(e) = round(len(e) x 64): the search's edge costs */
   uint32_t turn_units[181]; /* orc_turn_units per deviation 0..180 */
 } batch;
 
@@ -565,234 +519,185 @@ static void phase_a(batch* B, ws* w, int32_t t, orc_counters* C) {
 
 /* ------------------------------------------------------------ S4 */
 /* A candidate at offset 0 is a node candidate (S2's node snap): its routes
- * start at that node with nothing left to drive; an edge candidate's start at
- * its edge's end node after the rest of the edge. */
+ * start at that node with nothing left to drive and no heading; an edge
+ * candidate's start at its edge's end node after the rest of the edge,
+ * entered with the edge's end heading. */
 static int32_t src_node(const orc_graph* g, int32_t e, float off) { return off == 0.0f ? g->efrom[e] : g->eto[e]; }
 static float src_start(const orc_graph* g, int32_t e, float off) { return off == 0.0f ? 0.0f : g->elen[e] - off; }
 #define NO_HEAD 0xFFFFu /* a node candidate's side of a route: no turn */
+static unsigned src_hin(const orc_graph* g, int32_t e, float off) { return off == 0.0f ? NO_HEAD : g->ehead_in[e]; }
 static uint32_t turn_cost_units(const batch* B, unsigned hin, unsigned hout) {
   return (hin == NO_HEAD || hout == NO_HEAD) ? 0u : B->turn_units[orc_turn_deg(hin, hout)];
 }
+/* the cost bound of a search bounded by B metres */
+static uint32_t cost_bound(float B) { return (uint32_t)floor((double)B * 64.0); }
 
-/* ------------------------------------------------------------ turn-aware routes (experiment)
- * SURVEY Appendix B picks a transition's route by "distance
- * cost plus turn penalty"; the spec picks it by distance alone and adds that
- * route's turns.  With orc_params.turn_aware the oracle instead runs an
- * edge-labelled search -- a label per edge, i.e. per (node, incoming edge) --
- * minimising dist + units / 64 (ties: the smaller distance, then the smaller
- * edge), so scripts/turn_aware_rate.py can measure how often the two rules
- * choose different routes, transitions, states and segments.  The GPU
- * implements the spec only. */
-struct ehn {
-  double c;
-  int32_t e;
-};
-static double ecost(float d, uint32_t u) { return (double)d + (double)u * 0.015625; }
-static void ehpush(ws* w, double c, int32_t e) {
-  if (w->ehn_n == w->ehcap) {
-    w->ehcap = w->ehcap ? w->ehcap * 2 : 1024;
-    w->eheap = (struct ehn*)realloc(w->eheap, w->ehcap * sizeof(struct ehn));
+static int set_edge(ws* w, int32_t g, uint64_t k) {
+  if (w->elab[g] != w->stamp) {
+    w->elab[g] = w->stamp;
+    w->elist[w->ne++] = g;
+  } else if (k >= w->ek[g]) {
+    return 0;
   }
-  size_t i = w->ehn_n++;
-  while (i > 0) {
-    size_t q = (i - 1) / 2;
-    if (w->eheap[q].c <= c) break;
-    w->eheap[i] = w->eheap[q];
-    i = q;
+  w->ek[g] = k;
+  hpush(w, k, g);
+  return 1;
+}
+static void set_node(ws* w, int32_t v, uint64_t k) {
+  if (w->nlab[v] != w->stamp) {
+    w->nlab[v] = w->stamp;
+    w->nn++;
+    w->nk[v] = k;
+  } else if (k < w->nk[v]) {
+    w->nk[v] = k;
   }
-  w->eheap[i].c = c;
-  w->eheap[i].e = e;
 }
-static struct ehn ehpop(ws* w) {
-  struct ehn top = w->eheap[0], last = w->eheap[--w->ehn_n];
-  size_t i = 0;
-  while (1) {
-    size_t c = 2 * i + 1;
-    if (c >= w->ehn_n) break;
-    if (c + 1 < w->ehn_n && w->eheap[c + 1].c < w->eheap[c].c) ++c;
-    if (w->eheap[c].c >= last.c) break;
-    w->eheap[i] = w->eheap[c];
-    i = c;
-  }
-  if (w->ehn_n) w->eheap[i] = last;
-  return top;
-}
-static uint32_t uadd(uint32_t a, uint32_t b) {
-  const uint32_t s = a + b;
-  return s > TURN_UNITS_MAX ? TURN_UNITS_MAX : s;
-}
-static void ta_relax(ws* w, int32_t f, float d, uint32_t un, int32_t pe) {
-  const uint32_t s = w->estamp;
-  const double c = ecost(d, un);
-  if (w->elab[f] != s) {
-    w->elab[f] = s;
-  } else {
-    if (w->edone[f] == s) return;
-    const double oc = ecost(w->ed[f], w->eu[f]);
-    if (!(c < oc || (c == oc && (d < w->ed[f] || (d == w->ed[f] && pe < w->ep[f]))))) return;
-  }
-  w->ed[f] = d;
-  w->eu[f] = un;
-  w->ep[f] = pe;
-  ehpush(w, c, f);
-}
-/* labels of every edge whose route from node u (arriving with heading hin,
-   NO_HEAD for a node candidate) stays within distance `bound` */
-static void ta_search(const batch* B, ws* w, int32_t u, unsigned hin, float bound) {
+
+/* The labels of a search from node u entered with heading hin, bounded by
+ * cost cmax.  Returns 0, or -1 when more than ORC_SEARCH_LIMIT labels. */
+static int ta_search(const batch* B, ws* w, int32_t u, unsigned hin, uint32_t cmax, orc_counters* C, int route) {
   const orc_graph* g = B->g;
-  if (++w->estamp == 0) {
+  if (++w->stamp == 0) {
     memset(w->elab, 0, sizeof(uint32_t) * (size_t)g->h.n_edges);
-    memset(w->edone, 0, sizeof(uint32_t) * (size_t)g->h.n_edges);
-    w->estamp = 1;
+    memset(w->nlab, 0, sizeof(uint32_t) * (size_t)g->h.n_nodes);
+    w->stamp = 1;
   }
-  const uint32_t s = w->estamp;
-  w->ehn_n = 0;
+  w->hn = 0;
+  w->ne = w->nn = 0;
+  set_node(w, u, NONE_PRED);
   for (int32_t e = g->out_off[u]; e < g->out_off[u + 1]; ++e) {
-    const float d = g->elen[e];
-    if (!(d <= bound)) continue;
-    ta_relax(w, e, d, turn_cost_units(B, hin, g->ehead_out[e]), -1);
+    const uint32_t c = turn_cost_units(B, hin, g->ehead_out[e]);
+    if (c <= cmax) set_edge(w, e, ((uint64_t)c << 32) | NONE_PRED);
   }
-  while (w->ehn_n) {
-    const struct ehn h = ehpop(w);
+  while (w->hn) {
+    const khn h = hpop(w);
     const int32_t e = h.e;
-    if (w->edone[e] == s || h.c != ecost(w->ed[e], w->eu[e])) continue;
-    w->edone[e] = s;
+    if (h.k != w->ek[e]) continue;
+    const uint64_t ca = (h.k >> 32) + (uint64_t)B->elen64[e];
+    if (ca > cmax) continue;
     const int32_t v = g->eto[e];
+    set_node(w, v, (ca << 32) | (uint32_t)e);
     for (int32_t f = g->out_off[v]; f < g->out_off[v + 1]; ++f) {
-      const float nd = w->ed[e] + g->elen[f];
-      if (!(nd <= bound)) continue;
-      ta_relax(w, f, nd, uadd(w->eu[e], turn_cost_units(B, g->ehead_in[e], g->ehead_out[f])), e);
+      const uint64_t c = ca + turn_cost_units(B, g->ehead_in[e], g->ehead_out[f]);
+      if (c <= cmax) set_edge(w, f, (c << 32) | (uint32_t)e);
     }
+    if (w->ne + w->nn > ORC_SEARCH_LIMIT) return -1;
   }
+  if (w->ne + w->nn > ORC_SEARCH_LIMIT) return -1;
+  /* work counters: the departure labels, and the edges a label relaxes
+     (its end node's out-edges, when the arrival is within the bound) */
+  int64_t relaxed = 0;
+  for (int k = 0; k < w->ne; ++k) {
+    const int32_t e = w->elist[k];
+    if ((w->ek[e] >> 32) + (uint64_t)B->elen64[e] <= cmax) relaxed += g->out_off[g->eto[e] + 1] - g->out_off[g->eto[e]];
+  }
+  if (route) {
+    C->route_searches++;
+    C->route_nodes_settled += w->ne;
+    C->route_edges_relaxed += relaxed;
+  } else {
+    C->searches++;
+    C->nodes_settled += w->ne;
+    C->edges_relaxed += relaxed;
+  }
+  return 0;
 }
-/* the cheapest route from the search's source into edge ej (offset oj):
-   returns 0 when none; *last = the route's last edge (-1: the empty route) */
-static int ta_target(const batch* B, const ws* w, int32_t u, unsigned hin, int32_t ej, float oj, float* dist,
-                     uint32_t* units, int32_t* last) {
-  const orc_graph* g = B->g;
-  const int32_t v = g->efrom[ej];
-  const unsigned hout = oj == 0.0f ? NO_HEAD : g->ehead_out[ej];
-  int found = 0;
-  double bc = 0.0;
-  float bd = 0.0f;
-  uint32_t bu = 0;
-  int32_t be = -1;
-  if (v == u) {
-    found = 1;
-    bu = turn_cost_units(B, hin, hout);
-    bc = ecost(0.0f, bu);
-  }
-  for (int32_t k = B->in_off[v]; k < B->in_off[v + 1]; ++k) {
-    const int32_t e = B->in_edge[k];
-    if (w->edone[e] != w->estamp) continue;
-    const uint32_t un = uadd(w->eu[e], turn_cost_units(B, g->ehead_in[e], hout));
-    const double c = ecost(w->ed[e], un);
-    if (!found || c < bc || (c == bc && (w->ed[e] < bd || (w->ed[e] == bd && e < be)))) {
-      found = 1;
-      bc = c;
-      bd = w->ed[e];
-      bu = un;
-      be = e;
-    }
-  }
-  *dist = bd;
-  *units = bu;
-  *last = be;
-  return found;
-}
-static unsigned src_hin(const orc_graph* g, int32_t e, float off) { return off == 0.0f ? NO_HEAD : g->ehead_in[e]; }
 
-static void ta_transitions(batch* B, ws* w, int64_t p) {
+/* The route of the last search to candidate (ej, oj): into edge ej (an edge
+ * candidate: its departure label, the turn into ej included) or to node
+ * from(ej) (a node candidate: its arrival label).  Returns 0 when unlabelled;
+ * else the route's fully traversed edges in order (path, when non-NULL, up to
+ * cap), their number, their summed length d (route order) and the route's
+ * turn units (clamped to 2^24 - 1). */
+static int ta_route(const batch* B, const ws* w, unsigned hin, int32_t ej, float oj, int32_t* path, int cap, int* plen,
+                    float* d, uint32_t* units) {
   const orc_graph* g = B->g;
-  const int64_t q = B->col_prev[p];
-  const int Kq = B->ncand[q], Kp = B->ncand[p];
-  const float gcv = B->gc[p];
-  const float bound = B->P->max_route_distance_factor * gcv;
-  float* T = B->trans + B->trans_off[p];
-  const int32_t* eq = B->cand_edge + q * ORC_KMAX;
-  const float* oq = B->cand_off + q * ORC_KMAX;
-  const int32_t* ep = B->cand_edge + p * ORC_KMAX;
-  const float* op = B->cand_off + p * ORC_KMAX;
-  for (int i = 0; i < Kq; ++i) {
-    const int32_t u = src_node(g, eq[i], oq[i]);
-    const unsigned hin = src_hin(g, eq[i], oq[i]);
-    const float start = src_start(g, eq[i], oq[i]);
-    ta_search(B, w, u, hin, bound);
-    for (int j = 0; j < Kp; ++j) {
-      T[i * Kp + j] = INF_F;
-      float r;
-      uint32_t units = 0;
-      if (ep[j] == eq[i] && op[j] >= oq[i]) {
-        r = op[j] - oq[i];
-      } else {
-        float d;
-        int32_t last;
-        if (!ta_target(B, w, u, hin, ep[j], op[j], &d, &units, &last)) continue;
-        const float sd = start + d;
-        r = sd + op[j];
-      }
-      if (r <= bound) T[i * Kp + j] = ((float)units * 0.015625f + fabsf(r - gcv)) / B->P->beta;
-    }
+  uint64_t k;
+  if (oj == 0.0f) {
+    const int32_t v = g->efrom[ej];
+    if (w->nlab[v] != w->stamp) return 0;
+    k = w->nk[v];
+  } else {
+    if (w->elab[ej] != w->stamp) return 0;
+    k = w->ek[ej];
   }
+  int32_t tmp[64];
+  int32_t* pp = path ? path : tmp;
+  const int pc = path ? cap : 64;
+  int n = 0;
+  uint32_t pr = (uint32_t)k;
+  while (pr != NONE_PRED) {
+    if (n < pc) pp[n] = (int32_t)pr;
+    ++n;
+    pr = (uint32_t)w->ek[pr];
+  }
+  /* forward: route order; a chain longer than the buffer is walked again */
+  float dd = 0.0f;
+  uint64_t un = 0;
+  unsigned h = hin;
+  for (int m = n - 1; m >= 0; --m) {
+    int32_t e;
+    if (n <= pc) {
+      e = pp[m];
+    } else {
+      int32_t x = (int32_t)(uint32_t)k;
+      for (int s2 = 0; s2 < m; ++s2) x = (int32_t)(uint32_t)w->ek[x];
+      e = x;
+    }
+    un += turn_cost_units(B, h, g->ehead_out[e]);
+    dd = dd + g->elen[e];
+    h = g->ehead_in[e];
+  }
+  if (oj != 0.0f) un += turn_cost_units(B, h, g->ehead_out[ej]);
+  if (path && n <= pc)
+    for (int a = 0, b = n - 1; a < b; ++a, --b) {
+      const int32_t t = pp[a];
+      pp[a] = pp[b];
+      pp[b] = t;
+    }
+  *plen = n;
+  *d = dd;
+  *units = un > TURN_UNITS_MAX ? TURN_UNITS_MAX : (uint32_t)un;
+  return 1;
 }
 
 static int transitions(batch* B, ws* w, int64_t p, orc_counters* C) {
-  if (B->P->turn_aware) {
-    ta_transitions(B, w, p);
-    return 0;
-  }
   const orc_graph* g = B->g;
   const int64_t q = B->col_prev[p];
   const int Kq = B->ncand[q], Kp = B->ncand[p];
   const float gcv = B->gc[p];
   const float bound = B->P->max_route_distance_factor * gcv;
+  const uint32_t cmax = cost_bound(bound);
   float* T = B->trans + B->trans_off[p];
   for (int k = 0; k < Kq * Kp; ++k) T[k] = INF_F;
   const int32_t* eq = B->cand_edge + q * ORC_KMAX;
   const float* oq = B->cand_off + q * ORC_KMAX;
   const int32_t* ep = B->cand_edge + p * ORC_KMAX;
   const float* op = B->cand_off + p * ORC_KMAX;
-  int32_t srcs[ORC_KMAX];
-  int ns = 0;
-  for (int i = 0; i < Kq; ++i) {
-    int32_t u = src_node(g, eq[i], oq[i]);
+  /* one search per distinct source (node, heading) */
+  for (int i0 = 0; i0 < Kq; ++i0) {
+    const int32_t u = src_node(g, eq[i0], oq[i0]);
+    const unsigned hin = src_hin(g, eq[i0], oq[i0]);
     int seen = 0;
-    for (int s = 0; s < ns; ++s) seen |= srcs[s] == u;
-    if (!seen) srcs[ns++] = u;
-  }
-  for (int s = 0; s < ns; ++s) {
-    const int32_t u = srcs[s];
-    if (dijkstra(g, w, u, bound, C, 0) < 0) return -1;
-    for (int i = 0; i < Kq; ++i) {
-      if (src_node(g, eq[i], oq[i]) != u) continue;
+    for (int k = 0; k < i0; ++k) seen |= src_node(g, eq[k], oq[k]) == u && src_hin(g, eq[k], oq[k]) == hin;
+    if (seen) continue;
+    if (ta_search(B, w, u, hin, cmax, C, 0) < 0) return -1;
+    for (int i = i0; i < Kq; ++i) {
+      if (src_node(g, eq[i], oq[i]) != u || src_hin(g, eq[i], oq[i]) != hin) continue;
       const float start = src_start(g, eq[i], oq[i]);
       for (int j = 0; j < Kp; ++j) {
         float r;
+        uint32_t units = 0;
         if (ep[j] == eq[i] && op[j] >= oq[i]) {
           r = op[j] - oq[i];
         } else {
-          const int32_t v = g->efrom[ep[j]];
-          if (w->lab[v] != w->stamp) continue;
-          const float sd = start + w->dist[v];
+          float d;
+          int n;
+          if (!ta_route(B, w, hin, ep[j], op[j], NULL, 0, &n, &d, &units)) continue;
+          const float sd = start + d;
           r = sd + op[j];
         }
         if (r <= bound) {
-          /* turn cost of the route: the turns from e_i into the
-             path, between its edges and into e_j, in integer 1/64 m units
-             (order-free, exact in a float below 2^24); a node candidate has
-             no heading, so no turn on its side */
-          uint32_t units = 0;
-          if (!(ep[j] == eq[i] && op[j] >= oq[i])) {
-            unsigned hn = op[j] == 0.0f ? NO_HEAD : g->ehead_out[ep[j]];
-            for (int32_t x = g->efrom[ep[j]]; x != u;) {
-              const int32_t e = w->pred[x];
-              units += turn_cost_units(B, g->ehead_in[e], hn);
-              hn = g->ehead_out[e];
-              x = g->efrom[e];
-            }
-            units += turn_cost_units(B, oq[i] == 0.0f ? NO_HEAD : g->ehead_in[eq[i]], hn);
-            if (units > TURN_UNITS_MAX) units = TURN_UNITS_MAX;
-          }
           const float tc = (float)units * 0.015625f;
           const float diff = fabsf(r - gcv);
           T[i * Kp + j] = (tc + diff) / B->P->beta;
@@ -964,7 +869,7 @@ static void group_chain(batch* B, tres* R, const travs* T) {
 }
 
 /* route of step p (from state at q = col_prev[p] to state at p) */
-static int route_step(batch* B, ws* w, int64_t p, int32_t* path, int* plen, int* same, float* R,
+static int route_step(batch* B, ws* w, int64_t p, int32_t* path, int pcap, int* plen, int* same, float* R,
                       orc_counters* C) {
   const orc_graph* g = B->g;
   const int64_t q = B->col_prev[p];
@@ -979,43 +884,15 @@ static int route_step(batch* B, ws* w, int64_t p, int32_t* path, int* plen, int*
   }
   *same = 0;
   const float bound = B->P->max_route_distance_factor * B->gc[p];
-  if (B->P->turn_aware) {
-    const int32_t u = src_node(g, ei, oi);
-    const unsigned hin = src_hin(g, ei, oi);
-    ta_search(B, w, u, hin, bound);
-    float d;
-    uint32_t units;
-    int32_t last;
-    if (!ta_target(B, w, u, hin, ej, oj, &d, &units, &last)) return -1;
-    int n = 0;
-    for (int32_t e = last; e >= 0; e = w->ep[e]) path[n++] = e;
-    for (int k = 0; k < n / 2; ++k) {
-      int32_t tmp = path[k];
-      path[k] = path[n - 1 - k];
-      path[n - 1 - k] = tmp;
-    }
-    *plen = n;
-    const float sd = src_start(g, ei, oi) + d;
-    *R = sd + oj;
-    return 0;
-  }
-  const int32_t u = src_node(g, ei, oi), v = g->efrom[ej];
-  if (dijkstra(g, w, u, bound, C, 1) < 0) return -1;
-  int n = 0;
-  for (int32_t x = v; x != u;) {
-    const int32_t e = w->pred[x];
-    path[n++] = e;
-    x = g->efrom[e];
-  }
-  for (int k = 0; k < n / 2; ++k) {
-    int32_t tmp = path[k];
-    path[k] = path[n - 1 - k];
-    path[n - 1 - k] = tmp;
-  }
-  *plen = n;
-  C->route_edges += n;
+  const int32_t u = src_node(g, ei, oi);
+  const unsigned hin = src_hin(g, ei, oi);
+  if (ta_search(B, w, u, hin, cost_bound(bound), C, 1) < 0) return -1;
+  float d;
+  uint32_t units;
+  if (!ta_route(B, w, hin, ej, oj, path, pcap, plen, &d, &units) || *plen > pcap) return -1;
+  C->route_edges += *plen;
   const float start = src_start(g, ei, oi);
-  const float sd = start + w->dist[v];
+  const float sd = start + d;
   *R = sd + oj;
   return 0;
 }
@@ -1171,13 +1048,13 @@ static int segments_of_trace(batch* B, ws* w, int32_t t, tres* R, orc_counters* 
       continue;
     }
     /* step lastp -> p */
-    if (pcap < 4096) {
-      pcap = 4096;
+    if (pcap < ORC_SEARCH_LIMIT + 1) {
+      pcap = ORC_SEARCH_LIMIT + 1; /* a route's edges are labelled edges of its search */
       path = (int32_t*)realloc(path, sizeof(int32_t) * (size_t)pcap);
     }
     int plen, same;
     float Rd;
-    if (route_step(B, w, p, path, &plen, &same, &Rd, C) < 0) {
+    if (route_step(B, w, p, path, pcap, &plen, &same, &Rd, C) < 0) {
       rc = -1;
       break;
     }
@@ -1337,19 +1214,12 @@ static void* worker(void* arg) {
   batch* B = A->B;
   ws w;
   memset(&w, 0, sizeof w);
-  const size_t nn = (size_t)B->g->h.n_nodes;
-  w.dist = (float*)malloc(sizeof(float) * nn);
-  w.pred = (int32_t*)malloc(sizeof(int32_t) * nn);
-  w.lab = (uint32_t*)calloc(nn, sizeof(uint32_t));
-  w.done = (uint32_t*)calloc(nn, sizeof(uint32_t));
-  if (B->P->turn_aware) {
-    const size_t ne = (size_t)B->g->h.n_edges;
-    w.ed = (float*)malloc(sizeof(float) * ne);
-    w.eu = (uint32_t*)malloc(sizeof(uint32_t) * ne);
-    w.ep = (int32_t*)malloc(sizeof(int32_t) * ne);
-    w.elab = (uint32_t*)calloc(ne, sizeof(uint32_t));
-    w.edone = (uint32_t*)calloc(ne, sizeof(uint32_t));
-  }
+  const size_t nn = (size_t)B->g->h.n_nodes, ne = (size_t)B->g->h.n_edges;
+  w.ek = (uint64_t*)malloc(sizeof(uint64_t) * (ne + 1));
+  w.nk = (uint64_t*)malloc(sizeof(uint64_t) * (nn + 1));
+  w.elab = (uint32_t*)calloc(ne + 1, sizeof(uint32_t));
+  w.nlab = (uint32_t*)calloc(nn + 1, sizeof(uint32_t));
+  w.elist = (int32_t*)malloc(sizeof(int32_t) * (ne + 1));
   orc_counters* C = &B->ctr[A->tid];
   while (1) {
     int t = atomic_fetch_add(&B->next, 1);
@@ -1357,17 +1227,12 @@ static void* worker(void* arg) {
     if (B->phase == 0) phase_a(B, &w, t, C);
     else phase_b(B, &w, t, C);
   }
-  free(w.dist);
-  free(w.pred);
-  free(w.lab);
-  free(w.done);
-  free(w.heap);
-  free(w.ed);
-  free(w.eu);
-  free(w.ep);
+  free(w.ek);
+  free(w.nk);
   free(w.elab);
-  free(w.edone);
-  free(w.eheap);
+  free(w.nlab);
+  free(w.elist);
+  free(w.heap);
   return NULL;
 }
 
@@ -1410,17 +1275,8 @@ int orc_match_batch(const orc_graph* g, const orc_params* p, const orc_report_cf
   B.time = time;
   B.acc = accuracy;
   B.count_unique = keep_stages;
-  if (p->turn_aware) {
-    const int32_t nn = g->h.n_nodes, ne = g->h.n_edges;
-    B.in_off = (int32_t*)calloc((size_t)nn + 1, 4);
-    B.in_edge = (int32_t*)malloc(sizeof(int32_t) * ((size_t)ne + 1));
-    for (int32_t e = 0; e < ne; ++e) B.in_off[g->eto[e] + 1]++;
-    for (int32_t v = 0; v < nn; ++v) B.in_off[v + 1] += B.in_off[v];
-    int32_t* fill = (int32_t*)malloc(sizeof(int32_t) * ((size_t)nn + 1));
-    memcpy(fill, B.in_off, sizeof(int32_t) * (size_t)nn);
-    for (int32_t e = 0; e < ne; ++e) B.in_edge[fill[g->eto[e]]++] = e;
-    free(fill);
-  }
+  B.elen64 = (uint32_t*)malloc(sizeof(uint32_t) * ((size_t)g->h.n_edges + 1));
+  for (int32_t e = 0; e < g->h.n_edges; ++e) B.elen64[e] = (uint32_t)floor((double)g->elen[e] * 64.0 + 0.5);
   for (int d = 0; d <= 180; ++d) B.turn_units[d] = orc_turn_units(p->turn_penalty_factor, d);
   const size_t PP = (size_t)P + 1;
   B.is_col = (uint8_t*)calloc(PP, 1);
@@ -1518,8 +1374,7 @@ int orc_match_batch(const orc_graph* g, const orc_params* p, const orc_report_cf
   }
   free(B.is_col);
   free(B.chain_start);
-  free(B.in_off);
-  free(B.in_edge);
+  free(B.elen64);
   free(B.terr);
   free(B.res);
   free(B.ctr);

@@ -26,7 +26,7 @@
 
 #define ORC_KMAX 32
 #define ORC_MAX_HITS 256         /* distinct edges within one probe radius */
-#define ORC_SEARCH_LIMIT 24576   /* nodes settled by one bounded search   */
+#define ORC_SEARCH_LIMIT 98304   /* labels (edges + nodes) of one bounded search */
 
 typedef struct orc_graph orc_graph;
 
@@ -35,10 +35,6 @@ typedef struct orc_params {
   float interpolation_distance, search_radius, max_search_radius, gps_accuracy;
   int max_candidates;
   float turn_penalty_factor; /* meili auto costing: 200 (0 = no turn costs) */
-  /* experiment: routes chosen by distance + turn cost with a
-     label per (node, incoming edge) instead of by distance alone; 0 = the
-     spec (what the GPU computes) */
-  int turn_aware;
 } orc_params;
 
 typedef struct orc_report_cfg {

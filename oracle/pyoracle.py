@@ -31,7 +31,7 @@ class Params(C.Structure):
     _fields_ = [("sigma_z", C.c_float), ("beta", C.c_float), ("max_route_distance_factor", C.c_float),
                 ("breakage_distance", C.c_float), ("interpolation_distance", C.c_float),
                 ("search_radius", C.c_float), ("max_search_radius", C.c_float), ("gps_accuracy", C.c_float),
-                ("max_candidates", C.c_int), ("turn_penalty_factor", C.c_float), ("turn_aware", C.c_int)]
+                ("max_candidates", C.c_int), ("turn_penalty_factor", C.c_float)]
 
 
 class ReportCfg(C.Structure):

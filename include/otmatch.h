@@ -354,7 +354,7 @@ int otm_get_stage_ms(otm_engine* eng, float* ms, int n);
  * one pair around each launch; enabled with otm_set_timing).  Kernel k is
  * named by otm_kernel_name(k), 0 <= k < OTM_NUM_KERNELS; the stage timings
  * above are sums of these. */
-#define OTM_NUM_KERNELS 20
+#define OTM_NUM_KERNELS 18
 int otm_get_kernel_ms(otm_engine* eng, float* ms, int n);
 const char* otm_kernel_name(int k);
 

@@ -164,6 +164,18 @@ int engine_init(otm_engine* E, const char* graph_path, int device, std::string* 
     E->dp.turn_units = (const uint32_t*)d;
   }
   {
+    // edge costs of the turn-aware searches: L(e) = round(len(e) x 64), in
+    // 1/64 m (DESIGN.md §3 rule 4; the oracle computes the same from the file)
+    const float* len = (const float*)E->host.section(OTMG_EDGE_LEN);
+    std::vector<uint32_t> l64((size_t)h.n_edges + 1, 0u);
+    for (int32_t e = 0; e < h.n_edges; ++e) l64[(size_t)e] = (uint32_t)std::floor((double)len[e] * 64.0 + 0.5);
+    void* d = nullptr;
+    HIPCHK(hipMalloc(&d, l64.size() * 4));
+    HIPCHK(hipMemcpy(d, l64.data(), l64.size() * 4, hipMemcpyHostToDevice));
+    E->graph_allocs.push_back(d);
+    g.e_len64 = (const uint32_t*)d;
+  }
+  {
     // The grid index of the candidate search.  The file's cells (meili's
     // 500 per 0.25 deg tile, ~55 m) may be merged m x m into coarser ones
     // (OTM_GRID_MULT, or grid_mult in the config): a probe's radius box then
@@ -346,17 +358,21 @@ static float auto_index_radius(const otm_engine* E) {
   return (float)(std::ceil(r / 50.0) * 50.0);
 }
 
-// Bounded distance index: part of flattening the graph into HBM, like the
-// tile preprocessing behind valhalla.Configure (py/reporter_service.py:279).
-// Row u = every node within rmax road metres of u, with D and predecessor
-// edge, in a per-row open-addressing table.  Two passes of the same
-// deterministic search: count, size + scan, insert.
+// Bounded route index: part of flattening the graph into HBM, like the tile
+// preprocessing behind valhalla.Configure (py/reporter_service.py:279).  One
+// row per search source of the turn-aware route rule (DESIGN.md §3 rule 4):
+// row e (< E) = the search from edge e's end node entered along e, row E + u =
+// the search from node u with no heading (node candidates); a row holds every
+// label within cost rmax x 64 (edge departure and node arrival labels) with
+// its cost, route distance, turn units and predecessor edge, in a per-row
+// open-addressing table.  Two passes of the same deterministic search: count,
+// size + scan, insert.
 int build_index(otm_engine* E, std::string* err) {
   E->idx = DevIndex{};
   E->idx.rmax = 0.0f;
   if (E->index_rmax < 0.0f) E->index_rmax = auto_index_radius(E);
   if (!(E->index_rmax > 0.0f)) return OTM_OK;
-  const int32_t N = E->g.n_nodes;
+  const int32_t N = E->g.n_edges + E->g.n_nodes;  // rows
   hipStream_t s = E->stream;
   hipEvent_t a, z;
   HIPCHK(hipEventCreate(&a));
@@ -389,7 +405,7 @@ int build_index(otm_engine* E, std::string* err) {
   }
   int64_t total = 0;
   for (int attempt = 0;; ++attempt) {
-    launch_index_build(E->g, E->dp.turn_units, E->index_rmax, row_cnt, nullptr, nullptr, nullptr, false, s);
+    launch_index_build(E->g, E->dp.turn_units, index_cost_bound(E->index_rmax), row_cnt, nullptr, nullptr, nullptr, false, s);
     launch_row_sizes(row_cnt, row_off, N, s);
     scan_i64(row_off, N, tmp, tmpb, s);
     launch_row_pack(row_cnt, row_off, rows, N, s);
@@ -417,7 +433,7 @@ int build_index(otm_engine* E, std::string* err) {
   HIPCHK(hipMemsetAsync(slot, 0xFF, ((size_t)total + 1) * 16, s));
   HIPCHK(hipMalloc(&pred, ((size_t)total + 1) * 4));
   E->graph_allocs.push_back(pred);
-  launch_index_build(E->g, E->dp.turn_units, E->index_rmax, row_cnt, rows, (uint4*)slot, (int32_t*)pred, true, s);
+  launch_index_build(E->g, E->dp.turn_units, index_cost_bound(E->index_rmax), row_cnt, rows, (uint4*)slot, (int32_t*)pred, true, s);
   HIPCHK(hipEventRecord(z, s));
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventSynchronize(z));
@@ -434,16 +450,8 @@ int build_index(otm_engine* E, std::string* err) {
   }
   E->index_slots = total;
   E->idx.rmax = E->index_rmax;
+  E->idx.cmax = index_cost_bound(E->index_rmax);
   E->idx.row = rows;
-  {
-    IdxRow* erow = nullptr;
-    HIPCHK(hipMalloc(&erow, (2 * (size_t)E->g.n_edges + 1) * sizeof(IdxRow)));
-    E->graph_allocs.push_back(erow);
-    launch_edge_rows(E->g, rows, erow, s);
-    HIPCHK(hipGetLastError());
-    HIPCHK(hipStreamSynchronize(s));
-    E->idx.erow = erow;
-  }
   E->idx.slot = (const uint4*)slot;
   E->idx.pred = (const int32_t*)pred;
   return OTM_OK;
@@ -460,7 +468,7 @@ void engine_free(otm_engine* E) {
       &E->cand_xeo,      &E->cand_xem,
       &E->probe,         &E->col_prev,     &E->kq_prev,        &E->trans_off,      &E->trans,          &E->bp,         &E->state,      &E->chosen,
       &E->chain_start,   &E->route_dist,   &E->ipos,   &E->path_off,       &E->path_len,       &E->path_pool,  &E->trace_err,
-      &E->overflow_list0, &E->overflow_list, &E->overflow_list2, &E->counters_i32, &E->scan_tmp, &E->snap,   &E->big_key,
+      &E->overflow_list0, &E->overflow_list2, &E->counters_i32, &E->scan_tmp, &E->snap,   &E->big_key,
       &E->big_lab,       &E->big_inq,      &E->big_fr,         &E->o_traces,       &E->o_seg_cnt,  &E->o_way_cnt,
       &E->o_segments,    &E->o_seg_gidx,   &E->o_way_ids,      &E->o_reports,  &E->o_rep_cnt,  &E->seg_ub,
       &E->f_seg_off,     &E->f_way_off,    &E->f_rep_off,      &E->f_segs,     &E->f_ways,     &E->f_reps,
@@ -530,7 +538,6 @@ static int engine_match_once(otm_engine* E, const DevBatch& b, hipStream_t s, st
   ENS(path_len, Pn * 4);
   ENS(trace_err, ((size_t)NT + 1) * 4);
   ENS(overflow_list0, Pn * 4);
-  ENS(overflow_list, Pn * 4);
   ENS(overflow_list2, Pn * 4);
   ENS(counters_i32, 64);
   ENS(snap, 192 + sizeof(BatchStatus));
@@ -590,7 +597,6 @@ static int engine_match_once(otm_engine* E, const DevBatch& b, hipStream_t s, st
   w.pool_cap = E->pool_cap;
   w.trace_err = P<int32_t>(E->trace_err);
   w.overflow_list0 = P<int32_t>(E->overflow_list0);
-  w.overflow_list = P<int32_t>(E->overflow_list);
   w.overflow_list2 = P<int32_t>(E->overflow_list2);
   w.idx = E->idx;
   w.counters_i32 = P<int32_t>(E->counters_i32);
@@ -1027,10 +1033,10 @@ int engine_spill_stats(otm_engine* E, otm_spill_stats* out) {
   // spills, [3] LDS-wave spills (per stage)
   out->cand_wave = v[5];
   out->trans_online = v[16 + 4];
-  out->trans_wave = v[16 + 0];
+  out->trans_wave = v[16 + 4];
   out->trans_global = v[16 + 3];
   out->route_online = v[32 + 4];
-  out->route_wave = v[32 + 0];
+  out->route_wave = v[32 + 4];
   out->route_global = v[32 + 3];
   out->pad = 0;
   return OTM_OK;

@@ -5,11 +5,12 @@
 //   K2 k_candidates   wave / probe     grid cells -> projections -> LDS edge hash
 //                                      -> bitonic sort -> top-K + emission
 //   K3 k_links        thread / point   chain links + transition-matrix sizes, scan
-//   K4 k_transitions  wave / column    bounded label-correcting search per source
-//                                      node, frontier + labels in LDS (global
-//                                      tier on LDS overflow)
+//   K4 k_trans_sub    8/16 lanes / col route-index probes per (source, target)
+//                                      pair; k_transitions: turn-aware search
+//                                      per source for what the index cannot
+//                                      answer (LDS, then global tier)
 //   K5 k_viterbi      wave / trace     min-sum decode, lanes = states
-//   K6 k_route        wave / step      re-run the winning search, predecessors
+//   K6 k_route_index  thread / step    the winning label's predecessor chain (k_route: search)
 //   K7 k_segments     thread / trace   traversals -> OSMLR segments (count+write)
 //   K8 k_report       thread / trace   reporter_service.py:110-215 + histogram
 #pragma once
@@ -23,10 +24,11 @@ constexpr int KMAX = 32;           // max candidates per column (== ORC_KMAX)
 constexpr int KIN = 8;             // inline candidate slots per point (DevWork::cand_eo / cand_em)
 constexpr int KX = KMAX - KIN;     // overflow candidate slots per point (DevWork::cand_xeo / cand_xem)
 constexpr int MAX_HITS = 256;      // distinct edges within one radius (spec limit)
-constexpr int SEARCH_LIMIT = 24576;  // nodes settled by one search (spec limit)
+constexpr int SEARCH_LIMIT = 98304;  // labels (edges + nodes) of one search (spec limit, == ORC_SEARCH_LIMIT)
 constexpr int LDS_TABLE_CAP = 256;   // K4/K6 LDS tier: table slots
-constexpr int LDS_TABLE_LIMIT = 192; // ... nodes before spilling to the global tier
-constexpr int BIG_TABLE_CAP = 32768; // global tier table slots (> SEARCH_LIMIT / 0.75)
+constexpr int LDS_TABLE_LIMIT = 192; // ... labels before spilling to the global tier
+constexpr int BIG_TABLE_LOG2 = 17;
+constexpr int BIG_TABLE_CAP = 1 << BIG_TABLE_LOG2;  // global tier table slots (> SEARCH_LIMIT / 0.75)
 constexpr int BIG_SLOTS = 128;       // concurrent global-tier searches
 
 struct DevGraph {
@@ -45,6 +47,7 @@ struct DevGraph {
   const uint32_t* cell_ent;
   const float4* ent_geo;  // per cell entry: shape segment endpoints (lat_a, lon_a, lat_b, lon_b)
   const uint16_t *e_head_out, *e_head_in;  // edge bearing at start / end, whole degrees (turn costs)
+  const uint32_t* e_len64;                 // L(e) = round(len(e) x 64): the route searches' edge costs (1/64 m)
   int32_t n_nodes, n_edges, n_segments, grid_rows, grid_cols;
   double lat0, lon0, cell;
   // spatial work order tiles: the node bbox cut into ORDER_SIDE^2 tiles
@@ -72,30 +75,36 @@ struct DevOrder {
   int32_t* cursor;    // [ORDER_TILES] scatter cursors
 };
 
-// Bounded distance index (built once per engine): for every
-// node u the nodes v with D(u,v) <= rmax, with D and the predecessor edge of
-// the search fixed point, held as one open-addressing hash table per row
-// (linear probing) so a lookup is about one 16-byte read.  A slot also
-// carries what the turn cost of the route u -> v needs: the turn units
-// between its own edges and the headings of its first and last edge.  cnt < 0
-// marks a row whose search exceeded the build table (queries on it use the
-// online tiers).
+// Bounded route index (built once per engine): one row per
+// source of the turn-aware route search -- row e < E: from edge e's end node,
+// entered along e; row E + u: from node u, no heading (node candidates) --
+// holding every label of that search within cost cmax (1/64 m): the departure
+// label of each edge (key = edge id) and the arrival label of each node (key
+// = NODE_KEY | node), as one open-addressing hash table per row (linear
+// probing).  A slot is {key, cost, route distance bits, turn units}: the
+// route to the edge's start turned into it (or to the node), so a transition
+// reads its distance and turn cost from one slot; predecessor edges in a
+// parallel array give the route.  cnt < 0 marks a row whose search exceeded
+// the build table (queries on it use the online tiers).
 struct IdxRow {
   int64_t off;    // first slot of the row's table
   int32_t cnt;    // entries, -1 incomplete
   uint32_t cap;   // table slots (0 for an empty or incomplete row)
 };
 struct DevIndex {
-  float rmax;  // 0: no index
-  const IdxRow* row;
-  const IdxRow* erow;    // [2E]: per edge the row of its end node, then of its start node (node candidates)
-  // {node (0xFFFFFFFF empty), D bits, turn units between the route's edges,
-  //  head_out(first edge) | head_in(last edge) << 16 (0xFFFFFFFF: v == u)}
+  float rmax;     // 0: no index
+  uint32_t cmax;  // its cost bound, floor(rmax x 64)
+  const IdxRow* row;   // [E + N]
   const uint4* slot;
   const int32_t* pred;   // per slot
 };
-constexpr int INDEX_BUILD_CAP = 2048;   // LDS table of the index builder
-constexpr int INDEX_BUILD_LIMIT = 1536; // nodes per row before the row is left incomplete
+constexpr uint32_t NODE_KEY = 0x80000000u;  // key of a node's arrival label (edges: their id, < 2^27)
+constexpr uint32_t NONE_PRED = 0xFFFFFFFFu; // label predecessor of a route's first edge / the source node
+constexpr int INDEX_BUILD_LOG2 = 11;
+constexpr int INDEX_BUILD_CAP = 1 << INDEX_BUILD_LOG2;  // LDS table of the index builder
+constexpr int INDEX_BUILD_LIMIT = 1536; // labels per row before the row is left incomplete
+// cost bound (1/64 m) of a search bounded by B metres (oracle cost_bound)
+__host__ __device__ inline uint32_t index_cost_bound(float B) { return (uint32_t)floor((double)B * 64.0); }
 
 // which kernels walk the spatial work order (env OTM_ORDER_MASK)
 constexpr int ORDER_CAND = 1, ORDER_TRANS = 2, ORDER_ROUTE = 4;
@@ -168,11 +177,10 @@ struct DevWork {
   int32_t pool_cap;
   int32_t* trace_err;    // [T]
   int32_t* overflow_list0; // [P] columns/steps the index could not answer
-  int32_t* overflow_list;  // [P] columns/steps the lane tier spilled
-  int32_t* overflow_list2; // [P] ... the LDS wave tier spilled
+  int32_t* overflow_list2; // [P] ... the LDS search tier spilled (and k_trans_sub's wide columns)
   int32_t* snap;           // [48] spill snapshots A (after K2), B (after K4), C (after K6)
-  int32_t* counters_i32;   // [0] list 1 count, [1] pool used, [2] pool overflow flag, [3] list 2 count,
-                           // [4] list 0 count
+  int32_t* counters_i32;   // [1] pool used, [2] pool overflow flag, [3] list 2 count, [4] list 0 count,
+                           // [6] wide list count
   int32_t* abort;          // [1] set when a capacity (transition matrices, path pool) was exceeded:
                            // every later kernel returns at once and the host redoes the batch
   int64_t trans_cap;       // floats allocated for w.trans
@@ -220,12 +228,10 @@ enum KernelId {
   KN_SCAN_TRANS,
   KN_TRANS_INDEX,
   KN_TRANS_WIDE,
-  KN_TRANS_LANE,
   KN_TRANS_WAVE,
   KN_TRANS_GLOBAL,
   KN_VITERBI,
   KN_ROUTE_INDEX,
-  KN_ROUTE_LANE,
   KN_ROUTE_WAVE,
   KN_ROUTE_GLOBAL,
   KN_SEG_BOUND,
@@ -253,8 +259,8 @@ void launch_candidates(const DevGraph& g, const DevBatch& b, const DevParams& p,
 void launch_links(const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s, const Marks& mk);
 // sets *w.abort when the scanned transition total exceeds w.trans_cap
 void launch_cap_check(const DevBatch& b, DevWork& w, hipStream_t s);
-// lane tier -> wave LDS tier -> global tier, spill lists on the device
-// (counters_i32[0] / [3] must be zero on entry)
+// index tier -> LDS search tier -> global tier, spill lists on the device
+// (counters_i32[3] / [4] / [6] must be zero on entry)
 void launch_transitions(const DevGraph& g, const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s,
                         const Marks& mk, int sub);
 void launch_viterbi(const DevBatch& b, DevWork& w, hipStream_t s, const Marks& mk);
@@ -276,7 +282,7 @@ void launch_compact(int32_t n_traces, const DevOut& o, const int32_t* seg_off, c
                     hipStream_t s);
 // index build: pass 0 counts rows (row_cnt), pass 1 inserts them into the
 // row tables (slot array pre-filled with 0xFF)
-void launch_index_build(const DevGraph& g, const uint32_t* turn_units, float rmax, int32_t* row_cnt,
+void launch_index_build(const DevGraph& g, const uint32_t* turn_units, uint32_t cmax, int32_t* row_cnt,
                         const IdxRow* rows, uint4* slot, int32_t* pred, bool write, hipStream_t s);
 void launch_row_sizes(const int32_t* row_cnt, int64_t* row_sizes, int32_t n, hipStream_t s);
 struct BatchStatus {
@@ -291,7 +297,6 @@ bool fold_bookkeeping();
 void launch_status(const int32_t* abort, const int64_t* ttotal, const int32_t* counters, BatchStatus* out,
                    hipStream_t s);
 void launch_row_pack(const int32_t* row_cnt, const int64_t* row_off, IdxRow* rows, int32_t n, hipStream_t s);
-void launch_edge_rows(const DevGraph& g, const IdxRow* rows, IdxRow* erow, hipStream_t s);
 // exclusive scan helpers (in place over n+1 elements: out[n] = total)
 void scan_i64(int64_t* d, int64_t n, void* tmp, size_t tmp_bytes, hipStream_t s);
 // exclusive scans of three per-trace counts (n <= FETCH_SCAN_MAX) in one

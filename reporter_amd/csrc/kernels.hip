@@ -994,23 +994,27 @@ __global__ void k_cap_check(DevBatch b, DevWork w) {
 
 
 
-// ============================================================== bounded search
-// Label-correcting single-source search in one wavefront.  Labels are 64-bit
-// (float distance bits << 32 | predecessor edge) updated with atomicMin, so
-// every label converges to the lexicographic minimum of (D(w)+len(e), e) over
-// in-edges: the unique fixed point, equal to what the oracle's Dijkstra (with
-// its (distance, edge) tie rule) computes, whatever the relaxation order.
-// Non-negative weights and monotone float rounding make "D(v) <= B" a
-// property of v alone, so the set of nodes ever inserted is exactly
-// {v : D(v) <= B} and the node count is order-independent too.
+// ============================================================== turn-aware bounded search
+// DESIGN.md §3 rule 4 (oracle ta_search): the route of a transition is the
+// cheapest by distance plus turn penalty.  A search from node u entered with
+// heading hin labels every edge g with its departure label -- the cheapest way
+// to be at g's start, turned into it -- and every node v with its arrival
+// label, each a 64-bit key cost << 32 | predecessor edge (costs in 1/64 m:
+// L(e) = round(len x 64) per edge, turn units per turn), bounded by cost cmax.
+// Label-correcting in one wavefront with 64-bit atomicMin: every label
+// converges to the minimum over its in-steps, the unique fixed point (every
+// step costs > 0), which the oracle's Dijkstra computes -- whatever the
+// relaxation order.  A key enters the table once (the set of keys ever
+// inserted is exactly those whose label is within cmax), so the count is
+// order-free too.
 struct Table {
-  uint32_t* key;            // node id or EMPTY
-  unsigned long long* lab;  // (dist bits << 32) | pred edge
+  uint32_t* key;            // edge id, NODE_KEY | node, or EMPTY
+  unsigned long long* lab;  // cost << 32 | predecessor edge
   uint32_t* inq;            // in next frontier
   uint32_t* fr0;            // frontier A (slot ids)
   uint32_t* fr1;            // frontier B
   int cap_log2;
-  int limit;                // max nodes before overflow
+  int limit;                // max labels before overflow
 };
 
 template <bool BIG>
@@ -1055,359 +1059,164 @@ __device__ __forceinline__ int table_find(const Table& T, uint32_t v) {
   return -1;
 }
 
-// returns >= 0 nodes settled, or -1 on overflow (more than T.limit nodes)
+// lower key's label to nl (inserting the key); an edge key whose cost fell
+// joins the next frontier
 template <bool BIG>
-__device__ int wave_search(const DevGraph& g, const Table& T, SearchShared& S, int32_t u, float B, int lane) {
+__device__ __forceinline__ void ta_relax(const Table& T, SearchShared& S, uint32_t* nxt, uint32_t key,
+                                         unsigned long long nl) {
+  const uint32_t mask = (1u << T.cap_log2) - 1u;
+  uint32_t slot = hash32(key) >> (32 - T.cap_log2);
+  int found = -1;
+  for (int i = 0; i <= (int)mask; ++i) {
+    const uint32_t old = atomicCAS(&T.key[slot], EMPTY, key);
+    if (old == EMPTY) {
+      if (atomicAdd(&S.count, 1) >= T.limit) S.over = 1;
+      found = (int)slot;
+      break;
+    }
+    if (old == key) {
+      found = (int)slot;
+      break;
+    }
+    slot = (slot + 1) & mask;
+  }
+  if (found < 0) {
+    S.over = 1;
+    return;
+  }
+  const unsigned long long old = atomicMin(&T.lab[found], nl);
+  // successors depend on the cost alone (their predecessor is this edge)
+  if (!(key & NODE_KEY) && nl < old && (uint32_t)(old >> 32) != (uint32_t)(nl >> 32)) {
+    if (atomicExch(&T.inq[found], 1u) == 0u) {
+      const int idx = atomicAdd(&S.nnext, 1);
+      Mem<BIG>::st(&nxt[idx], (uint32_t)found);
+    }
+  }
+}
+
+// returns >= 0 labels, or -1 on overflow (more than T.limit)
+template <bool BIG>
+__device__ int ta_search(const DevGraph& g, const uint32_t* TU, const Table& T, SearchShared& S, int32_t u,
+                         uint32_t hin, uint32_t cmax, int lane) {
   const int cap = 1 << T.cap_log2;
-  const uint32_t mask = (uint32_t)cap - 1u;
   for (int i = lane; i < cap; i += TB) {
     Mem<BIG>::st(&T.key[i], EMPTY);
     Mem<BIG>::st(&T.lab[i], LAB_NONE);
     Mem<BIG>::st(&T.inq[i], 0u);
   }
-  __syncthreads();
   if (lane == 0) {
-    const uint32_t slot = hash32((uint32_t)u) >> (32 - T.cap_log2);
-    Mem<BIG>::st(&T.key[slot], (uint32_t)u);
-    Mem<BIG>::st(&T.lab[slot], ((unsigned long long)fbits(0.0f) << 32) | 0xFFFFFFFFull);
-    Mem<BIG>::st(&T.inq[slot], 1u);
-    Mem<BIG>::st(&T.fr0[0], slot);
-    S.nfr = 1;
-    S.count = 1;
+    S.nfr = 0;
+    S.nnext = 0;
+    S.count = 0;
     S.over = 0;
   }
   __syncthreads();
   uint32_t* cur = T.fr0;
   uint32_t* nxt = T.fr1;
+  // the source node (arrival 0) and the route's possible first edges
+  if (lane == 0) ta_relax<BIG>(T, S, nxt, NODE_KEY | (uint32_t)u, (unsigned long long)NONE_PRED);
+  const int32_t e0 = g.out_off[u], e1 = g.out_off[u + 1];
+  for (int32_t e = e0 + lane; e < e1; e += TB) {
+    const uint32_t c = turn_units(TU, hin, g.e_head_out[e]);
+    if (c <= cmax) ta_relax<BIG>(T, S, nxt, (uint32_t)e, ((unsigned long long)c << 32) | NONE_PRED);
+  }
+  __syncthreads();
   while (true) {
-    const int nfr = S.nfr;
-    if (nfr == 0) break;
-    if (lane == 0) S.nnext = 0;
-    __syncthreads();
-    for (int f = lane; f < nfr; f += TB) {
-      const uint32_t s = Mem<BIG>::ld(&cur[f]);
-      if (BIG) atomicExch(&T.inq[s], 0u);
-      else T.inq[s] = 0u;
-      const int32_t n = (int32_t)Mem<BIG>::ld(&T.key[s]);
-      const float d = bitsf((uint32_t)(Mem<BIG>::ld(&T.lab[s]) >> 32));
-      const int32_t e0 = g.out_off[n], e1 = g.out_off[n + 1];
-      for (int32_t e = e0; e < e1; ++e) {
-        const float nd = d + g.e_len[e];
-        if (!(nd <= B)) continue;
-        const uint32_t v = (uint32_t)g.e_to[e];
-        uint32_t slot = hash32(v) >> (32 - T.cap_log2);
-        int found = -1;
-        for (int i = 0; i < cap; ++i) {
-          const uint32_t old = atomicCAS(&T.key[slot], EMPTY, v);
-          if (old == EMPTY) {
-            if (atomicAdd(&S.count, 1) >= T.limit) S.over = 1;
-            found = (int)slot;
-            break;
-          }
-          if (old == v) {
-            found = (int)slot;
-            break;
-          }
-          slot = (slot + 1) & mask;
-        }
-        if (found < 0) {
-          S.over = 1;
-          continue;
-        }
-        const unsigned long long nl = ((unsigned long long)fbits(nd) << 32) | (unsigned long long)(uint32_t)e;
-        const unsigned long long old = atomicMin(&T.lab[found], nl);
-        if (nl < old && (uint32_t)(old >> 32) != fbits(nd)) {
-          if (atomicExch(&T.inq[found], 1u) == 0u) {
-            const int idx = atomicAdd(&S.nnext, 1);
-            Mem<BIG>::st(&nxt[idx], (uint32_t)found);
-          }
-        }
-      }
+    if (lane == 0) {
+      S.nfr = S.nnext;
+      S.nnext = 0;
     }
-    __syncthreads();
-    const bool over = S.over != 0;
-    if (lane == 0) S.nfr = S.nnext;
     uint32_t* tmp = cur;
     cur = nxt;
     nxt = tmp;
     __syncthreads();
-    if (over) return -1;
+    const int nfr = S.nfr;
+    if (nfr == 0 || S.over) break;
+    for (int f = lane; f < nfr; f += TB) {
+      const uint32_t sl = Mem<BIG>::ld(&cur[f]);
+      if (BIG) atomicExch(&T.inq[sl], 0u);
+      else T.inq[sl] = 0u;
+      const int32_t e = (int32_t)Mem<BIG>::ld(&T.key[sl]);
+      const unsigned long long ca =
+          (unsigned long long)(uint32_t)(Mem<BIG>::ld(&T.lab[sl]) >> 32) + (unsigned long long)g.e_len64[e];
+      if (ca > cmax) continue;
+      const int32_t v = g.e_to[e];
+      ta_relax<BIG>(T, S, nxt, NODE_KEY | (uint32_t)v, (ca << 32) | (uint32_t)e);
+      const uint32_t hv = g.e_head_in[e];
+      for (int32_t h = g.out_off[v]; h < g.out_off[v + 1]; ++h) {
+        const unsigned long long c = ca + turn_units(TU, hv, g.e_head_out[h]);
+        if (c <= cmax) ta_relax<BIG>(T, S, nxt, (uint32_t)h, (c << 32) | (uint32_t)e);
+      }
+    }
+    __syncthreads();
   }
-  return S.count;
+  const bool over = S.over != 0;
+  const int count = S.count;
+  __syncthreads();
+  return over ? -1 : count;
 }
 
-// edges relaxed by the equivalent Dijkstra = sum of out-degrees of settled nodes
+// work counts of a converged search (oracle ta_search's counters): the
+// departure labels, and the edges they relax (their end node's out-edges,
+// when the arrival is within the bound)
 template <bool BIG>
-__device__ unsigned long long settled_outdeg(const DevGraph& g, const Table& T, int lane) {
-  unsigned long long s = 0;
+__device__ void ta_counts(const DevGraph& g, const Table& T, uint32_t cmax, int lane, unsigned long long& settled,
+                          unsigned long long& relaxed) {
+  unsigned long long st = 0, rl = 0;
   const int cap = 1 << T.cap_log2;
   for (int i = lane; i < cap; i += TB) {
     const uint32_t k = Mem<BIG>::ld(&T.key[i]);
-    if (k != EMPTY) s += (unsigned long long)(g.out_off[k + 1] - g.out_off[k]);
+    if (k == EMPTY || (k & NODE_KEY)) continue;
+    ++st;
+    const unsigned long long ca = (Mem<BIG>::ld(&T.lab[i]) >> 32) + (unsigned long long)g.e_len64[k];
+    if (ca <= cmax) rl += (unsigned long long)(g.out_off[g.e_to[k] + 1] - g.out_off[g.e_to[k]]);
   }
-  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
-  return s;
+  for (int o = 32; o > 0; o >>= 1) {
+    st += __shfl_xor(st, o, 64);
+    rl += __shfl_xor(rl, o, 64);
+  }
+  settled = st;
+  relaxed = rl;
 }
 
-// ============================================================== lane tier
-// Most bounded searches are tiny (city config: ~9 nodes settled, ~35 edges
-// relaxed), so the first tier runs one search per LANE: a plain Dijkstra with
-// linear-scan selection over a private table of LANE_CAP slots in LDS,
-// interleaved by thread (slot k of thread t at [k * blockDim + t]) so the 64
-// lanes of a wave hit 64 different banks.  Same fixed point as the wave tiers
-// (labels are the lexicographic min of (D(w)+len(e), e)); a search that needs
-// more than LANE_CAP nodes spills its whole column to the wave tier.
-constexpr uint32_t DONE = 0x80000000u;
-constexpr int LANE_TB = 128;
-// Below this many index misses the lane tier forwards its list to the wave
-// tier untouched: a few serial single-lane searches (~100+ us of dependent
-// LDS and global latency) would cost more than the wave tier's parallel ones.
-constexpr int64_t LANE_TIER_MIN = 4096;
-
-// PRED: keep predecessor edges (the route stage needs them, transitions only
-// need distances -- 8 instead of 12 bytes per slot buys a larger table)
-template <int CAP, bool PRED>
-__device__ __forceinline__ int lane_search(const DevGraph& g, uint32_t* K, float* D, int32_t* Pd, int32_t u, float B,
-                                           unsigned long long& relaxed) {
-  constexpr int S = LANE_TB;
-  K[0] = (uint32_t)u;
-  D[0] = 0.0f;
-  if (PRED) Pd[0] = -1;
-  int n = 1;
-  while (true) {
-    int best = -1;
-    float bd = 0.0f;
-    for (int k = 0; k < n; ++k) {
-      if (!(K[k * S] & DONE)) {
-        const float d = D[k * S];
-        if (best < 0 || d < bd) {
-          best = k;
-          bd = d;
-        }
-      }
-    }
-    if (best < 0) break;
-    const uint32_t x = K[best * S];
-    K[best * S] = x | DONE;
-    const int32_t e0 = g.out_off[x], e1 = g.out_off[x + 1];
-    relaxed += (unsigned long long)(e1 - e0);
-    for (int32_t e = e0; e < e1; ++e) {
-      const float nd = bd + g.e_len[e];
-      if (!(nd <= B)) continue;
-      const uint32_t v = (uint32_t)g.e_to[e];
-      int f = -1;
-      for (int k = 0; k < n; ++k)
-        if ((K[k * S] & ~DONE) == v) {
-          f = k;
-          break;
-        }
-      if (f < 0) {
-        if (n == CAP) return -1;
-        K[n * S] = v;
-        D[n * S] = nd;
-        if (PRED) Pd[n * S] = e;
-        ++n;
-      } else {
-        const float dv = D[f * S];
-        if (nd < dv) {
-          D[f * S] = nd;
-          if (PRED) Pd[f * S] = e;
-        } else if (PRED && nd == dv && e < Pd[f * S]) {
-          Pd[f * S] = e;
-        }
-      }
-    }
+// The route a converged label ends: its predecessor chain (fully traversed
+// edges), walked back from `pred0` into the lane's LDS buffer buf (stride TB,
+// CHAIN_BUF entries; a longer chain is re-walked per edge), then summed in
+// route order: the distance d and the turn units from heading hin through the
+// chain, plus the turn into hout (NO_HEAD: none).  predof(e) = e's departure
+// label's predecessor.
+constexpr int CHAIN_BUF = 32;
+template <class F>
+__device__ void chain_sums(const DevGraph& g, const uint32_t* TU, F predof, uint32_t pred0, uint32_t hin,
+                           uint32_t hout, int32_t* buf, float& d, uint32_t& units, int& n) {
+  int cnt = 0;
+  for (uint32_t p = pred0; p != NONE_PRED && cnt <= SEARCH_LIMIT; p = predof(p)) {
+    if (cnt < CHAIN_BUF) buf[cnt * TB] = (int32_t)p;
+    ++cnt;
   }
-  return n;
-}
-
-template <int CAP>
-__device__ __forceinline__ int lane_find(const uint32_t* K, int n, uint32_t v) {
-  for (int k = 0; k < n; ++k)
-    if ((K[k * LANE_TB] & ~DONE) == v) return k;
-  return -1;
-}
-
-template <int CAP>
-__global__ __launch_bounds__(LANE_TB) void k_trans_lane(DevGraph g, DevBatch b, DevParams P, DevWork w) {
-  if (*w.abort || trans_over_cap(b, w)) return;  // a capacity was exceeded: the host redoes the batch
-  __shared__ uint32_t sK[CAP * LANE_TB];
-  __shared__ float sD[CAP * LANE_TB];
-  __shared__ int32_t sP[CAP * LANE_TB];  // predecessor edges: the routes' turns
-  uint32_t* K = sK + threadIdx.x;
-  float* D = sD + threadIdx.x;
-  int32_t* Pd = sP + threadIdx.x;
-  unsigned long long c_search = 0, c_settled = 0, c_relaxed = 0, c_trans = 0;
-  const int64_t nwork = w.counters_i32[4];  // columns the index could not answer
-  if (nwork < LANE_TIER_MIN) {
-    // a handful of misses: one lane's serial search would set the stage's
-    // latency, so hand them all to the wave tier as they are
-    for (int64_t it = (int64_t)blockIdx.x * LANE_TB + threadIdx.x; it < nwork; it += (int64_t)gridDim.x * LANE_TB)
-      w.overflow_list[atomicAdd(&w.counters_i32[0], 1)] = w.overflow_list0[it];
-    return;
-  }
-  for (int64_t it = (int64_t)blockIdx.x * LANE_TB + threadIdx.x; it < nwork; it += (int64_t)gridDim.x * LANE_TB) {
-    const int64_t p = w.overflow_list0[it];
-    const int32_t q = w.col_prev[p];
-    const int Kq = w.ncand[q], Kp = w.ncand[p];
-    const float gcv = w.gc[p];
-    const float bound = P.factor * gcv;
-    float* Tm = w.trans + w.trans_off[p];
-    unsigned long long s_search = 0, s_settled = 0, s_relaxed = 0, s_trans = 0;
-    bool failed = false;
-    for (int i = 0; i < Kq && !failed; ++i) {
-      const int2 ri = crec(w, q, i);
-      const int32_t u = src_node(g, ri.x, __int_as_float(ri.y));
-      bool first = true;
-      for (int k = 0; k < i; ++k)
-        if (const int2 rk = crec(w, q, k); src_node(g, rk.x, __int_as_float(rk.y)) == u) {
-          first = false;
-          break;
-        }
-      if (!first) continue;
-      unsigned long long rel = 0;
-      const int n = lane_search<CAP, true>(g, K, D, Pd, u, bound, rel);
-      if (n < 0) {
-        failed = true;
-        break;
-      }
-      ++s_search;
-      s_settled += (unsigned long long)n;
-      s_relaxed += rel;
-      for (int ii = i; ii < Kq; ++ii) {
-        const int2 rii = crec(w, q, ii);
-        const int32_t ei = rii.x;
-        const float oi = __int_as_float(rii.y);
-        if (src_node(g, ei, oi) != u) continue;
-        const float start = src_start(g, ei, oi);
-        for (int j = 0; j < Kp; ++j) {
-          const int2 rj = crec(w, p, j);
-          const int32_t ej = rj.x;
-          const float oj = __int_as_float(rj.y);
-          float r;
-          bool ok = true;
-          int f = -1;
-          const bool same = ej == ei && oj >= oi;
-          if (same) {
-            r = oj - oi;
-          } else {
-            f = lane_find<CAP>(K, n, (uint32_t)g.e_from[ej]);
-            if (f < 0) {
-              ok = false;
-              r = 0.0f;
-            } else {
-              const float sd = start + D[f * LANE_TB];
-              r = sd + oj;
-            }
-          }
-          float cost = INFINITY;
-          if (ok && r <= bound) {
-            // the route's turns, walked back from e_j's start node to u
-            uint32_t units = 0;
-            if (!same) {
-              uint32_t hn = dst_head(g, ej, oj);
-              while ((K[f * LANE_TB] & ~DONE) != (uint32_t)u) {
-                const int32_t e = Pd[f * LANE_TB];
-                units += turn_units(P.turn_units, g.e_head_in[e], hn);
-                hn = g.e_head_out[e];
-                f = lane_find<CAP>(K, n, (uint32_t)g.e_from[e]);
-              }
-              units += turn_units(P.turn_units, src_head(g, ei, oi), hn);
-            }
-            cost = trans_cost(units, r, gcv, P.beta);
-            ++s_trans;
-          }
-          Tm[ii * Kp + j] = cost;
-        }
-      }
-    }
-    if (failed) {
-      const int slot = atomicAdd(&w.counters_i32[0], 1);
-      w.overflow_list[slot] = (int32_t)p;
+  float dd = 0.0f;
+  unsigned long long un = 0;
+  uint32_t h = hin;
+  for (int m = cnt - 1; m >= 0; --m) {
+    int32_t e;
+    if (cnt <= CHAIN_BUF) {
+      e = buf[m * TB];
     } else {
-      c_search += s_search;
-      c_settled += s_settled;
-      c_relaxed += s_relaxed;
-      c_trans += s_trans;
+      uint32_t x = pred0;
+      for (int k = 0; k < m; ++k) x = predof(x);
+      e = (int32_t)x;
     }
+    un += turn_units(TU, h, g.e_head_out[e]);
+    dd = dd + g.e_len[e];
+    h = g.e_head_in[e];
   }
-  if (w.ctr) {
-    cadd(&w.ctr->searches, c_search);
-    cadd(&w.ctr->nodes_settled, c_settled);
-    cadd(&w.ctr->edges_relaxed, c_relaxed);
-    cadd(&w.ctr->transitions, c_trans);
-  }
+  un += turn_units(TU, h, hout);
+  d = dd;
+  units = un > TURN_UNITS_MAX ? TURN_UNITS_MAX : (uint32_t)un;
+  n = cnt;
 }
 
-template <int CAP>
-__global__ __launch_bounds__(LANE_TB) void k_route_lane(DevGraph g, DevBatch b, DevParams P, DevWork w) {
-  if (*w.abort) return;  // a capacity was exceeded: the host redoes the batch
-  __shared__ uint32_t sK[CAP * LANE_TB];
-  __shared__ float sD[CAP * LANE_TB];
-  __shared__ int32_t sP[CAP * LANE_TB];
-  uint32_t* K = sK + threadIdx.x;
-  float* D = sD + threadIdx.x;
-  int32_t* Pd = sP + threadIdx.x;
-  unsigned long long c_search = 0, c_settled = 0, c_relaxed = 0, c_edges = 0;
-  const int64_t nwork = w.counters_i32[4];  // steps the index could not answer
-  if (nwork < LANE_TIER_MIN) {  // as in k_trans_lane
-    for (int64_t it = (int64_t)blockIdx.x * LANE_TB + threadIdx.x; it < nwork; it += (int64_t)gridDim.x * LANE_TB)
-      w.overflow_list[atomicAdd(&w.counters_i32[0], 1)] = w.overflow_list0[it];
-    return;
-  }
-  for (int64_t it = (int64_t)blockIdx.x * LANE_TB + threadIdx.x; it < nwork; it += (int64_t)gridDim.x * LANE_TB) {
-    const int64_t p = w.overflow_list0[it];
-    const int32_t q = w.col_prev[p];
-    const int2 ci = w.chosen[q], cj = w.chosen[p];
-    const int32_t ei = ci.x, ej = cj.x;
-    const float oi = __int_as_float(ci.y), oj = __int_as_float(cj.y);
-    const float bound = P.factor * w.gc[p];
-    const int32_t u = src_node(g, ei, oi), v = g.e_from[ej];
-    unsigned long long rel = 0;
-    const int n = lane_search<CAP, true>(g, K, D, Pd, u, bound, rel);
-    if (n < 0) {
-      const int slot = atomicAdd(&w.counters_i32[0], 1);
-      w.overflow_list[slot] = (int32_t)p;
-      continue;
-    }
-    const int fv = lane_find<CAP>(K, n, (uint32_t)v);
-    int len = 0;
-    for (int f = fv; (K[f * LANE_TB] & ~DONE) != (uint32_t)u;) {
-      ++len;
-      f = lane_find<CAP>(K, n, (uint32_t)g.e_from[Pd[f * LANE_TB]]);
-    }
-    const int off = len ? atomicAdd(&w.counters_i32[1], len) : 0;
-    if (off + len > w.pool_cap) {
-      w.counters_i32[2] = 1;
-      *w.abort = 1;
-      w.path_len[p] = -1;
-    } else {
-      int k = len;
-      for (int f = fv; (K[f * LANE_TB] & ~DONE) != (uint32_t)u;) {
-        const int32_t pe = Pd[f * LANE_TB];
-        w.path_pool[off + (--k)] = pe;
-        f = lane_find<CAP>(K, n, (uint32_t)g.e_from[pe]);
-      }
-      w.path_off[p] = off;
-      w.path_len[p] = len;
-    }
-    const float start = src_start(g, ei, oi);
-    const float sd = start + D[fv * LANE_TB];
-    w.route_dist[p] = sd + oj;
-    ++c_search;
-    c_settled += (unsigned long long)n;
-    c_relaxed += rel;
-    c_edges += (unsigned long long)len;
-  }
-  if (w.ctr) {
-    cadd(&w.ctr->route_searches, c_search);
-    cadd(&w.ctr->route_nodes_settled, c_settled);
-    cadd(&w.ctr->route_edges_relaxed, c_relaxed);
-    cadd(&w.ctr->route_edges, c_edges);
-  }
-}
-
-// ============================================================== distance index
+// ============================================================== route index
 __device__ __forceinline__ uint32_t idx_hash(uint32_t v) {
   v ^= v >> 16;
   v *= 0x85ebca6bu;
@@ -1446,9 +1255,9 @@ __device__ __forceinline__ uint32_t idx_next(uint32_t h, const IdxRow& R) {
   return h + 1u == R.cap ? 0u : h + 1u;
 }
 
-// Row lookup: linear probing in u's table.  Returns the slot (its contents in
-// *out) when v is in the row, -1 when absent (D(u,v) > rmax), -2 when the row
-// is incomplete.
+// Row lookup: linear probing in the row's table.  Returns the slot (its
+// contents in *out) when the key is in the row, -1 when absent (its label
+// beyond cmax), -2 when the row is incomplete.
 __device__ __forceinline__ int64_t idx_find(const DevIndex& X, const IdxRow& R, uint32_t v, uint4& out) {
   if (R.cnt < 0) return -2;
   if (R.cnt == 0) return -1;
@@ -1463,73 +1272,68 @@ __device__ __forceinline__ int64_t idx_find(const DevIndex& X, const IdxRow& R, 
     h = idx_next(h, R);
   }
 }
-__device__ __forceinline__ int64_t idx_find(const DevIndex& X, const IdxRow& R, uint32_t v, float& D) {
-  uint4 sl;
-  const int64_t k = idx_find(X, R, v, sl);
-  if (k >= 0) D = bitsf(sl.y);
-  return k;
+// the index row of a candidate as the source of a route: its edge's row
+// (entered along the edge), or its node's (a node candidate, no heading)
+__device__ __forceinline__ int64_t src_row(const DevGraph& g, int32_t e, float off) {
+  return cand_node(off) ? (int64_t)g.n_edges + g.e_from[e] : (int64_t)e;
 }
-// turn units of the route e_i -> (index route u -> v) -> e_j from v's slot
-#ifndef OTM_TRANS_TU_DIAG
-#define OTM_TRANS_TU_DIAG 0  // A/B diagnostic only (wrong results): every turn-table read at entry 0
-#endif
-__device__ __forceinline__ uint32_t idx_turn_units(const uint32_t* TU, const uint4& sl, uint32_t hin_i,
-                                                   uint32_t hout_j) {
-  if (OTM_TRANS_TU_DIAG) return TU[0] + sl.z + (hin_i ^ hout_j);
-  if (sl.w == NO_TURNS) return turn_units(TU, hin_i, hout_j);
-  return turn_units(TU, hin_i, sl.w & 0xFFFFu) + sl.z + turn_units(TU, sl.w >> 16, hout_j);
+// the label a route to a candidate ends on: its edge's departure label, or its
+// node's arrival label (a node candidate)
+__device__ __forceinline__ uint32_t dst_key(const DevGraph& g, int32_t e, float off) {
+  return cand_node(off) ? NODE_KEY | (uint32_t)g.e_from[e] : (uint32_t)e;
 }
 
-// Index build: one wavefront per source node u runs the bounded search with
-// bound rmax in an LDS table of INDEX_BUILD_CAP slots (same fixed point as the
-// online tiers), then inserts every settled node v into the row's table with
-// its distance, predecessor edge and the turns of the route u -> v (each lane
-// walks its entry's predecessor chain back to u in the LDS table).
+// Index build: one wavefront per row runs the row's search with bound cmax in
+// an LDS table of INDEX_BUILD_CAP slots (the online tiers' fixed point), then
+// inserts every label into the row's table with its cost, route distance and
+// turn units (each lane walks its label's predecessor chain in the LDS table)
+// and its predecessor edge.
 template <bool WRITE>
-__global__ __launch_bounds__(TB) void k_index_build(DevGraph g, const uint32_t* TU, float rmax, int32_t* row_cnt,
+__global__ __launch_bounds__(TB) void k_index_build(DevGraph g, const uint32_t* TU, uint32_t cmax, int32_t* row_cnt,
                                                     const IdxRow* rows, uint4* slot, int32_t* pred) {
   __shared__ uint32_t lkey[INDEX_BUILD_CAP];
   __shared__ unsigned long long llab[INDEX_BUILD_CAP];
   __shared__ uint32_t linq[INDEX_BUILD_CAP];
   __shared__ uint32_t lfr0[INDEX_BUILD_CAP];
   __shared__ uint32_t lfr1[INDEX_BUILD_CAP];
+  __shared__ int32_t cbuf[CHAIN_BUF * TB];
   __shared__ SearchShared S;
   const int lane = threadIdx.x;
-  const Table T{lkey, llab, linq, lfr0, lfr1, 11, INDEX_BUILD_LIMIT};
-  for (int32_t u = blockIdx.x; u < g.n_nodes; u += gridDim.x) {
-    const int settled = wave_search<false>(g, T, S, u, rmax, lane);
+  const Table T{lkey, llab, linq, lfr0, lfr1, INDEX_BUILD_LOG2, INDEX_BUILD_LIMIT};
+  const int64_t nrows = (int64_t)g.n_edges + g.n_nodes;
+  for (int64_t r = blockIdx.x; r < nrows; r += gridDim.x) {
+    const bool erow = r < g.n_edges;
+    const int32_t u = erow ? g.e_to[r] : (int32_t)(r - g.n_edges);
+    const uint32_t hin = erow ? (uint32_t)g.e_head_in[r] : NO_HEAD;
+    const int n = ta_search<false>(g, TU, T, S, u, hin, cmax, lane);
     if (!WRITE) {
-      if (lane == 0) row_cnt[u] = settled;  // -1: incomplete row
+      if (lane == 0) row_cnt[r] = n;  // -1: incomplete row
       continue;
     }
-    if (settled < 0) continue;
-    // insert the settled nodes into the row's table (slot order depends on
-    // CAS order; lookups do not)
-    const IdxRow R = rows[u];
+    if (n < 0) continue;
+    // insert the labels into the row's table (slot order depends on CAS
+    // order; lookups do not)
+    const IdxRow R = rows[r];
+    auto predof = [&](uint32_t e) {
+      const int sx = table_find<false>(T, e);
+      return sx < 0 ? NONE_PRED : (uint32_t)(llab[sx] & 0xFFFFFFFFull);
+    };
     for (int i = lane; i < INDEX_BUILD_CAP; i += TB) {
       const uint32_t k = lkey[i];
       if (k == EMPTY) continue;
       const unsigned long long lab = llab[i];
-      const int32_t pk = (int32_t)(uint32_t)(lab & 0xFFFFFFFFull);
-      // the route u -> k: turns between its edges, first / last edge headings
-      uint32_t inner = 0, heads = NO_TURNS;
-      if (k != (uint32_t)u) {
-        int32_t next = pk;
-        for (int32_t x = g.e_from[pk]; x != u;) {
-          const int sx = table_find<false>(T, (uint32_t)x);
-          const int32_t e = (int32_t)(uint32_t)(llab[sx] & 0xFFFFFFFFull);
-          inner += TU[turn_deg(g.e_head_in[e], g.e_head_out[next])];
-          next = e;
-          x = g.e_from[e];
-        }
-        heads = (uint32_t)g.e_head_out[next] | ((uint32_t)g.e_head_in[pk] << 16);
-      }
+      const uint32_t pk = (uint32_t)(lab & 0xFFFFFFFFull);
+      float d;
+      uint32_t units;
+      int len;
+      chain_sums(g, TU, predof, pk, hin, (k & NODE_KEY) ? NO_HEAD : (uint32_t)g.e_head_out[k], cbuf + lane, d, units,
+                 len);
       uint32_t h = idx_slot0(k, R);
       while (atomicCAS(&slot[R.off + h].x, EMPTY, k) != EMPTY) h = idx_next(h, R);
       slot[R.off + h].y = (uint32_t)(lab >> 32);
-      slot[R.off + h].z = inner;
-      slot[R.off + h].w = heads;
-      pred[R.off + h] = pk;
+      slot[R.off + h].z = fbits(d);
+      slot[R.off + h].w = units;
+      pred[R.off + h] = (int32_t)pk;
     }
     __syncthreads();
   }
@@ -1551,13 +1355,16 @@ __global__ void k_row_pack(const int32_t* row_cnt, const int64_t* row_off, IdxRo
 
 // K4 index tier: S lanes per column, TB / S columns in flight per wave,
 // lanes over the column's Kq x Kp (source candidate, target candidate) pairs;
-// each pair is one probe of the source node's index row, whose 16-byte slot
-// holds the route distance and its turns.  A column is a chain of ~5
-// dependent round trips (point -> previous column -> edges -> rows -> slots),
-// so several columns per wave multiply the misses in flight at the same
-// occupancy.  Columns with more pairs than S loop within their group; columns
-// the index cannot answer (bound > rmax, a source row incomplete, more than
-// KC candidates) go to the search tiers.
+// each pair is one probe of its source's index row (row ei, or E + from(ei)
+// for a node candidate) for its target's label (key ej, or NODE_KEY |
+// from(ej) for a node candidate), whose 16-byte slot holds the label's cost,
+// route distance and turn units.  A column is a chain of ~5 dependent round
+// trips (point -> previous column -> candidates -> rows -> slots), so several
+// columns per wave multiply the misses in flight at the same occupancy.
+// Columns with more pairs than S loop within their group; columns the index
+// cannot answer (cost bound > the index's, a source row incomplete, more than
+// KC candidates) go to the search tiers (w.overflow_list0, count
+// w.counters_i32[4]).
 // At 8 lanes per column (8 columns per wave) a column with more than
 // OTM_TRANS_KC8 candidates on either side goes to the wide list
 // (w.overflow_list2, count w.counters_i32[6]), which a 16-lane pass (LIST)
@@ -1573,7 +1380,7 @@ __global__ __launch_bounds__(TB, 8) void k_trans_sub(DevGraph g, DevBatch b, Dev
   // a pair reads its target and source as one 16-byte LDS word each
   constexpr int KC = S >= 16 ? 16 : OTM_TRANS_KC8;
   constexpr bool WIDE = KC < 16;
-  __shared__ int4 tg[NS][KC];  // target: edge, offset bits, from-node, start heading
+  __shared__ int4 tg[NS][KC];  // target: edge, offset bits, label key, -
   __shared__ int4 sr[NS][KC];  // source: edge, offset bits, remaining-length bits, end heading
   __shared__ IdxRow rq[NS][KC];
   // slot of candidate k in its column group's row: XOR-swizzled so that the
@@ -1584,11 +1391,9 @@ __global__ __launch_bounds__(TB, 8) void k_trans_sub(DevGraph g, DevBatch b, Dev
 #ifndef OTM_TRANS_SWZ
 #define OTM_TRANS_SWZ 1
 #endif
-  __shared__ uint32_t TU[TURN_TABLE];  // turn units per deviation
   const int lane = threadIdx.x, sg = lane / S, sl = lane % S;
   const unsigned long long smask = ((1ull << S) - 1ull) << (sg * S);
   const int swz = !OTM_TRANS_SWZ ? 0 : (S == 8 ? ((sg >> 1) & 1) * 4 : (sg & 1) * 8);
-  for (int k = lane; k < TURN_TABLE; k += TB) TU[k] = P.turn_units[k];
   const DevIndex& X = w.idx;
   unsigned long long c_search = 0, c_settled = 0, c_relaxed = 0, c_trans = 0;
   const bool ordered = !LIST && (P.order_mask & ORDER_TRANS) != 0;
@@ -1627,18 +1432,19 @@ __global__ __launch_bounds__(TB, 8) void k_trans_sub(DevGraph g, DevBatch b, Dev
     }
     act = act && q >= 0;
     const float bound = P.factor * gcv;
-    const bool idx_ok = X.rmax > 0.0f && bound <= X.rmax;
+    const uint32_t cq = index_cost_bound(bound);
+    const bool idx_ok = X.rmax > 0.0f && cq <= X.cmax;
     const bool wide = WIDE && act && idx_ok && (Kp > KC || Kq > KC);
     if (wide && sl == 0) w.overflow_list2[atomicAdd(&w.counters_i32[6], 1)] = (int32_t)p;
     act = act && !wide;
     bool bad = act && (!idx_ok || Kp > KC || Kq > KC);
-    // candidates of p (targets) and of q (sources), then edges, then rows
+    // candidates of p (targets) and of q (sources), then rows
     for (int k = sl; k < KC; k += S) {
       if (act && k < Kp) {
         const int2 c = crec(w, p, k);
         const int32_t e = c.x;
         const float o = __int_as_float(c.y);
-        tg[sg][k ^ swz] = make_int4(e, __float_as_int(o), g.e_from[e], (int)dst_head(g, e, o));
+        tg[sg][k ^ swz] = make_int4(e, __float_as_int(o), (int)dst_key(g, e, o), 0);
       }
       if (act && k < Kq) {
         const int2 c = crec(w, q, k);
@@ -1646,8 +1452,7 @@ __global__ __launch_bounds__(TB, 8) void k_trans_sub(DevGraph g, DevBatch b, Dev
         const float o = __int_as_float(c.y);
         sr[sg][k ^ swz] = make_int4(e, __float_as_int(o), __float_as_int(src_start(g, e, o)), (int)src_head(g, e, o));
         if (idx_ok) {
-          // erow[e]: the row of e's end node; erow[E + e]: of its start node
-          const IdxRow R = X.erow[cand_node(o) ? (int64_t)g.n_edges + e : (int64_t)e];
+          const IdxRow R = X.row[src_row(g, e, o)];
           rq[sg][k ^ swz] = R;
           bad = bad || R.cnt < 0;
         }
@@ -1692,7 +1497,8 @@ __global__ __launch_bounds__(TB, 8) void k_trans_sub(DevGraph g, DevBatch b, Dev
           if (idx >= npair) continue;
           const int i = idx / Kp, j = idx - (idx / Kp) * Kp;
           const int4 T = tg[sg][j ^ swz], Sx = sr[sg][i ^ swz];
-          const int32_t ej = T.x, vj = T.z, ei = Sx.x;
+          const uint32_t key = (uint32_t)T.z;
+          const int32_t ej = T.x, ei = Sx.x;
           const float oj = __int_as_float(T.y), oi = __int_as_float(Sx.y), si = __int_as_float(Sx.z);
           float r = 0.0f;
           bool ok = true;
@@ -1704,15 +1510,17 @@ __global__ __launch_bounds__(TB, 8) void k_trans_sub(DevGraph g, DevBatch b, Dev
             uint4 sv = s0[u];
             uint32_t h = h0[u];
             if (R.cnt > 0) {
-              while (sv.x != (uint32_t)vj && sv.x != EMPTY) {  // the rest of the linear probe (rare)
+              while (sv.x != key && sv.x != EMPTY) {  // the rest of the linear probe (rare)
                 h = idx_next(h, R);
                 sv = X.slot[R.off + h];
               }
             }
-            if (R.cnt > 0 && sv.x == (uint32_t)vj) {
-              const float sd = si + bitsf(sv.y);
+            // a label of the row beyond this column's cost bound is not one
+            // of its search's labels
+            if (R.cnt > 0 && sv.x == key && sv.y <= cq) {
+              const float sd = si + bitsf(sv.z);
               r = sd + oj;
-              units = idx_turn_units(TU, sv, (uint32_t)Sx.w, (uint32_t)T.w);
+              units = sv.w;
             } else {
               ok = false;
             }
@@ -1727,18 +1535,26 @@ __global__ __launch_bounds__(TB, 8) void k_trans_sub(DevGraph g, DevBatch b, Dev
       }
       if (w.ctr) {
         // algorithmic counts of the equivalent searches (per-lane partials,
-        // summed over the wave at the end): per distinct source, the row
-        // entries with D <= bound and their out-degrees
+        // summed over the wave at the end): per distinct source (node,
+        // heading), the row's departure labels within the bound and the
+        // out-degrees of those whose edge end is within it too
         for (int i = 0; i < Kq; ++i) {
+          const int4 Si = sr[sg][i ^ swz];
+          const int32_t ui = src_node(g, Si.x, __int_as_float(Si.y));
           bool first = true;
-          for (int k = 0; k < i; ++k) first = first && rq[sg][k ^ swz].off != rq[sg][i ^ swz].off;
+          for (int k = 0; k < i; ++k) {
+            const int4 Sk = sr[sg][k ^ swz];
+            first = first && !(src_node(g, Sk.x, __int_as_float(Sk.y)) == ui && Sk.w == Si.w);
+          }
           if (!first) continue;
           const IdxRow R = rq[sg][i ^ swz];
           for (int64_t k = sl; k < (int64_t)R.cap; k += S) {
             const uint4 slt = X.slot[R.off + k];
-            if (slt.x != EMPTY && bitsf(slt.y) <= bound) {
-              ++c_settled;
-              c_relaxed += (unsigned long long)(g.out_off[slt.x + 1] - g.out_off[slt.x]);
+            if (slt.x == EMPTY || (slt.x & NODE_KEY) || slt.y > cq) continue;
+            ++c_settled;
+            if ((unsigned long long)slt.y + g.e_len64[slt.x] <= cq) {
+              const int32_t v = g.e_to[slt.x];
+              c_relaxed += (unsigned long long)(g.out_off[v + 1] - g.out_off[v]);
             }
           }
           if (sl == 0) ++c_search;
@@ -1764,8 +1580,8 @@ __global__ __launch_bounds__(TB, 8) void k_trans_sub(DevGraph g, DevBatch b, Dev
   }
 }
 
-// K6 index tier: one lane per matched step; the path is read back from the
-// index row of the source node (predecessor edges), one table probe per edge.
+// K6 index tier: one lane per matched step; the route is the predecessor
+// chain of its target's label in its source's row, one probe per edge.
 // route / report waves-per-SIMD hints: 4 or 8 measured within noise (kept at 1)
 #ifndef OTM_ROUTE_WAVES
 #define OTM_ROUTE_WAVES 1
@@ -1793,28 +1609,26 @@ __global__ __launch_bounds__(256, OTM_ROUTE_WAVES) void k_route_index(DevGraph g
       continue;
     }
     const float bound = P.factor * w.gc[p];
-    const int32_t u = src_node(g, ei, oi), v = g.e_from[ej];
-    float Dv = 0.0f;
-    IdxRow R{};
+    const uint32_t cq = index_cost_bound(bound);
+    IdxRow Rw{};
     int64_t sv = -1;
-    if (X.rmax > 0.0f && bound <= X.rmax) {
-      R = X.row[u];
-      sv = idx_find(X, R, (uint32_t)v, Dv);
+    uint4 lab{};
+    if (X.rmax > 0.0f && cq <= X.cmax) {
+      Rw = X.row[src_row(g, ei, oi)];
+      sv = idx_find(X, Rw, dst_key(g, ej, oj), lab);
     }
-    if (sv < 0) {
+    if (sv < 0 || lab.y > cq) {
       const int slot = atomicAdd(&w.counters_i32[4], 1);
       w.overflow_list0[slot] = (int32_t)p;
       continue;
     }
     int len = 0;
-    for (int32_t x = v, px = w.idx.pred[sv]; x != u && len <= R.cnt;) {
+    for (uint32_t pe = (uint32_t)X.pred[sv]; pe != NONE_PRED && len <= Rw.cnt;) {
       ++len;
-      x = g.e_from[px];
-      if (x == u) break;
-      float dd;
-      const int64_t sx = idx_find(X, R, (uint32_t)x, dd);
+      uint4 tmp;
+      const int64_t sx = idx_find(X, Rw, pe, tmp);
       if (sx < 0) break;  // (cannot happen: predecessor chains stay in the row)
-      px = X.pred[sx];
+      pe = (uint32_t)X.pred[sx];
     }
     const int off = len ? atomicAdd(&w.counters_i32[1], len) : 0;
     if (off + len > w.pool_cap) {
@@ -1823,28 +1637,28 @@ __global__ __launch_bounds__(256, OTM_ROUTE_WAVES) void k_route_index(DevGraph g
       w.path_len[p] = -1;
     } else {
       int k = len;
-      for (int32_t x = v, px = X.pred[sv]; x != u;) {
-        w.path_pool[off + (--k)] = px;
-        x = g.e_from[px];
-        if (x == u) break;
-        float dd;
-        const int64_t sx = idx_find(X, R, (uint32_t)x, dd);
-        if (sx < 0 || k == 0) break;
-        px = X.pred[sx];
+      for (uint32_t pe = (uint32_t)X.pred[sv]; pe != NONE_PRED && k > 0;) {
+        w.path_pool[off + (--k)] = (int32_t)pe;
+        uint4 tmp;
+        const int64_t sx = idx_find(X, Rw, pe, tmp);
+        if (sx < 0) break;
+        pe = (uint32_t)X.pred[sx];
       }
       w.path_off[p] = off;
       w.path_len[p] = len;
     }
     const float start = src_start(g, ei, oi);
-    const float sd = start + Dv;
+    const float sd = start + bitsf(lab.z);
     w.route_dist[p] = sd + oj;
     if (w.ctr) {
       unsigned long long st = 0, rl = 0;
-      for (int64_t k = 0; k < (int64_t)R.cap; ++k) {
-        const uint4 sl = X.slot[R.off + k];
-        if (sl.x != EMPTY && bitsf(sl.y) <= bound) {
-          ++st;
-          rl += (unsigned long long)(g.out_off[sl.x + 1] - g.out_off[sl.x]);
+      for (int64_t k = 0; k < (int64_t)Rw.cap; ++k) {
+        const uint4 sl = X.slot[Rw.off + k];
+        if (sl.x == EMPTY || (sl.x & NODE_KEY) || sl.y > cq) continue;
+        ++st;
+        if ((unsigned long long)sl.y + g.e_len64[sl.x] <= cq) {
+          const int32_t v = g.e_to[sl.x];
+          rl += (unsigned long long)(g.out_off[v + 1] - g.out_off[v]);
         }
       }
       ++c_search;
@@ -1862,34 +1676,41 @@ __global__ __launch_bounds__(256, OTM_ROUTE_WAVES) void k_route_index(DevGraph g
 }
 
 // ============================================================== K4 transitions (wave tiers)
-// Columns spilled by the lane tier (list in w.overflow_list, count in
-// w.counters_i32[0], read on the device: no host round trip).  The LDS wave
-// tier spills further to `w.overflow_list2` / counters_i32[3], which the
+// Columns the index tier could not answer (list in w.overflow_list0, count in
+// w.counters_i32[4], read on the device: no host round trip): one turn-aware
+// search per distinct source (node, heading), the wave's table in LDS.  The
+// LDS tier spills to `w.overflow_list2` / counters_i32[3], which the
 // global-memory tier (BIG) drains.
 template <bool BIG>
-__global__ __launch_bounds__(TB) void k_transitions(DevGraph g, DevBatch b, DevParams P, DevWork w,
-                                                     int32_t n_overflow) {
+__global__ __launch_bounds__(TB) void k_transitions(DevGraph g, DevBatch b, DevParams P, DevWork w) {
   if (*w.abort || trans_over_cap(b, w)) return;
   __shared__ uint32_t lkey[BIG ? 1 : LDS_TABLE_CAP];
   __shared__ unsigned long long llab[BIG ? 1 : LDS_TABLE_CAP];
   __shared__ uint32_t linq[BIG ? 1 : LDS_TABLE_CAP];
   __shared__ uint32_t lfr0[BIG ? 1 : LDS_TABLE_CAP];
   __shared__ uint32_t lfr1[BIG ? 1 : LDS_TABLE_CAP];
+  __shared__ int32_t cbuf[CHAIN_BUF * TB];
+  __shared__ uint32_t TU[TURN_TABLE];
   __shared__ int32_t eq[KMAX], ep[KMAX];
   __shared__ float oq[KMAX], op[KMAX];
   __shared__ SearchShared S;
   const int lane = threadIdx.x;
+  for (int k = lane; k < TURN_TABLE; k += TB) TU[k] = P.turn_units[k];
   Table T;
   if (BIG) {
     const size_t base = (size_t)blockIdx.x * BIG_TABLE_CAP;
     T = Table{w.big_key + base, w.big_lab + base, w.big_inq + base, w.big_fr + 2 * base,
-              w.big_fr + 2 * base + BIG_TABLE_CAP, 15, SEARCH_LIMIT};
+              w.big_fr + 2 * base + BIG_TABLE_CAP, BIG_TABLE_LOG2, SEARCH_LIMIT};
   } else {
     T = Table{lkey, llab, linq, lfr0, lfr1, 8, LDS_TABLE_LIMIT};
   }
-  (void)n_overflow;
-  const int32_t* list = BIG ? w.overflow_list2 : w.overflow_list;
-  const int64_t nwork = BIG ? (int64_t)w.counters_i32[3] : (int64_t)w.counters_i32[0];
+  auto predof = [&](uint32_t e) {
+    const int sx = table_find<BIG>(T, e);
+    return sx < 0 ? NONE_PRED : (uint32_t)(Mem<BIG>::ld(&T.lab[sx]) & 0xFFFFFFFFull);
+  };
+  const int32_t* list = BIG ? w.overflow_list2 : w.overflow_list0;
+  const int64_t nwork = BIG ? (int64_t)w.counters_i32[3] : (int64_t)w.counters_i32[4];
+  __syncthreads();
   for (int64_t it = blockIdx.x; it < nwork; it += gridDim.x) {
     const int64_t p = (int64_t)list[it];
     const int32_t q = w.col_prev[p];
@@ -1897,6 +1718,7 @@ __global__ __launch_bounds__(TB) void k_transitions(DevGraph g, DevBatch b, DevP
     const int Kq = w.ncand[q], Kp = w.ncand[p];
     const float gcv = w.gc[p];
     const float bound = P.factor * gcv;
+    const uint32_t cq = index_cost_bound(bound);
     if (lane < Kq) {
       const int2 c = crec(w, q, lane);
       eq[lane] = c.x;
@@ -1908,12 +1730,14 @@ __global__ __launch_bounds__(TB) void k_transitions(DevGraph g, DevBatch b, DevP
       op[lane] = __int_as_float(c.y);
     }
     __syncthreads();
-    // distinct source nodes (first occurrence order)
+    // distinct sources (node, heading), first occurrence order
     const int32_t u_l = lane < Kq ? src_node(g, eq[lane], oq[lane]) : -1;
+    const uint32_t h_l = lane < Kq ? src_head(g, eq[lane], oq[lane]) : 0u;
     bool first = lane < Kq;
     for (int k = 0; k < Kq; ++k) {
       const int32_t uk = __shfl(u_l, k, 64);
-      if (k < lane && uk == u_l) first = false;
+      const uint32_t hk = __shfl(h_l, k, 64);
+      if (k < lane && uk == u_l && hk == h_l) first = false;
     }
     unsigned long long srcmask = __ballot(first);
     float* Tm = w.trans + w.trans_off[p];
@@ -1925,59 +1749,51 @@ __global__ __launch_bounds__(TB) void k_transitions(DevGraph g, DevBatch b, DevP
       const int sl = __ffsll((long long)srcmask) - 1;
       srcmask &= srcmask - 1;
       const int32_t u = __shfl(u_l, sl, 64);
-      const int settled = wave_search<BIG>(g, T, S, u, bound, lane);
-      if (settled < 0) {
+      const uint32_t hin = __shfl(h_l, sl, 64);
+      const int labels = ta_search<BIG>(g, TU, T, S, u, hin, cq, lane);
+      if (labels < 0) {
         failed = true;
         break;
       }
       unsigned long long ntr = 0;
       for (int idx = lane; idx < Kq * Kp; idx += TB) {
         const int i = idx / Kp, j = idx - (idx / Kp) * Kp;
-        if (src_node(g, eq[i], oq[i]) != u) continue;
+        if (src_node(g, eq[i], oq[i]) != u || src_head(g, eq[i], oq[i]) != hin) continue;
         const int32_t ei = eq[i], ej = ep[j];
         const float start = src_start(g, ei, oq[i]);
-        float r;
+        float r = 0.0f;
+        uint32_t units = 0;
         bool ok = true;
-        const bool same = ej == ei && op[j] >= oq[i];
-        if (same) {
+        if (ej == ei && op[j] >= oq[i]) {
           r = op[j] - oq[i];
         } else {
-          const int slot = table_find<BIG>(T, (uint32_t)g.e_from[ej]);
+          const uint32_t key = dst_key(g, ej, op[j]);
+          const int slot = table_find<BIG>(T, key);
           if (slot < 0) {
             ok = false;
-            r = 0.0f;
           } else {
-            const float D = bitsf((uint32_t)(Mem<BIG>::ld(&T.lab[slot]) >> 32));
-            const float sd = start + D;
+            float d;
+            int n;
+            chain_sums(g, TU, predof, (uint32_t)(Mem<BIG>::ld(&T.lab[slot]) & 0xFFFFFFFFull), hin,
+                       (key & NODE_KEY) ? NO_HEAD : (uint32_t)g.e_head_out[ej], cbuf + lane, d, units, n);
+            const float sd = start + d;
             r = sd + op[j];
           }
         }
         float cost = INFINITY;
         if (ok && r <= bound) {
-          // the route's turns, walked back over the converged labels
-          uint32_t units = 0;
-          if (!same) {
-            uint32_t hn = dst_head(g, ej, op[j]);
-            for (int32_t x = g.e_from[ej]; x != u;) {
-              const int sx = table_find<BIG>(T, (uint32_t)x);
-              const int32_t e = (int32_t)(uint32_t)(Mem<BIG>::ld(&T.lab[sx]) & 0xFFFFFFFFull);
-              units += turn_units(P.turn_units, g.e_head_in[e], hn);
-              hn = g.e_head_out[e];
-              x = g.e_from[e];
-            }
-            units += turn_units(P.turn_units, src_head(g, ei, oq[i]), hn);
-          }
           cost = trans_cost(units, r, gcv, P.beta);
           ++ntr;
         }
         Tm[i * Kp + j] = cost;
       }
       if (w.ctr) {
-        const unsigned long long od = settled_outdeg<BIG>(g, T, lane);
+        unsigned long long st, rl;
+        ta_counts<BIG>(g, T, cq, lane, st, rl);
         for (int o = 32; o > 0; o >>= 1) ntr += __shfl_xor(ntr, o, 64);
         c_search += 1;
-        c_settled += (unsigned long long)settled;
-        c_relaxed += od;
+        c_settled += st;
+        c_relaxed += rl;
         c_trans += ntr;
       }
       __syncthreads();
@@ -2387,32 +2203,40 @@ __global__ __launch_bounds__(TB, OTM_VIT_WAVES) void k_viterbi(DevBatch b, DevWo
 }
 
 // ============================================================== K6 route
+// Steps the index tier could not answer (w.overflow_list0 / counters_i32[4]):
+// the winning search again, its target label's predecessor chain as the path.
 template <bool BIG>
-__global__ __launch_bounds__(TB) void k_route(DevGraph g, DevBatch b, DevParams P, DevWork w, int32_t n_overflow) {
+__global__ __launch_bounds__(TB) void k_route(DevGraph g, DevBatch b, DevParams P, DevWork w) {
   if (*w.abort) return;
   __shared__ uint32_t lkey[BIG ? 1 : LDS_TABLE_CAP];
   __shared__ unsigned long long llab[BIG ? 1 : LDS_TABLE_CAP];
   __shared__ uint32_t linq[BIG ? 1 : LDS_TABLE_CAP];
   __shared__ uint32_t lfr0[BIG ? 1 : LDS_TABLE_CAP];
   __shared__ uint32_t lfr1[BIG ? 1 : LDS_TABLE_CAP];
+  __shared__ int32_t cbuf[CHAIN_BUF * TB];
+  __shared__ uint32_t TU[TURN_TABLE];
   __shared__ SearchShared S;
   const int lane = threadIdx.x;
+  for (int k = lane; k < TURN_TABLE; k += TB) TU[k] = P.turn_units[k];
   Table T;
   if (BIG) {
     const size_t base = (size_t)blockIdx.x * BIG_TABLE_CAP;
     T = Table{w.big_key + base, w.big_lab + base, w.big_inq + base, w.big_fr + 2 * base,
-              w.big_fr + 2 * base + BIG_TABLE_CAP, 15, SEARCH_LIMIT};
+              w.big_fr + 2 * base + BIG_TABLE_CAP, BIG_TABLE_LOG2, SEARCH_LIMIT};
   } else {
     T = Table{lkey, llab, linq, lfr0, lfr1, 8, LDS_TABLE_LIMIT};
   }
-  (void)n_overflow;
-  const int32_t* list = BIG ? w.overflow_list2 : w.overflow_list;
-  const int64_t nwork = BIG ? (int64_t)w.counters_i32[3] : (int64_t)w.counters_i32[0];
+  auto predof = [&](uint32_t e) {
+    const int sx = table_find<BIG>(T, e);
+    return sx < 0 ? NONE_PRED : (uint32_t)(Mem<BIG>::ld(&T.lab[sx]) & 0xFFFFFFFFull);
+  };
+  const int32_t* list = BIG ? w.overflow_list2 : w.overflow_list0;
+  const int64_t nwork = BIG ? (int64_t)w.counters_i32[3] : (int64_t)w.counters_i32[4];
+  __syncthreads();
   for (int64_t it = blockIdx.x; it < nwork; it += gridDim.x) {
     const int64_t p = (int64_t)list[it];
     const int32_t q = w.col_prev[p];
-    const int i = w.state[q], j = w.state[p];
-    const int2 ci = crec(w, q, i), cj = crec(w, p, j);
+    const int2 ci = w.chosen[q], cj = w.chosen[p];
     const int32_t ei = ci.x, ej = cj.x;
     const float oi = __int_as_float(ci.y), oj = __int_as_float(cj.y);
     if (ei == ej && oj >= oi) {
@@ -2420,9 +2244,11 @@ __global__ __launch_bounds__(TB) void k_route(DevGraph g, DevBatch b, DevParams 
       continue;
     }
     const float bound = P.factor * w.gc[p];
-    const int32_t u = src_node(g, ei, oi), v = g.e_from[ej];
-    const int settled = wave_search<BIG>(g, T, S, u, bound, lane);
-    if (settled < 0) {
+    const uint32_t cq = index_cost_bound(bound);
+    const int32_t u = src_node(g, ei, oi);
+    const uint32_t hin = src_head(g, ei, oi);
+    const int labels = ta_search<BIG>(g, TU, T, S, u, hin, cq, lane);
+    if (labels < 0) {
       if (lane == 0) {
         if (!BIG) {
           const int slot = atomicAdd(&w.counters_i32[3], 1);
@@ -2434,42 +2260,40 @@ __global__ __launch_bounds__(TB) void k_route(DevGraph g, DevBatch b, DevParams 
       __syncthreads();
       continue;
     }
-    unsigned long long od = 0;
-    if (w.ctr) od = settled_outdeg<BIG>(g, T, lane);
+    unsigned long long st = 0, rl = 0;
+    if (w.ctr) ta_counts<BIG>(g, T, cq, lane, st, rl);
     if (lane == 0) {
-      const int vs = table_find<BIG>(T, (uint32_t)v);
-      const float D = bitsf((uint32_t)(Mem<BIG>::ld(&T.lab[vs]) >> 32));
-      int n = 0;
-      for (int32_t x = v; x != u;) {
-        const int sx = table_find<BIG>(T, (uint32_t)x);
-        const int32_t pe = (int32_t)(uint32_t)(Mem<BIG>::ld(&T.lab[sx]) & 0xFFFFFFFFull);
-        ++n;
-        x = g.e_from[pe];
-      }
-      const int off = atomicAdd(&w.counters_i32[1], n);
-      if (off + n > w.pool_cap) {
-        w.counters_i32[2] = 1;
-      *w.abort = 1;
-        w.path_len[p] = -1;
+      const uint32_t key = dst_key(g, ej, oj);
+      const int vs = table_find<BIG>(T, key);
+      if (vs < 0) {
+        // (cannot happen: the step's transition was finite)
+        atomicCAS(&w.trace_err[w.pt_trace[p]], 0, OTM_TERR_SEARCH_OVERFLOW);
       } else {
-        int k = n;
-        for (int32_t x = v; x != u;) {
-          const int sx = table_find<BIG>(T, (uint32_t)x);
-          const int32_t pe = (int32_t)(uint32_t)(Mem<BIG>::ld(&T.lab[sx]) & 0xFFFFFFFFull);
-          w.path_pool[off + (--k)] = pe;
-          x = g.e_from[pe];
+        const uint32_t pk = (uint32_t)(Mem<BIG>::ld(&T.lab[vs]) & 0xFFFFFFFFull);
+        float d;
+        uint32_t units;
+        int n;
+        chain_sums(g, TU, predof, pk, hin, NO_HEAD, cbuf, d, units, n);
+        const int off = atomicAdd(&w.counters_i32[1], n);
+        if (off + n > w.pool_cap) {
+          w.counters_i32[2] = 1;
+          *w.abort = 1;
+          w.path_len[p] = -1;
+        } else {
+          int k = n;
+          for (uint32_t pe = pk; pe != NONE_PRED && k > 0; pe = predof(pe)) w.path_pool[off + (--k)] = (int32_t)pe;
+          w.path_off[p] = off;
+          w.path_len[p] = n;
         }
-        w.path_off[p] = off;
-        w.path_len[p] = n;
-      }
-      const float start = src_start(g, ei, oi);
-      const float sd = start + D;
-      w.route_dist[p] = sd + oj;
-      if (w.ctr) {
-        cadd(&w.ctr->route_searches, 1);
-        cadd(&w.ctr->route_nodes_settled, (unsigned long long)settled);
-        cadd(&w.ctr->route_edges_relaxed, od);
-        cadd(&w.ctr->route_edges, (unsigned long long)n);
+        const float start = src_start(g, ei, oi);
+        const float sd = start + d;
+        w.route_dist[p] = sd + oj;
+        if (w.ctr) {
+          cadd(&w.ctr->route_searches, 1);
+          cadd(&w.ctr->route_nodes_settled, st);
+          cadd(&w.ctr->route_edges_relaxed, rl);
+          cadd(&w.ctr->route_edges, (unsigned long long)n);
+        }
       }
     }
     __syncthreads();
@@ -3510,17 +3334,14 @@ void launch_fetch_scan(int32_t n, const int32_t* c0, const int32_t* c1, const in
 
 const char* const kKernelNames[KN_COUNT] = {
     "k_columns",       "spatial_order",  "k_cand_lane",    "k_candidates",     "k_links",         "scan_trans_off",  "k_trans_sub",
-    "k_trans_wide",    "k_trans_lane",    "k_transitions",  "k_transitions_big", "k_viterbi",      "k_route_index",   "k_route_lane",
+    "k_trans_wide",    "k_transitions",  "k_transitions_big", "k_viterbi",      "k_route_index",
     "k_route",         "k_route_big",    "k_seg_bound",      "scan_seg_bound",  "k_segments",       "k_report"};
 
 namespace {
 // The spill tiers run on lists the previous tier filled on the device; they
 // read the list length themselves (fixed grids, no host round trip) and exit
 // at once when the list is empty.
-constexpr int LANE_CAP = 24;        // route stage: 12 B per slot
-constexpr int LANE_CAP_TRANS = 24;  // transitions: 12 B per slot (predecessors give the route's turns)
 constexpr int SPILL_GRID = 4096;
-constexpr int LANE_GRID = 2048;
 constexpr int WIDE_GRID = 2048;  // k_trans_sub's wide-column pass (grid-strides over its list)
 }  // namespace
 
@@ -3601,10 +3422,8 @@ void launch_transitions(const DevGraph& g, const DevBatch& b, const DevParams& p
     mk.begin(KN_TRANS_WIDE, s);
     mk.end(KN_TRANS_WIDE, s);
   }
-  TIMED(KN_TRANS_LANE, hipLaunchKernelGGL(k_trans_lane<LANE_CAP_TRANS>, dim3(LANE_GRID), dim3(LANE_TB), 0, s, g, b,
-                                          p, w));
-  TIMED(KN_TRANS_WAVE, hipLaunchKernelGGL(k_transitions<false>, dim3(SPILL_GRID), dim3(TB), 0, s, g, b, p, w, 0));
-  TIMED(KN_TRANS_GLOBAL, hipLaunchKernelGGL(k_transitions<true>, dim3(BIG_SLOTS), dim3(TB), 0, s, g, b, p, w, 0));
+  TIMED(KN_TRANS_WAVE, hipLaunchKernelGGL(k_transitions<false>, dim3(SPILL_GRID), dim3(TB), 0, s, g, b, p, w));
+  TIMED(KN_TRANS_GLOBAL, hipLaunchKernelGGL(k_transitions<true>, dim3(BIG_SLOTS), dim3(TB), 0, s, g, b, p, w));
 }
 void launch_viterbi(const DevBatch& b, DevWork& w, hipStream_t s, const Marks& mk) {
   TIMED(KN_VITERBI, hipLaunchKernelGGL(k_viterbi, dim3(grid_for(b.n_traces, 1, WAVE_GRID_CAP)), dim3(TB), 0, s, b,
@@ -3614,9 +3433,8 @@ void launch_route(const DevGraph& g, const DevBatch& b, const DevParams& p, DevW
                   const Marks& mk) {
   TIMED(KN_ROUTE_INDEX, hipLaunchKernelGGL(k_route_index, dim3(order_grid(b.n_points, 256, 1 << 30)), dim3(256), 0,
                                            s, g, b, p, w));
-  TIMED(KN_ROUTE_LANE, hipLaunchKernelGGL(k_route_lane<LANE_CAP>, dim3(LANE_GRID), dim3(LANE_TB), 0, s, g, b, p, w));
-  TIMED(KN_ROUTE_WAVE, hipLaunchKernelGGL(k_route<false>, dim3(SPILL_GRID), dim3(TB), 0, s, g, b, p, w, 0));
-  TIMED(KN_ROUTE_GLOBAL, hipLaunchKernelGGL(k_route<true>, dim3(BIG_SLOTS), dim3(TB), 0, s, g, b, p, w, 0));
+  TIMED(KN_ROUTE_WAVE, hipLaunchKernelGGL(k_route<false>, dim3(SPILL_GRID), dim3(TB), 0, s, g, b, p, w));
+  TIMED(KN_ROUTE_GLOBAL, hipLaunchKernelGGL(k_route<true>, dim3(BIG_SLOTS), dim3(TB), 0, s, g, b, p, w));
 }
 void launch_segments(const DevGraph& g, const DevBatch& b, DevWork& w, DevOut& o, bool write, hipStream_t s,
                      const Marks& mk) {
@@ -3663,29 +3481,19 @@ void launch_report(const DevBatch& b, const DevReportCfg& rc, DevWork& w, DevOut
 }
 #undef TIMED
 
-void launch_index_build(const DevGraph& g, const uint32_t* turn_units, float rmax, int32_t* row_cnt,
+void launch_index_build(const DevGraph& g, const uint32_t* turn_units, uint32_t cmax, int32_t* row_cnt,
                         const IdxRow* rows, uint4* slot, int32_t* pred, bool write, hipStream_t s) {
-  const int grid = grid_for(g.n_nodes, 1, 256 * 16);
+  const int grid = grid_for((int64_t)g.n_edges + g.n_nodes, 1, 256 * 16);
   if (write)
-    hipLaunchKernelGGL(k_index_build<true>, dim3(grid), dim3(TB), 0, s, g, turn_units, rmax, row_cnt, rows, slot,
+    hipLaunchKernelGGL(k_index_build<true>, dim3(grid), dim3(TB), 0, s, g, turn_units, cmax, row_cnt, rows, slot,
                        pred);
   else
-    hipLaunchKernelGGL(k_index_build<false>, dim3(grid), dim3(TB), 0, s, g, turn_units, rmax, row_cnt, rows, slot,
+    hipLaunchKernelGGL(k_index_build<false>, dim3(grid), dim3(TB), 0, s, g, turn_units, cmax, row_cnt, rows, slot,
                        pred);
 }
 void launch_row_sizes(const int32_t* row_cnt, int64_t* row_sizes, int32_t n, hipStream_t s) {
   hipLaunchKernelGGL(k_row_sizes, dim3(grid_for((int64_t)n + 1, 256, 1 << 30)), dim3(256), 0, s, row_cnt, row_sizes,
                      n);
-}
-__global__ void k_edge_rows(DevGraph g, const IdxRow* rows, IdxRow* erow) {
-  const int32_t e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e < g.n_edges) {
-    erow[e] = rows[g.e_to[e]];
-    erow[(int64_t)g.n_edges + e] = rows[g.e_from[e]];  // node candidates' source rows
-  }
-}
-void launch_edge_rows(const DevGraph& g, const IdxRow* rows, IdxRow* erow, hipStream_t s) {
-  hipLaunchKernelGGL(k_edge_rows, dim3(grid_for((int64_t)g.n_edges, 256, 1 << 30)), dim3(256), 0, s, g, rows, erow);
 }
 void launch_row_pack(const int32_t* row_cnt, const int64_t* row_off, IdxRow* rows, int32_t n, hipStream_t s) {
   hipLaunchKernelGGL(k_row_pack, dim3(grid_for((int64_t)n, 256, 1 << 30)), dim3(256), 0, s, row_cnt, row_off, rows, n);

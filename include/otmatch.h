@@ -374,7 +374,10 @@ int otm_get_spill_stats(otm_engine* eng, otm_spill_stats* out);
 /* Stage outputs of the last batch, for parity tests (device -> host copy).
  * what: 0 ncand i32[P], 1 cand_edge i32[P*KMAX], 2 cand_off f32[P*KMAX],
  * 3 cand_emis f32[P*KMAX], 4 trans_off i64[P+1], 5 trans f32[total],
- * 6 state i32[P], 7 col_prev i32[P], 8 route_dist f32[P], 9 gc f32[P]. */
+ * 6 state i32[P], 7 col_prev i32[P], 8 route_dist f32[P], 9 gc f32[P],
+ * 10 ipos f32[P]; the batch inputs as the GPU request reader decoded them
+ * (otm_report_batch; also a host batch of more than 2^18 points): 11 trace_off
+ * i64[T+1], 12 lat f32[P], 13 lon f32[P], 14 time f64[P], 15 accuracy f32[P]. */
 int otm_debug_fetch(otm_engine* eng, int what, void* dst, size_t bytes,
                     size_t* needed);
 int otm_kmax(void);

@@ -432,31 +432,11 @@ void run_requests(otm_engine* E, std::vector<Req>& rq, std::vector<int>& codes, 
   }
 }
 
-void report_many(otm_engine* E, int n, const char* const* reqs, const size_t* lens, int* codes, char** resps,
-                 size_t* resp_lens) {
-  const double t0 = now_ms();
-  std::vector<Req> rq((size_t)n);
-  std::vector<int> c((size_t)n, 0);
-  std::vector<std::string> bodies((size_t)n);
-  std::vector<int> todo;
-  par_for((size_t)n, [&](size_t a, size_t e) {
-    for (size_t k = a; k < e; ++k) {
-      const std::string_view body(reqs[k], lens[k]);
-      if (fast_requests() && otm::fast_request(body, &rq[k].tp, &rq[k].uuid)) {
-        rq[k].fast = true;
-        continue;
-      }
-      const int code = otm::parse_request("/report", body, &rq[k].dom, &bodies[k]);
-      if (code) c[k] = code;
-    }
-  });
-  for (int k = 0; k < n; ++k)
-    if (!c[(size_t)k]) todo.push_back(k);
-  const double t1 = now_ms();
-  run_requests(E, rq, c, bodies, todo, false);
-  const double t2 = now_ms();
-  // every response body or none: a failed allocation frees the ones already
-  // made (the caller gets only the error, nothing to otm_free)
+// every request's response copied into its own malloc'd buffer (otm_free):
+// all of them or none -- a failed allocation frees the ones already made
+// (the caller gets only the error, nothing to otm_free)
+void copy_out(int n, const std::vector<int>& c, const std::vector<std::string>& bodies, int* codes, char** resps,
+              size_t* resp_lens) {
   std::atomic<bool> oom{false};
   par_for((size_t)n, [&](size_t a, size_t e) {
     for (size_t k = a; k < e; ++k) {
@@ -478,6 +458,34 @@ void report_many(otm_engine* E, int n, const char* const* reqs, const size_t* le
     }
     throw std::bad_alloc();
   }
+}
+
+// the host readers: every body parsed on the host threads (fast_request, or
+// the json.loads-semantics DOM), one GPU batch, responses on the host threads
+void report_many_host(otm_engine* E, int n, const char* const* reqs, const size_t* lens, int* codes, char** resps,
+                      size_t* resp_lens) {
+  const double t0 = now_ms();
+  std::vector<Req> rq((size_t)n);
+  std::vector<int> c((size_t)n, 0);
+  std::vector<std::string> bodies((size_t)n);
+  std::vector<int> todo;
+  par_for((size_t)n, [&](size_t a, size_t e) {
+    for (size_t k = a; k < e; ++k) {
+      const std::string_view body(reqs[k], lens[k]);
+      if (fast_requests() && otm::fast_request(body, &rq[k].tp, &rq[k].uuid)) {
+        rq[k].fast = true;
+        continue;
+      }
+      const int code = otm::parse_request("/report", body, &rq[k].dom, &bodies[k]);
+      if (code) c[k] = code;
+    }
+  });
+  for (int k = 0; k < n; ++k)
+    if (!c[(size_t)k]) todo.push_back(k);
+  const double t1 = now_ms();
+  run_requests(E, rq, c, bodies, todo, false);
+  const double t2 = now_ms();
+  copy_out(n, c, bodies, codes, resps, resp_lens);
   const double t3 = now_ms();
   // the response strings released by the pool threads that wrote them (their
   // allocator arenas), the requests with them
@@ -494,6 +502,116 @@ void report_many(otm_engine* E, int n, const char* const* reqs, const size_t* le
                  "tail %.2f, copy out %.2f, free %.2f ms\n",
                  n, t1 - t0, t_extract_ms, t_pack_ms, t_gpu_ms, t_write_ms,
                  (t2 - t1) - t_extract_ms - t_pack_ms - t_gpu_ms - t_write_ms, t3 - t2, t4 - t3);
+}
+
+// The GPU request reader (requests.hip) for a batch of at least
+// OTM_GPU_JSON_MIN requests (default 32) on a one-device engine; OTM_GPU_JSON=0
+// keeps every body on the host readers (A/B and the parity tests)
+bool gpu_reader(const otm_engine* E, int n) {
+  if (!E->members.empty()) return false;
+  const char* v = std::getenv("OTM_GPU_JSON");
+  if (v && *v == '0') return false;
+  const char* m = std::getenv("OTM_GPU_JSON_MIN");
+  return n >= (m ? std::atoi(m) : 32);
+}
+
+// otm_report_batch with the bodies read on the GPU: staged into one pinned
+// blob by the host threads, copied to HBM once, decoded and matched there
+// (engine_match_requests); the responses written on the host threads.  Bodies
+// outside the Java batcher's exact form are read by the host readers after, as
+// one more batch (report_many_host: the same results and error contract).
+void report_many_device(otm_engine* E, int n, const char* const* reqs, const size_t* lens, int* codes,
+                        char** resps, size_t* resp_lens) {
+  const double t0 = now_ms();
+  std::vector<int> c((size_t)n, 0);
+  std::vector<std::string> bodies((size_t)n);
+  std::vector<int> rest;  // left to the host readers
+  std::vector<int> inv;   // invalid speeds per accepted trace (stderr lines)
+  std::vector<int> which;
+  double t1 = t0, t2 = t0, t3 = t0;
+  int rc;
+  std::string err;
+  {
+    std::lock_guard<std::mutex> lk(E->mu);
+    size_t bytes = 0;
+    for (int k = 0; k < n; ++k) bytes += lens[k];
+    int64_t* off = nullptr;
+    char* dst = nullptr;
+    rc = otm::engine_stage_requests(E, n, bytes, &off, &dst, &err);
+    if (!rc) {
+      off[0] = 0;
+      for (int k = 0; k < n; ++k) off[k + 1] = off[k] + (int64_t)lens[k];
+      par_for((size_t)n, [&](size_t a, size_t e) {
+        for (size_t k = a; k < e; ++k)
+          if (lens[k]) std::memcpy(dst + off[k], reqs[k], lens[k]);
+      });
+      t1 = now_ms();
+      const uint8_t* ok = nullptr;
+      int32_t nt = 0;
+      otm_results r;
+      rc = otm::engine_match_requests(E, n, bytes, &ok, &nt, &err);
+      if (!rc) rc = otm::engine_fetch(E, &r, &err);
+      t2 = now_ms();
+      if (!rc) {
+        which.reserve((size_t)nt);
+        for (int k = 0; k < n; ++k) (ok[k] ? which : rest).push_back(k);
+        inv.assign(which.size(), 0);
+        par_for(which.size(), [&](size_t a, size_t e) {
+          for (size_t m = a; m < e; ++m) {
+            const int k = which[m];
+            thread_local std::string scratch;
+            scratch.clear();
+            c[(size_t)k] = otm::write_report_response(r, (int32_t)m, &scratch);
+            bodies[(size_t)k].assign(scratch);
+            inv[m] = r.traces[m].code == 200 ? r.traces[m].invalid_speeds : 0;
+          }
+        });
+        t3 = now_ms();
+      }
+    }
+  }
+  if (rc) {
+    // a staging or device failure: the whole batch through the host readers
+    // (their own 400s, and 500s for what reaches the device)
+    report_many_host(E, n, reqs, lens, codes, resps, resp_lens);
+    return;
+  }
+  // the reference's stderr lines of the GPU-read requests, in request order
+  for (size_t m = 0; m < which.size(); ++m)
+    for (int q = 0; q < inv[m]; ++q) std::fputs("Speed exceeds 200kph\n", stderr);
+  if (!rest.empty()) {
+    const size_t nr = rest.size();
+    std::vector<const char*> rq(nr);
+    std::vector<size_t> rl(nr), ol(nr, 0);
+    std::vector<int> rcodes(nr, 500);
+    std::vector<char*> rr(nr, nullptr);
+    for (size_t m = 0; m < nr; ++m) {
+      rq[m] = reqs[rest[m]];
+      rl[m] = lens[rest[m]];
+    }
+    report_many_host(E, (int)nr, rq.data(), rl.data(), rcodes.data(), rr.data(), ol.data());
+    // (their bodies move into place below: copied like the others, then freed)
+    for (size_t m = 0; m < nr; ++m) {
+      c[(size_t)rest[m]] = rcodes[m];
+      bodies[(size_t)rest[m]].assign(rr[m], ol[m]);
+      std::free(rr[m]);
+    }
+  }
+  copy_out(n, c, bodies, codes, resps, resp_lens);
+  const double t4 = now_ms();
+  par_for((size_t)n, [&](size_t a, size_t e) {
+    for (size_t k = a; k < e; ++k) std::string().swap(bodies[k]);
+  });
+  if (json_profile())
+    std::fprintf(stderr, "[otm json gpu] %d requests (%zu on the host readers): stage %.2f, gpu %.2f, write %.2f, "
+                 "copy out %.2f, free %.2f ms\n",
+                 n, rest.size(), t1 - t0, t2 - t1, t3 - t2, t4 - t3, now_ms() - t4);
+}
+
+void report_many(otm_engine* E, int n, const char* const* reqs, const size_t* lens, int* codes, char** resps,
+                 size_t* resp_lens) {
+  if (gpu_reader(E, n)) report_many_device(E, n, reqs, lens, codes, resps, resp_lens);
+  else report_many_host(E, n, reqs, lens, codes, resps, resp_lens);
 }
 
 // Requests per async batch (OTM_ASYNC_BATCH): small enough that a burst of
@@ -540,6 +658,7 @@ void worker_loop(otm_engine* E, int wi) {
       reqs[(size_t)k] = batch[(size_t)k].body.data();
       lens[(size_t)k] = batch[(size_t)k].body.size();
     }
+    const double tw0 = now_ms();
     try {
       report_many(ctx, n, reqs.data(), lens.data(), codes.data(), resps.data(), rl.data());
     } catch (...) {
@@ -551,9 +670,13 @@ void worker_loop(otm_engine* E, int wi) {
         rl[(size_t)k] = 0;
       }
     }
+    const double tw1 = now_ms();
     {
       std::unique_lock<std::mutex> lk(E->qmu);
       E->qcv.wait(lk, [&] { return E->pub_seq == seq; });
+      if (json_profile())
+        std::fprintf(stderr, "[otm async] worker %d batch %llu: %d requests, start %.2f, ran %.2f, published +%.2f ms\n", wi,
+                     (unsigned long long)seq, n, tw0, tw1 - tw0, now_ms() - tw1);
       for (int k = 0; k < n; ++k)
         E->done.push_back(otm_result{batch[(size_t)k].tag, codes[(size_t)k], resps[(size_t)k], rl[(size_t)k]});
       ++E->pub_seq;

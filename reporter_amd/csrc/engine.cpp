@@ -473,13 +473,15 @@ void engine_free(otm_engine* E) {
       &E->o_segments,    &E->o_seg_gidx,   &E->o_way_ids,      &E->o_reports,  &E->o_rep_cnt,  &E->seg_ub,
       &E->f_seg_off,     &E->f_way_off,    &E->f_rep_off,      &E->f_segs,     &E->f_ways,     &E->f_reps,
       &E->f_traces,
-      &E->abort_flag,    &E->rs_blob,      &E->ord_tile,      &E->ord_cnt,      &E->ord_cursor,     &E->ord_grp,    &E->ord_item};
+      &E->abort_flag,    &E->rs_blob,      &E->ord_tile,      &E->ord_cnt,      &E->ord_cursor,     &E->ord_grp,    &E->ord_item,
+      &E->d_req,         &E->req_cnt,      &E->req_ok};
   for (auto* b : bufs) {
     if (b->p) (void)hipFree(b->p);
     b->p = nullptr;
     b->cap = 0;
   }
-  for (auto* b : {&E->h_traces, &E->h_segs, &E->h_reps_dense, &E->h_ways, &E->h_tot, &E->h_in, &E->h_status}) {
+  for (auto* b : {&E->h_traces, &E->h_segs, &E->h_reps_dense, &E->h_ways, &E->h_tot, &E->h_in, &E->h_status,
+                  &E->h_req, &E->h_req_ok}) {
     if (b->p) (void)hipHostFree(b->p);
     b->p = nullptr;
     b->cap = 0;
@@ -822,6 +824,77 @@ int engine_match_host(otm_engine* E, const otm_batch* in, std::string* err) {
   return engine_match(E, b, s, err);
 }
 
+// The staging blob of engine_match_requests: int64 offsets[n + 1] (padded to
+// 16 bytes), then the body bytes (16-byte aligned: the readers load aligned
+// 16-byte words), then REQ_PAD zero bytes (the last window's loads stay inside)
+static constexpr size_t REQ_PAD = 64;
+static size_t req_hdr_bytes(int32_t n) { return (((size_t)n + 1) * 8 + 15) & ~(size_t)15; }
+static size_t req_blob_bytes(int32_t n, size_t bytes) { return req_hdr_bytes(n) + bytes + REQ_PAD; }
+
+int engine_stage_requests(otm_engine* E, int32_t n, size_t bytes, int64_t** off, char** body, std::string* err) {
+  int rc;
+  if (n < 0) {
+    *err = "invalid request count";
+    return OTM_EINVAL;
+  }
+  if ((rc = ensure_pinned(E->h_req, req_blob_bytes(n, bytes), err))) return rc;
+  char* h = (char*)E->h_req.p;
+  std::memset(h + req_hdr_bytes(n) + bytes, 0, REQ_PAD);
+  *off = (int64_t*)h;
+  *body = h + req_hdr_bytes(n);
+  return OTM_OK;
+}
+
+int engine_match_requests(otm_engine* E, int32_t n, size_t bytes, const uint8_t** ok, int32_t* n_traces,
+                          std::string* err) {
+  int rc;
+  hipStream_t s = E->stream;
+  const size_t total = req_blob_bytes(n, bytes);
+  if ((rc = ensure(E->d_req, total, err))) return rc;
+  if ((rc = ensure(E->req_cnt, ((size_t)n + 1) * 8, err))) return rc;
+  if ((rc = ensure(E->req_ok, (size_t)n + 1, err))) return rc;
+  if ((rc = ensure_pinned(E->h_req_ok, (size_t)n + 8 + 8, err))) return rc;
+  if ((rc = ensure(E->scan_tmp, scan_tmp_bytes(n) + 256, err))) return rc;
+  // a valid point takes at least 39 bytes (`{"lat":0,"lon":0,"time":0,"accuracy":0}`)
+  // plus its separator: the batch arrays sized by that bound before the count is known
+  const size_t np_max = bytes / 39 + 1;
+  if ((rc = ensure(E->in_off, ((size_t)n + 1) * 8, err))) return rc;
+  if ((rc = ensure(E->in_lat, np_max * 4, err))) return rc;
+  if ((rc = ensure(E->in_lon, np_max * 4, err))) return rc;
+  if ((rc = ensure(E->in_time, np_max * 8, err))) return rc;
+  if ((rc = ensure(E->in_acc, np_max * 4, err))) return rc;
+  HIPCHK(big_copy(E->d_req.p, E->h_req.p, total, hipMemcpyHostToDevice, s));
+  const int64_t* off = (const int64_t*)E->d_req.p;
+  const unsigned char* body = (const unsigned char*)E->d_req.p + req_hdr_bytes(n);
+  int64_t* cnt = P<int64_t>(E->req_cnt);
+  launch_req_scan(body, off, n, cnt, P<uint8_t>(E->req_ok), s);
+  scan_i64(cnt, n, E->scan_tmp.p, E->scan_tmp.cap, s);
+  DevBatch b{};
+  b.trace_off = (const int64_t*)E->in_off.p;
+  b.lat = (const float*)E->in_lat.p;
+  b.lon = (const float*)E->in_lon.p;
+  b.time = (const double*)E->in_time.p;
+  b.acc = (const float*)E->in_acc.p;
+  launch_req_fill(body, off, n, cnt, P<uint8_t>(E->req_ok), b, P<int64_t>(E->in_off), s);
+  // the batch's size and the flags: one synchronisation before the match
+  char* h = (char*)E->h_req_ok.p;
+  HIPCHK(hipMemcpyAsync(h, cnt + n, 8, hipMemcpyDeviceToHost, s));
+  if (n) HIPCHK(hipMemcpyAsync(h + 8, E->req_ok.p, (size_t)n, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(s));
+  int64_t tot;
+  std::memcpy(&tot, h, 8);
+  b.n_traces = (int32_t)(tot >> 40);
+  b.n_points = tot & (((int64_t)1 << 40) - 1);
+  *ok = (const uint8_t*)(h + 8);
+  *n_traces = b.n_traces;
+  if ((size_t)b.n_points > np_max) {
+    *err = "request reader: point count beyond its bound";
+    return OTM_EDEVICE;
+  }
+  return engine_match(E, b, s, err);
+}
+
 int engine_fetch(otm_engine* E, otm_results* out, std::string* err) {
   hipStream_t s = E->stream;
   const int32_t NT = E->last_T;
@@ -1013,6 +1086,13 @@ int engine_debug_fetch(otm_engine* E, int what, void* dst, size_t bytes, size_t*
     case 8: src = E->route_dist.p; n = Pn * 4; break;
     case 9: src = E->gc.p; n = Pn * 4; break;
     case 10: src = E->ipos.p; n = Pn * 4; break;
+    // the last batch's inputs as the GPU request reader decoded them
+    // (engine_match_requests; also a host batch of more than 2^18 points)
+    case 11: src = E->in_off.p; n = ((size_t)E->last_T + 1) * 8; break;
+    case 12: src = E->in_lat.p; n = Pn * 4; break;
+    case 13: src = E->in_lon.p; n = Pn * 4; break;
+    case 14: src = E->in_time.p; n = Pn * 8; break;
+    case 15: src = E->in_acc.p; n = Pn * 4; break;
     default: *err = "unknown debug buffer"; return OTM_EINVAL;
   }
   if (needed) *needed = n;

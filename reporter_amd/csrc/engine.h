@@ -93,6 +93,9 @@ struct otm_engine {
   // host copies of the last fetched results
   // (pinned: the D2H copies run at PCIe speed without a staging hop)
   Buf h_traces, h_segs, h_reps_dense, h_ways, h_tot, h_in, h_status;
+  // request bodies read on the GPU (engine_match_requests): the pinned staging
+  // blob (offsets, then bytes), its device copy, per-request counts and flags
+  Buf h_req, d_req, req_cnt, req_ok, h_req_ok;
   // timing
   bool timing = false;
   hipEvent_t kev[2 * otm::KN_COUNT] = {};
@@ -131,6 +134,16 @@ void engine_free(otm_engine* E);
 int engine_match(otm_engine* E, const DevBatch& b, hipStream_t s, std::string* err);
 // stage a host batch to the device and match it
 int engine_match_host(otm_engine* E, const otm_batch* in, std::string* err);
+// The /report request bodies read on the GPU: engine_stage_requests returns a
+// pinned host staging buffer for n requests of `bytes` body bytes in all:
+// int64 offsets[n + 1] (into the bytes) and the bytes; the caller fills both
+// and calls engine_match_requests, which copies it to HBM, decodes the
+// bodies of the Java batcher's exact form (requests.hip) into a batch and
+// matches it.  *ok[r] (valid until the next call) says which requests the
+// batch holds, in request order; the others are the caller's to read.
+int engine_stage_requests(otm_engine* E, int32_t n, size_t bytes, int64_t** off, char** body, std::string* err);
+int engine_match_requests(otm_engine* E, int32_t n, size_t bytes, const uint8_t** ok, int32_t* n_traces,
+                          std::string* err);
 // copy results of the last batch to host vectors and describe them
 int engine_fetch(otm_engine* E, otm_results* out, std::string* err);
 int engine_debug_fetch(otm_engine* E, int what, void* dst, size_t bytes, size_t* needed, std::string* err);

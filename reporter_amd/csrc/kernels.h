@@ -297,6 +297,14 @@ bool fold_bookkeeping();
 void launch_status(const int32_t* abort, const int64_t* ttotal, const int32_t* counters, BatchStatus* out,
                    hipStream_t s);
 void launch_row_pack(const int32_t* row_cnt, const int64_t* row_off, IdxRow* rows, int32_t n, hipStream_t s);
+// the /report request bytes read on the GPU (requests.hip): per request of
+// the staged blob (bytes [off[r], off[r+1])), accepted << 40 | points in cnt
+// and ok[r]; after an exclusive scan of cnt (n + 1 entries), the accepted
+// requests' points into out's arrays and their offsets into trace_off
+void launch_req_scan(const unsigned char* blob, const int64_t* off, int32_t n, int64_t* cnt, uint8_t* ok,
+                     hipStream_t s);
+void launch_req_fill(const unsigned char* blob, const int64_t* off, int32_t n, const int64_t* pre,
+                     const uint8_t* ok, const DevBatch& out, int64_t* trace_off, hipStream_t s);
 // exclusive scan helpers (in place over n+1 elements: out[n] = total)
 void scan_i64(int64_t* d, int64_t n, void* tmp, size_t tmp_bytes, hipStream_t s);
 // exclusive scans of three per-trace counts (n <= FETCH_SCAN_MAX) in one

@@ -1,0 +1,278 @@
+// requests.hip -- the /report request bytes read on the GPU.
+//
+// The Java batcher writes every request as
+//   {"uuid":"K","trace":[{"lat":L,"lon":L,"time":T,"accuracy":A},...]}
+// (Batch.java:52-61, Point.java:39-45).  otm_report_batch stages the bodies
+// into one pinned blob, copies it to HBM once, and these kernels read it: one
+// wavefront per request validates that exact form and decodes its points
+// straight into the batch's SoA arrays, as host fast_request (report.cpp)
+// would -- the same accepted grammar subset and the same number conversions,
+// so a body the GPU accepts yields the host reader's points bit for bit.  A
+// body outside the form (other key orders, whitespace, escapes, exponents,
+// long literals, fewer than two points) is left to the host readers, whose
+// results and error contract are unchanged.
+//
+// Per request: the header `{"uuid":"` + printable uuid + `","trace":[`, the
+// trailer `]}`, and the points region in between.  The region is walked in
+// 4 KB windows staged in LDS (+ a 256-byte margin: a point that starts in a
+// window ends in its margin, or the body goes to the host); a lane owns the
+// '{' bytes of its 64-byte slice and parses those points from LDS.  Each point must be followed by ",{" or by
+// the end of the region, and it starts with '{', so the checks cover every
+// byte of the region; a '{' can occur nowhere else in a valid region, so the
+// point count is the '{' count.
+#include <cstdlib>
+
+#include "kernels.h"
+
+namespace otm {
+namespace {
+
+constexpr int RTB = 64;      // one wave per request
+constexpr int CH = 4096;     // window step: 64 bytes per lane
+constexpr int MARGIN = 256;  // a point starting in a step ends within this margin past it
+constexpr int WBUF = CH + MARGIN + 16;  // + the 16-byte alignment of the window's loads
+constexpr int WLOADS = (WBUF + 16 * RTB - 1) / (16 * RTB);  // 16-byte loads per lane per window
+
+__constant__ double kP10[16] = {1e0, 1e1, 1e2,  1e3,  1e4,  1e5,  1e6,  1e7,
+                                1e8, 1e9, 1e10, 1e11, 1e12, 1e13, 1e14, 1e15};
+
+struct Cur {
+  const unsigned char* L;  // window bytes (LDS)
+  int i, lim;              // position, end of readable bytes
+  __device__ int ch(int k) const { return k < lim ? (int)L[k] : -1; }
+  __device__ bool lit(const char* w) {
+    int k = 0;
+    for (; w[k]; ++k)
+      if (ch(i + k) != (unsigned char)w[k]) return false;
+    i += k;
+    return true;
+  }
+  __device__ bool digit(int k) const { return (unsigned)(ch(k) - '0') < 10u; }
+  // a JSON number as report.cpp fast_request's num() reads it: int -> exact
+  // double; float of <= 15 significant digits -> (double)m / 10^frac, the
+  // correctly rounded value; anything else (exponent, longer literal) fails
+  __device__ bool num(double* d) {
+    const int a = i;
+    const bool neg = ch(i) == '-';
+    if (neg) ++i;
+    if (!digit(i)) return false;
+    unsigned long long m = 0;
+    int nd = 0;
+    if (ch(i) == '0') {
+      ++i;
+      nd = 1;
+    } else {
+      while (digit(i)) {
+        m = m * 10ull + (unsigned long long)(ch(i) - '0');
+        ++nd;
+        ++i;
+      }
+    }
+    if (ch(i) == '.') {
+      if (!digit(i + 1)) return false;
+      ++i;
+      int frac = 0;
+      while (digit(i)) {
+        m = m * 10ull + (unsigned long long)(ch(i) - '0');
+        ++nd;
+        ++frac;
+        ++i;
+      }
+      if (ch(i) == 'e' || ch(i) == 'E') return false;
+      if (nd > 15) return false;  // host from_chars territory
+      const double v = (double)m / kP10[frac];
+      *d = neg ? -v : v;
+      return true;
+    }
+    if (ch(i) == 'e' || ch(i) == 'E') return false;
+    if (i - a > 18) return false;
+    const long long v = neg ? -(long long)m : (long long)m;
+    *d = (double)v;
+    return true;
+  }
+};
+
+// one point at window offset j; on success its values and the offset just
+// past it (the region's end, or the next point's '{')
+__device__ bool parse_point(const unsigned char* L, int j, int lim, int rend, double* la, double* lo, double* ti,
+                            double* ac) {
+  Cur c{L, j, lim};
+  if (!c.lit("{\"lat\":") || !c.num(la)) return false;
+  if (!c.lit(",\"lon\":") || !c.num(lo)) return false;
+  if (!c.lit(",\"time\":") || !c.num(ti)) return false;
+  if (!c.lit(",\"accuracy\":") || !c.num(ac)) return false;
+  if (c.ch(c.i) != '}') return false;
+  ++c.i;
+  if (c.i == rend) return true;  // the region's last point
+  return c.ch(c.i) == ',' && c.ch(c.i + 1) == '{';
+}
+
+__device__ __forceinline__ int wave_scan_incl(int v, int lane) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int n = __shfl_up(v, o, 64);
+    if (lane >= o) v += n;
+  }
+  return v;
+}
+
+// The header of request [a, e): the region [t0, t1) between `","trace":[`
+// and the final `]}`, or false.  Lane-parallel search for the uuid's end.
+__device__ bool req_header(const unsigned char* blob, int64_t a, int64_t e, int lane, int64_t* t0, int64_t* t1) {
+  const char* H = "{\"uuid\":\"";
+  if (e - a < 9 + 11 + 2) return false;
+  bool ok = true;
+  if (lane < 9) ok = blob[a + lane] == (unsigned char)H[lane];
+  if (!__all(ok)) return false;
+  // the uuid's closing quote: first '"' at >= a + 9; every byte before it
+  // printable ASCII without a backslash
+  int64_t q = -1;
+  for (int64_t base = a + 9; base < e && q < 0; base += 64) {
+    const int64_t k = base + lane;
+    const int c = k < e ? (int)blob[k] : -1;
+    const bool quote = c == '"';
+    const bool bad = k < e && !quote && (c < 0x20 || c > 0x7e || c == '\\');
+    const unsigned long long qm = __ballot(quote);
+    const unsigned long long bm = __ballot(bad);
+    const int first = qm ? __ffsll((long long)qm) - 1 : 64;
+    // a bad byte before the quote (or before the end of this chunk with no quote)
+    const unsigned long long before = first >= 64 ? ~0ull : ((1ull << first) - 1ull);
+    if (bm & before) return false;
+    if (qm) q = base + first;
+  }
+  if (q < 0) return false;
+  const char* T = "\",\"trace\":[";
+  if (q + 11 + 2 > e) return false;
+  ok = true;
+  if (lane < 11) ok = blob[q + lane] == (unsigned char)T[lane];
+  if (!__all(ok)) return false;
+  if (blob[e - 2] != ']' || blob[e - 1] != '}') return false;
+  *t0 = q + 11;
+  *t1 = e - 2;
+  return *t1 > *t0;
+}
+
+// Walk request r's points region; PASS 0 validates and counts, PASS 1 writes
+// the points of an accepted request at out + base.  Windows of CH bytes
+// (+ MARGIN) are staged in LDS with 16-byte aligned loads, all of a lane's in
+// flight at once; a lane owns the '{' bytes of its 64-byte slice of the step.
+template <int PASS>
+__device__ bool walk_points(const unsigned char* blob, int64_t t0, int64_t t1, int lane, unsigned char* L, int64_t base,
+                            const DevBatch* out, int* npts) {
+  int count = 0;
+  bool good = true;
+  for (int64_t w0 = t0; w0 < t1; w0 += CH) {
+    const int64_t al = w0 & ~(int64_t)15;  // the blob is 16-byte aligned and padded past its end
+    const int sh = (int)(w0 - al);
+    const int lim = (int)min<int64_t>((int64_t)(CH + MARGIN), t1 - w0);
+    const uint4* src = (const uint4*)(blob + al);
+    const int nld = (sh + lim + 15) >> 4;  // 16-byte words covering [w0, w0 + lim)
+    uint4 v[WLOADS];
+#pragma unroll
+    for (int u = 0; u < WLOADS; ++u) {
+      const int k = u * RTB + lane;
+      v[u] = k < nld ? src[k] : make_uint4(0u, 0u, 0u, 0u);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < WLOADS; ++u) {
+      const int k = u * RTB + lane;
+      if (k < nld) ((uint4*)L)[k] = v[u];
+    }
+    __syncthreads();
+    const unsigned char* W = L + sh;  // W[0] = byte w0
+    // the points that start in this lane's 64 bytes of the step: a valid
+    // point is >= 39 bytes, so at most two ('{' bytes beyond two: the body is
+    // invalid, and the lane's third '{' fails it below)
+    int mine = 0, k0 = -1, k1 = -1;
+    const int s0 = lane * 64, s1 = min(s0 + 64, min(CH, lim));
+    for (int k = s0; k < s1; ++k) {
+      if (W[k] != '{') continue;
+      if (mine == 0) k0 = k;
+      else if (mine == 1) k1 = k;
+      ++mine;
+    }
+    const int incl = wave_scan_incl(mine, lane);
+    const int idx = count + incl - mine;
+    if (w0 == t0 && lane == 0 && W[0] != '{') good = false;  // the region starts with a point
+    if (mine > 2) good = false;
+    // the lanes parse their points in lockstep (first points, then second)
+    for (int m = 0; m < 2; ++m) {
+      const int k = m == 0 ? k0 : k1;
+      if (PASS == 2 || __ballot(k >= 0) == 0ull) break;  // (PASS 2: diagnostic, no parsing)
+      if (k < 0) continue;
+      double la, lo, ti, ac;
+      const bool ok = parse_point(W, k, lim, (int)(t1 - w0), &la, &lo, &ti, &ac);
+      good = good && ok;
+      if (PASS == 1 && ok) {
+        const int64_t p = base + idx + m;
+        // extract_points' conversions (report.cpp)
+        ((float*)out->lat)[p] = (float)la;
+        ((float*)out->lon)[p] = (float)lo;
+        ((double*)out->time)[p] = ti;
+        ((float*)out->acc)[p] = (float)ac;
+      }
+    }
+    count += __shfl(incl, 63, 64);
+    if (!__all(good)) return false;
+  }
+  *npts = count;
+  return good;
+}
+
+// pass 0: per request, accepted << 40 | points (0 when left to the host)
+__global__ __launch_bounds__(RTB) void k_req_scan(const unsigned char* blob, const int64_t* off, int32_t n,
+                                                  int64_t* cnt, uint8_t* ok, int mode) {
+  __shared__ __attribute__((aligned(16))) unsigned char L[WBUF];
+  const int lane = threadIdx.x;
+  for (int32_t r = blockIdx.x; r < n; r += gridDim.x) {
+    const int64_t a = off[r], e = off[r + 1];
+    int64_t t0 = 0, t1 = 0;
+    int np = 0;
+    bool acc = req_header(blob, a, e, lane, &t0, &t1);
+    if (mode == 1) np = 2;
+    else if (mode == 2) acc = acc && walk_points<2>(blob, t0, t1, lane, L, 0, nullptr, &np) && np >= 2;
+    else acc = acc && walk_points<0>(blob, t0, t1, lane, L, 0, nullptr, &np) && np >= 2;
+    if (lane == 0) {
+      cnt[r] = acc ? ((int64_t)1 << 40) | (int64_t)np : 0;
+      ok[r] = acc ? 1 : 0;
+    }
+  }
+  if (blockIdx.x == 0 && lane == 0) cnt[n] = 0;
+}
+
+// pass 1 (cnt scanned): the accepted requests' points and trace offsets
+__global__ __launch_bounds__(RTB) void k_req_fill(const unsigned char* blob, const int64_t* off, int32_t n,
+                                                  const int64_t* pre, const uint8_t* ok, DevBatch out,
+                                                  int64_t* trace_off) {
+  __shared__ __attribute__((aligned(16))) unsigned char L[WBUF];
+  const int lane = threadIdx.x;
+  constexpr int64_t MASK = ((int64_t)1 << 40) - 1;
+  if (blockIdx.x == 0 && lane == 0) trace_off[pre[n] >> 40] = pre[n] & MASK;
+  for (int32_t r = blockIdx.x; r < n; r += gridDim.x) {
+    if (!ok[r]) continue;
+    const int64_t a = off[r], e = off[r + 1];
+    int64_t t0 = 0, t1 = 0;
+    int np = 0;
+    (void)req_header(blob, a, e, lane, &t0, &t1);
+    if (lane == 0) trace_off[pre[r] >> 40] = pre[r] & MASK;
+    (void)walk_points<1>(blob, t0, t1, lane, L, pre[r] & MASK, &out, &np);
+  }
+}
+
+}  // namespace
+
+void launch_req_scan(const unsigned char* blob, const int64_t* off, int32_t n, int64_t* cnt, uint8_t* ok,
+                     hipStream_t s) {
+  const int grid = n < 65536 ? (n > 0 ? n : 1) : 65536;
+  static const int mode = std::getenv("OTM_REQ_DIAG") ? std::atoi(std::getenv("OTM_REQ_DIAG")) : 0;
+  hipLaunchKernelGGL(k_req_scan, dim3(grid), dim3(RTB), 0, s, blob, off, n, cnt, ok, mode);
+}
+
+void launch_req_fill(const unsigned char* blob, const int64_t* off, int32_t n, const int64_t* pre,
+                     const uint8_t* ok, const DevBatch& out, int64_t* trace_off, hipStream_t s) {
+  const int grid = n < 65536 ? (n > 0 ? n : 1) : 65536;
+  hipLaunchKernelGGL(k_req_fill, dim3(grid), dim3(RTB), 0, s, blob, off, n, pre, ok, out, trace_off);
+}
+
+}  // namespace otm

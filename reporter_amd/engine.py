@@ -284,7 +284,10 @@ class Engine(object):
     _DEBUG = {"ncand": (0, np.int32), "cand_edge": (1, np.int32), "cand_off": (2, np.float32),
               "cand_emis": (3, np.float32), "trans_off": (4, np.int64), "trans": (5, np.float32),
               "state": (6, np.int32), "col_prev": (7, np.int32), "route_dist": (8, np.float32),
-              "gc": (9, np.float32), "ipos": (10, np.float32)}
+              "gc": (9, np.float32), "ipos": (10, np.float32),
+              # the last batch's inputs as the GPU request reader decoded them
+              "in_trace_off": (11, np.int64), "in_lat": (12, np.float32), "in_lon": (13, np.float32),
+              "in_time": (14, np.float64), "in_acc": (15, np.float32)}
 
     def debug(self, name):
         what, dt = self._DEBUG[name]

@@ -491,20 +491,29 @@ def main():
                 ta = time.perf_counter() - ta
                 return ta, np.concatenate(parts)
 
-            async_run()  # warm: the pipeline's clone and its buffers
-            ta, rr = async_run()
-            in_order = bool((np.diff(rr["tag"].astype(np.int64)) == 1).all())
-            same = all(rr["code"][i] == gpu_resp[i][0] and C.string_at(int(rr["body"][i]), int(rr["len"][i])) ==
-                       gpu_resp[i][1] for i in range(len(gpu_resp)))
-            for pb in rr["body"]:
-                L.otm_free(C.c_void_p(int(pb)))
+            async_run()  # warm: the pipeline's clones and their buffers
+            # three timed runs (the host side of a run varies with the box's
+            # CPU quota and allocator state): the mean is `value`
+            runs = []
+            for _ in range(3):
+                ta, rr = async_run()
+                runs.append(ta)
+                in_order = bool((np.diff(rr["tag"].astype(np.int64)) == 1).all())
+                same = all(rr["code"][i] == gpu_resp[i][0] and C.string_at(int(rr["body"][i]), int(rr["len"][i])) ==
+                           gpu_resp[i][1] for i in range(len(gpu_resp)))
+                for pb in rr["body"]:
+                    L.otm_free(C.c_void_p(int(pb)))
+                if not (in_order and same):
+                    break
+            ta = sum(runs) / len(runs)
             json_async = {"value": P * args.async_rounds / ta, "unit": "points/s", "requests": int(len(rr)),
-                          "seconds": ta, "results_in_submit_order": in_order,
+                          "seconds": ta, "seconds_per_run": runs,
+                          "best": P * args.async_rounds / min(runs), "results_in_submit_order": in_order,
                           "first_responses_byte_equal_to_json_report": bool(same),
                           "includes": "otm_submit_batch of the 10k Java request bodies x %d in a row (copies into the "
                                       "queue), otm_poll until every response is back: the async pipeline, %s "
-                                      "workers on their own batch contexts" %
-                                      (args.async_rounds, os.environ.get("OTM_ASYNC_WORKERS", "2"))}
+                                      "workers on their own batch contexts; mean of 3 runs" %
+                                      (args.async_rounds, os.environ.get("OTM_ASYNC_WORKERS", "3"))}
         json_leg = {"value": P / jel, "unit": "points/s", "ms_per_call": jel * 1e3, "calls": args.json_calls,
                     "async": json_async,
                     "single_request_latency": single,

@@ -381,6 +381,12 @@ int otm_get_spill_stats(otm_engine* eng, otm_spill_stats* out);
 int otm_debug_fetch(otm_engine* eng, int what, void* dst, size_t bytes,
                     size_t* needed);
 int otm_kmax(void);
+/* The GPU response writer's float formatting run on the host (test hooks):
+ * Python's repr of d into out (>= 32 bytes), its length or -1 where the
+ * writer leaves a body to the host writer; py_round3 as report() rounds
+ * lengths, 1 or 0 (unsupported). */
+int otm_debug_py_repr(double d, char* out);
+int otm_debug_py_round3(double x, double* out);
 /* Which HIP runtime this library is bound to ("<path> hip_runtime_version=N"):
  * a host that also runs torch must load torch first so both share one. */
 const char* otm_runtime_info(void);

@@ -161,6 +161,8 @@ def _declare(L):
         "otm_get_spill_stats": (C.c_int, [vp, C.POINTER(SpillStats)]),
         "otm_debug_fetch": (C.c_int, [vp, C.c_int, vp, sz, psz]),
         "otm_kmax": (C.c_int, []),
+        "otm_debug_py_repr": (C.c_int, [C.c_double, C.c_char_p]),
+        "otm_debug_py_round3": (C.c_int, [C.c_double, C.POINTER(C.c_double)]),
         "otm_batcher_defaults": (None, [C.POINTER(BatcherCfg)]),
         "otm_batcher_create": (C.c_int, [vp, C.POINTER(BatcherCfg), REPORT_FN, vp, pp]),
         "otm_batcher_destroy": (None, [vp]),

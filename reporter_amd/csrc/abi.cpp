@@ -21,6 +21,7 @@
 
 #include "engine.h"
 #include "json.h"
+#include "pyrepr.h"
 #include "report.h"
 
 using otm::json::Kind;
@@ -432,32 +433,127 @@ void run_requests(otm_engine* E, std::vector<Req>& rq, std::vector<int>& codes, 
   }
 }
 
-// every request's response copied into its own malloc'd buffer (otm_free):
-// all of them or none -- a failed allocation frees the ones already made
-// (the caller gets only the error, nothing to otm_free)
-void copy_out(int n, const std::vector<int>& c, const std::vector<std::string>& bodies, int* codes, char** resps,
-              size_t* resp_lens) {
+// Response arenas: the bodies of one request batch cut from one allocation
+// instead of one malloc each (10k mallocs per batch from many threads, each
+// first-touching fresh heap pages, measured 2-20 ms per batch inside the
+// bench against 0.5 ms warm).  otm_free recognises a pointer inside a live
+// arena by its address range and releases the arena with its last body; any
+// other pointer is std::free'd as before.  A released arena is kept (up to
+// ARENA_CACHE bytes in all) for the next batch, so its pages stay mapped.
+namespace arena {
+constexpr int SLOTS = 64;
+constexpr size_t ARENA_CACHE = (size_t)256 << 20;
+enum : int { FREE = 0, LIVE = 1, CACHED = 2 };
+struct Slot {
+  std::atomic<int> state{FREE};
+  std::atomic<uintptr_t> lo{0}, hi{0};
+  std::atomic<int64_t> refs{0};
+  char* base = nullptr;
+  size_t cap = 0;
+};
+Slot g_slot[SLOTS];
+std::mutex g_mu;
+size_t g_cached = 0;  // under g_mu
+
+// an arena of >= bytes for nbodies bodies, or nullptr (the caller mallocs each)
+char* acquire(size_t bytes, int64_t nbodies) {
+  if (nbodies <= 0) return nullptr;
+  std::lock_guard<std::mutex> lk(g_mu);
+  int best = -1, free_slot = -1;
+  for (int i = 0; i < SLOTS; ++i) {
+    const int st = g_slot[i].state.load();
+    if (st == CACHED && g_slot[i].cap >= bytes && (best < 0 || g_slot[i].cap < g_slot[best].cap)) best = i;
+    if (st == FREE && free_slot < 0) free_slot = i;
+  }
+  if (best < 0) {
+    if (free_slot < 0) return nullptr;
+    char* p = (char*)std::malloc(bytes);
+    if (!p) return nullptr;
+    best = free_slot;
+    g_slot[best].base = p;
+    g_slot[best].cap = bytes;
+  } else {
+    g_cached -= g_slot[best].cap;
+  }
+  Slot& S = g_slot[best];
+  S.refs.store(nbodies);
+  S.lo.store((uintptr_t)S.base);
+  S.hi.store((uintptr_t)S.base + S.cap);
+  S.state.store(LIVE);
+  return S.base;
+}
+
+void release(Slot& S) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (g_cached + S.cap <= ARENA_CACHE) {
+    g_cached += S.cap;
+    S.state.store(CACHED);
+  } else {
+    S.state.store(FREE);
+    std::free(S.base);
+    S.base = nullptr;
+    S.cap = 0;
+  }
+}
+
+// otm_free: a body inside a live arena, or a plain allocation
+void free_body(void* p) {
+  if (!p) return;
+  const uintptr_t a = (uintptr_t)p;
+  for (int i = 0; i < SLOTS; ++i) {
+    Slot& S = g_slot[i];
+    if (S.state.load(std::memory_order_acquire) == LIVE && a >= S.lo.load() && a < S.hi.load()) {
+      if (S.refs.fetch_sub(1) == 1) release(S);
+      return;
+    }
+  }
+  std::free(p);
+}
+}  // namespace arena
+
+// each response of a batch into its place in one arena (or its own malloc'd
+// buffer when no arena is to be had): src(k) -> (pointer, length); returns
+// false when out of host memory (nothing left allocated)
+template <class Src>
+bool place_bodies(int n, Src src, char** resps, size_t* resp_lens) {
+  std::vector<size_t> off((size_t)n + 1, 0);
+  for (int k = 0; k < n; ++k) off[(size_t)k + 1] = off[(size_t)k] + src(k).second + 1;
+  char* base = arena::acquire(off[(size_t)n], n);
   std::atomic<bool> oom{false};
   par_for((size_t)n, [&](size_t a, size_t e) {
     for (size_t k = a; k < e; ++k) {
-      codes[k] = c[k];
-      resps[k] = (char*)std::malloc(bodies[k].size() + 1);
-      if (!resps[k]) {
+      const std::pair<const char*, size_t> b = src((int)k);
+      char* p = base ? base + off[k] : (char*)std::malloc(b.second + 1);
+      if (!p) {
         oom = true;
+        resps[k] = nullptr;
         continue;
       }
-      std::memcpy(resps[k], bodies[k].data(), bodies[k].size());
-      resps[k][bodies[k].size()] = 0;
-      resp_lens[k] = bodies[k].size();
+      if (b.second) std::memcpy(p, b.first, b.second);
+      p[b.second] = 0;
+      resps[k] = p;
+      resp_lens[k] = b.second;
     }
   });
   if (oom) {
     for (int k = 0; k < n; ++k) {
-      std::free(resps[k]);
+      arena::free_body(resps[k]);
       resps[k] = nullptr;
     }
-    throw std::bad_alloc();
+    return false;
   }
+  return true;
+}
+
+// every request's response placed for the caller (otm_free releases each):
+// all of them or none -- a failed allocation frees the ones already made
+// (the caller gets only the error, nothing to otm_free)
+void copy_out(int n, const std::vector<int>& c, const std::vector<std::string>& bodies, int* codes, char** resps,
+              size_t* resp_lens) {
+  for (int k = 0; k < n; ++k) codes[k] = c[(size_t)k];
+  if (!place_bodies(n, [&](int k) { return std::pair<const char*, size_t>(bodies[(size_t)k].data(), bodies[(size_t)k].size()); },
+                    resps, resp_lens))
+    throw std::bad_alloc();
 }
 
 // the host readers: every body parsed on the host threads (fast_request, or
@@ -515,22 +611,33 @@ bool gpu_reader(const otm_engine* E, int n) {
   return n >= (m ? std::atoi(m) : 32);
 }
 
-// otm_report_batch with the bodies read on the GPU: staged into one pinned
-// blob by the host threads, copied to HBM once, decoded and matched there
-// (engine_match_requests); the responses written on the host threads.  Bodies
-// outside the Java batcher's exact form are read by the host readers after, as
-// one more batch (report_many_host: the same results and error contract).
+// The GPU response writer (responses.hip) behind the GPU request reader;
+// OTM_GPU_WRITE=0 writes the responses on the host threads instead
+bool gpu_writer() {
+  const char* v = std::getenv("OTM_GPU_WRITE");
+  return !(v && *v == '0');
+}
+
+// otm_report_batch on the GPU: the bodies staged into one pinned blob by the
+// host threads, copied to HBM once, decoded and matched there
+// (engine_match_requests), the response bodies written there
+// (engine_write_responses) and copied back as one blob, from which each
+// response is cut into its own allocation.  Bodies outside the Java
+// batcher's exact form are read by the host readers after, as one more batch
+// (report_many_host: the same results and error contract); a body the GPU
+// writer leaves (a 500, a float outside its range) is written on the host
+// from the batch's typed records.
 void report_many_device(otm_engine* E, int n, const char* const* reqs, const size_t* lens, int* codes,
                         char** resps, size_t* resp_lens) {
   const double t0 = now_ms();
-  std::vector<int> c((size_t)n, 0);
-  std::vector<std::string> bodies((size_t)n);
   std::vector<int> rest;  // left to the host readers
-  std::vector<int> inv;   // invalid speeds per accepted trace (stderr lines)
+  std::vector<int> inv;   // invalid speeds per GPU-read request (stderr lines)
   std::vector<int> which;
   double t1 = t0, t2 = t0, t3 = t0;
   int rc;
   std::string err;
+  for (int k = 0; k < n; ++k) resps[k] = nullptr;
+  std::atomic<bool> oom{false};
   {
     std::lock_guard<std::mutex> lk(E->mu);
     size_t bytes = 0;
@@ -549,30 +656,77 @@ void report_many_device(otm_engine* E, int n, const char* const* reqs, const siz
       const uint8_t* ok = nullptr;
       int32_t nt = 0;
       otm_results r;
+      bool typed = false;
+      const char* blob = nullptr;
+      const int64_t* boff = nullptr;
+      const uint8_t* hostw = nullptr;
+      const otm_trace_result* trs = nullptr;
       rc = otm::engine_match_requests(E, n, bytes, &ok, &nt, &err);
-      if (!rc) rc = otm::engine_fetch(E, &r, &err);
+      if (!rc) {
+        if (gpu_writer()) {
+          rc = otm::engine_write_responses(E, &blob, &boff, &hostw, &trs, &err);
+          bool any = false;
+          for (int32_t m = 0; !rc && m < nt && !any; ++m) any = hostw[m] != 0;
+          if (!rc && any) {
+            rc = otm::engine_fetch(E, &r, &err);  // the typed records for the host writer
+            typed = true;
+          }
+        } else {
+          rc = otm::engine_fetch(E, &r, &err);
+          typed = true;
+          trs = r.traces;
+        }
+      }
       t2 = now_ms();
       if (!rc) {
         which.reserve((size_t)nt);
         for (int k = 0; k < n; ++k) (ok[k] ? which : rest).push_back(k);
         inv.assign(which.size(), 0);
-        par_for(which.size(), [&](size_t a, size_t e) {
-          for (size_t m = a; m < e; ++m) {
-            const int k = which[m];
-            thread_local std::string scratch;
-            scratch.clear();
-            c[(size_t)k] = otm::write_report_response(r, (int32_t)m, &scratch);
-            bodies[(size_t)k].assign(scratch);
-            inv[m] = r.traces[m].code == 200 ? r.traces[m].invalid_speeds : 0;
-          }
-        });
+        // the bodies the GPU did not write (host writer, from the typed records)
+        std::vector<std::string> hb(typed ? which.size() : 0);
+        if (typed)
+          par_for(which.size(), [&](size_t a, size_t e) {
+            for (size_t m = a; m < e; ++m)
+              if (!blob || hostw[m]) codes[which[m]] = otm::write_report_response(r, (int32_t)m, &hb[m]);
+          });
+        for (size_t m = 0; m < which.size(); ++m) {
+          if (blob && !hostw[m]) codes[which[m]] = 200;
+          inv[m] = trs[m].code == 200 ? trs[m].invalid_speeds : 0;
+        }
+        // each GPU-read request's response cut from one arena (otm_free)
+        std::vector<char*> wr(which.size(), nullptr);
+        std::vector<size_t> wl(which.size(), 0);
+        if (!place_bodies(
+                (int)which.size(),
+                [&](int m) {
+                  if (blob && !hostw[m]) return std::pair<const char*, size_t>(blob + boff[m], (size_t)(boff[m + 1] - boff[m]));
+                  return std::pair<const char*, size_t>(hb[(size_t)m].data(), hb[(size_t)m].size());
+                },
+                wr.data(), wl.data()))
+          oom = true;
+        for (size_t m = 0; m < which.size(); ++m) {
+          resps[which[m]] = wr[m];
+          resp_lens[which[m]] = wl[m];
+        }
+        (void)typed;
         t3 = now_ms();
       }
     }
   }
+  auto free_all = [&] {
+    for (int k = 0; k < n; ++k) {
+      arena::free_body(resps[k]);
+      resps[k] = nullptr;
+    }
+  };
+  if (oom) {
+    free_all();
+    throw std::bad_alloc();
+  }
   if (rc) {
     // a staging or device failure: the whole batch through the host readers
     // (their own 400s, and 500s for what reaches the device)
+    free_all();
     report_many_host(E, n, reqs, lens, codes, resps, resp_lens);
     return;
   }
@@ -589,23 +743,22 @@ void report_many_device(otm_engine* E, int n, const char* const* reqs, const siz
       rq[m] = reqs[rest[m]];
       rl[m] = lens[rest[m]];
     }
-    report_many_host(E, (int)nr, rq.data(), rl.data(), rcodes.data(), rr.data(), ol.data());
-    // (their bodies move into place below: copied like the others, then freed)
+    try {
+      report_many_host(E, (int)nr, rq.data(), rl.data(), rcodes.data(), rr.data(), ol.data());
+    } catch (...) {
+      free_all();
+      throw;
+    }
     for (size_t m = 0; m < nr; ++m) {
-      c[(size_t)rest[m]] = rcodes[m];
-      bodies[(size_t)rest[m]].assign(rr[m], ol[m]);
-      std::free(rr[m]);
+      codes[rest[m]] = rcodes[m];
+      resps[rest[m]] = rr[m];
+      resp_lens[rest[m]] = ol[m];
     }
   }
-  copy_out(n, c, bodies, codes, resps, resp_lens);
-  const double t4 = now_ms();
-  par_for((size_t)n, [&](size_t a, size_t e) {
-    for (size_t k = a; k < e; ++k) std::string().swap(bodies[k]);
-  });
   if (json_profile())
-    std::fprintf(stderr, "[otm json gpu] %d requests (%zu on the host readers): stage %.2f, gpu %.2f, write %.2f, "
-                 "copy out %.2f, free %.2f ms\n",
-                 n, rest.size(), t1 - t0, t2 - t1, t3 - t2, t4 - t3, now_ms() - t4);
+    std::fprintf(stderr, "[otm json gpu] %d requests (%zu on the host readers): stage %.2f, gpu %.2f, copy out %.2f, "
+                 "host readers %.2f ms\n",
+                 n, rest.size(), t1 - t0, t2 - t1, t3 - t2, now_ms() - t3);
 }
 
 void report_many(otm_engine* E, int n, const char* const* reqs, const size_t* lens, int* codes, char** resps,
@@ -615,18 +768,20 @@ void report_many(otm_engine* E, int n, const char* const* reqs, const size_t* le
 }
 
 // Requests per async batch (OTM_ASYNC_BATCH): small enough that a burst of
-// submissions splits over the pipeline's workers, large enough to fill the GPU.
+// submissions splits over the pipeline's workers, large enough to fill the GPU
+// (profiles/r03_s2/async_ab.txt: 3 workers x 16384 the steadiest, ~250M points/s
+// on 10k-request submissions; 2 x 8192 ~220M; 1 worker ~150M).
 size_t async_batch() {
   const char* e = std::getenv("OTM_ASYNC_BATCH");  // (read per batch: tests switch it)
-  return e ? (size_t)std::max(1, std::atoi(e)) : (size_t)8192;
+  return e ? (size_t)std::max(1, std::atoi(e)) : (size_t)16384;
 }
-// Pipeline depth (OTM_ASYNC_WORKERS, default 2): batch contexts working at
+// Pipeline depth (OTM_ASYNC_WORKERS, default 3): batch contexts working at
 // once.  A multi-device engine or a clone runs one (its members / parent own
 // the other contexts).
 int async_workers(const otm_engine* E) {
   if (!E->members.empty() || E->parent) return 1;
   const char* e = std::getenv("OTM_ASYNC_WORKERS");
-  return e ? std::max(1, std::min(8, std::atoi(e))) : 2;
+  return e ? std::max(1, std::min(8, std::atoi(e))) : 3;
 }
 
 // Worker wi of the async pipeline: take the next batch (in submit order, a
@@ -703,7 +858,12 @@ extern "C" {
 
 const char* otm_last_error(const otm_engine*) { return t_err.empty() ? otm::thread_error() : t_err.c_str(); }
 
-void otm_free(void* p) { std::free(p); }
+void otm_free(void* p) { arena::free_body(p); }
+
+// the GPU response writer's number formatting, compiled for the host: the
+// checks of tests/test_pyrepr.py against Python's own repr / round
+int otm_debug_py_repr(double d, char* out) { return otm::pyrepr::py_repr(d, out); }
+int otm_debug_py_round3(double x, double* out) { return otm::pyrepr::py_round3(x, out) ? 1 : 0; }
 
 int otm_kmax(void) { return otm::KMAX; }
 
@@ -891,7 +1051,7 @@ void otm_engine_destroy(otm_engine* E) {
     }
     E->qcv.notify_all();
     for (auto& t : E->workers) t.join();  // (queued requests are finished first)
-    for (auto& r : E->done) std::free(r.body);
+    for (auto& r : E->done) arena::free_body(r.body);
     for (otm_engine* C : E->actx) otm_engine_destroy(C);
   }
   if (!E->members.empty()) {
@@ -1201,7 +1361,9 @@ static int otm_match_device_impl(otm_engine* E, const otm_batch* in, void* strea
   b.time = in->time;
   b.acc = in->accuracy;
   std::string err;
+  E->spin_waits = true;  // (wait_batch: the caller's threads drive the GPU)
   int rc = otm::engine_match(E, b, (hipStream_t)stream, &err);
+  E->spin_waits = false;
   return rc ? fail(rc, err) : OTM_OK;
 }
 

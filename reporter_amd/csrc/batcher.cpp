@@ -410,7 +410,7 @@ void complete(otm_batcher* B, uint32_t k, int trim, int code, char* body, size_t
   } else {
     // clean()/close() discard the response; the batch object stays in the
     // store even when emptied (store.get returned it, nothing puts it back)
-    std::free(body);
+    otm_free(body);
   }
   ks.waiting = false;
   if (ks.ob < ks.oe && !ks.queued) {
@@ -592,7 +592,7 @@ int issue_json(otm_batcher* B, size_t r0, size_t r1) {
       size_t blen = 0;
       otm_encode_request(ks.key.c_str(), (int)la.size(), la.data(), lo.data(), tm.data(), ac.data(), &body, &blen);
       B->reqs[i].body.assign(body, blen);
-      std::free(body);
+      otm_free(body);
       rp[i - r0] = B->reqs[i].body.data();
       rl[i - r0] = B->reqs[i].body.size();
     }
@@ -611,7 +611,7 @@ int issue_json(otm_batcher* B, size_t r0, size_t r1) {
     // of this chunk completes that way; the drain goes on with the next.
     B->err = "matcher callback failed";
     B->st.null_responses += n;
-    for (int i = 0; i < n; ++i) std::free(outs[(size_t)i]);
+    for (int i = 0; i < n; ++i) otm_free(outs[(size_t)i]);
     par(B, (size_t)n, [&](Sink& sk, size_t a, size_t e) {
       for (size_t i = a; i < e; ++i) complete(B, B->reqs[r0 + i].key, -2, 0, nullptr, 0, sk);
     });
@@ -748,8 +748,8 @@ static int otm_batcher_create_impl(otm_engine* eng, const otm_batcher_cfg* cfg, 
 void otm_batcher_destroy(otm_batcher* B) {
   if (!B) return;
   for (auto& f : B->out) {
-    std::free(f.key);
-    std::free(f.body);
+    otm_free(f.key);
+    otm_free(f.body);
   }
   delete B;
 }

@@ -55,6 +55,31 @@ static T* P(otm_engine::Buf& b) {
   return (T*)b.p;
 }
 
+// A batch's host waits.  Large batches block on an event, so the waiting
+// thread sleeps instead of spinning: with several batch contexts in flight
+// (the async pipeline, the bench's in-flight contexts) spinning waiters hold
+// CPUs the host threads need (the GPU box grants 16), and the cgroup then
+// throttles the whole process.  Small batches (latency-bound single requests
+// and batcher rounds) spin as hipStreamSynchronize does, and so do
+// otm_match_device batches (their caller drives the GPU from its own threads:
+// measured 1.27 vs 1.25G points/s on the bench's device leg, while the host
+// leg went 0.57 -> 0.80G and the async JSON path 170 -> 221M with blocking
+// waits).  OTM_BLOCKING_SYNC=0 spins always.
+static hipError_t wait_batch(otm_engine* E, hipStream_t s, int64_t points) {
+  static const int64_t min_pts = [] {
+    const char* v = std::getenv("OTM_BLOCKING_SYNC");
+    return v && *v == '0' ? INT64_MAX : (int64_t)65536;
+  }();
+  if (points < min_pts || E->spin_waits) return hipStreamSynchronize(s);
+  if (!E->sync_ev) {
+    const hipError_t e = hipEventCreateWithFlags(&E->sync_ev, hipEventBlockingSync | hipEventDisableTiming);
+    if (e != hipSuccess) return e;
+  }
+  const hipError_t e = hipEventRecord(E->sync_ev, s);
+  if (e != hipSuccess) return e;
+  return hipEventSynchronize(E->sync_ev);
+}
+
 int build_index(otm_engine* E, std::string* err);
 
 // exp(x), 0 <= x <= 4: Taylor series in double with a fixed term order, so the
@@ -474,18 +499,22 @@ void engine_free(otm_engine* E) {
       &E->f_seg_off,     &E->f_way_off,    &E->f_rep_off,      &E->f_segs,     &E->f_ways,     &E->f_reps,
       &E->f_traces,
       &E->abort_flag,    &E->rs_blob,      &E->ord_tile,      &E->ord_cnt,      &E->ord_cursor,     &E->ord_grp,    &E->ord_item,
-      &E->d_req,         &E->req_cnt,      &E->req_ok};
+      &E->d_req,         &E->req_cnt,      &E->req_ok,
+      &E->resp_hdr,      &E->resp_seg,     &E->resp_rep,       &E->resp_hlen,      &E->resp_slen,  &E->resp_rlen,
+      &E->resp_blen,     &E->resp_host,    &E->resp_blob};
   for (auto* b : bufs) {
     if (b->p) (void)hipFree(b->p);
     b->p = nullptr;
     b->cap = 0;
   }
   for (auto* b : {&E->h_traces, &E->h_segs, &E->h_reps_dense, &E->h_ways, &E->h_tot, &E->h_in, &E->h_status,
-                  &E->h_req, &E->h_req_ok}) {
+                  &E->h_req, &E->h_req_ok, &E->h_resp, &E->h_resp_meta}) {
     if (b->p) (void)hipHostFree(b->p);
     b->p = nullptr;
     b->cap = 0;
   }
+  if (E->sync_ev) (void)hipEventDestroy(E->sync_ev);
+  E->sync_ev = nullptr;
   if (E->ctr) (void)hipFree(E->ctr);
   if (E->ctr_save) (void)hipFree(E->ctr_save);
   E->ctr = E->ctr_save = nullptr;
@@ -715,7 +744,7 @@ int engine_match(otm_engine* E, const DevBatch& b, hipStream_t s, std::string* e
     BatchStatus* dst = (BatchStatus*)(P<char>(E->snap) + 192);
     launch_status(P<int32_t>(E->abort_flag), P<int64_t>(E->trans_off) + NP, P<int32_t>(E->counters_i32), dst, s);
     HIPCHK(hipMemcpyAsync(E->h_status.p, dst, sizeof(BatchStatus), hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
+    HIPCHK(wait_batch(E, s, NP));
     const BatchStatus st = *(const BatchStatus*)E->h_status.p;
     const int32_t ab = st.abort;
     const int64_t ttotal = st.ttotal;
@@ -881,7 +910,7 @@ int engine_match_requests(otm_engine* E, int32_t n, size_t bytes, const uint8_t*
   HIPCHK(hipMemcpyAsync(h, cnt + n, 8, hipMemcpyDeviceToHost, s));
   if (n) HIPCHK(hipMemcpyAsync(h + 8, E->req_ok.p, (size_t)n, hipMemcpyDeviceToHost, s));
   HIPCHK(hipGetLastError());
-  HIPCHK(hipStreamSynchronize(s));
+  HIPCHK(wait_batch(E, s, (int64_t)(bytes / 40)));
   int64_t tot;
   std::memcpy(&tot, h, 8);
   b.n_traces = (int32_t)(tot >> 40);
@@ -895,7 +924,9 @@ int engine_match_requests(otm_engine* E, int32_t n, size_t bytes, const uint8_t*
   return engine_match(E, b, s, err);
 }
 
-int engine_fetch(otm_engine* E, otm_results* out, std::string* err) {
+// The last batch's results compacted on the device into the dense f_*
+// arrays (traces with dense offsets); *NS / *NW / *NR their totals.
+static int fetch_compact(otm_engine* E, int32_t* NS_, int32_t* NW_, int32_t* NR_, std::string* err) {
   hipStream_t s = E->stream;
   const int32_t NT = E->last_T;
   int rc;
@@ -916,7 +947,7 @@ int engine_fetch(otm_engine* E, otm_results* out, std::string* err) {
     HIPCHK(hipMemcpyAsync(tot, so + NT, 4, hipMemcpyDeviceToHost, s));
     HIPCHK(hipMemcpyAsync(tot + 1, wo + NT, 4, hipMemcpyDeviceToHost, s));
     HIPCHK(hipMemcpyAsync(tot + 2, ro + NT, 4, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
+    HIPCHK(wait_batch(E, s, E->last_P));
   } else if (NT) {
     HIPCHK(hipMemcpyAsync(so, E->o_seg_cnt.p, (size_t)NT * 4, hipMemcpyDeviceToDevice, s));
     HIPCHK(hipMemcpyAsync(wo, E->o_way_cnt.p, (size_t)NT * 4, hipMemcpyDeviceToDevice, s));
@@ -930,7 +961,7 @@ int engine_fetch(otm_engine* E, otm_results* out, std::string* err) {
     HIPCHK(hipMemcpyAsync(tot, so + NT, 4, hipMemcpyDeviceToHost, s));
     HIPCHK(hipMemcpyAsync(tot + 1, wo + NT, 4, hipMemcpyDeviceToHost, s));
     HIPCHK(hipMemcpyAsync(tot + 2, ro + NT, 4, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
+    HIPCHK(wait_batch(E, s, E->last_P));
   }
   const int32_t NS = tot[0], NW = tot[1], NR = tot[2];
   ENS_F(f_segs, ((size_t)NS + 1) * sizeof(otm_segment));
@@ -951,6 +982,18 @@ int engine_fetch(otm_engine* E, otm_results* out, std::string* err) {
   }
   E->last_S = NS;
   E->last_W = NW;
+  *NS_ = NS;
+  *NW_ = NW;
+  *NR_ = NR;
+  return OTM_OK;
+}
+
+int engine_fetch(otm_engine* E, otm_results* out, std::string* err) {
+  hipStream_t s = E->stream;
+  const int32_t NT = E->last_T;
+  int32_t NS, NW, NR;
+  int rc;
+  if ((rc = fetch_compact(E, &NS, &NW, &NR, err))) return rc;
   if ((rc = ensure_pinned(E->h_traces, ((size_t)NT + 1) * sizeof(otm_trace_result), err))) return rc;
   if ((rc = ensure_pinned(E->h_segs, ((size_t)NS + 1) * sizeof(otm_segment), err))) return rc;
   if ((rc = ensure_pinned(E->h_reps_dense, ((size_t)NR + 1) * sizeof(otm_report_rec), err))) return rc;
@@ -960,7 +1003,7 @@ int engine_fetch(otm_engine* E, otm_results* out, std::string* err) {
   if (NS) HIPCHK(big_copy(E->h_segs.p, E->f_segs.p, (size_t)NS * sizeof(otm_segment), d2h, s));
   if (NR) HIPCHK(big_copy(E->h_reps_dense.p, E->f_reps.p, (size_t)NR * sizeof(otm_report_rec), d2h, s));
   if (NW) HIPCHK(big_copy(E->h_ways.p, E->f_ways.p, (size_t)NW * 8, d2h, s));
-  HIPCHK(hipStreamSynchronize(s));
+  HIPCHK(wait_batch(E, s, E->last_P));
   out->n_traces = NT;
   out->n_segments = NS;
   out->n_reports = NR;
@@ -969,6 +1012,63 @@ int engine_fetch(otm_engine* E, otm_results* out, std::string* err) {
   out->segments = (const otm_segment*)E->h_segs.p;
   out->reports = (const otm_report_rec*)E->h_reps_dense.p;
   out->way_ids = (const int64_t*)E->h_ways.p;
+  return OTM_OK;
+}
+
+int engine_write_responses(otm_engine* E, const char** blob, const int64_t** off, const uint8_t** host,
+                           const otm_trace_result** traces, std::string* err) {
+  hipStream_t s = E->stream;
+  const int32_t NT = E->last_T;
+  int32_t NS, NW, NR;
+  int rc;
+  if ((rc = fetch_compact(E, &NS, &NW, &NR, err))) return rc;
+  const size_t hdr_b = (size_t)NT * RESP_HDR_SLOT + 64, seg_b = resp_seg_scratch(NS, NW),
+               rep_b = (size_t)NR * RESP_REP_SLOT + 64;
+  ENS_F(resp_hdr, hdr_b);
+  ENS_F(resp_seg, seg_b);
+  ENS_F(resp_rep, rep_b);
+  ENS_F(resp_hlen, ((size_t)NT + 1) * 4);
+  ENS_F(resp_slen, ((size_t)NS + 1) * 4);
+  ENS_F(resp_rlen, ((size_t)NR + 1) * 4);
+  ENS_F(resp_blen, ((size_t)NT + 1) * 8);
+  ENS_F(resp_host, (size_t)NT + 1);
+  // a body is at most its pieces plus the joins (commas, the fixed middle and end)
+  const size_t blob_b = hdr_b + seg_b + rep_b + (size_t)NT * 96 + (size_t)NS + (size_t)NR;
+  ENS_F(resp_blob, blob_b);
+  if ((rc = ensure(E->scan_tmp, scan_tmp_bytes(NT) + 256, err))) return rc;
+  RespIn in{NT, NS, NR, (const otm_trace_result*)E->f_traces.p, (const otm_segment*)E->f_segs.p,
+            P<int64_t>(E->f_ways), (const otm_report_rec*)E->f_reps.p};
+  RespWork w{P<char>(E->resp_hdr),   P<char>(E->resp_seg),     P<char>(E->resp_rep),    P<int32_t>(E->resp_hlen),
+             P<int32_t>(E->resp_slen), P<int32_t>(E->resp_rlen), P<int64_t>(E->resp_blen), P<uint8_t>(E->resp_host)};
+  if (NT) {
+    launch_resp_items(in, w, s);
+    launch_resp_len(in, w, s);
+    scan_i64(w.blen, NT, E->scan_tmp.p, E->scan_tmp.cap, s);
+    launch_resp_copy(in, w, w.blen, P<char>(E->resp_blob), s);
+  }
+  // the offsets, flags and trace records, then the bodies
+  const size_t off_b = ((size_t)NT + 1) * 8;
+  if ((rc = ensure_pinned(E->h_resp_meta, off_b + (size_t)NT + 8, err))) return rc;
+  if ((rc = ensure_pinned(E->h_traces, ((size_t)NT + 1) * sizeof(otm_trace_result), err))) return rc;
+  char* meta = (char*)E->h_resp_meta.p;
+  std::memset(meta, 0, off_b);
+  if (NT) {
+    HIPCHK(hipMemcpyAsync(meta, w.blen, off_b, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(meta + off_b, w.host, (size_t)NT, hipMemcpyDeviceToHost, s));
+    HIPCHK(big_copy(E->h_traces.p, E->f_traces.p, (size_t)NT * sizeof(otm_trace_result), hipMemcpyDeviceToHost, s));
+  }
+  HIPCHK(hipGetLastError());
+  HIPCHK(wait_batch(E, s, E->last_P));
+  const int64_t total = ((const int64_t*)meta)[NT];
+  if ((rc = ensure_pinned(E->h_resp, (size_t)total + 16, err))) return rc;
+  if (total) {
+    HIPCHK(big_copy(E->h_resp.p, E->resp_blob.p, (size_t)total, hipMemcpyDeviceToHost, s));
+    HIPCHK(wait_batch(E, s, E->last_P));
+  }
+  *blob = (const char*)E->h_resp.p;
+  *off = (const int64_t*)meta;
+  *host = (const uint8_t*)(meta + off_b);
+  *traces = (const otm_trace_result*)E->h_traces.p;
   return OTM_OK;
 }
 

@@ -30,6 +30,8 @@ struct otm_engine {
   int device = 0;
   int n_clones = 0;  // clones made of this engine (their stream slots)
   hipStream_t stream = nullptr;
+  hipEvent_t sync_ev = nullptr;  // blocking-sync event of large batches' host waits
+  bool spin_waits = false;       // otm_match_device in progress: spin-wait (engine.cpp wait_batch)
   otm::HostGraph host;
   otm::DevGraph g{};
   std::vector<void*> graph_allocs;
@@ -96,6 +98,10 @@ struct otm_engine {
   // request bodies read on the GPU (engine_match_requests): the pinned staging
   // blob (offsets, then bytes), its device copy, per-request counts and flags
   Buf h_req, d_req, req_cnt, req_ok, h_req_ok;
+  // response bodies written on the GPU (engine_write_responses): piece slots,
+  // lengths, the dense blob, and its pinned host copy with offsets and flags
+  Buf resp_hdr, resp_seg, resp_rep, resp_hlen, resp_slen, resp_rlen, resp_blen, resp_host, resp_blob;
+  Buf h_resp, h_resp_meta;
   // timing
   bool timing = false;
   hipEvent_t kev[2 * otm::KN_COUNT] = {};
@@ -144,6 +150,13 @@ int engine_match_host(otm_engine* E, const otm_batch* in, std::string* err);
 int engine_stage_requests(otm_engine* E, int32_t n, size_t bytes, int64_t** off, char** body, std::string* err);
 int engine_match_requests(otm_engine* E, int32_t n, size_t bytes, const uint8_t** ok, int32_t* n_traces,
                           std::string* err);
+// The last batch's /report response bodies written on the GPU
+// (responses.hip): trace t's body is blob[off[t], off[t + 1]) unless host[t]
+// (a 500, or a float the GPU does not format: the host writes those from
+// engine_fetch's records); traces[t] its result record.  The pointers stay
+// valid until the next batch.
+int engine_write_responses(otm_engine* E, const char** blob, const int64_t** off, const uint8_t** host,
+                           const otm_trace_result** traces, std::string* err);
 // copy results of the last batch to host vectors and describe them
 int engine_fetch(otm_engine* E, otm_results* out, std::string* err);
 int engine_debug_fetch(otm_engine* E, int what, void* dst, size_t bytes, size_t* needed, std::string* err);

@@ -18,6 +18,8 @@
 
 #include <cstdint>
 
+#include "otmatch.h"
+
 namespace otm {
 
 constexpr int KMAX = 32;           // max candidates per column (== ORC_KMAX)
@@ -305,6 +307,28 @@ void launch_req_scan(const unsigned char* blob, const int64_t* off, int32_t n, i
                      hipStream_t s);
 void launch_req_fill(const unsigned char* blob, const int64_t* off, int32_t n, const int64_t* pre,
                      const uint8_t* ok, const DevBatch& out, int64_t* trace_off, hipStream_t s);
+// the /report response bodies written on the GPU (responses.hip) from a
+// batch's dense results (engine_fetch's compaction, device side)
+constexpr int RESP_HDR_SLOT = 512;  // bytes of a trace's header piece
+constexpr int RESP_SEG_SLOT = 320;  // ... of a segment object, + 21 per way id
+constexpr int RESP_REP_SLOT = 192;  // ... of a datastore report object
+struct RespIn {
+  int32_t nt, ns, nr;
+  const otm_trace_result* traces;
+  const otm_segment* segs;
+  const int64_t* ways;
+  const otm_report_rec* reps;
+};
+struct RespWork {
+  char *hdr, *seg, *rep;       // piece slots
+  int32_t *hlen, *slen, *rlen;  // piece lengths (-1: a float the host formats)
+  int64_t* blen;               // [nt + 1] body lengths, scanned in place into offsets
+  uint8_t* host;               // [nt] 1: the host writes this body
+};
+size_t resp_seg_scratch(int32_t ns, int32_t nw);
+void launch_resp_items(const RespIn& in, const RespWork& w, hipStream_t s);
+void launch_resp_len(const RespIn& in, const RespWork& w, hipStream_t s);
+void launch_resp_copy(const RespIn& in, const RespWork& w, const int64_t* boff, char* blob, hipStream_t s);
 // exclusive scan helpers (in place over n+1 elements: out[n] = total)
 void scan_i64(int64_t* d, int64_t n, void* tmp, size_t tmp_bytes, hipStream_t s);
 // exclusive scans of three per-trace counts (n <= FETCH_SCAN_MAX) in one

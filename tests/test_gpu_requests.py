@@ -1,5 +1,6 @@
-"""The GPU request reader (reporter_amd/csrc/requests.hip): otm_report_batch's
-bodies decoded on the device.  A body in the Java batcher's exact form
+"""The GPU request reader and response writer (reporter_amd/csrc/requests.hip,
+responses.hip): otm_report_batch's bodies decoded and its responses written
+on the device.  A body in the Java batcher's exact form
 (Batch.java:52-61, Point.java:39-45) must decode to the host reader's points
 bit for bit (report.cpp fast_request, itself pinned against the DOM path in
 test_fast_request.py), every other body must be left to the host readers,
@@ -81,7 +82,8 @@ def test_gpu_reader_points_match_host_reader(small_graph):
         assert tuple(g[a:e].tobytes() for g in got) == want[:4], body[:80]
 
 
-def test_gpu_reader_mixed_bodies_byte_equal_to_host_readers(small_graph, oracle, monkeypatch):
+@pytest.mark.parametrize("writer", ["1", "0"], ids=["gpu_writer", "host_writer"])
+def test_gpu_reader_mixed_bodies_byte_equal_to_host_readers(small_graph, oracle, monkeypatch, writer):
     """Java bodies mixed with mutated ones (whitespace, key orders, escapes,
     exponents, bigints, one-point traces, malformed JSON): the GPU reader takes
     exactly the exact-form bodies, and every response (code and body) equals the
@@ -100,7 +102,13 @@ def test_gpu_reader_mixed_bodies_byte_equal_to_host_readers(small_graph, oracle,
                b'{"uuid":"x","trace":[{"lat":1,"lon":2,"time":3,"accuracy":4},,{"lat":1,"lon":2,"time":9,"accuracy":4}]}',
                b'{"uuid":"x","trace":[{"lat":1,"lon":2,"time":3,"accuracy":4}{"lat":1,"lon":2,"time":9,"accuracy":4}]}',
                b'{"uuid":"{","trace":[{"lat":1,"lon":2,"time":3,"accuracy":4},{"lat":1.0e1,"lon":2,"time":9,"accuracy":4}]}']
+    # times below the GPU writer's float range (2^-10): those bodies' floats
+    # are formatted by the host writer from the typed records
+    for b in base[:6]:
+        cnt = iter(range(1, 10 ** 6))
+        bodies.append(re.sub(r'"time":[0-9]+', lambda m: '"time":0.0000%03d' % next(cnt), b.decode()).encode())
     assert 0 < sum(map(gpu_form, bodies)) < len(bodies)
+    monkeypatch.setenv("OTM_GPU_WRITE", writer)
     g = oracle.Graph(small_graph)
     with Engine(graph_path=small_graph) as eng:
         got = eng.report_batch(bodies)
@@ -112,7 +120,8 @@ def test_gpu_reader_mixed_bodies_byte_equal_to_host_readers(small_graph, oracle,
         assert cr == oracle.handle_request(g, body), body[:80]
 
 
-def test_gpu_reader_long_bodies_and_windows(small_graph, oracle):
+@pytest.mark.parametrize("writer", ["1", "0"], ids=["gpu_writer", "host_writer"])
+def test_gpu_reader_long_bodies_and_windows(small_graph, oracle, monkeypatch, writer):
     """traces long enough to span many of the reader's 1 KB windows, with
     points of every length, and uuids of every length up to 300 bytes"""
     b = synth.make_traces(small_graph, 40, 400, seed=73)
@@ -122,6 +131,7 @@ def test_gpu_reader_long_bodies_and_windows(small_graph, oracle):
         bodies.append(encode_request("u" * (t * 7 + 1), b["lat"][a:e], b["lon"][a:e], b["time"][a:e].astype(np.int64),
                                      b["accuracy"][a:e].astype(np.int32)))
     assert all(gpu_form(x) for x in bodies)
+    monkeypatch.setenv("OTM_GPU_WRITE", writer)
     g = oracle.Graph(small_graph)
     with Engine(graph_path=small_graph) as eng:
         got = eng.report_batch(bodies)

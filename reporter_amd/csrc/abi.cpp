@@ -648,10 +648,29 @@ void report_many_device(otm_engine* E, int n, const char* const* reqs, const siz
     if (!rc) {
       off[0] = 0;
       for (int k = 0; k < n; ++k) off[k + 1] = off[k] + (int64_t)lens[k];
-      par_for((size_t)n, [&](size_t a, size_t e) {
-        for (size_t k = a; k < e; ++k)
-          if (lens[k]) std::memcpy(dst + off[k], reqs[k], lens[k]);
-      });
+      // staged in pieces of ~16 MB, each on its way to HBM while the next is
+      // copied (the host copy and the DMA overlap)
+      constexpr size_t PIECE = (size_t)16 << 20;
+      int k0 = 0;
+      size_t from = 0;
+      while (!rc && k0 < n) {
+        int k1 = k0;
+        while (k1 < n && (size_t)off[k1 + 1] - from <= PIECE) ++k1;
+        if (k1 == k0) ++k1;  // one body larger than a piece
+        par_for((size_t)(k1 - k0), [&](size_t a, size_t e) {
+          for (size_t m = a; m < e; ++m) {
+            const size_t k = (size_t)k0 + m;
+            if (lens[k]) std::memcpy(dst + off[k], reqs[k], lens[k]);
+          }
+        });
+        const size_t to = (size_t)off[k1];
+        rc = otm::engine_push_requests(E, n, bytes, from, to, &err);
+        from = to;
+        k0 = k1;
+      }
+      if (!rc && n == 0) rc = otm::engine_push_requests(E, n, bytes, 0, 0, &err);
+    }
+    if (!rc) {
       t1 = now_ms();
       const uint8_t* ok = nullptr;
       int32_t nt = 0;
@@ -661,7 +680,7 @@ void report_many_device(otm_engine* E, int n, const char* const* reqs, const siz
       const int64_t* boff = nullptr;
       const uint8_t* hostw = nullptr;
       const otm_trace_result* trs = nullptr;
-      rc = otm::engine_match_requests(E, n, bytes, &ok, &nt, &err);
+      rc = otm::engine_match_requests(E, n, bytes, true, &ok, &nt, &err);
       if (!rc) {
         if (gpu_writer()) {
           rc = otm::engine_write_responses(E, &blob, &boff, &hostw, &trs, &err);

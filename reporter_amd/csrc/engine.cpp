@@ -874,8 +874,20 @@ int engine_stage_requests(otm_engine* E, int32_t n, size_t bytes, int64_t** off,
   return OTM_OK;
 }
 
-int engine_match_requests(otm_engine* E, int32_t n, size_t bytes, const uint8_t** ok, int32_t* n_traces,
-                          std::string* err) {
+// the device copy of the staging blob, and one piece of it on its way: body
+// bytes [from, to) (with the offsets header when from == 0, the padding when
+// to == bytes), so the host can stage the next piece while this one moves
+int engine_push_requests(otm_engine* E, int32_t n, size_t bytes, size_t from, size_t to, std::string* err) {
+  int rc;
+  if ((rc = ensure(E->d_req, req_blob_bytes(n, bytes), err))) return rc;
+  const size_t a = from ? req_hdr_bytes(n) + from : 0;
+  const size_t b = req_hdr_bytes(n) + (to >= bytes ? bytes + REQ_PAD : to);
+  if (b > a) HIPCHK(big_copy((char*)E->d_req.p + a, (const char*)E->h_req.p + a, b - a, hipMemcpyHostToDevice, E->stream));
+  return OTM_OK;
+}
+
+int engine_match_requests(otm_engine* E, int32_t n, size_t bytes, bool pushed, const uint8_t** ok,
+                          int32_t* n_traces, std::string* err) {
   int rc;
   hipStream_t s = E->stream;
   const size_t total = req_blob_bytes(n, bytes);
@@ -892,7 +904,7 @@ int engine_match_requests(otm_engine* E, int32_t n, size_t bytes, const uint8_t*
   if ((rc = ensure(E->in_lon, np_max * 4, err))) return rc;
   if ((rc = ensure(E->in_time, np_max * 8, err))) return rc;
   if ((rc = ensure(E->in_acc, np_max * 4, err))) return rc;
-  HIPCHK(big_copy(E->d_req.p, E->h_req.p, total, hipMemcpyHostToDevice, s));
+  if (!pushed) HIPCHK(big_copy(E->d_req.p, E->h_req.p, total, hipMemcpyHostToDevice, s));
   const int64_t* off = (const int64_t*)E->d_req.p;
   const unsigned char* body = (const unsigned char*)E->d_req.p + req_hdr_bytes(n);
   int64_t* cnt = P<int64_t>(E->req_cnt);

@@ -148,8 +148,11 @@ int engine_match_host(otm_engine* E, const otm_batch* in, std::string* err);
 // matches it.  *ok[r] (valid until the next call) says which requests the
 // batch holds, in request order; the others are the caller's to read.
 int engine_stage_requests(otm_engine* E, int32_t n, size_t bytes, int64_t** off, char** body, std::string* err);
-int engine_match_requests(otm_engine* E, int32_t n, size_t bytes, const uint8_t** ok, int32_t* n_traces,
-                          std::string* err);
+// (engine_push_requests: a piece of the staged blob on its way to HBM, so
+// staging and copying overlap; pushed = every piece went that way)
+int engine_push_requests(otm_engine* E, int32_t n, size_t bytes, size_t from, size_t to, std::string* err);
+int engine_match_requests(otm_engine* E, int32_t n, size_t bytes, bool pushed, const uint8_t** ok,
+                          int32_t* n_traces, std::string* err);
 // The last batch's /report response bodies written on the GPU
 // (responses.hip): trace t's body is blob[off[t], off[t + 1]) unless host[t]
 // (a 500, or a float the GPU does not format: the host writes those from

@@ -494,7 +494,7 @@ void engine_free(otm_engine* E) {
       &E->probe,         &E->col_prev,     &E->kq_prev,        &E->trans_off,      &E->trans,          &E->bp,         &E->state,      &E->chosen,
       &E->chain_start,   &E->route_dist,   &E->ipos,   &E->path_off,       &E->path_len,       &E->path_pool,  &E->trace_err,
       &E->overflow_list0, &E->overflow_list2, &E->counters_i32, &E->scan_tmp, &E->snap,   &E->big_key,
-      &E->big_lab,       &E->big_inq,      &E->big_fr,         &E->o_traces,       &E->o_seg_cnt,  &E->o_way_cnt,
+      &E->big_lab,       &E->big_inq,      &E->big_fr,         &E->big_ins,        &E->big_prev,         &E->o_traces,       &E->o_seg_cnt,  &E->o_way_cnt,
       &E->o_segments,    &E->o_seg_gidx,   &E->o_way_ids,      &E->o_reports,  &E->o_rep_cnt,  &E->seg_ub,
       &E->f_seg_off,     &E->f_way_off,    &E->f_rep_off,      &E->f_segs,     &E->f_ways,     &E->f_reps,
       &E->f_traces,
@@ -527,10 +527,21 @@ void engine_free(otm_engine* E) {
 static int ensure_big(otm_engine* E, std::string* err) {
   const size_t n = (size_t)BIG_SLOTS * BIG_TABLE_CAP;
   int rc;
+  const void* before = E->big_prev.p;
   if ((rc = ensure(E->big_key, n * 4, err))) return rc;
   if ((rc = ensure(E->big_lab, n * 8, err))) return rc;
   if ((rc = ensure(E->big_inq, n * 4, err))) return rc;
   if ((rc = ensure(E->big_fr, n * 8, err))) return rc;
+  if ((rc = ensure(E->big_ins, (size_t)BIG_SLOTS * SEARCH_LIMIT * 4, err))) return rc;
+  if ((rc = ensure(E->big_prev, (size_t)BIG_SLOTS * 4, err))) return rc;
+  if (E->big_prev.p != before) {
+    // fresh tables start clean (each search then clears only what the last
+    // one inserted: kernels.hip ta_search)
+    HIPCHK(hipMemsetAsync(E->big_key.p, 0xFF, n * 4, E->stream));
+    HIPCHK(hipMemsetAsync(E->big_lab.p, 0xFF, n * 8, E->stream));
+    HIPCHK(hipMemsetAsync(E->big_inq.p, 0, n * 4, E->stream));
+    HIPCHK(hipMemsetAsync(E->big_prev.p, 0, (size_t)BIG_SLOTS * 4, E->stream));
+  }
   return OTM_OK;
 }
 
@@ -675,6 +686,8 @@ static int engine_match_once(otm_engine* E, const DevBatch& b, hipStream_t s, st
   w.big_lab = P<unsigned long long>(E->big_lab);
   w.big_inq = P<uint32_t>(E->big_inq);
   w.big_fr = P<uint32_t>(E->big_fr);
+  w.big_ins = P<uint32_t>(E->big_ins);
+  w.big_prev = P<int32_t>(E->big_prev);
   launch_transitions(E->g, b, dp, w, s, mk, E->trans_lanes);
   // spill snapshot B: columns per transition tier (Viterbi does not touch
   // the counters; they start over for the route tiers)

@@ -66,7 +66,7 @@ struct otm_engine {
   Buf pt_trace, is_col, prevc, nextc, gc, ncand, cand_eo, cand_em, cand_xeo, cand_xem, probe, col_prev, kq_prev, trans_off, trans, bp, state, chosen,
       chain_start, route_dist, ipos, path_off, path_len, path_pool, trace_err, overflow_list0, overflow_list2,
       counters_i32, scan_tmp, snap;
-  Buf big_key, big_lab, big_inq, big_fr;
+  Buf big_key, big_lab, big_inq, big_fr, big_ins, big_prev;
   Buf ord_tile, ord_cnt, ord_cursor, ord_grp, ord_item;  // spatial work order
   Buf abort_flag;                                       // capacity overflow of the batch in flight
   Buf rs_blob;                                          // otm_report_segments_device in/out

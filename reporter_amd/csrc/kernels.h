@@ -31,7 +31,10 @@ constexpr int LDS_TABLE_CAP = 256;   // K4/K6 LDS tier: table slots
 constexpr int LDS_TABLE_LIMIT = 192; // ... labels before spilling to the global tier
 constexpr int BIG_TABLE_LOG2 = 17;
 constexpr int BIG_TABLE_CAP = 1 << BIG_TABLE_LOG2;  // global tier table slots (> SEARCH_LIMIT / 0.75)
-constexpr int BIG_SLOTS = 128;       // concurrent global-tier searches
+#ifndef OTM_BIG_SLOTS
+#define OTM_BIG_SLOTS 512
+#endif
+constexpr int BIG_SLOTS = OTM_BIG_SLOTS;  // concurrent global-tier searches
 
 struct DevGraph {
   const float *node_lat, *node_lon;
@@ -193,6 +196,8 @@ struct DevWork {
   unsigned long long* big_lab;
   uint32_t* big_inq;
   uint32_t* big_fr;
+  uint32_t* big_ins;       // [BIG_SLOTS * SEARCH_LIMIT] slots each table's last search inserted
+  int32_t* big_prev;       // [BIG_SLOTS] their count (-1: clear the whole table)
   DevCounters* ctr;        // nullptr when counting is off
 };
 

@@ -1015,6 +1015,11 @@ struct Table {
   uint32_t* fr1;            // frontier B
   int cap_log2;
   int limit;                // max labels before overflow
+  // global tier only: the slots the last search inserted (its first `limit`)
+  // and how many (*prev, -1: unknown), so the next search clears those instead
+  // of the whole 128K-slot table (the tables start clean: engine.cpp ensure_big)
+  uint32_t* ins = nullptr;
+  int32_t* prev = nullptr;
 };
 
 template <bool BIG>
@@ -1070,7 +1075,9 @@ __device__ __forceinline__ void ta_relax(const Table& T, SearchShared& S, uint32
   for (int i = 0; i <= (int)mask; ++i) {
     const uint32_t old = atomicCAS(&T.key[slot], EMPTY, key);
     if (old == EMPTY) {
-      if (atomicAdd(&S.count, 1) >= T.limit) S.over = 1;
+      const int c = atomicAdd(&S.count, 1);
+      if (c >= T.limit) S.over = 1;
+      else if (BIG) Mem<true>::st(&T.ins[c], slot);
       found = (int)slot;
       break;
     }
@@ -1099,10 +1106,22 @@ template <bool BIG>
 __device__ int ta_search(const DevGraph& g, const uint32_t* TU, const Table& T, SearchShared& S, int32_t u,
                          uint32_t hin, uint32_t cmax, int lane) {
   const int cap = 1 << T.cap_log2;
-  for (int i = lane; i < cap; i += TB) {
-    Mem<BIG>::st(&T.key[i], EMPTY);
-    Mem<BIG>::st(&T.lab[i], LAB_NONE);
-    Mem<BIG>::st(&T.inq[i], 0u);
+  // a clean table: the LDS tier's whole, the global tier's the slots its last
+  // search inserted (all of them after an overflow)
+  const int pc = BIG ? Mem<true>::ld(T.prev) : -1;
+  if (pc < 0) {
+    for (int i = lane; i < cap; i += TB) {
+      Mem<BIG>::st(&T.key[i], EMPTY);
+      Mem<BIG>::st(&T.lab[i], LAB_NONE);
+      Mem<BIG>::st(&T.inq[i], 0u);
+    }
+  } else {
+    for (int i = lane; i < pc; i += TB) {
+      const uint32_t sl = Mem<true>::ld(&T.ins[i]);
+      Mem<BIG>::st(&T.key[sl], EMPTY);
+      Mem<BIG>::st(&T.lab[sl], LAB_NONE);
+      Mem<BIG>::st(&T.inq[sl], 0u);
+    }
   }
   if (lane == 0) {
     S.nfr = 0;
@@ -1152,6 +1171,7 @@ __device__ int ta_search(const DevGraph& g, const uint32_t* TU, const Table& T, 
   }
   const bool over = S.over != 0;
   const int count = S.count;
+  if (BIG && lane == 0) Mem<true>::st(T.prev, over || count > T.limit ? -1 : count);
   __syncthreads();
   return over ? -1 : count;
 }
@@ -1700,7 +1720,8 @@ __global__ __launch_bounds__(TB) void k_transitions(DevGraph g, DevBatch b, DevP
   if (BIG) {
     const size_t base = (size_t)blockIdx.x * BIG_TABLE_CAP;
     T = Table{w.big_key + base, w.big_lab + base, w.big_inq + base, w.big_fr + 2 * base,
-              w.big_fr + 2 * base + BIG_TABLE_CAP, BIG_TABLE_LOG2, SEARCH_LIMIT};
+              w.big_fr + 2 * base + BIG_TABLE_CAP, BIG_TABLE_LOG2, SEARCH_LIMIT,
+              w.big_ins + (size_t)blockIdx.x * SEARCH_LIMIT, w.big_prev + blockIdx.x};
   } else {
     T = Table{lkey, llab, linq, lfr0, lfr1, 8, LDS_TABLE_LIMIT};
   }
@@ -2222,7 +2243,8 @@ __global__ __launch_bounds__(TB) void k_route(DevGraph g, DevBatch b, DevParams 
   if (BIG) {
     const size_t base = (size_t)blockIdx.x * BIG_TABLE_CAP;
     T = Table{w.big_key + base, w.big_lab + base, w.big_inq + base, w.big_fr + 2 * base,
-              w.big_fr + 2 * base + BIG_TABLE_CAP, BIG_TABLE_LOG2, SEARCH_LIMIT};
+              w.big_fr + 2 * base + BIG_TABLE_CAP, BIG_TABLE_LOG2, SEARCH_LIMIT,
+              w.big_ins + (size_t)blockIdx.x * SEARCH_LIMIT, w.big_prev + blockIdx.x};
   } else {
     T = Table{lkey, llab, linq, lfr0, lfr1, 8, LDS_TABLE_LIMIT};
   }

@@ -727,7 +727,6 @@ void report_many_device(otm_engine* E, int n, const char* const* reqs, const siz
           resps[which[m]] = wr[m];
           resp_lens[which[m]] = wl[m];
         }
-        (void)typed;
         t3 = now_ms();
       }
     }

@@ -1040,8 +1040,8 @@ int engine_fetch(otm_engine* E, otm_results* out, std::string* err) {
   return OTM_OK;
 }
 
-int engine_write_responses(otm_engine* E, const char** blob, const int64_t** off, const uint8_t** host,
-                           const otm_trace_result** traces, std::string* err) {
+int engine_write_responses(otm_engine* E, const int64_t** off, const uint8_t** host,
+                           const otm_trace_result** traces, int64_t* total, std::string* err) {
   hipStream_t s = E->stream;
   const int32_t NT = E->last_T;
   int32_t NS, NW, NR;
@@ -1058,7 +1058,7 @@ int engine_write_responses(otm_engine* E, const char** blob, const int64_t** off
   ENS_F(resp_blen, ((size_t)NT + 1) * 8);
   ENS_F(resp_host, (size_t)NT + 1);
   // a body is at most its pieces plus the joins (commas, the fixed middle and end)
-  const size_t blob_b = hdr_b + seg_b + rep_b + (size_t)NT * 96 + (size_t)NS + (size_t)NR;
+  const size_t blob_b = hdr_b + seg_b + rep_b + (size_t)NT * 97 + (size_t)NS + (size_t)NR;  // (+ the NULs)
   ENS_F(resp_blob, blob_b);
   if ((rc = ensure(E->scan_tmp, scan_tmp_bytes(NT) + 256, err))) return rc;
   RespIn in{NT, NS, NR, (const otm_trace_result*)E->f_traces.p, (const otm_segment*)E->f_segs.p,
@@ -1084,16 +1084,27 @@ int engine_write_responses(otm_engine* E, const char** blob, const int64_t** off
   }
   HIPCHK(hipGetLastError());
   HIPCHK(wait_batch(E, s, E->last_P));
-  const int64_t total = ((const int64_t*)meta)[NT];
-  if ((rc = ensure_pinned(E->h_resp, (size_t)total + 16, err))) return rc;
-  if (total) {
-    HIPCHK(big_copy(E->h_resp.p, E->resp_blob.p, (size_t)total, hipMemcpyDeviceToHost, s));
-    HIPCHK(wait_batch(E, s, E->last_P));
-  }
-  *blob = (const char*)E->h_resp.p;
+  *total = ((const int64_t*)meta)[NT];
   *off = (const int64_t*)meta;
   *host = (const uint8_t*)(meta + off_b);
   *traces = (const otm_trace_result*)E->h_traces.p;
+  return OTM_OK;
+}
+
+// the body blob of the last engine_write_responses (total bytes) into dst --
+// page-locked host memory (the caller's response arena) -- or, with dst null,
+// into the engine's own pinned buffer; *blob: where it landed
+int engine_copy_responses(otm_engine* E, char* dst, int64_t total, const char** blob, std::string* err) {
+  int rc;
+  if (!dst) {
+    if ((rc = ensure_pinned(E->h_resp, (size_t)total + 16, err))) return rc;
+    dst = (char*)E->h_resp.p;
+  }
+  if (total) {
+    HIPCHK(big_copy(dst, E->resp_blob.p, (size_t)total, hipMemcpyDeviceToHost, E->stream));
+    HIPCHK(wait_batch(E, E->stream, E->last_P));
+  }
+  *blob = dst;
   return OTM_OK;
 }
 

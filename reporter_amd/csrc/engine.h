@@ -154,12 +154,16 @@ int engine_push_requests(otm_engine* E, int32_t n, size_t bytes, size_t from, si
 int engine_match_requests(otm_engine* E, int32_t n, size_t bytes, bool pushed, const uint8_t** ok,
                           int32_t* n_traces, std::string* err);
 // The last batch's /report response bodies written on the GPU
-// (responses.hip): trace t's body is blob[off[t], off[t + 1]) unless host[t]
-// (a 500, or a float the GPU does not format: the host writes those from
-// engine_fetch's records); traces[t] its result record.  The pointers stay
-// valid until the next batch.
-int engine_write_responses(otm_engine* E, const char** blob, const int64_t** off, const uint8_t** host,
-                           const otm_trace_result** traces, std::string* err);
+// (responses.hip) into a device blob of *total bytes: trace t's body is
+// blob[off[t], off[t + 1] - 1), NUL-terminated, unless host[t] (a 500, or a
+// float the GPU does not format: the host writes those from engine_fetch's
+// records; no bytes in the blob); traces[t] its result record.  The pointers
+// stay valid until the next batch.  engine_copy_responses brings the blob to
+// dst (page-locked, e.g. the caller's response arena) or, with dst null, to
+// the engine's own pinned buffer.
+int engine_write_responses(otm_engine* E, const int64_t** off, const uint8_t** host,
+                           const otm_trace_result** traces, int64_t* total, std::string* err);
+int engine_copy_responses(otm_engine* E, char* dst, int64_t total, const char** blob, std::string* err);
 // copy results of the last batch to host vectors and describe them
 int engine_fetch(otm_engine* E, otm_results* out, std::string* err);
 int engine_debug_fetch(otm_engine* E, int what, void* dst, size_t bytes, size_t* needed, std::string* err);

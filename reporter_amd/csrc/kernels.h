@@ -315,7 +315,7 @@ void launch_req_fill(const unsigned char* blob, const int64_t* off, int32_t n, c
 // the /report response bodies written on the GPU (responses.hip) from a
 // batch's dense results (engine_fetch's compaction, device side)
 constexpr int RESP_HDR_SLOT = 512;  // bytes of a trace's header piece
-constexpr int RESP_SEG_SLOT = 320;  // ... of a segment object, + 21 per way id
+constexpr int RESP_SEG_SLOT = 320;  // ... of a segment object, + 24 per way id (8-byte aligned)
 constexpr int RESP_REP_SLOT = 192;  // ... of a datastore report object
 struct RespIn {
   int32_t nt, ns, nr;

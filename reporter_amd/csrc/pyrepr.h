@@ -33,23 +33,54 @@ OTM_HD uint64_t dbits(double d) {
   return x.u;
 }
 
-OTM_HD int put_u64(uint64_t v, char* o) {
-  char t[20];
+// A byte sink is any type with put(char).  CharSink: a plain buffer.
+struct CharSink {
+  char* p;
+  int n;
+  OTM_HD void put(char c) { p[n++] = c; }
+};
+
+// up to 16 decimal digits of v (at least minw, zero-padded), most significant
+// first: built in a 128-bit string register (each new, less significant...
+// digit shifted in below: byte 0 ends up the first character), so no
+// digit array is indexed at run time
+template <class S>
+OTM_HD void put_digits16(uint64_t v, int minw, S& o) {
+  u128 str = 0;
   int n = 0;
   do {
-    t[n++] = (char)('0' + v % 10u);
+    str = (str << 8) | (u128)('0' + (unsigned)(v % 10u));
     v /= 10u;
-  } while (v);
-  for (int k = 0; k < n; ++k) o[k] = t[n - 1 - k];
-  return n;
+    ++n;
+  } while (v || n < minw);
+  for (int i = 0; i < n; ++i) o.put((char)(uint8_t)(str >> (8 * i)));
+}
+
+template <class S>
+OTM_HD void put_u64(uint64_t v, S& o) {
+  constexpr uint64_t P16 = 10000000000000000ull;
+  if (v >= P16) {
+    put_digits16(v / P16, 0, o);
+    put_digits16(v % P16, 16, o);
+  } else {
+    put_digits16(v, 0, o);
+  }
+}
+
+template <class S>
+OTM_HD void put_i64(int64_t v, S& o) {
+  if (v < 0) {
+    o.put('-');
+    put_u64((uint64_t)0 - (uint64_t)v, o);
+  } else {
+    put_u64((uint64_t)v, o);
+  }
 }
 
 OTM_HD int put_i64(int64_t v, char* o) {
-  if (v < 0) {
-    o[0] = '-';
-    return 1 + put_u64((uint64_t)0 - (uint64_t)v, o + 1);
-  }
-  return put_u64((uint64_t)v, o);
+  CharSink s{o, 0};
+  put_i64(v, s);
+  return s.n;
 }
 
 OTM_HD u128 pow10u(int k) {
@@ -58,23 +89,25 @@ OTM_HD u128 pow10u(int k) {
   return p;
 }
 
-// repr(d) into o (at most 24 bytes); returns the length, or -1 (the host's)
-OTM_HD int py_repr(double d, char* o) {
+// repr(d) into the sink (at most 24 bytes); false: d is outside the range
+// (the sink may hold part of it; the host writes that body)
+template <class S>
+OTM_HD bool py_repr(double d, S& o) {
   const uint64_t b = dbits(d);
   const bool neg = (b >> 63) != 0;
   const int ef = (int)((b >> 52) & 0x7FF);
   const uint64_t fr = b & ((1ull << 52) - 1);
-  int n = 0;
-  if (neg) o[n++] = '-';
   if (ef == 0 && fr == 0) {
-    o[n++] = '0';
-    o[n++] = '.';
-    o[n++] = '0';
-    return n;
+    if (neg) o.put('-');
+    o.put('0');
+    o.put('.');
+    o.put('0');
+    return true;
   }
   // d = M x 2^e2; supported: 2^-10 <= |d| < 2^52
   const int e2 = ef - 1075;
-  if (ef == 0 || e2 >= 0 || e2 < -62) return -1;
+  if (ef == 0 || e2 >= 0 || e2 < -62) return false;
+  if (neg) o.put('-');
   const uint64_t M = fr | (1ull << 52);
   // Burger & Dybvig: value r/s, neighbours' half-gaps mm/mp (all scaled)
   u128 r, s, mp, mm;
@@ -122,8 +155,14 @@ OTM_HD int py_repr(double d, char* o) {
       }
     }
   }
-  // digits: 0.D1 D2 ... x 10^k
-  char dg[20];
+  // digits: 0.D1 D2 ... x 10^k, each written as it is fixed, in Python's
+  // repr layout (fixed notation for -4 < k <= 16: always, in this range)
+  const int decpt = k;
+  if (decpt <= 0) {
+    o.put('0');
+    o.put('.');
+    for (int i = 0; i < -decpt; ++i) o.put('0');
+  }
   int nd = 0;
   while (true) {
     r *= 10u;
@@ -136,11 +175,7 @@ OTM_HD int py_repr(double d, char* o) {
     }
     const bool lo = incl ? (r <= mm) : (r < mm);
     const bool hi = incl ? (r + mp >= s) : (r + mp > s);
-    if (!lo && !hi) {
-      dg[nd++] = (char)('0' + dig);
-      if (nd > 17) return -1;
-      continue;
-    }
+    const bool last = lo || hi;
     if (lo && hi) {
       const u128 r2 = r << 1;
       // closer of the two; exactly half-way: the even digit (dtoa's
@@ -150,28 +185,23 @@ OTM_HD int py_repr(double d, char* o) {
       ++dig;
     }
     // (dig == 10 cannot happen: the high test stops a digit earlier)
-    dg[nd++] = (char)('0' + dig);
-    break;
+    if (nd == 17) return false;
+    if (decpt > 0 && nd == decpt) o.put('.');
+    o.put((char)('0' + dig));
+    ++nd;
+    if (last) break;
   }
-  if (nd > 17) return -1;
-  // Python repr layout (fixed for -4 < k <= 16: always, in this range)
-  const int decpt = k;
-  if (decpt <= 0) {
-    o[n++] = '0';
-    o[n++] = '.';
-    for (int i = 0; i < -decpt; ++i) o[n++] = '0';
-    for (int i = 0; i < nd; ++i) o[n++] = dg[i];
-  } else if (decpt >= nd) {
-    for (int i = 0; i < nd; ++i) o[n++] = dg[i];
-    for (int i = nd; i < decpt; ++i) o[n++] = '0';
-    o[n++] = '.';
-    o[n++] = '0';
-  } else {
-    for (int i = 0; i < decpt; ++i) o[n++] = dg[i];
-    o[n++] = '.';
-    for (int i = decpt; i < nd; ++i) o[n++] = dg[i];
+  if (decpt > 0 && nd <= decpt) {
+    for (int i = nd; i < decpt; ++i) o.put('0');
+    o.put('.');
+    o.put('0');
   }
-  return n;
+  return true;
+}
+
+OTM_HD int py_repr(double d, char* o) {
+  CharSink s{o, 0};
+  return py_repr(d, s) ? s.n : -1;
 }
 
 // py_round3 (report.cpp / json.cpp): x rounded half-even to 3 decimals on its

@@ -11,7 +11,8 @@
 //                 -1 (a 500 body or an unformattable float: the host writes it);
 //   k_resp_copy   a wave per trace: the pieces and the fixed joins into the
 //                 trace's place in one dense blob (offsets: a scan of the
-//                 lengths), which one copy brings to the host.
+//                 lengths), each body NUL-terminated, so that one copy into
+//                 the caller's response arena leaves every body in place.
 #include "kernels.h"
 #include "otmatch.h"
 #include "pyrepr.h"
@@ -21,18 +22,30 @@ namespace {
 
 constexpr int RESP_TB = 256;
 
+// a piece's bytes, gathered 8 at a time and stored as whole 8-byte words
+// (slots are 8-byte aligned; the last word may run past the piece into its
+// slot's slack): a byte store per character cost a 64-line store instruction
 struct Out {
   char* p;
   int n;
-  __device__ void lit(const char* s) {
-    for (int k = 0; s[k]; ++k) p[n++] = s[k];
+  uint64_t acc;
+  __device__ __forceinline__ void put(char c) {
+    acc |= (uint64_t)(uint8_t)c << (8 * (n & 7));
+    if ((++n & 7) == 0) {
+      *(uint64_t*)(p + n - 8) = acc;
+      acc = 0;
+    }
   }
-  __device__ void i64(int64_t v) { n += pyrepr::put_i64(v, p + n); }
-  __device__ bool f64(double d) {
-    const int m = pyrepr::py_repr(d, p + n);
-    if (m < 0) return false;
-    n += m;
-    return true;
+  template <int N>
+  __device__ __forceinline__ void lit(const char (&s)[N]) {
+#pragma unroll 1
+    for (int k = 0; k < N - 1; ++k) put(s[k]);
+  }
+  __device__ __forceinline__ void i64(int64_t v) { pyrepr::put_i64(v, *this); }
+  __device__ __forceinline__ bool f64(double d) { return pyrepr::py_repr(d, *this); }
+  __device__ __forceinline__ int done() {
+    if (n & 7) *(uint64_t*)(p + (n & ~7)) = acc;
+    return n;
   }
 };
 
@@ -41,7 +54,7 @@ __device__ const char kReps[] = ",\"reports\":[";
 constexpr int MID_LEN = sizeof(kMid) - 1;
 constexpr int REPS_LEN = sizeof(kReps) - 1;
 
-__device__ int64_t seg_slot(int32_t s, int32_t way_off) { return (int64_t)s * RESP_SEG_SLOT + 21ll * way_off; }
+__device__ int64_t seg_slot(int32_t s, int32_t way_off) { return (int64_t)s * RESP_SEG_SLOT + 24ll * way_off; }
 
 __global__ __launch_bounds__(RESP_TB) void k_resp_items(RespIn in, RespWork w) {
   const int64_t nitems = (int64_t)in.nt + in.ns + in.nr;
@@ -49,7 +62,7 @@ __global__ __launch_bounds__(RESP_TB) void k_resp_items(RespIn in, RespWork w) {
     if (it < in.nt) {
       const int32_t t = (int32_t)it;
       const otm_trace_result tr = in.traces[t];
-      Out o{w.hdr + (int64_t)t * RESP_HDR_SLOT, 0};
+      Out o{w.hdr + (int64_t)t * RESP_HDR_SLOT, 0, 0};
       bool ok = tr.code == 200;
       if (ok) {
         // write_report_response: the stats block, shape_used, up to the segments
@@ -77,11 +90,11 @@ __global__ __launch_bounds__(RESP_TB) void k_resp_items(RespIn in, RespWork w) {
         }
         o.lit(",\"segment_matcher\":{\"segments\":[");
       }
-      w.hlen[t] = ok ? o.n : -1;
+      w.hlen[t] = o.done() >= 0 && ok ? o.n : -1;
     } else if (it < (int64_t)in.nt + in.ns) {
       const int32_t s = (int32_t)(it - in.nt);
       const otm_segment g = in.segs[s];
-      Out o{w.seg + seg_slot(s, g.way_off), 0};
+      Out o{w.seg + seg_slot(s, g.way_off), 0, 0};
       bool ok = true;
       o.lit("{");
       if (g.segment_id >= 0) {
@@ -104,17 +117,18 @@ __global__ __launch_bounds__(RESP_TB) void k_resp_items(RespIn in, RespWork w) {
       o.i64(g.queue_length);
       o.lit(",\"length\":");
       o.i64(g.length);
-      o.lit((g.flags & OTM_SEG_INTERNAL) ? ",\"internal\":true" : ",\"internal\":false");
+      if (g.flags & OTM_SEG_INTERNAL) o.lit(",\"internal\":true");
+      else o.lit(",\"internal\":false");
       o.lit(",\"begin_shape_index\":");
       o.i64(g.begin_shape_index);
       o.lit(",\"end_shape_index\":");
       o.i64(g.end_shape_index);
       o.lit("}");
-      w.slen[s] = ok ? o.n : -1;
+      w.slen[s] = o.done() >= 0 && ok ? o.n : -1;
     } else {
       const int32_t r = (int32_t)(it - in.nt - in.ns);
       const otm_report_rec p = in.reps[r];
-      Out o{w.rep + (int64_t)r * RESP_REP_SLOT, 0};
+      Out o{w.rep + (int64_t)r * RESP_REP_SLOT, 0, 0};
       bool ok = true;
       o.lit("{\"id\":");
       o.i64(p.id);
@@ -133,7 +147,7 @@ __global__ __launch_bounds__(RESP_TB) void k_resp_items(RespIn in, RespWork w) {
         o.i64(p.next_id);
       }
       o.lit("}");
-      w.rlen[r] = ok ? o.n : -1;
+      w.rlen[r] = o.done() >= 0 && ok ? o.n : -1;
     }
   }
 }
@@ -161,7 +175,7 @@ __global__ __launch_bounds__(RESP_TB) void k_resp_len(RespIn in, RespWork w) {
     }
   }
   n += 2;
-  w.blen[t] = ok ? n : 0;
+  w.blen[t] = ok ? n + 1 : 0;  // + the NUL the caller's string needs
   w.host[t] = ok ? 0 : 1;
 }
 
@@ -210,13 +224,14 @@ __global__ __launch_bounds__(64) void k_resp_copy(RespIn in, RespWork w, const i
     if (lane == 0) {
       d[n] = '}';
       d[n + 1] = '}';
+      d[n + 2] = '\0';
     }
   }
 }
 
 }  // namespace
 
-size_t resp_seg_scratch(int32_t ns, int32_t nw) { return (size_t)ns * RESP_SEG_SLOT + 21ull * (size_t)nw + 64; }
+size_t resp_seg_scratch(int32_t ns, int32_t nw) { return (size_t)ns * RESP_SEG_SLOT + 24ull * (size_t)nw + 64; }
 
 void launch_resp_items(const RespIn& in, const RespWork& w, hipStream_t s) {
   const int64_t n = (int64_t)in.nt + in.ns + in.nr;

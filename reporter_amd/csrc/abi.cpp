@@ -539,6 +539,68 @@ void free_body(void* p) {
 }
 }  // namespace arena
 
+// Submission slabs: otm_submit_batch copies its bodies into one allocation,
+// page-locked from SLAB_PINNED_MIN bytes up, so the worker's batch goes to HBM
+// straight from it (report_many_device's direct pieces): one host copy per
+// body instead of two (the submit copy and the staging copy), and no malloc
+// per request.  Released page-locked slabs are kept (up to SLAB_CACHE bytes)
+// for later submissions; the small ones are plain mallocs.
+namespace slabs {
+constexpr size_t SLAB_PINNED_MIN = (size_t)1 << 20;
+size_t pinned_min() {  // OTM_SLAB_PINNED_MIN overrides (tests: every slab page-locked)
+  const char* e = std::getenv("OTM_SLAB_PINNED_MIN");
+  return e ? (size_t)std::strtoull(e, nullptr, 10) : SLAB_PINNED_MIN;
+}
+constexpr size_t SLAB_CACHE = (size_t)512 << 20;
+std::mutex g_mu;
+std::vector<ReqSlab*> g_cache;  // under g_mu
+size_t g_cached = 0;
+
+void release(ReqSlab* s) {
+  if (s->pinned) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (g_cached + s->cap <= SLAB_CACHE) {
+      g_cache.push_back(s);
+      g_cached += s->cap;
+      return;
+    }
+  }
+  if (s->pinned) (void)hipHostFree(s->base);
+  else std::free(s->base);
+  delete s;
+}
+
+// a slab of >= bytes (throws std::bad_alloc when there is no memory at all)
+std::shared_ptr<ReqSlab> acquire(size_t bytes) {
+  ReqSlab* s = nullptr;
+  if (bytes >= pinned_min()) {
+    {
+      std::lock_guard<std::mutex> lk(g_mu);
+      size_t best = g_cache.size();
+      for (size_t i = 0; i < g_cache.size(); ++i)
+        if (g_cache[i]->cap >= bytes && (best == g_cache.size() || g_cache[i]->cap < g_cache[best]->cap)) best = i;
+      if (best < g_cache.size()) {
+        s = g_cache[best];
+        g_cache[best] = g_cache.back();
+        g_cache.pop_back();
+        g_cached -= s->cap;
+      }
+    }
+    if (!s) {
+      const size_t cap = (bytes + SLAB_PINNED_MIN - 1) & ~(SLAB_PINNED_MIN - 1);
+      void* p = nullptr;
+      if (hipHostMalloc(&p, cap, hipHostMallocDefault) == hipSuccess && p) s = new ReqSlab{(char*)p, cap, true};
+    }
+  }
+  if (!s) {
+    char* p = (char*)std::malloc(bytes ? bytes : 1);
+    if (!p) throw std::bad_alloc();
+    s = new ReqSlab{p, bytes, false};
+  }
+  return std::shared_ptr<ReqSlab>(s, release);
+}
+}  // namespace slabs
+
 // each response of a batch into its place in one arena (or its own malloc'd
 // buffer when no arena is to be had): src(k) -> (pointer, length); returns
 // false when out of host memory (nothing left allocated)
@@ -656,7 +718,7 @@ bool gpu_writer() {
 // writer leaves (a 500, a float outside its range) is written on the host
 // from the batch's typed records.
 void report_many_device(otm_engine* E, int n, const char* const* reqs, const size_t* lens, int* codes,
-                        char** resps, size_t* resp_lens) {
+                        char** resps, size_t* resp_lens, const uint8_t* pinned) {
   const double t0 = now_ms();
   std::vector<int> rest;  // left to the host readers
   std::vector<int> inv;   // invalid speeds per GPU-read request (stderr lines)
@@ -672,7 +734,9 @@ void report_many_device(otm_engine* E, int n, const char* const* reqs, const siz
     for (int k = 0; k < n; ++k) bytes += lens[k];
     int64_t* off = nullptr;
     char* dst = nullptr;
-    rc = otm::engine_stage_requests(E, n, bytes, &off, &dst, &err);
+    bool all_pinned = pinned != nullptr;
+    for (int k = 0; all_pinned && k < n; ++k) all_pinned = pinned[k] != 0;
+    rc = otm::engine_stage_requests(E, n, bytes, !all_pinned, &off, &dst, &err);
     if (!rc) {
       off[0] = 0;
       for (int k = 0; k < n; ++k) off[k + 1] = off[k] + (int64_t)lens[k];
@@ -685,18 +749,27 @@ void report_many_device(otm_engine* E, int n, const char* const* reqs, const siz
         int k1 = k0;
         while (k1 < n && (size_t)off[k1 + 1] - from <= PIECE) ++k1;
         if (k1 == k0) ++k1;  // one body larger than a piece
-        par_for((size_t)(k1 - k0), [&](size_t a, size_t e) {
-          for (size_t m = a; m < e; ++m) {
-            const size_t k = (size_t)k0 + m;
-            if (lens[k]) std::memcpy(dst + off[k], reqs[k], lens[k]);
-          }
-        });
+        const bool direct = pinned && pinned[k0];
+        if (direct) {
+          // a run of bodies adjacent in one page-locked submission slab:
+          // copied to HBM from there, not staged
+          k1 = k0 + 1;
+          while (k1 < n && pinned[k1] && reqs[k1] == reqs[k1 - 1] + lens[k1 - 1]) ++k1;
+        } else {
+          while (k1 > k0 + 1 && pinned && pinned[k1 - 1]) --k1;  // (the staged piece stops at a slab run)
+          par_for((size_t)(k1 - k0), [&](size_t a, size_t e) {
+            for (size_t m = a; m < e; ++m) {
+              const size_t k = (size_t)k0 + m;
+              if (lens[k]) std::memcpy(dst + off[k], reqs[k], lens[k]);
+            }
+          });
+        }
         const size_t to = (size_t)off[k1];
-        rc = otm::engine_push_requests(E, n, bytes, from, to, &err);
+        rc = otm::engine_push_requests(E, n, bytes, from, to, direct ? reqs[k0] : nullptr, &err);
         from = to;
         k0 = k1;
       }
-      if (!rc && n == 0) rc = otm::engine_push_requests(E, n, bytes, 0, 0, &err);
+      if (!rc && n == 0) rc = otm::engine_push_requests(E, n, bytes, 0, 0, nullptr, &err);
     }
     if (!rc) {
       t1 = now_ms();
@@ -838,9 +911,10 @@ void report_many_device(otm_engine* E, int n, const char* const* reqs, const siz
                  n, rest.size(), t1 - t0, t2 - t1, t3 - t2, now_ms() - t3);
 }
 
+// (pinned[k]: body k lies in page-locked memory, e.g. a submission slab)
 void report_many(otm_engine* E, int n, const char* const* reqs, const size_t* lens, int* codes, char** resps,
-                 size_t* resp_lens) {
-  if (gpu_reader(E, n)) report_many_device(E, n, reqs, lens, codes, resps, resp_lens);
+                 size_t* resp_lens, const uint8_t* pinned = nullptr) {
+  if (gpu_reader(E, n)) report_many_device(E, n, reqs, lens, codes, resps, resp_lens, pinned);
   else report_many_host(E, n, reqs, lens, codes, resps, resp_lens);
 }
 
@@ -874,8 +948,13 @@ void worker_loop(otm_engine* E, int wi) {
       std::unique_lock<std::mutex> lk(E->qmu);
       E->qcv.wait(lk, [&] { return E->stop || !E->queue.empty(); });
       if (E->queue.empty()) return;  // stopping, nothing left
+      // up to cap requests; a submission that does not fit whole waits for
+      // the next batch (unless it alone exceeds cap), so batches keep the
+      // submissions' sizes and each is one run of one slab
       const size_t cap = async_batch();
       while (!E->queue.empty() && batch.size() < cap) {
+        const otm_engine::Pending& f = E->queue.front();
+        if (!batch.empty() && f.slab != batch.back().slab && batch.size() + f.run_left > cap) break;
         batch.push_back(std::move(E->queue.front()));
         E->queue.pop_front();
       }
@@ -886,13 +965,15 @@ void worker_loop(otm_engine* E, int wi) {
     std::vector<size_t> lens((size_t)n), rl((size_t)n, 0);
     std::vector<int> codes((size_t)n, 500);
     std::vector<char*> resps((size_t)n, nullptr);
+    std::vector<uint8_t> pin((size_t)n, 0);
     for (int k = 0; k < n; ++k) {
-      reqs[(size_t)k] = batch[(size_t)k].body.data();
-      lens[(size_t)k] = batch[(size_t)k].body.size();
+      reqs[(size_t)k] = batch[(size_t)k].p;
+      lens[(size_t)k] = batch[(size_t)k].len;
+      pin[(size_t)k] = batch[(size_t)k].slab->pinned ? 1 : 0;
     }
     const double tw0 = now_ms();
     try {
-      report_many(ctx, n, reqs.data(), lens.data(), codes.data(), resps.data(), rl.data());
+      report_many(ctx, n, reqs.data(), lens.data(), codes.data(), resps.data(), rl.data(), pin.data());
     } catch (...) {
       // out of host memory (report_many freed what it made): the batch's
       // requests complete with a null body and code 500
@@ -1340,7 +1421,9 @@ static int otm_submit_impl(otm_engine* E, const char* req, size_t len, uint64_t 
   std::lock_guard<std::mutex> lk(E->qmu);
   if (!E->worker_started) start_workers(E);
   if (E->queue.size() >= (1u << 22)) return fail(OTM_EAGAIN, "submit queue full");
-  E->queue.push_back(otm_engine::Pending{tag, std::string(req, len)});
+  std::shared_ptr<ReqSlab> slab = slabs::acquire(len);
+  if (len) std::memcpy(slab->base, req, len);
+  E->queue.push_back(otm_engine::Pending{tag, slab->base, len, std::move(slab), 1});
   E->qcv.notify_all();
   return OTM_OK;
 }
@@ -1348,10 +1431,17 @@ static int otm_submit_impl(otm_engine* E, const char* req, size_t len, uint64_t 
 static int otm_submit_batch_impl(otm_engine* E, int n, const char* const* reqs, const size_t* lens,
                                  const uint64_t* tags) {
   if (!E || n < 0 || (n && (!reqs || !lens || !tags))) return fail(OTM_EINVAL, "bad arguments");
-  // the copies outside the queue lock, over the host threads
+  // the bodies copied into one slab (page-locked when large), outside the
+  // queue lock, over the host threads
+  std::vector<size_t> off((size_t)n + 1, 0);
+  for (int k = 0; k < n; ++k) off[(size_t)k + 1] = off[(size_t)k] + lens[k];
+  std::shared_ptr<ReqSlab> slab = slabs::acquire(off[(size_t)n]);
   std::vector<otm_engine::Pending> items((size_t)n);
   par_for((size_t)n, [&](size_t a, size_t e) {
-    for (size_t k = a; k < e; ++k) items[k] = otm_engine::Pending{tags[k], std::string(reqs[k], lens[k])};
+    for (size_t k = a; k < e; ++k) {
+      if (lens[k]) std::memcpy(slab->base + off[k], reqs[k], lens[k]);
+      items[k] = otm_engine::Pending{tags[k], slab->base + off[k], lens[k], slab, (size_t)n - k};
+    }
   });
   {
     std::lock_guard<std::mutex> lk(E->qmu);

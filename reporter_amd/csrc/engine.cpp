@@ -873,11 +873,19 @@ static constexpr size_t REQ_PAD = 64;
 static size_t req_hdr_bytes(int32_t n) { return (((size_t)n + 1) * 8 + 15) & ~(size_t)15; }
 static size_t req_blob_bytes(int32_t n, size_t bytes) { return req_hdr_bytes(n) + bytes + REQ_PAD; }
 
-int engine_stage_requests(otm_engine* E, int32_t n, size_t bytes, int64_t** off, char** body, std::string* err) {
+int engine_stage_requests(otm_engine* E, int32_t n, size_t bytes, bool bodies, int64_t** off, char** body,
+                          std::string* err) {
   int rc;
   if (n < 0) {
     *err = "invalid request count";
     return OTM_EINVAL;
+  }
+  if (!bodies) {
+    // every body goes to HBM from the caller's page-locked memory: the header alone
+    if ((rc = ensure_pinned(E->h_req, req_hdr_bytes(n), err))) return rc;
+    *off = (int64_t*)E->h_req.p;
+    *body = nullptr;
+    return OTM_OK;
   }
   if ((rc = ensure_pinned(E->h_req, req_blob_bytes(n, bytes), err))) return rc;
   char* h = (char*)E->h_req.p;
@@ -889,13 +897,26 @@ int engine_stage_requests(otm_engine* E, int32_t n, size_t bytes, int64_t** off,
 
 // the device copy of the staging blob, and one piece of it on its way: body
 // bytes [from, to) (with the offsets header when from == 0, the padding when
-// to == bytes), so the host can stage the next piece while this one moves
-int engine_push_requests(otm_engine* E, int32_t n, size_t bytes, size_t from, size_t to, std::string* err) {
+// to == bytes), so the host can stage the next piece while this one moves.
+// With src (page-locked host memory holding body bytes [from, to)) the bodies
+// are copied from there instead of the staging buffer.
+int engine_push_requests(otm_engine* E, int32_t n, size_t bytes, size_t from, size_t to, const char* src,
+                         std::string* err) {
   int rc;
   if ((rc = ensure(E->d_req, req_blob_bytes(n, bytes), err))) return rc;
-  const size_t a = from ? req_hdr_bytes(n) + from : 0;
-  const size_t b = req_hdr_bytes(n) + (to >= bytes ? bytes + REQ_PAD : to);
-  if (b > a) HIPCHK(big_copy((char*)E->d_req.p + a, (const char*)E->h_req.p + a, b - a, hipMemcpyHostToDevice, E->stream));
+  char* d = (char*)E->d_req.p;
+  const char* h = (const char*)E->h_req.p;
+  const size_t hdr = req_hdr_bytes(n);
+  const hipMemcpyKind h2d = hipMemcpyHostToDevice;
+  if (!src) {
+    const size_t a = from ? hdr + from : 0;
+    const size_t b = hdr + (to >= bytes ? bytes + REQ_PAD : to);
+    if (b > a) HIPCHK(big_copy(d + a, h + a, b - a, h2d, E->stream));
+    return OTM_OK;
+  }
+  if (from == 0) HIPCHK(hipMemcpyAsync(d, h, hdr, h2d, E->stream));
+  if (to > from) HIPCHK(big_copy(d + hdr + from, src, to - from, h2d, E->stream));
+  if (to >= bytes) HIPCHK(hipMemsetAsync(d + hdr + bytes, 0, REQ_PAD, E->stream));
   return OTM_OK;
 }
 

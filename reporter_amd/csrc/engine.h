@@ -4,6 +4,7 @@
 
 #include <condition_variable>
 #include <deque>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -12,6 +13,14 @@
 #include "kernels.h"
 #include "otm_internal.h"
 #include "otmatch.h"
+
+// One submission's request bodies, copied into one allocation (abi.cpp
+// slabs::acquire; released to a cache when its last request is done)
+struct ReqSlab {
+  char* base = nullptr;
+  size_t cap = 0;
+  bool pinned = false;
+};
 
 struct otm_engine {
   const otm_engine* parent = nullptr;  // a clone shares its parent's graph and index (otm_engine_clone)
@@ -112,9 +121,15 @@ struct otm_engine {
   // clones it owns), so one batch's host parse / response writing overlaps
   // another's GPU work; batches are taken and their results published in
   // submit order (abi.cpp worker_loop)
+  // a submitted request: its body inside the slab its submission copied
+  // every body into (page-locked when large: the worker's batch copies it to
+  // HBM from there, with no staging copy)
   struct Pending {
     uint64_t tag;
-    std::string body;
+    const char* p;
+    size_t len;
+    std::shared_ptr<ReqSlab> slab;
+    size_t run_left;  // requests of its submission from this one on (itself included)
   };
   std::mutex qmu;
   std::condition_variable qcv;
@@ -147,10 +162,15 @@ int engine_match_host(otm_engine* E, const otm_batch* in, std::string* err);
 // bodies of the Java batcher's exact form (requests.hip) into a batch and
 // matches it.  *ok[r] (valid until the next call) says which requests the
 // batch holds, in request order; the others are the caller's to read.
-int engine_stage_requests(otm_engine* E, int32_t n, size_t bytes, int64_t** off, char** body, std::string* err);
+// (bodies false: the caller pushes every body from its own page-locked
+// memory; the staging buffer then holds the offsets alone, *body null)
+int engine_stage_requests(otm_engine* E, int32_t n, size_t bytes, bool bodies, int64_t** off, char** body,
+                          std::string* err);
 // (engine_push_requests: a piece of the staged blob on its way to HBM, so
 // staging and copying overlap; pushed = every piece went that way)
-int engine_push_requests(otm_engine* E, int32_t n, size_t bytes, size_t from, size_t to, std::string* err);
+// (src: those bytes from page-locked host memory instead of the staging buffer)
+int engine_push_requests(otm_engine* E, int32_t n, size_t bytes, size_t from, size_t to, const char* src,
+                         std::string* err);
 int engine_match_requests(otm_engine* E, int32_t n, size_t bytes, bool pushed, const uint8_t** ok,
                           int32_t* n_traces, std::string* err);
 // The last batch's /report response bodies written on the GPU

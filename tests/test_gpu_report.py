@@ -281,15 +281,24 @@ def test_one_engine_from_many_threads(small_graph):
         assert [pos[t] for t in tags] == sorted(pos[t] for t in tags), u
 
 
-@pytest.mark.parametrize("workers,batch", [("1", "8192"), ("2", "37"), ("3", "11")])
-def test_async_pipeline_order_and_bodies(small_graph, monkeypatch, workers, batch):
+@pytest.mark.parametrize("workers,batch,pinned_min,gpu_min", [
+    ("1", "8192", None, None), ("2", "37", None, None), ("3", "11", None, None),
+    # page-locked submission slabs (every submission; or the first only, by
+    # size), batches cut inside and across slabs, the GPU reader on them
+    ("1", "8192", "1", None), ("2", "37", "1", None), ("3", "50", "1", "1"), ("2", "200", "full", None)])
+def test_async_pipeline_order_and_bodies(small_graph, monkeypatch, workers, batch, pinned_min, gpu_min):
     """otm_submit_batch / otm_poll through the async pipeline (workers on
     their own batch contexts, OTM_ASYNC_WORKERS; small OTM_ASYNC_BATCH forces
     many batches in flight): every body byte-equal to the sequential answer,
-    each uuid's results in submit order, every tag once."""
+    each uuid's results in submit order, every tag once.  With
+    OTM_SLAB_PINNED_MIN the submissions' slabs are page-locked and the
+    worker's batches go to HBM straight from them (runs of adjacent bodies),
+    mixed with staged pieces where a batch spans a small slab."""
     from reporter_amd import encode_request
     monkeypatch.setenv("OTM_ASYNC_WORKERS", workers)
     monkeypatch.setenv("OTM_ASYNC_BATCH", batch)
+    if gpu_min is not None:
+        monkeypatch.setenv("OTM_GPU_JSON_MIN", gpu_min)
     b = synth.make_traces(small_graph, 120, 30, seed=93)
     bodies = []
     for t in range(120):
@@ -297,10 +306,20 @@ def test_async_pipeline_order_and_bodies(small_graph, monkeypatch, workers, batc
         bodies.append(encode_request("veh%d" % (t % 17), b["lat"][a:e], b["lon"][a:e],
                                      b["time"][a:e].astype(np.int64), b["accuracy"][a:e].astype(np.int32)))
     bodies += [b"", b'{"uuid":"x","trace":[]}']
+    if pinned_min == "full":  # a whole submission's slab page-locked, half of one not
+        pinned_min = str(sum(len(x) for x in bodies))
+    if pinned_min is not None:
+        monkeypatch.setenv("OTM_SLAB_PINNED_MIN", pinned_min)
     with Engine(graph_path=small_graph) as eng:
         want = eng.report_batch(bodies)
         tags = list(range(5000, 5000 + 3 * len(bodies)))
         for r in range(3):
+            if r == 1 and os.environ.get("OTM_SLAB_PINNED_MIN", "1") not in ("0", "1"):
+                # the middle submission split so its slabs fall below the bound
+                h = len(bodies) // 2
+                eng.submit_batch(bodies[:h], tags[r * len(bodies):r * len(bodies) + h])
+                eng.submit_batch(bodies[h:], tags[r * len(bodies) + h:(r + 1) * len(bodies)])
+                continue
             eng.submit_batch(bodies, tags[r * len(bodies):(r + 1) * len(bodies)])
         polled = []
         while len(polled) < len(tags):

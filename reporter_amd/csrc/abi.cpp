@@ -765,11 +765,11 @@ void report_many_device(otm_engine* E, int n, const char* const* reqs, const siz
           });
         }
         const size_t to = (size_t)off[k1];
-        rc = otm::engine_push_requests(E, n, bytes, from, to, direct ? reqs[k0] : nullptr, &err);
+        rc = otm::engine_push_requests(E, n, bytes, from, to, direct ? reqs[k0] : nullptr, k1, &err);
         from = to;
         k0 = k1;
       }
-      if (!rc && n == 0) rc = otm::engine_push_requests(E, n, bytes, 0, 0, nullptr, &err);
+      if (!rc && n == 0) rc = otm::engine_push_requests(E, n, bytes, 0, 0, nullptr, 0, &err);
     }
     if (!rc) {
       t1 = now_ms();

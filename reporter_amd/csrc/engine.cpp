@@ -499,7 +499,7 @@ void engine_free(otm_engine* E) {
       &E->f_seg_off,     &E->f_way_off,    &E->f_rep_off,      &E->f_segs,     &E->f_ways,     &E->f_reps,
       &E->f_traces,
       &E->abort_flag,    &E->rs_blob,      &E->ord_tile,      &E->ord_cnt,      &E->ord_cursor,     &E->ord_grp,    &E->ord_item,
-      &E->d_req,         &E->req_cnt,      &E->req_ok,
+      &E->d_req,         &E->req_cnt,      &E->req_ok,     &E->req_lat,    &E->req_lon,    &E->req_time,   &E->req_acc,
       &E->resp_hdr,      &E->resp_seg,     &E->resp_rep,       &E->resp_hlen,      &E->resp_slen,  &E->resp_rlen,
       &E->resp_blen,     &E->resp_host,    &E->resp_blob};
   for (auto* b : bufs) {
@@ -515,6 +515,10 @@ void engine_free(otm_engine* E) {
   }
   if (E->sync_ev) (void)hipEventDestroy(E->sync_ev);
   E->sync_ev = nullptr;
+  for (hipEvent_t ev : E->req_ev) (void)hipEventDestroy(ev);
+  E->req_ev.clear();
+  if (E->req_copy) (void)hipStreamDestroy(E->req_copy);
+  E->req_copy = nullptr;
   if (E->ctr) (void)hipFree(E->ctr);
   if (E->ctr_save) (void)hipFree(E->ctr_save);
   E->ctr = E->ctr_save = nullptr;
@@ -880,6 +884,17 @@ int engine_stage_requests(otm_engine* E, int32_t n, size_t bytes, bool bodies, i
     *err = "invalid request count";
     return OTM_EINVAL;
   }
+  // the device side for the reads behind each pushed piece
+  const size_t slots = req_sparse_slots(n, bytes);
+  if ((rc = ensure(E->d_req, req_blob_bytes(n, bytes), err))) return rc;
+  if ((rc = ensure(E->req_cnt, ((size_t)n + 1) * 8, err))) return rc;
+  if ((rc = ensure(E->req_ok, (size_t)n + 1, err))) return rc;
+  if ((rc = ensure(E->req_lat, slots * 4, err))) return rc;
+  if ((rc = ensure(E->req_lon, slots * 4, err))) return rc;
+  if ((rc = ensure(E->req_time, slots * 8, err))) return rc;
+  if ((rc = ensure(E->req_acc, slots * 4, err))) return rc;
+  E->req_read = 0;
+  E->req_piece = 0;
   if (!bodies) {
     // every body goes to HBM from the caller's page-locked memory: the header alone
     if ((rc = ensure_pinned(E->h_req, req_hdr_bytes(n), err))) return rc;
@@ -900,23 +915,59 @@ int engine_stage_requests(otm_engine* E, int32_t n, size_t bytes, bool bodies, i
 // to == bytes), so the host can stage the next piece while this one moves.
 // With src (page-locked host memory holding body bytes [from, to)) the bodies
 // are copied from there instead of the staging buffer.
+static DevBatch req_sparse(otm_engine* E) {
+  DevBatch sp{};
+  sp.lat = (const float*)E->req_lat.p;
+  sp.lon = (const float*)E->req_lon.p;
+  sp.time = (const double*)E->req_time.p;
+  sp.acc = (const float*)E->req_acc.p;
+  return sp;
+}
+
+// read requests [E->req_read, upto) of the device blob (requests.hip)
+static void read_requests(otm_engine* E, int32_t n, int32_t upto) {
+  if (upto <= E->req_read) return;
+  const unsigned char* d = (const unsigned char*)E->d_req.p;
+  launch_req_read(d + req_hdr_bytes(n), (const int64_t*)d, E->req_read, upto, n, P<int64_t>(E->req_cnt),
+                  P<uint8_t>(E->req_ok), req_sparse(E), E->stream);
+  E->req_read = upto;
+}
+
+// The pieces go to HBM on a copy stream of their own, each followed by an
+// event that the batch stream waits on before it reads the piece's requests,
+// so one piece's read overlaps the next piece's copy.
 int engine_push_requests(otm_engine* E, int32_t n, size_t bytes, size_t from, size_t to, const char* src,
-                         std::string* err) {
-  int rc;
-  if ((rc = ensure(E->d_req, req_blob_bytes(n, bytes), err))) return rc;
+                         int32_t upto, std::string* err) {
+  if (!E->req_copy) HIPCHK(hipStreamCreateWithFlags(&E->req_copy, hipStreamNonBlocking));
+  while (E->req_ev.size() < E->req_piece + 2) {  // [0]: the fence, [1 + p]: piece p
+    hipEvent_t ev = nullptr;
+    HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    E->req_ev.push_back(ev);
+  }
+  hipStream_t c = E->req_copy;
   char* d = (char*)E->d_req.p;
   const char* h = (const char*)E->h_req.p;
   const size_t hdr = req_hdr_bytes(n);
   const hipMemcpyKind h2d = hipMemcpyHostToDevice;
+  if (E->req_piece == 0) {
+    // the copies must not overtake the batch stream's earlier work on d_req
+    HIPCHK(hipEventRecord(E->req_ev[0], E->stream));
+    HIPCHK(hipStreamWaitEvent(c, E->req_ev[0], 0));
+  }
   if (!src) {
     const size_t a = from ? hdr + from : 0;
     const size_t b = hdr + (to >= bytes ? bytes + REQ_PAD : to);
-    if (b > a) HIPCHK(big_copy(d + a, h + a, b - a, h2d, E->stream));
-    return OTM_OK;
+    if (b > a) HIPCHK(big_copy(d + a, h + a, b - a, h2d, c));
+  } else {
+    if (from == 0) HIPCHK(hipMemcpyAsync(d, h, hdr, h2d, c));
+    if (to > from) HIPCHK(big_copy(d + hdr + from, src, to - from, h2d, c));
+    if (to >= bytes) HIPCHK(hipMemsetAsync(d + hdr + bytes, 0, REQ_PAD, c));
   }
-  if (from == 0) HIPCHK(hipMemcpyAsync(d, h, hdr, h2d, E->stream));
-  if (to > from) HIPCHK(big_copy(d + hdr + from, src, to - from, h2d, E->stream));
-  if (to >= bytes) HIPCHK(hipMemsetAsync(d + hdr + bytes, 0, REQ_PAD, E->stream));
+  hipEvent_t ev = E->req_ev[1 + E->req_piece++];
+  HIPCHK(hipEventRecord(ev, c));
+  HIPCHK(hipStreamWaitEvent(E->stream, ev, 0));
+  read_requests(E, n, upto < n ? upto : n);
+  HIPCHK(hipGetLastError());
   return OTM_OK;
 }
 
@@ -925,9 +976,6 @@ int engine_match_requests(otm_engine* E, int32_t n, size_t bytes, bool pushed, c
   int rc;
   hipStream_t s = E->stream;
   const size_t total = req_blob_bytes(n, bytes);
-  if ((rc = ensure(E->d_req, total, err))) return rc;
-  if ((rc = ensure(E->req_cnt, ((size_t)n + 1) * 8, err))) return rc;
-  if ((rc = ensure(E->req_ok, (size_t)n + 1, err))) return rc;
   if ((rc = ensure_pinned(E->h_req_ok, (size_t)n + 8 + 8, err))) return rc;
   if ((rc = ensure(E->scan_tmp, scan_tmp_bytes(n) + 256, err))) return rc;
   // a valid point takes at least 39 bytes (`{"lat":0,"lon":0,"time":0,"accuracy":0}`)
@@ -940,9 +988,9 @@ int engine_match_requests(otm_engine* E, int32_t n, size_t bytes, bool pushed, c
   if ((rc = ensure(E->in_acc, np_max * 4, err))) return rc;
   if (!pushed) HIPCHK(big_copy(E->d_req.p, E->h_req.p, total, hipMemcpyHostToDevice, s));
   const int64_t* off = (const int64_t*)E->d_req.p;
-  const unsigned char* body = (const unsigned char*)E->d_req.p + req_hdr_bytes(n);
   int64_t* cnt = P<int64_t>(E->req_cnt);
-  launch_req_scan(body, off, n, cnt, P<uint8_t>(E->req_ok), s);
+  read_requests(E, n, n);  // (the requests no push read yet; n == 0: cnt[0] = 0)
+  if (n == 0) HIPCHK(hipMemsetAsync(cnt, 0, 8, s));
   scan_i64(cnt, n, E->scan_tmp.p, E->scan_tmp.cap, s);
   DevBatch b{};
   b.trace_off = (const int64_t*)E->in_off.p;
@@ -950,7 +998,7 @@ int engine_match_requests(otm_engine* E, int32_t n, size_t bytes, bool pushed, c
   b.lon = (const float*)E->in_lon.p;
   b.time = (const double*)E->in_time.p;
   b.acc = (const float*)E->in_acc.p;
-  launch_req_fill(body, off, n, cnt, P<uint8_t>(E->req_ok), b, P<int64_t>(E->in_off), s);
+  launch_req_compact(off, n, cnt, P<uint8_t>(E->req_ok), req_sparse(E), b, P<int64_t>(E->in_off), s);
   // the batch's size and the flags: one synchronisation before the match
   char* h = (char*)E->h_req_ok.p;
   HIPCHK(hipMemcpyAsync(h, cnt + n, 8, hipMemcpyDeviceToHost, s));

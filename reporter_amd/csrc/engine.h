@@ -107,6 +107,11 @@ struct otm_engine {
   // request bodies read on the GPU (engine_match_requests): the pinned staging
   // blob (offsets, then bytes), its device copy, per-request counts and flags
   Buf h_req, d_req, req_cnt, req_ok, h_req_ok;
+  Buf req_lat, req_lon, req_time, req_acc;  // the reader's sparse point slots (requests.hip)
+  int32_t req_read = 0;                     // requests of the staged batch read so far
+  hipStream_t req_copy = nullptr;           // the request pieces' H2D copies (created at first use)
+  std::vector<hipEvent_t> req_ev;           // [0] the copies' fence, [1 + p]: piece p copied
+  size_t req_piece = 0;                     // pieces of the staged batch pushed so far
   // response bodies written on the GPU (engine_write_responses): piece slots,
   // lengths, the dense blob, and its pinned host copy with offsets and flags
   Buf resp_hdr, resp_seg, resp_rep, resp_hlen, resp_slen, resp_rlen, resp_blen, resp_host, resp_blob;
@@ -168,9 +173,11 @@ int engine_stage_requests(otm_engine* E, int32_t n, size_t bytes, bool bodies, i
                           std::string* err);
 // (engine_push_requests: a piece of the staged blob on its way to HBM, so
 // staging and copying overlap; pushed = every piece went that way)
-// (src: those bytes from page-locked host memory instead of the staging buffer)
+// (src: those bytes from page-locked host memory instead of the staging buffer;
+// upto: the requests [0, upto) are then whole on the device, and those not yet
+// read are read behind the copy, while the host stages the next piece)
 int engine_push_requests(otm_engine* E, int32_t n, size_t bytes, size_t from, size_t to, const char* src,
-                         std::string* err);
+                         int32_t upto, std::string* err);
 int engine_match_requests(otm_engine* E, int32_t n, size_t bytes, bool pushed, const uint8_t** ok,
                           int32_t* n_traces, std::string* err);
 // The last batch's /report response bodies written on the GPU

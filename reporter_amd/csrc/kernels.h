@@ -304,14 +304,17 @@ bool fold_bookkeeping();
 void launch_status(const int32_t* abort, const int64_t* ttotal, const int32_t* counters, BatchStatus* out,
                    hipStream_t s);
 void launch_row_pack(const int32_t* row_cnt, const int64_t* row_off, IdxRow* rows, int32_t n, hipStream_t s);
-// the /report request bytes read on the GPU (requests.hip): per request of
-// the staged blob (bytes [off[r], off[r+1])), accepted << 40 | points in cnt
-// and ok[r]; after an exclusive scan of cnt (n + 1 entries), the accepted
+// the /report request bytes read on the GPU (requests.hip): per request r of
+// [r0, r1) of the staged blob (bytes [off[r], off[r+1])), accepted << 40 |
+// points in cnt[r] and ok[r], its points into the sparse arrays
+// (req_sparse_slots entries; cnt[n] = 0 by the launch that ends at n); after
+// an exclusive scan of cnt (n + 1 entries), the compaction moves the accepted
 // requests' points into out's arrays and their offsets into trace_off
-void launch_req_scan(const unsigned char* blob, const int64_t* off, int32_t n, int64_t* cnt, uint8_t* ok,
-                     hipStream_t s);
-void launch_req_fill(const unsigned char* blob, const int64_t* off, int32_t n, const int64_t* pre,
-                     const uint8_t* ok, const DevBatch& out, int64_t* trace_off, hipStream_t s);
+size_t req_sparse_slots(int32_t n, size_t bytes);
+void launch_req_read(const unsigned char* blob, const int64_t* off, int32_t r0, int32_t r1, int32_t n, int64_t* cnt,
+                     uint8_t* ok, const DevBatch& sparse, hipStream_t s);
+void launch_req_compact(const int64_t* off, int32_t n, const int64_t* pre, const uint8_t* ok, const DevBatch& sparse,
+                        const DevBatch& out, int64_t* trace_off, hipStream_t s);
 // the /report response bodies written on the GPU (responses.hip) from a
 // batch's dense results (engine_fetch's compaction, device side)
 constexpr int RESP_HDR_SLOT = 512;  // bytes of a trace's header piece

@@ -152,13 +152,12 @@ __device__ bool req_header(const unsigned char* blob, int64_t a, int64_t e, int 
   return *t1 > *t0;
 }
 
-// Walk request r's points region; PASS 0 validates and counts, PASS 1 writes
-// the points of an accepted request at out + base.  Windows of CH bytes
-// (+ MARGIN) are staged in LDS with 16-byte aligned loads, all of a lane's in
-// flight at once; a lane owns the '{' bytes of its 64-byte slice of the step.
-template <int PASS>
+// Walk request r's points region: validate and count, and write each point
+// that parses at out + base + its index (below cap).  Windows of
+// CH bytes (+ MARGIN) are staged in LDS with 16-byte aligned loads, all of a
+// lane's in flight at once; a lane owns the '{' bytes of its 64-byte slice.
 __device__ bool walk_points(const unsigned char* blob, int64_t t0, int64_t t1, int lane, unsigned char* L, int64_t base,
-                            const DevBatch* out, int* npts) {
+                            int64_t cap, const DevBatch* out, int* npts) {
   int count = 0;
   bool good = true;
   for (int64_t w0 = t0; w0 < t1; w0 += CH) {
@@ -204,7 +203,7 @@ __device__ bool walk_points(const unsigned char* blob, int64_t t0, int64_t t1, i
       double la, lo, ti, ac;
       const bool ok = parse_point(W, k, lim, (int)(t1 - w0), &la, &lo, &ti, &ac);
       good = good && ok;
-      if (PASS == 1 && ok) {
+      if (ok && idx + m < cap) {  // (cap: an invalid body's stray '{'s write nothing past its range)
         const int64_t p = base + idx + m;
         // extract_points' conversions (report.cpp)
         ((float*)out->lat)[p] = (float)la;
@@ -220,56 +219,71 @@ __device__ bool walk_points(const unsigned char* blob, int64_t t0, int64_t t1, i
   return good;
 }
 
-// pass 0: per request, accepted << 40 | points (0 when left to the host)
-__global__ __launch_bounds__(RTB) void k_req_scan(const unsigned char* blob, const int64_t* off, int32_t n,
-                                                  int64_t* cnt, uint8_t* ok) {
+// Request r's points land in a sparse slot range first: a valid point takes
+// >= 39 bytes, so request r (len_r bytes) holds at most len_r / 39 points and
+// the ranges [r + off[r] / 39, + len_r / 39) never overlap (floor(a/39) +
+// floor(b/39) <= floor((a+b)/39)).  So one pass can validate, count and
+// write, piece by piece as the blob arrives, and a compaction after the scan
+// of the counts moves the accepted points into the dense batch.
+__device__ __forceinline__ int64_t sparse_base(int32_t r, int64_t a) { return (int64_t)r + a / 39; }
+
+// per request of [r0, r1): accepted << 40 | points in cnt (0: the host
+// readers take it), ok[r], its points at their sparse slots
+__global__ __launch_bounds__(RTB) void k_req_read(const unsigned char* blob, const int64_t* off, int32_t r0,
+                                                  int32_t r1, int32_t n, int64_t* cnt, uint8_t* ok, DevBatch sp) {
   __shared__ __attribute__((aligned(16))) unsigned char L[WBUF];
   const int lane = threadIdx.x;
-  for (int32_t r = blockIdx.x; r < n; r += gridDim.x) {
+  for (int32_t r = r0 + blockIdx.x; r < r1; r += gridDim.x) {
     const int64_t a = off[r], e = off[r + 1];
     int64_t t0 = 0, t1 = 0;
     int np = 0;
     bool acc = req_header(blob, a, e, lane, &t0, &t1);
-    acc = acc && walk_points<0>(blob, t0, t1, lane, L, 0, nullptr, &np) && np >= 2;
+    acc = acc && walk_points(blob, t0, t1, lane, L, sparse_base(r, a), (e - a) / 39, &sp, &np) && np >= 2;
     if (lane == 0) {
       cnt[r] = acc ? ((int64_t)1 << 40) | (int64_t)np : 0;
       ok[r] = acc ? 1 : 0;
     }
   }
-  if (blockIdx.x == 0 && lane == 0) cnt[n] = 0;
+  if (r1 == n && blockIdx.x == 0 && lane == 0) cnt[n] = 0;
 }
 
-// pass 1 (cnt scanned): the accepted requests' points and trace offsets
-__global__ __launch_bounds__(RTB) void k_req_fill(const unsigned char* blob, const int64_t* off, int32_t n,
-                                                  const int64_t* pre, const uint8_t* ok, DevBatch out,
-                                                  int64_t* trace_off) {
-  __shared__ __attribute__((aligned(16))) unsigned char L[WBUF];
+// (cnt scanned into pre) the accepted requests' points from their sparse
+// slots into the dense batch, and the trace offsets: a wave per request
+__global__ __launch_bounds__(RTB) void k_req_compact(const int64_t* off, int32_t n, const int64_t* pre,
+                                                     const uint8_t* ok, DevBatch sp, DevBatch out,
+                                                     int64_t* trace_off) {
   const int lane = threadIdx.x;
   constexpr int64_t MASK = ((int64_t)1 << 40) - 1;
   if (blockIdx.x == 0 && lane == 0) trace_off[pre[n] >> 40] = pre[n] & MASK;
   for (int32_t r = blockIdx.x; r < n; r += gridDim.x) {
     if (!ok[r]) continue;
-    const int64_t a = off[r], e = off[r + 1];
-    int64_t t0 = 0, t1 = 0;
-    int np = 0;
-    (void)req_header(blob, a, e, lane, &t0, &t1);
-    if (lane == 0) trace_off[pre[r] >> 40] = pre[r] & MASK;
-    (void)walk_points<1>(blob, t0, t1, lane, L, pre[r] & MASK, &out, &np);
+    const int64_t d = pre[r] & MASK, m = (pre[r + 1] & MASK) - d;
+    const int64_t s = sparse_base(r, off[r]);
+    if (lane == 0) trace_off[pre[r] >> 40] = d;
+    for (int64_t i = lane; i < m; i += RTB) {
+      ((float*)out.lat)[d + i] = sp.lat[s + i];
+      ((float*)out.lon)[d + i] = sp.lon[s + i];
+      ((double*)out.time)[d + i] = sp.time[s + i];
+      ((float*)out.acc)[d + i] = sp.acc[s + i];
+    }
   }
 }
 
 }  // namespace
 
-void launch_req_scan(const unsigned char* blob, const int64_t* off, int32_t n, int64_t* cnt, uint8_t* ok,
-                     hipStream_t s) {
-  const int grid = n < 65536 ? (n > 0 ? n : 1) : 65536;
-  hipLaunchKernelGGL(k_req_scan, dim3(grid), dim3(RTB), 0, s, blob, off, n, cnt, ok);
+size_t req_sparse_slots(int32_t n, size_t bytes) { return (size_t)n + bytes / 39 + 1; }
+
+void launch_req_read(const unsigned char* blob, const int64_t* off, int32_t r0, int32_t r1, int32_t n, int64_t* cnt,
+                     uint8_t* ok, const DevBatch& sparse, hipStream_t s) {
+  const int32_t m = r1 - r0;
+  const int grid = m < 65536 ? (m > 0 ? m : 1) : 65536;
+  hipLaunchKernelGGL(k_req_read, dim3(grid), dim3(RTB), 0, s, blob, off, r0, r1, n, cnt, ok, sparse);
 }
 
-void launch_req_fill(const unsigned char* blob, const int64_t* off, int32_t n, const int64_t* pre,
-                     const uint8_t* ok, const DevBatch& out, int64_t* trace_off, hipStream_t s) {
+void launch_req_compact(const int64_t* off, int32_t n, const int64_t* pre, const uint8_t* ok, const DevBatch& sparse,
+                        const DevBatch& out, int64_t* trace_off, hipStream_t s) {
   const int grid = n < 65536 ? (n > 0 ? n : 1) : 65536;
-  hipLaunchKernelGGL(k_req_fill, dim3(grid), dim3(RTB), 0, s, blob, off, n, pre, ok, out, trace_off);
+  hipLaunchKernelGGL(k_req_compact, dim3(grid), dim3(RTB), 0, s, off, n, pre, ok, sparse, out, trace_off);
 }
 
 }  // namespace otm

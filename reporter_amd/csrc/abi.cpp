@@ -547,6 +547,7 @@ void free_body(void* p) {
 // for later submissions; the small ones are plain mallocs.
 namespace slabs {
 constexpr size_t SLAB_PINNED_MIN = (size_t)1 << 20;
+constexpr size_t SLAB_MAX = (size_t)128 << 20;  // one slab per submission up to this
 size_t pinned_min() {  // OTM_SLAB_PINNED_MIN overrides (tests: every slab page-locked)
   const char* e = std::getenv("OTM_SLAB_PINNED_MIN");
   return e ? (size_t)std::strtoull(e, nullptr, 10) : SLAB_PINNED_MIN;
@@ -570,10 +571,11 @@ void release(ReqSlab* s) {
   delete s;
 }
 
-// a slab of >= bytes (throws std::bad_alloc when there is no memory at all)
-std::shared_ptr<ReqSlab> acquire(size_t bytes) {
+// a slab of >= bytes, page-locked from pinned_min() up unless !may_pin
+// (throws std::bad_alloc when there is no memory at all)
+std::shared_ptr<ReqSlab> acquire(size_t bytes, bool may_pin = true) {
   ReqSlab* s = nullptr;
-  if (bytes >= pinned_min()) {
+  if (may_pin && bytes >= pinned_min()) {
     {
       std::lock_guard<std::mutex> lk(g_mu);
       size_t best = g_cache.size();
@@ -954,7 +956,7 @@ void worker_loop(otm_engine* E, int wi) {
       const size_t cap = async_batch();
       while (!E->queue.empty() && batch.size() < cap) {
         const otm_engine::Pending& f = E->queue.front();
-        if (!batch.empty() && f.slab != batch.back().slab && batch.size() + f.run_left > cap) break;
+        if (!batch.empty() && f.sub != batch.back().sub && batch.size() + f.run_left > cap) break;
         batch.push_back(std::move(E->queue.front()));
         E->queue.pop_front();
       }
@@ -1423,7 +1425,7 @@ static int otm_submit_impl(otm_engine* E, const char* req, size_t len, uint64_t 
   if (E->queue.size() >= (1u << 22)) return fail(OTM_EAGAIN, "submit queue full");
   std::shared_ptr<ReqSlab> slab = slabs::acquire(len);
   if (len) std::memcpy(slab->base, req, len);
-  E->queue.push_back(otm_engine::Pending{tag, slab->base, len, std::move(slab), 1});
+  E->queue.push_back(otm_engine::Pending{tag, slab->base, len, std::move(slab), 1, E->n_subs++});
   E->qcv.notify_all();
   return OTM_OK;
 }
@@ -1432,22 +1434,32 @@ static int otm_submit_batch_impl(otm_engine* E, int n, const char* const* reqs, 
                                  const uint64_t* tags) {
   if (!E || n < 0 || (n && (!reqs || !lens || !tags))) return fail(OTM_EINVAL, "bad arguments");
   // the bodies copied into one slab (page-locked when large), outside the
-  // queue lock, over the host threads
+  // queue lock, over the host threads; a submission beyond SLAB_MAX bytes
+  // gets an allocation per body instead (page-locking that much per
+  // submission costs more than the staging copy it saves)
   std::vector<size_t> off((size_t)n + 1, 0);
   for (int k = 0; k < n; ++k) off[(size_t)k + 1] = off[(size_t)k] + lens[k];
-  std::shared_ptr<ReqSlab> slab = slabs::acquire(off[(size_t)n]);
+  const char* mx = std::getenv("OTM_SLAB_MAX");  // (tests lower it)
+  const bool one = off[(size_t)n] <= (mx ? (size_t)std::strtoull(mx, nullptr, 10) : slabs::SLAB_MAX);
+  std::shared_ptr<ReqSlab> slab = one ? slabs::acquire(off[(size_t)n]) : nullptr;
   std::vector<otm_engine::Pending> items((size_t)n);
   par_for((size_t)n, [&](size_t a, size_t e) {
     for (size_t k = a; k < e; ++k) {
-      if (lens[k]) std::memcpy(slab->base + off[k], reqs[k], lens[k]);
-      items[k] = otm_engine::Pending{tags[k], slab->base + off[k], lens[k], slab, (size_t)n - k};
+      std::shared_ptr<ReqSlab> s = one ? slab : slabs::acquire(lens[k], false);
+      char* p = one ? slab->base + off[k] : s->base;
+      if (lens[k]) std::memcpy(p, reqs[k], lens[k]);
+      items[k] = otm_engine::Pending{tags[k], p, lens[k], std::move(s), (size_t)n - k, 0};
     }
   });
   {
     std::lock_guard<std::mutex> lk(E->qmu);
     if (!E->worker_started) start_workers(E);
     if (E->queue.size() + (size_t)n > (1u << 22)) return fail(OTM_EAGAIN, "submit queue full");
-    for (auto& it : items) E->queue.push_back(std::move(it));
+    const uint64_t sub = E->n_subs++;
+    for (auto& it : items) {
+      it.sub = sub;
+      E->queue.push_back(std::move(it));
+    }
   }
   E->qcv.notify_all();
   return OTM_OK;

@@ -135,7 +135,9 @@ struct otm_engine {
     size_t len;
     std::shared_ptr<ReqSlab> slab;
     size_t run_left;  // requests of its submission from this one on (itself included)
+    uint64_t sub;     // its submission's number
   };
+  uint64_t n_subs = 0;  // submissions so far (under qmu)
   std::mutex qmu;
   std::condition_variable qcv;
   std::deque<Pending> queue;

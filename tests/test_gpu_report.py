@@ -285,7 +285,9 @@ def test_one_engine_from_many_threads(small_graph):
     ("1", "8192", None, None), ("2", "37", None, None), ("3", "11", None, None),
     # page-locked submission slabs (every submission; or the first only, by
     # size), batches cut inside and across slabs, the GPU reader on them
-    ("1", "8192", "1", None), ("2", "37", "1", None), ("3", "50", "1", "1"), ("2", "200", "full", None)])
+    ("1", "8192", "1", None), ("2", "37", "1", None), ("3", "50", "1", "1"), ("2", "200", "full", None),
+    # submissions beyond OTM_SLAB_MAX: an allocation per body, batches cut inside a submission
+    ("3", "64", "slab_max", None)])
 def test_async_pipeline_order_and_bodies(small_graph, monkeypatch, workers, batch, pinned_min, gpu_min):
     """otm_submit_batch / otm_poll through the async pipeline (workers on
     their own batch contexts, OTM_ASYNC_WORKERS; small OTM_ASYNC_BATCH forces
@@ -308,6 +310,9 @@ def test_async_pipeline_order_and_bodies(small_graph, monkeypatch, workers, batc
     bodies += [b"", b'{"uuid":"x","trace":[]}']
     if pinned_min == "full":  # a whole submission's slab page-locked, half of one not
         pinned_min = str(sum(len(x) for x in bodies))
+    if pinned_min == "slab_max":
+        monkeypatch.setenv("OTM_SLAB_MAX", "1000")
+        pinned_min = "1"
     if pinned_min is not None:
         monkeypatch.setenv("OTM_SLAB_PINNED_MIN", pinned_min)
     with Engine(graph_path=small_graph) as eng:

@@ -491,7 +491,13 @@ def main():
                 ta = time.perf_counter() - ta
                 return ta, np.concatenate(parts)
 
-            async_run()  # warm: the pipeline's clones and their buffers
+            # warm: the pipeline's clones and their buffers -- twice, since a
+            # worker that took no batch in the first run would size its
+            # context inside the first timed one; the warm bodies released
+            # like the timed ones (their arenas back to the cache)
+            for _ in range(2):
+                for pb in async_run()[1]["body"]:
+                    L.otm_free(C.c_void_p(int(pb)))
             # three timed runs (the host side of a run varies with the box's
             # CPU quota and allocator state): the mean is `value`
             runs = []
@@ -512,7 +518,7 @@ def main():
                           "first_responses_byte_equal_to_json_report": bool(same),
                           "includes": "otm_submit_batch of the 10k Java request bodies x %d in a row (copies into the "
                                       "queue), otm_poll until every response is back: the async pipeline, %s "
-                                      "workers on their own batch contexts; mean of 3 runs" %
+                                      "workers on their own batch contexts; mean of 3 runs after 2 warm ones" %
                                       (args.async_rounds, os.environ.get("OTM_ASYNC_WORKERS", "3"))}
         json_leg = {"value": P / jel, "unit": "points/s", "ms_per_call": jel * 1e3, "calls": args.json_calls,
                     "async": json_async,

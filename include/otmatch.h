@@ -74,7 +74,6 @@ typedef struct otm_engine otm_engine;
  *   DESIGN.md §8. */
 int otm_engine_create(const char* cfg_path, const int* devices, int ndev,
                       otm_engine** out);
-/* Members of an engine: ndev of a multi-device engine, 1 otherwise. */
 /* The matcher parameters a config file gives, without a device: meili's
  * "default" section with the mode's section ("meili.mode", default "auto")
  * on top, as valhalla.Configure (py/reporter_service.py:279) reads the meili
@@ -85,6 +84,7 @@ typedef struct otm_meili_params {
   int32_t max_candidates;
 } otm_meili_params;
 int otm_config_meili(const char* cfg_path, otm_meili_params* out);
+/* Members of an engine: ndev of a multi-device engine, 1 otherwise. */
 int otm_engine_members(const otm_engine* eng);
 /* Member i of a multi-device engine (NULL when out of range); a one-device
  * engine is its own member 0.  Owned by eng. */
@@ -163,8 +163,8 @@ int otm_submit(otm_engine* eng, const char* req, size_t len, uint64_t tag);
 /* n requests at once (a Kafka poll's records): the same as n otm_submit
  * calls in order, the bodies copied over the library's host threads.  The
  * async path is a pipeline: each worker runs whole request batches on its
- * own batch context (OTM_ASYNC_WORKERS, default 2; OTM_ASYNC_BATCH requests
- * per batch, default 8192), so one batch's parse and response writing overlap
+ * own batch context (OTM_ASYNC_WORKERS, default 3; OTM_ASYNC_BATCH requests
+ * per batch, default 16384), so one batch's parse and response writing overlap
  * another's GPU work; results are published in submit order. */
 int otm_submit_batch(otm_engine* eng, int n, const char* const* reqs, const size_t* lens, const uint64_t* tags);
 /* Fills up to max results; waits at most timeout_us for the first one.
@@ -173,8 +173,15 @@ int otm_poll(otm_engine* eng, otm_result* out, int max, int timeout_us);
 
 /* Java request encoder (Batch.report + Point.Serder.put_json,
  * Batch.java:52-61, Point.java:39-45): float32 lat/lon through
- * DecimalFormat("###.######") HALF_EVEN, long time, int accuracy.
- * *out is allocated by the library. */
+ * DecimalFormat("###.######") HALF_EVEN, long time, int accuracy, in the
+ * bytes HttpClient.POST sends: new StringEntity(body) is ISO-8859-1
+ * (HttpClient.java:26), so the uuid -- the Kafka record key, given here as
+ * its UTF-8 bytes and read as StringDeserializer reads it (JDK 8, U+FFFD for
+ * malformed input) -- goes out unescaped with U+0080..U+00FF as single bytes
+ * and anything above U+00FF as '?'.  Such a body is what the reference
+ * service answers 400 ('utf-8' codec ...) when a Latin-1 byte breaks its
+ * body.decode('utf-8') (py/reporter_service.py:99); otm_report answers it
+ * the same.  *out is allocated by the library. */
 int otm_encode_request(const char* uuid, int n, const float* lat,
                        const float* lon, const int64_t* time,
                        const int32_t* accuracy, char** out, size_t* out_len);
@@ -360,9 +367,11 @@ const char* otm_kernel_name(int k);
 
 /* How much work of the last batch each fallback tier took:
  * probes the lane candidate tier handed to the wave tier; transition columns
- * the distance index could not answer, then those the lane search spilled to
- * the LDS wave search, then to the global-memory search; the same for the
- * route stage's steps. */
+ * the route index could not answer (trans_online), then those the LDS wave
+ * search spilled to the global-memory search (trans_global); the same for the
+ * route stage's steps.  trans_wave / route_wave are kept for the layout and
+ * equal trans_online / route_online: every online search starts in the LDS
+ * wave tier since round 3 (the lane-per-search tier is gone). */
 typedef struct otm_spill_stats {
   int32_t cand_wave;
   int32_t trans_online, trans_wave, trans_global;
@@ -387,6 +396,11 @@ int otm_kmax(void);
  * lengths, 1 or 0 (unsupported). */
 int otm_debug_py_repr(double d, char* out);
 int otm_debug_py_round3(double x, double* out);
+/* Test hook: the response arenas' otm_free under contention from threads
+ * (each round: every thread cuts bodies from an arena, then all free a
+ * strided share of everyone's, with plain allocations through the same
+ * scan).  Returns the arenas left live after (0 expected), -1 on bad args. */
+int otm_debug_arena_stress(int threads, int rounds);
 /* Which HIP runtime this library is bound to ("<path> hip_runtime_version=N"):
  * a host that also runs torch must load torch first so both share one. */
 const char* otm_runtime_info(void);
@@ -428,7 +442,15 @@ int otm_batcher_create(otm_engine* eng, const otm_batcher_cfg* cfg, otm_report_f
                        otm_batcher** out);
 void otm_batcher_destroy(otm_batcher* b);
 /* Formatted records in stream order: (key, Point, record timestamp in ms)
- * (BatchingProcessor.process, :56-85, with context.timestamp() = ts_ms). */
+ * (BatchingProcessor.process, :56-85, with context.timestamp() = ts_ms).
+ * keys are the records' key bytes on the formatted topic, read as Kafka's
+ * StringDeserializer reads them (JDK 8 UTF-8, U+FFFD for malformed input:
+ * keys that decode to one Java String are one key; forwarded keys are that
+ * String's UTF-8).  Each request body carries the key as HttpClient sends it
+ * (otm_encode_request): in binary mode a key whose body the service would
+ * reject or read differently (a Latin-1 byte, a quote, a backslash, a
+ * control character) is answered through the byte-level /report path, so
+ * it gets the reference's response (its 400 body included). */
 int otm_batcher_process(otm_batcher* b, int n, const char* const* keys, const size_t* key_lens, const float* lat,
                         const float* lon, const int32_t* accuracy, const int64_t* time, const int64_t* ts_ms);
 /* Run every queued operation to completion (matcher calls included). */

@@ -97,7 +97,8 @@ public final class OtmMatcher {
   /** Same contract as HttpClient.POST: the response body, or null on a failure of the call. */
   public static String POST(String url, String body) {
     try (Arena a = Arena.ofConfined()) {
-      byte[] b = body.getBytes(StandardCharsets.UTF_8);
+      // new StringEntity(body) (HttpClient.java:26): ISO-8859-1, '?' for a character above U+00FF
+      byte[] b = body.getBytes(StandardCharsets.ISO_8859_1);
       MemorySegment req = a.allocate(b.length);
       MemorySegment.copy(b, 0, req, ValueLayout.JAVA_BYTE, 0, b.length);
       MemorySegment resp = a.allocate(ValueLayout.ADDRESS);
@@ -114,7 +115,8 @@ public final class OtmMatcher {
   /** Queue one /report request; its result comes back from poll() with this tag. */
   public static boolean submit(String body, long tag) {
     try (Arena a = Arena.ofConfined()) {
-      byte[] b = body.getBytes(StandardCharsets.UTF_8);
+      // new StringEntity(body) (HttpClient.java:26): ISO-8859-1, '?' for a character above U+00FF
+      byte[] b = body.getBytes(StandardCharsets.ISO_8859_1);
       MemorySegment req = a.allocate(b.length);
       MemorySegment.copy(b, 0, req, ValueLayout.JAVA_BYTE, 0, b.length);
       return (int) SUBMIT.invokeExact(ENGINE, req, (long) b.length, tag) == 0;

@@ -3,7 +3,8 @@
  *
  * Binds org.opentraffic.reporter.OtmJni (integration/java/.../OtmJni.java) to libotmatch.so.  OtmJni.POST
  * replaces HttpClient.POST at Batch.java:63 with the same contract: the body reporter_service.py would
- * answer (any status), or null when the call itself fails (HttpClient.java:37-39).
+ * answer (any status), or null when the call itself fails (HttpClient.java:37-39).  The String <-> bytes
+ * steps stay in Java (OtmJni.POST), in HttpClient's charsets: ISO-8859-1 out, UTF-8 back.
  *
  * Build (needs a JDK, absent from this image):
  *   gcc -O2 -shared -fPIC -I$JAVA_HOME/include -I$JAVA_HOME/include/linux -I../../include \
@@ -25,20 +26,22 @@ JNIEXPORT void JNICALL Java_org_opentraffic_reporter_OtmJni_init(JNIEnv* env, jc
   (*env)->ReleaseStringUTFChars(env, cfg, p);
 }
 
-JNIEXPORT jstring JNICALL Java_org_opentraffic_reporter_OtmJni_POST(JNIEnv* env, jclass c, jstring url,
-                                                                    jstring body) {
+/* OtmJni.report(byte[]): the request bytes as HttpClient would send them (OtmJni.POST encodes the String
+ * with ISO-8859-1 first, as new StringEntity(body) does, HttpClient.java:26), the response bytes back; the
+ * Java side decodes them as UTF-8 (HttpClient.java:33).  null when the call itself fails. */
+JNIEXPORT jbyteArray JNICALL Java_org_opentraffic_reporter_OtmJni_report(JNIEnv* env, jclass c, jbyteArray body) {
   (void)c;
-  (void)url; /* ignored: the matcher is in process */
   if (!g_eng || !body) return NULL;
-  /* Batch.java builds pure-ASCII bodies (digits, keys, the uuid), so modified UTF-8 == UTF-8 here */
-  const char* b = (*env)->GetStringUTFChars(env, body, 0);
-  jsize n = (*env)->GetStringUTFLength(env, body);
+  jsize n = (*env)->GetArrayLength(env, body);
+  jbyte* b = (*env)->GetByteArrayElements(env, body, NULL);
+  if (!b) return NULL;
   char* resp = NULL;
   size_t rn = 0;
-  otm_report(g_eng, b, (size_t)n, &resp, &rn);
-  (*env)->ReleaseStringUTFChars(env, body, b);
+  otm_report(g_eng, (const char*)b, (size_t)n, &resp, &rn);
+  (*env)->ReleaseByteArrayElements(env, body, b, JNI_ABORT);
   if (!resp) return NULL;
-  jstring out = (*env)->NewStringUTF(env, resp); /* bodies are NUL-terminated, ensure_ascii JSON */
+  jbyteArray out = (*env)->NewByteArray(env, (jsize)rn);
+  if (out) (*env)->SetByteArrayRegion(env, out, 0, (jsize)rn, (const jbyte*)resp);
   otm_free(resp);
   return out;
 }

@@ -87,7 +87,10 @@ class Batch(object):
     def body(self, key):
         parts = ['{"lat":%s,"lon":%s,"time":%d,"accuracy":%d}' % (decimal6(p.lat), decimal6(p.lon), p.time,
                                                                   p.accuracy) for p in self.points]
-        return ('{"uuid":"' + key + '","trace":[' + ",".join(parts) + "]}").encode()
+        # HttpClient.POST sends it through new StringEntity(body) (HttpClient.java:26):
+        # ISO-8859-1, '?' for a character above U+00FF (one per code point: a Java
+        # surrogate pair is one Python character)
+        return ('{"uuid":"' + key + '","trace":[' + ",".join(parts) + "]}").encode("latin-1", "replace")
 
     def report(self, key, post, min_dist, min_size, min_elapsed):
         if (float(self.max_separation) < min_dist or len(self.points) < min_size or
@@ -153,5 +156,6 @@ class BatchingProcessor(object):
         self.time_to_key.append((ts, key))
 
     def close(self):
-        for k in sorted(self.store):  # in-memory store = TreeMap: key order
+        # in-memory store = TreeMap: String.compareTo order, i.e. UTF-16 code units
+        for k in sorted(self.store, key=lambda x: x.encode("utf-16-be", "surrogatepass")):
             self.store[k].report(k, self._post, 0, 2, 0)

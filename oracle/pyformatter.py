@@ -19,7 +19,8 @@ reference's own format examples -- Reporter.java:35-43, README.md:23-27):
   Double.toString            shortest repr digits, JDK >= 19 rules
   joda DateTimeFormat        y M d H m s S patterns, UTC, default year 2000
   Jackson JsonNode           readTree (first value), get, asText/asLong/asDouble
-  Kafka StringDeserializer   bytes.decode('utf-8', 'replace')
+  Kafka StringDeserializer   new String(bytes, UTF8) of JDK 8 (java_utf8_decode)
+  Kafka StringSerializer     String.getBytes(UTF8): an unpaired surrogate -> '?'
 """
 import json
 import math
@@ -41,6 +42,92 @@ def java_digit(ch):
     if o > 0xFFFF or 0x0DE6 <= o <= 0x0DEF or 0xA9F0 <= o <= 0xA9F9:
         return -1
     return unicodedata.decimal(ch, -1) if unicodedata.category(ch) == "Nd" else -1
+
+
+def java_utf8_decode(b):
+    """new String(bytes, UTF_8) in JDK 8 (sun.nio.cs.UTF_8 ArrayDecoder, REPLACE),
+    as a Python str.  Differs from bytes.decode('utf-8', 'replace') on encoded
+    surrogates: JDK 8 replaces a whole ED A0..BF xx sequence (or a truncated
+    ED A0..BF) with ONE U+FFFD, Python with one per byte."""
+    R = "\ufffd"
+    out = []
+    i, n = 0, len(b)
+    while i < n:
+        c = b[i]
+        i += 1
+        if c < 0x80:
+            out.append(chr(c))
+            continue
+        if 0xC2 <= c <= 0xDF:
+            if i >= n:
+                out.append(R)
+                break
+            if b[i] & 0xC0 != 0x80:
+                out.append(R)
+            else:
+                out.append(chr(((c & 0x1F) << 6) | (b[i] & 0x3F)))
+                i += 1
+            continue
+        if 0xE0 <= c <= 0xEF:
+            if n - i >= 2:
+                c2, c3 = b[i], b[i + 1]
+                bad2 = (c == 0xE0 and 0x80 <= c2 <= 0x9F) or c2 & 0xC0 != 0x80
+                if bad2 or c3 & 0xC0 != 0x80:
+                    out.append(R)
+                    i += 0 if bad2 else 1
+                    continue
+                cp = ((c & 0xF) << 12) | ((c2 & 0x3F) << 6) | (c3 & 0x3F)
+                out.append(R if 0xD800 <= cp <= 0xDFFF else chr(cp))
+                i += 2
+                continue
+            if i < n and ((c == 0xE0 and 0x80 <= b[i] <= 0x9F) or b[i] & 0xC0 != 0x80):
+                out.append(R)
+                continue
+            out.append(R)
+            break
+        if 0xF0 <= c <= 0xF7:
+            def bad_second(x):
+                return c > 0xF4 or (c == 0xF0 and not 0x90 <= x <= 0xBF) or (c == 0xF4 and not 0x80 <= x <= 0x8F) \
+                    or x & 0xC0 != 0x80
+            if n - i >= 3:
+                c2, c3, c4 = b[i], b[i + 1], b[i + 2]
+                cp = ((c & 7) << 18) | ((c2 & 0x3F) << 12) | ((c3 & 0x3F) << 6) | (c4 & 0x3F)
+                if any(x & 0xC0 != 0x80 for x in (c2, c3, c4)) or not 0x10000 <= cp <= 0x10FFFF:
+                    out.append(R)
+                    if bad_second(c2):
+                        pass
+                    elif c3 & 0xC0 != 0x80:
+                        i += 1
+                    else:
+                        i += 2
+                    continue
+                out.append(chr(cp))
+                i += 3
+                continue
+            if c > 0xF4 or (i < n and bad_second(b[i])):
+                out.append(R)
+                continue
+            i += 1
+            if i < n and b[i] & 0xC0 != 0x80:
+                out.append(R)
+                continue
+            out.append(R)
+            break
+        out.append(R)
+    return "".join(out)
+
+
+def java_serialize_key(s):
+    """Kafka StringSerializer's String.getBytes(UTF8), read back: an unpaired
+    surrogate (a JSON \\ud800 escape the Formatter kept) becomes '?'."""
+    return "".join("?" if 0xD800 <= ord(ch) <= 0xDFFF else ch for ch in s)
+
+
+def java_latin1(s):
+    """String.getBytes(ISO_8859_1) (httpcore StringEntity's default charset,
+    HttpClient.java:26): above U+00FF -> '?' (a supplementary character, one
+    surrogate pair in Java, is one '?')."""
+    return bytes(ord(ch) if ord(ch) <= 0xFF else 0x3F for ch in s)
 
 
 class Drop(Exception):
@@ -608,7 +695,7 @@ class Formatter(object):
     def format(self, message):
         """Formatter.format: bytes -> (key, lat, lon, accuracy, time); Drop if the reference throws."""
         if isinstance(message, bytes):
-            message = message.decode("utf-8", "replace")
+            message = java_utf8_decode(message)
         return self._sv(message) if self.sv else self._json(message)
 
     def _sv(self, msg):
@@ -651,4 +738,4 @@ class Formatter(object):
             acc = d2i(d)
         else:
             acc = d2i(float(math.ceil(d)))
-        return as_text(node[uk]), lat, lon, acc, time
+        return java_serialize_key(as_text(node[uk])), lat, lon, acc, time

@@ -128,7 +128,7 @@ class Batcher(object):
 
     def batch(self, key):
         """(points [(lat, lon, accuracy, time)], max_separation) stored for key, or None."""
-        kb = key.encode("utf-8")
+        kb = key if isinstance(key, bytes) else key.encode("utf-8")
         ms = C.c_float()
         n = lib().otm_batcher_batch(self.h, kb, len(kb), 0, None, None, None, None, C.byref(ms))
         if n < 0:

@@ -20,6 +20,7 @@
 #include <thread>
 
 #include "engine.h"
+#include "javastr.h"
 #include "json.h"
 #include "pyrepr.h"
 #include "report.h"
@@ -515,12 +516,19 @@ char* acquire(size_t bytes, int64_t nbodies, bool pinned = false) {
 
 void release(Slot& S) {
   std::lock_guard<std::mutex> lk(g_mu);
+  // out of every address range, then out of LIVE, before the memory can go
+  // back to the allocator: free_body's lock-free scan must never match a
+  // pointer the allocator hands out again inside the old range.  hi goes
+  // first: a scan reads lo then hi, so it sees [old lo, old hi) or an empty
+  // range, never [0, old hi)
+  S.hi.store(0);
+  S.lo.store(0);
   if (g_cached + S.cap <= ARENA_CACHE) {
     g_cached += S.cap;
     S.state.store(CACHED);
   } else {
-    drop(S);
     S.state.store(FREE);
+    drop(S);
   }
 }
 
@@ -720,7 +728,7 @@ bool gpu_writer() {
 // writer leaves (a 500, a float outside its range) is written on the host
 // from the batch's typed records.
 void report_many_device(otm_engine* E, int n, const char* const* reqs, const size_t* lens, int* codes,
-                        char** resps, size_t* resp_lens, const uint8_t* pinned) {
+                        char** resps, size_t* resp_lens, const void* const* pinned) {
   const double t0 = now_ms();
   std::vector<int> rest;  // left to the host readers
   std::vector<int> inv;   // invalid speeds per GPU-read request (stderr lines)
@@ -737,7 +745,7 @@ void report_many_device(otm_engine* E, int n, const char* const* reqs, const siz
     int64_t* off = nullptr;
     char* dst = nullptr;
     bool all_pinned = pinned != nullptr;
-    for (int k = 0; all_pinned && k < n; ++k) all_pinned = pinned[k] != 0;
+    for (int k = 0; all_pinned && k < n; ++k) all_pinned = pinned[k] != nullptr;
     rc = otm::engine_stage_requests(E, n, bytes, !all_pinned, &off, &dst, &err);
     if (!rc) {
       off[0] = 0;
@@ -754,11 +762,12 @@ void report_many_device(otm_engine* E, int n, const char* const* reqs, const siz
         const bool direct = pinned && pinned[k0];
         if (direct) {
           // a run of bodies adjacent in one page-locked submission slab:
-          // copied to HBM from there, not staged
+          // copied to HBM from there, not staged (two slabs that happen to be
+          // adjacent in memory are two allocations: two copies)
           k1 = k0 + 1;
-          while (k1 < n && pinned[k1] && reqs[k1] == reqs[k1 - 1] + lens[k1 - 1]) ++k1;
+          while (k1 < n && pinned[k1] == pinned[k0] && reqs[k1] == reqs[k1 - 1] + lens[k1 - 1]) ++k1;
         } else {
-          while (k1 > k0 + 1 && pinned && pinned[k1 - 1]) --k1;  // (the staged piece stops at a slab run)
+          while (k1 > k0 + 1 && pinned && pinned[k1 - 1] != nullptr) --k1;  // (the staged piece stops at a slab run)
           par_for((size_t)(k1 - k0), [&](size_t a, size_t e) {
             for (size_t m = a; m < e; ++m) {
               const size_t k = (size_t)k0 + m;
@@ -913,9 +922,12 @@ void report_many_device(otm_engine* E, int n, const char* const* reqs, const siz
                  n, rest.size(), t1 - t0, t2 - t1, t3 - t2, now_ms() - t3);
 }
 
-// (pinned[k]: body k lies in page-locked memory, e.g. a submission slab)
+// (pinned[k]: the page-locked submission slab body k lies in, or null)
 void report_many(otm_engine* E, int n, const char* const* reqs, const size_t* lens, int* codes, char** resps,
-                 size_t* resp_lens, const uint8_t* pinned = nullptr) {
+                 size_t* resp_lens, const void* const* pinned = nullptr) {
+  // the batch buffers, pinned staging and copy streams this thread creates
+  // belong on the engine's device, whatever device the calling thread is on
+  if (E->members.empty() && E->device >= 0) (void)hipSetDevice(E->device);
   if (gpu_reader(E, n)) report_many_device(E, n, reqs, lens, codes, resps, resp_lens, pinned);
   else report_many_host(E, n, reqs, lens, codes, resps, resp_lens);
 }
@@ -943,6 +955,9 @@ int async_workers(const otm_engine* E) {
 // uuid's results come back in submit order.
 void worker_loop(otm_engine* E, int wi) {
   otm_engine* ctx = wi == 0 ? E : E->actx[(size_t)wi - 1];
+  // a new thread starts on device 0: everything it creates for ctx (its
+  // streams' buffers, page-locked staging) goes on ctx's device
+  if (ctx->members.empty() && ctx->device >= 0) (void)hipSetDevice(ctx->device);
   while (true) {
     std::vector<otm_engine::Pending> batch;
     uint64_t seq;
@@ -967,11 +982,11 @@ void worker_loop(otm_engine* E, int wi) {
     std::vector<size_t> lens((size_t)n), rl((size_t)n, 0);
     std::vector<int> codes((size_t)n, 500);
     std::vector<char*> resps((size_t)n, nullptr);
-    std::vector<uint8_t> pin((size_t)n, 0);
+    std::vector<const void*> pin((size_t)n, nullptr);
     for (int k = 0; k < n; ++k) {
       reqs[(size_t)k] = batch[(size_t)k].p;
       lens[(size_t)k] = batch[(size_t)k].len;
-      pin[(size_t)k] = batch[(size_t)k].slab->pinned ? 1 : 0;
+      pin[(size_t)k] = batch[(size_t)k].slab->pinned ? batch[(size_t)k].slab.get() : nullptr;
     }
     const double tw0 = now_ms();
     try {
@@ -1026,6 +1041,53 @@ int otm_debug_py_repr(double d, char* out) { return otm::pyrepr::py_repr(d, out)
 int otm_debug_py_round3(double x, double* out) { return otm::pyrepr::py_round3(x, out) ? 1 : 0; }
 
 int otm_kmax(void) { return otm::KMAX; }
+
+// The arenas' lock-free otm_free under contention (run by
+// tests/test_host.py, and so under TSan by tests/test_sanitizers.py): per
+// round every thread cuts bodies from an arena of its own, then all threads
+// free a strided share of every thread's bodies, interleaved with plain
+// malloc'd pointers (which must never match an arena).  Returns the number of
+// arenas left LIVE afterwards (0 when every last body released its arena).
+int otm_debug_arena_stress(int threads, int rounds) {
+  if (threads < 1 || threads > 64 || rounds < 0) return -1;
+  constexpr int NB = 16;
+  std::vector<std::vector<char*>> bodies((size_t)threads, std::vector<char*>(NB, nullptr));
+  std::mutex mu;
+  std::condition_variable cv;
+  int arrived = 0;
+  uint64_t gen = 0;
+  auto barrier = [&] {
+    std::unique_lock<std::mutex> lk(mu);
+    const uint64_t g = gen;
+    if (++arrived == threads) {
+      arrived = 0;
+      ++gen;
+      cv.notify_all();
+    } else {
+      cv.wait(lk, [&] { return gen != g; });
+    }
+  };
+  std::vector<std::thread> th;
+  for (int t = 0; t < threads; ++t)
+    th.emplace_back([&, t] {
+      for (int r = 0; r < rounds; ++r) {
+        const size_t each = 64 + (size_t)((r * 7 + t * 13) % 200);
+        char* base = arena::acquire(each * NB, NB);
+        for (int k = 0; k < NB; ++k) bodies[(size_t)t][(size_t)k] = base ? base + each * (size_t)k : (char*)std::malloc(each);
+        barrier();
+        for (int q = 0; q < threads; ++q)
+          for (int k = t; k < NB; k += threads) {
+            arena::free_body(bodies[(size_t)q][(size_t)k]);
+            arena::free_body(std::malloc(each));  // a plain pointer through the same scan
+          }
+        barrier();
+      }
+    });
+  for (auto& x : th) x.join();
+  int live = 0;
+  for (int i = 0; i < arena::SLOTS; ++i) live += arena::g_slot[i].state.load() == arena::LIVE ? 1 : 0;
+  return live;
+}
 
 const char* otm_runtime_info(void) {
   static thread_local std::string info;
@@ -1480,27 +1542,11 @@ int otm_poll(otm_engine* E, otm_result* out, int max, int timeout_us) {
 
 int otm_encode_request(const char* uuid, int n, const float* lat, const float* lon, const int64_t* time,
                        const int32_t* accuracy, char** out, size_t* out_len) {
-  // Batch.java:52-61 + Point.java:39-45
+  if (!uuid || n < 0 || !out || (n > 0 && (!lat || !lon || !time || !accuracy))) return fail(OTM_EINVAL, "bad arguments");
+  // Batch.java:52-61 + Point.java:39-45, then StringEntity's ISO-8859-1
+  // (HttpClient.java:26): the uuid is the record key, given here as UTF-8
   std::string s;
-  s.reserve(9 + std::strlen(uuid) + 11 + (size_t)n * 72 + 2);
-  s.append("{\"uuid\":\"");
-  s.append(uuid);
-  s.append("\",\"trace\":[");
-  for (int k = 0; k < n; ++k) {
-    s.append("{\"lat\":");
-    otm::java_decimal6(lat[k], &s);
-    s.append(",\"lon\":");
-    otm::java_decimal6(lon[k], &s);
-    s.append(",\"time\":");
-    otm::json::put_int(time[k], &s);
-    s.append(",\"accuracy\":");
-    otm::json::put_int(accuracy[k], &s);
-    s.append("},");
-  }
-  // sb.replace(len-1, len+1, "]}"): the trailing ',' becomes "]}"; with no
-  // points the '[' itself is replaced (Batch.java:60)
-  s.pop_back();
-  s.append("]}");
+  otm::encode_request(otm::jstr::key_on_wire(uuid), n, lat, lon, time, accuracy, &s);
   *out = dup_out(s, out_len);
   return OTM_OK;
 }

@@ -44,6 +44,7 @@
 #include <vector>
 
 #include "engine.h"
+#include "javastr.h"
 #include "json.h"
 #include "report.h"
 
@@ -140,7 +141,9 @@ struct Op {
 };
 
 struct KeyState {
-  std::string key;
+  std::string key;   // the key as StringSerializer writes it (javastr.h kafka_key)
+  std::string wire;  // the key inside the /report body as HttpClient sends it (ISO-8859-1)
+  bool plain = true; // that body parses as the binary path reads it (javastr.h wire_key_plain)
   JBatch batch;
   bool in_store = false;
   uint32_t ob = 0, oe = 0;  // pending operations: otm_batcher::ops[ob, oe)
@@ -286,13 +289,17 @@ struct otm_batcher {
 
 namespace {
 
+// k: a canonical key (kafka_key applied)
 uint32_t key_id(otm_batcher* B, const char* k, size_t n) {
   auto it = B->index.find(std::string_view(k, n));
   if (it != B->index.end()) return it->second;
   const uint32_t id = (uint32_t)B->keys.size();
   B->key_text.emplace_back(k, n);
   B->keys.emplace_back();
-  B->keys.back().key = B->key_text.back();
+  KeyState& ks = B->keys.back();
+  ks.key = B->key_text.back();
+  ks.wire = otm::jstr::key_on_wire(ks.key);
+  ks.plain = otm::jstr::wire_key_plain(ks.wire);
   B->index.emplace(std::string_view(B->key_text.back()), id);
   return id;
 }
@@ -588,11 +595,7 @@ int issue_json(otm_batcher* B, size_t r0, size_t r1) {
         tm.push_back(p.time);
         ac.push_back(p.acc);
       }
-      char* body = nullptr;
-      size_t blen = 0;
-      otm_encode_request(ks.key.c_str(), (int)la.size(), la.data(), lo.data(), tm.data(), ac.data(), &body, &blen);
-      B->reqs[i].body.assign(body, blen);
-      otm_free(body);
+      otm::encode_request(ks.wire, (int)la.size(), la.data(), lo.data(), tm.data(), ac.data(), &B->reqs[i].body);
       rp[i - r0] = B->reqs[i].body.data();
       rl[i - r0] = B->reqs[i].body.size();
     }
@@ -706,7 +709,20 @@ int drain(otm_batcher* B) {
       for (size_t i = r0; i < r1; ++i) B->st.request_points += B->reqs[i].npts;
       B->st.requests += (int64_t)(r1 - r0);
       B->st.match_batches++;
-      int rc = (B->fn || B->cfg.json_path) ? issue_json(B, r0, r1) : issue_binary(B, r0, r1);
+      int rc;
+      if (B->fn || B->cfg.json_path) {
+        rc = issue_json(B, r0, r1);
+      } else {
+        // keys whose body the service would not read as the binary path does
+        // (a Latin-1 byte that breaks body.decode('utf-8'), a quote, a
+        // backslash, a control character) take the byte-level path, which
+        // answers them exactly (their 400s included)
+        auto mid = std::stable_partition(B->reqs.begin() + (ptrdiff_t)r0, B->reqs.begin() + (ptrdiff_t)r1,
+                                         [&](const Request& q) { return B->keys[q.key].plain; });
+        const size_t m = (size_t)(mid - B->reqs.begin());
+        rc = m > r0 ? issue_binary(B, r0, m) : OTM_OK;
+        if (!rc && r1 > m) rc = issue_json(B, m, r1);
+      }
       if (rc) return rc;
     }
     B->reqs.clear();
@@ -758,8 +774,25 @@ static int otm_batcher_process_impl(otm_batcher* B, int n, const char* const* ke
                         const float* lon, const int32_t* accuracy, const int64_t* time, const int64_t* ts_ms) {
   if (!B || n < 0) return OTM_EINVAL;
   const int64_t t0 = now_us();
+  // keys as the Java host holds them: StringDeserializer then StringSerializer
+  // (javastr.h); only a key with a byte >= 0x80 can change
+  std::vector<std::string> canon;
+  std::vector<int32_t> canon_at;
+  for (int i = 0; i < n; ++i) {
+    std::string c;
+    if (otm::jstr::kafka_key(std::string_view(keys[i], key_lens[i]), &c)) {
+      if (canon_at.empty()) canon_at.assign((size_t)n, -1);
+      canon_at[(size_t)i] = (int32_t)canon.size();
+      canon.push_back(std::move(c));
+    }
+  }
   std::vector<uint32_t> ids;
-  key_ids(B, (size_t)n, [&](size_t i) { return std::string_view(keys[i], key_lens[i]); }, &ids);
+  key_ids(B, (size_t)n,
+          [&](size_t i) {
+            if (!canon_at.empty() && canon_at[i] >= 0) return std::string_view(canon[(size_t)canon_at[i]]);
+            return std::string_view(keys[i], key_lens[i]);
+          },
+          &ids);
   for (int i = 0; i < n; ++i) ingest(B, ids[(size_t)i], JPoint{lat[i], lon[i], accuracy[i], time[i]}, ts_ms[i]);
   B->st.us_enqueue += now_us() - t0;
   if (B->cfg.max_pending > 0 && (int64_t)B->log.size() > B->cfg.max_pending) return drain(B);
@@ -811,7 +844,8 @@ static int otm_batcher_close_impl(otm_batcher* B) {
   std::vector<uint32_t> ks;
   for (uint32_t k = 0; k < (uint32_t)B->keys.size(); ++k)
     if (B->keys[k].in_store) ks.push_back(k);
-  std::sort(ks.begin(), ks.end(), [&](uint32_t a, uint32_t b) { return B->keys[a].key < B->keys[b].key; });
+  std::sort(ks.begin(), ks.end(),
+            [&](uint32_t a, uint32_t b) { return otm::jstr::compare(B->keys[a].key, B->keys[b].key) < 0; });
   for (uint32_t k : ks) {
     Op c{};
     c.kind = OP_CLOSE;
@@ -854,7 +888,9 @@ int otm_batcher_get_stats(const otm_batcher* B, otm_batcher_stats* s) {
 int otm_batcher_batch(const otm_batcher* B, const char* key, size_t key_len, int max, float* lat, float* lon,
                       int32_t* accuracy, int64_t* time, float* max_separation) {
   if (!B || !key) return OTM_EINVAL;
-  auto it = B->index.find(std::string_view(key, key_len));
+  std::string canon;
+  auto it = otm::jstr::kafka_key(std::string_view(key, key_len), &canon) ? B->index.find(canon)
+                                                                          : B->index.find(std::string_view(key, key_len));
   if (it == B->index.end() || !B->keys[it->second].in_store) return -1;
   const JBatch& b = B->keys[it->second].batch;
   const int n = (int)b.pts.size();

@@ -1,5 +1,6 @@
 // engine.h -- the otm_engine: one GPU, its HBM-resident graph, batch buffers.
 #pragma once
+#include <atomic>
 #include <hip/hip_runtime.h>
 
 #include <condition_variable>
@@ -37,7 +38,7 @@ struct otm_engine {
   std::vector<otm_report_rec> g_reps;
   std::vector<int64_t> g_ways;
   int device = 0;
-  int n_clones = 0;  // clones made of this engine (their stream slots)
+  std::atomic<int> n_clones{0};  // clones made of this engine (their stream slots; clones race with the async start)
   hipStream_t stream = nullptr;
   hipEvent_t sync_ev = nullptr;  // blocking-sync event of large batches' host waits
   bool spin_waits = false;       // otm_match_device in progress: spin-wait (engine.cpp wait_batch)

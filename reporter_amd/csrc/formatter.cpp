@@ -10,6 +10,7 @@
 #include <thread>
 
 #include "json.h"
+#include "javastr.h"
 #include "otmatch.h"
 
 namespace otm {
@@ -42,68 +43,12 @@ size_t decode_cp(std::string_view s, size_t i, uint32_t* cp) {
   return (size_t)n;
 }
 
-void put_cp(uint32_t cp, std::string* o) {
-  if (cp < 0x80) {
-    o->push_back((char)cp);
-  } else if (cp < 0x800) {
-    o->push_back((char)(0xC0 | (cp >> 6)));
-    o->push_back((char)(0x80 | (cp & 0x3F)));
-  } else if (cp < 0x10000) {
-    o->push_back((char)(0xE0 | (cp >> 12)));
-    o->push_back((char)(0x80 | ((cp >> 6) & 0x3F)));
-    o->push_back((char)(0x80 | (cp & 0x3F)));
-  } else {
-    o->push_back((char)(0xF0 | (cp >> 18)));
-    o->push_back((char)(0x80 | ((cp >> 12) & 0x3F)));
-    o->push_back((char)(0x80 | ((cp >> 6) & 0x3F)));
-    o->push_back((char)(0x80 | (cp & 0x3F)));
-  }
-}
-
-// Kafka's StringDeserializer: new String(bytes, UTF_8), each maximal
-// ill-formed subsequence replaced by U+FFFD.  Returns false (and leaves *out
+// Kafka's StringDeserializer: new String(bytes, UTF_8) of JDK 8, malformed
+// input replaced by U+FFFD (javastr.h).  Returns false (and leaves *out
 // alone) when the bytes are already well-formed, the common case.
 bool utf8_sanitize(std::string_view s, std::string* out) {
   if (json::utf8_error(s).empty()) return false;
-  out->clear();
-  size_t i = 0;
-  const size_t n = s.size();
-  while (i < n) {
-    const unsigned char c = (unsigned char)s[i];
-    if (c < 0x80) {
-      out->push_back((char)c);
-      ++i;
-      continue;
-    }
-    int need;
-    unsigned char lo = 0x80, hi = 0xBF;
-    if (c >= 0xC2 && c <= 0xDF) need = 1;
-    else if (c >= 0xE0 && c <= 0xEF) {
-      need = 2;
-      if (c == 0xE0) lo = 0xA0;
-      if (c == 0xED) hi = 0x9F;
-    } else if (c >= 0xF0 && c <= 0xF4) {
-      need = 3;
-      if (c == 0xF0) lo = 0x90;
-      if (c == 0xF4) hi = 0x8F;
-    } else {
-      put_cp(0xFFFD, out);
-      ++i;
-      continue;
-    }
-    size_t k = i + 1;
-    int got = 0;
-    while (got < need && k < n) {
-      const unsigned char d = (unsigned char)s[k];
-      const unsigned char l = got == 0 ? lo : 0x80, h = got == 0 ? hi : 0xBF;
-      if (d < l || d > h) break;
-      ++k;
-      ++got;
-    }
-    if (got == need) out->append(s.substr(i, k - i));
-    else put_cp(0xFFFD, out);
-    i = k;
-  }
+  *out = jstr::utf8_encode(jstr::utf8_decode(s));
   return true;
 }
 
@@ -1187,6 +1132,10 @@ bool Formatter::format_json(std::string_view msg, std::string* key, FormattedPoi
   pt->time = time;
   pt->accuracy = java_d2i(std::ceil(as_double(*av)));
   *key = as_text(*uv);
+  // the key goes out through StringSerializer: an unpaired surrogate (a lone
+  // \uD800 escape, which Jackson keeps) is written as '?'
+  std::string k2;
+  if (jstr::wtf8_key(*key, &k2)) key->swap(k2);
   return true;
 }
 

@@ -63,6 +63,31 @@ void java_decimal6(float f, std::string* o) {
   o->append(mag);
 }
 
+void encode_request(std::string_view wire_uuid, int n, const float* lat, const float* lon, const int64_t* time,
+                    const int32_t* accuracy, std::string* out) {
+  std::string& s = *out;
+  s.clear();
+  s.reserve(9 + wire_uuid.size() + 11 + (size_t)n * 72 + 2);
+  s.append("{\"uuid\":\"");
+  s.append(wire_uuid);  // unescaped, as sb.append(key) (Batch.java:55)
+  s.append("\",\"trace\":[");
+  for (int k = 0; k < n; ++k) {
+    s.append("{\"lat\":");
+    java_decimal6(lat[k], &s);
+    s.append(",\"lon\":");
+    java_decimal6(lon[k], &s);
+    s.append(",\"time\":");
+    json::put_int(time[k], &s);
+    s.append(",\"accuracy\":");
+    json::put_int(accuracy[k], &s);
+    s.append("},");
+  }
+  // sb.replace(len-1, len+1, "]}"): the trailing ',' becomes "]}"; with no
+  // points the '[' itself is replaced (Batch.java:60)
+  s.pop_back();
+  s.append("]}");
+}
+
 std::string error_body(const std::string& msg) { return "{\"error\":\"" + msg + "\"}"; }
 
 const char* trace_error_text(int kind) {

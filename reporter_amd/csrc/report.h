@@ -52,5 +52,9 @@ std::string error_body(const std::string& msg);
 
 // Java DecimalFormat("###.######") of a float (Point.java:29,41-42)
 void java_decimal6(float f, std::string* o);
+// Batch.report's body (Batch.java:52-61, Point.java:39-45) with the uuid
+// given as its bytes on the wire (javastr.h key_on_wire); *out is replaced
+void encode_request(std::string_view wire_uuid, int n, const float* lat, const float* lon, const int64_t* time,
+                    const int32_t* accuracy, std::string* out);
 
 }  // namespace otm

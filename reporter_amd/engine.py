@@ -310,14 +310,17 @@ def report_segments(body, match_output, engine=None):
 
 
 def encode_request(uuid, lat, lon, time, accuracy):
-    """The Java batcher's request bytes (Batch.java:52-61, Point.java:39-45)."""
+    """The Java batcher's request bytes (Batch.java:52-61, Point.java:39-45) as
+    HttpClient.POST sends them (ISO-8859-1, HttpClient.java:26).  uuid: the
+    record key, a str or its UTF-8 bytes."""
     lat = np.ascontiguousarray(lat, dtype=np.float32)
     lon = np.ascontiguousarray(lon, dtype=np.float32)
     tm = np.ascontiguousarray(time, dtype=np.int64)
     acc = np.ascontiguousarray(accuracy, dtype=np.int32)
     out = C.c_void_p()
     n = C.c_size_t()
-    _check(lib().otm_encode_request(uuid.encode("utf-8"), len(lat), lat.ctypes.data, lon.ctypes.data,
+    ub = uuid if isinstance(uuid, bytes) else uuid.encode("utf-8")
+    _check(lib().otm_encode_request(ub, len(lat), lat.ctypes.data, lon.ctypes.data,
                                     tm.ctypes.data, acc.ctypes.data, C.byref(out), C.byref(n)))
     return take(out, n.value)
 

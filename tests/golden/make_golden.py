@@ -13,6 +13,11 @@ its input/output behaviour as JSON data under tests/golden/:
   request_cases.json  -- the HTTP-level error contract of parse_trace /
                          handle_request (:85-106, :218-240) for malformed bodies.
   env_cases.json      -- make_thread_locals' env parsing quirks (:55-62).
+  transport_cases.json -- the /report bytes of Java keys (uuids) outside
+                         ASCII, as HttpClient.POST sends them (StringEntity's
+                         ISO-8859-1, HttpClient.java:26; '?' above U+00FF), and
+                         the reference's answer to those bytes
+                         (body.decode('utf-8') at :99, then :218-240).
   decode_cases.json   -- generate_test_trace.decode (py/generate_test_trace.py:9-29)
   synth_cases.json    -- generate_test_trace.synthesize_gps (:31-73), stddev=0,
                          wall clock pinned.
@@ -341,6 +346,84 @@ def make_env_cases(mod):
     return out
 
 
+# ---------------------------------------------------------------- transport (HttpClient charsets)
+# (coordinates exact in float32, so the Java batcher writes exactly this text)
+TRANSPORT_TRACE = ('{"lat":14.5,"lon":121.25,"time":1000,"accuracy":5},'
+                   '{"lat":14.5,"lon":121.5,"time":1010,"accuracy":5}')
+# Java Strings as UTF-16 code units (a lone surrogate included)
+TRANSPORT_KEYS = [
+    ("latin1_e_acute", [0xE9]),
+    ("latin1_two", [0x61, 0xE9, 0xE8]),
+    ("latin1_y_diaeresis", [0xFF]),
+    ("latin1_trailing_lead_byte", [0x78, 0xC3]),
+    ("latin1_pair_forms_utf8", [0xC3, 0xA9]),            # "Ã©" -> C3 A9 = UTF-8 for U+00E9
+    ("latin1_four_forms_utf8", [0xF0, 0x9F, 0x98, 0x80]),  # -> F0 9F 98 80 = UTF-8 for U+1F600
+    ("latin1_forms_surrogate", [0xED, 0xA0, 0x80]),      # -> ED A0 80: Python rejects surrogates
+    ("latin1_nbsp", [0xA0]),
+    ("cjk", [0x65E5, 0x672C]),                           # -> "??"
+    ("supplementary", [0x61, 0xD83D, 0xDE00, 0x62]),     # a surrogate pair -> one '?'
+    ("lone_high_surrogate", [0xD800, 0x61]),
+    ("lone_low_surrogate", [0x61, 0xDC00]),
+    ("replacement_char", [0xFFFD]),
+    ("mixed", [0x75, 0x2D, 0x65E5, 0xE9]),
+    ("quote", [0x61, 0x22, 0x62]),                        # sb.append(key) is unescaped (Batch.java:55)
+    ("backslash", [0x61, 0x5C, 0x62]),
+    ("backslash_u", [0x5C, 0x75, 0x30, 0x30, 0x65, 0x39]),
+    ("control", [0x61, 0x01]),
+    ("delete", [0x7F]),
+    ("ascii", [0x76, 0x65, 0x68, 0x30, 0x31]),
+]
+
+
+def java_latin1(units):
+    """String.getBytes(ISO_8859_1) on UTF-16 code units (JDK 8 REPLACE): a
+    unit above U+00FF becomes '?', a high+low surrogate pair one '?'."""
+    out = bytearray()
+    i = 0
+    while i < len(units):
+        u = units[i]
+        if u <= 0xFF:
+            out.append(u)
+        else:
+            if 0xD800 <= u <= 0xDBFF and i + 1 < len(units) and 0xDC00 <= units[i + 1] <= 0xDFFF:
+                i += 1
+            out.append(0x3F)
+        i += 1
+    return bytes(out)
+
+
+def java_utf8(units):
+    """String.getBytes(UTF_8) (Kafka's StringSerializer): the record key's
+    bytes on the formatted topic; an unpaired surrogate becomes '?'."""
+    out = bytearray()
+    i = 0
+    while i < len(units):
+        u = units[i]
+        if 0xD800 <= u <= 0xDBFF and i + 1 < len(units) and 0xDC00 <= units[i + 1] <= 0xDFFF:
+            out += chr(0x10000 + ((u - 0xD800) << 10) + (units[i + 1] - 0xDC00)).encode("utf-8")
+            i += 2
+            continue
+        out += b"?" if 0xD800 <= u <= 0xDFFF else chr(u).encode("utf-8")
+        i += 1
+    return bytes(out)
+
+
+def make_transport_cases(mod):
+    set_env({})
+    init_thread_locals(mod)
+    _StubMatcher.canned = '{"segments":[]}'
+    cases = []
+    for name, units in TRANSPORT_KEYS:
+        key_wire = java_latin1(units)
+        body = b'{"uuid":"' + key_wire + b'","trace":[' + TRANSPORT_TRACE.encode() + b"]}"
+        _StubMatcher.last_input = None
+        code, resp, err = run_handler(mod, body)
+        cases.append({"name": name, "key_utf16": units, "key_utf8_hex": java_utf8(units).hex(),
+                      "body_hex": body.hex(), "code": code, "response": resp,
+                      "match_input": _StubMatcher.last_input})
+    return cases
+
+
 # ---------------------------------------------------------------- decode / synthesize_gps
 def encode_polyline6(coords_lonlat):
     """Test-side encoder (Google polyline algorithm, precision 1e6) used only
@@ -416,6 +499,7 @@ def main():
     dump("report_cases.json", make_report_cases(mod))
     dump("request_cases.json", make_request_cases(mod))
     dump("env_cases.json", make_env_cases(mod))
+    dump("transport_cases.json", make_transport_cases(mod))
     gtt = load_generate_test_trace()
     dump("decode_cases.json", make_decode_cases(gtt))
     dump("synth_cases.json", make_synth_cases(gtt))

@@ -102,6 +102,8 @@ def sv_corpus(rng, n, sep, dated):
             msg += sep * rng.randint(1, 3)
         if rng.random() < 0.03:
             msg = msg.encode("utf-8") + b"\xff\xfe"
+        elif rng.random() < 0.03:  # an encoded surrogate: one U+FFFD in JDK 8, three in Python's 'replace'
+            msg = b"\xed\xa0\x80" + msg.encode("utf-8") + b"\xed\xa0"
         msgs.append(msg)
     return msgs
 
@@ -121,7 +123,7 @@ def json_value(rng, kind):
     if kind == "date":
         return '"%s"' % rng.choice(DATES) if r < 0.8 else rng.choice(["1495037969", "null"])
     if kind == "key":
-        return rng.choice(['"uuid_abcdef"', '"\\u00fcn\\u00efc\\ud83d\\ude00"', "12345", "1.5", "1e21", "true",
+        return rng.choice(['"uuid_abcdef"', '"\\u00fcn\\u00efc\\ud83d\\ude00"', '"\\ud800x\\udc00"', "12345", "1.5", "1e21", "true",
                            "null", "{}", '""', "1.0E-5", "100", "0.001"])
     raise ValueError(kind)
 

@@ -34,3 +34,35 @@ def test_gpu_batcher_on_multi_device_engine(small_graph, json_path):
         nb = run_native(recs, Batcher(engine=grp, json_path=json_path, threads=4))
         st = compare(bp, nb, recs)
         assert st["forwarded"] > 10
+
+
+@pytest.mark.parametrize("json_path,threads", [(False, 0), (True, 0), (False, 4)],
+                         ids=["binary", "json", "binary_threads"])
+def test_gpu_batcher_exotic_keys(small_graph, json_path, threads):
+    """Keys outside ASCII (HttpClient's ISO-8859-1 body, HttpClient.java:26): in
+    binary mode a key whose body the service would reject or read differently
+    takes the byte-level path; forwarded records (the 400 bodies among them),
+    counts and stored batches equal the serial restatement's."""
+    from test_transport import check_exotic_keys
+    with Engine(graph_path=small_graph) as eng:
+        check_exotic_keys(small_graph, lambda body: eng.report(body)[1],
+                          Batcher(engine=eng, json_path=json_path, threads=threads))
+
+
+def test_gpu_report_transport_bodies(small_graph, oracle):
+    """The reference-recorded transport cases through otm_report and
+    otm_report_batch (40 bodies: the GPU request reader takes the batch and
+    hands non-ASCII uuids to the host readers): the 400 bodies are the
+    reference's own, the 200 bodies the oracle's."""
+    from test_transport import CASES
+    g = oracle.Graph(small_graph)
+    bodies = [bytes.fromhex(c["body_hex"]) for c in CASES] * 2
+    want = []
+    for c, b in zip(CASES * 2, bodies):
+        w = oracle.handle_request(g, b)
+        if c["code"] != 200:
+            assert w == (c["code"], c["response"])
+        want.append(w)
+    with Engine(graph_path=small_graph) as eng:
+        assert [eng.report(b) for b in bodies[:len(CASES)]] == want[:len(CASES)]
+        assert eng.report_batch(bodies) == want

@@ -353,3 +353,33 @@ def test_valhalla_module_shim(small_graph, oracle, tmp_path):
         assert code == 200 and m.Match(body.decode()) == want
     with pytest.raises(RuntimeError):
         m.Match('{"uuid":"x","trace":[{"lat":1}]}')
+
+
+def _gpu_count():
+    import torch
+    return torch.cuda.device_count()
+
+
+@pytest.mark.skipif(_gpu_count() < 2, reason="needs a second GPU (the gpurun box has one; the driver's node has 8)")
+def test_engine_on_device_1_json_and_async(small_graph):
+    """An engine on device 1: otm_report_batch and the async
+    workers (new host threads, which start on device 0) create their buffers,
+    page-locked staging and copy streams on the engine's device; answers
+    byte-equal to a device-0 engine's."""
+    from reporter_amd import encode_request
+    b = synth.make_traces(small_graph, 80, 30, seed=97)
+    bodies = []
+    for t in range(80):
+        a, e = b["trace_off"][t], b["trace_off"][t + 1]
+        bodies.append(encode_request("veh%d" % t, b["lat"][a:e], b["lon"][a:e], b["time"][a:e].astype(np.int64),
+                                     b["accuracy"][a:e].astype(np.int32)))
+    with Engine(graph_path=small_graph, device=0) as e0:
+        want = e0.report_batch(bodies)
+    with Engine(graph_path=small_graph, device=1) as e1:
+        assert e1.report_batch(bodies) == want
+        tags = list(range(len(bodies)))
+        e1.submit_batch(bodies, tags)
+        polled = []
+        while len(polled) < len(tags):
+            polled += e1.poll(4096, 2000000)
+        assert sorted((t, c, s) for t, c, s in polled) == [(t, want[t][0], want[t][1]) for t in tags]

@@ -237,3 +237,14 @@ def test_null_engine_request_calls_fail_cleanly():
     body = b'{"uuid":"a","trace":[]}'
     assert L.otm_report(None, body, len(body), C.byref(out), C.byref(n)) < 0
     assert L.otm_match_json(None, body, len(body), C.byref(out), C.byref(n)) < 0
+
+
+def test_arena_free_under_contention():
+    """otm_free's lock-free arena scan while other threads release arenas and
+    free plain pointers: every arena is released by its last body
+    and no plain pointer is taken for an arena body (this also runs under
+    TSan in tests/test_sanitizers.py)."""
+    from reporter_amd._lib import lib
+    assert lib().otm_debug_arena_stress(8, 200) == 0
+    assert lib().otm_debug_arena_stress(3, 50) == 0
+    assert lib().otm_debug_arena_stress(0, 1) == -1

@@ -21,7 +21,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ASAN_LIB = os.path.join(ROOT, "reporter_amd", "lib", "asan", "libotmatch.so")
 ASAN_ORACLE = os.path.join(ROOT, "oracle", "build", "asan", "libotm_oracle.so")
 MODULES = ["tests/test_golden.py", "tests/test_host.py", "tests/test_formatter.py", "tests/test_batcher.py",
-           "tests/test_tiles.py", "tests/test_fast_request.py"]
+           "tests/test_tiles.py", "tests/test_fast_request.py", "tests/test_transport.py"]
 
 
 def _runtime():

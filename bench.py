@@ -19,7 +19,7 @@ the launch stream.  The line's `roofline` object is the dominant kernel's.
 
 `--config 4` measures BASELINE's config 4 the same way instead (state-scale
 highway graph, 100k vehicles x 100 probes, 30 s sampling, sigma 50 m,
-radius 100 m), and `--config 3` one GPU's uuid shard of config 3 (100 x 100 km
+radius 200 m), and `--config 3` one GPU's uuid shard of config 3 (100 x 100 km
 metro graph, 125k vehicles x 100 probes = 12.5M points per GPU): secondary
 lines, not the headline.
 
@@ -52,7 +52,7 @@ WORKLOAD = {
     3: ("100x100 km metro", "config3-metro shard: %d vehicles x %d GPS points per GPU (%d points; 1M vehicles over "
                             "8 GPUs), 5 s, sigma 15 m, accuracy 15 m, radius 50 m, uuid-sharded"),
     4: ("500x500 km highway-heavy state", "config4-state: %d vehicles x %d GPS points per GPU (%d points), 30 s, "
-                                          "sigma 50 m, accuracy 50 m, radius 100 m, uuid-sharded"),
+                                          "sigma 50 m, accuracy 50 m, radius 200 m, uuid-sharded"),
 }
 
 # kernel -> (stage, main tier of the stage?)
@@ -553,13 +553,28 @@ def main():
         tr_args["points_per_vehicle"] = args.points
         tr_args.pop("n_vehicles", None)
         poff, pedges = synth.true_paths(graph, len(ids), vehicle_ids=ids, **tr_args)
-        truth_gpu = synth.segment_agreement(graph, poff, pedges, res)
+        outlier = synth.outlier_points(graph, batch["true_edge"], orc["ncand"], orc["cand_edge"], orc["cand_off"],
+                                       batch["trace_off"], orc["gc"])
+        truth_gpu = synth.segment_agreement(graph, poff, pedges, res, trace_off=batch["trace_off"], outlier=outlier)
+        bd = truth_gpu["breakdown"]
         agreement = {"segment_id_sequences_equal_vs_oracle": seq_eq / float(max(nt, 1)), "traces": nt,
                      "all_outputs_bit_identical": bool(same),
                      "vs_ground_truth": {"segment_id_agreement": truth_gpu["segment_id_agreement"],
                                          "sequences_exact": truth_gpu["sequences_exact"],
+                                         "interior_agreement": bd["interior_agreement"],
+                                         "interior_agreement_outside_outliers":
+                                             bd["interior_agreement_outside_outliers"],
+                                         "end_share": bd["end_share"],
+                                         "driven_segments": bd["driven_segments"],
+                                         "errors": {k: bd[k] for k in synth.ERROR_CLASSES},
+                                         "outlier_columns": bd["outlier_points"],
                                          "what": "per trace, the OSMLR segment-id sequence the synthetic vehicle "
-                                                 "drove vs the matched one: sum of LCS / sum of max length"},
+                                                 "drove vs the matched one: sum of LCS / sum of max length; "
+                                                 "errors by class (synth.classify_sequences): start/end partial "
+                                                 "segments, interior ones (inserted_outlier: over a column whose "
+                                                 "road had no candidate within the search radius); "
+                                                 "interior_agreement = 1 - interior errors / driven segments, "
+                                                 "end_share = start/end errors / all errors (DESIGN.md 3.2)"},
                      "meili": "unavailable (parity vs meili unpinned)"}
         sbytes = stage_bytes(orc["counters"], orc["ncand"], orc["col_prev"], P)
         probe_bytes = index_probe_bytes(orc["ncand"], orc["col_prev"], orc["cand_edge"], orc["cand_off"])

@@ -529,6 +529,19 @@ static unsigned src_hin(const orc_graph* g, int32_t e, float off) { return off =
 static uint32_t turn_cost_units(const batch* B, unsigned hin, unsigned hout) {
   return (hin == NO_HEAD || hout == NO_HEAD) ? 0u : B->turn_units[orc_turn_deg(hin, hout)];
 }
+/* Rule 4's same-edge step from (e, oi) to (e, oj): the route along the edge
+ * when oj is not before oi; when oj is behind oi and both are edge
+ * candidates, a stay: GPS noise moved the later probe back along the edge
+ * (vehicles do not reverse along a directed edge), so the step has route
+ * distance 0, no turns and no traversal, and the position on the edge stays
+ * at the largest offset reached.  (A backward step otherwise needs a loop
+ * around the block, or a U-turn onto the opposite edge and back, which the
+ * matched segments then show: VERDICT r3 #2) */
+static int same_edge_step(int32_t ei, float oi, int32_t ej, float oj) {
+  return ei == ej && (oj >= oi || (oj > 0.0f && oi > 0.0f));
+}
+static float same_edge_dist(float oi, float oj) { return oj >= oi ? oj - oi : 0.0f; }
+
 /* the cost bound of a search bounded by B metres */
 static uint32_t cost_bound(float B) { return (uint32_t)floor((double)B * 64.0); }
 
@@ -688,8 +701,8 @@ static int transitions(batch* B, ws* w, int64_t p, orc_counters* C) {
       for (int j = 0; j < Kp; ++j) {
         float r;
         uint32_t units = 0;
-        if (ep[j] == eq[i] && op[j] >= oq[i]) {
-          r = op[j] - oq[i];
+        if (same_edge_step(eq[i], oq[i], ep[j], op[j])) {
+          r = same_edge_dist(oq[i], op[j]);
         } else {
           float d;
           int n;
@@ -877,9 +890,9 @@ static int route_step(batch* B, ws* w, int64_t p, int32_t* path, int pcap, int* 
   const int32_t ei = B->cand_edge[q * ORC_KMAX + i], ej = B->cand_edge[p * ORC_KMAX + j];
   const float oi = B->cand_off[q * ORC_KMAX + i], oj = B->cand_off[p * ORC_KMAX + j];
   *plen = 0;
-  if (ei == ej && oj >= oi) {
+  if (same_edge_step(ei, oi, ej, oj)) {
     *same = 1;
-    *R = oj - oi;
+    *R = same_edge_dist(oi, oj);
     return 0;
   }
   *same = 0;
@@ -1017,6 +1030,7 @@ static int segments_of_trace(batch* B, ws* w, int32_t t, tres* R, orc_counters* 
   trav cur = {0};
   int64_t lastp = -1;
   int rc = 0;
+  float curmax = 0.0f; /* the open traversal's largest state offset */
   for (int64_t p = a; p <= b; ++p) {
     const int is_state = p < b && B->is_col[p] && B->state[p] >= 0;
     if (p < b && !is_state) continue;
@@ -1024,8 +1038,7 @@ static int segments_of_trace(batch* B, ws* w, int32_t t, tres* R, orc_counters* 
     if (open && new_chain) {
       /* close the open chain; a chain ending on a node candidate ends at the
          node: the traversal opened there never left it */
-      const int32_t sl = B->state[lastp];
-      cur.off1 = B->cand_off[lastp * ORC_KMAX + sl];
+      cur.off1 = curmax; /* the largest offset of the open traversal's states (rule 4's stays) */
       cur.t1 = B->time[lastp];
       cur.sh1 = (int32_t)(lastp - a);
       if (cur.off1 != 0.0f) tpush(&T, cur);
@@ -1042,6 +1055,7 @@ static int segments_of_trace(batch* B, ws* w, int32_t t, tres* R, orc_counters* 
       cur.off0 = oj;
       cur.t0 = B->time[p];
       cur.sh0 = (int32_t)(p - a);
+      curmax = oj;
       open = 1;
       nstate = 1;
       lastp = p;
@@ -1088,6 +1102,9 @@ static int segments_of_trace(batch* B, ws* w, int32_t t, tres* R, orc_counters* 
       cur.edge = ej;
       cur.off0 = 0.0f;
       step_bound(B, a, lastp, p, Rd, x, &cur.t0, &cur.sh0);
+      curmax = oj;
+    } else if (oj > curmax) {
+      curmax = oj;
     }
     nstate++;
     lastp = p;

@@ -186,6 +186,16 @@ __device__ __forceinline__ uint32_t src_head(const DevGraph& g, int32_t e, float
 __device__ __forceinline__ uint32_t dst_head(const DevGraph& g, int32_t e, float off) {
   return cand_node(off) ? NO_HEAD : (uint32_t)g.e_head_out[e];
 }
+// DESIGN.md §3 rule 4, same edge: from (e, oi) to (e, oj) the route is along
+// the edge when oj is not before oi; when oj is behind oi and both are edge
+// candidates the step is a stay (GPS noise moved the later probe back; a
+// vehicle does not reverse along a directed edge): route distance 0, no
+// turns, no traversal, the position on the edge staying at the largest offset
+// reached.  oracle/otm_oracle.c same_edge_step / same_edge_dist.
+__device__ __forceinline__ bool same_edge_step(int32_t ei, float oi, int32_t ej, float oj) {
+  return ei == ej && (oj >= oi || (!cand_node(oj) && !cand_node(oi)));
+}
+__device__ __forceinline__ float same_edge_dist(float oi, float oj) { return oj >= oi ? oj - oi : 0.0f; }
 // turn units of one turn (none when either side is a node candidate)
 __device__ __forceinline__ uint32_t turn_units(const uint32_t* TU, uint32_t hin, uint32_t hout) {
   return (hin == NO_HEAD || hout == NO_HEAD) ? 0u : TU[turn_deg(hin, hout)];
@@ -1504,7 +1514,7 @@ __global__ __launch_bounds__(TB, 8) void k_trans_sub(DevGraph g, DevBatch b, Dev
             const int i = idx / Kp, j = idx - (idx / Kp) * Kp;
             const int4 T = tg[sg][j ^ swz], Sx = sr[sg][i ^ swz];
             const IdxRow R = rq[sg][i ^ swz];
-            const bool same = T.x == Sx.x && __int_as_float(T.y) >= __int_as_float(Sx.y);
+            const bool same = same_edge_step(Sx.x, __int_as_float(Sx.y), T.x, __int_as_float(T.y));
             if (!same && R.cnt > 0) {
               h0[u] = idx_slot0((uint32_t)T.z, R);
               s0[u] = X.slot[R.off + h0[u]];
@@ -1523,8 +1533,8 @@ __global__ __launch_bounds__(TB, 8) void k_trans_sub(DevGraph g, DevBatch b, Dev
           float r = 0.0f;
           bool ok = true;
           uint32_t units = 0;
-          if (ej == ei && oj >= oi) {
-            r = oj - oi;
+          if (same_edge_step(ei, oi, ej, oj)) {
+            r = same_edge_dist(oi, oj);
           } else {
             const IdxRow R = rq[sg][i ^ swz];
             uint4 sv = s0[u];
@@ -1624,8 +1634,8 @@ __global__ __launch_bounds__(256, OTM_ROUTE_WAVES) void k_route_index(DevGraph g
     const int2 ci = w.chosen[q], cj = w.chosen[p];
     const int32_t ei = ci.x, ej = cj.x;
     const float oi = __int_as_float(ci.y), oj = __int_as_float(cj.y);
-    if (ei == ej && oj >= oi) {
-      w.route_dist[p] = oj - oi;
+    if (same_edge_step(ei, oi, ej, oj)) {
+      w.route_dist[p] = same_edge_dist(oi, oj);
       continue;
     }
     const float bound = P.factor * w.gc[p];
@@ -1785,8 +1795,8 @@ __global__ __launch_bounds__(TB) void k_transitions(DevGraph g, DevBatch b, DevP
         float r = 0.0f;
         uint32_t units = 0;
         bool ok = true;
-        if (ej == ei && op[j] >= oq[i]) {
-          r = op[j] - oq[i];
+        if (same_edge_step(ei, oq[i], ej, op[j])) {
+          r = same_edge_dist(oq[i], op[j]);
         } else {
           const uint32_t key = dst_key(g, ej, op[j]);
           const int slot = table_find<BIG>(T, key);
@@ -2261,8 +2271,8 @@ __global__ __launch_bounds__(TB) void k_route(DevGraph g, DevBatch b, DevParams 
     const int2 ci = w.chosen[q], cj = w.chosen[p];
     const int32_t ei = ci.x, ej = cj.x;
     const float oi = __int_as_float(ci.y), oj = __int_as_float(cj.y);
-    if (ei == ej && oj >= oi) {
-      if (lane == 0) w.route_dist[p] = oj - oi;
+    if (same_edge_step(ei, oi, ej, oj)) {
+      if (lane == 0) w.route_dist[p] = same_edge_dist(oi, oj);
       continue;
     }
     const float bound = P.factor * w.gc[p];
@@ -2509,12 +2519,13 @@ __device__ void segments_trace(const DevGraph& g, const DevWork& w, DevOut& o, i
   int nstate = 0;
   Trav cur{};
   int lastp = -1;
+  float curmax = 0.0f;
   for (int p = 0; p <= n; ++p) {
     const int st = p < n ? S.state(p) : -1;
     if (p < n && st < 0) continue;
     const bool new_chain = p == n || S.cs(p);
     if (open && new_chain) {
-      cur.off1 = S.off(lastp);
+      cur.off1 = curmax;  // the open traversal's largest state offset (rule 4's stays)
       cur.t1 = S.time(lastp);
       cur.sh1 = lastp;
       if (nstate >= 2) {
@@ -2534,6 +2545,7 @@ __device__ void segments_trace(const DevGraph& g, const DevWork& w, DevOut& o, i
       cur.off0 = oj;
       cur.t0 = S.time(p);
       cur.sh0 = p;
+      curmax = oj;
       open = true;
       nstate = 1;
       lastp = p;
@@ -2544,7 +2556,7 @@ __device__ void segments_trace(const DevGraph& g, const DevWork& w, DevOut& o, i
     const int32_t ca = lastp, cb = p;
     const int32_t ei = cur.edge;
     const float oi = S.off(lastp);
-    const bool same = ei == ej && oj >= oi;
+    const bool same = same_edge_step(ei, oi, ej, oj);
     if (!same) {
       // close the traversal on the state's edge, unless the state is a node
       // candidate: its route starts at the node
@@ -2580,6 +2592,9 @@ __device__ void segments_trace(const DevGraph& g, const DevWork& w, DevOut& o, i
       cur.off0 = 0.0f;
       step_bound(*S.b, w, S.a, ca, cb, Rd, ta, tb, x, cur.t0, sh);
       cur.sh0 = sh;
+      curmax = oj;
+    } else if (oj > curmax) {
+      curmax = oj;
     }
     ++nstate;
     lastp = p;
@@ -2665,7 +2680,7 @@ __device__ __forceinline__ StateStep state_step(const DevWork& w, int64_t a, con
   const int2 ci = w.chosen[q];
   r.ei = ci.x;
   r.oi = __int_as_float(ci.y);
-  r.same = r.step && r.ei == r.ej && r.oj >= r.oi;
+  r.same = r.step && same_edge_step(r.ei, r.oi, r.ej, r.oj);
   r.plen = 0;
   r.poff = 0;
   if (r.step && !r.same) {
@@ -2823,11 +2838,18 @@ __global__ __launch_bounds__(TB) void k_segments(DevGraph g, DevBatch b, DevWork
       }
       if (r.last && !r.cs && !cand_node(r.oj)) {
         const int jo = S.lopen[k];
+        // the traversal ends at the largest offset of its states (the opener
+        // jo's and every stay after it: rule 4)
+        float omax = r.oj;
+        for (int kk = jo; kk < k; ++kk) {
+          const float o2 = __int_as_float(w.chosen[a + S.sidx[kk]].y);
+          omax = o2 > omax ? o2 : omax;
+        }
         S.t_edge[slot] = r.ej;
         S.t_off0[slot] = S.o_off0[jo];
         S.t_t0[slot] = S.o_t0[jo];
         S.t_sh0[slot] = S.o_sh0[jo];
-        S.t_off1[slot] = r.oj;
+        S.t_off1[slot] = omax;
         S.t_t1[slot] = b.time[a + r.pl];
         S.t_sh1[slot] = (int16_t)r.pl;
         S.t_chain[slot] = chk;
@@ -3238,7 +3260,7 @@ __global__ __launch_bounds__(256) void k_seg_bound(DevGraph g, DevBatch b, DevPa
       if (p >= 0 && w.col_prev[p] == q && !w.chain_start[p] && w.state[p] >= 0 && w.path_len[p] >= 0 &&
           w.trace_err[w.pt_trace[k]] == 0) {
         const int2 ci = w.chosen[q], cj = w.chosen[p];
-        if (!(ci.x == cj.x && __int_as_float(cj.y) >= __int_as_float(ci.y)))
+        if (!same_edge_step(ci.x, __int_as_float(ci.y), cj.x, __int_as_float(cj.y)))
           w.ipos[k] = interp_pos(g, b, P, w, q, p, k);
       }
     }

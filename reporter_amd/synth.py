@@ -7,7 +7,7 @@ seeded synthetic road network plus seeded probe traces:
             per edge end, stddev 0: py/generate_test_trace.py:31-73)
   config 2  city 20 x 20 km, 10k vehicles x 100 points, 5 s, sigma 15 m
   config 3  metro 100 x 100 km, 1M vehicles x 100 points (uuid-sharded)
-  config 4  state 500 x 500 km highway-heavy, 30 s, sigma 50 m, radius 100 m
+  config 4  state 500 x 500 km highway-heavy, 30 s, sigma 50 m, radius 200 m
 """
 import ctypes as C
 import os
@@ -31,7 +31,10 @@ CONFIGS = {
                        highway_every=8, complex_every=0, seg_max_m=5000),
             traces=dict(n_vehicles=100000, points_per_vehicle=100, interval_s=30.0, noise_sigma_m=50.0,
                         accuracy=50.0),
-            meili=dict(search_radius=100.0, max_search_radius=100.0)),
+            # "wide search_radius" (BASELINE config 4): 4 sigma of the 50 m noise.  At 100 m, 4.7 % of
+            # the columns had no candidate on their road and 12 % of the driven segments came out wrong
+            # around them; at 200 m 0.008 % and 0.05 % (profiles/r04_accuracy/)
+            meili=dict(search_radius=200.0, max_search_radius=200.0)),
 }
 
 
@@ -137,42 +140,181 @@ def _dedup(seq):
     return out
 
 
-def _lcs(a, b):
-    if not a or not b:
-        return 0
-    prev = [0] * (len(b) + 1)
-    for x in a:
-        cur = [0]
-        for j, y in enumerate(b):
-            cur.append(prev[j] + 1 if x == y else max(prev[j + 1], cur[j]))
-        prev = cur
-    return prev[-1]
+def _lcs_pairs(a, b):
+    """One LCS alignment of a and b as index pairs (i, j), increasing."""
+    n, m = len(a), len(b)
+    if n == 0 or m == 0:
+        return []
+    L = np.zeros((n + 1, m + 1), np.int32)
+    for i in range(n - 1, -1, -1):
+        for j in range(m - 1, -1, -1):
+            L[i, j] = L[i + 1, j + 1] + 1 if a[i] == b[j] else max(L[i + 1, j], L[i, j + 1])
+    out = []
+    i = j = 0
+    while i < n and j < m:
+        if a[i] == b[j]:
+            out.append((i, j))
+            i += 1
+            j += 1
+        elif L[i + 1, j] >= L[i, j + 1]:
+            i += 1
+        else:
+            j += 1
+    return out
 
 
-def segment_agreement(graph_path, path_off, path_edges, results):
+ERROR_CLASSES = ("start_missed", "start_extra", "end_missed", "end_extra", "dropped", "inserted_outlier",
+                 "inserted_uturn", "inserted_other", "reverse", "swap")
+INTERIOR_CLASSES = ("dropped", "inserted_outlier", "inserted_uturn", "inserted_other", "reverse", "swap")
+END_CLASSES = ("start_missed", "start_extra", "end_missed", "end_extra")
+
+
+def classify_sequences(T, G, twin, at_outlier=lambda k0, k1: False):
+    """Where a matched segment sequence G departs from the driven one T.
+
+    An LCS alignment pairs them; what it leaves unpaired is an error:
+      start_* / end_*  before the first / after the last pair: the trace's
+                       first / last partial segment, whose heading and extent
+                       the trace does not observe past its end point;
+      interior, between two pairs:
+        dropped           driven segments with nothing matched in their place
+        inserted_outlier  matched segments over points whose road had no
+                          candidate within the search radius (at_outlier(k0,
+                          k1): the points from G[k0]'s end to G[k1]'s start)
+        inserted_uturn    onto the opposite direction of a neighbouring
+                          segment and back (B, rev(B), B)
+        inserted_other    any other matched segment nothing was driven for
+        reverse           a matched segment the opposite of a driven one
+        swap              otherwise (a parallel street, another route)
+    twin: segment id -> ids of its opposite direction."""
+    c = dict((k, 0) for k in ERROR_CLASSES)
+    pairs = _lcs_pairs(T, G)
+    c.update(truth=len(T), matched=len(G), no_overlap=0, paired=len(pairs))
+    if not pairs:
+        c["no_overlap"] = 1
+        c["start_missed"] = len(T)
+        c["start_extra"] = len(G)
+        return c
+    (i0, j0), (i1, j1) = pairs[0], pairs[-1]
+    c["start_missed"], c["start_extra"] = i0, j0
+    c["end_missed"], c["end_extra"] = len(T) - 1 - i1, len(G) - 1 - j1
+    for (pa, pb), (qa, qb) in zip(pairs, pairs[1:]):
+        miss = T[pa + 1:qa]
+        extra = G[pb + 1:qb]
+        if miss and extra:
+            rev = sum(1 for x in extra if twin.get(x, set()) & set(miss))
+            c["reverse"] += rev
+            c["swap"] += max(len(miss), len(extra)) - rev
+        elif miss:
+            c["dropped"] += len(miss)
+        elif extra:
+            if at_outlier(pb, qb):
+                c["inserted_outlier"] += len(extra)
+            elif all(x in twin.get(G[pb], set()) | twin.get(G[qb], set()) | {G[pb], G[qb]} for x in extra):
+                c["inserted_uturn"] += len(extra)
+            else:
+                c["inserted_other"] += len(extra)
+    return c
+
+
+def _graph_section(graph_path, k, dtype):
+    import struct
+    raw = np.fromfile(graph_path, dtype=np.uint8)
+    hs = struct.calcsize("<8sII4i2iq3d4dQ")
+    o, n = struct.unpack_from("<QQ", raw, hs + 16 * k)
+    return np.frombuffer(raw, dtype=dtype, count=n // np.dtype(dtype).itemsize, offset=o).copy()
+
+
+def outlier_points(graph_path, true_edge, ncand, cand_edge, cand_off, trace_off, gc, kmax=32):
+    """Per point: True for an HMM column whose true edge had no candidate --
+    neither an edge candidate on it nor a node candidate at one of its end
+    nodes (the probe fell outside its road's search radius).  Candidates and
+    gc from a matcher's stage outputs (the oracle's, keep_stages=True): a
+    point is a column when it starts its trace or has gc > 0 (rule 1: an
+    interpolated point has none, a column is >= interpolation_distance from
+    the previous one)."""
+    e_from = _graph_section(graph_path, 3, np.int32)  # OTMG_EDGE_FROM
+    e_to = _graph_section(graph_path, 4, np.int32)    # OTMG_EDGE_TO
+    P = len(true_edge)
+    ce = np.asarray(cand_edge).reshape(P, kmax)
+    co = np.asarray(cand_off).reshape(P, kmax)
+    valid = np.arange(kmax)[None, :] < np.asarray(ncand)[:, None]
+    te = np.asarray(true_edge)[:, None]
+    on_edge = (ce == te) & (co > 0)
+    cf = e_from[np.clip(ce, 0, len(e_from) - 1)]
+    at_node = (co == 0) & ((cf == e_from[te]) | (cf == e_to[te]))
+    col = np.asarray(gc) > 0
+    col[np.asarray(trace_off)[:-1][np.diff(trace_off) > 0]] = True
+    return col & ~np.any(valid & (on_edge | at_node), axis=1)
+
+
+def segment_agreement(graph_path, path_off, path_edges, results, trace_off=None, outlier=None, per_trace=None):
     """Implementation-independent accuracy of a matched batch against the
     generator's ground truth: per trace the OSMLR segment-id sequence the
     vehicle drove (segments of its true edges, consecutive repeats merged)
     against the matched one (segments with an id, in order).  Returns
     {"segment_id_agreement": sum LCS / sum max(len), "sequences_exact":
-    fraction of traces whose sequences are equal, "traces": n}."""
+    fraction of traces whose sequences are equal, "traces": n, "breakdown":
+    the error classes of classify_sequences summed over traces, with
+    "interior_agreement" = 1 - interior errors / driven segments and
+    "end_share" = the start/end errors' share of all errors}.  outlier (per
+    point, outlier_points) and trace_off attribute insertions to probes
+    outside their road's radius; per_trace (a list) receives each trace's
+    classes."""
     ids = segment_ids(graph_path)
     eseg = edge_segments(graph_path)
+    eopp = _graph_section(graph_path, 13, np.int32)  # OTMG_EDGE_OPP
+    twin = {}
+    for e in np.nonzero((eseg >= 0) & (eopp >= 0))[0]:
+        o = eopp[e]
+        if eseg[o] >= 0:
+            twin.setdefault(int(ids[eseg[e]]), set()).add(int(ids[eseg[o]]))
     tr = results.traces if hasattr(results, "traces") else results["traces"]
     segs = results.segments if hasattr(results, "segments") else results["segments"]
     lcs = den = exact = 0
+    tot = dict((k, 0) for k in ERROR_CLASSES)
+    tot.update(truth=0, matched=0, no_overlap=0, paired=0)
     for t in range(len(tr)):
         e = path_edges[path_off[t]:path_off[t + 1]]
         sg = eseg[e]
         truth = _dedup(ids[sg[sg >= 0]].tolist())
         a, n = int(tr["seg_off"][t]), int(tr["seg_cnt"][t])
-        m = segs["segment_id"][a:a + n]
-        got = _dedup(m[m >= 0].astype(np.uint64).tolist())
-        lcs += _lcs(truth, got)
+        m = segs["segment_id"][a:a + n].astype(np.int64)
+        bsi = segs["begin_shape_index"][a:a + n]
+        esi = segs["end_shape_index"][a:a + n]
+        got, rng = [], []
+        for x, bi, ei in zip(m.tolist(), bsi.tolist(), esi.tolist()):
+            if x < 0:
+                continue
+            if got and got[-1] == x:
+                rng[-1][1] = ei
+            else:
+                got.append(x)
+                rng.append([bi, ei])
+        at = (lambda k0, k1: False)
+        if outlier is not None and trace_off is not None:
+            p0 = int(trace_off[t])
+            at = (lambda k0, k1, p0=p0, rng=rng: bool(outlier[p0 + rng[k0][1]:p0 + rng[k1][0] + 1].any()))
+        c = classify_sequences(truth, got, twin, at)
+        if per_trace is not None:
+            per_trace.append(c)
+        for k, v in c.items():
+            tot[k] += v
+        lcs += c["paired"]
         den += max(len(truth), len(got))
         exact += truth == got
+    interior = sum(tot[k] for k in INTERIOR_CLASSES)
+    ends = sum(tot[k] for k in END_CLASSES)
+    driven = max(tot["truth"], 1)
+    bd = dict(tot)
+    bd.update(driven_segments=tot["truth"], interior_errors=interior, end_errors=ends,
+              interior_agreement=1.0 - interior / float(driven),
+              interior_agreement_outside_outliers=1.0 - (interior - tot["inserted_outlier"]) / float(driven),
+              end_share=ends / float(max(ends + interior, 1)))
+    if outlier is not None:
+        bd["outlier_points"] = int(np.asarray(outlier).sum())
     return {"segment_id_agreement": lcs / float(max(den, 1)), "sequences_exact": exact / float(max(len(tr), 1)),
-            "traces": len(tr)}
+            "traces": len(tr), "breakdown": bd}
 
 
 def slice_batch(b, t0, t1):

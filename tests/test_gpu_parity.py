@@ -335,7 +335,10 @@ def test_interpolated_points_hand_road(tmp_path, oracle, results_equal):
     path, _ = handgraph.straight_road(str(tmp_path / "road.otmg"), lat=40.0, n_nodes=5)
     traces = [[(0.0002, 0.0), (0.00025, 1.0), (0.00022, 2.0), (0.0003, 3.0), (0.0011, 10.0), (0.0021, 20.0)],
               [(0.0005, 0.0), (0.0005, 5.0), (0.0005, 10.0), (0.0005, 15.0), (0.0015, 25.0)],
-              [(0.0002, 0.0), (0.00028, 1.0), (0.0012, 30.0), (0.0022, 40.0), (0.0032, 50.0)]]
+              [(0.0002, 0.0), (0.00028, 1.0), (0.0012, 30.0), (0.0022, 40.0), (0.0032, 50.0)],
+              # rule 4's stay: a probe behind the previous column on the same edge (test_interp.py)
+              [(0.0002, 0.0), (0.0006, 5.0), (0.00045, 10.0), (0.0009, 15.0), (0.0014, 20.0)],
+              [(0.0002, 0.0), (0.0006, 5.0), (0.00045, 10.0)]]
     lon = np.concatenate([np.array([p[0] for p in t], np.float32) for t in traces])
     tm = np.concatenate([np.array([p[1] for p in t], np.float64) for t in traces])
     off = np.concatenate([[0], np.cumsum([len(t) for t in traces])]).astype(np.int64)
@@ -346,6 +349,7 @@ def test_interpolated_points_hand_road(tmp_path, oracle, results_equal):
     assert list(s["begin_shape_index"][:3]) == [0, 3, 4]
     assert list(s["end_shape_index"][:3]) == [3, 4, 5]
     assert res.traces["shape_used"][2] == 1
+    assert res.traces["seg_cnt"][3] == 2 and res.traces["seg_cnt"][4] == 1
 
 
 def test_empty_batch(small_graph):

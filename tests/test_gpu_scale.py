@@ -7,7 +7,7 @@ splits, and the uuid shard partition of config 3.
   config 3  one GPU's shard of the metro run: 1M vehicles / 8 GPUs x 100
             points (12.5M points) on the 100 x 100 km graph
   config 4  state-scale graph (500 x 500 km, highway-heavy), 30 s sampling,
-            sigma 50 m, radius 100 m: 20k vehicles x 100 points
+            sigma 50 m, radius 200 m: 20k vehicles x 100 points
 """
 import os
 

@@ -124,3 +124,38 @@ def test_shape_used_can_land_on_an_interpolated_point(road, oracle):
     s = r["segments"]
     assert list(s["begin_shape_index"])[:2] == [0, 1]
     assert r["traces"]["shape_used"][0] == 1
+
+
+# DESIGN.md §3 rule 4: a probe that projects behind the previous column on the
+# same directed edge is a stay (GPS noise; vehicles do not reverse): route
+# distance 0, no traversal, no U-turn onto the opposite edge and back.
+# x: 17 m, 51 m, 38 m (13 m behind: a column, not interpolated), 77 m, then edge 2.
+TRACE_BACK = [(0.0002, 0.0), (0.0006, 5.0), (0.00045, 10.0), (0.0009, 15.0), (0.0014, 20.0)]
+
+
+def test_backward_probe_on_same_edge_is_a_stay(road, oracle):
+    path, fwd = road
+    r = oracle.match_batch(oracle.Graph(path), _batch([TRACE_BACK]), keep_stages=True)
+    e = [int(r["cand_edge"][i * 32 + s]) for i, s in enumerate(r["state"])]
+    o = [float(r["cand_off"][i * 32 + s]) for i, s in enumerate(r["state"])]
+    assert e[:4] == [fwd[0]] * 4 and e[4] == fwd[1]
+    assert o[2] < o[1]  # behind the previous column
+    assert r["route_dist"][2] == 0.0
+    # the next step starts from the stay's own offset (the HMM's state)
+    assert r["route_dist"][3] == pytest.approx(o[3] - o[2], abs=1e-4)
+    s = r["segments"]
+    assert list(s["segment_id"]) == [8, 16]  # no opposite-direction segment
+    assert list(s["begin_shape_index"]) == [0, 3] and list(s["end_shape_index"]) == [3, 4]
+    t = 15.0 + 5.0 * ((_x(0.001) - _x(0.0009)) / (_x(0.0014) - _x(0.0009)))
+    assert s["end_time"][0] == pytest.approx(t, rel=1e-6)
+
+
+def test_chain_ending_on_a_stay_ends_at_the_farthest_offset(road, oracle):
+    # the last state is the stay: the traversal still ends at 51 m (the
+    # farthest offset reached), timed and indexed at the last state
+    path, _ = road
+    r = oracle.match_batch(oracle.Graph(path), _batch([TRACE_BACK[:3]]), keep_stages=True)
+    s = r["segments"]
+    assert list(s["segment_id"]) == [8]
+    assert list(s["begin_shape_index"]) == [0] and list(s["end_shape_index"]) == [2]
+    assert s["length"][0] == -1

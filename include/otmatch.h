@@ -270,8 +270,12 @@ typedef struct otm_trace_result {
 } otm_trace_result;
 #define OTM_TERR_NONE 0
 #define OTM_TERR_ZERODIV 1         /* "float division by zero" */
-#define OTM_TERR_CAND_OVERFLOW 2   /* > OTM_MAX_HITS edges within radius */
-#define OTM_TERR_SEARCH_OVERFLOW 3 /* bounded search settled too many nodes */
+/* 2 and 3 were the 256-edge and 98,304-label spec limits until round 3;
+ * round 4 has no such limits (the batch's tables grow on demand), so they
+ * only report what cannot happen on a consistent graph (a finite transition
+ * whose route search misses its target) or a failed host allocation */
+#define OTM_TERR_CAND_OVERFLOW 2   /* (oracle) candidate workspace allocation failed */
+#define OTM_TERR_SEARCH_OVERFLOW 3 /* a route search could not reproduce its transition */
 #define OTM_TERR_ZERODIV_INT 4     /* "division by zero" (int / int in report()) */
 
 /* Host-side result arrays of one batch (owned by the engine until the next
@@ -376,7 +380,11 @@ typedef struct otm_spill_stats {
   int32_t cand_wave;
   int32_t trans_online, trans_wave, trans_global;
   int32_t route_online, route_wave, route_global;
-  int32_t pad;
+  /* round 4, no spec limits: probes with more distinct edges in their radius
+   * than the LDS tier holds (cand_big), searches past the global tier's
+   * label limit (trans_huge / route_huge), and how many times the batch was
+   * run to size its buffers and tables (attempts, 1 = no redo) */
+  int32_t cand_big, trans_huge, route_huge, attempts;
 } otm_spill_stats;
 int otm_get_spill_stats(otm_engine* eng, otm_spill_stats* out);
 

@@ -272,9 +272,11 @@ static void seen_add(const orc_graph* g, seen_set* S, int32_t e, orc_counters* C
   }
 }
 
-/* returns number of candidates, or -1 on overflow */
+/* returns the number of candidates; *hits / *hcap: the distinct edges in
+ * range, grown as needed (no limit: round 4 dropped the 256-edge spec limit) */
 static int candidates(const orc_graph* g, const orc_params* P, float lat, float lon, float acc, int32_t* c_edge,
-                      float* c_off, float* c_emis, hit* hits, seen_set* seen, orc_counters* C) {
+                      float* c_off, float* c_emis, hit** hitsp, int* hcap, seen_set* seen, orc_counters* C) {
+  hit* hits = *hitsp;
   const float r = probe_radius(P, acc);
   const float r2 = r * r;
   const float ls = MPD_F * orc_cos_deg(lat);
@@ -316,7 +318,10 @@ static int candidates(const orc_graph* g, const orc_params* P, float lat, float 
               break;
             }
           if (f < 0) {
-            if (nh == ORC_MAX_HITS) return -1;
+            if (nh == *hcap) {
+              *hcap = *hcap ? *hcap * 2 : 256;
+              hits = *hitsp = (hit*)realloc(hits, sizeof(hit) * (size_t)*hcap);
+            }
             hits[nh].edge = e;
             hits[nh].sqd = sqd;
             hits[nh].off = off;
@@ -361,7 +366,7 @@ static int candidates(const orc_graph* g, const orc_params* P, float lat, float 
     hits[nk++] = x;
   }
   nh = nk;
-  qsort(hits, (size_t)nh, sizeof(hit), hit_cmp);
+  if (nh > 1) qsort(hits, (size_t)nh, sizeof(hit), hit_cmp);
   const int K = nh < P->max_candidates ? nh : P->max_candidates;
   const float ds = (2.0f * P->sigma_z) * P->sigma_z;
   for (int j = 0; j < K; ++j) {
@@ -405,7 +410,8 @@ typedef struct ws {
   int32_t ne, nn;         /* labelled edges / nodes */
   khn* heap;
   size_t hn, hcap;
-  hit hits[ORC_MAX_HITS + 1];
+  hit* hits; /* distinct edges of a probe (grown) */
+  int hitcap;
   seen_set seen;
 } ws;
 
@@ -505,7 +511,7 @@ static void phase_a(batch* B, ws* w, int32_t t, orc_counters* C) {
     C->columns++;
     B->gc[p] = gcv;
     int K = candidates(g, P, B->lat[p], B->lon[p], B->acc[p], B->cand_edge + p * ORC_KMAX,
-                       B->cand_off + p * ORC_KMAX, B->cand_emis + p * ORC_KMAX, w->hits,
+                       B->cand_off + p * ORC_KMAX, B->cand_emis + p * ORC_KMAX, &w->hits, &w->hitcap,
                        B->count_unique ? &w->seen : NULL, C);
     if (K < 0) {
       if (!B->terr[t]) B->terr[t] = TERR_CAND_OVERFLOW;
@@ -567,7 +573,8 @@ static void set_node(ws* w, int32_t v, uint64_t k) {
 }
 
 /* The labels of a search from node u entered with heading hin, bounded by
- * cost cmax.  Returns 0, or -1 when more than ORC_SEARCH_LIMIT labels. */
+ * cost cmax.  Returns 0 (no label limit since round 4: the workspace holds
+ * every edge and node of the graph). */
 static int ta_search(const batch* B, ws* w, int32_t u, unsigned hin, uint32_t cmax, orc_counters* C, int route) {
   const orc_graph* g = B->g;
   if (++w->stamp == 0) {
@@ -594,9 +601,7 @@ static int ta_search(const batch* B, ws* w, int32_t u, unsigned hin, uint32_t cm
       const uint64_t c = ca + turn_cost_units(B, g->ehead_in[e], g->ehead_out[f]);
       if (c <= cmax) set_edge(w, f, (c << 32) | (uint32_t)e);
     }
-    if (w->ne + w->nn > ORC_SEARCH_LIMIT) return -1;
   }
-  if (w->ne + w->nn > ORC_SEARCH_LIMIT) return -1;
   /* work counters: the departure labels, and the edges a label relaxes
      (its end node's out-edges, when the arrival is within the bound) */
   int64_t relaxed = 0;
@@ -1062,8 +1067,8 @@ static int segments_of_trace(batch* B, ws* w, int32_t t, tres* R, orc_counters* 
       continue;
     }
     /* step lastp -> p */
-    if (pcap < ORC_SEARCH_LIMIT + 1) {
-      pcap = ORC_SEARCH_LIMIT + 1; /* a route's edges are labelled edges of its search */
+    if (pcap < g->h.n_edges + 1) {
+      pcap = g->h.n_edges + 1; /* a route's edges are labelled edges of its search */
       path = (int32_t*)realloc(path, sizeof(int32_t) * (size_t)pcap);
     }
     int plen, same;
@@ -1250,6 +1255,7 @@ static void* worker(void* arg) {
   free(w.nlab);
   free(w.elist);
   free(w.heap);
+  free(w.hits);
   return NULL;
 }
 

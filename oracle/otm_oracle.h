@@ -25,8 +25,6 @@
 #include <stdint.h>
 
 #define ORC_KMAX 32
-#define ORC_MAX_HITS 256         /* distinct edges within one probe radius */
-#define ORC_SEARCH_LIMIT 98304   /* labels (edges + nodes) of one bounded search */
 
 typedef struct orc_graph orc_graph;
 

@@ -494,7 +494,10 @@ void engine_free(otm_engine* E) {
       &E->probe,         &E->col_prev,     &E->kq_prev,        &E->trans_off,      &E->trans,          &E->bp,         &E->state,      &E->chosen,
       &E->chain_start,   &E->route_dist,   &E->ipos,   &E->path_off,       &E->path_len,       &E->path_pool,  &E->trace_err,
       &E->overflow_list0, &E->overflow_list2, &E->counters_i32, &E->scan_tmp, &E->snap,   &E->big_key,
-      &E->big_lab,       &E->big_inq,      &E->big_fr,         &E->big_ins,        &E->big_prev,         &E->o_traces,       &E->o_seg_cnt,  &E->o_way_cnt,
+      &E->big_lab,       &E->big_inq,      &E->big_fr,         &E->big_ins,        &E->big_prev,
+      &E->huge_key,      &E->huge_lab,     &E->huge_inq,       &E->huge_fr,        &E->huge_ins,         &E->huge_prev,
+      &E->cbig_key,      &E->cbig_val,     &E->cbig_skey,
+      &E->overflow_list3, &E->o_traces,       &E->o_seg_cnt,  &E->o_way_cnt,
       &E->o_segments,    &E->o_seg_gidx,   &E->o_way_ids,      &E->o_reports,  &E->o_rep_cnt,  &E->seg_ub,
       &E->f_seg_off,     &E->f_way_off,    &E->f_rep_off,      &E->f_segs,     &E->f_ways,     &E->f_reps,
       &E->f_traces,
@@ -526,6 +529,31 @@ void engine_free(otm_engine* E) {
     if (e) (void)hipEventDestroy(e);
   if (E->stream) (void)hipStreamDestroy(E->stream);
   E->stream = nullptr;
+}
+
+// The huge search tier's tables (kernels.h HUGE_SLOTS): none until a search
+// outgrows the global tier; then 2^huge_log2 slots each, grown 4x and the batch
+// redone whenever a search does not fit (engine_match).
+static int ensure_huge(otm_engine* E, std::string* err) {
+  if (E->huge_log2 <= 0) return OTM_OK;
+  const size_t n = (size_t)HUGE_SLOTS << E->huge_log2;
+  int rc;
+  if ((rc = ensure(E->huge_key, n * 4, err))) return rc;
+  if ((rc = ensure(E->huge_lab, n * 8, err))) return rc;
+  if ((rc = ensure(E->huge_inq, n * 4, err))) return rc;
+  if ((rc = ensure(E->huge_fr, n * 8, err))) return rc;
+  if ((rc = ensure(E->huge_ins, (size_t)HUGE_SLOTS * huge_limit(E->huge_log2) * 4, err))) return rc;
+  if ((rc = ensure(E->huge_prev, (size_t)HUGE_SLOTS * 4, err))) return rc;
+  if (E->huge_ready_log2 != E->huge_log2) {
+    // (re)sized tables start clean, their "last inserted" lists marking the
+    // whole table for the first search (-1)
+    E->huge_ready_log2 = E->huge_log2;
+    HIPCHK(hipMemsetAsync(E->huge_key.p, 0xFF, n * 4, E->stream));
+    HIPCHK(hipMemsetAsync(E->huge_lab.p, 0xFF, n * 8, E->stream));
+    HIPCHK(hipMemsetAsync(E->huge_inq.p, 0, n * 4, E->stream));
+    HIPCHK(hipMemsetAsync(E->huge_prev.p, 0xFF, (size_t)HUGE_SLOTS * 4, E->stream));
+  }
+  return OTM_OK;
 }
 
 static int ensure_big(otm_engine* E, std::string* err) {
@@ -585,7 +613,8 @@ static int engine_match_once(otm_engine* E, const DevBatch& b, hipStream_t s, st
   ENS(trace_err, ((size_t)NT + 1) * 4);
   ENS(overflow_list0, Pn * 4);
   ENS(overflow_list2, Pn * 4);
-  ENS(counters_i32, 64);
+  ENS(overflow_list3, Pn * 4);
+  ENS(counters_i32, 64 * 4);  // 64 counters (kernels.h DevWork::counters_i32)
   ENS(snap, 192 + sizeof(BatchStatus));
   ENS(abort_flag, 16);
   // Capacities of the transition matrices and the path pool: sized from the
@@ -644,6 +673,7 @@ static int engine_match_once(otm_engine* E, const DevBatch& b, hipStream_t s, st
   w.trace_err = P<int32_t>(E->trace_err);
   w.overflow_list0 = P<int32_t>(E->overflow_list0);
   w.overflow_list2 = P<int32_t>(E->overflow_list2);
+  w.overflow_list3 = P<int32_t>(E->overflow_list3);
   w.idx = E->idx;
   w.counters_i32 = P<int32_t>(E->counters_i32);
   w.snap = P<int32_t>(E->snap);
@@ -692,6 +722,24 @@ static int engine_match_once(otm_engine* E, const DevBatch& b, hipStream_t s, st
   w.big_fr = P<uint32_t>(E->big_fr);
   w.big_ins = P<uint32_t>(E->big_ins);
   w.big_prev = P<int32_t>(E->big_prev);
+  if ((rc = ensure_huge(E, err))) return rc;
+  w.huge_key = P<uint32_t>(E->huge_key);
+  w.huge_lab = P<unsigned long long>(E->huge_lab);
+  w.huge_inq = P<uint32_t>(E->huge_inq);
+  w.huge_fr = P<uint32_t>(E->huge_fr);
+  w.huge_ins = P<uint32_t>(E->huge_ins);
+  w.huge_prev = P<int32_t>(E->huge_prev);
+  w.huge_log2 = E->huge_log2;
+  if (E->cand_log2 > 0) {  // k_candidates<true> clears its tables per probe
+    const size_t n = (size_t)CAND_BIG_SLOTS << E->cand_log2;
+    if ((rc = ensure(E->cbig_key, n * 4, err))) return rc;
+    if ((rc = ensure(E->cbig_val, n * 8, err))) return rc;
+    if ((rc = ensure(E->cbig_skey, n / 2 * 8, err))) return rc;
+  }
+  w.cbig_key = P<uint32_t>(E->cbig_key);
+  w.cbig_val = P<unsigned long long>(E->cbig_val);
+  w.cbig_skey = P<unsigned long long>(E->cbig_skey);
+  w.cand_log2 = E->cand_log2;
   launch_transitions(E->g, b, dp, w, s, mk, E->trans_lanes);
   // spill snapshot B: columns per transition tier (Viterbi does not touch
   // the counters; they start over for the route tiers)
@@ -767,12 +815,30 @@ int engine_match(otm_engine* E, const DevBatch& b, hipStream_t s, std::string* e
     const int64_t ttotal = st.ttotal;
     const int32_t cnt[3] = {st.cnt[0], st.cnt[1], st.cnt[2]};
     E->last_trans = ttotal;
+    E->last_attempts = attempt + 1;
     if (!ab) break;
-    if (attempt == 3) {
+    if (attempt == 16) {
       *err = "batch capacities could not be sized";
       return OTM_EDEVICE;
     }
     if (ttotal > E->trans_cap) E->trans_cap = ttotal + ttotal / 4 + 4096;
+    if (st.grow & 1) {
+      // a search outgrew the huge tier's tables (or found none): 4x the slots
+      if (E->huge_log2 >= 30) {
+        *err = "a route search outgrew 2^30 table slots";
+        return OTM_EDEVICE;
+      }
+      E->huge_log2 = E->huge_log2 ? E->huge_log2 + 2 : 19;
+    }
+    if (st.grow & 2) {
+      // a probe had more distinct edges in its radius than the candidate
+      // HBM tier's tables hold (or there were none): 4x the slots
+      if (E->cand_log2 >= 26) {
+        *err = "a candidate search outgrew 2^26 table slots";
+        return OTM_EDEVICE;
+      }
+      E->cand_log2 = E->cand_log2 ? E->cand_log2 + 2 : 13;
+    }
     if (cnt[2]) E->pool_cap = (int32_t)std::min<size_t>((size_t)cnt[1] * 2 + 1024, (size_t)INT32_MAX / 2);
   }
   if (E->timing) {
@@ -1323,7 +1389,12 @@ int engine_spill_stats(otm_engine* E, otm_spill_stats* out) {
   out->route_online = v[32 + 4];
   out->route_wave = v[32 + 4];
   out->route_global = v[32 + 3];
-  out->pad = 0;
+  int32_t c[32] = {};
+  if (E->snap.p && hipMemcpy(c, E->counters_i32.p, sizeof c, hipMemcpyDeviceToHost) != hipSuccess) return OTM_EDEVICE;
+  out->cand_big = c[24];
+  out->trans_huge = c[21];
+  out->route_huge = c[22];
+  out->attempts = E->last_attempts;
   return OTM_OK;
 }
 

@@ -77,6 +77,12 @@ struct otm_engine {
       chain_start, route_dist, ipos, path_off, path_len, path_pool, trace_err, overflow_list0, overflow_list2,
       counters_i32, scan_tmp, snap;
   Buf big_key, big_lab, big_inq, big_fr, big_ins, big_prev;
+  Buf huge_key, huge_lab, huge_inq, huge_fr, huge_ins, huge_prev, overflow_list3;
+  int32_t huge_log2 = 0;  // huge search tier: 2^huge_log2 slots per table (0: none yet; grown on demand)
+  int32_t huge_ready_log2 = 0;
+  Buf cbig_key, cbig_val, cbig_skey;
+  int32_t cand_log2 = 0;
+  int32_t last_attempts = 0;  // runs of the last batch (otm_spill_stats::attempts)  // candidate HBM tier: 2^cand_log2 slots per table (0: none yet; grown on demand)  // the layout the huge tables were last cleared for
   Buf ord_tile, ord_cnt, ord_cursor, ord_grp, ord_item;  // spatial work order
   Buf abort_flag;                                       // capacity overflow of the batch in flight
   Buf rs_blob;                                          // otm_report_segments_device in/out

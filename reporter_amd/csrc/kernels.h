@@ -25,8 +25,8 @@ namespace otm {
 constexpr int KMAX = 32;           // max candidates per column (== ORC_KMAX)
 constexpr int KIN = 8;             // inline candidate slots per point (DevWork::cand_eo / cand_em)
 constexpr int KX = KMAX - KIN;     // overflow candidate slots per point (DevWork::cand_xeo / cand_xem)
-constexpr int MAX_HITS = 256;      // distinct edges within one radius (spec limit)
-constexpr int SEARCH_LIMIT = 98304;  // labels (edges + nodes) of one search (spec limit, == ORC_SEARCH_LIMIT)
+constexpr int MAX_HITS = 256;      // distinct edges within one radius in the LDS tiers (beyond: the global tier)
+constexpr int SEARCH_LIMIT = 98304;  // labels (edges + nodes) of one global-tier search (beyond: the huge tier)
 constexpr int LDS_TABLE_CAP = 256;   // K4/K6 LDS tier: table slots
 constexpr int LDS_TABLE_LIMIT = 192; // ... labels before spilling to the global tier
 constexpr int BIG_TABLE_LOG2 = 17;
@@ -35,6 +35,15 @@ constexpr int BIG_TABLE_CAP = 1 << BIG_TABLE_LOG2;  // global tier table slots (
 #define OTM_BIG_SLOTS 512
 #endif
 constexpr int BIG_SLOTS = OTM_BIG_SLOTS;  // concurrent global-tier searches
+// The huge search tier (round 4): searches beyond SEARCH_LIMIT labels, in
+// HUGE_SLOTS tables of 2^huge_log2 slots sized by the host (grown and the
+// batch redone when a search does not fit: no label limit but memory)
+constexpr int HUGE_SLOTS = 8;
+// The candidate search's HBM tier (round 4): probes with more than MAX_HITS
+// distinct edges within their radius, CAND_BIG_SLOTS at a time, in tables of
+// 2^cand_log2 slots (half of them the sort keys) sized like the huge tier.
+constexpr int CAND_BIG_SLOTS = 64;
+__host__ __device__ inline int huge_limit(int log2) { return log2 > 2 ? 3 << (log2 - 2) : 0; }  // 0.75 x slots
 
 struct DevGraph {
   const float *node_lat, *node_lon;
@@ -184,8 +193,11 @@ struct DevWork {
   int32_t* overflow_list0; // [P] columns/steps the index could not answer
   int32_t* overflow_list2; // [P] ... the LDS search tier spilled (and k_trans_sub's wide columns)
   int32_t* snap;           // [48] spill snapshots A (after K2), B (after K4), C (after K6)
-  int32_t* counters_i32;   // [1] pool used, [2] pool overflow flag, [3] list 2 count, [4] list 0 count,
-                           // [6] wide list count
+  int32_t* counters_i32;   // [64]: [1] pool used, [2] pool overflow flag, [3] list 2 count, [4] list 0 count,
+                           // [5] candidate wave-tier count, [6] wide list count (0-15: per stage, snapshot
+                           // and reset); per batch: [20] Viterbi wide list, [21] / [22] huge-tier
+                           // transition / route searches, [23] huge grow flag, [24] candidate HBM-tier
+                           // probes, [25] its grow flag
   int32_t* abort;          // [1] set when a capacity (transition matrices, path pool) was exceeded:
                            // every later kernel returns at once and the host redoes the batch
   int64_t trans_cap;       // floats allocated for w.trans
@@ -198,6 +210,20 @@ struct DevWork {
   uint32_t* big_fr;
   uint32_t* big_ins;       // [BIG_SLOTS * SEARCH_LIMIT] slots each table's last search inserted
   int32_t* big_prev;       // [BIG_SLOTS] their count (-1: clear the whole table)
+  // huge-tier scratch ([HUGE_SLOTS << huge_log2] slots; huge_log2 == 0: none yet)
+  uint32_t* huge_key;
+  unsigned long long* huge_lab;
+  uint32_t* huge_inq;
+  uint32_t* huge_fr;
+  uint32_t* huge_ins;      // [HUGE_SLOTS * huge_limit(huge_log2)]
+  int32_t* huge_prev;      // [HUGE_SLOTS]
+  int32_t huge_log2;
+  // candidate HBM tier ([CAND_BIG_SLOTS << cand_log2] slots; cand_log2 == 0: none yet)
+  uint32_t* cbig_key;
+  unsigned long long* cbig_val;
+  unsigned long long* cbig_skey;  // [CAND_BIG_SLOTS << (cand_log2 - 1)]
+  int32_t cand_log2;
+  int32_t* overflow_list3; // [P] searches the global tier spilled (counts: [21] transitions, [22] route)
   DevCounters* ctr;        // nullptr when counting is off
 };
 
@@ -293,7 +319,7 @@ void launch_index_build(const DevGraph& g, const uint32_t* turn_units, uint32_t 
                         const IdxRow* rows, uint4* slot, int32_t* pred, bool write, hipStream_t s);
 void launch_row_sizes(const int32_t* row_cnt, int64_t* row_sizes, int32_t n, hipStream_t s);
 struct BatchStatus {
-  int32_t abort, pad;
+  int32_t abort, grow;  // grow bit 0: the huge search tier needs (larger) tables; bit 1: the candidate HBM tier
   int64_t ttotal;
   int32_t cnt[3], pad2;
 };

@@ -360,7 +360,7 @@ __global__ __launch_bounds__(TB) void k_columns(DevGraph g, DevBatch b, DevParam
   const int lane = threadIdx.x;
   if (OTM_FOLD_BOOKKEEPING && blockIdx.x == 0) {
     // the batch's tier counters and abort flag start at zero (k_batch_init)
-    if (lane < 16) w.counters_i32[lane] = 0;
+    if (lane < 32) w.counters_i32[lane] = 0;  // ([20]: the wide Viterbi list)
     if (lane == 0) *w.abort = 0;
   }
   for (int32_t t = blockIdx.x; t < b.n_traces; t += gridDim.x) {
@@ -736,18 +736,64 @@ __global__ __launch_bounds__(CAND_TB, OTM_CAND_WAVES) void k_cand_lane(DevGraph 
   }
 }
 
+template <bool BIG>
+struct Mem;
+template <>
+struct Mem<false> {  // LDS
+  template <class T>
+  __device__ static T ld(const T* p) {
+    return *p;
+  }
+  template <class T>
+  __device__ static void st(T* p, T v) {
+    *p = v;
+  }
+};
+template <>
+struct Mem<true> {  // global scratch: keep every access at L2 (agent scope)
+  template <class T>
+  __device__ static T ld(const T* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  template <class T>
+  __device__ static void st(T* p, T v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+};
+
 // Wave tier: one wavefront per spilled probe (list from the lane tier).
+// BIG = false: LDS tables (MAX_HITS distinct edges); a probe with more goes
+// to the list of the BIG form (overflow_list3, count [24]), whose tables
+// (2^cand_log2 slots per block, in HBM) the host sizes: none until needed,
+// grown 4x with the batch redone when a probe does not fit (no limit on the
+// edges within a radius but memory; round 4 dropped the 256-edge spec limit).
+template <bool BIG>
 __global__ __launch_bounds__(TB) void k_candidates(DevGraph g, DevBatch b, DevParams P, DevWork w) {
-  __shared__ uint32_t hkey[HCAP];
-  __shared__ unsigned long long hval[HCAP];
-  __shared__ unsigned long long skey[MAX_HITS];
+  __shared__ uint32_t l_hkey[BIG ? 1 : HCAP];
+  __shared__ unsigned long long l_hval[BIG ? 1 : HCAP];
+  __shared__ unsigned long long l_skey[BIG ? 1 : MAX_HITS];
   __shared__ int64_t cstart[64];
   __shared__ int cexcl[64];
   __shared__ int s_count, s_over, s_n;
   const int lane = threadIdx.x;
-  const int64_t nwork = w.counters_i32[5];
+  const int64_t nwork = BIG ? w.counters_i32[24] : w.counters_i32[5];
+  const int32_t* list = BIG ? w.overflow_list3 : w.overflow_list0;
+  if (BIG && nwork > 0 && w.cand_log2 == 0) {  // no tables yet: the host makes them, redoes the batch
+    for (int64_t it = (int64_t)blockIdx.x * TB + lane; it < nwork; it += (int64_t)gridDim.x * TB) w.ncand[list[it]] = 0;
+    if (blockIdx.x == 0 && lane == 0) {
+      w.counters_i32[25] = 1;
+      *w.abort = 1;
+    }
+    return;
+  }
+  const int hlog2 = BIG ? w.cand_log2 : 9;
+  const int hcap = 1 << hlog2;
+  const int max_hits = hcap / 2;
+  uint32_t* hkey = BIG ? w.cbig_key + (size_t)blockIdx.x * hcap : l_hkey;
+  unsigned long long* hval = BIG ? w.cbig_val + (size_t)blockIdx.x * hcap : l_hval;
+  unsigned long long* skey = BIG ? w.cbig_skey + (size_t)blockIdx.x * max_hits : l_skey;
   for (int64_t it = blockIdx.x; it < nwork; it += gridDim.x) {
-    const int64_t p = w.overflow_list0[it];
+    const int64_t p = list[it];
     const float4 pr = w.probe[p];  // {lat, lon, accuracy} of the column (K1), one line
     const float lat = pr.x, lon = pr.y;
     const float r = probe_radius(P, pr.z);
@@ -769,9 +815,9 @@ __global__ __launch_bounds__(TB) void k_candidates(DevGraph g, DevBatch b, DevPa
     }
     const int ncols = c1 - c0 + 1;
     const int ncells = (r1 - r0 + 1) * ncols;
-    for (int i = lane; i < HCAP; i += TB) {
-      hkey[i] = EMPTY;
-      hval[i] = LAB_NONE;
+    for (int i = lane; i < hcap; i += TB) {
+      Mem<BIG>::st(&hkey[i], (uint32_t)EMPTY);
+      Mem<BIG>::st(&hval[i], (unsigned long long)LAB_NONE);
     }
     if (lane == 0) {
       s_count = 0;
@@ -809,12 +855,12 @@ __global__ __launch_bounds__(TB) void k_candidates(DevGraph g, DevBatch b, DevPa
         float sqd, off;
         project(g, e, k, lat, lon, ls, sqd, off);
         if (!(sqd <= r2)) continue;
-        uint32_t slot = hash32((uint32_t)e) >> (32 - 9);
+        uint32_t slot = hash32((uint32_t)e) >> (32 - hlog2);
         bool placed = false;
-        for (int probe = 0; probe < HCAP; ++probe) {
+        for (int probe = 0; probe < hcap; ++probe) {
           const uint32_t old = atomicCAS(&hkey[slot], EMPTY, (uint32_t)e);
           if (old == EMPTY) {
-            if (atomicAdd(&s_count, 1) >= MAX_HITS) s_over = 1;
+            if (atomicAdd(&s_count, 1) >= max_hits) s_over = 1;
             placed = true;
             break;
           }
@@ -822,7 +868,7 @@ __global__ __launch_bounds__(TB) void k_candidates(DevGraph g, DevBatch b, DevPa
             placed = true;
             break;
           }
-          slot = (slot + 1) & (HCAP - 1);
+          slot = (slot + 1) & (uint32_t)(hcap - 1);
         }
         if (!placed) {
           s_over = 1;
@@ -835,8 +881,13 @@ __global__ __launch_bounds__(TB) void k_candidates(DevGraph g, DevBatch b, DevPa
     }
     if (s_over) {
       if (lane == 0) {
-        w.ncand[p] = 0;
-        atomicCAS(&w.trace_err[w.pt_trace[p]], 0, OTM_TERR_CAND_OVERFLOW);
+        if (!BIG) {
+          w.overflow_list3[atomicAdd(&w.counters_i32[24], 1)] = (int32_t)p;  // to the HBM tables
+        } else {
+          w.ncand[p] = 0;
+          w.counters_i32[25] = 1;  // the tables are too small: grow, redo the batch
+          *w.abort = 1;
+        }
       }
       __syncthreads();
       continue;
@@ -850,47 +901,51 @@ __global__ __launch_bounds__(TB) void k_candidates(DevGraph g, DevBatch b, DevPa
     // bits << 32 | a slot of the group), which writes the node candidate
     // sqdist bits << 32 | first outgoing edge << 5 into that slot -- so a node
     // sorts before an edge candidate of the same edge at the same distance.
-    for (int i = lane; i < HCAP; i += TB) {
-      if (hkey[i] != EMPTY) {
+    for (int i = lane; i < hcap; i += TB) {
+      const uint32_t hk = Mem<BIG>::ld(&hkey[i]);
+      if (hk != EMPTY) {
+        const unsigned long long hv = Mem<BIG>::ld(&hval[i]);
         const int idx = atomicAdd(&s_n, 1);
-        skey[idx] = (hval[i] & 0xFFFFFFFF00000000ull) | ((unsigned long long)hkey[i] << 5) | ((hval[i] & 15ull) << 1);
+        Mem<BIG>::st(&skey[idx],
+                     (hv & 0xFFFFFFFF00000000ull) | ((unsigned long long)hk << 5) | ((hv & 15ull) << 1));
       }
     }
     __syncthreads();
-    for (int i = lane; i < HCAP; i += TB) {
-      hkey[i] = EMPTY;
-      hval[i] = LAB_NONE;
+    for (int i = lane; i < hcap; i += TB) {
+      Mem<BIG>::st(&hkey[i], (uint32_t)EMPTY);
+      Mem<BIG>::st(&hval[i], (unsigned long long)LAB_NONE);
     }
     if (lane == 0) s_count = 0;  // from here: distinct candidates
     __syncthreads();
     const int n0 = s_n;
     for (int idx = lane; idx < n0; idx += TB) {
-      const unsigned long long key = skey[idx];
+      const unsigned long long key = Mem<BIG>::ld(&skey[idx]);
       const int32_t e = (int32_t)(((uint32_t)key) >> 5);
       float sqd, off;
       bool at_end;
       project(g, e, (int32_t)((key >> 1) & 15ull), lat, lon, ls, sqd, off, at_end);
       const int32_t v = snap_node(g, e, off, at_end);
       if (v < 0) {
-        skey[idx] = key | 1ull;
+        Mem<BIG>::st(&skey[idx], key | 1ull);
         atomicAdd(&s_count, 1);
       } else {
-        skey[idx] = LAB_NONE;
+        Mem<BIG>::st(&skey[idx], (unsigned long long)LAB_NONE);
         const uint32_t rep = (uint32_t)g.out_off[v];
-        uint32_t slot = hash32(rep) >> (32 - 9);
+        uint32_t slot = hash32(rep) >> (32 - hlog2);
         while (true) {
           const uint32_t old = atomicCAS(&hkey[slot], EMPTY, rep);
           if (old == EMPTY || old == rep) break;
-          slot = (slot + 1) & (HCAP - 1);
+          slot = (slot + 1) & (uint32_t)(hcap - 1);
         }
         atomicMin(&hval[slot], (key & 0xFFFFFFFF00000000ull) | (unsigned long long)idx);
       }
     }
     __syncthreads();
-    for (int i = lane; i < HCAP; i += TB) {
-      if (hkey[i] != EMPTY) {
-        const unsigned long long hv = hval[i];
-        skey[(int)(hv & 0xFFFFull)] = (hv & 0xFFFFFFFF00000000ull) | ((unsigned long long)hkey[i] << 5);
+    for (int i = lane; i < hcap; i += TB) {
+      const uint32_t hk = Mem<BIG>::ld(&hkey[i]);
+      if (hk != EMPTY) {
+        const unsigned long long hv = Mem<BIG>::ld(&hval[i]);
+        Mem<BIG>::st(&skey[(int)(hv & 0xFFFFFFFFull)], (hv & 0xFFFFFFFF00000000ull) | ((unsigned long long)hk << 5));
         atomicAdd(&s_count, 1);
       }
     }
@@ -899,7 +954,7 @@ __global__ __launch_bounds__(TB) void k_candidates(DevGraph g, DevBatch b, DevPa
     const int n = s_count;  // distinct candidates
     int N = 1;
     while (N < ns) N <<= 1;
-    for (int i = ns + lane; i < N; i += TB) skey[i] = LAB_NONE;
+    for (int i = ns + lane; i < N; i += TB) Mem<BIG>::st(&skey[i], (unsigned long long)LAB_NONE);
     __syncthreads();
     // bitonic sort ascending
     for (int kk = 2; kk <= N; kk <<= 1) {
@@ -907,11 +962,11 @@ __global__ __launch_bounds__(TB) void k_candidates(DevGraph g, DevBatch b, DevPa
         for (int i = lane; i < N; i += TB) {
           const int ixj = i ^ j;
           if (ixj > i) {
-            const unsigned long long x = skey[i], y = skey[ixj];
+            const unsigned long long x = Mem<BIG>::ld(&skey[i]), y = Mem<BIG>::ld(&skey[ixj]);
             const bool up = (i & kk) == 0;
             if ((x > y) == up) {
-              skey[i] = y;
-              skey[ixj] = x;
+              Mem<BIG>::st(&skey[i], y);
+              Mem<BIG>::st(&skey[ixj], x);
             }
           }
         }
@@ -920,7 +975,7 @@ __global__ __launch_bounds__(TB) void k_candidates(DevGraph g, DevBatch b, DevPa
     }
     const int K = n < P.max_candidates ? n : P.max_candidates;
     if (lane < K) {
-      const unsigned long long key = skey[lane];
+      const unsigned long long key = Mem<BIG>::ld(&skey[lane]);
       const int32_t e = (int32_t)(((uint32_t)key) >> 5);
       float sqd = bitsf((uint32_t)(key >> 32)), off = 0.0f;
       if (key & 1ull) project(g, e, (int32_t)((key >> 1) & 15ull), lat, lon, ls, sqd, off);
@@ -973,7 +1028,7 @@ __global__ __launch_bounds__(256) void k_links(DevBatch b, DevParams P, DevWork 
 // each on the stream, ~60 us per batch before).
 __global__ void k_batch_init(int32_t* counters, int32_t* abort) {
   const int t = threadIdx.x;
-  if (t < 16) counters[t] = 0;
+  if (t < 32) counters[t] = 0;
   if (t == 0) *abort = 0;
 }
 // spill snapshot: copy the 16 tier counters, optionally zeroing them for the
@@ -990,6 +1045,7 @@ __global__ void k_snap(int32_t* counters, int32_t* snap, int reset) {
 __global__ void k_status(const int32_t* abort, const int64_t* ttotal, const int32_t* counters, BatchStatus* out) {
   if (threadIdx.x == 0) {
     out->abort = *abort;
+    out->grow = (counters[23] != 0 ? 1 : 0) | (counters[25] != 0 ? 2 : 0);
     out->ttotal = *ttotal;
     out->cnt[0] = counters[0];
     out->cnt[1] = counters[1];
@@ -1030,31 +1086,6 @@ struct Table {
   // of the whole 128K-slot table (the tables start clean: engine.cpp ensure_big)
   uint32_t* ins = nullptr;
   int32_t* prev = nullptr;
-};
-
-template <bool BIG>
-struct Mem;
-template <>
-struct Mem<false> {  // LDS
-  template <class T>
-  __device__ static T ld(const T* p) {
-    return *p;
-  }
-  template <class T>
-  __device__ static void st(T* p, T v) {
-    *p = v;
-  }
-};
-template <>
-struct Mem<true> {  // global scratch: keep every access at L2 (agent scope)
-  template <class T>
-  __device__ static T ld(const T* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  template <class T>
-  __device__ static void st(T* p, T v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
 };
 
 struct SearchShared {
@@ -1220,7 +1251,7 @@ template <class F>
 __device__ void chain_sums(const DevGraph& g, const uint32_t* TU, F predof, uint32_t pred0, uint32_t hin,
                            uint32_t hout, int32_t* buf, float& d, uint32_t& units, int& n) {
   int cnt = 0;
-  for (uint32_t p = pred0; p != NONE_PRED && cnt <= SEARCH_LIMIT; p = predof(p)) {
+  for (uint32_t p = pred0; p != NONE_PRED && cnt < (1 << 26); p = predof(p)) {
     if (cnt < CHAIN_BUF) buf[cnt * TB] = (int32_t)p;
     ++cnt;
   }
@@ -1711,8 +1742,43 @@ __global__ __launch_bounds__(256, OTM_ROUTE_WAVES) void k_route_index(DevGraph g
 // search per distinct source (node, heading), the wave's table in LDS.  The
 // LDS tier spills to `w.overflow_list2` / counters_i32[3], which the
 // global-memory tier (BIG) drains.
-template <bool BIG>
+// the search table of a tier's block: LDS (0), global (1), huge (2)
+template <int TIER>
+__device__ __forceinline__ Table tier_table(const DevWork& w, uint32_t* lkey, unsigned long long* llab, uint32_t* linq,
+                                            uint32_t* lfr0, uint32_t* lfr1) {
+  if (TIER == 1) {
+    const size_t base = (size_t)blockIdx.x * BIG_TABLE_CAP;
+    return Table{w.big_key + base, w.big_lab + base, w.big_inq + base, w.big_fr + 2 * base,
+                 w.big_fr + 2 * base + BIG_TABLE_CAP, BIG_TABLE_LOG2, SEARCH_LIMIT,
+                 w.big_ins + (size_t)blockIdx.x * SEARCH_LIMIT, w.big_prev + blockIdx.x};
+  }
+  if (TIER == 2) {
+    const size_t cap = (size_t)1 << w.huge_log2;
+    const size_t base = (size_t)blockIdx.x * cap;
+    const int lim = huge_limit(w.huge_log2);
+    return Table{w.huge_key + base, w.huge_lab + base, w.huge_inq + base, w.huge_fr + 2 * base,
+                 w.huge_fr + 2 * base + cap, w.huge_log2, lim, w.huge_ins + (size_t)blockIdx.x * lim,
+                 w.huge_prev + blockIdx.x};
+  }
+  return Table{lkey, llab, linq, lfr0, lfr1, 8, LDS_TABLE_LIMIT};
+}
+// the huge tier has work but no tables yet: the host allocates them and
+// redoes the batch (returns true: the launch is done)
+__device__ __forceinline__ bool huge_unready(DevWork& w, int64_t nwork) {
+  if (nwork <= 0 || w.huge_log2 > 0) return false;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    w.counters_i32[23] = 1;
+    *w.abort = 1;
+  }
+  return true;
+}
+
+// TIER 0: LDS tables; 1: global tables (BIG_SLOTS x BIG_TABLE_CAP); 2: the
+// huge tier (HUGE_SLOTS x 2^huge_log2).  Spills: 0 -> list2 ([3]) -> 1 ->
+// list3 ([21]) -> 2 -> the host grows the huge tables and redoes the batch.
+template <int TIER>
 __global__ __launch_bounds__(TB) void k_transitions(DevGraph g, DevBatch b, DevParams P, DevWork w) {
+  constexpr bool BIG = TIER > 0;
   if (*w.abort || trans_over_cap(b, w)) return;
   __shared__ uint32_t lkey[BIG ? 1 : LDS_TABLE_CAP];
   __shared__ unsigned long long llab[BIG ? 1 : LDS_TABLE_CAP];
@@ -1726,21 +1792,15 @@ __global__ __launch_bounds__(TB) void k_transitions(DevGraph g, DevBatch b, DevP
   __shared__ SearchShared S;
   const int lane = threadIdx.x;
   for (int k = lane; k < TURN_TABLE; k += TB) TU[k] = P.turn_units[k];
-  Table T;
-  if (BIG) {
-    const size_t base = (size_t)blockIdx.x * BIG_TABLE_CAP;
-    T = Table{w.big_key + base, w.big_lab + base, w.big_inq + base, w.big_fr + 2 * base,
-              w.big_fr + 2 * base + BIG_TABLE_CAP, BIG_TABLE_LOG2, SEARCH_LIMIT,
-              w.big_ins + (size_t)blockIdx.x * SEARCH_LIMIT, w.big_prev + blockIdx.x};
-  } else {
-    T = Table{lkey, llab, linq, lfr0, lfr1, 8, LDS_TABLE_LIMIT};
-  }
+  Table T = tier_table<TIER>(w, lkey, llab, linq, lfr0, lfr1);
   auto predof = [&](uint32_t e) {
     const int sx = table_find<BIG>(T, e);
     return sx < 0 ? NONE_PRED : (uint32_t)(Mem<BIG>::ld(&T.lab[sx]) & 0xFFFFFFFFull);
   };
-  const int32_t* list = BIG ? w.overflow_list2 : w.overflow_list0;
-  const int64_t nwork = BIG ? (int64_t)w.counters_i32[3] : (int64_t)w.counters_i32[4];
+  const int32_t* list = TIER == 2 ? w.overflow_list3 : (BIG ? w.overflow_list2 : w.overflow_list0);
+  const int64_t nwork = TIER == 2 ? (int64_t)w.counters_i32[21]
+                                  : (BIG ? (int64_t)w.counters_i32[3] : (int64_t)w.counters_i32[4]);
+  if (TIER == 2 && huge_unready(w, nwork)) return;
   __syncthreads();
   for (int64_t it = blockIdx.x; it < nwork; it += gridDim.x) {
     const int64_t p = (int64_t)list[it];
@@ -1836,11 +1896,13 @@ __global__ __launch_bounds__(TB) void k_transitions(DevGraph g, DevBatch b, DevP
       cadd(&w.ctr->transitions, c_trans);
     }
     if (failed && lane == 0) {
-      if (!BIG) {
-        const int slot = atomicAdd(&w.counters_i32[3], 1);
-        w.overflow_list2[slot] = (int32_t)p;
+      if (TIER == 0) {
+        w.overflow_list2[atomicAdd(&w.counters_i32[3], 1)] = (int32_t)p;
+      } else if (TIER == 1) {
+        w.overflow_list3[atomicAdd(&w.counters_i32[21], 1)] = (int32_t)p;
       } else {
-        atomicCAS(&w.trace_err[w.pt_trace[p]], 0, OTM_TERR_SEARCH_OVERFLOW);
+        w.counters_i32[23] = 1;  // the huge tables are too small: grow, redo
+        *w.abort = 1;
       }
     }
     __syncthreads();
@@ -1976,10 +2038,13 @@ static_assert(VIT_EW >= KMAX, "one column's emissions fit a window");
 // Measured and not kept (profiles/r02_ab_viterbi.txt): a one-read backtrack
 // through trace-wide backpointer indices (0.159 vs 0.157 ms, and 16-bit
 // backpointers cost occupancy), one global round trip per window (equal).
-__global__ __launch_bounds__(TB, OTM_VIT_WAVES) void k_viterbi(DevBatch b, DevWork w) {
+// list / list_n: the traces to decode (null: all); snap: this launch takes
+// spill snapshot B (the first Viterbi launch of the batch)
+__global__ __launch_bounds__(TB, OTM_VIT_WAVES) void k_viterbi(DevBatch b, DevWork w, const int32_t* list,
+                                                               const int32_t* list_n, int snap) {
   // spill snapshot B: columns per transition tier (Viterbi does not touch the
   // counters; they start over for the route tiers)
-  if (OTM_FOLD_BOOKKEEPING && blockIdx.x == 0 && threadIdx.x == 0) fold_snap(w, 1, true);
+  if (OTM_FOLD_BOOKKEEPING && snap && blockIdx.x == 0 && threadIdx.x == 0) fold_snap(w, 1, true);
   if (*w.abort) return;  // a capacity was exceeded: the host redoes the batch
   __shared__ float sT[VIT_TW];
   __shared__ float sEm[VIT_EW];
@@ -1991,7 +2056,9 @@ __global__ __launch_bounds__(TB, OTM_VIT_WAVES) void k_viterbi(DevBatch b, DevWo
   __shared__ int16_t sCprev[VIT_PTS];
   __shared__ int8_t sKc[VIT_PTS];  // ncand of a column, -1 for a non-column point
   const int lane = threadIdx.x;
-  for (int32_t t = blockIdx.x; t < b.n_traces; t += gridDim.x) {
+  const int32_t nwork = list ? *list_n : b.n_traces;
+  for (int32_t it = blockIdx.x; it < nwork; it += gridDim.x) {
+    const int32_t t = list ? list[it] : it;
     const int64_t a = b.trace_off[t], e = b.trace_off[t + 1];
     const int n = (int)(e - a);
     if (w.trace_err[t] != 0) {
@@ -2233,11 +2300,286 @@ __global__ __launch_bounds__(TB, OTM_VIT_WAVES) void k_viterbi(DevBatch b, DevWo
   }
 }
 
+// K5, eight traces per wavefront.  The wave-per-trace form
+// above issues every per-column instruction for 64 lanes of which Kq <= 8
+// hold states (config 2: 4.0 candidates per column, config 4: 3.0), and its
+// time is the SIMDs' issue rate over those instructions.  Here a group of
+// eight lanes decodes one trace (lane j = state j), eight traces per wave:
+//  * a group first lists its trace's columns (point, candidates, linked to
+//    the previous column, the transition block's offset) in LDS; a trace with
+//    a column of more than 8 candidates, more than V8_PTS points or an error
+//    goes to the list the wave-per-trace form takes after;
+//  * the forward pass runs over column steps, one per group per step; the
+//    transition blocks and the emissions stream through a per-group LDS ring,
+//    refilled for every group at once when any group's next column is not
+//    resident (one round trip for all eight);
+//  * a chain's end records its argmin state; the backtrack is a backward walk
+//    over the columns after the forward pass, with 4-bit backpointers packed
+//    in one word per column;
+//  * state, chain_start and the chosen candidate go out point-parallel.
+// Same recurrence (min over i in order, strict <), tie rules and chain breaks
+// as viterbi_trace_global: bit-identical to the oracle.
+#ifndef OTM_VIT_SUB
+#define OTM_VIT_SUB 0
+#endif
+constexpr int V8_L = 8;          // lanes (states) per trace
+constexpr int V8_T = TB / V8_L;  // traces per wave
+constexpr int V8_PTS = 128;      // points per trace
+constexpr int V8_TW = 256;       // transition ring per trace (floats, power of two, >= 2 * 64)
+constexpr int V8_EP = 16;        // emission ring per trace (points, power of two)
+struct V8Lds {
+  float t[V8_T][V8_TW];
+  float em[V8_T][V8_EP * V8_L];
+  uint32_t bp[V8_T][V8_PTS];       // per column: 4-bit backpointer of each state
+  int16_t toff[V8_T][V8_PTS + 1];  // per column: its block's first float (from the trace's first), [nc]: the end
+  int8_t pl[V8_T][V8_PTS];         // column -> point
+  int8_t pcol[V8_T][V8_PTS];       // point -> column, -1
+  int8_t kc[V8_T][V8_PTS];         // column -> candidates
+  uint8_t fl[V8_T][V8_PTS];        // column flags: 1 linked, 2 chain start, 4 chain end (argmin state in bits 4..6)
+  int8_t st[V8_T][V8_PTS];         // column -> decoded state
+};
+__device__ __forceinline__ int wave_max_i(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const int x = __shfl_xor(v, o, 64);
+    v = x > v ? x : v;
+  }
+  return v;
+}
+__global__ __launch_bounds__(TB) void k_viterbi_sub(DevBatch b, DevWork w, int32_t* wide, int32_t* wide_n) {
+  // spill snapshot B (see k_viterbi)
+  if (OTM_FOLD_BOOKKEEPING && blockIdx.x == 0 && threadIdx.x == 0) fold_snap(w, 1, true);
+  if (*w.abort) return;
+  __shared__ V8Lds S;
+  const int lane = threadIdx.x;
+  const int g = lane >> 3, j = lane & 7;
+  for (int32_t tb = blockIdx.x * V8_T; tb < b.n_traces; tb += gridDim.x * V8_T) {
+    const int32_t t = tb + g;
+    bool act = t < b.n_traces;
+    int64_t a = 0;
+    int n = 0, nc = 0;
+    int64_t t0 = 0;
+    if (act) {
+      a = b.trace_off[t];
+      n = (int)(b.trace_off[t + 1] - a);
+      if (w.trace_err[t] != 0) {
+        for (int pl = j; pl < n; pl += V8_L) {
+          w.state[a + pl] = -1;
+          w.chain_start[a + pl] = 0;
+        }
+        act = false;
+      } else if (n > V8_PTS) {
+        if (j == 0) wide[atomicAdd(wide_n, 1)] = t;
+        act = false;
+      } else {
+        t0 = w.trans_off[a];
+      }
+    }
+    // ---- the group's columns (wave-uniform trip count; groups predicated)
+    bool wide_k = false;
+    const int nmax = wave_max_i(act ? n : 0);
+    // 64 points of every group's trace per round: each lane's eight points'
+    // loads all in flight before any is used (one round trip per round)
+    for (int c0 = 0; c0 < nmax; c0 += 8 * V8_L) {
+      uint8_t ic[8];
+      int32_t kq[8], cq[8];
+      int64_t tq[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int pl = c0 + u * V8_L + j;
+        ic[u] = 0;
+        kq[u] = 0;
+        cq[u] = -1;
+        tq[u] = 0;
+        if (act && pl < n) {
+          const int64_t p = a + pl;
+          ic[u] = w.is_col[p];
+          kq[u] = w.ncand[p];
+          cq[u] = w.col_prev[p];
+          tq[u] = w.trans_off[p];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int pl = c0 + u * V8_L + j;
+        const bool valid = act && pl < n;
+        const bool col = valid && ic[u] != 0;
+        const int kp = kq[u];
+        wide_k = wide_k || (col && kp > V8_L);
+        const unsigned long long m = __ballot(col);
+        const uint32_t bits = (uint32_t)(m >> (g * V8_L)) & 0xFFu;
+        if (col) {
+          const int idx = nc + __popc(bits & ((1u << j) - 1u));
+          S.pl[g][idx] = (int8_t)pl;
+          S.kc[g][idx] = (int8_t)(kp < V8_L ? kp : V8_L);
+          S.fl[g][idx] = (uint8_t)(cq[u] >= 0 && kp > 0 ? 1 : 0);
+          S.toff[g][idx] = (int16_t)(tq[u] - t0);
+          S.pcol[g][pl] = (int8_t)idx;
+        } else if (valid) {
+          S.pcol[g][pl] = -1;
+        }
+        nc += __popc(bits);
+      }
+    }
+    {
+      const unsigned long long wm = __ballot(wide_k);
+      if (act && ((wm >> (g * V8_L)) & 0xFFull) != 0ull) {
+        if (j == 0) wide[atomicAdd(wide_n, 1)] = t;
+        act = false;
+      }
+    }
+    if (act && j == 0) S.toff[g][nc] = (int16_t)(w.trans_off[a + n] - t0);
+    if (!act) nc = 0;
+    __syncthreads();
+    // ---- forward pass
+    const int ncmax = wave_max_i(nc);
+    float prev = INFINITY;
+    bool open = false;
+    int last = -1, lastK = 0;
+    int thi = 0, ehi = 0;  // floats / points resident in the rings (absolute, from the trace's first)
+    const int ttot = act ? (int)S.toff[g][nc] : 0;
+    auto end_chain = [&]() {
+      // argmin (value, state) over the group's lanes < lastK
+      float bv = j < lastK ? prev : INFINITY;
+      int bi = j;
+#pragma unroll
+      for (int o = 4; o > 0; o >>= 1) {
+        const float ov = __shfl_xor(bv, o, V8_L);
+        const int oi = __shfl_xor(bi, o, V8_L);
+        if (ov < bv || (ov == bv && oi < bi)) {
+          bv = ov;
+          bi = oi;
+        }
+      }
+      if (j == 0) S.fl[g][last] = (uint8_t)(S.fl[g][last] | 4u | ((uint32_t)bi << 4));
+    };
+    for (int c = 0; c < ncmax; ++c) {
+      const bool on = c < nc;
+      // the rings: refill every group when any group's column c is not resident
+      const int need_t = on ? (int)S.toff[g][c + 1] : 0;
+      const int cpt = on ? (int)S.pl[g][c] : 0;
+      if (__ballot(on && (need_t > thi || cpt >= ehi)) != 0ull) {
+        if (on) {
+          // every load of the refill in flight at once (one round trip):
+          // <= V8_TW / 8 ring floats and V8_EP emission rows per lane
+          const int tlo = S.toff[g][c];
+          const int th2 = tlo + V8_TW < ttot ? tlo + V8_TW : ttot;
+          const int f0 = thi > tlo ? thi : tlo;
+          const int eh2 = cpt + V8_EP < n ? cpt + V8_EP : n;
+          const int e0 = ehi > cpt ? ehi : cpt;
+          float v[V8_TW / V8_L];
+          float ev[V8_EP];
+#pragma unroll
+          for (int u = 0; u < V8_TW / V8_L; ++u) {
+            const int f = f0 + u * V8_L + j;
+            v[u] = f < th2 ? w.trans[t0 + f] : 0.0f;
+          }
+#pragma unroll
+          for (int u = 0; u < V8_EP; ++u) ev[u] = e0 + u < eh2 ? w.cand_em[(a + e0 + u) * KIN + j] : 0.0f;
+#pragma unroll
+          for (int u = 0; u < V8_TW / V8_L; ++u) {
+            const int f = f0 + u * V8_L + j;
+            if (f < th2) S.t[g][f & (V8_TW - 1)] = v[u];
+          }
+#pragma unroll
+          for (int u = 0; u < V8_EP; ++u)
+            if (e0 + u < eh2) S.em[g][((e0 + u) & (V8_EP - 1)) * V8_L + j] = ev[u];
+          thi = th2;
+          ehi = eh2;
+        }
+        __syncthreads();
+      }
+      // the previous column's scores of the group, all lanes active
+      float pv[V8_L];
+#pragma unroll
+      for (int i = 0; i < V8_L; ++i) pv[i] = __shfl(prev, (lane & ~(V8_L - 1)) | i, TB);
+      if (on) {
+        const int Kp = S.kc[g][c];
+        const uint32_t f = S.fl[g][c];
+        const int pt = S.pl[g][c];
+        if (Kp == 0) {
+          if (open) end_chain();
+          open = false;
+        } else {
+          const float em = S.em[g][(pt & (V8_EP - 1)) * V8_L + (j < Kp ? j : 0)];
+          bool started = false;
+          float cur = INFINITY;
+          if (open && (f & 1u)) {
+            const int base = S.toff[g][c];
+            float best = INFINITY;
+            int bi = -1;
+#pragma unroll
+            for (int i = 0; i < V8_L; ++i) {
+              if (i < lastK) {
+                const float v = pv[i] + S.t[g][(base + i * Kp + (j < Kp ? j : 0)) & (V8_TW - 1)];
+                if (v < best) {
+                  best = v;
+                  bi = i;
+                }
+              }
+            }
+            const bool alive = j < Kp && bi >= 0;
+            cur = alive ? best + em : INFINITY;
+            // the group's backpointers, one nibble per state, into one word
+            uint32_t word = (uint32_t)(alive ? bi : 15) << (4 * j);
+#pragma unroll
+            for (int o = 4; o > 0; o >>= 1) word |= (uint32_t)__shfl_xor((int)word, o, V8_L);
+            if (j == 0) S.bp[g][c] = word;
+            if (((__ballot(alive) >> (g * V8_L)) & 0xFFull) != 0ull) {
+              started = true;
+            } else {
+              end_chain();
+            }
+          } else if (open) {
+            end_chain();
+          }
+          if (!started) {
+            cur = j < Kp ? em : INFINITY;
+            if (j == 0) S.fl[g][c] = (uint8_t)(S.fl[g][c] | 2u);
+          }
+          prev = cur;
+          open = true;
+          last = c;
+          lastK = Kp;
+        }
+      }
+    }
+    if (act && open) end_chain();
+    __syncthreads();
+    // ---- backtrack: a backward walk over the columns (one lane per group)
+    if (j == 0) {
+      int sv = -1;
+      for (int c = nc - 1; c >= 0; --c) {
+        const uint32_t f = S.fl[g][c];
+        const uint32_t word = S.bp[g][c];
+        if (f & 4u) sv = (int)((f >> 4) & 7u);
+        S.st[g][c] = (int8_t)sv;
+        if (sv >= 0) sv = (f & 2u) ? -1 : (int)((word >> (4 * sv)) & 15u);
+      }
+    }
+    __syncthreads();
+    // ---- outputs, point-parallel
+    if (act) {
+      for (int pl = j; pl < n; pl += V8_L) {
+        const int c = S.pcol[g][pl];
+        const int sv = c >= 0 ? (int)S.st[g][c] : -1;
+        const int64_t p = a + pl;
+        w.state[p] = sv;
+        w.chain_start[p] = (uint8_t)(c >= 0 && (S.fl[g][c] & 2u) ? 1 : 0);
+        if (sv >= 0) w.chosen[p] = crec(w, p, sv);
+      }
+    }
+    __syncthreads();
+  }
+}
+
 // ============================================================== K6 route
 // Steps the index tier could not answer (w.overflow_list0 / counters_i32[4]):
 // the winning search again, its target label's predecessor chain as the path.
-template <bool BIG>
+// TIER as k_transitions (spill lists: list0 [4] -> list2 [3] -> list3 [22])
+template <int TIER>
 __global__ __launch_bounds__(TB) void k_route(DevGraph g, DevBatch b, DevParams P, DevWork w) {
+  constexpr bool BIG = TIER > 0;
   if (*w.abort) return;
   __shared__ uint32_t lkey[BIG ? 1 : LDS_TABLE_CAP];
   __shared__ unsigned long long llab[BIG ? 1 : LDS_TABLE_CAP];
@@ -2249,21 +2591,15 @@ __global__ __launch_bounds__(TB) void k_route(DevGraph g, DevBatch b, DevParams 
   __shared__ SearchShared S;
   const int lane = threadIdx.x;
   for (int k = lane; k < TURN_TABLE; k += TB) TU[k] = P.turn_units[k];
-  Table T;
-  if (BIG) {
-    const size_t base = (size_t)blockIdx.x * BIG_TABLE_CAP;
-    T = Table{w.big_key + base, w.big_lab + base, w.big_inq + base, w.big_fr + 2 * base,
-              w.big_fr + 2 * base + BIG_TABLE_CAP, BIG_TABLE_LOG2, SEARCH_LIMIT,
-              w.big_ins + (size_t)blockIdx.x * SEARCH_LIMIT, w.big_prev + blockIdx.x};
-  } else {
-    T = Table{lkey, llab, linq, lfr0, lfr1, 8, LDS_TABLE_LIMIT};
-  }
+  Table T = tier_table<TIER>(w, lkey, llab, linq, lfr0, lfr1);
   auto predof = [&](uint32_t e) {
     const int sx = table_find<BIG>(T, e);
     return sx < 0 ? NONE_PRED : (uint32_t)(Mem<BIG>::ld(&T.lab[sx]) & 0xFFFFFFFFull);
   };
-  const int32_t* list = BIG ? w.overflow_list2 : w.overflow_list0;
-  const int64_t nwork = BIG ? (int64_t)w.counters_i32[3] : (int64_t)w.counters_i32[4];
+  const int32_t* list = TIER == 2 ? w.overflow_list3 : (BIG ? w.overflow_list2 : w.overflow_list0);
+  const int64_t nwork = TIER == 2 ? (int64_t)w.counters_i32[22]
+                                  : (BIG ? (int64_t)w.counters_i32[3] : (int64_t)w.counters_i32[4]);
+  if (TIER == 2 && huge_unready(w, nwork)) return;
   __syncthreads();
   for (int64_t it = blockIdx.x; it < nwork; it += gridDim.x) {
     const int64_t p = (int64_t)list[it];
@@ -2282,11 +2618,13 @@ __global__ __launch_bounds__(TB) void k_route(DevGraph g, DevBatch b, DevParams 
     const int labels = ta_search<BIG>(g, TU, T, S, u, hin, cq, lane);
     if (labels < 0) {
       if (lane == 0) {
-        if (!BIG) {
-          const int slot = atomicAdd(&w.counters_i32[3], 1);
-          w.overflow_list2[slot] = (int32_t)p;
+        if (TIER == 0) {
+          w.overflow_list2[atomicAdd(&w.counters_i32[3], 1)] = (int32_t)p;
+        } else if (TIER == 1) {
+          w.overflow_list3[atomicAdd(&w.counters_i32[22], 1)] = (int32_t)p;
         } else {
-          atomicCAS(&w.trace_err[w.pt_trace[p]], 0, OTM_TERR_SEARCH_OVERFLOW);
+          w.counters_i32[23] = 1;  // the huge tables are too small: grow, redo
+          *w.abort = 1;
         }
       }
       __syncthreads();
@@ -3426,7 +3764,10 @@ void launch_candidates(const DevGraph& g, const DevBatch& b, const DevParams& p,
                        const Marks& mk) {
   TIMED(KN_CAND_LANE, hipLaunchKernelGGL(k_cand_lane, dim3(order_grid(b.n_points, CAND_TB, 1 << 30)),
                                          dim3(CAND_TB), 0, s, g, b, p, w));
-  TIMED(KN_CAND_WAVE, hipLaunchKernelGGL(k_candidates, dim3(4096), dim3(TB), 0, s, g, b, p, w));
+  mk.begin(KN_CAND_WAVE, s);
+  hipLaunchKernelGGL(k_candidates<false>, dim3(4096), dim3(TB), 0, s, g, b, p, w);
+  hipLaunchKernelGGL(k_candidates<true>, dim3(CAND_BIG_SLOTS), dim3(TB), 0, s, g, b, p, w);
+  mk.end(KN_CAND_WAVE, s);
 }
 void launch_links(const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s, const Marks& mk) {
   TIMED(KN_LINKS, hipLaunchKernelGGL(k_links, dim3(grid_for(b.n_points + 1, 256, 1 << 30)), dim3(256), 0, s, b, p,
@@ -3466,19 +3807,43 @@ void launch_transitions(const DevGraph& g, const DevBatch& b, const DevParams& p
     mk.begin(KN_TRANS_WIDE, s);
     mk.end(KN_TRANS_WIDE, s);
   }
-  TIMED(KN_TRANS_WAVE, hipLaunchKernelGGL(k_transitions<false>, dim3(SPILL_GRID), dim3(TB), 0, s, g, b, p, w));
-  TIMED(KN_TRANS_GLOBAL, hipLaunchKernelGGL(k_transitions<true>, dim3(BIG_SLOTS), dim3(TB), 0, s, g, b, p, w));
+  TIMED(KN_TRANS_WAVE, hipLaunchKernelGGL(k_transitions<0>, dim3(SPILL_GRID), dim3(TB), 0, s, g, b, p, w));
+  mk.begin(KN_TRANS_GLOBAL, s);
+  hipLaunchKernelGGL(k_transitions<1>, dim3(BIG_SLOTS), dim3(TB), 0, s, g, b, p, w);
+  hipLaunchKernelGGL(k_transitions<2>, dim3(HUGE_SLOTS), dim3(TB), 0, s, g, b, p, w);
+  mk.end(KN_TRANS_GLOBAL, s);
 }
 void launch_viterbi(const DevBatch& b, DevWork& w, hipStream_t s, const Marks& mk) {
-  TIMED(KN_VITERBI, hipLaunchKernelGGL(k_viterbi, dim3(grid_for(b.n_traces, 1, WAVE_GRID_CAP)), dim3(TB), 0, s, b,
-                                       w));
+  static const bool sub = [] {
+    const char* e = std::getenv("OTM_VIT_SUB");  // A/B: 0 = the wave-per-trace form for every trace
+    return e ? std::atoi(e) != 0 : OTM_VIT_SUB != 0;
+  }();
+  if (!sub) {
+    TIMED(KN_VITERBI, hipLaunchKernelGGL(k_viterbi, dim3(grid_for(b.n_traces, 1, WAVE_GRID_CAP)), dim3(TB), 0, s, b,
+                                         w, (const int32_t*)nullptr, (const int32_t*)nullptr, 1));
+    return;
+  }
+  // eight traces per wave; the traces it cannot take (a column wider than 8
+  // candidates, longer than V8_PTS points) listed for the wave-per-trace form
+  // (list: overflow_list0, free between the transition and route stages;
+  // count: counters_i32[20], zeroed by K1)
+  int32_t* lst = w.overflow_list0;
+  int32_t* cnt = w.counters_i32 + 20;
+  mk.begin(KN_VITERBI, s);
+  hipLaunchKernelGGL(k_viterbi_sub, dim3(grid_for(b.n_traces, V8_T, WAVE_GRID_CAP)), dim3(TB), 0, s, b, w, lst, cnt);
+  hipLaunchKernelGGL(k_viterbi, dim3(grid_for(b.n_traces, 1, 1024)), dim3(TB), 0, s, b, w, (const int32_t*)lst,
+                     (const int32_t*)cnt, 0);
+  mk.end(KN_VITERBI, s);
 }
 void launch_route(const DevGraph& g, const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s,
                   const Marks& mk) {
   TIMED(KN_ROUTE_INDEX, hipLaunchKernelGGL(k_route_index, dim3(order_grid(b.n_points, 256, 1 << 30)), dim3(256), 0,
                                            s, g, b, p, w));
-  TIMED(KN_ROUTE_WAVE, hipLaunchKernelGGL(k_route<false>, dim3(SPILL_GRID), dim3(TB), 0, s, g, b, p, w));
-  TIMED(KN_ROUTE_GLOBAL, hipLaunchKernelGGL(k_route<true>, dim3(BIG_SLOTS), dim3(TB), 0, s, g, b, p, w));
+  TIMED(KN_ROUTE_WAVE, hipLaunchKernelGGL(k_route<0>, dim3(SPILL_GRID), dim3(TB), 0, s, g, b, p, w));
+  mk.begin(KN_ROUTE_GLOBAL, s);
+  hipLaunchKernelGGL(k_route<1>, dim3(BIG_SLOTS), dim3(TB), 0, s, g, b, p, w);
+  hipLaunchKernelGGL(k_route<2>, dim3(HUGE_SLOTS), dim3(TB), 0, s, g, b, p, w);
+  mk.end(KN_ROUTE_GLOBAL, s);
 }
 void launch_segments(const DevGraph& g, const DevBatch& b, DevWork& w, DevOut& o, bool write, hipStream_t s,
                      const Marks& mk) {

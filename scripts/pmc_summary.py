@@ -34,7 +34,10 @@ def short(name):
         return "k_segments_large"
     alias = {"k_trans_lane<32>": "k_trans_lane", "k_transitions<false>": "k_transitions",
              "k_transitions<true>": "k_transitions_big", "k_route_lane<24>": "k_route_lane",
-             "k_route<false>": "k_route", "k_route<true>": "k_route_big", "k_segments<true>": "k_segments",
+             "k_route<false>": "k_route", "k_route<true>": "k_route_big",
+             "k_transitions<0>": "k_transitions", "k_transitions<1>": "k_transitions_big",
+             "k_transitions<2>": "k_transitions_huge", "k_route<0>": "k_route", "k_route<1>": "k_route_big",
+             "k_route<2>": "k_route_huge", "k_segments<true>": "k_segments",
              "k_segments<128, 256>": "k_segments", "k_segments<256, 512>": "k_segments_large",
              # the transition index tier's launch slot (otm_kernel_name) runs one of these forms
              "k_trans_sub<4, false>": "k_trans_sub", "k_trans_sub<8, false>": "k_trans_sub", "k_trans_sub<16, false>": "k_trans_sub",

@@ -155,3 +155,23 @@ def straight_road(path, lat=40.0, lon0=0.0, step_deg=0.001, n_nodes=5, two_way=T
             edges.append(dict(**{"from": i + 1, "to": i}, way=100 + i, seg=-1, level=0))
     ids = write(path, nodes, edges, segs)
     return path, [ids[2 * i if two_way else i] for i in range(n_nodes - 1)]
+
+
+def star(path, lat=40.0, lon=0.0, n_spokes=200, length_m=90.0):
+    """A hub with n_spokes two-way straight spokes of length_m, evenly spread
+    in bearing: 2 x n_spokes directed edges within length_m of the hub (the
+    dense-intersection case past the LDS candidate tier's MAX_HITS).  Each
+    outbound spoke is its own level-0 segment (id (i + 1) << 3); inbound
+    spokes carry none.  Returns (path, outbound edge ids, inbound edge ids)."""
+    ls = MPD * math.cos(math.radians(lat))
+    nodes = [(lat, lon)]
+    edges, segs = [], []
+    for i in range(n_spokes):
+        a = 2.0 * math.pi * i / n_spokes
+        nodes.append((lat + length_m * math.cos(a) / MPD, lon + length_m * math.sin(a) / ls))
+        segs.append(((i + 1) << 3, None))
+        edges.append(dict(**{"from": 0, "to": i + 1}, way=5000 + i, seg=i, seg_pos=0, flags=SEG_BEGIN | SEG_END,
+                          level=0))
+        edges.append(dict(**{"from": i + 1, "to": 0}, way=5000 + i, seg=-1, level=0))
+    ids = write(path, nodes, edges, segs)
+    return path, [ids[2 * i] for i in range(n_spokes)], [ids[2 * i + 1] for i in range(n_spokes)]

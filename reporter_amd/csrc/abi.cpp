@@ -286,6 +286,53 @@ bool json_profile() {
 }
 thread_local double t_gpu_ms = 0.0, t_pack_ms = 0.0, t_write_ms = 0.0, t_extract_ms = 0.0;
 
+// The reference's stderr line per invalid speed (reporter_service.py): to
+// stderr, or -- inside a chunk of a pipelined call -- to the chunk's buffer,
+// which the caller prints in chunk order once every chunk is done
+thread_local std::string* t_errbuf = nullptr;
+void speed_lines(int n) {
+  for (int q = 0; q < n; ++q) {
+    if (t_errbuf) t_errbuf->append("Speed exceeds 200kph\n");
+    else std::fputs("Speed exceeds 200kph\n", stderr);
+  }
+}
+
+// A batch's turn in an H2DOrder (engine.h): the constructor waits until
+// every earlier ticket has queued its request copies; after() queues E's
+// copies behind them on the device; pass() marks E's copies for the next
+// ticket and hands the turn on (the destructor does, on any early exit).
+class H2DTurn {
+ public:
+  H2DTurn(otm::H2DOrder* o, uint64_t t) : o_(o), t_(t) {
+    if (!o_) return;
+    std::unique_lock<std::mutex> lk(o_->m);
+    o_->cv.wait(lk, [&] { return o_->next == t_; });
+  }
+  void after(otm_engine* E) {
+    if (o_ && t_ > 0 && o_->ev[(t_ - 1) & 1]) (void)otm::engine_push_after(E, o_->ev[(t_ - 1) & 1]);
+  }
+  void pass(otm_engine* E) {
+    if (!o_ || passed_) return;
+    passed_ = true;
+    hipEvent_t& ev = o_->ev[t_ & 1];
+    if (E && !ev) (void)hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+    if (E && ev) (void)otm::engine_push_mark(E, ev);
+    {
+      std::lock_guard<std::mutex> lk(o_->m);
+      o_->next = t_ + 1;
+    }
+    o_->cv.notify_all();
+  }
+  ~H2DTurn() { pass(nullptr); }
+  H2DTurn(const H2DTurn&) = delete;
+  H2DTurn& operator=(const H2DTurn&) = delete;
+
+ private:
+  otm::H2DOrder* o_;
+  uint64_t t_;
+  bool passed_ = false;
+};
+
 // One request of a batch: its DOM (parse_request), or -- for the Java
 // batcher's own bytes -- its points and uuid read directly (fast_request).
 struct Req {
@@ -420,7 +467,7 @@ void run_requests(otm_engine* E, std::vector<Req>& rq, std::vector<int>& codes, 
       if (!match_only)
         for (size_t n = 0; n < which.size(); ++n) {
           const int inv = r.traces[n].code == 200 ? r.traces[n].invalid_speeds : 0;
-          for (int q = 0; q < inv; ++q) std::fputs("Speed exceeds 200kph\n", stderr);
+          speed_lines(inv);
         }
       t_write_ms = now_ms() - tg1;
     }
@@ -728,7 +775,9 @@ bool gpu_writer() {
 // writer leaves (a 500, a float outside its range) is written on the host
 // from the batch's typed records.
 void report_many_device(otm_engine* E, int n, const char* const* reqs, const size_t* lens, int* codes,
-                        char** resps, size_t* resp_lens, const void* const* pinned) {
+                        char** resps, size_t* resp_lens, const void* const* pinned, otm::H2DOrder* ord,
+                        uint64_t ticket) {
+  H2DTurn turn(ord, ticket);  // (before the context's lock: a turn never waits holding one)
   const double t0 = now_ms();
   std::vector<int> rest;  // left to the host readers
   std::vector<int> inv;   // invalid speeds per GPU-read request (stderr lines)
@@ -747,6 +796,7 @@ void report_many_device(otm_engine* E, int n, const char* const* reqs, const siz
     bool all_pinned = pinned != nullptr;
     for (int k = 0; all_pinned && k < n; ++k) all_pinned = pinned[k] != nullptr;
     rc = otm::engine_stage_requests(E, n, bytes, !all_pinned, &off, &dst, &err);
+    turn.after(E);
     if (!rc) {
       off[0] = 0;
       for (int k = 0; k < n; ++k) off[k + 1] = off[k] + (int64_t)lens[k];
@@ -782,6 +832,7 @@ void report_many_device(otm_engine* E, int n, const char* const* reqs, const siz
       }
       if (!rc && n == 0) rc = otm::engine_push_requests(E, n, bytes, 0, 0, nullptr, 0, &err);
     }
+    turn.pass(E);
     if (!rc) {
       t1 = now_ms();
       const uint8_t* ok = nullptr;
@@ -893,7 +944,7 @@ void report_many_device(otm_engine* E, int n, const char* const* reqs, const siz
   }
   // the reference's stderr lines of the GPU-read requests, in request order
   for (size_t m = 0; m < which.size(); ++m)
-    for (int q = 0; q < inv[m]; ++q) std::fputs("Speed exceeds 200kph\n", stderr);
+    speed_lines(inv[m]);
   if (!rest.empty()) {
     const size_t nr = rest.size();
     std::vector<const char*> rq(nr);
@@ -922,14 +973,107 @@ void report_many_device(otm_engine* E, int n, const char* const* reqs, const siz
                  n, rest.size(), t1 - t0, t2 - t1, t3 - t2, now_ms() - t3);
 }
 
-// (pinned[k]: the page-locked submission slab body k lies in, or null)
+// (pinned[k]: the page-locked submission slab body k lies in, or null;
+// ord / ticket: the batch's place in an H2DOrder, or null)
 void report_many(otm_engine* E, int n, const char* const* reqs, const size_t* lens, int* codes, char** resps,
-                 size_t* resp_lens, const void* const* pinned = nullptr) {
+                 size_t* resp_lens, const void* const* pinned = nullptr, otm::H2DOrder* ord = nullptr,
+                 uint64_t ticket = 0) {
   // the batch buffers, pinned staging and copy streams this thread creates
   // belong on the engine's device, whatever device the calling thread is on
   if (E->members.empty() && E->device >= 0) (void)hipSetDevice(E->device);
-  if (gpu_reader(E, n)) report_many_device(E, n, reqs, lens, codes, resps, resp_lens, pinned);
-  else report_many_host(E, n, reqs, lens, codes, resps, resp_lens);
+  if (gpu_reader(E, n)) {
+    report_many_device(E, n, reqs, lens, codes, resps, resp_lens, pinned, ord, ticket);
+  } else {
+    H2DTurn(ord, ticket).pass(nullptr);  // (no copies of its own: the turn moves on)
+    report_many_host(E, n, reqs, lens, codes, resps, resp_lens);
+  }
+}
+
+// A large otm_report_batch as a pipeline (OTM_PIPE_CHUNKS, default 4, chunks
+// of about equal bytes; batches under OTM_PIPE_MIN requests, default 4096,
+// stay whole): chunk k runs on its own batch context (this engine, then its
+// pipeline clones) on its own thread, the chunks' request copies cross the
+// link one after another in chunk order (H2DOrder), so chunk k+1's bytes move
+// while chunk k runs its kernels and chunk k's responses come back while k+1
+// runs.  Each chunk is the same request/response contract as a whole batch
+// (every response depends only on its own request); the stderr lines come
+// out in chunk order.
+int pipe_chunks() {
+  const char* e = std::getenv("OTM_PIPE_CHUNKS");
+  return e ? std::max(1, std::min(8, std::atoi(e))) : 4;
+}
+int pipe_min() {
+  const char* e = std::getenv("OTM_PIPE_MIN");
+  return e ? std::max(2, std::atoi(e)) : 4096;
+}
+
+void report_many_pipelined(otm_engine* E, int n, const char* const* reqs, const size_t* lens, int* codes,
+                           char** resps, size_t* resp_lens) {
+  int C = pipe_chunks();
+  if (!gpu_reader(E, n) || !E->members.empty() || E->parent || n < pipe_min() || C < 2) {
+    report_many(E, n, reqs, lens, codes, resps, resp_lens);
+    return;
+  }
+  std::vector<otm_engine*> ctx{E};
+  {
+    std::lock_guard<std::mutex> lk(E->pmu);
+    while ((int)E->pctx.size() < C - 1) {
+      otm_engine* X = nullptr;
+      if (otm_engine_clone(E, &X) != OTM_OK) break;  // fewer chunks, same results
+      E->pctx.push_back(X);
+    }
+    for (int k = 0; k < C - 1 && k < (int)E->pctx.size(); ++k) ctx.push_back(E->pctx[(size_t)k]);
+  }
+  C = (int)ctx.size();
+  size_t total = 0;
+  for (int k = 0; k < n; ++k) total += lens[k];
+  std::vector<int> cut((size_t)C + 1, n);
+  cut[0] = 0;
+  size_t acc = 0;
+  for (int k = 0, c = 1; k < n && c < C; ++k) {
+    acc += lens[k];
+    if (acc * (size_t)C >= total * (size_t)c) cut[(size_t)c++] = k + 1;
+  }
+  for (int c = 1; c <= C; ++c) cut[(size_t)c] = std::max(cut[(size_t)c], cut[(size_t)c - 1]);
+  otm::H2DOrder ord;
+  std::vector<std::string> lines((size_t)C);
+  std::vector<std::exception_ptr> errs((size_t)C);
+  auto chunk = [&](int c) {
+    std::string* saved = t_errbuf;
+    t_errbuf = &lines[(size_t)c];
+    try {
+      const int a = cut[(size_t)c], m = cut[(size_t)c + 1] - a;
+      report_many(ctx[(size_t)c], m, reqs + a, lens + a, codes + a, resps + a, resp_lens + a, nullptr, &ord,
+                  (uint64_t)c);
+    } catch (...) {
+      errs[(size_t)c] = std::current_exception();
+    }
+    t_errbuf = saved;
+  };
+  for (int k = 0; k < n; ++k) resps[k] = nullptr;
+  std::vector<std::thread> th;
+  std::vector<int> here{0};  // chunks on the caller, in chunk order
+  for (int c = 1; c < C; ++c) {
+    try {
+      th.emplace_back(chunk, c);
+    } catch (...) {
+      here.push_back(c);  // no thread to be had: on the caller, after the earlier chunks
+    }
+  }
+  for (int c : here) chunk(c);
+  for (auto& t : th) t.join();
+  for (hipEvent_t ev : ord.ev)
+    if (ev) (void)hipEventDestroy(ev);
+  for (auto& x : errs)
+    if (x) {
+      for (int k = 0; k < n; ++k) {
+        arena::free_body(resps[k]);
+        resps[k] = nullptr;
+      }
+      std::rethrow_exception(x);  // to the entry point's guard
+    }
+  for (const std::string& s : lines)
+    if (!s.empty()) std::fputs(s.c_str(), stderr);
 }
 
 // Requests per async batch (OTM_ASYNC_BATCH): small enough that a burst of
@@ -947,6 +1091,16 @@ int async_workers(const otm_engine* E) {
   if (!E->members.empty() || E->parent) return 1;
   const char* e = std::getenv("OTM_ASYNC_WORKERS");
   return e ? std::max(1, std::min(8, std::atoi(e))) : 3;
+}
+
+// The workers' request copies in take order (H2DOrder; OTM_ASYNC_ORDER=0:
+// each as soon as its worker stages it, the A/B)
+bool async_ordered() {
+  static const bool on = [] {
+    const char* v = std::getenv("OTM_ASYNC_ORDER");
+    return !(v && *v == '0');
+  }();
+  return on;
 }
 
 // Worker wi of the async pipeline: take the next batch (in submit order, a
@@ -990,7 +1144,8 @@ void worker_loop(otm_engine* E, int wi) {
     }
     const double tw0 = now_ms();
     try {
-      report_many(ctx, n, reqs.data(), lens.data(), codes.data(), resps.data(), rl.data(), pin.data());
+      report_many(ctx, n, reqs.data(), lens.data(), codes.data(), resps.data(), rl.data(), pin.data(),
+                  async_ordered() ? &E->aorder : nullptr, seq);
     } catch (...) {
       // out of host memory (report_many freed what it made): the batch's
       // requests complete with a null body and code 500
@@ -1275,7 +1430,10 @@ void otm_engine_destroy(otm_engine* E) {
     for (auto& t : E->workers) t.join();  // (queued requests are finished first)
     for (auto& r : E->done) arena::free_body(r.body);
     for (otm_engine* C : E->actx) otm_engine_destroy(C);
+    for (hipEvent_t ev : E->aorder.ev)
+      if (ev) (void)hipEventDestroy(ev);
   }
+  for (otm_engine* C : E->pctx) otm_engine_destroy(C);
   if (!E->members.empty()) {
     otm::member_pool_free(E);
     for (otm_engine* m : E->members) otm_engine_destroy(m);
@@ -1305,7 +1463,7 @@ static int otm_report_impl(otm_engine* E, const char* req, size_t len, char** re
 static int otm_report_batch_impl(otm_engine* E, int n, const char* const* reqs, const size_t* lens, char** resps,
                      size_t* resp_lens, int* codes) {
   if (!E || n < 0) return fail(OTM_EINVAL, "bad arguments");
-  report_many(E, n, reqs, lens, codes, resps, resp_lens);
+  report_many_pipelined(E, n, reqs, lens, codes, resps, resp_lens);
   return OTM_OK;
 }
 
@@ -1470,7 +1628,7 @@ static int otm_report_segments_device_impl(otm_engine* E, int n, const char* con
       c[(size_t)k] = otm::write_report_response(r, t, &out, &matcher[(size_t)k]);
       bodies[(size_t)k] = std::move(out);
       const int inv = tr[(size_t)t].code == 200 ? tr[(size_t)t].invalid_speeds : 0;
-      for (int q = 0; q < inv; ++q) std::fputs("Speed exceeds 200kph\n", stderr);
+      speed_lines(inv);
     }
   }
   for (int k = 0; k < n; ++k) {

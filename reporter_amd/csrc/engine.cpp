@@ -702,6 +702,16 @@ static int engine_match_once(otm_engine* E, const DevBatch& b, hipStream_t s, st
     mk.begin(KN_ORDER, s);
     mk.end(KN_ORDER, s);
   }
+  if (E->cand_log2 > 0) {  // k_candidates<true> clears its tables per probe
+    const size_t n = (size_t)CAND_BIG_SLOTS << E->cand_log2;
+    if ((rc = ensure(E->cbig_key, n * 4, err))) return rc;
+    if ((rc = ensure(E->cbig_val, n * 8, err))) return rc;
+    if ((rc = ensure(E->cbig_skey, n / 2 * 8, err))) return rc;
+  }
+  w.cbig_key = P<uint32_t>(E->cbig_key);
+  w.cbig_val = P<unsigned long long>(E->cbig_val);
+  w.cbig_skey = P<unsigned long long>(E->cbig_skey);
+  w.cand_log2 = E->cand_log2;
   launch_candidates(E->g, b, dp, w, s, mk);
   // spill snapshot A: candidate probes the lane tier handed to the wave tier;
   // the counters start over for the transition tiers (links, scan and the
@@ -730,16 +740,6 @@ static int engine_match_once(otm_engine* E, const DevBatch& b, hipStream_t s, st
   w.huge_ins = P<uint32_t>(E->huge_ins);
   w.huge_prev = P<int32_t>(E->huge_prev);
   w.huge_log2 = E->huge_log2;
-  if (E->cand_log2 > 0) {  // k_candidates<true> clears its tables per probe
-    const size_t n = (size_t)CAND_BIG_SLOTS << E->cand_log2;
-    if ((rc = ensure(E->cbig_key, n * 4, err))) return rc;
-    if ((rc = ensure(E->cbig_val, n * 8, err))) return rc;
-    if ((rc = ensure(E->cbig_skey, n / 2 * 8, err))) return rc;
-  }
-  w.cbig_key = P<uint32_t>(E->cbig_key);
-  w.cbig_val = P<unsigned long long>(E->cbig_val);
-  w.cbig_skey = P<unsigned long long>(E->cbig_skey);
-  w.cand_log2 = E->cand_log2;
   launch_transitions(E->g, b, dp, w, s, mk, E->trans_lanes);
   // spill snapshot B: columns per transition tier (Viterbi does not touch
   // the counters; they start over for the route tiers)
@@ -1035,6 +1035,16 @@ int engine_push_requests(otm_engine* E, int32_t n, size_t bytes, size_t from, si
   read_requests(E, n, upto < n ? upto : n);
   HIPCHK(hipGetLastError());
   return OTM_OK;
+}
+
+int engine_push_after(otm_engine* E, hipEvent_t ev) {
+  if (!E->req_copy && hipStreamCreateWithFlags(&E->req_copy, hipStreamNonBlocking) != hipSuccess) return OTM_EDEVICE;
+  return hipStreamWaitEvent(E->req_copy, ev, 0) == hipSuccess ? OTM_OK : OTM_EDEVICE;
+}
+
+int engine_push_mark(otm_engine* E, hipEvent_t ev) {
+  if (!E->req_copy && hipStreamCreateWithFlags(&E->req_copy, hipStreamNonBlocking) != hipSuccess) return OTM_EDEVICE;
+  return hipEventRecord(ev, E->req_copy) == hipSuccess ? OTM_OK : OTM_EDEVICE;
 }
 
 int engine_match_requests(otm_engine* E, int32_t n, size_t bytes, bool pushed, const uint8_t** ok,

@@ -23,6 +23,20 @@ struct ReqSlab {
   bool pinned = false;
 };
 
+namespace otm {
+// The order in which batch contexts copy request bytes to HBM (a pipelined
+// otm_report_batch's chunks; the async workers' batches): ticket t's copies
+// queue behind ticket t-1's on the device (ev[(t - 1) & 1], recorded on t-1's
+// copy stream), so the host-to-device link carries one batch at a time, in
+// order, while the earlier batches run their kernels (abi.cpp H2DTurn).
+struct H2DOrder {
+  std::mutex m;
+  std::condition_variable cv;
+  uint64_t next = 0;
+  hipEvent_t ev[2] = {nullptr, nullptr};
+};
+}  // namespace otm
+
 struct otm_engine {
   const otm_engine* parent = nullptr;  // a clone shares its parent's graph and index (otm_engine_clone)
   // a multi-device engine (otm_engine_create with ndev > 1, group.cpp): one
@@ -151,6 +165,11 @@ struct otm_engine {
   std::deque<otm_result> done;
   std::vector<std::thread> workers;
   std::vector<otm_engine*> actx;  // the workers' clones (worker i >= 1 runs on actx[i - 1])
+  otm::H2DOrder aorder;           // the workers' batches' copies, in take order
+  // a pipelined otm_report_batch (abi.cpp report_many_pipelined): chunk
+  // k >= 1 runs on pctx[k - 1] (made at the first such call)
+  std::mutex pmu;
+  std::vector<otm_engine*> pctx;
   uint64_t take_seq = 0, pub_seq = 0;
   bool stop = false;
   bool worker_started = false;
@@ -189,6 +208,10 @@ int engine_push_requests(otm_engine* E, int32_t n, size_t bytes, size_t from, si
                          int32_t upto, std::string* err);
 int engine_match_requests(otm_engine* E, int32_t n, size_t bytes, bool pushed, const uint8_t** ok,
                           int32_t* n_traces, std::string* err);
+// H2DOrder's two ends on E's request-copy stream: the copies E pushes next
+// wait for ev; ev marks the copies E has pushed so far
+int engine_push_after(otm_engine* E, hipEvent_t ev);
+int engine_push_mark(otm_engine* E, hipEvent_t ev);
 // The last batch's /report response bodies written on the GPU
 // (responses.hip) into a device blob of *total bytes: trace t's body is
 // blob[off[t], off[t + 1] - 1), NUL-terminated, unless host[t] (a 500, or a

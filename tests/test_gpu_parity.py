@@ -399,6 +399,43 @@ def test_json_report_path_byte_equal(small_graph, oracle):
             assert seen[k] == got[k]
 
 
+@pytest.mark.parametrize("chunks", ["2", "4"])
+def test_json_report_pipelined_chunks(small_graph, oracle, monkeypatch, capfd, chunks):
+    """otm_report_batch as a pipeline of chunks on their own batch contexts
+    (abi.cpp report_many_pipelined, H2DOrder): the same bodies as one batch,
+    and the stderr speed lines in the same order."""
+    b = synth.make_traces(small_graph, 60, 40, seed=23)
+    off = b["trace_off"]
+    bodies = []
+    for t in range(60):
+        a, e = off[t], off[t + 1]
+        idx = np.arange(a, e)
+        tm = b["time"][a:e].astype(np.int64)
+        if t % 7 == 3:  # every 8th point, 5 s apart: speeds past 200 km/h (stderr lines)
+            idx = idx[::8]
+            tm = tm[0] + 5 * np.arange(len(idx), dtype=np.int64)
+        bodies.append(encode_request("veh%d" % t, b["lat"][idx], b["lon"][idx], tm,
+                                     b["accuracy"][idx].astype(np.int32)))
+    bodies[10] = b"{"  # a 400 among them
+    bodies[20] = bodies[20].replace(b'"trace":', b'"trace" :')  # a body for the host readers
+    monkeypatch.setenv("OTM_PIPE_MIN", str(1 << 30))
+    with Engine(graph_path=small_graph) as eng:
+        capfd.readouterr()
+        whole = eng.report_batch(bodies)
+        _, err_whole = capfd.readouterr()
+        monkeypatch.setenv("OTM_PIPE_MIN", "2")
+        monkeypatch.setenv("OTM_PIPE_CHUNKS", chunks)
+        piped = eng.report_batch(bodies)
+        _, err_piped = capfd.readouterr()
+        again = eng.report_batch(bodies)  # the pipeline's contexts reused
+        capfd.readouterr()
+    assert piped == whole and again == whole
+    assert err_piped == err_whole and "Speed exceeds 200kph" in err_whole
+    g = oracle.Graph(small_graph)
+    for body, got in zip(bodies, whole):
+        assert got == oracle.handle_request(g, body), body[:80]
+
+
 def test_histogram_matches_reports(small_graph):
     import torch
     b = synth.make_traces(small_graph, 300, 100, seed=23)

@@ -2300,44 +2300,24 @@ __global__ __launch_bounds__(TB, OTM_VIT_WAVES) void k_viterbi(DevBatch b, DevWo
   }
 }
 
-// K5, eight traces per wavefront.  The wave-per-trace form
-// above issues every per-column instruction for 64 lanes of which Kq <= 8
-// hold states (config 2: 4.0 candidates per column, config 4: 3.0), and its
-// time is the SIMDs' issue rate over those instructions.  Here a group of
-// eight lanes decodes one trace (lane j = state j), eight traces per wave:
-//  * a group first lists its trace's columns (point, candidates, linked to
-//    the previous column, the transition block's offset) in LDS; a trace with
-//    a column of more than 8 candidates, more than V8_PTS points or an error
-//    goes to the list the wave-per-trace form takes after;
-//  * the forward pass runs over column steps, one per group per step; the
-//    transition blocks and the emissions stream through a per-group LDS ring,
-//    refilled for every group at once when any group's next column is not
-//    resident (one round trip for all eight);
-//  * a chain's end records its argmin state; the backtrack is a backward walk
-//    over the columns after the forward pass, with 4-bit backpointers packed
-//    in one word per column;
-//  * state, chain_start and the chosen candidate go out point-parallel.
+// K5, G lanes per trace (G = 8 or 16: 64 / G traces per wavefront; DESIGN.md
+// §5 K5).  The wave-per-trace form above is VALU-issue bound (round 3 PMC:
+// 534M VALU instructions over 10M points at config 4, 82 % of the SIMDs'
+// cycles) with Kq <= 8 of its 64 lanes holding states; here one instruction
+// stream steps 64 / G traces.  A group (lane j = state j) walks its trace's
+// points in order:
+//  * metadata of G points per round trip (lane k holds point c0 + k; a step
+//    reads it by shuffle), no LDS copy of the trace;
+//  * a column's emissions and its Kq x Kp transition block straight from HBM
+//    (the block is contiguous in the trace's stream), every load of a step in
+//    flight at once; the waves per SIMD hide the round trip;
+//  * a column's backpointers as four ballot bit planes (no shuffle chain), one
+//    word per point in LDS; a chain's end records its argmin state;
+//  * after the forward pass one lane per group walks the trace backward.
+// A trace with a column of more than G candidates, or more than VG_PTS
+// points, goes to the next form's list (G = 8 -> G = 16 -> the wave form).
 // Same recurrence (min over i in order, strict <), tie rules and chain breaks
 // as viterbi_trace_global: bit-identical to the oracle.
-#ifndef OTM_VIT_SUB
-#define OTM_VIT_SUB 0
-#endif
-constexpr int V8_L = 8;          // lanes (states) per trace
-constexpr int V8_T = TB / V8_L;  // traces per wave
-constexpr int V8_PTS = 128;      // points per trace
-constexpr int V8_TW = 256;       // transition ring per trace (floats, power of two, >= 2 * 64)
-constexpr int V8_EP = 16;        // emission ring per trace (points, power of two)
-struct V8Lds {
-  float t[V8_T][V8_TW];
-  float em[V8_T][V8_EP * V8_L];
-  uint32_t bp[V8_T][V8_PTS];       // per column: 4-bit backpointer of each state
-  int16_t toff[V8_T][V8_PTS + 1];  // per column: its block's first float (from the trace's first), [nc]: the end
-  int8_t pl[V8_T][V8_PTS];         // column -> point
-  int8_t pcol[V8_T][V8_PTS];       // point -> column, -1
-  int8_t kc[V8_T][V8_PTS];         // column -> candidates
-  uint8_t fl[V8_T][V8_PTS];        // column flags: 1 linked, 2 chain start, 4 chain end (argmin state in bits 4..6)
-  int8_t st[V8_T][V8_PTS];         // column -> decoded state
-};
 __device__ __forceinline__ int wave_max_i(int v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -2346,228 +2326,206 @@ __device__ __forceinline__ int wave_max_i(int v) {
   }
   return v;
 }
-__global__ __launch_bounds__(TB) void k_viterbi_sub(DevBatch b, DevWork w, int32_t* wide, int32_t* wide_n) {
+#ifndef OTM_VG_WAVES
+#define OTM_VG_WAVES 6
+#endif
+constexpr int VG_PTS = 128;  // points per trace
+constexpr uint8_t VG_COL = 1, VG_CS = 2, VG_END = 4;  // point flags (VG_END: argmin state in bits 3..7)
+template <int G>
+struct VgWord {
+  using T = uint32_t;
+};
+template <>
+struct VgWord<16> {
+  using T = unsigned long long;
+};
+template <int G>
+__global__ __launch_bounds__(TB, OTM_VG_WAVES) void k_viterbi_g(DevBatch b, DevWork w, const int32_t* list, const int32_t* list_n,
+                                                     int32_t* rej, int32_t* rej_n, int snap) {
+  static_assert(G == 8 || G == 16, "8 or 16 lanes per trace");
+  using Word = typename VgWord<G>::T;  // 4 bit planes of G backpointer bits
+  constexpr int NT = TB / G;
   // spill snapshot B (see k_viterbi)
-  if (OTM_FOLD_BOOKKEEPING && blockIdx.x == 0 && threadIdx.x == 0) fold_snap(w, 1, true);
+  if (OTM_FOLD_BOOKKEEPING && snap && blockIdx.x == 0 && threadIdx.x == 0) fold_snap(w, 1, true);
   if (*w.abort) return;
-  __shared__ V8Lds S;
+  __shared__ Word sBp[NT][VG_PTS];
+  __shared__ uint8_t sFl[NT][VG_PTS];  // flags; after the walk: VG_CS | (state + 1) << 3
   const int lane = threadIdx.x;
-  const int g = lane >> 3, j = lane & 7;
-  for (int32_t tb = blockIdx.x * V8_T; tb < b.n_traces; tb += gridDim.x * V8_T) {
-    const int32_t t = tb + g;
-    bool act = t < b.n_traces;
+  const int g = lane / G, j = lane % G, gb = g * G;
+  const Word gmask = (Word)(((unsigned long long)1 << G) - 1ull);
+  const int32_t ntr = list ? *list_n : b.n_traces;
+  for (int32_t tb = blockIdx.x * NT; tb < ntr; tb += gridDim.x * NT) {
+    const int32_t it = tb + g;
+    bool act = it < ntr;
+    const int32_t t = act ? (list ? list[it] : it) : 0;
     int64_t a = 0;
-    int n = 0, nc = 0;
+    int n = 0;
     int64_t t0 = 0;
     if (act) {
       a = b.trace_off[t];
       n = (int)(b.trace_off[t + 1] - a);
+      t0 = w.trans_off[a];
       if (w.trace_err[t] != 0) {
-        for (int pl = j; pl < n; pl += V8_L) {
+        for (int pl = j; pl < n; pl += G) {
           w.state[a + pl] = -1;
           w.chain_start[a + pl] = 0;
         }
         act = false;
-      } else if (n > V8_PTS) {
-        if (j == 0) wide[atomicAdd(wide_n, 1)] = t;
-        act = false;
-      } else {
-        t0 = w.trans_off[a];
       }
     }
-    // ---- the group's columns (wave-uniform trip count; groups predicated)
-    bool wide_k = false;
-    const int nmax = wave_max_i(act ? n : 0);
-    // 64 points of every group's trace per round: each lane's eight points'
-    // loads all in flight before any is used (one round trip per round)
-    for (int c0 = 0; c0 < nmax; c0 += 8 * V8_L) {
-      uint8_t ic[8];
-      int32_t kq[8], cq[8];
-      int64_t tq[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int pl = c0 + u * V8_L + j;
-        ic[u] = 0;
-        kq[u] = 0;
-        cq[u] = -1;
-        tq[u] = 0;
-        if (act && pl < n) {
-          const int64_t p = a + pl;
-          ic[u] = w.is_col[p];
-          kq[u] = w.ncand[p];
-          cq[u] = w.col_prev[p];
-          tq[u] = w.trans_off[p];
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int pl = c0 + u * V8_L + j;
-        const bool valid = act && pl < n;
-        const bool col = valid && ic[u] != 0;
-        const int kp = kq[u];
-        wide_k = wide_k || (col && kp > V8_L);
-        const unsigned long long m = __ballot(col);
-        const uint32_t bits = (uint32_t)(m >> (g * V8_L)) & 0xFFu;
-        if (col) {
-          const int idx = nc + __popc(bits & ((1u << j) - 1u));
-          S.pl[g][idx] = (int8_t)pl;
-          S.kc[g][idx] = (int8_t)(kp < V8_L ? kp : V8_L);
-          S.fl[g][idx] = (uint8_t)(cq[u] >= 0 && kp > 0 ? 1 : 0);
-          S.toff[g][idx] = (int16_t)(tq[u] - t0);
-          S.pcol[g][pl] = (int8_t)idx;
-        } else if (valid) {
-          S.pcol[g][pl] = -1;
-        }
-        nc += __popc(bits);
-      }
+    // a trace this form cannot take: to the next form's list
+    bool take = act && n <= VG_PTS;
+    if (take) {
+      bool wide = false;
+      for (int pl = j; pl < n; pl += G) wide = wide || (w.is_col[a + pl] && w.ncand[a + pl] > G);
+      take = ((__ballot(wide) >> gb) & (unsigned long long)gmask) == 0ull;
     }
-    {
-      const unsigned long long wm = __ballot(wide_k);
-      if (act && ((wm >> (g * V8_L)) & 0xFFull) != 0ull) {
-        if (j == 0) wide[atomicAdd(wide_n, 1)] = t;
-        act = false;
-      }
+    if (act && !take) {
+      if (j == 0) rej[atomicAdd(rej_n, 1)] = t;
+      act = false;
     }
-    if (act && j == 0) S.toff[g][nc] = (int16_t)(w.trans_off[a + n] - t0);
-    if (!act) nc = 0;
-    __syncthreads();
-    // ---- forward pass
-    const int ncmax = wave_max_i(nc);
+    if (!act) n = 0;
+    const int nmax = wave_max_i(n);
+    for (int pl = j; pl < n; pl += G) sFl[g][pl] = 0;
+    // ---- forward pass (wave-uniform step count; groups predicated)
     float prev = INFINITY;
     bool open = false;
     int last = -1, lastK = 0;
-    int thi = 0, ehi = 0;  // floats / points resident in the rings (absolute, from the trace's first)
-    const int ttot = act ? (int)S.toff[g][nc] : 0;
     auto end_chain = [&]() {
-      // argmin (value, state) over the group's lanes < lastK
+      // argmin (value, state) over the group's lanes < lastK, ties to the lower state
       float bv = j < lastK ? prev : INFINITY;
       int bi = j;
 #pragma unroll
-      for (int o = 4; o > 0; o >>= 1) {
-        const float ov = __shfl_xor(bv, o, V8_L);
-        const int oi = __shfl_xor(bi, o, V8_L);
+      for (int o = G / 2; o > 0; o >>= 1) {
+        const float ov = __shfl_xor(bv, o, G);
+        const int oi = __shfl_xor(bi, o, G);
         if (ov < bv || (ov == bv && oi < bi)) {
           bv = ov;
           bi = oi;
         }
       }
-      if (j == 0) S.fl[g][last] = (uint8_t)(S.fl[g][last] | 4u | ((uint32_t)bi << 4));
+      if (j == 0) sFl[g][last] = (uint8_t)(sFl[g][last] | VG_END | (bi << 3));
     };
-    for (int c = 0; c < ncmax; ++c) {
-      const bool on = c < nc;
-      // the rings: refill every group when any group's column c is not resident
-      const int need_t = on ? (int)S.toff[g][c + 1] : 0;
-      const int cpt = on ? (int)S.pl[g][c] : 0;
-      if (__ballot(on && (need_t > thi || cpt >= ehi)) != 0ull) {
-        if (on) {
-          // every load of the refill in flight at once (one round trip):
-          // <= V8_TW / 8 ring floats and V8_EP emission rows per lane
-          const int tlo = S.toff[g][c];
-          const int th2 = tlo + V8_TW < ttot ? tlo + V8_TW : ttot;
-          const int f0 = thi > tlo ? thi : tlo;
-          const int eh2 = cpt + V8_EP < n ? cpt + V8_EP : n;
-          const int e0 = ehi > cpt ? ehi : cpt;
-          float v[V8_TW / V8_L];
-          float ev[V8_EP];
-#pragma unroll
-          for (int u = 0; u < V8_TW / V8_L; ++u) {
-            const int f = f0 + u * V8_L + j;
-            v[u] = f < th2 ? w.trans[t0 + f] : 0.0f;
-          }
-#pragma unroll
-          for (int u = 0; u < V8_EP; ++u) ev[u] = e0 + u < eh2 ? w.cand_em[(a + e0 + u) * KIN + j] : 0.0f;
-#pragma unroll
-          for (int u = 0; u < V8_TW / V8_L; ++u) {
-            const int f = f0 + u * V8_L + j;
-            if (f < th2) S.t[g][f & (V8_TW - 1)] = v[u];
-          }
-#pragma unroll
-          for (int u = 0; u < V8_EP; ++u)
-            if (e0 + u < eh2) S.em[g][((e0 + u) & (V8_EP - 1)) * V8_L + j] = ev[u];
-          thi = th2;
-          ehi = eh2;
+    for (int c0 = 0; c0 < nmax; c0 += G) {
+      // G points' metadata, one per lane: flags | candidates, block offset
+      int m_k = 0, m_to = 0;
+      {
+        const int pl = c0 + j;
+        if (pl < n) {
+          const int64_t p = a + pl;
+          const int ic = w.is_col[p];
+          const int nc = w.ncand[p];
+          const int32_t q = w.col_prev[p];
+          m_to = (int)(w.trans_off[p] - t0);
+          m_k = ic ? (nc | 0x100 | (q >= 0 ? 0x200 : 0)) : 0;
         }
-        __syncthreads();
       }
-      // the previous column's scores of the group, all lanes active
-      float pv[V8_L];
-#pragma unroll
-      for (int i = 0; i < V8_L; ++i) pv[i] = __shfl(prev, (lane & ~(V8_L - 1)) | i, TB);
-      if (on) {
-        const int Kp = S.kc[g][c];
-        const uint32_t f = S.fl[g][c];
-        const int pt = S.pl[g][c];
-        if (Kp == 0) {
+      for (int k = 0; k < G; ++k) {
+        const int pl = c0 + k;
+        const int mk = __shfl(m_k, gb + k, TB);
+        const int to = __shfl(m_to, gb + k, TB);
+        const bool on = pl < n && (mk & 0x100);
+        const int Kp = mk & 0xFF;
+        if (on && Kp == 0) {
           if (open) end_chain();
           open = false;
-        } else {
-          const float em = S.em[g][(pt & (V8_EP - 1)) * V8_L + (j < Kp ? j : 0)];
-          bool started = false;
-          float cur = INFINITY;
-          if (open && (f & 1u)) {
-            const int base = S.toff[g][c];
-            float best = INFINITY;
-            int bi = -1;
+        }
+        const bool col = on && Kp > 0;
+        const bool link = col && open && (mk & 0x200);
+        const int64_t p = a + pl;
+        const int jj = j < Kp ? j : 0;
+        // every load of the step in flight before any is used
+        float em = 0.0f;
+        if (col) em = cemis(w, p, jj);
+        float tv[G];
 #pragma unroll
-            for (int i = 0; i < V8_L; ++i) {
-              if (i < lastK) {
-                const float v = pv[i] + S.t[g][(base + i * Kp + (j < Kp ? j : 0)) & (V8_TW - 1)];
-                if (v < best) {
-                  best = v;
-                  bi = i;
-                }
+        for (int i = 0; i < G; ++i) {
+          tv[i] = INFINITY;
+          if (__ballot(link && i < lastK) == 0ull) break;
+          if (link && i < lastK) tv[i] = w.trans[t0 + to + i * Kp + jj];
+        }
+        bool started = false;
+        float cur = INFINITY;
+        if (__ballot(link) != 0ull) {
+          float best = INFINITY;
+          int bi = -1;
+#pragma unroll
+          for (int i = 0; i < G; ++i) {
+            if (__ballot(link && i < lastK) == 0ull) break;
+            const float pv = __shfl(prev, gb + i, TB);
+            if (link && i < lastK) {
+              const float v = pv + tv[i];
+              if (v < best) {
+                best = v;
+                bi = i;
               }
             }
-            const bool alive = j < Kp && bi >= 0;
-            cur = alive ? best + em : INFINITY;
-            // the group's backpointers, one nibble per state, into one word
-            uint32_t word = (uint32_t)(alive ? bi : 15) << (4 * j);
-#pragma unroll
-            for (int o = 4; o > 0; o >>= 1) word |= (uint32_t)__shfl_xor((int)word, o, V8_L);
-            if (j == 0) S.bp[g][c] = word;
-            if (((__ballot(alive) >> (g * V8_L)) & 0xFFull) != 0ull) {
-              started = true;
-            } else {
-              end_chain();
-            }
-          } else if (open) {
-            end_chain();
           }
+          const bool alive = link && j < Kp && bi >= 0;
+          if (link) cur = alive ? best + em : INFINITY;
+          // the backpointers as four bit planes of the group's G bits
+          const int bb = alive ? bi : 15;
+          Word word = 0;
+#pragma unroll
+          for (int bit = 0; bit < 4; ++bit)
+            word |= (Word)((__ballot(((bb >> bit) & 1) != 0) >> gb) & (unsigned long long)gmask) << (bit * G);
+          if (link && j == 0) sBp[g][pl] = word;
+          const bool any = ((__ballot(alive) >> gb) & (unsigned long long)gmask) != 0ull;
+          if (link) {
+            if (any) started = true;
+            else end_chain();
+          }
+        }
+        if (col && !link && open) end_chain();
+        if (col) {
           if (!started) {
             cur = j < Kp ? em : INFINITY;
-            if (j == 0) S.fl[g][c] = (uint8_t)(S.fl[g][c] | 2u);
+            if (j == 0) sFl[g][pl] = VG_COL | VG_CS;
+          } else if (j == 0) {
+            sFl[g][pl] = VG_COL;
           }
           prev = cur;
           open = true;
-          last = c;
+          last = pl;
           lastK = Kp;
         }
       }
     }
     if (act && open) end_chain();
     __syncthreads();
-    // ---- backtrack: a backward walk over the columns (one lane per group)
+    // ---- backtrack: one lane per group walks the trace backward
     if (j == 0) {
       int sv = -1;
-      for (int c = nc - 1; c >= 0; --c) {
-        const uint32_t f = S.fl[g][c];
-        const uint32_t word = S.bp[g][c];
-        if (f & 4u) sv = (int)((f >> 4) & 7u);
-        S.st[g][c] = (int8_t)sv;
-        if (sv >= 0) sv = (f & 2u) ? -1 : (int)((word >> (4 * sv)) & 15u);
+      for (int pl = n - 1; pl >= 0; --pl) {
+        const uint32_t f = sFl[g][pl];
+        if (!(f & VG_COL)) {
+          sFl[g][pl] = 0;
+          continue;
+        }
+        if (f & VG_END) sv = (int)(f >> 3);
+        sFl[g][pl] = (uint8_t)((f & VG_CS) | ((sv + 1) << 3));
+        if (sv >= 0) {
+          if (f & VG_CS) {
+            sv = -1;
+          } else {
+            const Word wd = sBp[g][pl];
+            int x = 0;
+#pragma unroll
+            for (int bit = 0; bit < 4; ++bit) x |= (int)((wd >> (bit * G + sv)) & 1u) << bit;
+            sv = x;
+          }
+        }
       }
     }
     __syncthreads();
-    // ---- outputs, point-parallel
-    if (act) {
-      for (int pl = j; pl < n; pl += V8_L) {
-        const int c = S.pcol[g][pl];
-        const int sv = c >= 0 ? (int)S.st[g][c] : -1;
-        const int64_t p = a + pl;
-        w.state[p] = sv;
-        w.chain_start[p] = (uint8_t)(c >= 0 && (S.fl[g][c] & 2u) ? 1 : 0);
-        if (sv >= 0) w.chosen[p] = crec(w, p, sv);
-      }
+    // ---- outputs, point-parallel within the group
+    for (int pl = j; pl < n; pl += G) {
+      const uint32_t f = sFl[g][pl];
+      const int sv = (int)(f >> 3) - 1;
+      const int64_t p = a + pl;
+      w.state[p] = sv;
+      w.chain_start[p] = (uint8_t)((f & VG_CS) ? 1 : 0);
+      if (sv >= 0) w.chosen[p] = crec(w, p, sv);
     }
     __syncthreads();
   }
@@ -3814,25 +3772,36 @@ void launch_transitions(const DevGraph& g, const DevBatch& b, const DevParams& p
   mk.end(KN_TRANS_GLOBAL, s);
 }
 void launch_viterbi(const DevBatch& b, DevWork& w, hipStream_t s, const Marks& mk) {
-  static const bool sub = [] {
-    const char* e = std::getenv("OTM_VIT_SUB");  // A/B: 0 = the wave-per-trace form for every trace
-    return e ? std::atoi(e) != 0 : OTM_VIT_SUB != 0;
+  static const int form = [] {
+    const char* e = std::getenv("OTM_VIT_FORM");  // A/B: 64 = the wave-per-trace form for every trace
+    return e ? std::atoi(e) : 8;
   }();
-  if (!sub) {
+  if (form == 64) {
     TIMED(KN_VITERBI, hipLaunchKernelGGL(k_viterbi, dim3(grid_for(b.n_traces, 1, WAVE_GRID_CAP)), dim3(TB), 0, s, b,
                                          w, (const int32_t*)nullptr, (const int32_t*)nullptr, 1));
     return;
   }
-  // eight traces per wave; the traces it cannot take (a column wider than 8
-  // candidates, longer than V8_PTS points) listed for the wave-per-trace form
-  // (list: overflow_list0, free between the transition and route stages;
-  // count: counters_i32[20], zeroed by K1)
-  int32_t* lst = w.overflow_list0;
-  int32_t* cnt = w.counters_i32 + 20;
+  // 8 lanes per trace over every trace; what it cannot take (a column wider
+  // than 8 candidates, more than VG_PTS points) to 16 lanes per trace; what
+  // that cannot take to the wave-per-trace form.  Lists: overflow_list0 (count
+  // counters_i32[20]) and overflow_list2 ([26]), both free between the
+  // transition and route stages; the counts are zeroed by K1.
+  int32_t* l8 = w.overflow_list0;
+  int32_t* n8 = w.counters_i32 + 20;
+  int32_t* l16 = w.overflow_list2;
+  int32_t* n16 = w.counters_i32 + 26;
   mk.begin(KN_VITERBI, s);
-  hipLaunchKernelGGL(k_viterbi_sub, dim3(grid_for(b.n_traces, V8_T, WAVE_GRID_CAP)), dim3(TB), 0, s, b, w, lst, cnt);
-  hipLaunchKernelGGL(k_viterbi, dim3(grid_for(b.n_traces, 1, 1024)), dim3(TB), 0, s, b, w, (const int32_t*)lst,
-                     (const int32_t*)cnt, 0);
+  if (form == 16) {
+    hipLaunchKernelGGL(k_viterbi_g<16>, dim3(grid_for(b.n_traces, TB / 16, WAVE_GRID_CAP)), dim3(TB), 0, s, b, w,
+                       (const int32_t*)nullptr, (const int32_t*)nullptr, l16, n16, 1);
+  } else {
+    hipLaunchKernelGGL(k_viterbi_g<8>, dim3(grid_for(b.n_traces, TB / 8, WAVE_GRID_CAP)), dim3(TB), 0, s, b, w,
+                       (const int32_t*)nullptr, (const int32_t*)nullptr, l8, n8, 1);
+    hipLaunchKernelGGL(k_viterbi_g<16>, dim3(grid_for(b.n_traces / 8 + 1, TB / 16, 2048)), dim3(TB), 0, s, b, w,
+                       (const int32_t*)l8, (const int32_t*)n8, l16, n16, 0);
+  }
+  hipLaunchKernelGGL(k_viterbi, dim3(grid_for(b.n_traces / 64 + 1, 1, 1024)), dim3(TB), 0, s, b, w,
+                     (const int32_t*)l16, (const int32_t*)n16, 0);
   mk.end(KN_VITERBI, s);
 }
 void launch_route(const DevGraph& g, const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s,

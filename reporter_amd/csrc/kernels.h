@@ -97,7 +97,7 @@ struct DevOrder {
 // = NODE_KEY | node), as one open-addressing hash table per row (linear
 // probing).  A slot is {key, cost, route distance bits, turn units}: the
 // route to the edge's start turned into it (or to the node), so a transition
-// reads its distance and turn cost from one slot; predecessor edges in a
+// reads its distance and turn cost from one slot; predecessor slots in a
 // parallel array give the route.  cnt < 0 marks a row whose search exceeded
 // the build table (queries on it use the online tiers).
 struct IdxRow {
@@ -110,7 +110,7 @@ struct DevIndex {
   uint32_t cmax;  // its cost bound, floor(rmax x 64)
   const IdxRow* row;   // [E + N]
   const uint4* slot;
-  const int32_t* pred;   // per slot
+  const int32_t* pred;   // per slot: its label's predecessor's slot in the row (-1: the route's first edge)
 };
 constexpr uint32_t NODE_KEY = 0x80000000u;  // key of a node's arrival label (edges: their id, < 2^27)
 constexpr uint32_t NONE_PRED = 0xFFFFFFFFu; // label predecessor of a route's first edge / the source node

@@ -1294,9 +1294,25 @@ __device__ __forceinline__ uint32_t idx_hash(uint32_t v) {
 #ifndef OTM_IDX_LOAD_PCT
 #define OTM_IDX_LOAD_PCT 20
 #endif
+// OTM_IDX_HOME = 1 (round 4): a label's home in a row's table is its road's
+// lower-numbered node (an edge key: min(from, to); a node key: the node), and
+// a home hashes to an aligned group of IDX_GROUP slots, one 128-B line; linear
+// probing from there.  The labels a column probes in one row are its target
+// candidates -- a node and the two directions of the roads at it -- so they
+// share a few homes (0.42 homes per key on config 2, 0.45 on config 4,
+// against one line per key with a home per key: OTM_IDX_HOME = 0).  Rows are
+// whole groups, so every row starts on a line.
+#ifndef OTM_IDX_HOME
+#define OTM_IDX_HOME 1
+#endif
+constexpr int IDX_GROUP = 8;
 __host__ __device__ __forceinline__ int64_t idx_row_cap(int32_t c) {
   if (c <= 0) return 0;
-#if OTM_IDX_LOAD_PCT
+#if OTM_IDX_HOME
+  int64_t cap = ((int64_t)c * 100 + OTM_IDX_LOAD_PCT - 1) / OTM_IDX_LOAD_PCT;
+  if (cap <= c) cap = (int64_t)c + 1;
+  return (cap + IDX_GROUP - 1) / IDX_GROUP * IDX_GROUP;
+#elif OTM_IDX_LOAD_PCT
   const int64_t cap = ((int64_t)c * 100 + OTM_IDX_LOAD_PCT - 1) / OTM_IDX_LOAD_PCT;
   return cap > c ? cap : (int64_t)c + 1;
 #else
@@ -1305,11 +1321,25 @@ __host__ __device__ __forceinline__ int64_t idx_row_cap(int32_t c) {
   return cap;
 #endif
 }
-__device__ __forceinline__ uint32_t idx_slot0(uint32_t v, const IdxRow& R) {
-#if OTM_IDX_LOAD_PCT
-  return (uint32_t)(((uint64_t)idx_hash(v) * (uint64_t)R.cap) >> 32);
+// the hash of a label's home (the lookups of a column compute it once per target)
+__device__ __forceinline__ uint32_t idx_home_hash(const DevGraph& g, uint32_t key) {
+#if OTM_IDX_HOME
+  if (key & NODE_KEY) return idx_hash(key & ~NODE_KEY);
+  const uint32_t u = (uint32_t)g.e_from[key], v = (uint32_t)g.e_to[key];
+  return idx_hash(u < v ? u : v);
 #else
-  return idx_hash(v) & (R.cap - 1u);
+  (void)g;
+  return idx_hash(key);
+#endif
+}
+// first slot of a label in row R from its home hash
+__device__ __forceinline__ uint32_t idx_slot0(uint32_t hh, const IdxRow& R) {
+#if OTM_IDX_HOME
+  return (uint32_t)(((uint64_t)hh * (uint64_t)(R.cap / IDX_GROUP)) >> 32) * IDX_GROUP;
+#elif OTM_IDX_LOAD_PCT
+  return (uint32_t)(((uint64_t)hh * (uint64_t)R.cap) >> 32);
+#else
+  return hh & (R.cap - 1u);
 #endif
 }
 __device__ __forceinline__ uint32_t idx_next(uint32_t h, const IdxRow& R) {
@@ -1319,10 +1349,11 @@ __device__ __forceinline__ uint32_t idx_next(uint32_t h, const IdxRow& R) {
 // Row lookup: linear probing in the row's table.  Returns the slot (its
 // contents in *out) when the key is in the row, -1 when absent (its label
 // beyond cmax), -2 when the row is incomplete.
-__device__ __forceinline__ int64_t idx_find(const DevIndex& X, const IdxRow& R, uint32_t v, uint4& out) {
+__device__ __forceinline__ int64_t idx_find(const DevGraph& g, const DevIndex& X, const IdxRow& R, uint32_t v,
+                                            uint4& out) {
   if (R.cnt < 0) return -2;
   if (R.cnt == 0) return -1;
-  uint32_t h = idx_slot0(v, R);
+  uint32_t h = idx_slot0(idx_home_hash(g, v), R);
   while (true) {
     const uint4 sl = X.slot[R.off + h];
     if (sl.x == v) {
@@ -1347,8 +1378,9 @@ __device__ __forceinline__ uint32_t dst_key(const DevGraph& g, int32_t e, float 
 // Index build: one wavefront per row runs the row's search with bound cmax in
 // an LDS table of INDEX_BUILD_CAP slots (the online tiers' fixed point), then
 // inserts every label into the row's table with its cost, route distance and
-// turn units (each lane walks its label's predecessor chain in the LDS table)
-// and its predecessor edge.
+// turn units (each lane walks its label's predecessor chain in the LDS table),
+// and then, the row's slots all placed, its predecessor's slot in the row
+// (-1: the route's first edge), so a path is walked slot to slot.
 template <bool WRITE>
 __global__ __launch_bounds__(TB) void k_index_build(DevGraph g, const uint32_t* TU, uint32_t cmax, int32_t* row_cnt,
                                                     const IdxRow* rows, uint4* slot, int32_t* pred) {
@@ -1389,12 +1421,22 @@ __global__ __launch_bounds__(TB) void k_index_build(DevGraph g, const uint32_t* 
       int len;
       chain_sums(g, TU, predof, pk, hin, (k & NODE_KEY) ? NO_HEAD : (uint32_t)g.e_head_out[k], cbuf + lane, d, units,
                  len);
-      uint32_t h = idx_slot0(k, R);
+      uint32_t h = idx_slot0(idx_home_hash(g, k), R);
       while (atomicCAS(&slot[R.off + h].x, EMPTY, k) != EMPTY) h = idx_next(h, R);
       slot[R.off + h].y = (uint32_t)(lab >> 32);
       slot[R.off + h].z = fbits(d);
       slot[R.off + h].w = units;
-      pred[R.off + h] = (int32_t)pk;
+    }
+    __syncthreads();
+    const DevIndex X{0.0f, 0u, rows, slot, pred};
+    for (int i = lane; i < INDEX_BUILD_CAP; i += TB) {
+      const uint32_t k = lkey[i];
+      if (k == EMPTY) continue;
+      const uint32_t pk = (uint32_t)(llab[i] & 0xFFFFFFFFull);
+      uint4 tmp;
+      const int64_t sk = idx_find(g, X, R, k, tmp);
+      const int64_t sp = pk == NONE_PRED ? -1 : idx_find(g, X, R, pk, tmp);
+      pred[sk] = sp < 0 ? -1 : (int32_t)(sp - R.off);
     }
     __syncthreads();
   }
@@ -1505,7 +1547,8 @@ __global__ __launch_bounds__(TB, 8) void k_trans_sub(DevGraph g, DevBatch b, Dev
         const int2 c = crec(w, p, k);
         const int32_t e = c.x;
         const float o = __int_as_float(c.y);
-        tg[sg][k ^ swz] = make_int4(e, __float_as_int(o), (int)dst_key(g, e, o), 0);
+        const uint32_t key = dst_key(g, e, o);
+        tg[sg][k ^ swz] = make_int4(e, __float_as_int(o), (int)key, (int)idx_home_hash(g, key));
       }
       if (act && k < Kq) {
         const int2 c = crec(w, q, k);
@@ -1547,7 +1590,7 @@ __global__ __launch_bounds__(TB, 8) void k_trans_sub(DevGraph g, DevBatch b, Dev
             const IdxRow R = rq[sg][i ^ swz];
             const bool same = same_edge_step(Sx.x, __int_as_float(Sx.y), T.x, __int_as_float(T.y));
             if (!same && R.cnt > 0) {
-              h0[u] = idx_slot0((uint32_t)T.z, R);
+              h0[u] = idx_slot0((uint32_t)T.w, R);
               s0[u] = X.slot[R.off + h0[u]];
             }
           }
@@ -1676,21 +1719,16 @@ __global__ __launch_bounds__(256, OTM_ROUTE_WAVES) void k_route_index(DevGraph g
     uint4 lab{};
     if (X.rmax > 0.0f && cq <= X.cmax) {
       Rw = X.row[src_row(g, ei, oi)];
-      sv = idx_find(X, Rw, dst_key(g, ej, oj), lab);
+      sv = idx_find(g, X, Rw, dst_key(g, ej, oj), lab);
     }
     if (sv < 0 || lab.y > cq) {
       const int slot = atomicAdd(&w.counters_i32[4], 1);
       w.overflow_list0[slot] = (int32_t)p;
       continue;
     }
+    // the path: the label's predecessor slots in the row, back to the first edge
     int len = 0;
-    for (uint32_t pe = (uint32_t)X.pred[sv]; pe != NONE_PRED && len <= Rw.cnt;) {
-      ++len;
-      uint4 tmp;
-      const int64_t sx = idx_find(X, Rw, pe, tmp);
-      if (sx < 0) break;  // (cannot happen: predecessor chains stay in the row)
-      pe = (uint32_t)X.pred[sx];
-    }
+    for (int32_t ps = X.pred[sv]; ps >= 0 && len <= Rw.cnt; ps = X.pred[Rw.off + ps]) ++len;
     const int off = len ? atomicAdd(&w.counters_i32[1], len) : 0;
     if (off + len > w.pool_cap) {
       w.counters_i32[2] = 1;
@@ -1698,13 +1736,8 @@ __global__ __launch_bounds__(256, OTM_ROUTE_WAVES) void k_route_index(DevGraph g
       w.path_len[p] = -1;
     } else {
       int k = len;
-      for (uint32_t pe = (uint32_t)X.pred[sv]; pe != NONE_PRED && k > 0;) {
-        w.path_pool[off + (--k)] = (int32_t)pe;
-        uint4 tmp;
-        const int64_t sx = idx_find(X, Rw, pe, tmp);
-        if (sx < 0) break;
-        pe = (uint32_t)X.pred[sx];
-      }
+      for (int32_t ps = X.pred[sv]; ps >= 0 && k > 0; ps = X.pred[Rw.off + ps])
+        w.path_pool[off + (--k)] = (int32_t)X.slot[Rw.off + ps].x;
       w.path_off[p] = off;
       w.path_len[p] = len;
     }

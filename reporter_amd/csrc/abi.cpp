@@ -1663,14 +1663,25 @@ static int otm_submit_batch_impl(otm_engine* E, int n, const char* const* reqs, 
   const bool one = off[(size_t)n] <= (mx ? (size_t)std::strtoull(mx, nullptr, 10) : slabs::SLAB_MAX);
   std::shared_ptr<ReqSlab> slab = one ? slabs::acquire(off[(size_t)n]) : nullptr;
   std::vector<otm_engine::Pending> items((size_t)n);
-  par_for((size_t)n, [&](size_t a, size_t e) {
-    for (size_t k = a; k < e; ++k) {
-      std::shared_ptr<ReqSlab> s = one ? slab : slabs::acquire(lens[k], false);
-      char* p = one ? slab->base + off[k] : s->base;
-      if (lens[k]) std::memcpy(p, reqs[k], lens[k]);
-      items[k] = otm_engine::Pending{tags[k], p, lens[k], std::move(s), (size_t)n - k, 0};
-    }
-  });
+  if (one) {
+    // the copies over the host threads; the slab's references taken on this
+    // thread after (one shared count: no cross-thread contention on it)
+    par_for((size_t)n, [&](size_t a, size_t e) {
+      for (size_t k = a; k < e; ++k)
+        if (lens[k]) std::memcpy(slab->base + off[k], reqs[k], lens[k]);
+    });
+    for (size_t k = 0; k < (size_t)n; ++k)
+      items[k] = otm_engine::Pending{tags[k], slab->base + off[k], lens[k], slab, (size_t)n - k, 0};
+  } else {
+    par_for((size_t)n, [&](size_t a, size_t e) {
+      for (size_t k = a; k < e; ++k) {
+        std::shared_ptr<ReqSlab> s = slabs::acquire(lens[k], false);
+        char* p = s->base;
+        if (lens[k]) std::memcpy(p, reqs[k], lens[k]);
+        items[k] = otm_engine::Pending{tags[k], p, lens[k], std::move(s), (size_t)n - k, 0};
+      }
+    });
+  }
   {
     std::lock_guard<std::mutex> lk(E->qmu);
     if (!E->worker_started) start_workers(E);

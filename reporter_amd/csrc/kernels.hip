@@ -518,6 +518,11 @@ constexpr int CAND_LANE_CAP = OTM_CAND_LANE_CAP;
 #define OTM_CAND_WAVES 8
 #endif
 constexpr int CAND_TB = OTM_CAND_TB;
+// lane tier: whole 64-B record and 32-B emission blocks per point (1), or only
+// the 16-B pieces that hold candidates (0)
+#ifndef OTM_CAND_WHOLE
+#define OTM_CAND_WHOLE 1
+#endif
 #ifndef OTM_CAND_INFL
 #define OTM_CAND_INFL 2
 #endif
@@ -701,6 +706,8 @@ __global__ __launch_bounds__(CAND_TB, OTM_CAND_WAVES) void k_cand_lane(DevGraph 
     float emv[4];
 #pragma unroll
     for (int j = 0; j < KIN; j += 2) {
+      // OTM_CAND_WHOLE = 0: only the 16-B pieces holding candidates (the A/B)
+      if (!OTM_CAND_WHOLE && j >= K && !((j & 3) == 2 && j - 2 < K)) break;
       int32_t e2[2];
       float o2[2];
 #pragma unroll
@@ -720,7 +727,7 @@ __global__ __launch_bounds__(CAND_TB, OTM_CAND_WAVES) void k_cand_lane(DevGraph 
         }
         emv[(j + u) & 3] = emj;
       }
-      eo4[j >> 1] = make_int4(e2[0], __float_as_int(o2[0]), e2[1], __float_as_int(o2[1]));
+      if (OTM_CAND_WHOLE || j < K) eo4[j >> 1] = make_int4(e2[0], __float_as_int(o2[0]), e2[1], __float_as_int(o2[1]));
       if ((j & 3) == 2) em4[j >> 2] = make_float4(emv[0], emv[1], emv[2], emv[3]);
     }
 

@@ -491,7 +491,7 @@ void engine_free(otm_engine* E) {
       &E->pt_trace,
       &E->is_col,        &E->prevc,        &E->nextc,        &E->gc,             &E->ncand,          &E->cand_eo,      &E->cand_em,
       &E->cand_xeo,      &E->cand_xem,
-      &E->probe,         &E->col_prev,     &E->kq_prev,        &E->trans_off,      &E->trans,          &E->bp,         &E->state,      &E->chosen,
+      &E->probe,         &E->col_prev,     &E->kq_prev,        &E->vmeta,        &E->trans_off,      &E->trans,          &E->bp,         &E->state,      &E->chosen,
       &E->chain_start,   &E->route_dist,   &E->ipos,   &E->path_off,       &E->path_len,       &E->path_pool,  &E->trace_err,
       &E->overflow_list0, &E->overflow_list2, &E->counters_i32, &E->scan_tmp, &E->snap,   &E->big_key,
       &E->big_lab,       &E->big_inq,      &E->big_fr,         &E->big_ins,        &E->big_prev,
@@ -601,6 +601,7 @@ static int engine_match_once(otm_engine* E, const DevBatch& b, hipStream_t s, st
   ENS(probe, Pn * 16);
   ENS(col_prev, Pn * 4);
   ENS(kq_prev, Pn * 4);
+  ENS(vmeta, Pn);
   ENS(trans_off, Pn * 8);
   ENS(bp, Pn * KMAX);
   ENS(state, Pn * 4);
@@ -659,6 +660,7 @@ static int engine_match_once(otm_engine* E, const DevBatch& b, hipStream_t s, st
   w.cand_xem = P<float>(E->cand_xem);
   w.col_prev = P<int32_t>(E->col_prev);
   w.kq_prev = P<int32_t>(E->kq_prev);
+  w.vmeta = P<uint8_t>(E->vmeta);
   w.trans_off = P<int64_t>(E->trans_off);
   w.bp = P<uint8_t>(E->bp);
   w.state = P<int32_t>(E->state);

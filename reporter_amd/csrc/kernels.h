@@ -177,6 +177,7 @@ struct DevWork {
   float* cand_xem;       // [P*KX]
   int32_t* col_prev;     // [P] linked previous column, -1
   int32_t* kq_prev;      // [P] candidates of the linked previous column (K3), so K4 reads them with p's own words
+  uint8_t* vmeta;        // [P] K5's byte per point (K3): candidates | column << 6 | linked << 7
   int64_t* trans_off;    // [P+1]
   float* trans;          // [total]
   uint8_t* bp;           // [P*KMAX]

@@ -1028,6 +1028,8 @@ __global__ __launch_bounds__(256) void k_links(DevBatch b, DevParams P, DevWork 
   w.col_prev[p] = cp;
   w.kq_prev[p] = kq;
   w.trans_off[p] = cnt;
+  // Viterbi's byte (k_viterbi_g): ncand <= KMAX = 32 fits six bits
+  w.vmeta[p] = (uint8_t)((w.is_col[p] ? (w.ncand[p] | 0x40) : 0) | (cp >= 0 ? 0x80 : 0));
 }
 
 // Batch bookkeeping in single-wave kernels rather than memset / memcpy
@@ -2417,7 +2419,10 @@ __global__ __launch_bounds__(TB, OTM_VG_WAVES) void k_viterbi_g(DevBatch b, DevW
     bool take = act && n <= VG_PTS;
     if (take) {
       bool wide = false;
-      for (int pl = j; pl < n; pl += G) wide = wide || (w.is_col[a + pl] && w.ncand[a + pl] > G);
+      for (int pl = j; pl < n; pl += G) {
+        const int vm = w.vmeta[a + pl];
+        wide = wide || ((vm & 0x40) && (vm & 0x3F) > G);
+      }
       take = ((__ballot(wide) >> gb) & (unsigned long long)gmask) == 0ull;
     }
     if (act && !take) {
@@ -2431,6 +2436,7 @@ __global__ __launch_bounds__(TB, OTM_VG_WAVES) void k_viterbi_g(DevBatch b, DevW
     float prev = INFINITY;
     bool open = false;
     int last = -1, lastK = 0;
+    int acc = 0;  // the trace's transition floats before this column (K3's Kq x Kp counts, summed in order)
     auto end_chain = [&]() {
       // argmin (value, state) over the group's lanes < lastK, ties to the lower state
       float bv = j < lastK ? prev : INFINITY;
@@ -2447,31 +2453,23 @@ __global__ __launch_bounds__(TB, OTM_VG_WAVES) void k_viterbi_g(DevBatch b, DevW
       if (j == 0) sFl[g][last] = (uint8_t)(sFl[g][last] | VG_END | (bi << 3));
     };
     for (int c0 = 0; c0 < nmax; c0 += G) {
-      // G points' metadata, one per lane: flags | candidates, block offset
-      int m_k = 0, m_to = 0;
-      {
-        const int pl = c0 + j;
-        if (pl < n) {
-          const int64_t p = a + pl;
-          const int ic = w.is_col[p];
-          const int nc = w.ncand[p];
-          const int32_t q = w.col_prev[p];
-          m_to = (int)(w.trans_off[p] - t0);
-          m_k = ic ? (nc | 0x100 | (q >= 0 ? 0x200 : 0)) : 0;
-        }
-      }
+      // G points' metadata bytes (K3's vmeta), one per lane
+      const int m_k = c0 + j < n ? (int)w.vmeta[a + c0 + j] : 0;
       for (int k = 0; k < G; ++k) {
         const int pl = c0 + k;
         const int mk = __shfl(m_k, gb + k, TB);
-        const int to = __shfl(m_to, gb + k, TB);
-        const bool on = pl < n && (mk & 0x100);
-        const int Kp = mk & 0xFF;
+        const bool on = pl < n && (mk & 0x40);
+        const int Kp = mk & 0x3F;
         if (on && Kp == 0) {
           if (open) end_chain();
           open = false;
         }
         const bool col = on && Kp > 0;
-        const bool link = col && open && (mk & 0x200);
+        const bool link = col && open && (mk & 0x80);
+        // a linked column's block follows the trace's earlier ones (its
+        // previous column is the open chain's last)
+        const int to = acc;
+        if (link) acc += lastK * Kp;
         const int64_t p = a + pl;
         const int jj = j < Kp ? j : 0;
         // every load of the step in flight before any is used

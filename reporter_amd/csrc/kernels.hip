@@ -1303,18 +1303,21 @@ __device__ __forceinline__ uint32_t idx_hash(uint32_t v) {
 #ifndef OTM_IDX_LOAD_PCT
 #define OTM_IDX_LOAD_PCT 20
 #endif
-// OTM_IDX_HOME = 1 (round 4): a label's home in a row's table is its road's
-// lower-numbered node (an edge key: min(from, to); a node key: the node), and
-// a home hashes to an aligned group of IDX_GROUP slots, one 128-B line; linear
-// probing from there.  The labels a column probes in one row are its target
-// candidates -- a node and the two directions of the roads at it -- so they
-// share a few homes (0.42 homes per key on config 2, 0.45 on config 4,
-// against one line per key with a home per key: OTM_IDX_HOME = 0).  Rows are
-// whole groups, so every row starts on a line.
+// OTM_IDX_HOME = 1 (round 4's A/B, not kept): a label's home in a row's
+// table is its road's lower-numbered node (an edge key: min(from, to); a node
+// key: the node), and a home hashes to an aligned group of IDX_GROUP slots,
+// one 128-B line, linear probing from there.  A column's target candidates --
+// a node and the two directions of the roads at it -- share a few homes (0.42
+// homes per key on config 2, 0.45 on config 4), but the lookups then walk the
+// merged runs of several homes slot by slot, each a dependent load:
+// k_trans_sub 0.248 -> 0.370 ms on config 2, 2.29 -> 5.25 ms on config 4
+// (profiles/r04_ab/index_home/).  Default 0: a home per key.
 #ifndef OTM_IDX_HOME
-#define OTM_IDX_HOME 1
+#define OTM_IDX_HOME 0
 #endif
+#if OTM_IDX_HOME
 constexpr int IDX_GROUP = 8;
+#endif
 __host__ __device__ __forceinline__ int64_t idx_row_cap(int32_t c) {
   if (c <= 0) return 0;
 #if OTM_IDX_HOME
@@ -2347,19 +2350,23 @@ __global__ __launch_bounds__(TB, OTM_VIT_WAVES) void k_viterbi(DevBatch b, DevWo
 // 534M VALU instructions over 10M points at config 4, 82 % of the SIMDs'
 // cycles) with Kq <= 8 of its 64 lanes holding states; here one instruction
 // stream steps 64 / G traces.  A group (lane j = state j) walks its trace's
-// points in order:
-//  * metadata of G points per round trip (lane k holds point c0 + k; a step
-//    reads it by shuffle), no LDS copy of the trace;
-//  * a column's emissions and its Kq x Kp transition block straight from HBM
-//    (the block is contiguous in the trace's stream), every load of a step in
-//    flight at once; the waves per SIMD hide the round trip;
+// points in chunks of G:
+//  * a chunk's transition blocks (contiguous in the trace's stream, bounded
+//    by K3's trans_off) and its points' emissions are loaded into registers
+//    one chunk ahead -- in flight while the group steps through the current
+//    chunk -- and staged through a per-group LDS window at the chunk's start
+//    (a chunk whose blocks exceed the window reads them from HBM per step);
+//    the per-point metadata is K3's one byte (vmeta), loaded two chunks ahead;
+//  * a step reads its point's byte by shuffle and its block from LDS;
 //  * a column's backpointers as four ballot bit planes (no shuffle chain), one
 //    word per point in LDS; a chain's end records its argmin state;
 //  * after the forward pass one lane per group walks the trace backward.
-// A trace with a column of more than G candidates, or more than VG_PTS
-// points, goes to the next form's list (G = 8 -> G = 16 -> the wave form).
-// Same recurrence (min over i in order, strict <), tie rules and chain breaks
-// as viterbi_trace_global: bit-identical to the oracle.
+// (Round 4's first form loaded each step's block from HBM at the step: one
+// exposed round trip per point, 0.645 ms on config 2 against 0.155 for the
+// wave form.)  A trace with a column of more than G candidates, or more than
+// VG_PTS points, goes to the next form's list (G = 8 -> G = 16 -> the wave
+// form).  Same recurrence (min over i in order, strict <), tie rules and chain
+// breaks as viterbi_trace_global: bit-identical to the oracle.
 __device__ __forceinline__ int wave_max_i(int v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -2369,7 +2376,7 @@ __device__ __forceinline__ int wave_max_i(int v) {
   return v;
 }
 #ifndef OTM_VG_WAVES
-#define OTM_VG_WAVES 6
+#define OTM_VG_WAVES 3
 #endif
 constexpr int VG_PTS = 128;  // points per trace
 constexpr uint8_t VG_COL = 1, VG_CS = 2, VG_END = 4;  // point flags (VG_END: argmin state in bits 3..7)
@@ -2382,14 +2389,19 @@ struct VgWord<16> {
   using T = unsigned long long;
 };
 template <int G>
-__global__ __launch_bounds__(TB, OTM_VG_WAVES) void k_viterbi_g(DevBatch b, DevWork w, const int32_t* list, const int32_t* list_n,
-                                                     int32_t* rej, int32_t* rej_n, int snap) {
+__global__ __launch_bounds__(TB, OTM_VG_WAVES) void k_viterbi_g(DevBatch b, DevWork w, const int32_t* list,
+                                                                const int32_t* list_n, int32_t* rej, int32_t* rej_n,
+                                                                int snap) {
   static_assert(G == 8 || G == 16, "8 or 16 lanes per trace");
   using Word = typename VgWord<G>::T;  // 4 bit planes of G backpointer bits
   constexpr int NT = TB / G;
+  constexpr int VT = 16 * G;  // transition floats per chunk window (16 per lane)
+  constexpr int U = VT / G;
   // spill snapshot B (see k_viterbi)
   if (OTM_FOLD_BOOKKEEPING && snap && blockIdx.x == 0 && threadIdx.x == 0) fold_snap(w, 1, true);
   if (*w.abort) return;
+  __shared__ float sT[NT][VT];
+  __shared__ float sE[NT][G * G];  // [point of the chunk][state]
   __shared__ Word sBp[NT][VG_PTS];
   __shared__ uint8_t sFl[NT][VG_PTS];  // flags; after the walk: VG_CS | (state + 1) << 3
   const int lane = threadIdx.x;
@@ -2430,8 +2442,36 @@ __global__ __launch_bounds__(TB, OTM_VG_WAVES) void k_viterbi_g(DevBatch b, DevW
       act = false;
     }
     if (!act) n = 0;
-    const int nmax = wave_max_i(n);
+    const int nch = (wave_max_i(n) + G - 1) / G;
     for (int pl = j; pl < n; pl += G) sFl[g][pl] = 0;
+    // ---- the chunk pipeline: metadata and T range two chunks ahead, data one
+    auto ld_meta = [&](int c) { return c * G + j < n ? (int)w.vmeta[a + c * G + j] : 0; };
+    auto ld_range = [&](int c, int& lo, int& hi) {
+      lo = hi = 0;
+      if (c * G < n) {
+        lo = (int)(w.trans_off[a + c * G] - t0);
+        hi = (int)(w.trans_off[a + (c * G + G < n ? c * G + G : n)] - t0);
+      }
+    };
+    float pT[U], pE[G];
+    auto ld_data = [&](int c, int m, int lo, int hi) {
+      const bool fits = hi - lo <= VT;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int f = lo + u * G + j;
+        pT[u] = fits && f < hi ? w.trans[t0 + f] : 0.0f;
+      }
+#pragma unroll
+      for (int k = 0; k < G; ++k) {
+        const int mk = __shfl(m, gb + k, TB);
+        pE[k] = (mk & 0x40) && j < (mk & 0x3F) ? cemis(w, a + c * G + k, j) : 0.0f;
+      }
+    };
+    int mA = ld_meta(0), mB = ld_meta(1);
+    int loA, hiA, loB, hiB;
+    ld_range(0, loA, hiA);
+    ld_range(1, loB, hiB);
+    ld_data(0, mA, loA, hiA);
     // ---- forward pass (wave-uniform step count; groups predicated)
     float prev = INFINITY;
     bool open = false;
@@ -2452,12 +2492,24 @@ __global__ __launch_bounds__(TB, OTM_VG_WAVES) void k_viterbi_g(DevBatch b, DevW
       }
       if (j == 0) sFl[g][last] = (uint8_t)(sFl[g][last] | VG_END | (bi << 3));
     };
-    for (int c0 = 0; c0 < nmax; c0 += G) {
-      // G points' metadata bytes (K3's vmeta), one per lane
-      const int m_k = c0 + j < n ? (int)w.vmeta[a + c0 + j] : 0;
+    for (int c = 0; c < nch; ++c) {
+      // stage chunk c, then start chunk c + 1's loads
+#pragma unroll
+      for (int u = 0; u < U; ++u) sT[g][u * G + j] = pT[u];
+#pragma unroll
+      for (int k = 0; k < G; ++k) sE[g][k * G + j] = pE[k];
+      const int m_c = mA, lo_c = loA, hi_c = hiA;
+      mA = mB;
+      loA = loB;
+      hiA = hiB;
+      mB = ld_meta(c + 2);
+      ld_range(c + 2, loB, hiB);
+      __syncthreads();
+      if (c + 1 < nch) ld_data(c + 1, mA, loA, hiA);
+      const bool fits = hi_c - lo_c <= VT;
       for (int k = 0; k < G; ++k) {
-        const int pl = c0 + k;
-        const int mk = __shfl(m_k, gb + k, TB);
+        const int pl = c * G + k;
+        const int mk = __shfl(m_c, gb + k, TB);
         const bool on = pl < n && (mk & 0x40);
         const int Kp = mk & 0x3F;
         if (on && Kp == 0) {
@@ -2470,17 +2522,15 @@ __global__ __launch_bounds__(TB, OTM_VG_WAVES) void k_viterbi_g(DevBatch b, DevW
         // previous column is the open chain's last)
         const int to = acc;
         if (link) acc += lastK * Kp;
-        const int64_t p = a + pl;
         const int jj = j < Kp ? j : 0;
-        // every load of the step in flight before any is used
-        float em = 0.0f;
-        if (col) em = cemis(w, p, jj);
+        const float em = sE[g][k * G + jj];
         float tv[G];
 #pragma unroll
         for (int i = 0; i < G; ++i) {
           tv[i] = INFINITY;
           if (__ballot(link && i < lastK) == 0ull) break;
-          if (link && i < lastK) tv[i] = w.trans[t0 + to + i * Kp + jj];
+          if (link && i < lastK)
+            tv[i] = fits ? sT[g][to - lo_c + i * Kp + jj] : w.trans[t0 + to + i * Kp + jj];
         }
         bool started = false;
         float cur = INFINITY;
@@ -2528,6 +2578,7 @@ __global__ __launch_bounds__(TB, OTM_VG_WAVES) void k_viterbi_g(DevBatch b, DevW
           lastK = Kp;
         }
       }
+      __syncthreads();  // (the next chunk's staging overwrites the windows)
     }
     if (act && open) end_chain();
     __syncthreads();

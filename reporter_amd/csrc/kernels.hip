@@ -2350,7 +2350,7 @@ __global__ __launch_bounds__(TB, OTM_VIT_WAVES) void k_viterbi(DevBatch b, DevWo
 // 534M VALU instructions over 10M points at config 4, 82 % of the SIMDs'
 // cycles) with Kq <= 8 of its 64 lanes holding states; here one instruction
 // stream steps 64 / G traces.  A group (lane j = state j) walks its trace's
-// points in chunks of G:
+// points in chunks of OTM_VG_CHUNK:
 //  * a chunk's transition blocks (contiguous in the trace's stream, bounded
 //    by K3's trans_off) and its points' emissions are loaded into registers
 //    one chunk ahead -- in flight while the group steps through the current
@@ -2378,6 +2378,12 @@ __device__ __forceinline__ int wave_max_i(int v) {
 #ifndef OTM_VG_WAVES
 #define OTM_VG_WAVES 3
 #endif
+// points per chunk: 8 or 16 overflowed the 16-float-per-lane window on most of
+// config 2's chunks (~20 transition floats per column), whose steps then read
+// their blocks from HBM one round trip each (form 8: 0.699 ms, config 2)
+#ifndef OTM_VG_CHUNK
+#define OTM_VG_CHUNK 4
+#endif
 constexpr int VG_PTS = 128;  // points per trace
 constexpr uint8_t VG_COL = 1, VG_CS = 2, VG_END = 4;  // point flags (VG_END: argmin state in bits 3..7)
 template <int G>
@@ -2397,11 +2403,13 @@ __global__ __launch_bounds__(TB, OTM_VG_WAVES) void k_viterbi_g(DevBatch b, DevW
   constexpr int NT = TB / G;
   constexpr int VT = 16 * G;  // transition floats per chunk window (16 per lane)
   constexpr int U = VT / G;
+  constexpr int CH = OTM_VG_CHUNK;  // points per chunk (<= G)
+  static_assert(CH <= G, "a chunk's metadata is one byte per lane");
   // spill snapshot B (see k_viterbi)
   if (OTM_FOLD_BOOKKEEPING && snap && blockIdx.x == 0 && threadIdx.x == 0) fold_snap(w, 1, true);
   if (*w.abort) return;
   __shared__ float sT[NT][VT];
-  __shared__ float sE[NT][G * G];  // [point of the chunk][state]
+  __shared__ float sE[NT][CH * G];  // [point of the chunk][state]
   __shared__ Word sBp[NT][VG_PTS];
   __shared__ uint8_t sFl[NT][VG_PTS];  // flags; after the walk: VG_CS | (state + 1) << 3
   const int lane = threadIdx.x;
@@ -2442,18 +2450,18 @@ __global__ __launch_bounds__(TB, OTM_VG_WAVES) void k_viterbi_g(DevBatch b, DevW
       act = false;
     }
     if (!act) n = 0;
-    const int nch = (wave_max_i(n) + G - 1) / G;
+    const int nch = (wave_max_i(n) + CH - 1) / CH;
     for (int pl = j; pl < n; pl += G) sFl[g][pl] = 0;
     // ---- the chunk pipeline: metadata and T range two chunks ahead, data one
-    auto ld_meta = [&](int c) { return c * G + j < n ? (int)w.vmeta[a + c * G + j] : 0; };
+    auto ld_meta = [&](int c) { return j < CH && c * CH + j < n ? (int)w.vmeta[a + c * CH + j] : 0; };
     auto ld_range = [&](int c, int& lo, int& hi) {
       lo = hi = 0;
-      if (c * G < n) {
-        lo = (int)(w.trans_off[a + c * G] - t0);
-        hi = (int)(w.trans_off[a + (c * G + G < n ? c * G + G : n)] - t0);
+      if (c * CH < n) {
+        lo = (int)(w.trans_off[a + c * CH] - t0);
+        hi = (int)(w.trans_off[a + (c * CH + CH < n ? c * CH + CH : n)] - t0);
       }
     };
-    float pT[U], pE[G];
+    float pT[U], pE[CH];
     auto ld_data = [&](int c, int m, int lo, int hi) {
       const bool fits = hi - lo <= VT;
 #pragma unroll
@@ -2462,9 +2470,9 @@ __global__ __launch_bounds__(TB, OTM_VG_WAVES) void k_viterbi_g(DevBatch b, DevW
         pT[u] = fits && f < hi ? w.trans[t0 + f] : 0.0f;
       }
 #pragma unroll
-      for (int k = 0; k < G; ++k) {
+      for (int k = 0; k < CH; ++k) {
         const int mk = __shfl(m, gb + k, TB);
-        pE[k] = (mk & 0x40) && j < (mk & 0x3F) ? cemis(w, a + c * G + k, j) : 0.0f;
+        pE[k] = (mk & 0x40) && j < (mk & 0x3F) ? cemis(w, a + c * CH + k, j) : 0.0f;
       }
     };
     int mA = ld_meta(0), mB = ld_meta(1);
@@ -2497,7 +2505,7 @@ __global__ __launch_bounds__(TB, OTM_VG_WAVES) void k_viterbi_g(DevBatch b, DevW
 #pragma unroll
       for (int u = 0; u < U; ++u) sT[g][u * G + j] = pT[u];
 #pragma unroll
-      for (int k = 0; k < G; ++k) sE[g][k * G + j] = pE[k];
+      for (int k = 0; k < CH; ++k) sE[g][k * G + j] = pE[k];
       const int m_c = mA, lo_c = loA, hi_c = hiA;
       mA = mB;
       loA = loB;
@@ -2507,8 +2515,8 @@ __global__ __launch_bounds__(TB, OTM_VG_WAVES) void k_viterbi_g(DevBatch b, DevW
       __syncthreads();
       if (c + 1 < nch) ld_data(c + 1, mA, loA, hiA);
       const bool fits = hi_c - lo_c <= VT;
-      for (int k = 0; k < G; ++k) {
-        const int pl = c * G + k;
+      for (int k = 0; k < CH; ++k) {
+        const int pl = c * CH + k;
         const int mk = __shfl(m_c, gb + k, TB);
         const bool on = pl < n && (mk & 0x40);
         const int Kp = mk & 0x3F;

@@ -17,6 +17,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 #include <hipcub/hipcub.hpp>
 
@@ -2454,16 +2455,18 @@ __global__ __launch_bounds__(TB, OTM_VG_WAVES) void k_viterbi_g(DevBatch b, DevW
     for (int pl = j; pl < n; pl += G) sFl[g][pl] = 0;
     // ---- the chunk pipeline: metadata and T range two chunks ahead, data one
     auto ld_meta = [&](int c) { return j < CH && c * CH + j < n ? (int)w.vmeta[a + c * CH + j] : 0; };
-    auto ld_range = [&](int c, int& lo, int& hi) {
-      lo = hi = 0;
+    // (the raw offsets: the subtraction waits for the loads, so it is done
+    // where they are used, a chunk later)
+    auto ld_range = [&](int c, int64_t& lo, int64_t& hi) {
+      lo = hi = t0;
       if (c * CH < n) {
-        lo = (int)(w.trans_off[a + c * CH] - t0);
-        hi = (int)(w.trans_off[a + (c * CH + CH < n ? c * CH + CH : n)] - t0);
+        lo = w.trans_off[a + c * CH];
+        hi = w.trans_off[a + (c * CH + CH < n ? c * CH + CH : n)];
       }
     };
     float pT[U], pE[CH];
     auto ld_data = [&](int c, int m, int lo, int hi) {
-      const bool fits = hi - lo <= VT;
+      const bool fits = hi - lo <= VT;  // (lo, hi: from the trace's first float)
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int f = lo + u * G + j;
@@ -2476,10 +2479,10 @@ __global__ __launch_bounds__(TB, OTM_VG_WAVES) void k_viterbi_g(DevBatch b, DevW
       }
     };
     int mA = ld_meta(0), mB = ld_meta(1);
-    int loA, hiA, loB, hiB;
+    int64_t loA, hiA, loB, hiB;
     ld_range(0, loA, hiA);
     ld_range(1, loB, hiB);
-    ld_data(0, mA, loA, hiA);
+    ld_data(0, mA, (int)(loA - t0), (int)(hiA - t0));
     // ---- forward pass (wave-uniform step count; groups predicated)
     float prev = INFINITY;
     bool open = false;
@@ -2506,16 +2509,17 @@ __global__ __launch_bounds__(TB, OTM_VG_WAVES) void k_viterbi_g(DevBatch b, DevW
       for (int u = 0; u < U; ++u) sT[g][u * G + j] = pT[u];
 #pragma unroll
       for (int k = 0; k < CH; ++k) sE[g][k * G + j] = pE[k];
-      const int m_c = mA, lo_c = loA, hi_c = hiA;
+      const int m_c = mA, lo_c = (int)(loA - t0), hi_c = (int)(hiA - t0);
       mA = mB;
       loA = loB;
       hiA = hiB;
       mB = ld_meta(c + 2);
       ld_range(c + 2, loB, hiB);
       __syncthreads();
-      if (c + 1 < nch) ld_data(c + 1, mA, loA, hiA);
-      const bool fits = hi_c - lo_c <= VT;
-      for (int k = 0; k < CH; ++k) {
+      if (c + 1 < nch) ld_data(c + 1, mA, (int)(loA - t0), (int)(hiA - t0));
+      // FAST: every group's chunk fits its window, so the steps touch no HBM
+      // (a load there would make the step wait for the chunk's prefetches)
+      auto step = [&](int k, auto fast) {
         const int pl = c * CH + k;
         const int mk = __shfl(m_c, gb + k, TB);
         const bool on = pl < n && (mk & 0x40);
@@ -2532,13 +2536,24 @@ __global__ __launch_bounds__(TB, OTM_VG_WAVES) void k_viterbi_g(DevBatch b, DevW
         if (link) acc += lastK * Kp;
         const int jj = j < Kp ? j : 0;
         const float em = sE[g][k * G + jj];
+        // a group whose chunk overflowed its window: this column's block into
+        // the window first (<= G x G floats), so the recurrence below reads
+        // LDS only and holds no register a global load wrote (no wait there
+        // on the next chunk's prefetches)
+        int tb = to - lo_c;
+        if constexpr (!decltype(fast)::value) {
+          if (hi_c - lo_c > VT) {
+            tb = 0;
+            if (link)
+              for (int f = j; f < lastK * Kp; f += G) sT[g][f] = w.trans[t0 + to + f];
+          }
+        }
         float tv[G];
 #pragma unroll
         for (int i = 0; i < G; ++i) {
           tv[i] = INFINITY;
           if (__ballot(link && i < lastK) == 0ull) break;
-          if (link && i < lastK)
-            tv[i] = fits ? sT[g][to - lo_c + i * Kp + jj] : w.trans[t0 + to + i * Kp + jj];
+          if (link && i < lastK) tv[i] = sT[g][tb + i * Kp + jj];
         }
         bool started = false;
         float cur = INFINITY;
@@ -2585,6 +2600,11 @@ __global__ __launch_bounds__(TB, OTM_VG_WAVES) void k_viterbi_g(DevBatch b, DevW
           last = pl;
           lastK = Kp;
         }
+      };
+      if (__ballot(hi_c - lo_c > VT) == 0ull) {
+        for (int k = 0; k < CH; ++k) step(k, std::true_type{});
+      } else {
+        for (int k = 0; k < CH; ++k) step(k, std::false_type{});
       }
       __syncthreads();  // (the next chunk's staging overwrites the windows)
     }

@@ -2359,8 +2359,8 @@ __global__ __launch_bounds__(TB, OTM_VIT_WAVES) void k_viterbi(DevBatch b, DevWo
 //    (a chunk whose blocks exceed the window reads them from HBM per step);
 //    the per-point metadata is K3's one byte (vmeta), loaded two chunks ahead;
 //  * a step reads its point's byte by shuffle and its block from LDS;
-//  * a column's backpointers as four ballot bit planes (no shuffle chain), one
-//    word per point in LDS; a chain's end records its argmin state;
+//  * a column's backpointers as one byte per state in LDS; a chain's end
+//    records its argmin state;
 //  * after the forward pass one lane per group walks the trace backward.
 // (Round 4's first form loaded each step's block from HBM at the step: one
 // exposed round trip per point, 0.645 ms on config 2 against 0.155 for the
@@ -2388,19 +2388,10 @@ __device__ __forceinline__ int wave_max_i(int v) {
 constexpr int VG_PTS = 128;  // points per trace
 constexpr uint8_t VG_COL = 1, VG_CS = 2, VG_END = 4;  // point flags (VG_END: argmin state in bits 3..7)
 template <int G>
-struct VgWord {
-  using T = uint32_t;
-};
-template <>
-struct VgWord<16> {
-  using T = unsigned long long;
-};
-template <int G>
 __global__ __launch_bounds__(TB, OTM_VG_WAVES) void k_viterbi_g(DevBatch b, DevWork w, const int32_t* list,
                                                                 const int32_t* list_n, int32_t* rej, int32_t* rej_n,
                                                                 int snap) {
   static_assert(G == 8 || G == 16, "8 or 16 lanes per trace");
-  using Word = typename VgWord<G>::T;  // 4 bit planes of G backpointer bits
   constexpr int NT = TB / G;
   constexpr int VT = 16 * G;  // transition floats per chunk window (16 per lane)
   constexpr int U = VT / G;
@@ -2411,11 +2402,11 @@ __global__ __launch_bounds__(TB, OTM_VG_WAVES) void k_viterbi_g(DevBatch b, DevW
   if (*w.abort) return;
   __shared__ float sT[NT][VT];
   __shared__ float sE[NT][CH * G];  // [point of the chunk][state]
-  __shared__ Word sBp[NT][VG_PTS];
+  __shared__ uint8_t sBp[NT][VG_PTS][G];  // backpointer of each state (0xFF: dead)
   __shared__ uint8_t sFl[NT][VG_PTS];  // flags; after the walk: VG_CS | (state + 1) << 3
   const int lane = threadIdx.x;
   const int g = lane / G, j = lane % G, gb = g * G;
-  const Word gmask = (Word)(((unsigned long long)1 << G) - 1ull);
+  const unsigned long long gmask = (1ull << G) - 1ull;
   const int32_t ntr = list ? *list_n : b.n_traces;
   for (int32_t tb = blockIdx.x * NT; tb < ntr; tb += gridDim.x * NT) {
     const int32_t it = tb + g;
@@ -2444,7 +2435,7 @@ __global__ __launch_bounds__(TB, OTM_VG_WAVES) void k_viterbi_g(DevBatch b, DevW
         const int vm = w.vmeta[a + pl];
         wide = wide || ((vm & 0x40) && (vm & 0x3F) > G);
       }
-      take = ((__ballot(wide) >> gb) & (unsigned long long)gmask) == 0ull;
+      take = ((__ballot(wide) >> gb) & gmask) == 0ull;
     }
     if (act && !take) {
       if (j == 0) rej[atomicAdd(rej_n, 1)] = t;
@@ -2517,9 +2508,13 @@ __global__ __launch_bounds__(TB, OTM_VG_WAVES) void k_viterbi_g(DevBatch b, DevW
       ld_range(c + 2, loB, hiB);
       __syncthreads();
       if (c + 1 < nch) ld_data(c + 1, mA, (int)(loA - t0), (int)(hiA - t0));
-      // FAST: every group's chunk fits its window, so the steps touch no HBM
-      // (a load there would make the step wait for the chunk's prefetches)
-      auto step = [&](int k, auto fast) {
+      // A step, for every group at once: its point's byte by shuffle, its
+      // emission and block from LDS, Kq in fours (loads issued together), its
+      // backpointers as one byte per state in LDS.  The loop bounds are
+      // wave-uniform ballots, not unrolled to G (round 4's unrolled form spent
+      // ~600 instructions per step).
+      const bool big = hi_c - lo_c > VT;  // this group's chunk overflowed its window
+      for (int k = 0; k < CH; ++k) {
         const int pl = c * CH + k;
         const int mk = __shfl(m_c, gb + k, TB);
         const bool on = pl < n && (mk & 0x40);
@@ -2536,54 +2531,44 @@ __global__ __launch_bounds__(TB, OTM_VG_WAVES) void k_viterbi_g(DevBatch b, DevW
         if (link) acc += lastK * Kp;
         const int jj = j < Kp ? j : 0;
         const float em = sE[g][k * G + jj];
-        // a group whose chunk overflowed its window: this column's block into
-        // the window first (<= G x G floats), so the recurrence below reads
-        // LDS only and holds no register a global load wrote (no wait there
-        // on the next chunk's prefetches)
         int tb = to - lo_c;
-        if constexpr (!decltype(fast)::value) {
-          if (hi_c - lo_c > VT) {
+        if (__ballot(big && link) != 0ull) {
+          // the column's block (<= G x G floats) into the window first, so
+          // the recurrence reads LDS only
+          if (big) {
             tb = 0;
             if (link)
               for (int f = j; f < lastK * Kp; f += G) sT[g][f] = w.trans[t0 + to + f];
           }
-        }
-        float tv[G];
-#pragma unroll
-        for (int i = 0; i < G; ++i) {
-          tv[i] = INFINITY;
-          if (__ballot(link && i < lastK) == 0ull) break;
-          if (link && i < lastK) tv[i] = sT[g][tb + i * Kp + jj];
         }
         bool started = false;
         float cur = INFINITY;
         if (__ballot(link) != 0ull) {
           float best = INFINITY;
           int bi = -1;
+          const float* Tm = &sT[g][tb + jj];
+          for (int i0 = 0; __ballot(link && i0 < lastK) != 0ull; i0 += 4) {
+            float tv[4], pv[4];
 #pragma unroll
-          for (int i = 0; i < G; ++i) {
-            if (__ballot(link && i < lastK) == 0ull) break;
-            const float pv = __shfl(prev, gb + i, TB);
-            if (link && i < lastK) {
-              const float v = pv + tv[i];
-              if (v < best) {
+            for (int u = 0; u < 4; ++u) {
+              const int i = i0 + u;
+              tv[u] = link && i < lastK ? Tm[i * Kp] : INFINITY;
+              pv[u] = __shfl(prev, gb + (i < G ? i : 0), TB);
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              const float v = pv[u] + tv[u];
+              if (link && i0 + u < lastK && v < best) {
                 best = v;
-                bi = i;
+                bi = i0 + u;
               }
             }
           }
           const bool alive = link && j < Kp && bi >= 0;
-          if (link) cur = alive ? best + em : INFINITY;
-          // the backpointers as four bit planes of the group's G bits
-          const int bb = alive ? bi : 15;
-          Word word = 0;
-#pragma unroll
-          for (int bit = 0; bit < 4; ++bit)
-            word |= (Word)((__ballot(((bb >> bit) & 1) != 0) >> gb) & (unsigned long long)gmask) << (bit * G);
-          if (link && j == 0) sBp[g][pl] = word;
-          const bool any = ((__ballot(alive) >> gb) & (unsigned long long)gmask) != 0ull;
           if (link) {
-            if (any) started = true;
+            cur = alive ? best + em : INFINITY;
+            sBp[g][pl][j] = (uint8_t)(alive ? bi : 0xFF);
+            if (((__ballot(alive) >> gb) & (unsigned long long)gmask) != 0ull) started = true;
             else end_chain();
           }
         }
@@ -2600,11 +2585,6 @@ __global__ __launch_bounds__(TB, OTM_VG_WAVES) void k_viterbi_g(DevBatch b, DevW
           last = pl;
           lastK = Kp;
         }
-      };
-      if (__ballot(hi_c - lo_c > VT) == 0ull) {
-        for (int k = 0; k < CH; ++k) step(k, std::true_type{});
-      } else {
-        for (int k = 0; k < CH; ++k) step(k, std::false_type{});
       }
       __syncthreads();  // (the next chunk's staging overwrites the windows)
     }
@@ -2625,11 +2605,7 @@ __global__ __launch_bounds__(TB, OTM_VG_WAVES) void k_viterbi_g(DevBatch b, DevW
           if (f & VG_CS) {
             sv = -1;
           } else {
-            const Word wd = sBp[g][pl];
-            int x = 0;
-#pragma unroll
-            for (int bit = 0; bit < 4; ++bit) x |= (int)((wd >> (bit * G + sv)) & 1u) << bit;
-            sv = x;
+            sv = sBp[g][pl][sv];
           }
         }
       }

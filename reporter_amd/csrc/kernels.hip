@@ -2368,6 +2368,14 @@ __global__ __launch_bounds__(TB, OTM_VIT_WAVES) void k_viterbi(DevBatch b, DevWo
 // VG_PTS points, goes to the next form's list (G = 8 -> G = 16 -> the wave
 // form).  Same recurrence (min over i in order, strict <), tie rules and chain
 // breaks as viterbi_trace_global: bit-identical to the oracle.
+// The block is one wavefront (TB = 64): its LDS operations execute in issue
+// order, so a chunk's staging only needs the compiler kept from moving LDS
+// accesses across this point.  __syncthreads() would also wait for every
+// global load in flight -- the next chunks' prefetches.
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+}
 __device__ __forceinline__ int wave_max_i(int v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -2444,36 +2452,50 @@ __global__ __launch_bounds__(TB, OTM_VG_WAVES) void k_viterbi_g(DevBatch b, DevW
     if (!act) n = 0;
     const int nch = (wave_max_i(n) + CH - 1) / CH;
     for (int pl = j; pl < n; pl += G) sFl[g][pl] = 0;
-    // ---- the chunk pipeline: metadata and T range two chunks ahead, data one
-    auto ld_meta = [&](int c) { return j < CH && c * CH + j < n ? (int)w.vmeta[a + c * CH + j] : 0; };
-    // (the raw offsets: the subtraction waits for the loads, so it is done
-    // where they are used, a chunk later)
-    auto ld_range = [&](int c, int64_t& lo, int64_t& hi) {
-      lo = hi = t0;
-      if (c * CH < n) {
-        lo = w.trans_off[a + c * CH];
-        hi = w.trans_off[a + (c * CH + CH < n ? c * CH + CH : n)];
-      }
+    // ---- the chunk pipeline: data two chunks ahead (two register sets, A for
+    // even chunks, B for odd), metadata and T range four ahead
+    // Every pipeline load is issued unconditionally (indices clamped into the
+    // trace, results masked after): a fixed count per chunk lets the compiler
+    // wait for exactly the older set, not for everything in flight.
+    const int nl = n > 0 ? n - 1 : 0;  // (a trace's last point; 0 for an idle group)
+    // (raw: a step reads lane k < CH's byte, and only for a point pl < n)
+    auto ld_meta = [&](int c) {
+      const int pl = c * CH + j;
+      return (int)w.vmeta[a + (pl < nl ? pl : nl)];
     };
-    float pT[U], pE[CH];
-    auto ld_data = [&](int c, int m, int lo, int hi) {
-      const bool fits = hi - lo <= VT;  // (lo, hi: from the trace's first float)
+    // (the raw offsets: the subtraction waits for the loads, so it is done
+    // where they are used, chunks later)
+    auto ld_range = [&](int c, int64_t& lo, int64_t& hi) {
+      const int p0 = c * CH < n ? c * CH : n, p1 = c * CH + CH < n ? c * CH + CH : n;
+      lo = w.trans_off[a + p0];
+      hi = w.trans_off[a + p1];
+    };
+    float pTa[U], pEa[CH], pTb[U], pEb[CH];
+    auto ld_data = [&](int c, int m, int lo, int hi, float (&pT)[U], float (&pE)[CH]) {
+      // raw values, no select on them here (a select would wait for the
+      // load): the steps read only a window's valid floats and a point's
+      // candidates (lo, hi: from the trace's first float; past hi, the
+      // stream's capacity headroom)
+      (void)m;
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int f = lo + u * G + j;
-        pT[u] = fits && f < hi ? w.trans[t0 + f] : 0.0f;
+        pT[u] = w.trans[t0 + (f < hi ? f : lo)];
       }
 #pragma unroll
       for (int k = 0; k < CH; ++k) {
-        const int mk = __shfl(m, gb + k, TB);
-        pE[k] = (mk & 0x40) && j < (mk & 0x3F) ? cemis(w, a + c * CH + k, j) : 0.0f;
+        const int pl = c * CH + k < nl ? c * CH + k : nl;
+        pE[k] = j < KIN ? w.cand_em[(a + pl) * KIN + j] : w.cand_xem[(a + pl) * KX + (j - KIN)];
       }
     };
-    int mA = ld_meta(0), mB = ld_meta(1);
-    int64_t loA, hiA, loB, hiB;
-    ld_range(0, loA, hiA);
-    ld_range(1, loB, hiB);
-    ld_data(0, mA, (int)(loA - t0), (int)(hiA - t0));
+    int m0 = ld_meta(0), m1 = ld_meta(1), m2 = ld_meta(2), m3 = ld_meta(3);
+    int64_t lo0, hi0, lo1, hi1, lo2, hi2, lo3, hi3;
+    ld_range(0, lo0, hi0);
+    ld_range(1, lo1, hi1);
+    ld_range(2, lo2, hi2);
+    ld_range(3, lo3, hi3);
+    ld_data(0, m0, (int)(lo0 - t0), (int)(hi0 - t0), pTa, pEa);
+    ld_data(1, m1, (int)(lo1 - t0), (int)(hi1 - t0), pTb, pEb);
     // ---- forward pass (wave-uniform step count; groups predicated)
     float prev = INFINITY;
     bool open = false;
@@ -2494,20 +2516,13 @@ __global__ __launch_bounds__(TB, OTM_VG_WAVES) void k_viterbi_g(DevBatch b, DevW
       }
       if (j == 0) sFl[g][last] = (uint8_t)(sFl[g][last] | VG_END | (bi << 3));
     };
-    for (int c = 0; c < nch; ++c) {
-      // stage chunk c, then start chunk c + 1's loads
+    auto stage = [&](const float (&pT)[U], const float (&pE)[CH]) {
 #pragma unroll
       for (int u = 0; u < U; ++u) sT[g][u * G + j] = pT[u];
 #pragma unroll
       for (int k = 0; k < CH; ++k) sE[g][k * G + j] = pE[k];
-      const int m_c = mA, lo_c = (int)(loA - t0), hi_c = (int)(hiA - t0);
-      mA = mB;
-      loA = loB;
-      hiA = hiB;
-      mB = ld_meta(c + 2);
-      ld_range(c + 2, loB, hiB);
-      __syncthreads();
-      if (c + 1 < nch) ld_data(c + 1, mA, (int)(loA - t0), (int)(hiA - t0));
+    };
+    auto chunk = [&](int c, int m_c, int lo_c, int hi_c) {
       // A step, for every group at once: its point's byte by shuffle, its
       // emission and block from LDS, Kq in fours (loads issued together), its
       // backpointers as one byte per state in LDS.  The loop bounds are
@@ -2586,7 +2601,41 @@ __global__ __launch_bounds__(TB, OTM_VG_WAVES) void k_viterbi_g(DevBatch b, DevW
           lastK = Kp;
         }
       }
-      __syncthreads();  // (the next chunk's staging overwrites the windows)
+    };
+    for (int c = 0; c < nch; c += 2) {
+      // chunk c from set A; chunk c + 2's loads into A behind it
+      stage(pTa, pEa);
+      const int ma = m0, la = (int)(lo0 - t0), ha = (int)(hi0 - t0);
+      const int mn0 = ld_meta(c + 4);
+      int64_t ln0, hn0;
+      ld_range(c + 4, ln0, hn0);
+      wave_sync();
+      ld_data(c + 2, m2, (int)(lo2 - t0), (int)(hi2 - t0), pTa, pEa);
+      chunk(c, ma, la, ha);
+      wave_sync();  // (the next chunk's staging overwrites the windows)
+      if (c + 1 >= nch) break;
+      // chunk c + 1 from set B; chunk c + 3's loads into B
+      stage(pTb, pEb);
+      const int mb = m1, lb = (int)(lo1 - t0), hb = (int)(hi1 - t0);
+      const int mn1 = ld_meta(c + 5);
+      int64_t ln1, hn1;
+      ld_range(c + 5, ln1, hn1);
+      wave_sync();
+      ld_data(c + 3, m3, (int)(lo3 - t0), (int)(hi3 - t0), pTb, pEb);
+      chunk(c + 1, mb, lb, hb);
+      wave_sync();
+      m0 = m2;
+      lo0 = lo2;
+      hi0 = hi2;
+      m1 = m3;
+      lo1 = lo3;
+      hi1 = hi3;
+      m2 = mn0;
+      lo2 = ln0;
+      hi2 = hn0;
+      m3 = mn1;
+      lo3 = ln1;
+      hi3 = hn1;
     }
     if (act && open) end_chain();
     __syncthreads();

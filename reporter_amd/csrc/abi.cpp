@@ -989,18 +989,20 @@ void report_many(otm_engine* E, int n, const char* const* reqs, const size_t* le
   }
 }
 
-// A large otm_report_batch as a pipeline (OTM_PIPE_CHUNKS, default 4, chunks
-// of about equal bytes; batches under OTM_PIPE_MIN requests, default 4096,
-// stay whole): chunk k runs on its own batch context (this engine, then its
-// pipeline clones) on its own thread, the chunks' request copies cross the
-// link one after another in chunk order (H2DOrder), so chunk k+1's bytes move
-// while chunk k runs its kernels and chunk k's responses come back while k+1
-// runs.  Each chunk is the same request/response contract as a whole batch
-// (every response depends only on its own request); the stderr lines come
-// out in chunk order.
+// A large otm_report_batch as a pipeline (OTM_PIPE_CHUNKS chunks of about
+// equal bytes, default 1 = one batch; batches under OTM_PIPE_MIN requests,
+// default 4096, stay whole): chunk k runs on its own batch context (this
+// engine, then its pipeline clones) on its own thread, the chunks' request
+// copies cross the link one after another in chunk order (H2DOrder), so chunk
+// k+1's bytes move while chunk k runs its kernels and chunk k's responses come
+// back while k+1 runs.  Each chunk is the same request/response contract as a
+// whole batch (every response depends only on its own request); the stderr
+// lines come out in chunk order.  Measured not faster on 10k requests (2 or 4
+// chunks 156-173M points/s against 162-169M whole, profiles/r04_ab/json_*),
+// so off by default.
 int pipe_chunks() {
   const char* e = std::getenv("OTM_PIPE_CHUNKS");
-  return e ? std::max(1, std::min(8, std::atoi(e))) : 4;
+  return e ? std::max(1, std::min(8, std::atoi(e))) : 1;
 }
 int pipe_min() {
   const char* e = std::getenv("OTM_PIPE_MIN");

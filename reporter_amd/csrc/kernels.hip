@@ -3914,10 +3914,19 @@ void launch_transitions(const DevGraph& g, const DevBatch& b, const DevParams& p
   mk.end(KN_TRANS_GLOBAL, s);
 }
 void launch_viterbi(const DevBatch& b, DevWork& w, hipStream_t s, const Marks& mk) {
-  static const int form = [] {
-    const char* e = std::getenv("OTM_VIT_FORM");  // A/B: 64 = the wave-per-trace form for every trace
-    return e ? std::atoi(e) : 8;
-  }();
+  // the form: OTM_VIT_FORM (8, 16 or 64) for A/B; by default the grouped
+  // forms from OTM_VIT_G_MIN traces up (default 32768), the wave form below:
+  // a small batch's waves all fit the GPU at once, so its time is one wave's
+  // (~100 steps of a latency-bound chain either way), while a large batch's
+  // is wave rounds, which 8 traces per wave divide (round-4 A/B,
+  // profiles/r04_ab/vit_form_*: config 2 0.157 ms wave form vs 0.50 grouped,
+  // config 4 1.13 vs 0.73)
+  // (read per batch: tests switch them)
+  const char* fe = std::getenv("OTM_VIT_FORM");
+  const char* ge = std::getenv("OTM_VIT_G_MIN");
+  const int forced = fe ? std::atoi(fe) : 0;
+  const int gmin = ge ? std::atoi(ge) : 32768;
+  const int form = forced ? forced : (b.n_traces >= gmin ? 8 : 64);
   if (form == 64) {
     TIMED(KN_VITERBI, hipLaunchKernelGGL(k_viterbi, dim3(grid_for(b.n_traces, 1, WAVE_GRID_CAP)), dim3(TB), 0, s, b,
                                          w, (const int32_t*)nullptr, (const int32_t*)nullptr, 1));

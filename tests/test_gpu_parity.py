@@ -436,6 +436,28 @@ def test_json_report_pipelined_chunks(small_graph, oracle, monkeypatch, capfd, c
         assert got == oracle.handle_request(g, body), body[:80]
 
 
+@pytest.mark.parametrize("form", ["8", "16", "64"])
+def test_viterbi_forms(small_graph, rural_graph, oracle, results_equal, monkeypatch, form):
+    """K5's three forms (kernels.hip launch_viterbi: 8 or 16 lanes per trace,
+    each handing what it cannot take to the next, and the wave form) on the
+    same batches, every stage bit-identical to the oracle: long traces past
+    the grouped forms' 128 points, columns wider than 8 and 16 candidates
+    (a 120 m radius in the city), chain breaks (gaps past the breakage
+    distance) and a sparse rural graph."""
+    monkeypatch.setenv("OTM_VIT_FORM", form)
+    b = synth.make_traces(small_graph, 300, 60, seed=29)
+    _run_both(small_graph, b, oracle, results_equal, counters=False)
+    wide = synth.make_traces(small_graph, 120, 50, interval_s=5.0, noise_sigma_m=25.0, accuracy=25.0, seed=31)
+    _run_both(small_graph, wide, oracle, results_equal, meili=dict(search_radius=120.0, max_search_radius=120.0),
+              counters=False)
+    long_ = synth.make_traces(small_graph, 20, 300, interval_s=5.0, seed=37)
+    _run_both(small_graph, long_, oracle, results_equal, counters=False)
+    gaps = synth.make_traces(small_graph, 100, 40, interval_s=240.0, noise_sigma_m=15.0, accuracy=15.0, seed=41)
+    _run_both(small_graph, gaps, oracle, results_equal, meili=dict(breakage_distance=800.0), counters=False)
+    rural = synth.make_traces(rural_graph, 200, 60, interval_s=30.0, noise_sigma_m=50.0, accuracy=50.0, seed=43)
+    _run_both(rural_graph, rural, oracle, results_equal, counters=False)
+
+
 def test_histogram_matches_reports(small_graph):
     import torch
     b = synth.make_traces(small_graph, 300, 100, seed=23)

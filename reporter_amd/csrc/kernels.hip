@@ -2408,9 +2408,11 @@ __global__ __launch_bounds__(TB, OTM_VG_WAVES) void k_viterbi_g(DevBatch b, DevW
   // spill snapshot B (see k_viterbi)
   if (OTM_FOLD_BOOKKEEPING && snap && blockIdx.x == 0 && threadIdx.x == 0) fold_snap(w, 1, true);
   if (*w.abort) return;
-  __shared__ float sT[NT][VT];
-  __shared__ float sE[NT][CH * G];  // [point of the chunk][state]
-  __shared__ uint8_t sBp[NT][VG_PTS][G];  // backpointer of each state (0xFF: dead)
+  // (group rows padded by one word: the groups' same offsets on different banks;
+  // unpadded, 44 % of the LDS cycles were bank conflicts, config 2)
+  __shared__ float sT[NT][VT + 1];
+  __shared__ float sE[NT][CH * G + 1];  // [point of the chunk][state]
+  __shared__ uint8_t sBp[NT][VG_PTS * G + 4];  // backpointer of each state (0xFF: dead), [point * G + state]
   __shared__ uint8_t sFl[NT][VG_PTS];  // flags; after the walk: VG_CS | (state + 1) << 3
   const int lane = threadIdx.x;
   const int g = lane / G, j = lane % G, gb = g * G;
@@ -2582,7 +2584,7 @@ __global__ __launch_bounds__(TB, OTM_VG_WAVES) void k_viterbi_g(DevBatch b, DevW
           const bool alive = link && j < Kp && bi >= 0;
           if (link) {
             cur = alive ? best + em : INFINITY;
-            sBp[g][pl][j] = (uint8_t)(alive ? bi : 0xFF);
+            sBp[g][pl * G + j] = (uint8_t)(alive ? bi : 0xFF);
             if (((__ballot(alive) >> gb) & (unsigned long long)gmask) != 0ull) started = true;
             else end_chain();
           }
@@ -2654,7 +2656,7 @@ __global__ __launch_bounds__(TB, OTM_VG_WAVES) void k_viterbi_g(DevBatch b, DevW
           if (f & VG_CS) {
             sv = -1;
           } else {
-            sv = sBp[g][pl][sv];
+            sv = sBp[g][pl * G + sv];
           }
         }
       }
@@ -3948,7 +3950,8 @@ void launch_viterbi(const DevBatch& b, DevWork& w, hipStream_t s, const Marks& m
   } else {
     hipLaunchKernelGGL(k_viterbi_g<8>, dim3(grid_for(b.n_traces, TB / 8, WAVE_GRID_CAP)), dim3(TB), 0, s, b, w,
                        (const int32_t*)nullptr, (const int32_t*)nullptr, l8, n8, 1);
-    hipLaunchKernelGGL(k_viterbi_g<16>, dim3(grid_for(b.n_traces / 8 + 1, TB / 16, 2048)), dim3(TB), 0, s, b, w,
+    // (sized for every trace: a block whose list entries ran out exits at once)
+    hipLaunchKernelGGL(k_viterbi_g<16>, dim3(grid_for(b.n_traces, TB / 16, WAVE_GRID_CAP)), dim3(TB), 0, s, b, w,
                        (const int32_t*)l8, (const int32_t*)n8, l16, n16, 0);
   }
   hipLaunchKernelGGL(k_viterbi, dim3(grid_for(b.n_traces / 64 + 1, 1, 1024)), dim3(TB), 0, s, b, w,

@@ -76,6 +76,39 @@ __device__ __forceinline__ float seg_sqdist(float alat, float alon, float blat, 
   return px * px + py * py;
 }
 
+// seg_sqdist for the lane tier's scan, with a division-free early out: a
+// segment whose whole line lies farther than the radius (cross(a, v)^2 >
+// r2m x |v|^2, r2m = r^2 x 1.001) is a miss, reported as +inf; any other is
+// seg_sqdist's exact value (same operations).  The 0.1 % margin is far above
+// the few-ulp rounding of the cross product and of seg_sqdist itself, so a
+// segment the test drops is one seg_sqdist would have put beyond r^2 too.
+#ifndef OTM_CAND_LINE_TEST
+#define OTM_CAND_LINE_TEST 1
+#endif
+__device__ __forceinline__ float seg_sqdist_r(float alat, float alon, float blat, float blon, float lat, float lon,
+                                              float ls, float r2m) {
+  const float ax = (alon - lon) * ls;
+  const float ay = (alat - lat) * MPD_F;
+  const float bx = (blon - lon) * ls;
+  const float by = (blat - lat) * MPD_F;
+  const float vx = bx - ax;
+  const float vy = by - ay;
+  const float l2 = vx * vx + vy * vy;
+  if (OTM_CAND_LINE_TEST) {
+    const float cr = ax * vy - ay * vx;
+    if (cr * cr > r2m * l2) return INFINITY;
+  }
+  float t = 0.0f;
+  if (l2 > 0.0f) {
+    const float dot = ax * vx + ay * vy;
+    t = -dot / l2;
+    t = t < 0.0f ? 0.0f : (t > 1.0f ? 1.0f : t);
+  }
+  const float px = ax + t * vx;
+  const float py = ay + t * vy;
+  return px * px + py * py;
+}
+
 __device__ __forceinline__ void project(const DevGraph& g, int32_t e, int32_t k, float lat, float lon, float ls,
                                         float& sqd, float& off_out, bool& at_end) {
   const int32_t a = g.e_shape_off[e] + k, b = a + 1;
@@ -568,6 +601,7 @@ __global__ __launch_bounds__(CAND_TB, OTM_CAND_WAVES) void k_cand_lane(DevGraph 
     const float lat = pr.x, lon = pr.y;
     const float r = probe_radius(P, pr.z);
     const float r2 = r * r;
+    const float r2m = r2 * 1.001f;  // (seg_sqdist_r's early-out margin)
     const float ls = MPD_F * cos_deg(lat);
     const float dlat = r / MPD_F;
     const float dlon = r / ls;
@@ -606,7 +640,7 @@ __global__ __launch_bounds__(CAND_TB, OTM_CAND_WAVES) void k_cand_lane(DevGraph 
             if (q + u < q1) {
               const float4 G = g.ent_geo[q + u];
               en[u] = g.cell_ent[q + u];
-              sq[u] = seg_sqdist(G.x, G.y, G.z, G.w, lat, lon, ls);
+              sq[u] = seg_sqdist_r(G.x, G.y, G.z, G.w, lat, lon, ls, r2m);
             }
           }
 #pragma unroll

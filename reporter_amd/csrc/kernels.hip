@@ -82,8 +82,11 @@ __device__ __forceinline__ float seg_sqdist(float alat, float alon, float blat, 
 // seg_sqdist's exact value (same operations).  The 0.1 % margin is far above
 // the few-ulp rounding of the cross product and of seg_sqdist itself, so a
 // segment the test drops is one seg_sqdist would have put beyond r^2 too.
+// Measured slower (round 4, bit-identical: k_cand_lane 0.229 vs 0.221 ms on
+// config 2, 1.89 vs 1.85 on config 4; profiles/r04_ab/cand_line/): the
+// branch splits the wave where the division did not; off by default.
 #ifndef OTM_CAND_LINE_TEST
-#define OTM_CAND_LINE_TEST 1
+#define OTM_CAND_LINE_TEST 0
 #endif
 __device__ __forceinline__ float seg_sqdist_r(float alat, float alon, float blat, float blon, float lat, float lon,
                                               float ls, float r2m) {

@@ -2421,8 +2421,13 @@ __device__ __forceinline__ int wave_max_i(int v) {
   }
   return v;
 }
-#ifndef OTM_VG_WAVES
-#define OTM_VG_WAVES 3
+// waves per SIMD: 8 lanes per trace fits 4 in 128 VGPRs with a 12-float
+// window per lane; 16 lanes per trace spills at 4, so 3
+#ifndef OTM_VG8_WAVES
+#define OTM_VG8_WAVES 4
+#endif
+#ifndef OTM_VG8_U
+#define OTM_VG8_U 8
 #endif
 // points per chunk: 8 or 16 overflowed the 16-float-per-lane window on most of
 // config 2's chunks (~20 transition floats per column), whose steps then read
@@ -2433,13 +2438,13 @@ __device__ __forceinline__ int wave_max_i(int v) {
 constexpr int VG_PTS = 128;  // points per trace
 constexpr uint8_t VG_COL = 1, VG_CS = 2, VG_END = 4;  // point flags (VG_END: argmin state in bits 3..7)
 template <int G>
-__global__ __launch_bounds__(TB, OTM_VG_WAVES) void k_viterbi_g(DevBatch b, DevWork w, const int32_t* list,
+__global__ __launch_bounds__(TB, G == 8 ? OTM_VG8_WAVES : 3) void k_viterbi_g(DevBatch b, DevWork w, const int32_t* list,
                                                                 const int32_t* list_n, int32_t* rej, int32_t* rej_n,
                                                                 int snap) {
   static_assert(G == 8 || G == 16, "8 or 16 lanes per trace");
   constexpr int NT = TB / G;
-  constexpr int VT = 16 * G;  // transition floats per chunk window (16 per lane)
-  constexpr int U = VT / G;
+  constexpr int U = G == 8 ? OTM_VG8_U : 16;  // transition floats per lane per chunk
+  constexpr int VT = U * G;                    // ... per chunk window
   constexpr int CH = OTM_VG_CHUNK;  // points per chunk (<= G)
   static_assert(CH <= G, "a chunk's metadata is one byte per lane");
   // spill snapshot B (see k_viterbi)
@@ -2449,7 +2454,8 @@ __global__ __launch_bounds__(TB, OTM_VG_WAVES) void k_viterbi_g(DevBatch b, DevW
   // unpadded, 44 % of the LDS cycles were bank conflicts, config 2)
   __shared__ float sT[NT][VT + 1];
   __shared__ float sE[NT][CH * G + 1];  // [point of the chunk][state]
-  __shared__ uint8_t sBp[NT][VG_PTS * G + 4];  // backpointer of each state (0xFF: dead), [point * G + state]
+  // backpointers, a nibble per state (15: dead), two states a byte: [point * G / 2 + state / 2]
+  __shared__ uint8_t sBp[NT][VG_PTS * G / 2 + 4];
   __shared__ uint8_t sFl[NT][VG_PTS];  // flags; after the walk: VG_CS | (state + 1) << 3
   const int lane = threadIdx.x;
   const int g = lane / G, j = lane % G, gb = g * G;
@@ -2621,7 +2627,9 @@ __global__ __launch_bounds__(TB, OTM_VG_WAVES) void k_viterbi_g(DevBatch b, DevW
           const bool alive = link && j < Kp && bi >= 0;
           if (link) {
             cur = alive ? best + em : INFINITY;
-            sBp[g][pl * G + j] = (uint8_t)(alive ? bi : 0xFF);
+            const int nib = alive ? bi : 15;
+            const int pair = __shfl_xor(nib, 1, G);  // (every lane of a linked group is here)
+            if (!(j & 1)) sBp[g][pl * (G / 2) + (j >> 1)] = (uint8_t)(nib | (pair << 4));
             if (((__ballot(alive) >> gb) & (unsigned long long)gmask) != 0ull) started = true;
             else end_chain();
           }
@@ -2693,7 +2701,7 @@ __global__ __launch_bounds__(TB, OTM_VG_WAVES) void k_viterbi_g(DevBatch b, DevW
           if (f & VG_CS) {
             sv = -1;
           } else {
-            sv = sBp[g][pl * G + sv];
+            sv = (sBp[g][pl * (G / 2) + (sv >> 1)] >> ((sv & 1) * 4)) & 15;
           }
         }
       }

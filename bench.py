@@ -338,6 +338,7 @@ def main():
     ms_per_step = elapsed * 1e3 / args.steps
     spill = eng.spill_stats()
     index = eng.index_info()
+    grid = eng.grid_info()
 
     # ---- host-inclusive leg (config 2 "via Java FFM host"): the binary C-ABI
     # call the host makes, otm_match_soa, from host arrays to host results --
@@ -750,6 +751,7 @@ def main():
                 args.config][0],
             "config": {"workload": WORKLOAD[args.config][1] % (len(ids), args.points, P),
                        "points_per_gpu": P, "vehicles_per_gpu": len(ids), "graph": ginfo,
+                       "candidate_grid_mult": grid.get("mult"),
                        "batches_in_flight": inflight,
                        "parallelism": "uuid shards x%d, %d batches in flight per GPU (HIP streams), RCCL "
                                       "reduce-scatter of %dx%d histograms per timed window" %

@@ -106,18 +106,18 @@ uint32_t turn_units(float factor, int d) {
 // Grid multiplier when the config names none: the m that minimises the
 // modelled cost of a probe's cell walk, ROW_COST x rows + entries scanned,
 // with rows = box / (m cell) + 1 for a radius box of 2 x search_radius and
-// entries = (entries per file cell) x m^2 x rows^2.  ROW_COST = 80 entries is
-// fitted to the candidate kernel's times on configs 2 and 4 (DESIGN.md §5;
-// round 4 refit at config 4's 200 m radius, profiles/r04_ab/grid_inflight/:
-// m = 6 / 8 / 10 / 12 / 16 gave 1.77 / 1.59 / 1.57 / 1.59 / 1.70 ms where
-// ROW_COST 32 had picked 5-6 at 1.84): the city (2.9 entries per 56 m cell,
-// 50 m radius) gets 2 (m = 1 / 2 / 3: 0.243 / 0.222 / 0.261 ms), the state
-// graph (0.35 per cell, 200 m) 8.
+// entries = (entries per file cell) x m^2 x rows^2.  The row cost, in
+// entries, grows as the graph thins -- 40 x sqrt(2.9 / density), an empirical
+// fit to the candidate kernel's times on configs 2 and 4 (round 4,
+// profiles/r04_ab/grid_inflight/): the city (2.9 entries per 56 m cell, 50 m
+// radius) gets 2 (m = 1 / 2 / 3: 0.243 / 0.222 / 0.261 ms), the state graph
+// (0.35 per cell, 200 m) 9 (m = 6 / 8 / 10 / 12 / 16: 1.77 / 1.59 / 1.57 /
+// 1.59 / 1.70 ms, where round 3's constant 32 picked 5-6 at 1.84 ms).
 static int auto_grid_mult(const otm_engine* E) {
-  constexpr double ROW_COST = 80.0;
   const auto& h = E->host.h;
   const double cells = std::max(1.0, (double)h.grid_rows * (double)h.grid_cols);
   const double dens = (double)h.n_cell_entries / cells;
+  const double ROW_COST = std::min(160.0, std::max(32.0, 40.0 * std::sqrt(2.9 / std::max(dens, 1e-3))));
   const double cell_m = h.grid_cell_deg * 111195.0;
   const double box = 2.0 * std::max(1.0, (double)E->mc.search_radius);
   int best = 1;

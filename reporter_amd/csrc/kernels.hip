@@ -565,10 +565,12 @@ constexpr int CAND_TB = OTM_CAND_TB;
 #endif
 constexpr int CAND_INFL = OTM_CAND_INFL;
 // transition index tier: pairs per lane whose first slot loads are issued
-// together: 2 measured 0.337 -> 0.302 ms on config 2, 1.956 -> 1.888 ms on
-// config 4; 3 and 4 slower (0.365 / 0.436 ms: registers, 4 spills)
+// together.  Round 2 measured 2 best (0.337 -> 0.302 ms on config 2, 1.956 ->
+// 1.888 ms on config 4; 3 and 4 slower: registers, spills); on round 4's
+// kernel 1 is (0.213 / 0.251 / 0.298 ms for 1 / 2 / 3 on config 2, 2.164 /
+// 2.351 / 2.478 ms on config 4, profiles/r04_ab/trans_batch/)
 #ifndef OTM_TRANS_BATCH
-#define OTM_TRANS_BATCH 2
+#define OTM_TRANS_BATCH 1
 #endif
 
 // wave-reduce a per-lane count and add it to a device counter (all 64 lanes active)

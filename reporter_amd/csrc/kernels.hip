@@ -546,8 +546,10 @@ constexpr uint32_t NODE_ENT = 0x80000000u;
 // (0.39 ms with the wave tier vs 0.40 at 12, 0.45 at 16): a smaller LDS list
 // buys occupancy; the ~1 % of probes with more edges in range spill.
 constexpr int CAND_LANE_CAP = OTM_CAND_LANE_CAP;
+// lane tier block size: 256 (round 4: k_cand_lane 1.518 vs 1.576 ms at 128 on
+// config 4, 0.220 vs 0.222 on config 2; 64 no better, profiles/r04_ab/knobs/)
 #ifndef OTM_CAND_TB
-#define OTM_CAND_TB 128
+#define OTM_CAND_TB 256
 #endif
 // min waves per SIMD for the lane tier: 8 caps it at 64 VGPRs (0.276 ->
 // 0.255 ms on config 2, 3.86 -> 3.76 ms on config 4; 6 measured no change)

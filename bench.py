@@ -338,6 +338,7 @@ def main():
     ms_per_step = elapsed * 1e3 / args.steps
     spill = eng.spill_stats()
     index = eng.index_info()
+    index_levels = eng.index_levels()
     grid = eng.grid_info()
 
     # ---- host-inclusive leg (config 2 "via Java FFM host"): the binary C-ABI
@@ -650,6 +651,7 @@ def main():
         roof["index_build_ms"] = index["build_ms"]
         roof["index_radius_m"] = index["radius_m"]
         roof["index_entries"] = index["entries"]
+        roof["index_near"] = index_levels
 
     # ---- CPU baseline: the oracle on this GPU's batch, host threads.  Two
     # figures on the same bounded sample: binary (trace arrays in, typed

@@ -335,6 +335,14 @@ int otm_graph_info(const otm_engine* eng, int64_t* n_nodes, int64_t* n_edges,
 int otm_index_info(const otm_engine* eng, float* rmax, int64_t* entries,
                    int32_t* incomplete_rows, float* build_ms);
 
+/* The near indexes: the same rows at smaller radii (config
+ * "otm":{"index_near_m": [r, ...]}, [] = none; absent: one at 0.45 R when the
+ * index's tables reach 16 GB).  A transition or route query probes the
+ * smallest whose radius covers its bound, so its probes land in smaller
+ * tables; results are identical.  Writes up to `cap` radii (smallest first)
+ * and entry counts; returns the number of near indexes, or < 0 on error. */
+int otm_index_levels(const otm_engine* eng, float* radii, int64_t* entries, int cap);
+
 /* The candidate search's grid index on the device: the graph file's cells
  * (meili's 500 per 0.25 deg tile) merged mult x mult (config
  * "otm":{"grid_mult": m} or env OTM_GRID_MULT; absent or 0: chosen from the

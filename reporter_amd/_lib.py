@@ -151,6 +151,7 @@ def _declare(L):
         "otm_graph_info": (C.c_int, [vp, C.POINTER(i64), C.POINTER(i64), C.POINTER(i64)]),
         "otm_index_info": (C.c_int, [vp, C.POINTER(C.c_float), C.POINTER(i64), C.POINTER(i32),
                                      C.POINTER(C.c_float)]),
+        "otm_index_levels": (C.c_int, [vp, C.POINTER(C.c_float), C.POINTER(i64), C.c_int]),
         "otm_grid_info": (C.c_int, [vp, C.POINTER(C.c_double), C.POINTER(i32), C.POINTER(i32), C.POINTER(i64),
                                     C.POINTER(i32)]),
         "otm_set_counting": (C.c_int, [vp, C.c_int]),

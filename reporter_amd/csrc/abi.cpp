@@ -1367,6 +1367,28 @@ static int otm_engine_create_impl(const char* cfg_path, const int* devices, int 
   const Value* ir = o->get("index_radius_m");
   if (ir && ir->is_num()) E->index_rmax = (float)ir->num();
   if (const char* er = std::getenv("OTM_INDEX_RADIUS")) E->index_rmax = (float)std::atof(er);  // A/B override
+  // near index radii: a number or a list of numbers (0 or []: none)
+  const Value* inr = o->get("index_near_m");
+  if (inr && inr->is_num()) {
+    E->index_near_set = true;
+    E->index_near_m = {(float)inr->num()};
+  } else if (inr && inr->kind == otm::json::Kind::Arr) {
+    E->index_near_set = true;
+    E->index_near_m.clear();
+    for (const Value& v : inr->items)
+      if (v.is_num()) E->index_near_m.push_back((float)v.num());
+  }
+  if (const char* en = std::getenv("OTM_INDEX_NEAR")) {  // A/B override: comma-separated metres (0: none)
+    E->index_near_set = true;
+    E->index_near_m.clear();
+    for (const char* c = en; *c;) {
+      char* end = nullptr;
+      const float v = std::strtof(c, &end);
+      if (end == c) break;
+      E->index_near_m.push_back(v);
+      c = *end == ',' ? end + 1 : end;
+    }
+  }
   const Value* gm = o->get("grid_mult");
   if (gm && gm->kind == Kind::Int) E->grid_mult = (int)gm->i;
   if (const char* v = std::getenv("OTM_GRID_MULT")) E->grid_mult = std::atoi(v);
@@ -1819,6 +1841,21 @@ int otm_index_info(const otm_engine* E, float* rmax, int64_t* entries, int32_t* 
   if (incomplete_rows) *incomplete_rows = E->index_incomplete_rows;
   if (build_ms) *build_ms = E->index_build_ms;
   return OTM_OK;
+}
+
+int otm_index_levels(const otm_engine* E, float* radii, int64_t* entries, int cap) {
+  if (!E) return fail(OTM_EINVAL, "engine is NULL");
+  if (!E->members.empty()) E = E->members[0];
+  int n = 0;
+  for (int l = 0; l < otm::NEAR_LEVELS; ++l) {
+    if (!(E->idxn[l].rmax > 0.0f)) continue;
+    if (n < cap) {
+      if (radii) radii[n] = E->idxn[l].rmax;
+      if (entries) entries[n] = E->index_near_level_entries[l];
+    }
+    ++n;
+  }
+  return n;
 }
 
 int otm_grid_info(const otm_engine* E, double* cell_deg, int32_t* rows, int32_t* cols, int64_t* entries,

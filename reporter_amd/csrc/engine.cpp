@@ -346,6 +346,8 @@ int engine_clone(const otm_engine* P, otm_engine* C, std::string* err) {
   C->host.h = P->host.h;  // the header only: a clone reads no host graph sections
   C->g = P->g;
   C->idx = P->idx;
+  for (int l = 0; l < NEAR_LEVELS; ++l) C->idxn[l] = P->idxn[l];
+  for (int l = 0; l < NEAR_LEVELS; ++l) C->index_near_level_entries[l] = P->index_near_level_entries[l];
   C->index_rmax = P->index_rmax;
   C->index_entries = P->index_entries;
   C->index_slots = P->index_slots;
@@ -395,45 +397,32 @@ static float auto_index_radius(const otm_engine* E) {
 // its cost, route distance, turn units and predecessor edge, in a per-row
 // open-addressing table.  Two passes of the same deterministic search: count,
 // size + scan, insert.
-int build_index(otm_engine* E, std::string* err) {
-  E->idx = DevIndex{};
-  E->idx.rmax = 0.0f;
-  if (E->index_rmax < 0.0f) E->index_rmax = auto_index_radius(E);
-  if (!(E->index_rmax > 0.0f)) return OTM_OK;
+namespace {
+struct IndexBuilt {
+  DevIndex X{};
+  int64_t entries = 0, slots = 0;
+  int32_t incomplete = 0;
+};
+// One index at radius *r: count, size + scan, insert.  With `shrink`, a radius
+// whose slot tables exceed `budget` is cut (rows shrink as R^2) and counted
+// again, down to 100 m (then no index: *r = 0); without, such an index is
+// left out (*r = 0).
+int build_index_at(otm_engine* E, float* r, bool shrink, size_t budget, IndexBuilt& out, std::string* err) {
+  out = IndexBuilt{};
   const int32_t N = E->g.n_edges + E->g.n_nodes;  // rows
   hipStream_t s = E->stream;
-  hipEvent_t a, z;
-  HIPCHK(hipEventCreate(&a));
-  HIPCHK(hipEventCreate(&z));
-  HIPCHK(hipEventRecord(a, s));
   int32_t* row_cnt = nullptr;
   int64_t* row_off = nullptr;
   IdxRow* rows = nullptr;
   HIPCHK(hipMalloc(&row_cnt, ((size_t)N + 1) * 4));
-  E->graph_allocs.push_back(row_cnt);
   HIPCHK(hipMalloc(&row_off, ((size_t)N + 1) * 8));
-  E->graph_allocs.push_back(row_off);
   HIPCHK(hipMalloc(&rows, ((size_t)N + 1) * sizeof(IdxRow)));
-  E->graph_allocs.push_back(rows);
   size_t tmpb = scan_tmp_bytes(N) + 256;
   void* tmp = nullptr;
   HIPCHK(hipMalloc(&tmp, tmpb));
-  // HBM budget for the slot tables (20 B per slot: 16 B slot + 4 B predecessor): half of what is free
-  // after the graph, or OTM_INDEX_BUDGET_MB.  A graph whose rows at this
-  // radius exceed it gets a smaller radius (rows shrink as R^2), counted
-  // again; below 100 m the index is left off and the online tiers answer
-  // everything (same results, slower).
-  size_t budget = 0;
-  if (const char* bm = std::getenv("OTM_INDEX_BUDGET_MB")) {
-    budget = (size_t)std::strtoull(bm, nullptr, 0) << 20;
-  } else {
-    size_t fr = 0, tot = 0;
-    HIPCHK(hipMemGetInfo(&fr, &tot));
-    budget = fr / 2;
-  }
   int64_t total = 0;
   for (int attempt = 0;; ++attempt) {
-    launch_index_build(E->g, E->dp.turn_units, index_cost_bound(E->index_rmax), row_cnt, nullptr, nullptr, nullptr, false, s);
+    launch_index_build(E->g, E->dp.turn_units, index_cost_bound(*r), row_cnt, nullptr, nullptr, nullptr, false, s);
     launch_row_sizes(row_cnt, row_off, N, s);
     scan_i64(row_off, N, tmp, tmpb, s);
     launch_row_pack(row_cnt, row_off, rows, N, s);
@@ -441,47 +430,105 @@ int build_index(otm_engine* E, std::string* err) {
     HIPCHK(hipStreamSynchronize(s));
     const double need = ((double)total + 1.0) * 20.0;
     if (need <= (double)budget) break;
-    const float r = (float)(std::floor(E->index_rmax * std::sqrt((double)budget / need) * 0.9 / 50.0) * 50.0);
-    if (attempt == 4 || r < 100.0f) {
+    const float rr = (float)(std::floor(*r * std::sqrt((double)budget / need) * 0.9 / 50.0) * 50.0);
+    if (!shrink || attempt == 4 || rr < 100.0f) {
       (void)hipFree(tmp);
-      E->index_rmax = 0.0f;  // index off
-      E->index_entries = 0;
-      E->index_slots = 0;
-      E->index_incomplete_rows = 0;
-      HIPCHK(hipEventDestroy(a));
-      HIPCHK(hipEventDestroy(z));
+      (void)hipFree(rows);
+      (void)hipFree(row_off);
+      (void)hipFree(row_cnt);
+      *r = 0.0f;  // no index
       return OTM_OK;
     }
-    E->index_rmax = r;
+    *r = rr;
   }
   (void)hipFree(tmp);
+  E->graph_allocs.push_back(row_cnt);
+  E->graph_allocs.push_back(row_off);
+  E->graph_allocs.push_back(rows);
   void *slot = nullptr, *pred = nullptr;
   HIPCHK(hipMalloc(&slot, ((size_t)total + 1) * 16));
   E->graph_allocs.push_back(slot);
   HIPCHK(hipMemsetAsync(slot, 0xFF, ((size_t)total + 1) * 16, s));
   HIPCHK(hipMalloc(&pred, ((size_t)total + 1) * 4));
   E->graph_allocs.push_back(pred);
-  launch_index_build(E->g, E->dp.turn_units, index_cost_bound(E->index_rmax), row_cnt, rows, (uint4*)slot, (int32_t*)pred, true, s);
-  HIPCHK(hipEventRecord(z, s));
+  launch_index_build(E->g, E->dp.turn_units, index_cost_bound(*r), row_cnt, rows, (uint4*)slot, (int32_t*)pred, true, s);
   HIPCHK(hipGetLastError());
+  std::vector<int32_t> cnt((size_t)N);
+  HIPCHK(hipMemcpyAsync(cnt.data(), row_cnt, (size_t)N * 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  for (int32_t c : cnt) {
+    out.incomplete += c < 0;
+    out.entries += c > 0 ? c : 0;
+  }
+  out.slots = total;
+  out.X.rmax = *r;
+  out.X.cmax = index_cost_bound(*r);
+  out.X.row = rows;
+  out.X.slot = (const uint4*)slot;
+  out.X.pred = (const int32_t*)pred;
+  return OTM_OK;
+}
+
+// free HBM / 2, or OTM_INDEX_BUDGET_MB
+size_t index_budget() {
+  if (const char* bm = std::getenv("OTM_INDEX_BUDGET_MB")) return (size_t)std::strtoull(bm, nullptr, 0) << 20;
+  size_t fr = 0, tot = 0;
+  if (hipMemGetInfo(&fr, &tot) != hipSuccess) return 0;
+  return fr / 2;
+}
+}  // namespace
+
+int build_index(otm_engine* E, std::string* err) {
+  E->idx = DevIndex{};
+  for (auto& x : E->idxn) x = DevIndex{};
+  E->idx.rmax = 0.0f;
+  if (E->index_rmax < 0.0f) E->index_rmax = auto_index_radius(E);
+  if (!(E->index_rmax > 0.0f)) return OTM_OK;
+  hipStream_t s = E->stream;
+  hipEvent_t a, z;
+  HIPCHK(hipEventCreate(&a));
+  HIPCHK(hipEventCreate(&z));
+  HIPCHK(hipEventRecord(a, s));
+  // HBM budget for the slot tables (20 B per slot: 16 B slot + 4 B
+  // predecessor): half of what is free after the graph.  A graph whose rows at
+  // this radius exceed it gets a smaller radius; below 100 m the index is left
+  // off and the online tiers answer everything (same results, slower).
+  IndexBuilt full;
+  int rc = build_index_at(E, &E->index_rmax, true, index_budget(), full, err);
+  if (rc != OTM_OK) return rc;
+  E->idx = full.X;
+  E->index_entries = full.entries;
+  E->index_slots = full.slots;
+  E->index_incomplete_rows = full.incomplete;
+  // the near indexes: the same rows at smaller radii, each for the columns
+  // whose bound it is the smallest to cover (its tables a fraction of the
+  // size, so their probes share lines and cache); one that does not fit what
+  // is left is skipped
+  std::vector<float> radii;
+  if (E->index_near_set) {
+    radii = E->index_near_m;
+  } else if ((double)full.slots * 20.0 >= OTM_INDEX_NEAR_MIN_GB * 1e9) {
+    for (float f : std::initializer_list<float> OTM_INDEX_NEAR_FRACS) radii.push_back(E->index_rmax * f);
+  }
+  for (float& r : radii) r = (float)(std::floor(r / 50.0) * 50.0);
+  std::sort(radii.begin(), radii.end());
+  radii.erase(std::unique(radii.begin(), radii.end()), radii.end());
+  int nl = 0;
+  for (float rn : radii) {
+    if (nl == NEAR_LEVELS || !(E->idx.rmax > 0.0f) || rn < 100.0f || rn >= E->idx.rmax) continue;
+    IndexBuilt near;
+    rc = build_index_at(E, &rn, false, index_budget(), near, err);
+    if (rc != OTM_OK) return rc;
+    if (rn > 0.0f) {
+      E->index_near_level_entries[nl] = near.entries;
+      E->idxn[nl++] = near.X;
+    }
+  }
+  HIPCHK(hipEventRecord(z, s));
   HIPCHK(hipEventSynchronize(z));
   HIPCHK(hipEventElapsedTime(&E->index_build_ms, a, z));
   (void)hipEventDestroy(a);
   (void)hipEventDestroy(z);
-  std::vector<int32_t> cnt((size_t)N);
-  HIPCHK(hipMemcpy(cnt.data(), row_cnt, (size_t)N * 4, hipMemcpyDeviceToHost));
-  E->index_incomplete_rows = 0;
-  E->index_entries = 0;
-  for (int32_t c : cnt) {
-    E->index_incomplete_rows += c < 0;
-    E->index_entries += c > 0 ? c : 0;
-  }
-  E->index_slots = total;
-  E->idx.rmax = E->index_rmax;
-  E->idx.cmax = index_cost_bound(E->index_rmax);
-  E->idx.row = rows;
-  E->idx.slot = (const uint4*)slot;
-  E->idx.pred = (const int32_t*)pred;
   return OTM_OK;
 }
 
@@ -680,6 +727,7 @@ static int engine_match_once(otm_engine* E, const DevBatch& b, hipStream_t s, st
   w.overflow_list2 = P<int32_t>(E->overflow_list2);
   w.overflow_list3 = P<int32_t>(E->overflow_list3);
   w.idx = E->idx;
+  for (int l = 0; l < NEAR_LEVELS; ++l) w.idxn[l] = E->idxn[l];
   w.counters_i32 = P<int32_t>(E->counters_i32);
   w.snap = P<int32_t>(E->snap);
   w.ctr = E->counting ? E->ctr : nullptr;

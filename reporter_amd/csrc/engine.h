@@ -70,6 +70,14 @@ struct otm_engine {
   int32_t grid_rows = 0, grid_cols = 0;
   int64_t grid_entries = 0;
   otm::DevIndex idx{};
+  // near indexes (DevWork::idxn, smallest radius first, rmax 0: none): the same
+  // rows at the radii index_near_m (not set: OTM_INDEX_NEAR_FRACS x index_rmax
+  // when the index reaches OTM_INDEX_NEAR_MIN_GB), each probed by the columns
+  // whose bound it is the smallest to cover
+  otm::DevIndex idxn[otm::NEAR_LEVELS]{};
+  std::vector<float> index_near_m;
+  bool index_near_set = false;
+  int64_t index_near_level_entries[otm::NEAR_LEVELS]{};
   int64_t index_entries = 0;
   int64_t index_slots = 0;  // hash-table slots (16 B each + 4 B predecessor)
   int32_t index_incomplete_rows = 0;

@@ -114,6 +114,21 @@ struct DevIndex {
 };
 constexpr uint32_t NODE_KEY = 0x80000000u;  // key of a node's arrival label (edges: their id, < 2^27)
 constexpr uint32_t NONE_PRED = 0xFFFFFFFFu; // label predecessor of a route's first edge / the source node
+// near indexes: at most NEAR_LEVELS smaller radii of the same rows
+// (engine.cpp build_index).  By default one, at OTM_INDEX_NEAR_FRACS x the
+// index's radius, when the index's tables reach OTM_INDEX_NEAR_MIN_GB: a
+// large index's probes miss the caches, and a column whose bound the near
+// index covers then probes tables a fraction of the size (config 3: 137 GB,
+// k_trans_sub 4.65 -> 3.31 ms at 600 m of 1,250; config 4: 62 GB, 2.17 ->
+// 1.74 ms at 3.5 km of 10); a small one's probes hit the caches already and
+// two tables split them (config 2: 5 GB, 0.210 -> 0.225 ms at 400 m).
+constexpr int NEAR_LEVELS = 3;
+#ifndef OTM_INDEX_NEAR_FRACS
+#define OTM_INDEX_NEAR_FRACS {0.45f}
+#endif
+#ifndef OTM_INDEX_NEAR_MIN_GB
+#define OTM_INDEX_NEAR_MIN_GB 16.0
+#endif
 constexpr int INDEX_BUILD_LOG2 = 11;
 constexpr int INDEX_BUILD_CAP = 1 << INDEX_BUILD_LOG2;  // LDS table of the index builder
 constexpr int INDEX_BUILD_LIMIT = 1536; // labels per row before the row is left incomplete
@@ -203,6 +218,8 @@ struct DevWork {
                            // every later kernel returns at once and the host redoes the batch
   int64_t trans_cap;       // floats allocated for w.trans
   DevIndex idx;
+  DevIndex idxn[NEAR_LEVELS];  // near indexes, smallest radius first (rmax 0: none): a column
+                               // probes the first whose cmax covers its cost bound
   DevOrder ord;
   // global-tier scratch
   uint32_t* big_key;

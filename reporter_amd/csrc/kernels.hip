@@ -1345,24 +1345,46 @@ __device__ __forceinline__ uint32_t idx_hash(uint32_t v) {
 #ifndef OTM_IDX_LOAD_PCT
 #define OTM_IDX_LOAD_PCT 20
 #endif
-// OTM_IDX_HOME = 1 (round 4's A/B, not kept): a label's home in a row's
-// table is its road's lower-numbered node (an edge key: min(from, to); a node
-// key: the node), and a home hashes to an aligned group of IDX_GROUP slots,
-// one 128-B line, linear probing from there.  A column's target candidates --
-// a node and the two directions of the roads at it -- share a few homes (0.42
-// homes per key on config 2, 0.45 on config 4), but the lookups then walk the
-// merged runs of several homes slot by slot, each a dependent load:
-// k_trans_sub 0.248 -> 0.370 ms on config 2, 2.29 -> 5.25 ms on config 4
-// (profiles/r04_ab/index_home/).  Default 0: a home per key.
+// OTM_IDX_HOME = 1 (round 4's first A/B, not kept): a label's home in a
+// row's table is its road's lower-numbered node (an edge key: min(from, to);
+// a node key: the node), and a home hashes to an aligned group of 8 slots,
+// one 128-B line, linear probing slot by slot from there.  A column's target
+// candidates -- a node and the two directions of the roads at it -- share a
+// few homes (0.42 homes per key on config 2, 0.45 on config 4), but the
+// lookups then walk the merged runs of several homes one dependent load at a
+// time: k_trans_sub 0.248 -> 0.370 ms on config 2, 2.29 -> 5.25 ms on config 4
+// (profiles/r04_ab/index_home/).
+// OTM_IDX_BUCKET = 1: the same homes, but a row's table is a run of 8-slot
+// buckets (one 128-B line each) and a lookup reads its home's whole bucket
+// with eight independent 16-B loads of that line, going on to the next bucket
+// only when the bucket is full without the key.  Probes of one source row for
+// targets sharing a home fetch one line.  Buckets are filled to
+// OTM_IDX_BUCKET_LOAD percent on average.
+#ifndef OTM_IDX_BUCKET
+#define OTM_IDX_BUCKET 0
+#endif
+#ifndef OTM_IDX_BUCKET_LOAD
+#define OTM_IDX_BUCKET_LOAD 35
+#endif
+// OTM_IDX_BUCKET_KEYS = 1: k_trans_sub reads the bucket's 8 keys, then the
+// matching slot (a second, cache-hit load of the same line) -- 8 registers a
+// probe instead of 32
+#ifndef OTM_IDX_BUCKET_KEYS
+#define OTM_IDX_BUCKET_KEYS 0
+#endif
 #ifndef OTM_IDX_HOME
-#define OTM_IDX_HOME 0
+#define OTM_IDX_HOME OTM_IDX_BUCKET
 #endif
 #if OTM_IDX_HOME
 constexpr int IDX_GROUP = 8;
 #endif
 __host__ __device__ __forceinline__ int64_t idx_row_cap(int32_t c) {
   if (c <= 0) return 0;
-#if OTM_IDX_HOME
+#if OTM_IDX_BUCKET
+  int64_t nb = ((int64_t)c * 100 + (int64_t)OTM_IDX_BUCKET_LOAD * IDX_GROUP - 1) / ((int64_t)OTM_IDX_BUCKET_LOAD * IDX_GROUP);
+  if (nb * IDX_GROUP <= c) nb = (int64_t)c / IDX_GROUP + 1;
+  return nb * IDX_GROUP;
+#elif OTM_IDX_HOME
   int64_t cap = ((int64_t)c * 100 + OTM_IDX_LOAD_PCT - 1) / OTM_IDX_LOAD_PCT;
   if (cap <= c) cap = (int64_t)c + 1;
   return (cap + IDX_GROUP - 1) / IDX_GROUP * IDX_GROUP;
@@ -1399,6 +1421,37 @@ __device__ __forceinline__ uint32_t idx_slot0(uint32_t hh, const IdxRow& R) {
 __device__ __forceinline__ uint32_t idx_next(uint32_t h, const IdxRow& R) {
   return h + 1u == R.cap ? 0u : h + 1u;
 }
+#if OTM_IDX_BUCKET
+__device__ __forceinline__ uint32_t idx_next_bucket(uint32_t h, const IdxRow& R) {
+  return h + IDX_GROUP == R.cap ? 0u : h + IDX_GROUP;
+}
+// one bucket of row R from slot h: the eight slots are loaded before any is
+// looked at (one line, one round trip)
+struct IdxBucket {
+  uint4 s[IDX_GROUP];
+};
+__device__ __forceinline__ void idx_load_bucket(const uint4* slot, const IdxRow& R, uint32_t h, IdxBucket& B) {
+  const uint4* p = slot + R.off + h;
+#pragma unroll
+  for (int i = 0; i < IDX_GROUP; ++i) B.s[i] = p[i];
+}
+// the key's slot index in the bucket (its contents in out), -1 when absent
+// from a bucket that has an empty slot (absent from the row), -2 when the
+// bucket is full without it (look in the next)
+__device__ __forceinline__ int idx_scan_bucket(const IdxBucket& B, uint32_t v, uint4& out) {
+  int m = -2;
+  bool empty = false;
+#pragma unroll
+  for (int i = 0; i < IDX_GROUP; ++i) {
+    if (B.s[i].x == v) {
+      m = i;
+      out = B.s[i];
+    }
+    empty = empty || B.s[i].x == EMPTY;
+  }
+  return m >= 0 ? m : (empty ? -1 : -2);
+}
+#endif
 
 // Row lookup: linear probing in the row's table.  Returns the slot (its
 // contents in *out) when the key is in the row, -1 when absent (its label
@@ -1408,6 +1461,16 @@ __device__ __forceinline__ int64_t idx_find(const DevGraph& g, const DevIndex& X
   if (R.cnt < 0) return -2;
   if (R.cnt == 0) return -1;
   uint32_t h = idx_slot0(idx_home_hash(g, v), R);
+#if OTM_IDX_BUCKET
+  while (true) {
+    IdxBucket B;
+    idx_load_bucket(X.slot, R, h, B);
+    const int m = idx_scan_bucket(B, v, out);
+    if (m >= 0) return R.off + h + m;
+    if (m == -1) return -1;
+    h = idx_next_bucket(h, R);
+  }
+#endif
   while (true) {
     const uint4 sl = X.slot[R.off + h];
     if (sl.x == v) {
@@ -1476,7 +1539,20 @@ __global__ __launch_bounds__(TB) void k_index_build(DevGraph g, const uint32_t* 
       chain_sums(g, TU, predof, pk, hin, (k & NODE_KEY) ? NO_HEAD : (uint32_t)g.e_head_out[k], cbuf + lane, d, units,
                  len);
       uint32_t h = idx_slot0(idx_home_hash(g, k), R);
+#if OTM_IDX_BUCKET
+      // the first free slot of the first bucket with one, from the home's
+      // (a lookup stops at a bucket with an empty slot)
+      uint32_t t = 0;
+      while (atomicCAS(&slot[R.off + h + t].x, EMPTY, k) != EMPTY) {
+        if (++t == IDX_GROUP) {
+          t = 0;
+          h = idx_next_bucket(h, R);
+        }
+      }
+      h += t;
+#else
       while (atomicCAS(&slot[R.off + h].x, EMPTY, k) != EMPTY) h = idx_next(h, R);
+#endif
       slot[R.off + h].y = (uint32_t)(lab >> 32);
       slot[R.off + h].z = fbits(d);
       slot[R.off + h].w = units;
@@ -1529,8 +1605,13 @@ __global__ void k_row_pack(const int32_t* row_cnt, const int64_t* row_off, IdxRo
 #ifndef OTM_TRANS_KC8
 #define OTM_TRANS_KC8 8
 #endif
+// waves per SIMD the register budget is sized for (a bucket probe holds its
+// 8 slots, 32 registers)
+#ifndef OTM_TRANS_WAVES
+#define OTM_TRANS_WAVES (OTM_IDX_BUCKET && !OTM_IDX_BUCKET_KEYS ? 6 : 8)
+#endif
 template <int S, bool LIST>
-__global__ __launch_bounds__(TB, 8) void k_trans_sub(DevGraph g, DevBatch b, DevParams P, DevWork w) {
+__global__ __launch_bounds__(TB, OTM_TRANS_WAVES) void k_trans_sub(DevGraph g, DevBatch b, DevParams P, DevWork w) {
   if (*w.abort || trans_over_cap(b, w)) return;  // a capacity was exceeded: the host redoes the batch
   static_assert(S == 8 || S == 16, "8 lanes per column (two passes) or 16 (one pass / the wide pass)");
   constexpr int NS = TB / S;
@@ -1591,6 +1672,16 @@ __global__ __launch_bounds__(TB, 8) void k_trans_sub(DevGraph g, DevBatch b, Dev
     const float bound = P.factor * gcv;
     const uint32_t cq = index_cost_bound(bound);
     const bool idx_ok = X.rmax > 0.0f && cq <= X.cmax;
+    // the near index when it covers the bound (same answers, smaller tables)
+    const IdxRow* xrow = X.row;
+    const uint4* xslot = X.slot;
+#pragma unroll
+    for (int l = NEAR_LEVELS - 1; l >= 0; --l) {
+      if (w.idxn[l].rmax > 0.0f && cq <= w.idxn[l].cmax) {
+        xrow = w.idxn[l].row;
+        xslot = w.idxn[l].slot;
+      }
+    }
     const bool wide = WIDE && act && idx_ok && (Kp > KC || Kq > KC);
     if (wide && sl == 0) w.overflow_list2[atomicAdd(&w.counters_i32[6], 1)] = (int32_t)p;
     act = act && !wide;
@@ -1610,7 +1701,7 @@ __global__ __launch_bounds__(TB, 8) void k_trans_sub(DevGraph g, DevBatch b, Dev
         const float o = __int_as_float(c.y);
         sr[sg][k ^ swz] = make_int4(e, __float_as_int(o), __float_as_int(src_start(g, e, o)), (int)src_head(g, e, o));
         if (idx_ok) {
-          const IdxRow R = X.row[src_row(g, e, o)];
+          const IdxRow R = xrow[src_row(g, e, o)];
           rq[sg][k ^ swz] = R;
           bad = bad || R.cnt < 0;
         }
@@ -1626,6 +1717,85 @@ __global__ __launch_bounds__(TB, 8) void k_trans_sub(DevGraph g, DevBatch b, Dev
     if (act) {
       float* Tm = w.trans + toff;
       unsigned long long ntr = 0;
+#if OTM_IDX_BUCKET
+      // one pair per lane per step: its home's bucket of its source's row
+      const int npair = Kq * Kp;
+      for (int idx = sl; idx < npair; idx += S) {
+        const int i = idx / Kp, j = idx - (idx / Kp) * Kp;
+        const int4 T = tg[sg][j ^ swz], Sx = sr[sg][i ^ swz];
+        const IdxRow R = rq[sg][i ^ swz];
+        const uint32_t key = (uint32_t)T.z;
+        const int32_t ej = T.x, ei = Sx.x;
+        const float oj = __int_as_float(T.y), oi = __int_as_float(Sx.y), si = __int_as_float(Sx.z);
+        const bool same = same_edge_step(ei, oi, ej, oj);
+#if OTM_IDX_BUCKET_KEYS
+        // keys first (8 registers), the matching slot after (the same line)
+        uint32_t bk[IDX_GROUP];
+        uint32_t h = 0;
+        if (!same && R.cnt > 0) {
+          h = idx_slot0((uint32_t)T.w, R);
+#pragma unroll
+          for (int t = 0; t < IDX_GROUP; ++t) bk[t] = xslot[R.off + h + t].x;
+        }
+#else
+        IdxBucket B;
+        uint32_t h = 0;
+        if (!same && R.cnt > 0) {
+          h = idx_slot0((uint32_t)T.w, R);
+          idx_load_bucket(xslot, R, h, B);
+        }
+#endif
+        float r = 0.0f;
+        bool ok = true;
+        uint32_t units = 0;
+        if (same) {
+          r = same_edge_dist(oi, oj);
+        } else {
+          uint4 sv = make_uint4(EMPTY, 0u, 0u, 0u);
+          int m = -1;
+          if (R.cnt > 0) {
+#if OTM_IDX_BUCKET_KEYS
+            while (true) {
+              bool empty = false;
+              m = -2;
+#pragma unroll
+              for (int t = IDX_GROUP - 1; t >= 0; --t) {
+                m = bk[t] == key ? t : m;
+                empty = empty || bk[t] == EMPTY;
+              }
+              if (m >= 0 || empty) break;
+              h = idx_next_bucket(h, R);  // the home's bucket full without the key (rare)
+#pragma unroll
+              for (int t = 0; t < IDX_GROUP; ++t) bk[t] = xslot[R.off + h + t].x;
+            }
+            if (m >= 0) sv = xslot[R.off + h + m];
+#else
+            m = idx_scan_bucket(B, key, sv);
+            while (m == -2) {  // the home's bucket full without the key (rare)
+              h = idx_next_bucket(h, R);
+              idx_load_bucket(xslot, R, h, B);
+              m = idx_scan_bucket(B, key, sv);
+            }
+#endif
+          }
+          // a label of the row beyond this column's cost bound is not one
+          // of its search's labels
+          if (m >= 0 && sv.y <= cq) {
+            const float sd = si + bitsf(sv.z);
+            r = sd + oj;
+            units = sv.w;
+          } else {
+            ok = false;
+          }
+        }
+        float cost = INFINITY;
+        if (ok && r <= bound) {
+          cost = trans_cost(units, r, gcv, P.beta);
+          ++ntr;
+        }
+        Tm[i * Kp + j] = cost;
+      }
+#else
       // OTM_TRANS_BATCH pairs per lane per step: every pair's first slot is
       // loaded before any is resolved, so their probes are in flight together
       constexpr int NB = OTM_TRANS_BATCH;
@@ -1645,7 +1815,7 @@ __global__ __launch_bounds__(TB, 8) void k_trans_sub(DevGraph g, DevBatch b, Dev
             const bool same = same_edge_step(Sx.x, __int_as_float(Sx.y), T.x, __int_as_float(T.y));
             if (!same && R.cnt > 0) {
               h0[u] = idx_slot0((uint32_t)T.w, R);
-              s0[u] = X.slot[R.off + h0[u]];
+              s0[u] = xslot[R.off + h0[u]];
             }
           }
         }
@@ -1670,7 +1840,7 @@ __global__ __launch_bounds__(TB, 8) void k_trans_sub(DevGraph g, DevBatch b, Dev
             if (R.cnt > 0) {
               while (sv.x != key && sv.x != EMPTY) {  // the rest of the linear probe (rare)
                 h = idx_next(h, R);
-                sv = X.slot[R.off + h];
+                sv = xslot[R.off + h];
               }
             }
             // a label of the row beyond this column's cost bound is not one
@@ -1691,6 +1861,7 @@ __global__ __launch_bounds__(TB, 8) void k_trans_sub(DevGraph g, DevBatch b, Dev
           Tm[i * Kp + j] = cost;
         }
       }
+#endif
       if (w.ctr) {
         // algorithmic counts of the equivalent searches (per-lane partials,
         // summed over the wave at the end): per distinct source (node,
@@ -1707,7 +1878,7 @@ __global__ __launch_bounds__(TB, 8) void k_trans_sub(DevGraph g, DevBatch b, Dev
           if (!first) continue;
           const IdxRow R = rq[sg][i ^ swz];
           for (int64_t k = sl; k < (int64_t)R.cap; k += S) {
-            const uint4 slt = X.slot[R.off + k];
+            const uint4 slt = xslot[R.off + k];
             if (slt.x == EMPTY || (slt.x & NODE_KEY) || slt.y > cq) continue;
             ++c_settled;
             if ((unsigned long long)slt.y + g.e_len64[slt.x] <= cq) {
@@ -1771,9 +1942,15 @@ __global__ __launch_bounds__(256, OTM_ROUTE_WAVES) void k_route_index(DevGraph g
     IdxRow Rw{};
     int64_t sv = -1;
     uint4 lab{};
+    // the near index when it covers the bound (the same labels and paths)
+    int lvl = -1;
+#pragma unroll
+    for (int l = NEAR_LEVELS - 1; l >= 0; --l)
+      if (w.idxn[l].rmax > 0.0f && cq <= w.idxn[l].cmax) lvl = l;
+    const DevIndex& Xc = lvl >= 0 ? w.idxn[lvl] : X;
     if (X.rmax > 0.0f && cq <= X.cmax) {
-      Rw = X.row[src_row(g, ei, oi)];
-      sv = idx_find(g, X, Rw, dst_key(g, ej, oj), lab);
+      Rw = Xc.row[src_row(g, ei, oi)];
+      sv = idx_find(g, Xc, Rw, dst_key(g, ej, oj), lab);
     }
     if (sv < 0 || lab.y > cq) {
       const int slot = atomicAdd(&w.counters_i32[4], 1);
@@ -1782,7 +1959,7 @@ __global__ __launch_bounds__(256, OTM_ROUTE_WAVES) void k_route_index(DevGraph g
     }
     // the path: the label's predecessor slots in the row, back to the first edge
     int len = 0;
-    for (int32_t ps = X.pred[sv]; ps >= 0 && len <= Rw.cnt; ps = X.pred[Rw.off + ps]) ++len;
+    for (int32_t ps = Xc.pred[sv]; ps >= 0 && len <= Rw.cnt; ps = Xc.pred[Rw.off + ps]) ++len;
     const int off = len ? atomicAdd(&w.counters_i32[1], len) : 0;
     if (off + len > w.pool_cap) {
       w.counters_i32[2] = 1;
@@ -1790,8 +1967,8 @@ __global__ __launch_bounds__(256, OTM_ROUTE_WAVES) void k_route_index(DevGraph g
       w.path_len[p] = -1;
     } else {
       int k = len;
-      for (int32_t ps = X.pred[sv]; ps >= 0 && k > 0; ps = X.pred[Rw.off + ps])
-        w.path_pool[off + (--k)] = (int32_t)X.slot[Rw.off + ps].x;
+      for (int32_t ps = Xc.pred[sv]; ps >= 0 && k > 0; ps = Xc.pred[Rw.off + ps])
+        w.path_pool[off + (--k)] = (int32_t)Xc.slot[Rw.off + ps].x;
       w.path_off[p] = off;
       w.path_len[p] = len;
     }
@@ -1801,7 +1978,7 @@ __global__ __launch_bounds__(256, OTM_ROUTE_WAVES) void k_route_index(DevGraph g
     if (w.ctr) {
       unsigned long long st = 0, rl = 0;
       for (int64_t k = 0; k < (int64_t)Rw.cap; ++k) {
-        const uint4 sl = X.slot[Rw.off + k];
+        const uint4 sl = Xc.slot[Rw.off + k];
         if (sl.x == EMPTY || (sl.x & NODE_KEY) || sl.y > cq) continue;
         ++st;
         if ((unsigned long long)sl.y + g.e_len64[sl.x] <= cq) {

@@ -26,11 +26,16 @@ def _check(rc):
         raise OtmError("libotmatch error %d: %s" % (rc, _lib.last_error()))
 
 
-def write_config(path, graph_path, index_radius_m=None, grid_mult=None, trans_lanes=None, **meili):
-    """Write an engine config: {"otm":{"graph":...,"index_radius_m":R},"meili":{"default":{...}}}."""
+def write_config(path, graph_path, index_radius_m=None, grid_mult=None, trans_lanes=None, index_near_m=None,
+                 **meili):
+    """Write an engine config: {"otm":{"graph":...,"index_radius_m":R},"meili":{"default":{...}}}.
+    index_near_m: the near indexes' radii (a list; [] for none; default a
+    fraction of the index radius, engine.cpp build_index)."""
     otm = {"graph": os.path.abspath(graph_path)}
     if index_radius_m is not None:
         otm["index_radius_m"] = index_radius_m
+    if index_near_m is not None:
+        otm["index_near_m"] = list(index_near_m)
     if grid_mult is not None:
         otm["grid_mult"] = grid_mult
     if trans_lanes is not None:
@@ -53,7 +58,7 @@ class Results(object):
 
 class Engine(object):
     def __init__(self, config_path=None, graph_path=None, device=0, index_radius_m=None, grid_mult=None,
-                 trans_lanes=None, devices=None, **meili):
+                 trans_lanes=None, devices=None, index_near_m=None, **meili):
         """Either a config file (valhalla.Configure-style) or a graph path.
         devices=[d0, d1, ...] makes a multi-device engine (otm_engine_create
         with ndev > 1): traces go to member murmur2(uuid) % ndev."""
@@ -65,7 +70,7 @@ class Engine(object):
             fd, self._tmp = tempfile.mkstemp(suffix=".json", prefix="otm_cfg_")
             os.close(fd)
             config_path = write_config(self._tmp, graph_path, index_radius_m=index_radius_m, grid_mult=grid_mult,
-                                       trans_lanes=trans_lanes, **meili)
+                                       trans_lanes=trans_lanes, index_near_m=index_near_m, **meili)
         h = C.c_void_p()
         devs = list(devices) if devices is not None else [device]
         dev = (C.c_int * len(devs))(*devs)
@@ -241,6 +246,15 @@ class Engine(object):
         r, e, i, ms = C.c_float(), C.c_int64(), C.c_int32(), C.c_float()
         _check(lib().otm_index_info(self.h, C.byref(r), C.byref(e), C.byref(i), C.byref(ms)))
         return {"radius_m": r.value, "entries": e.value, "incomplete_rows": i.value, "build_ms": ms.value}
+
+    def index_levels(self):
+        """The near indexes: [{"radius_m": r, "entries": n}, ...], smallest radius first."""
+        r = (C.c_float * 8)()
+        e = (C.c_int64 * 8)()
+        n = lib().otm_index_levels(self.h, r, e, 8)
+        if n < 0:
+            raise OtmError("otm_index_levels failed: %s" % _lib.last_error())
+        return [{"radius_m": r[i], "entries": e[i]} for i in range(min(n, 8))]
 
     def grid_info(self):
         cd, r, c, n, m = C.c_double(), C.c_int32(), C.c_int32(), C.c_int64(), C.c_int32()

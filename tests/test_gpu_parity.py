@@ -61,10 +61,10 @@ def _stage_compare(eng, orc, batch):
 
 
 def _run_both(graph, batch, oracle, results_equal, meili=None, stages=True, counters=True, index_radius_m=None,
-              grid_mult=None, trans_lanes=None):
+              grid_mult=None, trans_lanes=None, index_near_m=None):
     meili = meili or {}
     with Engine(graph_path=graph, index_radius_m=index_radius_m, grid_mult=grid_mult, trans_lanes=trans_lanes,
-                **meili) as eng:
+                index_near_m=index_near_m, **meili) as eng:
         eng.set_counting(counters)
         res = eng.match(batch)
         p = oracle.params(**meili)
@@ -96,6 +96,16 @@ def test_city_sample_sigma15(small_graph, oracle, results_equal, batch_path, rad
     res, orc = _run_both(small_graph, b, oracle, results_equal, index_radius_m=radius, grid_mult=grid_mult)
     assert (res.traces["code"] == 200).mean() > 0.95
     assert len(res.segments) > 1000 and len(res.reports) > 50
+
+
+@pytest.mark.parametrize("near", [[], [300.0], [150.0, 300.0, 600.0]], ids=["none", "one", "three"])
+def test_near_indexes(small_graph, oracle, results_equal, near):
+    # columns probe the smallest near index covering their bound (the same
+    # rows at a smaller radius), the rest the full index: every stage, route
+    # and counter identical to the oracle with none, one or three levels.
+    # 15 s sampling spreads the bounds (5 x gc) over all of them.
+    b = synth.make_traces(small_graph, 200, 60, interval_s=15.0, noise_sigma_m=15.0, accuracy=15.0, seed=41)
+    _run_both(small_graph, b, oracle, results_equal, index_radius_m=1250.0, index_near_m=near)
 
 
 @pytest.mark.parametrize("lanes", [8, 16])
@@ -170,6 +180,15 @@ def test_index_info(small_graph):
         assert eng.index_info()["radius_m"] == 1250.0
     with Engine(graph_path=small_graph, index_radius_m=0) as eng:
         assert eng.index_info()["entries"] == 0
+        assert eng.index_levels() == []
+    # near indexes: none by default on a small index, else the radii asked
+    # below the index's, smallest first, each with fewer entries
+    with Engine(graph_path=small_graph, index_radius_m=1250.0) as eng:
+        assert eng.index_levels() == []
+    with Engine(graph_path=small_graph, index_radius_m=1250.0, index_near_m=[600.0, 300.0, 2000.0]) as eng:
+        lv = eng.index_levels()
+        assert [x["radius_m"] for x in lv] == [300.0, 600.0]
+        assert 0 < lv[0]["entries"] < lv[1]["entries"] < eng.index_info()["entries"]
 
 
 @pytest.mark.parametrize("expect", ["shrunk", "off"])

@@ -541,7 +541,7 @@ void engine_free(otm_engine* E) {
       &E->pt_trace,
       &E->is_col,        &E->prevc,        &E->nextc,        &E->gc,             &E->ncand,          &E->cand_eo,      &E->cand_em,
       &E->cand_xeo,      &E->cand_xem,
-      &E->probe,         &E->col_prev,     &E->kq_prev,        &E->vmeta,        &E->trans_off,      &E->trans,          &E->bp,         &E->state,      &E->chosen,
+      &E->probe,         &E->col_prev,     &E->kq_prev,        &E->vmeta,  &E->colrec, &E->colrec_pos,        &E->trans_off,      &E->trans,          &E->bp,         &E->state,      &E->chosen,
       &E->chain_start,   &E->route_dist,   &E->ipos,   &E->path_off,       &E->path_len,       &E->path_pool,  &E->trace_err,
       &E->overflow_list0, &E->overflow_list2, &E->counters_i32, &E->scan_tmp, &E->snap,   &E->big_key,
       &E->big_lab,       &E->big_inq,      &E->big_fr,         &E->big_ins,        &E->big_prev,
@@ -652,6 +652,8 @@ static int engine_match_once(otm_engine* E, const DevBatch& b, hipStream_t s, st
   ENS(col_prev, Pn * 4);
   ENS(kq_prev, Pn * 4);
   ENS(vmeta, Pn);
+  ENS(colrec, Pn * 16);
+  ENS(colrec_pos, Pn * 4);
   ENS(trans_off, Pn * 8);
   ENS(bp, Pn * KMAX);
   ENS(state, Pn * 4);
@@ -711,6 +713,13 @@ static int engine_match_once(otm_engine* E, const DevBatch& b, hipStream_t s, st
   w.col_prev = P<int32_t>(E->col_prev);
   w.kq_prev = P<int32_t>(E->kq_prev);
   w.vmeta = P<uint8_t>(E->vmeta);
+  {
+    // ordered column records for K4 (OTM_TRANS_COLREC=0: the per-point arrays)
+    static const char* ce = std::getenv("OTM_TRANS_COLREC");
+    const bool on = !ce || std::atoi(ce) != 0;
+    w.colrec = on ? P<int4>(E->colrec) : nullptr;
+    w.colrec_pos = on ? P<int32_t>(E->colrec_pos) : nullptr;
+  }
   w.trans_off = P<int64_t>(E->trans_off);
   w.bp = P<uint8_t>(E->bp);
   w.state = P<int32_t>(E->state);

@@ -95,7 +95,7 @@ struct otm_engine {
   // batch inputs (host batches are staged here)
   Buf in_off, in_lat, in_lon, in_time, in_acc, in_blob;
   // work
-  Buf pt_trace, is_col, prevc, nextc, gc, ncand, cand_eo, cand_em, cand_xeo, cand_xem, probe, col_prev, kq_prev, vmeta, trans_off, trans, bp, state, chosen,
+  Buf pt_trace, is_col, prevc, nextc, gc, ncand, cand_eo, cand_em, cand_xeo, cand_xem, probe, col_prev, kq_prev, vmeta, colrec, colrec_pos, trans_off, trans, bp, state, chosen,
       chain_start, route_dist, ipos, path_off, path_len, path_pool, trace_err, overflow_list0, overflow_list2,
       counters_i32, scan_tmp, snap;
   Buf big_key, big_lab, big_inq, big_fr, big_ins, big_prev;

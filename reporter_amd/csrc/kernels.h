@@ -217,6 +217,11 @@ struct DevWork {
   int32_t* abort;          // [1] set when a capacity (transition matrices, path pool) was exceeded:
                            // every later kernel returns at once and the host redoes the batch
   int64_t trans_cap;       // floats allocated for w.trans
+  // K4's column records in spatial-order position, written by K3 at the
+  // position the order scatter noted per column (colrec_pos): {p, col_prev,
+  // kq_prev | ncand << 8, gc bits}; null: k_trans_sub reads the per-point arrays
+  int4* colrec;
+  int32_t* colrec_pos;
   DevIndex idx;
   DevIndex idxn[NEAR_LEVELS];  // near indexes, smallest radius first (rmax 0: none): a column
                                // probes the first whose cmax covers its cost bound

@@ -374,6 +374,7 @@ __global__ __launch_bounds__(256) void k_order_scatter(DevBatch b, DevWork w, co
     const int t = col ? (int)tile[p] : 0;
     const int pos = wave_agg_slot(cursor, t, col);
     if (col) item[pos] = (int32_t)p;
+    if (col && w.colrec_pos) w.colrec_pos[p] = pos;  // where K3 writes the column's K4 record
   }
 }
 
@@ -1070,6 +1071,11 @@ __global__ __launch_bounds__(256) void k_links(DevBatch b, DevParams P, DevWork 
   w.col_prev[p] = cp;
   w.kq_prev[p] = kq;
   w.trans_off[p] = cnt;
+  // K4's record of the column in spatial-order position (k_trans_sub then
+  // reads it with one coalesced load instead of an order lookup and five
+  // scattered ones)
+  if (w.colrec && (P.order_mask & ORDER_TRANS) && w.is_col[p])
+    w.colrec[w.colrec_pos[p]] = make_int4((int32_t)p, cp, kq | (w.ncand[p] << 8), __float_as_int(w.gc[p]));
   // Viterbi's byte (k_viterbi_g): ncand <= KMAX = 32 fits six bits
   w.vmeta[p] = (uint8_t)((w.is_col[p] ? (w.ncand[p] | 0x40) : 0) | (cp >= 0 ? 0x80 : 0));
 }
@@ -1654,14 +1660,22 @@ __global__ __launch_bounds__(TB, OTM_TRANS_WAVES) void k_trans_sub(DevGraph g, D
     const int64_t it = base + sg;
     bool act = it < end;
     int64_t p = 0;
-    if (act) p = LIST ? (int64_t)w.overflow_list2[it] : (ordered ? (int64_t)w.ord.item[it] : it);
     // the column's words in one round trip (K3 wrote the previous column's
-    // candidate count beside the link)
+    // candidate count beside the link): its ordered record, or the arrays
     int32_t q = -1;
     int Kp = 0, Kq = 0;
     float gcv = 0.0f;
     int64_t toff = 0;
-    if (act) {
+    if (act && ordered && w.colrec) {
+      const int4 A = w.colrec[it];
+      p = A.x;
+      toff = w.trans_off[p];  // (the scan's, after K3)
+      q = A.y;
+      Kq = A.z & 255;
+      Kp = A.z >> 8;
+      gcv = __int_as_float(A.w);
+    } else if (act) {
+      p = LIST ? (int64_t)w.overflow_list2[it] : (ordered ? (int64_t)w.ord.item[it] : it);
       q = w.col_prev[p];
       Kq = w.kq_prev[p];
       Kp = w.ncand[p];

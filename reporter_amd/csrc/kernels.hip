@@ -589,6 +589,7 @@ __device__ __forceinline__ void wave_cadd(unsigned long long* c, unsigned long l
 // selection-sorts the first max_candidates by (sqdist, edge).  Probes with
 // more distinct edges in range spill to the wave kernel, which also applies
 // the MAX_HITS spec limit.
+template <bool CTR>
 __global__ __launch_bounds__(CAND_TB, OTM_CAND_WAVES) void k_cand_lane(DevGraph g, DevBatch b, DevParams P, DevWork w) {
   __shared__ uint32_t sE[CAND_LANE_CAP * CAND_TB];  // edge << 4 | shape segment
   __shared__ float sQ[CAND_LANE_CAP * CAND_TB];     // best squared distance
@@ -635,7 +636,7 @@ __global__ __launch_bounds__(CAND_TB, OTM_CAND_WAVES) void k_cand_lane(DevGraph 
       {
         const size_t rbase = (size_t)rr * (size_t)g.grid_cols;
         const int64_t q0 = g.cell_off[rbase + c0], q1 = g.cell_off[rbase + c1 + 1];
-        ents += (unsigned long long)(q1 - q0);
+        if (CTR) ents += (unsigned long long)(q1 - q0);
         // CAND_INFL entries' loads in flight per step, inserted in entry order: 2 keeps
         // the 64-VGPR cap without scratch (0.251 -> 0.246 ms config 2, 3.72 -> 3.66 ms config 4 against 4)
         for (int64_t q = q0; q < q1 && !spill; q += CAND_INFL) {
@@ -775,11 +776,13 @@ __global__ __launch_bounds__(CAND_TB, OTM_CAND_WAVES) void k_cand_lane(DevGraph 
     }
 
     w.ncand[p] = K;
-    c_cells += cells;
-    c_ent += ents;
-    c_cand += (unsigned long long)K;
+    if (CTR) {
+      c_cells += cells;
+      c_ent += ents;
+      c_cand += (unsigned long long)K;
+    }
   }
-  if (w.ctr) {
+  if (CTR) {
     wave_cadd(&w.ctr->cells_visited, c_cells);
     wave_cadd(&w.ctr->cell_entries_scanned, c_ent);
     wave_cadd(&w.ctr->candidates, c_cand);
@@ -4104,8 +4107,14 @@ void launch_order(const DevBatch& b, DevWork& w, hipStream_t s, const Marks& mk)
 
 void launch_candidates(const DevGraph& g, const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s,
                        const Marks& mk) {
-  TIMED(KN_CAND_LANE, hipLaunchKernelGGL(k_cand_lane, dim3(order_grid(b.n_points, CAND_TB, 1 << 30)),
-                                         dim3(CAND_TB), 0, s, g, b, p, w));
+  // (the work counters in their own instance: their registers cost the
+  // uncounted one entries in flight)
+  if (w.ctr)
+    TIMED(KN_CAND_LANE, hipLaunchKernelGGL(k_cand_lane<true>, dim3(order_grid(b.n_points, CAND_TB, 1 << 30)),
+                                           dim3(CAND_TB), 0, s, g, b, p, w));
+  else
+    TIMED(KN_CAND_LANE, hipLaunchKernelGGL(k_cand_lane<false>, dim3(order_grid(b.n_points, CAND_TB, 1 << 30)),
+                                           dim3(CAND_TB), 0, s, g, b, p, w));
   mk.begin(KN_CAND_WAVE, s);
   hipLaunchKernelGGL(k_candidates<false>, dim3(4096), dim3(TB), 0, s, g, b, p, w);
   hipLaunchKernelGGL(k_candidates<true>, dim3(CAND_BIG_SLOTS), dim3(TB), 0, s, g, b, p, w);

@@ -42,7 +42,9 @@ def short(name):
              # the transition index tier's launch slot (otm_kernel_name) runs one of these forms
              "k_trans_sub<4, false>": "k_trans_sub", "k_trans_sub<8, false>": "k_trans_sub", "k_trans_sub<16, false>": "k_trans_sub",
              "k_trans_sub<32, false>": "k_trans_sub", "k_trans_sub<64, false>": "k_trans_sub",
-             "k_trans_sub<16, true>": "k_trans_wide"}
+             "k_trans_sub<16, true>": "k_trans_wide",
+             # the candidate lane tier: uncounted / counted instances
+             "k_cand_lane<false>": "k_cand_lane", "k_cand_lane<true>": "k_cand_lane"}
     return alias.get(n, n)
 
 

@@ -1937,24 +1937,41 @@ __global__ __launch_bounds__(256, OTM_ROUTE_WAVES) void k_route_index(DevGraph g
   const DevIndex& X = w.idx;
   unsigned long long c_search = 0, c_settled = 0, c_relaxed = 0, c_edges = 0;
   const ItemRange R = item_range(w, b, (P.order_mask & ORDER_ROUTE) != 0, 256);
+  // K4's column records (K3, spatial-order position) give p, its link and gc
+  // in one coalesced load, so the link's chosen candidate loads with p's
+  const bool rec = R.ordered && w.colrec && (P.order_mask & ORDER_TRANS);
   for (int64_t it = R.i0; it < R.i1; it += R.stride) {
-    const int64_t p = R.ordered ? (int64_t)w.ord.item[it] : it;
+    int64_t p;
+    int32_t q = -1;
+    float gcv = 0.0f;
+    if (rec) {
+      const int4 A = w.colrec[it];
+      p = A.x;
+      q = A.y;
+      gcv = __int_as_float(A.w);
+    } else {
+      p = R.ordered ? (int64_t)w.ord.item[it] : it;
+    }
     if (!R.ordered && !w.is_col[p]) continue;
     // (non-column points keep the zeros K1 wrote; a re-run after a path-pool
     // overflow rewrites every column)
     w.route_dist[p] = 0.0f;
     w.path_len[p] = 0;
     w.path_off[p] = 0;
+    const int2 cq0 = w.chosen[q >= 0 ? q : p];  // (used only for a matched link)
     if (w.state[p] < 0 || w.chain_start[p]) continue;
-    const int32_t q = w.col_prev[p];
-    const int2 ci = w.chosen[q], cj = w.chosen[p];
+    if (!rec) {
+      q = w.col_prev[p];
+      gcv = w.gc[p];
+    }
+    const int2 ci = rec ? cq0 : w.chosen[q], cj = w.chosen[p];
     const int32_t ei = ci.x, ej = cj.x;
     const float oi = __int_as_float(ci.y), oj = __int_as_float(cj.y);
     if (same_edge_step(ei, oi, ej, oj)) {
       w.route_dist[p] = same_edge_dist(oi, oj);
       continue;
     }
-    const float bound = P.factor * w.gc[p];
+    const float bound = P.factor * gcv;
     const uint32_t cq = index_cost_bound(bound);
     IdxRow Rw{};
     int64_t sv = -1;

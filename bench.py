@@ -91,7 +91,8 @@ def parse():
     ap.add_argument("--host-pageable", action="store_true",
                     help="host-inclusive leg from pageable numpy arrays instead of otm_host_alloc buffers")
     ap.add_argument("--host-steps", type=int, default=-1,
-                    help="steps of the host-inclusive leg (otm_match_soa from host arrays; -1: --steps, 0: skip)")
+                    help="steps of the host-inclusive legs (otm_match_compact, then otm_match_soa, from host arrays; "
+                         "-1: --steps, 0: skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-check", action="store_true", help="skip the untimed oracle pass (agreement, bytes)")
     ap.add_argument("--traffic-json", default=None,
@@ -346,63 +347,87 @@ def main():
     # H2D of the inputs, every kernel, the compaction and the D2H copies --
     # with the same batches in flight; not `value`
     host_leg = None
-    host_steps = args.steps if args.host_steps < 0 else args.host_steps
+    host_steps = args.host_steps if args.host_steps >= 0 else args.steps
     if host_steps > 0:
         import ctypes as C
-        # the host's SoA buffers in page-locked memory (otm_host_alloc), as a
-        # Java FFM host would allocate them, filled outside the timed region
+        from reporter_amd.engine import compact_batch
         L = _lib.lib()
-        pinned, hptr = [], {}
-        for k in ("trace_off", "lat", "lon", "time", "accuracy"):
-            a = np.ascontiguousarray(batch[k])
-            if args.host_pageable:
-                hptr[k] = a.ctypes.data
-                continue
-            p_ = L.otm_host_alloc(a.nbytes)
-            if not p_:
-                raise RuntimeError("otm_host_alloc failed")
-            C.memmove(p_, a.ctypes.data, a.nbytes)
-            pinned.append(p_)
-            hptr[k] = p_
-        hb = _lib.Batch(len(batch["trace_off"]) - 1, P, hptr["trace_off"], hptr["lat"], hptr["lon"], hptr["time"],
-                        hptr["accuracy"])
+        pinned = []
+
+        def host_buffers(arrays):
+            # the host's buffers in page-locked memory (otm_host_alloc), as a
+            # Java FFM host would allocate them, filled outside the timed region
+            out = {}
+            for k, a in arrays.items():
+                a = np.ascontiguousarray(a)
+                if args.host_pageable:
+                    out[k] = a.ctypes.data
+                    continue
+                p_ = L.otm_host_alloc(max(a.nbytes, 1))
+                if not p_:
+                    raise RuntimeError("otm_host_alloc failed")
+                C.memmove(p_, a.ctypes.data, a.nbytes)
+                pinned.append(p_)
+                out[k] = p_
+            return out
+
+        nt_ = len(batch["trace_off"]) - 1
+        hp = host_buffers({k: batch[k] for k in ("trace_off", "lat", "lon", "time", "accuracy")})
+        hb = _lib.Batch(nt_, P, hp["trace_off"], hp["lat"], hp["lon"], hp["time"], hp["accuracy"])
+        cb = compact_batch(batch)
+        hc = host_buffers(cb)
+        hcb = _lib.BatchCompact(nt_, P, hc["trace_off"], hc["time_base"], hc["lat"], hc["lon"], hc["time_delta"],
+                                hc["accuracy"])
         outs = [_lib.Results() for _ in engines]
 
-        def host_step(i):
-            rc = _lib.lib().otm_match_soa(engines[i].h, C.byref(hb), C.byref(outs[i]))
-            if rc != 0:
+        def run_leg(call):
+            for i in range(inflight):
+                call(i)
+            hticket = itertools.count()
+            hgate = threading.Barrier(inflight + 1)
+
+            def hworker(i):
+                hgate.wait()
+                if args.host_stagger_ms > 0:
+                    time.sleep(i * args.host_stagger_ms / 1e3)
+                while next(hticket) < host_steps:
+                    call(i)
+
+            hthreads = [threading.Thread(target=hworker, args=(i,)) for i in range(inflight)]
+            for t in hthreads:
+                t.start()
+            torch.cuda.synchronize(dev)
+            th0 = time.perf_counter()
+            hgate.wait()
+            for t in hthreads:
+                t.join()
+            torch.cuda.synchronize(dev)
+            return time.perf_counter() - th0
+
+        def soa_step(i):
+            if _lib.lib().otm_match_soa(engines[i].h, C.byref(hb), C.byref(outs[i])) != 0:
                 raise RuntimeError("otm_match_soa: %s" % _lib.last_error())
 
-        for i in range(inflight):
-            host_step(i)
-        hticket = itertools.count()
-        hgate = threading.Barrier(inflight + 1)
+        def compact_step(i):
+            if _lib.lib().otm_match_compact(engines[i].h, C.byref(hcb), C.byref(outs[i])) != 0:
+                raise RuntimeError("otm_match_compact: %s" % _lib.last_error())
 
-        def hworker(i):
-            hgate.wait()
-            if args.host_stagger_ms > 0:
-                time.sleep(i * args.host_stagger_ms / 1e3)
-            while next(hticket) < host_steps:
-                host_step(i)
-
-        hthreads = [threading.Thread(target=hworker, args=(i,)) for i in range(inflight)]
-        for t in hthreads:
-            t.start()
-        torch.cuda.synchronize(dev)
-        th0 = time.perf_counter()
-        hgate.wait()
-        for t in hthreads:
-            t.join()
-        torch.cuda.synchronize(dev)
-        hel = time.perf_counter() - th0
+        hel_c = run_leg(compact_step)
+        hel_s = run_leg(soa_step)
         for p_ in pinned:
             L.otm_host_free(p_)
-        host_leg = {"value": P * host_steps / hel, "unit": "points/s", "ms_per_step": hel * 1e3 / host_steps,
+        in_c = sum(np.asarray(v).nbytes for v in cb.values()) / P
+        host_leg = {"value": P * host_steps / hel_c, "unit": "points/s", "ms_per_step": hel_c * 1e3 / host_steps,
                     "steps": host_steps, "batches_in_flight": inflight,
                     "host_buffers": "pageable" if args.host_pageable else "page-locked (otm_host_alloc)",
-                    "includes": "otm_match_soa from the host arrays: H2D of the inputs "
-                                "(24 B/point), all kernels, result compaction, D2H of traces / segments / reports "
-                                "/ way ids into pinned host buffers; JSON not included"}
+                    "input_bytes_per_point": round(in_c, 2),
+                    "includes": "otm_match_compact from the host arrays in the Java host's own types (float lat/lon, "
+                                "int32 time delta from a per-trace int64 base, int16 accuracy): H2D of the inputs, "
+                                "their widening on the device, all kernels, result compaction, D2H of traces / "
+                                "segments / reports / way ids into pinned host buffers; JSON not included",
+                    "soa": {"value": P * host_steps / hel_s, "ms_per_step": hel_s * 1e3 / host_steps,
+                            "input_bytes_per_point": 24.0 + 8.0 * (nt_ + 1) / P,
+                            "includes": "the same through otm_match_soa (double time, float accuracy)"}}
         hist.zero_()
         speed_sum.zero_()
 
@@ -421,14 +446,24 @@ def main():
         outs = (C.c_void_p * nb)()
         olens = (C.c_size_t * nb)()
         codes = (C.c_int * nb)()
+        # the drop-in's request arena (otm_request_arena_alloc): the Java host
+        # writes body.getBytes(ISO_8859_1) into it in place of a heap array,
+        # so the bodies go to HBM straight from there; filled once here (the
+        # fill time is reported beside, it is the host's own encoding)
+        from reporter_amd import RequestArena
+        tf = time.perf_counter()
+        arena = RequestArena(bodies)
+        arena_fill_ms = (time.perf_counter() - tf) * 1e3
+        srcs = {"arena": (arena.ptrs, arena.lens), "copied": (arr, lens)}
 
         gpu_resp = []  # the first responses of the last call (the CPU baseline checks its own against them)
 
-        def json_call():
+        def json_call(src="arena"):
             # the call alone is timed; releasing the 10k bodies (otm_free
             # through ctypes, ~5 ms of Python) happens after
+            ra, rl = srcs[src]
             t = time.perf_counter()
-            if L.otm_report_batch(eng.h, nb, arr, lens, outs, olens, codes) != 0:
+            if L.otm_report_batch(eng.h, nb, ra, rl, outs, olens, codes) != 0:
                 raise RuntimeError("otm_report_batch: %s" % _lib.last_error())
             t = time.perf_counter() - t
             nbytes = 0
@@ -440,12 +475,21 @@ def main():
                 L.otm_free(outs[i])
             return t, nbytes
 
+        json_call("copied")
+        jel_c = 0.0
+        copied_resp = None
+        for _ in range(args.json_calls):
+            t, resp_bytes = json_call("copied")
+            jel_c += t
+        jel_c /= args.json_calls
+        copied_resp = list(gpu_resp)
         json_call()
         jel = 0.0
         for _ in range(args.json_calls):
             t, resp_bytes = json_call()
             jel += t
         jel /= args.json_calls
+        arena_equal = copied_resp == gpu_resp
         # single-request latency: otm_report, one request at a time (the
         # reference's synchronous HttpClient.POST per record, Batch.java:63)
         lat_ms = []
@@ -471,13 +515,14 @@ def main():
             rbuf = (_lib.Result * cap)()
             tag_arrs = [(C.c_uint64 * nb)(*range(r * nb, (r + 1) * nb)) for r in range(args.async_rounds)]
 
-            def async_run():
+            def async_run(src="arena"):
+                ra, rl = srcs[src]
                 total = nb * args.async_rounds
                 parts = []
                 got = 0
                 ta = time.perf_counter()
                 for r in range(args.async_rounds):
-                    if L.otm_submit_batch(eng.h, nb, arr, lens, tag_arrs[r]) != 0:
+                    if L.otm_submit_batch(eng.h, nb, ra, rl, tag_arrs[r]) != 0:
                         raise RuntimeError("otm_submit_batch: %s" % _lib.last_error())
                     n = L.otm_poll(eng.h, rbuf, cap, 0)
                     if n > 0:
@@ -493,42 +538,58 @@ def main():
                 ta = time.perf_counter() - ta
                 return ta, np.concatenate(parts)
 
-            # warm: the pipeline's clones and their buffers -- twice, since a
-            # worker that took no batch in the first run would size its
-            # context inside the first timed one; the warm bodies released
-            # like the timed ones (their arenas back to the cache)
-            for _ in range(2):
-                for pb in async_run()[1]["body"]:
-                    L.otm_free(C.c_void_p(int(pb)))
-            # three timed runs (the host side of a run varies with the box's
-            # CPU quota and allocator state): the mean is `value`
-            runs = []
-            for _ in range(3):
-                ta, rr = async_run()
-                runs.append(ta)
-                in_order = bool((np.diff(rr["tag"].astype(np.int64)) == 1).all())
-                same = all(rr["code"][i] == gpu_resp[i][0] and C.string_at(int(rr["body"][i]), int(rr["len"][i])) ==
-                           gpu_resp[i][1] for i in range(len(gpu_resp)))
-                for pb in rr["body"]:
-                    L.otm_free(C.c_void_p(int(pb)))
-                if not (in_order and same):
-                    break
-            ta = sum(runs) / len(runs)
-            json_async = {"value": P * args.async_rounds / ta, "unit": "points/s", "requests": int(len(rr)),
-                          "seconds": ta, "seconds_per_run": runs,
-                          "best": P * args.async_rounds / min(runs), "results_in_submit_order": in_order,
-                          "first_responses_byte_equal_to_json_report": bool(same),
-                          "includes": "otm_submit_batch of the 10k Java request bodies x %d in a row (copies into the "
-                                      "queue), otm_poll until every response is back: the async pipeline, %s "
-                                      "workers on their own batch contexts; mean of 3 runs after 2 warm ones" %
-                                      (args.async_rounds, os.environ.get("OTM_ASYNC_WORKERS", "3"))}
+            def async_leg(src):
+                # warm: the pipeline's clones and their buffers -- twice, since a
+                # worker that took no batch in the first run would size its
+                # context inside the first timed one; the warm bodies released
+                # like the timed ones (their arenas back to the cache)
+                for _ in range(2):
+                    for pb in async_run(src)[1]["body"]:
+                        L.otm_free(C.c_void_p(int(pb)))
+                # three timed runs (the host side of a run varies with the box's
+                # CPU quota and allocator state): the mean is `value`
+                runs = []
+                for _ in range(3):
+                    ta, rr = async_run(src)
+                    runs.append(ta)
+                    in_order = bool((np.diff(rr["tag"].astype(np.int64)) == 1).all())
+                    same = all(rr["code"][i] == gpu_resp[i][0] and
+                               C.string_at(int(rr["body"][i]), int(rr["len"][i])) == gpu_resp[i][1]
+                               for i in range(len(gpu_resp)))
+                    for pb in rr["body"]:
+                        L.otm_free(C.c_void_p(int(pb)))
+                    if not (in_order and same):
+                        break
+                ta = sum(runs) / len(runs)
+                return {"value": P * args.async_rounds / ta, "unit": "points/s", "requests": int(len(rr)),
+                        "seconds": ta, "seconds_per_run": runs,
+                        "best": P * args.async_rounds / min(runs), "results_in_submit_order": in_order,
+                        "first_responses_byte_equal_to_json_report": bool(same)}
+
+            json_async = async_leg("arena")
+            json_async["includes"] = (
+                "otm_submit_batch of the 10k Java request bodies x %d in a row from the request arena (referenced, "
+                "not copied), otm_poll until every response is back: the async pipeline, %s workers on their own "
+                "batch contexts; mean of 3 runs after 2 warm ones" %
+                (args.async_rounds, os.environ.get("OTM_ASYNC_WORKERS", "3")))
+            json_async["copied"] = async_leg("copied")
+            json_async["copied"]["includes"] = "the same bodies from Python bytes objects (copied into the queue)"
+        arena.release()
         json_leg = {"value": P / jel, "unit": "points/s", "ms_per_call": jel * 1e3, "calls": args.json_calls,
                     "async": json_async,
+                    "request_arena": {"fill_ms": arena_fill_ms, "bytes": arena.bytes,
+                                      "responses_byte_equal_to_copied": bool(arena_equal),
+                                      "note": "the bodies written once into the arena before the calls (the Java "
+                                              "host's getBytes writes there instead of a heap array)"},
+                    "copied": {"value": P / jel_c, "ms_per_call": jel_c * 1e3,
+                               "includes": "otm_report_batch over the same bodies from Python bytes objects "
+                                           "(staged through the library's host threads)"},
                     "single_request_latency": single,
                     "requests_per_call": nb, "request_bytes": int(sum(len(x) for x in bodies)),
                     "response_bytes": int(resp_bytes), "status_200": int(sum(1 for i in range(nb) if codes[i] == 200)),
-                    "includes": "otm_report_batch: request JSON parse (the Java bytes without a DOM), H2D, all "
-                                "kernels, compaction, D2H, response JSON writing; one call at a time"}
+                    "includes": "otm_report_batch over the bodies in a request arena: H2D straight from the arena, "
+                                "request JSON read, all kernels, compaction, response JSON writing, D2H into the "
+                                "response arena; one call at a time"}
         hist.zero_()
         speed_sum.zero_()
 
@@ -554,11 +615,17 @@ def main():
         tr_args = dict(cfg["traces"])
         tr_args["points_per_vehicle"] = args.points
         tr_args.pop("n_vehicles", None)
-        poff, pedges = synth.true_paths(graph, len(ids), vehicle_ids=ids, **tr_args)
+        poff, pedges, penter = synth.true_paths_timed(graph, len(ids), vehicle_ids=ids, **tr_args)
         outlier = synth.outlier_points(graph, batch["true_edge"], orc["ncand"], orc["cand_edge"], orc["cand_off"],
                                        batch["trace_off"], orc["gc"])
         truth_gpu = synth.segment_agreement(graph, poff, pedges, res, trace_off=batch["trace_off"], outlier=outlier)
         bd = truth_gpu["breakdown"]
+        # what the datastore receives: report()'s reports for the driven route
+        # with its true times vs the matched batch's
+        rep_truth = synth.report_agreement(graph, poff, pedges, penter, batch["trace_off"], batch["time"], res)
+        rep_truth["what"] = ("per trace, report()'s datastore reports for the driven route at its true times vs "
+                             "the matched ones: pairs by LCS over (id, next_id); start/end vs interior errors; "
+                             "for the pairs |t0|, |t1| errors (s) and the reported speed's relative error")
         agreement = {"segment_id_sequences_equal_vs_oracle": seq_eq / float(max(nt, 1)), "traces": nt,
                      "all_outputs_bit_identical": bool(same),
                      "vs_ground_truth": {"segment_id_agreement": truth_gpu["segment_id_agreement"],
@@ -570,6 +637,7 @@ def main():
                                          "driven_segments": bd["driven_segments"],
                                          "errors": {k: bd[k] for k in synth.ERROR_CLASSES},
                                          "outlier_columns": bd["outlier_points"],
+                                         "datastore_reports": rep_truth,
                                          "what": "per trace, the OSMLR segment-id sequence the synthetic vehicle "
                                                  "drove vs the matched one: sum of LCS / sum of max length; "
                                                  "errors by class (synth.classify_sequences): start/end partial "

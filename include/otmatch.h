@@ -120,6 +120,20 @@ int otm_report_batch(otm_engine* eng, int n, const char* const* reqs,
                      const size_t* lens, char** resps, size_t* resp_lens,
                      int* codes);
 
+/* Request arenas: page-locked host memory owned by the library that a host
+ * writes its request bodies into -- the Java host's body.getBytes(ISO_8859_1)
+ * (HttpClient.java:26 sends those bytes) into a MemorySegment over the arena
+ * instead of a heap array (Batch.java:52-63).  otm_report_batch and
+ * otm_submit_batch recognise bodies inside an arena and send them to HBM
+ * straight from it, in pieces as large as the bodies lying back to back
+ * allow: no staging copy and no submission copy.  The caller may reuse an
+ * arena once otm_report_batch returns; bodies given to otm_submit_batch must
+ * stay unchanged until their results are polled (the submission holds the
+ * arena, so otm_request_arena_release only gives up the caller's hold).
+ * NULL on failure (otm_last_error). */
+void* otm_request_arena_alloc(size_t bytes);
+int otm_request_arena_release(void* arena);
+
 /* valhalla.SegmentMatcher().Match(json) (py/reporter_service.py:112):
  * request JSON (uuid + trace) in, {"segments":[...]} JSON out.  Returns 200
  * on success, 500 with {"error":...} otherwise. */
@@ -295,6 +309,26 @@ typedef struct otm_results {
  * pinned memory (otm_host_alloc) go to the device by DMA at full PCIe speed;
  * pageable inputs are staged by the HIP runtime. */
 int otm_match_soa(otm_engine* eng, const otm_batch* in, otm_results* out);
+/* The same batch in the Java host's own types, narrowed for the link (14 B
+ * per point instead of 24): Point's float lat/lon, its long time as an int32
+ * delta from a per-trace int64 base (epoch seconds), its int accuracy as an
+ * int16 (Point.java:16-25; Batch.java:52-61 sends exactly these integers).
+ * time[i] = (double)(time_base[t] + time_delta[i]), accuracy[i] =
+ * (float)accuracy16[i] -- widened on the device, results identical to
+ * otm_match_soa on the widened batch.  A trace whose times span more than
+ * 2^31 s or whose accuracies leave [-32768, 32767] goes through
+ * otm_match_soa instead. */
+typedef struct otm_batch_compact {
+  int32_t n_traces;
+  int64_t n_points;
+  const int64_t* trace_off;  /* n_traces + 1 */
+  const int64_t* time_base;  /* n_traces: epoch seconds */
+  const float* lat;
+  const float* lon;
+  const int32_t* time_delta; /* seconds after the trace's time_base */
+  const int16_t* accuracy;   /* metres; <= 0 means "not given" */
+} otm_batch_compact;
+int otm_match_compact(otm_engine* eng, const otm_batch_compact* in, otm_results* out);
 /* Page-locked host memory for a host's batch buffers (hipHostMalloc): a Java
  * host maps it as a MemorySegment and fills its SoA arrays in place.
  * NULL on failure; release with otm_host_free (not otm_free). */
@@ -604,6 +638,12 @@ int otm_tile_files_bbox(double minx, double miny, double maxx, double maxy, cons
  * edge count (cap 0 sizes the call) or a negative error. */
 int64_t otm_synth_true_paths(const char* graph_path, const otm_synth_trace_params* p,
                              int64_t* path_off, int32_t* path_edges, int64_t cap);
+/* The same with the time (epoch seconds) the vehicle entered each path edge
+ * (it drives each edge at constant speed; the first edge's entry precedes the
+ * first probe): the true segment times behind the datastore-report accuracy
+ * figure (reporter_amd/synth.py report_agreement). */
+int64_t otm_synth_true_paths_timed(const char* graph_path, const otm_synth_trace_params* p,
+                                   int64_t* path_off, int32_t* path_edges, double* enter_time, int64_t cap);
 
 /* Kafka's default key partitioner (murmur2, seed 0x9747b28c) -- the shard of
  * a uuid: (murmur2(key) & 0x7fffffff) % n. */

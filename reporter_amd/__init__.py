@@ -15,7 +15,8 @@ include/otmatch.h).  This package is its Python host face:
   datastore   a rank's histogram flush body and POST
   synth, tracegen  seeded synthetic graphs and traces, config-1 requests (harness tooling)
 """
-from .engine import Engine, OtmError, Results, encode_request, murmur2_partition, report_segments, write_config
+from .engine import (Engine, OtmError, RequestArena, Results, encode_request, murmur2_partition, report_segments,
+                     write_config)
 
-__all__ = ["Engine", "OtmError", "Results", "encode_request", "murmur2_partition", "report_segments",
+__all__ = ["Engine", "OtmError", "RequestArena", "Results", "encode_request", "murmur2_partition", "report_segments",
            "write_config"]

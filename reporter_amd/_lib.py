@@ -23,6 +23,14 @@ class Batch(C.Structure):
                 ("lon", C.c_void_p), ("time", C.c_void_p), ("accuracy", C.c_void_p)]
 
 
+class BatchCompact(C.Structure):
+    """otm_batch_compact: int64 time bases per trace, int32 time deltas and
+    int16 accuracies per point (include/otmatch.h)."""
+    _fields_ = [("n_traces", C.c_int32), ("n_points", C.c_int64), ("trace_off", C.c_void_p),
+                ("time_base", C.c_void_p), ("lat", C.c_void_p), ("lon", C.c_void_p), ("time_delta", C.c_void_p),
+                ("accuracy", C.c_void_p)]
+
+
 class Results(C.Structure):
     _fields_ = [("n_traces", C.c_int32), ("n_segments", C.c_int32), ("n_reports", C.c_int32),
                 ("n_way_ids", C.c_int32), ("traces", C.c_void_p), ("segments", C.c_void_p), ("reports", C.c_void_p),
@@ -140,6 +148,9 @@ def _declare(L):
         "otm_submit_batch": (C.c_int, [vp, C.c_int, vp, vp, vp]),
         "otm_encode_request": (C.c_int, [C.c_char_p, C.c_int, vp, vp, vp, vp, pp, psz]),
         "otm_match_soa": (C.c_int, [vp, C.POINTER(Batch), C.POINTER(Results)]),
+        "otm_match_compact": (C.c_int, [vp, C.POINTER(BatchCompact), C.POINTER(Results)]),
+        "otm_request_arena_alloc": (vp, [sz]),
+        "otm_request_arena_release": (C.c_int, [vp]),
         "otm_host_alloc": (vp, [sz]),
         "otm_host_free": (None, [vp]),
         "otm_match_device": (C.c_int, [vp, C.POINTER(Batch), vp]),
@@ -187,6 +198,7 @@ def _declare(L):
         "otm_synth_traces": (C.c_int, [C.c_char_p, C.POINTER(SynthTraceParams), vp, vp, vp, vp, vp, vp, vp]),
         "otm_murmur2": (i32, [C.c_char_p, sz]),
         "otm_synth_true_paths": (i64, [C.c_char_p, C.POINTER(SynthTraceParams), vp, vp, i64]),
+        "otm_synth_true_paths_timed": (i64, [C.c_char_p, C.POINTER(SynthTraceParams), vp, vp, vp, i64]),
         "otm_tile_id": (i64, [C.c_int, C.c_double, C.c_double]),
         "otm_tile_file": (C.c_int, [i64, C.c_int, C.c_char_p, C.c_char_p, sz]),
         "otm_tile_files_bbox": (C.c_int, [C.c_double, C.c_double, C.c_double, C.c_double, C.c_char_p, pp, psz]),

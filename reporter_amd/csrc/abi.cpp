@@ -286,15 +286,9 @@ bool json_profile() {
 }
 thread_local double t_gpu_ms = 0.0, t_pack_ms = 0.0, t_write_ms = 0.0, t_extract_ms = 0.0;
 
-// The reference's stderr line per invalid speed (reporter_service.py): to
-// stderr, or -- inside a chunk of a pipelined call -- to the chunk's buffer,
-// which the caller prints in chunk order once every chunk is done
-thread_local std::string* t_errbuf = nullptr;
+// The reference's stderr line per invalid speed (reporter_service.py)
 void speed_lines(int n) {
-  for (int q = 0; q < n; ++q) {
-    if (t_errbuf) t_errbuf->append("Speed exceeds 200kph\n");
-    else std::fputs("Speed exceeds 200kph\n", stderr);
-  }
+  for (int q = 0; q < n; ++q) std::fputs("Speed exceeds 200kph\n", stderr);
 }
 
 // A batch's turn in an H2DOrder (engine.h): the constructor waits until
@@ -496,6 +490,10 @@ constexpr int SLOTS = 64;
 constexpr size_t ARENA_CACHE = (size_t)256 << 20;
 enum : int { FREE = 0, LIVE = 1, CACHED = 2 };
 struct Slot {
+  // gen is a seqlock over (state, lo, hi): odd while acquire() or release()
+  // rewrites them, so free_body's lock-free scan can tell a consistent
+  // snapshot from one torn across a release and a re-acquire
+  std::atomic<uint64_t> gen{0};
   std::atomic<int> state{FREE};
   std::atomic<uintptr_t> lo{0}, hi{0};
   std::atomic<int64_t> refs{0};
@@ -504,6 +502,7 @@ struct Slot {
   bool pinned = false;  // page-locked (hipHostMalloc): a device copy's target
 };
 Slot g_slot[SLOTS];
+std::atomic<int64_t> g_releases{0};  // arenas released by their last body (otm_debug_arena_stress)
 std::mutex g_mu;
 size_t g_cached = 0;  // under g_mu
 
@@ -554,29 +553,29 @@ char* acquire(size_t bytes, int64_t nbodies, bool pinned = false) {
     g_cached -= g_slot[best].cap;
   }
   Slot& S = g_slot[best];
+  S.gen.fetch_add(1);  // odd: being rewritten
   S.refs.store(nbodies);
   S.lo.store((uintptr_t)S.base);
   S.hi.store((uintptr_t)S.base + S.cap);
   S.state.store(LIVE);
+  S.gen.fetch_add(1);
   return S.base;
 }
 
 void release(Slot& S) {
   std::lock_guard<std::mutex> lk(g_mu);
-  // out of every address range, then out of LIVE, before the memory can go
-  // back to the allocator: free_body's lock-free scan must never match a
-  // pointer the allocator hands out again inside the old range.  hi goes
-  // first: a scan reads lo then hi, so it sees [old lo, old hi) or an empty
-  // range, never [0, old hi)
+  g_releases.fetch_add(1);
+  // out of every address range, then out of LIVE, inside one odd generation,
+  // before the memory can go back to the allocator: free_body's scan must
+  // never match a pointer the allocator hands out again inside the old range
+  S.gen.fetch_add(1);
   S.hi.store(0);
   S.lo.store(0);
-  if (g_cached + S.cap <= ARENA_CACHE) {
-    g_cached += S.cap;
-    S.state.store(CACHED);
-  } else {
-    S.state.store(FREE);
-    drop(S);
-  }
+  const bool keep = g_cached + S.cap <= ARENA_CACHE;
+  if (keep) g_cached += S.cap;
+  S.state.store(keep ? CACHED : FREE);
+  S.gen.fetch_add(1);
+  if (!keep) drop(S);
 }
 
 // otm_free: a body inside a live arena, or a plain allocation
@@ -585,9 +584,22 @@ void free_body(void* p) {
   const uintptr_t a = (uintptr_t)p;
   for (int i = 0; i < SLOTS; ++i) {
     Slot& S = g_slot[i];
-    if (S.state.load(std::memory_order_acquire) == LIVE && a >= S.lo.load() && a < S.hi.load()) {
-      if (S.refs.fetch_sub(1) == 1) release(S);
-      return;
+    // a consistent (gen, state, lo, hi) snapshot: the generation even and
+    // unchanged across the reads.  A LIVE range holding p at that instant is
+    // p's arena (a live body keeps its arena's refs above 0, so it cannot be
+    // released under us); a torn snapshot is read again.
+    while (true) {
+      const uint64_t g0 = S.gen.load(std::memory_order_acquire);
+      if (g0 & 1u) continue;
+      const int st = S.state.load(std::memory_order_acquire);
+      const uintptr_t lo = S.lo.load(std::memory_order_acquire), hi = S.hi.load(std::memory_order_acquire);
+      std::atomic_thread_fence(std::memory_order_acquire);
+      if (S.gen.load(std::memory_order_relaxed) != g0) continue;
+      if (st == LIVE && a >= lo && a < hi) {
+        if (S.refs.fetch_sub(1) == 1) release(S);
+        return;
+      }
+      break;
     }
   }
   std::free(p);
@@ -626,11 +638,12 @@ void release(ReqSlab* s) {
   delete s;
 }
 
-// a slab of >= bytes, page-locked from pinned_min() up unless !may_pin
-// (throws std::bad_alloc when there is no memory at all)
-std::shared_ptr<ReqSlab> acquire(size_t bytes, bool may_pin = true) {
+// a slab of >= bytes, page-locked from pinned_min() up (always with
+// must_pin, else nullptr when none is to be had) unless !may_pin (throws
+// std::bad_alloc when there is no memory at all)
+std::shared_ptr<ReqSlab> acquire(size_t bytes, bool may_pin = true, bool must_pin = false) {
   ReqSlab* s = nullptr;
-  if (may_pin && bytes >= pinned_min()) {
+  if (must_pin || (may_pin && bytes >= pinned_min())) {
     {
       std::lock_guard<std::mutex> lk(g_mu);
       size_t best = g_cache.size();
@@ -648,6 +661,7 @@ std::shared_ptr<ReqSlab> acquire(size_t bytes, bool may_pin = true) {
       void* p = nullptr;
       if (hipHostMalloc(&p, cap, hipHostMallocDefault) == hipSuccess && p) s = new ReqSlab{(char*)p, cap, true};
     }
+    if (!s && must_pin) return nullptr;
   }
   if (!s) {
     char* p = (char*)std::malloc(bytes ? bytes : 1);
@@ -657,6 +671,66 @@ std::shared_ptr<ReqSlab> acquire(size_t bytes, bool may_pin = true) {
   return std::shared_ptr<ReqSlab>(s, release);
 }
 }  // namespace slabs
+
+// Request arenas (otm_request_arena_alloc): page-locked slabs the host writes
+// its request bodies into, registered by address range.  otm_report_batch
+// and otm_submit_batch find their bodies here and send them to HBM straight
+// from the arena (report_many_device's direct pieces): no staging copy, no
+// submission copy.  A submission holds its arena (the shared slab) until its
+// batch has run, so release only gives up the caller's hold.
+namespace reqarena {
+struct Entry {
+  uintptr_t lo, hi;
+  std::shared_ptr<ReqSlab> slab;
+};
+std::mutex g_mu;
+std::vector<Entry> g_live;  // under g_mu
+
+void* alloc(size_t bytes) {
+  std::shared_ptr<ReqSlab> s = slabs::acquire(bytes ? bytes : 1, true, true);
+  if (!s) return nullptr;
+  std::lock_guard<std::mutex> lk(g_mu);
+  g_live.push_back(Entry{(uintptr_t)s->base, (uintptr_t)s->base + s->cap, s});
+  return s->base;
+}
+
+bool release(void* p) {
+  std::shared_ptr<ReqSlab> drop;  // (released after the lock)
+  std::lock_guard<std::mutex> lk(g_mu);
+  for (size_t i = 0; i < g_live.size(); ++i)
+    if (g_live[i].lo == (uintptr_t)p) {
+      drop = std::move(g_live[i].slab);
+      g_live[i] = std::move(g_live.back());
+      g_live.pop_back();
+      return true;
+    }
+  return false;
+}
+
+// the arena holding each body [reqs[k], reqs[k] + lens[k]) (all of it), or
+// null; returns whether every body lies in one
+bool find(int n, const char* const* reqs, const size_t* lens, std::vector<std::shared_ptr<ReqSlab>>* out) {
+  out->assign((size_t)n, nullptr);
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (g_live.empty()) return false;
+  bool all = true;
+  size_t last = 0;
+  for (int k = 0; k < n; ++k) {
+    const uintptr_t a = (uintptr_t)reqs[k], e = a + lens[k];
+    bool hit = false;
+    for (size_t t = 0; t < g_live.size() && !hit; ++t) {
+      const size_t i = (last + t) % g_live.size();  // (bodies of one call mostly share an arena)
+      if (a >= g_live[i].lo && e <= g_live[i].hi) {
+        (*out)[(size_t)k] = g_live[i].slab;
+        last = i;
+        hit = true;
+      }
+    }
+    all = all && hit;
+  }
+  return all;
+}
+}  // namespace reqarena
 
 // each response of a batch into its place in one arena (or its own malloc'd
 // buffer when no arena is to be had): src(k) -> (pointer, length); returns
@@ -814,8 +888,12 @@ void report_many_device(otm_engine* E, int n, const char* const* reqs, const siz
           // a run of bodies adjacent in one page-locked submission slab:
           // copied to HBM from there, not staged (two slabs that happen to be
           // adjacent in memory are two allocations: two copies)
+          // (cut at PIECE bytes too, so the reads of one piece overlap the
+          // next piece's DMA)
           k1 = k0 + 1;
-          while (k1 < n && pinned[k1] == pinned[k0] && reqs[k1] == reqs[k1 - 1] + lens[k1 - 1]) ++k1;
+          while (k1 < n && pinned[k1] == pinned[k0] && reqs[k1] == reqs[k1 - 1] + lens[k1 - 1] &&
+                 (size_t)off[k1 + 1] - from <= PIECE)
+            ++k1;
         } else {
           while (k1 > k0 + 1 && pinned && pinned[k1 - 1] != nullptr) --k1;  // (the staged piece stops at a slab run)
           par_for((size_t)(k1 - k0), [&](size_t a, size_t e) {
@@ -989,95 +1067,6 @@ void report_many(otm_engine* E, int n, const char* const* reqs, const size_t* le
   }
 }
 
-// A large otm_report_batch as a pipeline (OTM_PIPE_CHUNKS chunks of about
-// equal bytes, default 1 = one batch; batches under OTM_PIPE_MIN requests,
-// default 4096, stay whole): chunk k runs on its own batch context (this
-// engine, then its pipeline clones) on its own thread, the chunks' request
-// copies cross the link one after another in chunk order (H2DOrder), so chunk
-// k+1's bytes move while chunk k runs its kernels and chunk k's responses come
-// back while k+1 runs.  Each chunk is the same request/response contract as a
-// whole batch (every response depends only on its own request); the stderr
-// lines come out in chunk order.  Measured not faster on 10k requests (2 or 4
-// chunks 156-173M points/s against 162-169M whole, profiles/r04_ab/json_*),
-// so off by default.
-int pipe_chunks() {
-  const char* e = std::getenv("OTM_PIPE_CHUNKS");
-  return e ? std::max(1, std::min(8, std::atoi(e))) : 1;
-}
-int pipe_min() {
-  const char* e = std::getenv("OTM_PIPE_MIN");
-  return e ? std::max(2, std::atoi(e)) : 4096;
-}
-
-void report_many_pipelined(otm_engine* E, int n, const char* const* reqs, const size_t* lens, int* codes,
-                           char** resps, size_t* resp_lens) {
-  int C = pipe_chunks();
-  if (!gpu_reader(E, n) || !E->members.empty() || E->parent || n < pipe_min() || C < 2) {
-    report_many(E, n, reqs, lens, codes, resps, resp_lens);
-    return;
-  }
-  std::vector<otm_engine*> ctx{E};
-  {
-    std::lock_guard<std::mutex> lk(E->pmu);
-    while ((int)E->pctx.size() < C - 1) {
-      otm_engine* X = nullptr;
-      if (otm_engine_clone(E, &X) != OTM_OK) break;  // fewer chunks, same results
-      E->pctx.push_back(X);
-    }
-    for (int k = 0; k < C - 1 && k < (int)E->pctx.size(); ++k) ctx.push_back(E->pctx[(size_t)k]);
-  }
-  C = (int)ctx.size();
-  size_t total = 0;
-  for (int k = 0; k < n; ++k) total += lens[k];
-  std::vector<int> cut((size_t)C + 1, n);
-  cut[0] = 0;
-  size_t acc = 0;
-  for (int k = 0, c = 1; k < n && c < C; ++k) {
-    acc += lens[k];
-    if (acc * (size_t)C >= total * (size_t)c) cut[(size_t)c++] = k + 1;
-  }
-  for (int c = 1; c <= C; ++c) cut[(size_t)c] = std::max(cut[(size_t)c], cut[(size_t)c - 1]);
-  otm::H2DOrder ord;
-  std::vector<std::string> lines((size_t)C);
-  std::vector<std::exception_ptr> errs((size_t)C);
-  auto chunk = [&](int c) {
-    std::string* saved = t_errbuf;
-    t_errbuf = &lines[(size_t)c];
-    try {
-      const int a = cut[(size_t)c], m = cut[(size_t)c + 1] - a;
-      report_many(ctx[(size_t)c], m, reqs + a, lens + a, codes + a, resps + a, resp_lens + a, nullptr, &ord,
-                  (uint64_t)c);
-    } catch (...) {
-      errs[(size_t)c] = std::current_exception();
-    }
-    t_errbuf = saved;
-  };
-  for (int k = 0; k < n; ++k) resps[k] = nullptr;
-  std::vector<std::thread> th;
-  std::vector<int> here{0};  // chunks on the caller, in chunk order
-  for (int c = 1; c < C; ++c) {
-    try {
-      th.emplace_back(chunk, c);
-    } catch (...) {
-      here.push_back(c);  // no thread to be had: on the caller, after the earlier chunks
-    }
-  }
-  for (int c : here) chunk(c);
-  for (auto& t : th) t.join();
-  for (hipEvent_t ev : ord.ev)
-    if (ev) (void)hipEventDestroy(ev);
-  for (auto& x : errs)
-    if (x) {
-      for (int k = 0; k < n; ++k) {
-        arena::free_body(resps[k]);
-        resps[k] = nullptr;
-      }
-      std::rethrow_exception(x);  // to the entry point's guard
-    }
-  for (const std::string& s : lines)
-    if (!s.empty()) std::fputs(s.c_str(), stderr);
-}
-
 // Requests per async batch (OTM_ASYNC_BATCH): small enough that a burst of
 // submissions splits over the pipeline's workers, large enough to fill the GPU
 // (profiles/r03_s2/async_ab.txt: 3 workers x 16384 the steadiest, ~250M points/s
@@ -1192,6 +1181,22 @@ const char* otm_last_error(const otm_engine*) { return t_err.empty() ? otm::thre
 
 void otm_free(void* p) { arena::free_body(p); }
 
+void* otm_request_arena_alloc(size_t bytes) {
+  try {
+    void* p = reqarena::alloc(bytes);
+    if (!p) fail(OTM_ENOMEM, "no page-locked memory for a request arena");
+    return p;
+  } catch (...) {
+    fail(OTM_ENOMEM, "out of host memory");
+    return nullptr;
+  }
+}
+
+int otm_request_arena_release(void* arena) {
+  if (!arena) return OTM_OK;
+  return reqarena::release(arena) ? OTM_OK : fail(OTM_EINVAL, "not a request arena");
+}
+
 // the GPU response writer's number formatting, compiled for the host: the
 // checks of tests/test_pyrepr.py against Python's own repr / round
 int otm_debug_py_repr(double d, char* out) { return otm::pyrepr::py_repr(d, out); }
@@ -1204,7 +1209,10 @@ int otm_kmax(void) { return otm::KMAX; }
 // round every thread cuts bodies from an arena of its own, then all threads
 // free a strided share of every thread's bodies, interleaved with plain
 // malloc'd pointers (which must never match an arena).  Returns the number of
-// arenas left LIVE afterwards (0 when every last body released its arena).
+// arenas left LIVE afterwards plus the difference between the arenas cut and
+// the arenas released (0 when every arena was released once, by its own last
+// body: a body freed into the wrong arena releases one early, and the real
+// arena never).
 int otm_debug_arena_stress(int threads, int rounds) {
   if (threads < 1 || threads > 64 || rounds < 0) return -1;
   constexpr int NB = 16;
@@ -1225,11 +1233,14 @@ int otm_debug_arena_stress(int threads, int rounds) {
     }
   };
   std::vector<std::thread> th;
+  std::atomic<int64_t> cut{0};
+  const int64_t rel0 = arena::g_releases.load();
   for (int t = 0; t < threads; ++t)
     th.emplace_back([&, t] {
       for (int r = 0; r < rounds; ++r) {
         const size_t each = 64 + (size_t)((r * 7 + t * 13) % 200);
         char* base = arena::acquire(each * NB, NB);
+        if (base) cut.fetch_add(1);
         for (int k = 0; k < NB; ++k) bodies[(size_t)t][(size_t)k] = base ? base + each * (size_t)k : (char*)std::malloc(each);
         barrier();
         for (int q = 0; q < threads; ++q)
@@ -1243,7 +1254,7 @@ int otm_debug_arena_stress(int threads, int rounds) {
   for (auto& x : th) x.join();
   int live = 0;
   for (int i = 0; i < arena::SLOTS; ++i) live += arena::g_slot[i].state.load() == arena::LIVE ? 1 : 0;
-  return live;
+  return live + (int)std::llabs(cut.load() - (arena::g_releases.load() - rel0));
 }
 
 const char* otm_runtime_info(void) {
@@ -1457,7 +1468,6 @@ void otm_engine_destroy(otm_engine* E) {
     for (hipEvent_t ev : E->aorder.ev)
       if (ev) (void)hipEventDestroy(ev);
   }
-  for (otm_engine* C : E->pctx) otm_engine_destroy(C);
   if (!E->members.empty()) {
     otm::member_pool_free(E);
     for (otm_engine* m : E->members) otm_engine_destroy(m);
@@ -1487,7 +1497,16 @@ static int otm_report_impl(otm_engine* E, const char* req, size_t len, char** re
 static int otm_report_batch_impl(otm_engine* E, int n, const char* const* reqs, const size_t* lens, char** resps,
                      size_t* resp_lens, int* codes) {
   if (!E || n < 0) return fail(OTM_EINVAL, "bad arguments");
-  report_many_pipelined(E, n, reqs, lens, codes, resps, resp_lens);
+  // bodies in a request arena go to HBM straight from it
+  std::vector<std::shared_ptr<ReqSlab>> held;
+  reqarena::find(n, reqs, lens, &held);
+  std::vector<const void*> pin((size_t)n, nullptr);
+  bool any = false;
+  for (int k = 0; k < n; ++k) {
+    pin[(size_t)k] = held[(size_t)k].get();
+    any = any || pin[(size_t)k];
+  }
+  report_many(E, n, reqs, lens, codes, resps, resp_lens, any ? pin.data() : nullptr);
   return OTM_OK;
 }
 
@@ -1683,6 +1702,26 @@ static int otm_submit_batch_impl(otm_engine* E, int n, const char* const* reqs, 
   // submission costs more than the staging copy it saves)
   std::vector<size_t> off((size_t)n + 1, 0);
   for (int k = 0; k < n; ++k) off[(size_t)k + 1] = off[(size_t)k] + lens[k];
+  std::vector<std::shared_ptr<ReqSlab>> held;
+  if (n && reqarena::find(n, reqs, lens, &held)) {
+    // every body in a request arena: the submission holds the arenas (a
+    // shared count per body, taken on this thread), nothing is copied
+    std::vector<otm_engine::Pending> items((size_t)n);
+    for (size_t k = 0; k < (size_t)n; ++k)
+      items[k] = otm_engine::Pending{tags[k], reqs[k], lens[k], std::move(held[k]), (size_t)n - k, 0};
+    {
+      std::lock_guard<std::mutex> lk(E->qmu);
+      if (!E->worker_started) start_workers(E);
+      if (E->queue.size() + (size_t)n > (1u << 22)) return fail(OTM_EAGAIN, "submit queue full");
+      const uint64_t sub = E->n_subs++;
+      for (auto& it : items) {
+        it.sub = sub;
+        E->queue.push_back(std::move(it));
+      }
+    }
+    E->qcv.notify_all();
+    return OTM_OK;
+  }
   const char* mx = std::getenv("OTM_SLAB_MAX");  // (tests lower it)
   const bool one = off[(size_t)n] <= (mx ? (size_t)std::strtoull(mx, nullptr, 10) : slabs::SLAB_MAX);
   std::shared_ptr<ReqSlab> slab = one ? slabs::acquire(off[(size_t)n]) : nullptr;
@@ -1762,6 +1801,33 @@ static int otm_match_soa_impl(otm_engine* E, const otm_batch* in, otm_results* o
   std::lock_guard<std::mutex> lk(E->mu);
   std::string err;
   int rc = otm::match_host_fetch(E, in, nullptr, out, &err);
+  return rc ? fail(rc, err) : OTM_OK;
+}
+
+static int otm_match_compact_impl(otm_engine* E, const otm_batch_compact* in, otm_results* out) {
+  if (!E || !in || !out) return fail(OTM_EINVAL, "bad arguments");
+  std::lock_guard<std::mutex> lk(E->mu);
+  std::string err;
+  int rc;
+  if (E->members.empty()) {
+    (void)hipSetDevice(E->device);
+    rc = otm::engine_match_compact(E, in, &err);
+    if (!rc) rc = otm::engine_fetch(E, out, &err);
+  } else {
+    // a multi-device engine splits the batch on the host: widened there
+    const int32_t nt = in->n_traces;
+    if (nt < 0 || !in->trace_off || (nt > 0 && !in->time_base)) return fail(OTM_EINVAL, "invalid batch");
+    const int64_t np = in->trace_off[nt];
+    if (np < 0) return fail(OTM_EINVAL, "batch trace_off inconsistent with n_points");
+    std::vector<double> tm((size_t)np);
+    std::vector<float> acc((size_t)np);
+    for (int32_t t = 0; t < nt; ++t)
+      for (int64_t i = in->trace_off[t]; i < in->trace_off[t + 1] && i >= 0 && i < np; ++i)
+        tm[(size_t)i] = (double)(in->time_base[t] + (int64_t)in->time_delta[i]);
+    for (int64_t i = 0; i < np; ++i) acc[(size_t)i] = (float)in->accuracy[i];
+    const otm_batch b{nt, in->n_points, in->trace_off, in->lat, in->lon, tm.data(), acc.data()};
+    rc = otm::match_host_fetch(E, &b, nullptr, out, &err);
+  }
   return rc ? fail(rc, err) : OTM_OK;
 }
 
@@ -1982,6 +2048,16 @@ int otm_submit_batch(otm_engine* E, int n, const char* const* reqs, const size_t
 int otm_match_soa(otm_engine* E, const otm_batch* in, otm_results* out) {
   try {
     return otm_match_soa_impl(E, in, out);
+  } catch (const std::bad_alloc&) {
+    return fail(OTM_ENOMEM, "out of host memory");
+  } catch (const std::exception& e) {
+    return fail(OTM_EINVAL, std::string("internal error: ") + e.what());
+  }
+}
+
+int otm_match_compact(otm_engine* E, const otm_batch_compact* in, otm_results* out) {
+  try {
+    return otm_match_compact_impl(E, in, out);
   } catch (const std::bad_alloc&) {
     return fail(OTM_ENOMEM, "out of host memory");
   } catch (const std::exception& e) {

@@ -422,13 +422,13 @@ int build_index_at(otm_engine* E, float* r, bool shrink, size_t budget, IndexBui
   HIPCHK(hipMalloc(&tmp, tmpb));
   int64_t total = 0;
   for (int attempt = 0;; ++attempt) {
-    launch_index_build(E->g, E->dp.turn_units, index_cost_bound(*r), row_cnt, nullptr, nullptr, nullptr, false, s);
+    launch_index_build(E->g, E->dp.turn_units, index_cost_bound(*r), row_cnt, nullptr, nullptr, false, s);
     launch_row_sizes(row_cnt, row_off, N, s);
     scan_i64(row_off, N, tmp, tmpb, s);
     launch_row_pack(row_cnt, row_off, rows, N, s);
     HIPCHK(hipMemcpyAsync(&total, row_off + N, 8, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
-    const double need = ((double)total + 1.0) * 20.0;
+    const double need = ((double)total + 1.0) * IDX_SLOT_BYTES;
     if (need <= (double)budget) break;
     const float rr = (float)(std::floor(*r * std::sqrt((double)budget / need) * 0.9 / 50.0) * 50.0);
     if (!shrink || attempt == 4 || rr < 100.0f) {
@@ -445,13 +445,11 @@ int build_index_at(otm_engine* E, float* r, bool shrink, size_t budget, IndexBui
   E->graph_allocs.push_back(row_cnt);
   E->graph_allocs.push_back(row_off);
   E->graph_allocs.push_back(rows);
-  void *slot = nullptr, *pred = nullptr;
-  HIPCHK(hipMalloc(&slot, ((size_t)total + 1) * 16));
+  void* slot = nullptr;
+  HIPCHK(hipMalloc(&slot, ((size_t)total + 1) * IDX_SLOT_BYTES));
   E->graph_allocs.push_back(slot);
-  HIPCHK(hipMemsetAsync(slot, 0xFF, ((size_t)total + 1) * 16, s));
-  HIPCHK(hipMalloc(&pred, ((size_t)total + 1) * 4));
-  E->graph_allocs.push_back(pred);
-  launch_index_build(E->g, E->dp.turn_units, index_cost_bound(*r), row_cnt, rows, (uint4*)slot, (int32_t*)pred, true, s);
+  HIPCHK(hipMemsetAsync(slot, 0xFF, ((size_t)total + 1) * IDX_SLOT_BYTES, s));
+  launch_index_build(E->g, E->dp.turn_units, index_cost_bound(*r), row_cnt, rows, (uint4*)slot, true, s);
   HIPCHK(hipGetLastError());
   std::vector<int32_t> cnt((size_t)N);
   HIPCHK(hipMemcpyAsync(cnt.data(), row_cnt, (size_t)N * 4, hipMemcpyDeviceToHost, s));
@@ -465,7 +463,6 @@ int build_index_at(otm_engine* E, float* r, bool shrink, size_t budget, IndexBui
   out.X.cmax = index_cost_bound(*r);
   out.X.row = rows;
   out.X.slot = (const uint4*)slot;
-  out.X.pred = (const int32_t*)pred;
   return OTM_OK;
 }
 
@@ -483,14 +480,15 @@ int build_index(otm_engine* E, std::string* err) {
   for (auto& x : E->idxn) x = DevIndex{};
   E->idx.rmax = 0.0f;
   if (E->index_rmax < 0.0f) E->index_rmax = auto_index_radius(E);
+  E->index_rmax = std::min(E->index_rmax, INDEX_RMAX_CAP);  // (slot costs below 2^24)
   if (!(E->index_rmax > 0.0f)) return OTM_OK;
   hipStream_t s = E->stream;
   hipEvent_t a, z;
   HIPCHK(hipEventCreate(&a));
   HIPCHK(hipEventCreate(&z));
   HIPCHK(hipEventRecord(a, s));
-  // HBM budget for the slot tables (20 B per slot: 16 B slot + 4 B
-  // predecessor): half of what is free after the graph.  A graph whose rows at
+  // HBM budget for the slot tables (16 B per slot, the predecessor inside):
+  // half of what is free after the graph.  A graph whose rows at
   // this radius exceed it gets a smaller radius; below 100 m the index is left
   // off and the online tiers answer everything (same results, slower).
   IndexBuilt full;
@@ -507,7 +505,7 @@ int build_index(otm_engine* E, std::string* err) {
   std::vector<float> radii;
   if (E->index_near_set) {
     radii = E->index_near_m;
-  } else if ((double)full.slots * 20.0 >= OTM_INDEX_NEAR_MIN_GB * 1e9) {
+  } else if ((double)full.slots * IDX_SLOT_BYTES >= OTM_INDEX_NEAR_MIN_GB * 1e9) {
     for (float f : std::initializer_list<float> OTM_INDEX_NEAR_FRACS) radii.push_back(E->index_rmax * f);
   }
   for (float& r : radii) r = (float)(std::floor(r / 50.0) * 50.0);
@@ -886,20 +884,22 @@ int engine_match(otm_engine* E, const DevBatch& b, hipStream_t s, std::string* e
     if (ttotal > E->trans_cap) E->trans_cap = ttotal + ttotal / 4 + 4096;
     if (st.grow & 1) {
       // a search outgrew the huge tier's tables (or found none): 4x the slots
-      if (E->huge_log2 >= 30) {
-        *err = "a route search outgrew 2^30 table slots";
+      const int32_t next = E->huge_log2 ? E->huge_log2 + 2 : 19;
+      if (next > 29) {
+        *err = "a route search outgrew 2^29 table slots";
         return OTM_EDEVICE;
       }
-      E->huge_log2 = E->huge_log2 ? E->huge_log2 + 2 : 19;
+      E->huge_log2 = next;
     }
     if (st.grow & 2) {
       // a probe had more distinct edges in its radius than the candidate
       // HBM tier's tables hold (or there were none): 4x the slots
-      if (E->cand_log2 >= 26) {
-        *err = "a candidate search outgrew 2^26 table slots";
+      const int32_t next = E->cand_log2 ? E->cand_log2 + 2 : 13;
+      if (next > 25) {
+        *err = "a candidate search outgrew 2^25 table slots";
         return OTM_EDEVICE;
       }
-      E->cand_log2 = E->cand_log2 ? E->cand_log2 + 2 : 13;
+      E->cand_log2 = next;
     }
     if (cnt[2]) E->pool_cap = (int32_t)std::min<size_t>((size_t)cnt[1] * 2 + 1024, (size_t)INT32_MAX / 2);
   }
@@ -993,6 +993,75 @@ int engine_match_host(otm_engine* E, const otm_batch* in, std::string* err) {
   b.trace_off = (const int64_t*)E->in_off.p;
   b.lat = (const float*)E->in_lat.p;
   b.lon = (const float*)E->in_lon.p;
+  b.time = (const double*)E->in_time.p;
+  b.acc = (const float*)E->in_acc.p;
+  return engine_match(E, b, s, err);
+}
+
+// otm_match_compact: the host's compact batch (14 B per point: lat, lon,
+// an int32 time delta, an int16 accuracy; a per-trace int64 time base) to
+// HBM, then widened on the device (k_expand_compact) into the arrays every
+// stage reads.  Same results as engine_match_host on the widened batch;
+// 10 B per point less over PCIe.
+int engine_match_compact(otm_engine* E, const otm_batch_compact* in, std::string* err) {
+  const int32_t NT = in->n_traces;
+  if (NT < 0 || !in->trace_off || (NT > 0 && !in->time_base)) {
+    *err = "invalid batch";
+    return OTM_EINVAL;
+  }
+  const int64_t NP = in->trace_off[NT];
+  if (in->trace_off[0] != 0 || NP < 0 || (in->n_points && in->n_points != NP)) {
+    *err = "batch trace_off inconsistent with n_points";
+    return OTM_EINVAL;
+  }
+  for (int32_t t = 0; t < NT; ++t)
+    if (in->trace_off[t + 1] < in->trace_off[t]) {
+      *err = "batch trace_off not monotonic";
+      return OTM_EINVAL;
+    }
+  int rc;
+  const size_t b_off = ((size_t)NT + 1) * 8, b_base = (size_t)NT * 8, b_pt = (size_t)NP * 4,
+               b_acc = ((size_t)NP * 2 + 7) & ~(size_t)7;
+  // device: [offsets | time bases | lat | lon | time deltas | accuracies], then
+  // the widened time and accuracy arrays
+  const size_t total = b_off + b_base + 3 * b_pt + b_acc;
+  if ((rc = ensure(E->in_blob, total, err))) return rc;
+  if ((rc = ensure(E->in_time, (size_t)NP * 8 + 8, err))) return rc;
+  if ((rc = ensure(E->in_acc, (size_t)NP * 4 + 8, err))) return rc;
+  hipStream_t s = E->stream;
+  char* d = (char*)E->in_blob.p;
+  const size_t o_base = b_off, o_lat = o_base + b_base, o_lon = o_lat + b_pt, o_dt = o_lon + b_pt,
+               o_acc = o_dt + b_pt;
+  if (NP <= (int64_t)1 << 18) {
+    // small batches: one host copy into pinned staging, then ONE DMA
+    if ((rc = ensure_pinned(E->h_in, total, err))) return rc;
+    char* h = (char*)E->h_in.p;
+    std::memcpy(h, in->trace_off, b_off);
+    if (NT) std::memcpy(h + o_base, in->time_base, b_base);
+    if (NP) {
+      std::memcpy(h + o_lat, in->lat, b_pt);
+      std::memcpy(h + o_lon, in->lon, b_pt);
+      std::memcpy(h + o_dt, in->time_delta, b_pt);
+      std::memcpy(h + o_acc, in->accuracy, (size_t)NP * 2);
+    }
+    HIPCHK(hipMemcpyAsync(d, h, total, hipMemcpyHostToDevice, s));
+  } else {
+    const hipMemcpyKind h2d = hipMemcpyHostToDevice;
+    HIPCHK(hipMemcpyAsync(d, in->trace_off, b_off, h2d, s));
+    if (NT) HIPCHK(hipMemcpyAsync(d + o_base, in->time_base, b_base, h2d, s));
+    HIPCHK(big_copy(d + o_lat, in->lat, b_pt, h2d, s));
+    HIPCHK(big_copy(d + o_lon, in->lon, b_pt, h2d, s));
+    HIPCHK(big_copy(d + o_dt, in->time_delta, b_pt, h2d, s));
+    HIPCHK(big_copy(d + o_acc, in->accuracy, (size_t)NP * 2, h2d, s));
+  }
+  launch_expand_compact((const int64_t*)d, (const int64_t*)(d + o_base), (const int32_t*)(d + o_dt),
+                        (const int16_t*)(d + o_acc), (double*)E->in_time.p, (float*)E->in_acc.p, NT, s);
+  DevBatch b;
+  b.n_traces = NT;
+  b.n_points = NP;
+  b.trace_off = (const int64_t*)d;
+  b.lat = (const float*)(d + o_lat);
+  b.lon = (const float*)(d + o_lon);
   b.time = (const double*)E->in_time.p;
   b.acc = (const float*)E->in_acc.p;
   return engine_match(E, b, s, err);

@@ -24,8 +24,8 @@ struct ReqSlab {
 };
 
 namespace otm {
-// The order in which batch contexts copy request bytes to HBM (a pipelined
-// otm_report_batch's chunks; the async workers' batches): ticket t's copies
+// The order in which batch contexts copy request bytes to HBM (the async
+// workers' batches): ticket t's copies
 // queue behind ticket t-1's on the device (ev[(t - 1) & 1], recorded on t-1's
 // copy stream), so the host-to-device link carries one batch at a time, in
 // order, while the earlier batches run their kernels (abi.cpp H2DTurn).
@@ -101,10 +101,10 @@ struct otm_engine {
   Buf big_key, big_lab, big_inq, big_fr, big_ins, big_prev;
   Buf huge_key, huge_lab, huge_inq, huge_fr, huge_ins, huge_prev, overflow_list3;
   int32_t huge_log2 = 0;  // huge search tier: 2^huge_log2 slots per table (0: none yet; grown on demand)
-  int32_t huge_ready_log2 = 0;
+  int32_t huge_ready_log2 = 0;  // the layout the huge tables were last cleared for
   Buf cbig_key, cbig_val, cbig_skey;
-  int32_t cand_log2 = 0;
-  int32_t last_attempts = 0;  // runs of the last batch (otm_spill_stats::attempts)  // candidate HBM tier: 2^cand_log2 slots per table (0: none yet; grown on demand)  // the layout the huge tables were last cleared for
+  int32_t cand_log2 = 0;  // candidate HBM tier: 2^cand_log2 slots per table (0: none yet; grown on demand)
+  int32_t last_attempts = 0;  // runs of the last batch (otm_spill_stats::attempts)
   Buf ord_tile, ord_cnt, ord_cursor, ord_grp, ord_item;  // spatial work order
   Buf abort_flag;                                       // capacity overflow of the batch in flight
   Buf rs_blob;                                          // otm_report_segments_device in/out
@@ -174,10 +174,6 @@ struct otm_engine {
   std::vector<std::thread> workers;
   std::vector<otm_engine*> actx;  // the workers' clones (worker i >= 1 runs on actx[i - 1])
   otm::H2DOrder aorder;           // the workers' batches' copies, in take order
-  // a pipelined otm_report_batch (abi.cpp report_many_pipelined): chunk
-  // k >= 1 runs on pctx[k - 1] (made at the first such call)
-  std::mutex pmu;
-  std::vector<otm_engine*> pctx;
   uint64_t take_seq = 0, pub_seq = 0;
   bool stop = false;
   bool worker_started = false;
@@ -196,6 +192,7 @@ void engine_free(otm_engine* E);
 int engine_match(otm_engine* E, const DevBatch& b, hipStream_t s, std::string* err);
 // stage a host batch to the device and match it
 int engine_match_host(otm_engine* E, const otm_batch* in, std::string* err);
+int engine_match_compact(otm_engine* E, const otm_batch_compact* in, std::string* err);
 // The /report request bodies read on the GPU: engine_stage_requests returns a
 // pinned host staging buffer for n requests of `bytes` body bytes in all:
 // int64 offsets[n + 1] (into the bytes) and the bytes; the caller fills both

@@ -95,11 +95,13 @@ struct DevOrder {
 // holding every label of that search within cost cmax (1/64 m): the departure
 // label of each edge (key = edge id) and the arrival label of each node (key
 // = NODE_KEY | node), as one open-addressing hash table per row (linear
-// probing).  A slot is {key, cost, route distance bits, turn units}: the
-// route to the edge's start turned into it (or to the node), so a transition
-// reads its distance and turn cost from one slot; predecessor slots in a
-// parallel array give the route.  cnt < 0 marks a row whose search exceeded
-// the build table (queries on it use the online tiers).
+// probing from 2-slot buckets, 40 % load).  A slot is 16 bytes, {key, cost,
+// route distance bits, turn units} with the label's predecessor slot in the
+// cost's and units' top bytes (kernels.hip idx_slot_*): the route to the
+// edge's start turned into it (or to the node), so a transition reads its
+// distance and turn cost from one slot, and a route walks slot to slot.  cnt
+// < 0 marks a row whose search exceeded the build table (queries on it use
+// the online tiers).
 struct IdxRow {
   int64_t off;    // first slot of the row's table
   int32_t cnt;    // entries, -1 incomplete
@@ -109,9 +111,11 @@ struct DevIndex {
   float rmax;     // 0: no index
   uint32_t cmax;  // its cost bound, floor(rmax x 64)
   const IdxRow* row;   // [E + N]
-  const uint4* slot;
-  const int32_t* pred;   // per slot: its label's predecessor's slot in the row (-1: the route's first edge)
+  const uint4* slot;    // 16 B per slot, ~40 B per entry
 };
+constexpr int IDX_SLOT_BYTES = 16;
+// the index radius is capped so that every cost in a slot is below 2^24 (1/64 m)
+constexpr float INDEX_RMAX_CAP = 200000.0f;
 constexpr uint32_t NODE_KEY = 0x80000000u;  // key of a node's arrival label (edges: their id, < 2^27)
 constexpr uint32_t NONE_PRED = 0xFFFFFFFFu; // label predecessor of a route's first edge / the source node
 // near indexes: at most NEAR_LEVELS smaller radii of the same rows
@@ -339,7 +343,9 @@ void launch_compact(int32_t n_traces, const DevOut& o, const int32_t* seg_off, c
 // index build: pass 0 counts rows (row_cnt), pass 1 inserts them into the
 // row tables (slot array pre-filled with 0xFF)
 void launch_index_build(const DevGraph& g, const uint32_t* turn_units, uint32_t cmax, int32_t* row_cnt,
-                        const IdxRow* rows, uint4* slot, int32_t* pred, bool write, hipStream_t s);
+                        const IdxRow* rows, uint4* slot, bool write, hipStream_t s);
+// slots of a row of c entries (the index's load factor)
+int64_t index_row_cap(int32_t c);
 void launch_row_sizes(const int32_t* row_cnt, int64_t* row_sizes, int32_t n, hipStream_t s);
 struct BatchStatus {
   int32_t abort, grow;  // grow bit 0: the huge search tier needs (larger) tables; bit 1: the candidate HBM tier
@@ -347,6 +353,9 @@ struct BatchStatus {
   int32_t cnt[3], pad2;
 };
 void launch_batch_init(int32_t* counters, int32_t* abort, hipStream_t s);
+// otm_match_compact's inputs widened on the device (time = base + delta, accuracy as float)
+void launch_expand_compact(const int64_t* trace_off, const int64_t* tbase, const int32_t* dt, const int16_t* acc16,
+                           double* time, float* acc, int32_t n_traces, hipStream_t s);
 void launch_snap(int32_t* counters, int32_t* snap, bool reset, hipStream_t s);
 // batch bookkeeping folded into the stage kernels (no launches of their own)
 bool fold_bookkeeping();

@@ -1347,147 +1347,66 @@ __device__ __forceinline__ uint32_t idx_hash(uint32_t v) {
   return v;
 }
 
-// A row's table: OTM_IDX_LOAD_PCT = 0 sizes it to the power of two >= 2 x
-// entries and takes the hash's low bits; otherwise to entries x 100 / pct
-// slots, the hash mapped onto them by a multiply-high (no power-of-two
-// rounding: ~12 B per entry at 67 % instead of ~22 B).
+// A row's table: entries x 100 / OTM_IDX_LOAD_PCT slots rounded up to an even
+// count (at least one slot empty, so every probe ends), the hash mapped onto
+// its 2-slot buckets by a multiply-high.  A label's probe starts at its
+// bucket's first slot and goes on linearly; a lookup loads the bucket's two
+// slots (32 aligned bytes, one line) at once, which at this load holds the
+// label or ends the probe for nearly every lookup.  A slot is 16 bytes with
+// the predecessor inside (idx_slot_*): 16 x 100 / 40 = 40 B per entry
+// (round 4: 20 % load, 20-B slots, 100 B per entry).
 #ifndef OTM_IDX_LOAD_PCT
-#define OTM_IDX_LOAD_PCT 20
-#endif
-// OTM_IDX_HOME = 1 (round 4's first A/B, not kept): a label's home in a
-// row's table is its road's lower-numbered node (an edge key: min(from, to);
-// a node key: the node), and a home hashes to an aligned group of 8 slots,
-// one 128-B line, linear probing slot by slot from there.  A column's target
-// candidates -- a node and the two directions of the roads at it -- share a
-// few homes (0.42 homes per key on config 2, 0.45 on config 4), but the
-// lookups then walk the merged runs of several homes one dependent load at a
-// time: k_trans_sub 0.248 -> 0.370 ms on config 2, 2.29 -> 5.25 ms on config 4
-// (profiles/r04_ab/index_home/).
-// OTM_IDX_BUCKET = 1: the same homes, but a row's table is a run of 8-slot
-// buckets (one 128-B line each) and a lookup reads its home's whole bucket
-// with eight independent 16-B loads of that line, going on to the next bucket
-// only when the bucket is full without the key.  Probes of one source row for
-// targets sharing a home fetch one line.  Buckets are filled to
-// OTM_IDX_BUCKET_LOAD percent on average.
-#ifndef OTM_IDX_BUCKET
-#define OTM_IDX_BUCKET 0
-#endif
-#ifndef OTM_IDX_BUCKET_LOAD
-#define OTM_IDX_BUCKET_LOAD 35
-#endif
-// OTM_IDX_BUCKET_KEYS = 1: k_trans_sub reads the bucket's 8 keys, then the
-// matching slot (a second, cache-hit load of the same line) -- 8 registers a
-// probe instead of 32
-#ifndef OTM_IDX_BUCKET_KEYS
-#define OTM_IDX_BUCKET_KEYS 0
-#endif
-#ifndef OTM_IDX_HOME
-#define OTM_IDX_HOME OTM_IDX_BUCKET
-#endif
-#if OTM_IDX_HOME
-constexpr int IDX_GROUP = 8;
+#define OTM_IDX_LOAD_PCT 40
 #endif
 __host__ __device__ __forceinline__ int64_t idx_row_cap(int32_t c) {
   if (c <= 0) return 0;
-#if OTM_IDX_BUCKET
-  int64_t nb = ((int64_t)c * 100 + (int64_t)OTM_IDX_BUCKET_LOAD * IDX_GROUP - 1) / ((int64_t)OTM_IDX_BUCKET_LOAD * IDX_GROUP);
-  if (nb * IDX_GROUP <= c) nb = (int64_t)c / IDX_GROUP + 1;
-  return nb * IDX_GROUP;
-#elif OTM_IDX_HOME
   int64_t cap = ((int64_t)c * 100 + OTM_IDX_LOAD_PCT - 1) / OTM_IDX_LOAD_PCT;
   if (cap <= c) cap = (int64_t)c + 1;
-  return (cap + IDX_GROUP - 1) / IDX_GROUP * IDX_GROUP;
-#elif OTM_IDX_LOAD_PCT
-  const int64_t cap = ((int64_t)c * 100 + OTM_IDX_LOAD_PCT - 1) / OTM_IDX_LOAD_PCT;
-  return cap > c ? cap : (int64_t)c + 1;
-#else
-  int64_t cap = 2;
-  while (cap < 2 * (int64_t)c) cap <<= 1;
-  return cap;
-#endif
+  return (cap + 1) & ~(int64_t)1;
 }
-// the hash of a label's home (the lookups of a column compute it once per target)
-__device__ __forceinline__ uint32_t idx_home_hash(const DevGraph& g, uint32_t key) {
-#if OTM_IDX_HOME
-  if (key & NODE_KEY) return idx_hash(key & ~NODE_KEY);
-  const uint32_t u = (uint32_t)g.e_from[key], v = (uint32_t)g.e_to[key];
-  return idx_hash(u < v ? u : v);
-#else
-  (void)g;
-  return idx_hash(key);
-#endif
-}
-// first slot of a label in row R from its home hash
+// first slot of a label's probe in row R (its bucket's first slot)
 __device__ __forceinline__ uint32_t idx_slot0(uint32_t hh, const IdxRow& R) {
-#if OTM_IDX_HOME
-  return (uint32_t)(((uint64_t)hh * (uint64_t)(R.cap / IDX_GROUP)) >> 32) * IDX_GROUP;
-#elif OTM_IDX_LOAD_PCT
-  return (uint32_t)(((uint64_t)hh * (uint64_t)R.cap) >> 32);
-#else
-  return hh & (R.cap - 1u);
-#endif
+  return (uint32_t)(((uint64_t)hh * (uint64_t)(R.cap >> 1)) >> 32) << 1;
 }
 __device__ __forceinline__ uint32_t idx_next(uint32_t h, const IdxRow& R) {
   return h + 1u == R.cap ? 0u : h + 1u;
 }
-#if OTM_IDX_BUCKET
-__device__ __forceinline__ uint32_t idx_next_bucket(uint32_t h, const IdxRow& R) {
-  return h + IDX_GROUP == R.cap ? 0u : h + IDX_GROUP;
+// A slot {key, cost | pred lo << 24, route distance bits, units | pred hi << 24}:
+// cost and turn units below 2^24 (units <= cost <= the index's cmax, and the
+// index radius is capped so that cmax < 2^24), the 16-bit predecessor slot in
+// the row split over the two top bytes (IDX_NO_PRED: the route's first edge).
+constexpr uint32_t IDX_LOW24 = 0xFFFFFFu;
+constexpr uint32_t IDX_NO_PRED = 0xFFFFu;
+static_assert((int64_t)INDEX_BUILD_LIMIT * 100 / OTM_IDX_LOAD_PCT + 2 < (int64_t)IDX_NO_PRED,
+              "a row's slots must be numbered in 16 bits");
+__host__ __device__ __forceinline__ uint32_t idx_slot_cost(const uint4& s) { return s.y & IDX_LOW24; }
+__host__ __device__ __forceinline__ uint32_t idx_slot_units(const uint4& s) { return s.w & IDX_LOW24; }
+__host__ __device__ __forceinline__ int32_t idx_slot_pred(const uint4& s) {
+  const uint32_t p = (s.y >> 24) | ((s.w >> 24) << 8);
+  return p == IDX_NO_PRED ? -1 : (int32_t)p;
 }
-// one bucket of row R from slot h: the eight slots are loaded before any is
-// looked at (one line, one round trip)
-struct IdxBucket {
-  uint4 s[IDX_GROUP];
-};
-__device__ __forceinline__ void idx_load_bucket(const uint4* slot, const IdxRow& R, uint32_t h, IdxBucket& B) {
-  const uint4* p = slot + R.off + h;
-#pragma unroll
-  for (int i = 0; i < IDX_GROUP; ++i) B.s[i] = p[i];
-}
-// the key's slot index in the bucket (its contents in out), -1 when absent
-// from a bucket that has an empty slot (absent from the row), -2 when the
-// bucket is full without it (look in the next)
-__device__ __forceinline__ int idx_scan_bucket(const IdxBucket& B, uint32_t v, uint4& out) {
-  int m = -2;
-  bool empty = false;
-#pragma unroll
-  for (int i = 0; i < IDX_GROUP; ++i) {
-    if (B.s[i].x == v) {
-      m = i;
-      out = B.s[i];
-    }
-    empty = empty || B.s[i].x == EMPTY;
-  }
-  return m >= 0 ? m : (empty ? -1 : -2);
-}
-#endif
 
-// Row lookup: linear probing in the row's table.  Returns the slot (its
-// contents in *out) when the key is in the row, -1 when absent (its label
-// beyond cmax), -2 when the row is incomplete.
-__device__ __forceinline__ int64_t idx_find(const DevGraph& g, const DevIndex& X, const IdxRow& R, uint32_t v,
-                                            uint4& out) {
+// Row lookup: linear probing in the row's table from the key's bucket, a
+// bucket (two slots) per load.  Returns the slot (its contents in *out) when
+// the key is in the row, -1 when absent (its label beyond cmax), -2 when the
+// row is incomplete.
+__device__ __forceinline__ int64_t idx_find(const uint4* slot, const IdxRow& R, uint32_t v, uint4& out) {
   if (R.cnt < 0) return -2;
   if (R.cnt == 0) return -1;
-  uint32_t h = idx_slot0(idx_home_hash(g, v), R);
-#if OTM_IDX_BUCKET
+  uint32_t h = idx_slot0(idx_hash(v), R);
   while (true) {
-    IdxBucket B;
-    idx_load_bucket(X.slot, R, h, B);
-    const int m = idx_scan_bucket(B, v, out);
-    if (m >= 0) return R.off + h + m;
-    if (m == -1) return -1;
-    h = idx_next_bucket(h, R);
-  }
-#endif
-  while (true) {
-    const uint4 sl = X.slot[R.off + h];
-    if (sl.x == v) {
-      out = sl;
+    const uint4 a = slot[R.off + h], b = slot[R.off + h + 1];
+    if (a.x == v) {
+      out = a;
       return R.off + h;
     }
-    if (sl.x == EMPTY) return -1;
-    h = idx_next(h, R);
+    if (a.x == EMPTY) return -1;
+    if (b.x == v) {
+      out = b;
+      return R.off + h + 1;
+    }
+    if (b.x == EMPTY) return -1;
+    h = h + 2u == R.cap ? 0u : h + 2u;
   }
 }
 // the index row of a candidate as the source of a route: its edge's row
@@ -1506,10 +1425,10 @@ __device__ __forceinline__ uint32_t dst_key(const DevGraph& g, int32_t e, float 
 // inserts every label into the row's table with its cost, route distance and
 // turn units (each lane walks its label's predecessor chain in the LDS table),
 // and then, the row's slots all placed, its predecessor's slot in the row
-// (-1: the route's first edge), so a path is walked slot to slot.
+// (the route's first edge: none), so a path is walked slot to slot.
 template <bool WRITE>
 __global__ __launch_bounds__(TB) void k_index_build(DevGraph g, const uint32_t* TU, uint32_t cmax, int32_t* row_cnt,
-                                                    const IdxRow* rows, uint4* slot, int32_t* pred) {
+                                                    const IdxRow* rows, uint4* slot) {
   __shared__ uint32_t lkey[INDEX_BUILD_CAP];
   __shared__ unsigned long long llab[INDEX_BUILD_CAP];
   __shared__ uint32_t linq[INDEX_BUILD_CAP];
@@ -1547,35 +1466,25 @@ __global__ __launch_bounds__(TB) void k_index_build(DevGraph g, const uint32_t* 
       int len;
       chain_sums(g, TU, predof, pk, hin, (k & NODE_KEY) ? NO_HEAD : (uint32_t)g.e_head_out[k], cbuf + lane, d, units,
                  len);
-      uint32_t h = idx_slot0(idx_home_hash(g, k), R);
-#if OTM_IDX_BUCKET
-      // the first free slot of the first bucket with one, from the home's
-      // (a lookup stops at a bucket with an empty slot)
-      uint32_t t = 0;
-      while (atomicCAS(&slot[R.off + h + t].x, EMPTY, k) != EMPTY) {
-        if (++t == IDX_GROUP) {
-          t = 0;
-          h = idx_next_bucket(h, R);
-        }
-      }
-      h += t;
-#else
+      uint32_t h = idx_slot0(idx_hash(k), R);
       while (atomicCAS(&slot[R.off + h].x, EMPTY, k) != EMPTY) h = idx_next(h, R);
-#endif
-      slot[R.off + h].y = (uint32_t)(lab >> 32);
+      // (cost <= cmax < 2^24 and units <= cost: the top bytes are the
+      // predecessor's, written below)
+      slot[R.off + h].y = (uint32_t)(lab >> 32) & IDX_LOW24;
       slot[R.off + h].z = fbits(d);
-      slot[R.off + h].w = units;
+      slot[R.off + h].w = units & IDX_LOW24;
     }
     __syncthreads();
-    const DevIndex X{0.0f, 0u, rows, slot, pred};
     for (int i = lane; i < INDEX_BUILD_CAP; i += TB) {
       const uint32_t k = lkey[i];
       if (k == EMPTY) continue;
       const uint32_t pk = (uint32_t)(llab[i] & 0xFFFFFFFFull);
-      uint4 tmp;
-      const int64_t sk = idx_find(g, X, R, k, tmp);
-      const int64_t sp = pk == NONE_PRED ? -1 : idx_find(g, X, R, pk, tmp);
-      pred[sk] = sp < 0 ? -1 : (int32_t)(sp - R.off);
+      uint4 sk_v, tmp;
+      const int64_t sk = idx_find(slot, R, k, sk_v);
+      const int64_t sp = pk == NONE_PRED ? -1 : idx_find(slot, R, pk, tmp);
+      const uint32_t ps = sp < 0 ? IDX_NO_PRED : (uint32_t)(sp - R.off);
+      slot[sk].y = (sk_v.y & IDX_LOW24) | (ps & 0xFFu) << 24;
+      slot[sk].w = (sk_v.w & IDX_LOW24) | (ps >> 8) << 24;
     }
     __syncthreads();
   }
@@ -1614,10 +1523,9 @@ __global__ void k_row_pack(const int32_t* row_cnt, const int64_t* row_off, IdxRo
 #ifndef OTM_TRANS_KC8
 #define OTM_TRANS_KC8 8
 #endif
-// waves per SIMD the register budget is sized for (a bucket probe holds its
-// 8 slots, 32 registers)
+// waves per SIMD the register budget is sized for
 #ifndef OTM_TRANS_WAVES
-#define OTM_TRANS_WAVES (OTM_IDX_BUCKET && !OTM_IDX_BUCKET_KEYS ? 6 : 8)
+#define OTM_TRANS_WAVES 8
 #endif
 template <int S, bool LIST>
 __global__ __launch_bounds__(TB, OTM_TRANS_WAVES) void k_trans_sub(DevGraph g, DevBatch b, DevParams P, DevWork w) {
@@ -1710,7 +1618,7 @@ __global__ __launch_bounds__(TB, OTM_TRANS_WAVES) void k_trans_sub(DevGraph g, D
         const int32_t e = c.x;
         const float o = __int_as_float(c.y);
         const uint32_t key = dst_key(g, e, o);
-        tg[sg][k ^ swz] = make_int4(e, __float_as_int(o), (int)key, (int)idx_home_hash(g, key));
+        tg[sg][k ^ swz] = make_int4(e, __float_as_int(o), (int)key, (int)idx_hash(key));
       }
       if (act && k < Kq) {
         const int2 c = crec(w, q, k);
@@ -1734,96 +1642,19 @@ __global__ __launch_bounds__(TB, OTM_TRANS_WAVES) void k_trans_sub(DevGraph g, D
     if (act) {
       float* Tm = w.trans + toff;
       unsigned long long ntr = 0;
-#if OTM_IDX_BUCKET
-      // one pair per lane per step: its home's bucket of its source's row
-      const int npair = Kq * Kp;
-      for (int idx = sl; idx < npair; idx += S) {
-        const int i = idx / Kp, j = idx - (idx / Kp) * Kp;
-        const int4 T = tg[sg][j ^ swz], Sx = sr[sg][i ^ swz];
-        const IdxRow R = rq[sg][i ^ swz];
-        const uint32_t key = (uint32_t)T.z;
-        const int32_t ej = T.x, ei = Sx.x;
-        const float oj = __int_as_float(T.y), oi = __int_as_float(Sx.y), si = __int_as_float(Sx.z);
-        const bool same = same_edge_step(ei, oi, ej, oj);
-#if OTM_IDX_BUCKET_KEYS
-        // keys first (8 registers), the matching slot after (the same line)
-        uint32_t bk[IDX_GROUP];
-        uint32_t h = 0;
-        if (!same && R.cnt > 0) {
-          h = idx_slot0((uint32_t)T.w, R);
-#pragma unroll
-          for (int t = 0; t < IDX_GROUP; ++t) bk[t] = xslot[R.off + h + t].x;
-        }
-#else
-        IdxBucket B;
-        uint32_t h = 0;
-        if (!same && R.cnt > 0) {
-          h = idx_slot0((uint32_t)T.w, R);
-          idx_load_bucket(xslot, R, h, B);
-        }
-#endif
-        float r = 0.0f;
-        bool ok = true;
-        uint32_t units = 0;
-        if (same) {
-          r = same_edge_dist(oi, oj);
-        } else {
-          uint4 sv = make_uint4(EMPTY, 0u, 0u, 0u);
-          int m = -1;
-          if (R.cnt > 0) {
-#if OTM_IDX_BUCKET_KEYS
-            while (true) {
-              bool empty = false;
-              m = -2;
-#pragma unroll
-              for (int t = IDX_GROUP - 1; t >= 0; --t) {
-                m = bk[t] == key ? t : m;
-                empty = empty || bk[t] == EMPTY;
-              }
-              if (m >= 0 || empty) break;
-              h = idx_next_bucket(h, R);  // the home's bucket full without the key (rare)
-#pragma unroll
-              for (int t = 0; t < IDX_GROUP; ++t) bk[t] = xslot[R.off + h + t].x;
-            }
-            if (m >= 0) sv = xslot[R.off + h + m];
-#else
-            m = idx_scan_bucket(B, key, sv);
-            while (m == -2) {  // the home's bucket full without the key (rare)
-              h = idx_next_bucket(h, R);
-              idx_load_bucket(xslot, R, h, B);
-              m = idx_scan_bucket(B, key, sv);
-            }
-#endif
-          }
-          // a label of the row beyond this column's cost bound is not one
-          // of its search's labels
-          if (m >= 0 && sv.y <= cq) {
-            const float sd = si + bitsf(sv.z);
-            r = sd + oj;
-            units = sv.w;
-          } else {
-            ok = false;
-          }
-        }
-        float cost = INFINITY;
-        if (ok && r <= bound) {
-          cost = trans_cost(units, r, gcv, P.beta);
-          ++ntr;
-        }
-        Tm[i * Kp + j] = cost;
-      }
-#else
-      // OTM_TRANS_BATCH pairs per lane per step: every pair's first slot is
-      // loaded before any is resolved, so their probes are in flight together
+      // OTM_TRANS_BATCH pairs per lane per step: every pair's first bucket
+      // (two slots, one aligned 32-B piece of a line) is loaded before any is
+      // resolved, so their probes are in flight together
       constexpr int NB = OTM_TRANS_BATCH;
       const int npair = Kq * Kp;
       for (int idx0 = sl; idx0 < npair; idx0 += S * NB) {
-        uint4 s0[NB];
+        uint4 s0[NB], s1[NB];
         uint32_t h0[NB];
 #pragma unroll
         for (int u = 0; u < NB; ++u) {
           const int idx = idx0 + u * S;
           s0[u] = make_uint4(EMPTY, 0u, 0u, 0u);
+          s1[u] = s0[u];
           h0[u] = 0u;
           if (idx < npair) {
             const int i = idx / Kp, j = idx - (idx / Kp) * Kp;
@@ -1833,6 +1664,7 @@ __global__ __launch_bounds__(TB, OTM_TRANS_WAVES) void k_trans_sub(DevGraph g, D
             if (!same && R.cnt > 0) {
               h0[u] = idx_slot0((uint32_t)T.w, R);
               s0[u] = xslot[R.off + h0[u]];
+              s1[u] = xslot[R.off + h0[u] + 1];
             }
           }
         }
@@ -1853,8 +1685,9 @@ __global__ __launch_bounds__(TB, OTM_TRANS_WAVES) void k_trans_sub(DevGraph g, D
           } else {
             const IdxRow R = rq[sg][i ^ swz];
             uint4 sv = s0[u];
-            uint32_t h = h0[u];
-            if (R.cnt > 0) {
+            if (R.cnt > 0 && sv.x != key && sv.x != EMPTY) {
+              sv = s1[u];
+              uint32_t h = h0[u] + 1u;
               while (sv.x != key && sv.x != EMPTY) {  // the rest of the linear probe (rare)
                 h = idx_next(h, R);
                 sv = xslot[R.off + h];
@@ -1862,10 +1695,10 @@ __global__ __launch_bounds__(TB, OTM_TRANS_WAVES) void k_trans_sub(DevGraph g, D
             }
             // a label of the row beyond this column's cost bound is not one
             // of its search's labels
-            if (R.cnt > 0 && sv.x == key && sv.y <= cq) {
+            if (R.cnt > 0 && sv.x == key && idx_slot_cost(sv) <= cq) {
               const float sd = si + bitsf(sv.z);
               r = sd + oj;
-              units = sv.w;
+              units = idx_slot_units(sv);
             } else {
               ok = false;
             }
@@ -1878,7 +1711,6 @@ __global__ __launch_bounds__(TB, OTM_TRANS_WAVES) void k_trans_sub(DevGraph g, D
           Tm[i * Kp + j] = cost;
         }
       }
-#endif
       if (w.ctr) {
         // algorithmic counts of the equivalent searches (per-lane partials,
         // summed over the wave at the end): per distinct source (node,
@@ -1896,9 +1728,9 @@ __global__ __launch_bounds__(TB, OTM_TRANS_WAVES) void k_trans_sub(DevGraph g, D
           const IdxRow R = rq[sg][i ^ swz];
           for (int64_t k = sl; k < (int64_t)R.cap; k += S) {
             const uint4 slt = xslot[R.off + k];
-            if (slt.x == EMPTY || (slt.x & NODE_KEY) || slt.y > cq) continue;
+            if (slt.x == EMPTY || (slt.x & NODE_KEY) || idx_slot_cost(slt) > cq) continue;
             ++c_settled;
-            if ((unsigned long long)slt.y + g.e_len64[slt.x] <= cq) {
+            if ((unsigned long long)idx_slot_cost(slt) + g.e_len64[slt.x] <= cq) {
               const int32_t v = g.e_to[slt.x];
               c_relaxed += (unsigned long long)(g.out_off[v + 1] - g.out_off[v]);
             }
@@ -1984,16 +1816,17 @@ __global__ __launch_bounds__(256, OTM_ROUTE_WAVES) void k_route_index(DevGraph g
     const DevIndex& Xc = lvl >= 0 ? w.idxn[lvl] : X;
     if (X.rmax > 0.0f && cq <= X.cmax) {
       Rw = Xc.row[src_row(g, ei, oi)];
-      sv = idx_find(g, Xc, Rw, dst_key(g, ej, oj), lab);
+      sv = idx_find(Xc.slot, Rw, dst_key(g, ej, oj), lab);
     }
-    if (sv < 0 || lab.y > cq) {
+    if (sv < 0 || idx_slot_cost(lab) > cq) {
       const int slot = atomicAdd(&w.counters_i32[4], 1);
       w.overflow_list0[slot] = (int32_t)p;
       continue;
     }
-    // the path: the label's predecessor slots in the row, back to the first edge
+    // the path: the label's predecessor slots in the row, back to the first
+    // edge (a slot holds its label's edge and its predecessor's slot)
     int len = 0;
-    for (int32_t ps = Xc.pred[sv]; ps >= 0 && len <= Rw.cnt; ps = Xc.pred[Rw.off + ps]) ++len;
+    for (int32_t ps = idx_slot_pred(lab); ps >= 0 && len <= Rw.cnt; ps = idx_slot_pred(Xc.slot[Rw.off + ps])) ++len;
     const int off = len ? atomicAdd(&w.counters_i32[1], len) : 0;
     if (off + len > w.pool_cap) {
       w.counters_i32[2] = 1;
@@ -2001,8 +1834,11 @@ __global__ __launch_bounds__(256, OTM_ROUTE_WAVES) void k_route_index(DevGraph g
       w.path_len[p] = -1;
     } else {
       int k = len;
-      for (int32_t ps = Xc.pred[sv]; ps >= 0 && k > 0; ps = Xc.pred[Rw.off + ps])
-        w.path_pool[off + (--k)] = (int32_t)Xc.slot[Rw.off + ps].x;
+      for (int32_t ps = idx_slot_pred(lab); ps >= 0 && k > 0;) {
+        const uint4 sl = Xc.slot[Rw.off + ps];
+        w.path_pool[off + (--k)] = (int32_t)sl.x;
+        ps = idx_slot_pred(sl);
+      }
       w.path_off[p] = off;
       w.path_len[p] = len;
     }
@@ -2013,9 +1849,9 @@ __global__ __launch_bounds__(256, OTM_ROUTE_WAVES) void k_route_index(DevGraph g
       unsigned long long st = 0, rl = 0;
       for (int64_t k = 0; k < (int64_t)Rw.cap; ++k) {
         const uint4 sl = Xc.slot[Rw.off + k];
-        if (sl.x == EMPTY || (sl.x & NODE_KEY) || sl.y > cq) continue;
+        if (sl.x == EMPTY || (sl.x & NODE_KEY) || idx_slot_cost(sl) > cq) continue;
         ++st;
-        if ((unsigned long long)sl.y + g.e_len64[sl.x] <= cq) {
+        if ((unsigned long long)idx_slot_cost(sl) + g.e_len64[sl.x] <= cq) {
           const int32_t v = g.e_to[sl.x];
           rl += (unsigned long long)(g.out_off[v + 1] - g.out_off[v]);
         }
@@ -4147,6 +3983,27 @@ void launch_batch_init(int32_t* counters, int32_t* abort, hipStream_t s) {
 void launch_snap(int32_t* counters, int32_t* snap, bool reset, hipStream_t s) {
   hipLaunchKernelGGL(k_snap, dim3(1), dim3(64), 0, s, counters, snap, reset ? 1 : 0);
 }
+// The compact host batch (otm_match_compact) widened on the device: a wave per
+// trace, its points' time = base + delta (whole seconds, exact in a double)
+// and accuracy as float -- the arrays every stage reads.
+__global__ __launch_bounds__(256) void k_expand_compact(const int64_t* trace_off, const int64_t* tbase,
+                                                        const int32_t* dt, const int16_t* acc16, double* time,
+                                                        float* acc, int32_t n_traces) {
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (int64_t t = (int64_t)blockIdx.x * 4 + wv; t < n_traces; t += (int64_t)gridDim.x * 4) {
+    const int64_t a = trace_off[t], e = trace_off[t + 1], base = tbase[t];
+    for (int64_t i = a + lane; i < e; i += 64) {
+      time[i] = (double)(base + (int64_t)dt[i]);
+      acc[i] = (float)acc16[i];
+    }
+  }
+}
+void launch_expand_compact(const int64_t* trace_off, const int64_t* tbase, const int32_t* dt, const int16_t* acc16,
+                           double* time, float* acc, int32_t n_traces, hipStream_t s) {
+  if (n_traces <= 0) return;
+  hipLaunchKernelGGL(k_expand_compact, dim3(grid_for(((int64_t)n_traces + 3) / 4, 1, 1 << 20)), dim3(256), 0, s,
+                     trace_off, tbase, dt, acc16, time, acc, n_traces);
+}
 void launch_status(const int32_t* abort, const int64_t* ttotal, const int32_t* counters, BatchStatus* out,
                    hipStream_t s) {
   hipLaunchKernelGGL(k_status, dim3(1), dim3(64), 0, s, abort, ttotal, counters, out);
@@ -4280,15 +4137,14 @@ void launch_report(const DevBatch& b, const DevReportCfg& rc, DevWork& w, DevOut
 #undef TIMED
 
 void launch_index_build(const DevGraph& g, const uint32_t* turn_units, uint32_t cmax, int32_t* row_cnt,
-                        const IdxRow* rows, uint4* slot, int32_t* pred, bool write, hipStream_t s) {
+                        const IdxRow* rows, uint4* slot, bool write, hipStream_t s) {
   const int grid = grid_for((int64_t)g.n_edges + g.n_nodes, 1, 256 * 16);
   if (write)
-    hipLaunchKernelGGL(k_index_build<true>, dim3(grid), dim3(TB), 0, s, g, turn_units, cmax, row_cnt, rows, slot,
-                       pred);
+    hipLaunchKernelGGL(k_index_build<true>, dim3(grid), dim3(TB), 0, s, g, turn_units, cmax, row_cnt, rows, slot);
   else
-    hipLaunchKernelGGL(k_index_build<false>, dim3(grid), dim3(TB), 0, s, g, turn_units, cmax, row_cnt, rows, slot,
-                       pred);
+    hipLaunchKernelGGL(k_index_build<false>, dim3(grid), dim3(TB), 0, s, g, turn_units, cmax, row_cnt, rows, slot);
 }
+int64_t index_row_cap(int32_t c) { return idx_row_cap(c); }
 void launch_row_sizes(const int32_t* row_cnt, int64_t* row_sizes, int32_t n, hipStream_t s) {
   hipLaunchKernelGGL(k_row_sizes, dim3(grid_for((int64_t)n + 1, 256, 1 << 30)), dim3(256), 0, s, row_cnt, row_sizes,
                      n);

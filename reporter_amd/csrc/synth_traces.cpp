@@ -31,10 +31,13 @@ double heading(const HostGraph& g, int e, bool at_end) {
 }  // namespace
 
 // path (optional): the edges each vehicle drives from its first to its last
-// probe, in order, appended per vehicle; path_off[v] = where vehicle v's start
+// probe, in order, appended per vehicle; path_off[v] = where vehicle v's
+// start; enter (optional, with path): the time the vehicle entered each path
+// edge (the first edge's before the first probe, at the vehicle's speed)
 int synth_traces(const HostGraph& g, const otm_synth_trace_params* p, int64_t* trace_off, float* lat, float* lon,
                  double* time, float* accuracy, int32_t* true_edge, float* true_off,
-                 std::vector<int32_t>* path = nullptr, int64_t* path_off = nullptr) {
+                 std::vector<int32_t>* path = nullptr, int64_t* path_off = nullptr,
+                 std::vector<double>* enter = nullptr) {
   const int NE = g.h.n_edges;
   std::vector<int> starts;
   for (int e = 0; e < NE; ++e)
@@ -60,6 +63,7 @@ int synth_traces(const HostGraph& g, const otm_synth_trace_params* p, int64_t* t
       if (g.e_flags[edge] & OTM_EDGE_INTERNAL) lo = 6.0, hi = 9.0;
       return lo + f * (hi - lo);
     };
+    if (path && enter) enter->push_back(p->t0 - off / speed_of(e));
     for (int s = 0; s < p->points_per_vehicle; ++s) {
       // position on (e, off)
       int a = g.e_shape_off[e], b = g.e_shape_off[e + 1] - 1;
@@ -123,6 +127,7 @@ int synth_traces(const HostGraph& g, const otm_synth_trace_params* p, int64_t* t
         e = next;
         off = 0;
         if (path) path->push_back(e);
+        if (path && enter) enter->push_back(p->t0 + s * p->interval_s + (p->interval_s - dt));
       }
     }
   }
@@ -150,8 +155,9 @@ extern "C" int otm_synth_traces(const char* graph_path, const otm_synth_trace_pa
 // (same generator, same seeds), for implementation-independent accuracy
 // figures.  Fills path_off[n_vehicles + 1] and up to `cap` edges; returns the
 // total edge count (call with cap 0 to size), or a negative error.
-extern "C" int64_t otm_synth_true_paths(const char* graph_path, const otm_synth_trace_params* p, int64_t* path_off,
-                                        int32_t* path_edges, int64_t cap) {
+extern "C" int64_t otm_synth_true_paths_timed(const char* graph_path, const otm_synth_trace_params* p,
+                                              int64_t* path_off, int32_t* path_edges, double* enter_time,
+                                              int64_t cap) {
   otm::HostGraph g;
   std::string err;
   int rc = otm::load_graph(graph_path, &g, &err);
@@ -164,14 +170,21 @@ extern "C" int64_t otm_synth_true_paths(const char* graph_path, const otm_synth_
   std::vector<float> la(P), lo(P), acc(P);
   std::vector<double> tm(P);
   std::vector<int32_t> path;
+  std::vector<double> ent;
   std::vector<int64_t> poff((size_t)p->n_vehicles + 1);
   rc = otm::synth_traces(g, p, toff.data(), la.data(), lo.data(), tm.data(), acc.data(), nullptr, nullptr, &path,
-                         poff.data());
+                         poff.data(), enter_time ? &ent : nullptr);
   if (rc) return rc;
   if (path_off) std::memcpy(path_off, poff.data(), poff.size() * 8);
-  if (path_edges && cap > 0)
-    std::memcpy(path_edges, path.data(), (size_t)std::min<int64_t>(cap, (int64_t)path.size()) * 4);
+  const size_t m = (size_t)std::min<int64_t>(std::max<int64_t>(cap, 0), (int64_t)path.size());
+  if (path_edges && m) std::memcpy(path_edges, path.data(), m * 4);
+  if (enter_time && m) std::memcpy(enter_time, ent.data(), m * 8);
   return (int64_t)path.size();
+}
+
+extern "C" int64_t otm_synth_true_paths(const char* graph_path, const otm_synth_trace_params* p, int64_t* path_off,
+                                        int32_t* path_edges, int64_t cap) {
+  return otm_synth_true_paths_timed(graph_path, p, path_off, path_edges, nullptr, cap);
 }
 
 // Kafka DefaultPartitioner: murmur2 (seed 0x9747b28c) over the key bytes.

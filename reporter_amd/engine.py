@@ -46,6 +46,69 @@ def write_config(path, graph_path, index_radius_m=None, grid_mult=None, trans_la
     return path
 
 
+def compact_batch(batch):
+    """A batch narrowed to otm_batch_compact (the Java host's Point types):
+    int64 time base per trace (its first time), int32 time deltas, int16
+    accuracies.  Raises ValueError when a time is not a whole number of
+    seconds, a delta leaves int32 or an accuracy leaves int16 (such a batch
+    goes through Engine.match)."""
+    off = np.ascontiguousarray(batch["trace_off"], dtype=np.int64)
+    tm = np.asarray(batch["time"], dtype=np.float64)
+    acc = np.asarray(batch["accuracy"], dtype=np.float32)
+    ti = tm.astype(np.int64)
+    if not np.array_equal(ti.astype(np.float64), tm):
+        raise ValueError("compact batches carry whole-second times")
+    ia = acc.astype(np.int64)
+    if not np.array_equal(ia.astype(np.float32), acc) or (len(ia) and (ia.min() < -32768 or ia.max() > 32767)):
+        raise ValueError("compact batches carry int16 accuracies")
+    nt = len(off) - 1
+    lens = np.diff(off)
+    base = np.zeros(nt, dtype=np.int64)
+    nz = lens > 0
+    base[nz] = ti[off[:-1][nz]]
+    delta = ti - np.repeat(base, lens)
+    if len(delta) and (delta.min() < -2**31 or delta.max() >= 2**31):
+        raise ValueError("a trace's times span more than int32 seconds")
+    return {"trace_off": off, "time_base": base,
+            "lat": np.ascontiguousarray(batch["lat"], dtype=np.float32),
+            "lon": np.ascontiguousarray(batch["lon"], dtype=np.float32),
+            "time_delta": delta.astype(np.int32), "accuracy": ia.astype(np.int16)}
+
+
+class RequestArena(object):
+    """Request bodies written back to back into library-owned page-locked
+    memory (otm_request_arena_alloc), as the Java host writes its
+    body.getBytes(ISO_8859_1) into a MemorySegment over the arena; pass it to
+    Engine.report_batch / submit_batch in place of the bodies."""
+
+    def __init__(self, bodies):
+        bs = [b.encode("utf-8") if isinstance(b, str) else b for b in bodies]
+        self.n = len(bs)
+        total = sum(len(b) for b in bs)
+        self.base = lib().otm_request_arena_alloc(max(total, 1))
+        if not self.base:
+            raise OtmError("otm_request_arena_alloc: %s" % _lib.last_error())
+        blob = b"".join(bs)
+        C.memmove(self.base, blob, len(blob))
+        offs = np.zeros(self.n + 1, dtype=np.int64)
+        np.cumsum([len(b) for b in bs], out=offs[1:])
+        self.ptrs = (C.c_void_p * self.n)(*[self.base + int(o) for o in offs[:-1]])
+        self.ptrs = C.cast(self.ptrs, C.POINTER(C.c_char_p))
+        self.lens = (C.c_size_t * self.n)(*[len(b) for b in bs])
+        self.bytes = total
+
+    def release(self):
+        if self.base:
+            _check(lib().otm_request_arena_release(self.base))
+            self.base = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.release()
+
+
 class Results(object):
     """Host copy of one batch's results (numpy structured arrays)."""
 
@@ -146,10 +209,15 @@ class Engine(object):
         return code, take(out, n.value).decode("utf-8")
 
     def report_batch(self, bodies):
-        bs = [b.encode("utf-8") if isinstance(b, str) else b for b in bodies]
-        n = len(bs)
-        arr = (C.c_char_p * n)(*bs)
-        lens = (C.c_size_t * n)(*[len(b) for b in bs])
+        """otm_report_batch over request bodies (bytes / str), or over a
+        RequestArena's bodies (sent to HBM straight from the arena)."""
+        if isinstance(bodies, RequestArena):
+            n, arr, lens = bodies.n, bodies.ptrs, bodies.lens
+        else:
+            bs = [b.encode("utf-8") if isinstance(b, str) else b for b in bodies]
+            n = len(bs)
+            arr = (C.c_char_p * n)(*bs)
+            lens = (C.c_size_t * n)(*[len(b) for b in bs])
         outs = (C.c_void_p * n)()
         olens = (C.c_size_t * n)()
         codes = (C.c_int * n)()
@@ -187,11 +255,15 @@ class Engine(object):
         _check(lib().otm_submit(self.h, b, len(b), tag))
 
     def submit_batch(self, bodies, tags):
-        """otm_submit_batch: many requests in one call (in order)."""
-        bs = [b.encode("utf-8") if isinstance(b, str) else b for b in bodies]
-        n = len(bs)
-        arr = (C.c_char_p * n)(*bs)
-        lens = (C.c_size_t * n)(*[len(b) for b in bs])
+        """otm_submit_batch: many requests in one call (in order); a
+        RequestArena's bodies are referenced, not copied."""
+        if isinstance(bodies, RequestArena):
+            n, arr, lens = bodies.n, bodies.ptrs, bodies.lens
+        else:
+            bs = [b.encode("utf-8") if isinstance(b, str) else b for b in bodies]
+            n = len(bs)
+            arr = (C.c_char_p * n)(*bs)
+            lens = (C.c_size_t * n)(*[len(b) for b in bs])
         tg = (C.c_uint64 * n)(*tags)
         _check(lib().otm_submit_batch(self.h, n, arr, lens, tg))
 
@@ -214,6 +286,18 @@ class Engine(object):
                        tm.ctypes.data, acc.ctypes.data)
         r = _lib.Results()
         _check(lib().otm_match_soa(self.h, C.byref(b), C.byref(r)))
+        return Results(r)
+
+    def match_compact(self, batch):
+        """Host batch -> Results through otm_match_compact: the batch narrowed
+        to the Java host's own integers (compact_batch), 14 B per point over
+        the link, widened on the device."""
+        cb = compact_batch(batch)
+        b = _lib.BatchCompact(len(cb["trace_off"]) - 1, int(cb["trace_off"][-1]), cb["trace_off"].ctypes.data,
+                              cb["time_base"].ctypes.data, cb["lat"].ctypes.data, cb["lon"].ctypes.data,
+                              cb["time_delta"].ctypes.data, cb["accuracy"].ctypes.data)
+        r = _lib.Results()
+        _check(lib().otm_match_compact(self.h, C.byref(b), C.byref(r)))
         return Results(r)
 
     def match_device(self, trace_off, lat, lon, time, accuracy, stream=None):

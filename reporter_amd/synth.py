@@ -132,6 +132,27 @@ def true_paths(graph_path, n_vehicles, points_per_vehicle, interval_s=5.0, noise
     return off, edges[:n]
 
 
+def true_paths_timed(graph_path, n_vehicles, points_per_vehicle, interval_s=5.0, noise_sigma_m=15.0, accuracy=15.0,
+                     t0=1500000000.0, seed=7, vehicle_offset=0, vehicle_ids=None):
+    """true_paths with the time each vehicle entered each path edge:
+    (path_off, edges, enter_time)."""
+    ids = None
+    if vehicle_ids is not None:
+        ids = np.ascontiguousarray(vehicle_ids, dtype=np.int32)
+        n_vehicles = len(ids)
+    tp = _lib.SynthTraceParams(n_vehicles, points_per_vehicle, interval_s, noise_sigma_m, accuracy, t0, seed,
+                               vehicle_offset, ids.ctypes.data if ids is not None else None)
+    off = np.zeros(n_vehicles + 1, np.int64)
+    n = lib().otm_synth_true_paths_timed(graph_path.encode(), C.byref(tp), off.ctypes.data, None, None, 0)
+    if n < 0:
+        raise RuntimeError("otm_synth_true_paths_timed failed: %s" % _lib.last_error())
+    edges = np.zeros(max(n, 1), np.int32)
+    enter = np.zeros(max(n, 1), np.float64)
+    lib().otm_synth_true_paths_timed(graph_path.encode(), C.byref(tp), off.ctypes.data, edges.ctypes.data,
+                                     enter.ctypes.data, n)
+    return off, edges[:n], enter[:n]
+
+
 def _dedup(seq):
     out = []
     for x in seq:
@@ -315,6 +336,135 @@ def segment_agreement(graph_path, path_off, path_edges, results, trace_off=None,
         bd["outlier_points"] = int(np.asarray(outlier).sum())
     return {"segment_id_agreement": lcs / float(max(den, 1)), "sequences_exact": exact / float(max(len(tr), 1)),
             "traces": len(tr), "breakdown": bd}
+
+
+def true_segments(graph_path, path_off, path_edges, enter, last_time):
+    """Per trace, the segment list the vehicle drove as a Match output would
+    give it (the grouping and validity rules of DESIGN.md §3 rule 7, on the
+    true route with its true times): consecutive path edges of one OSMLR
+    segment (increasing position) or one run of unassociated edges of one
+    internal flag form a segment; its start time is valid when the vehicle
+    entered the segment's first edge after the trace began (the first path
+    edge was entered before the first probe), its end time when it left the
+    segment's last edge before the trace ended (the last path edge is left
+    after the last probe); length only when both are.  Returns a list of
+    lists of dicts (the Match JSON's segment objects)."""
+    eseg = _graph_section(graph_path, 8, np.int32)       # OTMG_EDGE_SEG
+    epos = _graph_section(graph_path, 9, np.int32)       # OTMG_EDGE_SEG_POS
+    eflg = _graph_section(graph_path, 10, np.uint8)      # OTMG_EDGE_FLAGS
+    gid = _graph_section(graph_path, 17, np.uint64)      # OTMG_SEG_ID
+    glen = _graph_section(graph_path, 18, np.float32)    # OTMG_SEG_LEN
+    out = []
+    for t in range(len(path_off) - 1):
+        a, e = int(path_off[t]), int(path_off[t + 1])
+        E = path_edges[a:e]
+        T = enter[a:e]
+        m = len(E)
+        segs = []
+        i = 0
+        while i < m:
+            j = i
+            while j + 1 < m:
+                x, y = int(E[j]), int(E[j + 1])
+                if eseg[y] >= 0:
+                    join = eseg[x] == eseg[y] and epos[y] == epos[x] + 1
+                else:
+                    join = eseg[x] < 0 and ((eflg[x] ^ eflg[y]) & 1) == 0
+                if not join:
+                    break
+                j += 1
+            f, l = int(E[i]), int(E[j])
+            sv = i > 0
+            ev = j < m - 1
+            d = {}
+            if eseg[f] >= 0:
+                sv = sv and bool(eflg[f] & 2)
+                ev = ev and bool(eflg[l] & 4)
+                d["segment_id"] = int(gid[eseg[f]])
+                d["length"] = int(np.floor(float(glen[eseg[f]]) + 0.5)) if (sv and ev) else -1
+                d["internal"] = False
+            else:
+                d["length"] = -1
+                d["internal"] = bool(eflg[f] & 1)
+            d["start_time"] = float(T[i]) if sv else -1
+            d["end_time"] = float(T[j + 1]) if ev else -1
+            d.update(queue_length=0, begin_shape_index=0, end_shape_index=0, way_ids=[])
+            segs.append(d)
+            i = j + 1
+        out.append(segs)
+    return out
+
+
+REPORT_ERROR_CLASSES = ("start_missed", "start_extra", "end_missed", "end_extra", "interior_missed",
+                        "interior_extra")
+
+
+def report_agreement(graph_path, path_off, path_edges, enter, trace_off, time, results):
+    """What the datastore receives, against the ground truth: per trace, the
+    reports report() (py/reporter_service.py:110-196, the product's host
+    restatement pinned by the reference's recorded cases) emits for the driven
+    route with its true times (true_segments), against the matched batch's
+    reports.  Reports pair up by an LCS over (id, next_id); unpaired ones
+    before the first or after the last pair are start / end errors, the rest
+    interior.  For the pairs: |t0 - true t0|, |t1 - true t1| (s) and the
+    relative error of the reported speed length / (t1 - t0)."""
+    import json as _json
+
+    from .engine import report_segments
+    truth = true_segments(graph_path, path_off, path_edges, enter, None)
+    tr = results.traces if hasattr(results, "traces") else results["traces"]
+    reps = results.reports if hasattr(results, "reports") else results["reports"]
+    c = dict((k, 0) for k in REPORT_ERROR_CLASSES)
+    n_truth = n_match = paired = den = exact = 0
+    dt0, dt1, dsp = [], [], []
+    for t in range(len(tr)):
+        p1 = int(trace_off[t + 1]) - 1
+        tl = float(time[p1])
+        ts = int(tl) if tl == int(tl) else repr(tl)
+        body = '{"uuid":"x","trace":[{"lat":0,"lon":0,"time":%s,"accuracy":5},{"lat":0,"lon":0,"time":%s,' \
+               '"accuracy":5}]}' % (ts, ts)
+        code, resp = report_segments(body, _json.dumps({"segments": truth[t]}, separators=(",", ":")))
+        want = _json.loads(resp).get("datastore", {}).get("reports", []) if code == 200 else []
+        a, n = int(tr["rep_off"][t]), int(tr["rep_cnt"][t])
+        got = reps[a:a + n]
+        kw = [(int(r["id"]), int(r.get("next_id", -1))) for r in want]
+        kg = [(int(x), int(y)) for x, y in zip(got["id"].tolist(), got["next_id"].tolist())]
+        pairs = _lcs_pairs(kw, kg)
+        n_truth += len(kw)
+        n_match += len(kg)
+        paired += len(pairs)
+        den += max(len(kw), len(kg))
+        exact += kw == kg
+        if not pairs:
+            c["start_missed"] += len(kw)
+            c["start_extra"] += len(kg)
+            continue
+        (i0, j0), (i1, j1) = pairs[0], pairs[-1]
+        c["start_missed"] += i0
+        c["start_extra"] += j0
+        c["end_missed"] += len(kw) - 1 - i1
+        c["end_extra"] += len(kg) - 1 - j1
+        for (pa, pb), (qa, qb) in zip(pairs, pairs[1:]):
+            c["interior_missed"] += qa - pa - 1
+            c["interior_extra"] += qb - pb - 1
+        for i, j in pairs:
+            w, g = want[i], got[j]
+            dt0.append(abs(float(g["t0"]) - float(w["t0"])))
+            dt1.append(abs(float(g["t1"]) - float(w["t1"])))
+            vw = float(w["length"]) / max(float(w["t1"]) - float(w["t0"]), 1e-9)
+            vg = float(g["length"]) / max(float(g["t1"]) - float(g["t0"]), 1e-9)
+            dsp.append(abs(vg - vw) / max(vw, 1e-9))
+    q = lambda xs, f: float(np.percentile(xs, f)) if xs else None  # noqa: E731
+    interior = c["interior_missed"] + c["interior_extra"]
+    return {"report_agreement": paired / float(max(den, 1)), "traces_exact": exact / float(max(len(tr), 1)),
+            "truth_reports": n_truth, "matched_reports": n_match, "paired": paired,
+            "interior_error_rate": interior / float(max(n_truth, 1)),
+            "errors": c,
+            "t0_abs_error_s": {"p50": q(dt0, 50), "p90": q(dt0, 90), "max": max(dt0) if dt0 else None},
+            "t1_abs_error_s": {"p50": q(dt1, 50), "p90": q(dt1, 90), "max": max(dt1) if dt1 else None},
+            "speed_rel_error": {"p50": q(dsp, 50), "p90": q(dsp, 90), "p99": q(dsp, 99),
+                                "within_1e-3": float(np.mean([x <= 1e-3 for x in dsp])) if dsp else None,
+                                "within_5pct": float(np.mean([x <= 0.05 for x in dsp])) if dsp else None}}
 
 
 def slice_batch(b, t0, t1):

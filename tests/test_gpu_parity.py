@@ -197,9 +197,9 @@ def test_index_hbm_budget(small_graph, oracle, results_equal, batch_path, monkey
     smaller radius, or left off; results stay identical to the oracle."""
     with Engine(graph_path=small_graph) as eng:
         full = eng.index_info()
-    # about a quarter of the full index's slot tables (~100 B per entry at the
-    # default 20 % load): the radius about halves
-    budget_mb = str(max(1, full["entries"] * 100 >> 22)) if expect == "shrunk" else "0"
+    # about a quarter of the full index's slot tables (~40 B per entry: 16-B
+    # slots at the default 40 % load): the radius about halves
+    budget_mb = str(max(1, full["entries"] * 40 >> 22)) if expect == "shrunk" else "0"
     monkeypatch.setenv("OTM_INDEX_BUDGET_MB", budget_mb)
     with Engine(graph_path=small_graph) as eng:
         info = eng.index_info()
@@ -418,43 +418,6 @@ def test_json_report_path_byte_equal(small_graph, oracle):
             assert seen[k] == got[k]
 
 
-@pytest.mark.parametrize("chunks", ["2", "4"])
-def test_json_report_pipelined_chunks(small_graph, oracle, monkeypatch, capfd, chunks):
-    """otm_report_batch as a pipeline of chunks on their own batch contexts
-    (abi.cpp report_many_pipelined, H2DOrder): the same bodies as one batch,
-    and the stderr speed lines in the same order."""
-    b = synth.make_traces(small_graph, 60, 40, seed=23)
-    off = b["trace_off"]
-    bodies = []
-    for t in range(60):
-        a, e = off[t], off[t + 1]
-        idx = np.arange(a, e)
-        tm = b["time"][a:e].astype(np.int64)
-        if t % 7 == 3:  # every 8th point, 5 s apart: speeds past 200 km/h (stderr lines)
-            idx = idx[::8]
-            tm = tm[0] + 5 * np.arange(len(idx), dtype=np.int64)
-        bodies.append(encode_request("veh%d" % t, b["lat"][idx], b["lon"][idx], tm,
-                                     b["accuracy"][idx].astype(np.int32)))
-    bodies[10] = b"{"  # a 400 among them
-    bodies[20] = bodies[20].replace(b'"trace":', b'"trace" :')  # a body for the host readers
-    monkeypatch.setenv("OTM_PIPE_MIN", str(1 << 30))
-    with Engine(graph_path=small_graph) as eng:
-        capfd.readouterr()
-        whole = eng.report_batch(bodies)
-        _, err_whole = capfd.readouterr()
-        monkeypatch.setenv("OTM_PIPE_MIN", "2")
-        monkeypatch.setenv("OTM_PIPE_CHUNKS", chunks)
-        piped = eng.report_batch(bodies)
-        _, err_piped = capfd.readouterr()
-        again = eng.report_batch(bodies)  # the pipeline's contexts reused
-        capfd.readouterr()
-    assert piped == whole and again == whole
-    assert err_piped == err_whole and "Speed exceeds 200kph" in err_whole
-    g = oracle.Graph(small_graph)
-    for body, got in zip(bodies, whole):
-        assert got == oracle.handle_request(g, body), body[:80]
-
-
 @pytest.mark.parametrize("form", ["8", "16", "64"])
 def test_viterbi_forms(small_graph, rural_graph, oracle, results_equal, monkeypatch, form):
     """K5's three forms (kernels.hip launch_viterbi: 8 or 16 lanes per trace,
@@ -591,3 +554,42 @@ def test_pinned_host_batch_copy_path(small_graph):
         finally:
             for p in keep:
                 L.otm_host_free(p)
+
+
+@pytest.mark.parametrize("size", ["small", "large"])
+def test_compact_host_batch(small_graph, oracle, results_equal, size):
+    """otm_match_compact (int32 time deltas, int16 accuracies, widened on the
+    device by k_expand_compact): the same results as otm_match_soa on the
+    widened batch, for the one-DMA small path and the large copy path (> 2^18
+    points), with empty and one-point traces and zero / negative / large
+    accuracies; and through a multi-device engine (widened on the host)."""
+    from reporter_amd.engine import compact_batch
+    n = 5000 if size == "large" else 300
+    b = synth.make_traces(small_graph, n, 60, seed=41)
+    lat, lon, tm, acc = (list(b[k]) for k in ("lat", "lon", "time", "accuracy"))
+    off = list(b["trace_off"])
+    for la, lo, t, a in [([], [], [], []), ([lat[0]], [lon[0]], [tm[0] + 7], [0.0]),
+                         ([lat[5], lat[6], lat[7]], [lon[5], lon[6], lon[7]], [tm[5], tm[5] + 4, tm[5] + 9],
+                          [-1.0, 500.0, 32767.0])]:
+        lat += la
+        lon += lo
+        tm += t
+        acc += a
+        off.append(off[-1] + len(la))
+    b = dict(trace_off=np.array(off, np.int64), lat=np.array(lat, np.float32), lon=np.array(lon, np.float32),
+             time=np.array(tm, np.float64), accuracy=np.array(acc, np.float32))
+    cb = compact_batch(b)
+    assert cb["time_delta"].dtype == np.int32 and cb["accuracy"].dtype == np.int16
+    keys = ("traces", "segments", "reports", "way_ids")
+    with Engine(graph_path=small_graph) as eng:
+        want = eng.match(b)
+        got = eng.match_compact(b)
+        assert [getattr(got, k).tobytes() for k in keys] == [getattr(want, k).tobytes() for k in keys]
+        npt.assert_array_equal(eng.debug("in_time")[:len(lat)], b["time"])
+        npt.assert_array_equal(eng.debug("in_acc")[:len(lat)], b["accuracy"])
+    if size == "small":
+        orc = oracle.match_batch(oracle.Graph(small_graph), b, nthreads=4)
+        results_equal(orc, want, "compact")
+        with Engine(graph_path=small_graph, devices=[0, 0]) as grp:
+            g = grp.match_compact(b)
+            assert [getattr(g, k).tobytes() for k in keys] == [getattr(want, k).tobytes() for k in keys]

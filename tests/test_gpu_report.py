@@ -383,3 +383,48 @@ def test_engine_on_device_1_json_and_async(small_graph):
         while len(polled) < len(tags):
             polled += e1.poll(4096, 2000000)
         assert sorted((t, c, s) for t, c, s in polled) == [(t, want[t][0], want[t][1]) for t in tags]
+
+
+@pytest.mark.parametrize("size", ["small", "pieces"])
+def test_request_arena_report_and_submit(small_graph, oracle, monkeypatch, size):
+    """Bodies written into a library-owned request arena
+    (otm_request_arena_alloc) go to HBM straight from it, through
+    otm_report_batch (direct pieces, cut at 16 MB: "pieces" spans more than
+    one) and otm_submit_batch (referenced, not copied): every response
+    byte-equal to the copied path's and to the oracle's, a malformed body and
+    a body for the host readers among them, and the arena reusable after."""
+    from reporter_amd import RequestArena, encode_request
+    n, pts = (60, 40) if size == "small" else (2600, 100)  # "pieces": ~17 MB of bodies
+    b = synth.make_traces(small_graph, n, pts, seed=97)
+    off = b["trace_off"]
+    bodies = [encode_request("veh%d" % t, b["lat"][off[t]:off[t + 1]], b["lon"][off[t]:off[t + 1]],
+                             b["time"][off[t]:off[t + 1]].astype(np.int64),
+                             b["accuracy"][off[t]:off[t + 1]].astype(np.int32)) for t in range(n)]
+    bodies[3] = b"{"
+    bodies[7] = bodies[7].replace(b'"trace":', b'"trace" :')
+    if size == "pieces":
+        assert sum(len(x) for x in bodies) > (16 << 20)
+    with Engine(graph_path=small_graph) as eng:
+        want = eng.report_batch(bodies)
+        with RequestArena(bodies) as ar:
+            assert eng.report_batch(ar) == want
+            assert eng.report_batch(ar) == want  # (reused)
+            tags = list(range(100, 100 + n))
+            eng.submit_batch(ar, tags)
+            polled = []
+            while len(polled) < n:
+                polled += eng.poll(4096, 2000000)
+        assert [t for t, _, _ in polled] == tags
+        assert [(c, r) for _, c, r in polled] == want
+        # a submission keeps its arena alive past the caller's release
+        ar2 = RequestArena(bodies[:50])
+        eng.submit_batch(ar2, list(range(50)))
+        ar2.release()
+        polled = []
+        while len(polled) < 50:
+            polled += eng.poll(4096, 2000000)
+        assert [(c, r) for _, c, r in polled] == want[:50]
+    if size == "small":
+        g = oracle.Graph(small_graph)
+        for body, got in zip(bodies, want):
+            assert got == oracle.handle_request(g, body), body[:60]

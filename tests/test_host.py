@@ -248,3 +248,22 @@ def test_arena_free_under_contention():
     assert lib().otm_debug_arena_stress(8, 200) == 0
     assert lib().otm_debug_arena_stress(3, 50) == 0
     assert lib().otm_debug_arena_stress(0, 1) == -1
+
+
+def test_request_arena_release_contract():
+    """otm_request_arena_release: NULL is a no-op, a pointer that is not an
+    arena is refused; otm_request_arena_alloc either gives page-locked memory
+    (a GPU box) or NULL with a message (no device here)."""
+    import ctypes as C
+    from reporter_amd._lib import last_error, lib
+    L = lib()
+    assert L.otm_request_arena_release(None) == 0
+    buf = C.create_string_buffer(64)
+    assert L.otm_request_arena_release(C.cast(buf, C.c_void_p)) < 0
+    p = L.otm_request_arena_alloc(1 << 16)
+    if p:
+        C.memset(p, 0x41, 1 << 16)
+        assert L.otm_request_arena_release(p) == 0
+        assert L.otm_request_arena_release(p) < 0  # (released once)
+    else:
+        assert "page-locked" in last_error()

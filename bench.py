@@ -340,6 +340,7 @@ def main():
     spill = eng.spill_stats()
     index = eng.index_info()
     index_levels = eng.index_levels()
+    index_tables = eng.index_tables()
     grid = eng.grid_info()
 
     # ---- host-inclusive leg (config 2 "via Java FFM host"): the binary C-ABI
@@ -827,6 +828,14 @@ def main():
                                       "reduce-scatter of %dx%d histograms per timed window" %
                                       (world, inflight, nseg, nbins)},
             "roofline": roof,
+            "route_index": {"radius_m": index["radius_m"], "entries": index["entries"],
+                            "near": index_levels, "table_bytes": index_tables["bytes"],
+                            "load_pct": index_tables["load_pct"],
+                            "bytes_per_entry": (index_tables["bytes"] /
+                                                float(max(index["entries"] + sum(x["entries"] for x in index_levels),
+                                                          1))),
+                            "budget_mb": os.environ.get("OTM_INDEX_BUDGET_MB"),
+                            "build_ms": index["build_ms"]},
             "kernel_ms": kern_avg,
             "stages": stages,
             "spill": spill,

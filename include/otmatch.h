@@ -358,11 +358,12 @@ int otm_hist_bind_ex(otm_engine* eng, void* dev_counts, int nbins, float bin_kph
 int otm_graph_info(const otm_engine* eng, int64_t* n_nodes, int64_t* n_edges,
                    int64_t* n_segments);
 
-/* The bounded distance index built at engine creation (config
+/* The bounded route index built at engine creation (config
  * "otm":{"index_radius_m": R}, 0 = none; absent: sized from the graph's node
  * density, ~140 nodes per row, capped at max_route_distance_factor x
- * breakage_distance, and shrunk to fit half the free HBM): for every node, all
- * nodes within R road metres with their distance and predecessor edge.
+ * breakage_distance, and shrunk to fit half the free HBM): for every search
+ * source (an edge's end entered along it, or a node), every label within R
+ * road metres with its cost, distance, turn units and predecessor.
  * Transition and route queries whose bound 5 x gc exceeds R, or whose row
  * overflowed the builder, run the online bounded search instead; the results
  * are identical either way. */
@@ -376,6 +377,13 @@ int otm_index_info(const otm_engine* eng, float* rmax, int64_t* entries,
  * tables; results are identical.  Writes up to `cap` radii (smallest first)
  * and entry counts; returns the number of near indexes, or < 0 on error. */
 int otm_index_levels(const otm_engine* eng, float* radii, int64_t* entries, int cap);
+
+/* The route index's device tables, full and near indexes together: hash
+ * slots and their bytes (16 B a slot, the label's predecessor inside), and
+ * the full index's table load in percent -- 30 when the tables fit half the
+ * free HBM (53 B per entry), else 40 (40 B per entry) before the radius is
+ * cut. */
+int otm_index_tables(const otm_engine* eng, int64_t* slots, int64_t* bytes, int32_t* load_pct);
 
 /* The candidate search's grid index on the device: the graph file's cells
  * (meili's 500 per 0.25 deg tile) merged mult x mult (config

@@ -1,6 +1,9 @@
 package org.opentraffic.reporter;
 
+import java.nio.ByteBuffer;
 import java.nio.charset.StandardCharsets;
+import java.util.ArrayList;
+import java.util.List;
 
 /**
  * JNI form of OtmMatcher for the reference's Java 8 target (pom.xml): HttpClient.POST's replacement at
@@ -19,6 +22,42 @@ public final class OtmJni {
 
   /** The /report call on request bytes: the response bytes, or null when the call fails. */
   private static native byte[] report(byte[] body);
+
+  /** A page-locked request arena of the library (otm_request_arena_alloc) as a direct buffer. */
+  private static native ByteBuffer arenaAlloc(long bytes);
+
+  private static native void arenaRelease(ByteBuffer arena);
+
+  /** otm_report_batch over body i = arena[off[i], off[i+1]); response bytes per body (null: failed). */
+  private static native byte[][] reportBatch(ByteBuffer arena, long[] off);
+
+  /**
+   * Many POSTs at once, one GPU batch: each body's ISO-8859-1 bytes (HttpClient.java:26) written into a
+   * request arena, sent to HBM from there; the responses read as UTF-8 (:33), null where the call failed.
+   */
+  public static List<String> POST_BATCH(String url, List<String> bodies) {
+    long total = 0;
+    for (String b : bodies) total += b.length();  // ISO-8859-1: one byte per char
+    List<String> out = new ArrayList<>(bodies.size());
+    ByteBuffer arena = arenaAlloc(total);
+    if (arena == null) {
+      for (String b : bodies) out.add(POST(url, b));
+      return out;
+    }
+    try {
+      long[] off = new long[bodies.size() + 1];
+      for (int i = 0; i < bodies.size(); ++i) {
+        arena.put(bodies.get(i).getBytes(StandardCharsets.ISO_8859_1));
+        off[i + 1] = arena.position();
+      }
+      byte[][] r = reportBatch(arena, off);
+      for (int i = 0; i < bodies.size(); ++i)
+        out.add(r == null || r[i] == null ? null : new String(r[i], StandardCharsets.UTF_8));
+    } finally {
+      arenaRelease(arena);
+    }
+    return out;
+  }
 
   /**
    * HttpClient.POST replacement: the response body, or null when the call fails.  The charset steps are

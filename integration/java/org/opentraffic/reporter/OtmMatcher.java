@@ -53,6 +53,20 @@ public final class OtmMatcher {
   private static final MethodHandle POLL = fn("otm_poll",
       FunctionDescriptor.of(ValueLayout.JAVA_INT, ValueLayout.ADDRESS, ValueLayout.ADDRESS, ValueLayout.JAVA_INT,
                             ValueLayout.JAVA_INT));
+  // int otm_report_batch(otm_engine*, int n, const char* const* reqs, const size_t* lens, char** resps,
+  //                      size_t* resp_lens, int* codes)
+  private static final MethodHandle REPORT_BATCH = fn("otm_report_batch",
+      FunctionDescriptor.of(ValueLayout.JAVA_INT, ValueLayout.ADDRESS, ValueLayout.JAVA_INT, ValueLayout.ADDRESS,
+                            ValueLayout.ADDRESS, ValueLayout.ADDRESS, ValueLayout.ADDRESS, ValueLayout.ADDRESS));
+  // int otm_submit_batch(otm_engine*, int n, const char* const* reqs, const size_t* lens, const uint64_t* tags)
+  private static final MethodHandle SUBMIT_BATCH = fn("otm_submit_batch",
+      FunctionDescriptor.of(ValueLayout.JAVA_INT, ValueLayout.ADDRESS, ValueLayout.JAVA_INT, ValueLayout.ADDRESS,
+                            ValueLayout.ADDRESS, ValueLayout.ADDRESS));
+  // void* otm_request_arena_alloc(size_t bytes); int otm_request_arena_release(void* arena)
+  private static final MethodHandle ARENA_ALLOC = fn("otm_request_arena_alloc",
+      FunctionDescriptor.of(ValueLayout.ADDRESS, ValueLayout.JAVA_LONG));
+  private static final MethodHandle ARENA_RELEASE = fn("otm_request_arena_release",
+      FunctionDescriptor.of(ValueLayout.JAVA_INT, ValueLayout.ADDRESS));
   // void otm_free(void*)
   private static final MethodHandle FREE = fn("otm_free", FunctionDescriptor.ofVoid(ValueLayout.ADDRESS));
   // const char* otm_last_error(const otm_engine*)
@@ -109,6 +123,85 @@ public final class OtmMatcher {
     } catch (Throwable t) {
       logger.error("otm_report failed for body " + body);
       return null;  // as HttpClient.POST on an exception (HttpClient.java:37-39)
+    }
+  }
+
+  /**
+   * Request bodies written straight into a library-owned page-locked request arena
+   * (otm_request_arena_alloc): the bytes new StringEntity(body) would send (ISO-8859-1, HttpClient.java:26)
+   * are encoded into the arena back to back, and otm_report_batch / otm_submit_batch send them to HBM from
+   * there -- no heap array, no staging copy in the library.
+   */
+  private static final class RequestArena implements AutoCloseable {
+    final MemorySegment base;
+    final MemorySegment ptrs, lens;
+    final int n;
+
+    RequestArena(List<String> bodies, Arena a) throws Throwable {
+      n = bodies.size();
+      long total = 0;
+      for (String b : bodies) total += b.length();  // ISO-8859-1: one byte per char ('?' above U+00FF)
+      MemorySegment p = (MemorySegment) ARENA_ALLOC.invokeExact(Math.max(total, 1L));
+      if (p.equals(MemorySegment.NULL)) throw new OutOfMemoryError("otm_request_arena_alloc");
+      base = p.reinterpret(Math.max(total, 1L));
+      ptrs = a.allocate(ValueLayout.ADDRESS, n);
+      lens = a.allocate(ValueLayout.JAVA_LONG, n);
+      long at = 0;
+      for (int i = 0; i < n; ++i) {
+        String b = bodies.get(i);
+        MemorySegment dst = base.asSlice(at, b.length());
+        for (int k = 0; k < b.length(); ++k) {
+          char ch = b.charAt(k);
+          dst.set(ValueLayout.JAVA_BYTE, k, (byte) (ch <= 0xFF ? ch : '?'));
+        }
+        ptrs.setAtIndex(ValueLayout.ADDRESS, i, dst);
+        lens.setAtIndex(ValueLayout.JAVA_LONG, i, b.length());
+        at += b.length();
+      }
+    }
+
+    @Override
+    public void close() throws Exception {
+      try {
+        int rc = (int) ARENA_RELEASE.invokeExact(base);
+      } catch (Throwable t) {
+        throw new Exception(t);
+      }
+    }
+  }
+
+  /**
+   * Many POSTs at once (the requests of one Kafka poll): the same contract as POST per body, in order, one
+   * GPU batch; the bodies go to the GPU from a request arena.  null entries where the call failed.
+   */
+  public static List<String> POST_BATCH(String url, List<String> bodies) {
+    List<String> out = new ArrayList<>();
+    try (Arena a = Arena.ofConfined(); RequestArena ra = new RequestArena(bodies, a)) {
+      int n = ra.n;
+      MemorySegment resps = a.allocate(ValueLayout.ADDRESS, n);
+      MemorySegment rlens = a.allocate(ValueLayout.JAVA_LONG, n);
+      MemorySegment codes = a.allocate(ValueLayout.JAVA_INT, n);
+      int rc = (int) REPORT_BATCH.invokeExact(ENGINE, n, ra.ptrs, ra.lens, resps, rlens, codes);
+      for (int i = 0; i < n; ++i)
+        out.add(rc != 0 ? null : takeBody(resps.getAtIndex(ValueLayout.ADDRESS, i), rlens.getAtIndex(ValueLayout.JAVA_LONG, i)));
+    } catch (Throwable t) {
+      logger.error("otm_report_batch failed");
+      while (out.size() < bodies.size()) out.add(null);
+    }
+    return out;
+  }
+
+  /**
+   * Queue many /report requests (results from poll() with these tags), straight from a request arena; the
+   * submission holds the arena until its results are back, so it is released here at once.
+   */
+  public static boolean submitBatch(List<String> bodies, long[] tags) {
+    try (Arena a = Arena.ofConfined(); RequestArena ra = new RequestArena(bodies, a)) {
+      MemorySegment tg = a.allocateFrom(ValueLayout.JAVA_LONG, tags);
+      return (int) SUBMIT_BATCH.invokeExact(ENGINE, ra.n, ra.ptrs, ra.lens, tg) == 0;
+    } catch (Throwable t) {
+      logger.error("otm_submit_batch failed");
+      return false;
     }
   }
 

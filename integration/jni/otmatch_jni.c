@@ -11,6 +11,7 @@
  *       otmatch_jni.c -L../../reporter_amd/lib -lotmatch -o libotmatch_jni.so
  */
 #include <jni.h>
+#include <stdlib.h>
 
 #include "otmatch.h"
 
@@ -43,6 +44,63 @@ JNIEXPORT jbyteArray JNICALL Java_org_opentraffic_reporter_OtmJni_report(JNIEnv*
   jbyteArray out = (*env)->NewByteArray(env, (jsize)rn);
   if (out) (*env)->SetByteArrayRegion(env, out, 0, (jsize)rn, (const jbyte*)resp);
   otm_free(resp);
+  return out;
+}
+
+/* OtmJni.arenaAlloc(long): a library-owned page-locked request arena (otm_request_arena_alloc) as a
+ * direct ByteBuffer the Java side writes its request bytes into. */
+JNIEXPORT jobject JNICALL Java_org_opentraffic_reporter_OtmJni_arenaAlloc(JNIEnv* env, jclass c, jlong bytes) {
+  (void)c;
+  void* p = otm_request_arena_alloc((size_t)(bytes > 0 ? bytes : 1));
+  return p ? (*env)->NewDirectByteBuffer(env, p, bytes > 0 ? bytes : 1) : NULL;
+}
+
+JNIEXPORT void JNICALL Java_org_opentraffic_reporter_OtmJni_arenaRelease(JNIEnv* env, jclass c, jobject arena) {
+  (void)c;
+  if (arena) otm_request_arena_release((*env)->GetDirectBufferAddress(env, arena));
+}
+
+/* OtmJni.reportBatch(ByteBuffer arena, long[] off): body i = arena[off[i], off[i+1]), sent to HBM straight
+ * from the arena by otm_report_batch; the response bytes back per body (null where the call failed). */
+JNIEXPORT jobjectArray JNICALL Java_org_opentraffic_reporter_OtmJni_reportBatch(JNIEnv* env, jclass c,
+                                                                              jobject arena, jlongArray off) {
+  (void)c;
+  if (!g_eng || !arena || !off) return NULL;
+  const char* base = (const char*)(*env)->GetDirectBufferAddress(env, arena);
+  const jsize n = (*env)->GetArrayLength(env, off) - 1;
+  if (!base || n < 0) return NULL;
+  jlong* o = (*env)->GetLongArrayElements(env, off, NULL);
+  const char** reqs = (const char**)malloc(sizeof(char*) * (size_t)(n ? n : 1));
+  size_t* lens = (size_t*)malloc(sizeof(size_t) * (size_t)(n ? n : 1));
+  char** resps = (char**)calloc((size_t)(n ? n : 1), sizeof(char*));
+  size_t* rlens = (size_t*)calloc((size_t)(n ? n : 1), sizeof(size_t));
+  int* codes = (int*)calloc((size_t)(n ? n : 1), sizeof(int));
+  jobjectArray out = NULL;
+  if (o && reqs && lens && resps && rlens && codes) {
+    for (jsize i = 0; i < n; ++i) {
+      reqs[i] = base + o[i];
+      lens[i] = (size_t)(o[i + 1] - o[i]);
+    }
+    const int rc = otm_report_batch(g_eng, (int)n, reqs, lens, resps, rlens, codes);
+    out = (*env)->NewObjectArray(env, n, (*env)->FindClass(env, "[B"), NULL);
+    for (jsize i = 0; out && i < n; ++i) {
+      if (rc == OTM_OK && resps[i]) {
+        jbyteArray b = (*env)->NewByteArray(env, (jsize)rlens[i]);
+        if (b) {
+          (*env)->SetByteArrayRegion(env, b, 0, (jsize)rlens[i], (const jbyte*)resps[i]);
+          (*env)->SetObjectArrayElement(env, out, i, b);
+          (*env)->DeleteLocalRef(env, b);
+        }
+      }
+      otm_free(resps[i]);
+    }
+  }
+  if (o) (*env)->ReleaseLongArrayElements(env, off, o, JNI_ABORT);
+  free(reqs);
+  free(lens);
+  free(resps);
+  free(rlens);
+  free(codes);
   return out;
 }
 

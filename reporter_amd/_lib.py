@@ -163,6 +163,7 @@ def _declare(L):
         "otm_index_info": (C.c_int, [vp, C.POINTER(C.c_float), C.POINTER(i64), C.POINTER(i32),
                                      C.POINTER(C.c_float)]),
         "otm_index_levels": (C.c_int, [vp, C.POINTER(C.c_float), C.POINTER(i64), C.c_int]),
+        "otm_index_tables": (C.c_int, [vp, C.POINTER(C.c_int64), C.POINTER(C.c_int64), C.POINTER(C.c_int32)]),
         "otm_grid_info": (C.c_int, [vp, C.POINTER(C.c_double), C.POINTER(i32), C.POINTER(i32), C.POINTER(i64),
                                     C.POINTER(i32)]),
         "otm_set_counting": (C.c_int, [vp, C.c_int]),
@@ -205,6 +206,8 @@ def _declare(L):
         "otm_runtime_info": (C.c_char_p, []),
     }
     for name, (res, args) in sig.items():
+        if os.environ.get("OTM_LIB") and not hasattr(L, name):
+            continue  # (an A/B build of an earlier library: its own entry points only)
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args

@@ -863,6 +863,10 @@ void report_many_device(otm_engine* E, int n, const char* const* reqs, const siz
   std::atomic<bool> oom{false};
   {
     std::lock_guard<std::mutex> lk(E->mu);
+    // an async worker's batch (ord): its copies on the batch stream (one
+    // stream per context, engine.h); a one-call batch: a copy stream, so each
+    // piece's read overlaps the next piece's copy
+    E->req_on_batch_stream = ord != nullptr;
     size_t bytes = 0;
     for (int k = 0; k < n; ++k) bytes += lens[k];
     int64_t* off = nullptr;
@@ -1906,6 +1910,16 @@ int otm_index_info(const otm_engine* E, float* rmax, int64_t* entries, int32_t* 
   if (entries) *entries = E->index_entries;
   if (incomplete_rows) *incomplete_rows = E->index_incomplete_rows;
   if (build_ms) *build_ms = E->index_build_ms;
+  return OTM_OK;
+}
+
+int otm_index_tables(const otm_engine* E, int64_t* slots, int64_t* bytes, int32_t* load_pct) {
+  if (!E) return fail(OTM_EINVAL, "engine is NULL");
+  if (!E->members.empty()) E = E->members[0];
+  const int64_t n = E->index_slots + E->index_near_slots;
+  if (slots) *slots = n;
+  if (bytes) *bytes = n * otm::IDX_SLOT_BYTES;
+  if (load_pct) *load_pct = E->idx.rmax > 0.0f ? E->idx.load_pct : 0;
   return OTM_OK;
 }
 

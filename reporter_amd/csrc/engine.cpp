@@ -351,6 +351,7 @@ int engine_clone(const otm_engine* P, otm_engine* C, std::string* err) {
   C->index_rmax = P->index_rmax;
   C->index_entries = P->index_entries;
   C->index_slots = P->index_slots;
+  C->index_near_slots = P->index_near_slots;
   C->index_incomplete_rows = P->index_incomplete_rows;
   C->index_build_ms = P->index_build_ms;
   C->small_points = P->small_points;
@@ -403,8 +404,10 @@ struct IndexBuilt {
   int64_t entries = 0, slots = 0;
   int32_t incomplete = 0;
 };
-// One index at radius *r: count, size + scan, insert.  With `shrink`, a radius
-// whose slot tables exceed `budget` is cut (rows shrink as R^2) and counted
+// One index at radius *r: count, size + scan, insert.  The tables take the
+// faster load (index_load_fast, 30 %) when they fit `budget`, else the denser
+// (index_load_dense, 40 %: 40 B per entry).  With `shrink`, a radius whose
+// dense tables still exceed `budget` is cut (rows shrink as R^2) and counted
 // again, down to 100 m (then no index: *r = 0); without, such an index is
 // left out (*r = 0).
 int build_index_at(otm_engine* E, float* r, bool shrink, size_t budget, IndexBuilt& out, std::string* err) {
@@ -421,13 +424,23 @@ int build_index_at(otm_engine* E, float* r, bool shrink, size_t budget, IndexBui
   void* tmp = nullptr;
   HIPCHK(hipMalloc(&tmp, tmpb));
   int64_t total = 0;
-  for (int attempt = 0;; ++attempt) {
-    launch_index_build(E->g, E->dp.turn_units, index_cost_bound(*r), row_cnt, nullptr, nullptr, false, s);
-    launch_row_sizes(row_cnt, row_off, N, s);
+  int pct = index_load_fast();
+  auto size_rows = [&](int load) -> int {
+    launch_row_sizes(row_cnt, row_off, N, load, s);
     scan_i64(row_off, N, tmp, tmpb, s);
     launch_row_pack(row_cnt, row_off, rows, N, s);
     HIPCHK(hipMemcpyAsync(&total, row_off + N, 8, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
+    return OTM_OK;
+  };
+  for (int attempt = 0;; ++attempt) {
+    launch_index_build(E->g, E->dp.turn_units, index_cost_bound(*r), row_cnt, nullptr, nullptr, false, s);
+    pct = index_load_fast();
+    if (size_rows(pct)) return OTM_EDEVICE;
+    if (((double)total + 1.0) * IDX_SLOT_BYTES > (double)budget) {
+      pct = index_load_dense();  // the same rows, denser tables
+      if (size_rows(pct)) return OTM_EDEVICE;
+    }
     const double need = ((double)total + 1.0) * IDX_SLOT_BYTES;
     if (need <= (double)budget) break;
     const float rr = (float)(std::floor(*r * std::sqrt((double)budget / need) * 0.9 / 50.0) * 50.0);
@@ -463,6 +476,7 @@ int build_index_at(otm_engine* E, float* r, bool shrink, size_t budget, IndexBui
   out.X.cmax = index_cost_bound(*r);
   out.X.row = rows;
   out.X.slot = (const uint4*)slot;
+  out.X.load_pct = pct;
   return OTM_OK;
 }
 
@@ -519,6 +533,7 @@ int build_index(otm_engine* E, std::string* err) {
     if (rc != OTM_OK) return rc;
     if (rn > 0.0f) {
       E->index_near_level_entries[nl] = near.entries;
+      E->index_near_slots += near.slots;
       E->idxn[nl++] = near.X;
     }
   }
@@ -1133,8 +1148,29 @@ static void read_requests(otm_engine* E, int32_t n, int32_t upto) {
 // The pieces go to HBM on a copy stream of their own, each followed by an
 // event that the batch stream waits on before it reads the piece's requests,
 // so one piece's read overlaps the next piece's copy.
+// With E->req_on_batch_stream (the async workers' contexts) the pieces go on
+// the batch stream itself, each read behind its copy: one stream, so one
+// hardware queue, per context (see otm_engine::req_on_batch_stream).
 int engine_push_requests(otm_engine* E, int32_t n, size_t bytes, size_t from, size_t to, const char* src,
                          int32_t upto, std::string* err) {
+  if (E->req_on_batch_stream) {
+    char* d = (char*)E->d_req.p;
+    const char* h = (const char*)E->h_req.p;
+    const size_t hdr = req_hdr_bytes(n);
+    const hipMemcpyKind h2d = hipMemcpyHostToDevice;
+    if (!src) {
+      const size_t a = from ? hdr + from : 0;
+      const size_t b = hdr + (to >= bytes ? bytes + REQ_PAD : to);
+      if (b > a) HIPCHK(big_copy(d + a, h + a, b - a, h2d, E->stream));
+    } else {
+      if (from == 0) HIPCHK(hipMemcpyAsync(d, h, hdr, h2d, E->stream));
+      if (to > from) HIPCHK(big_copy(d + hdr + from, src, to - from, h2d, E->stream));
+      if (to >= bytes) HIPCHK(hipMemsetAsync(d + hdr + bytes, 0, REQ_PAD, E->stream));
+    }
+    read_requests(E, n, upto < n ? upto : n);
+    HIPCHK(hipGetLastError());
+    return OTM_OK;
+  }
   if (!E->req_copy) HIPCHK(hipStreamCreateWithFlags(&E->req_copy, hipStreamNonBlocking));
   while (E->req_ev.size() < E->req_piece + 2) {  // [0]: the fence, [1 + p]: piece p
     hipEvent_t ev = nullptr;
@@ -1169,11 +1205,13 @@ int engine_push_requests(otm_engine* E, int32_t n, size_t bytes, size_t from, si
 }
 
 int engine_push_after(otm_engine* E, hipEvent_t ev) {
+  if (E->req_on_batch_stream) return hipStreamWaitEvent(E->stream, ev, 0) == hipSuccess ? OTM_OK : OTM_EDEVICE;
   if (!E->req_copy && hipStreamCreateWithFlags(&E->req_copy, hipStreamNonBlocking) != hipSuccess) return OTM_EDEVICE;
   return hipStreamWaitEvent(E->req_copy, ev, 0) == hipSuccess ? OTM_OK : OTM_EDEVICE;
 }
 
 int engine_push_mark(otm_engine* E, hipEvent_t ev) {
+  if (E->req_on_batch_stream) return hipEventRecord(ev, E->stream) == hipSuccess ? OTM_OK : OTM_EDEVICE;
   if (!E->req_copy && hipStreamCreateWithFlags(&E->req_copy, hipStreamNonBlocking) != hipSuccess) return OTM_EDEVICE;
   return hipEventRecord(ev, E->req_copy) == hipSuccess ? OTM_OK : OTM_EDEVICE;
 }

@@ -79,7 +79,8 @@ struct otm_engine {
   bool index_near_set = false;
   int64_t index_near_level_entries[otm::NEAR_LEVELS]{};
   int64_t index_entries = 0;
-  int64_t index_slots = 0;  // hash-table slots (16 B each + 4 B predecessor)
+  int64_t index_slots = 0;       // hash-table slots of the full index (16 B each, the predecessor inside)
+  int64_t index_near_slots = 0;  // ... of its near indexes
   int32_t index_incomplete_rows = 0;
   float index_build_ms = 0.0f;
   otm::MatchConfig mc;
@@ -139,6 +140,12 @@ struct otm_engine {
   Buf req_lat, req_lon, req_time, req_acc;  // the reader's sparse point slots (requests.hip)
   int32_t req_read = 0;                     // requests of the staged batch read so far
   hipStream_t req_copy = nullptr;           // the request pieces' H2D copies (created at first use)
+  // the request pieces' copies on the batch stream instead of req_copy: the
+  // async workers' contexts, so that three contexts hold three streams and
+  // never share one of the runtime's hardware queues (GPU_MAX_HW_QUEUES, 4),
+  // where a stream's wait on another batch's copies stalls every stream
+  // queued behind it
+  bool req_on_batch_stream = false;
   std::vector<hipEvent_t> req_ev;           // [0] the copies' fence, [1 + p]: piece p copied
   size_t req_piece = 0;                     // pieces of the staged batch pushed so far
   // response bodies written on the GPU (engine_write_responses): piece slots,

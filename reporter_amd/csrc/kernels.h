@@ -23,7 +23,11 @@
 namespace otm {
 
 constexpr int KMAX = 32;           // max candidates per column (== ORC_KMAX)
-constexpr int KIN = 8;             // inline candidate slots per point (DevWork::cand_eo / cand_em)
+// inline candidate slots per point (DevWork::cand_eo / cand_em); 4 (a point's
+// blocks half the size, slots 4.. in the overflow) measured slower on configs
+// 2 and 4
+constexpr int KIN = 8;
+static_assert(KIN == 4 || KIN == 8, "inline blocks of 4 or 8 slots (whole 16-B emission pieces)");
 constexpr int KX = KMAX - KIN;     // overflow candidate slots per point (DevWork::cand_xeo / cand_xem)
 constexpr int MAX_HITS = 256;      // distinct edges within one radius in the LDS tiers (beyond: the global tier)
 constexpr int SEARCH_LIMIT = 98304;  // labels (edges + nodes) of one global-tier search (beyond: the huge tier)
@@ -95,7 +99,7 @@ struct DevOrder {
 // holding every label of that search within cost cmax (1/64 m): the departure
 // label of each edge (key = edge id) and the arrival label of each node (key
 // = NODE_KEY | node), as one open-addressing hash table per row (linear
-// probing from 2-slot buckets, 40 % load).  A slot is 16 bytes, {key, cost,
+// probing from 2-slot buckets at 30 or 40 % load).  A slot is 16 bytes, {key, cost,
 // route distance bits, turn units} with the label's predecessor slot in the
 // cost's and units' top bytes (kernels.hip idx_slot_*): the route to the
 // edge's start turned into it (or to the node), so a transition reads its
@@ -111,7 +115,8 @@ struct DevIndex {
   float rmax;     // 0: no index
   uint32_t cmax;  // its cost bound, floor(rmax x 64)
   const IdxRow* row;   // [E + N]
-  const uint4* slot;    // 16 B per slot, ~40 B per entry
+  const uint4* slot;    // 16 B per slot: 53 B per entry at 30 % load, 40 B at 40 %
+  int load_pct;         // the tables' load
 };
 constexpr int IDX_SLOT_BYTES = 16;
 // the index radius is capped so that every cost in a slot is below 2^24 (1/64 m)
@@ -344,9 +349,11 @@ void launch_compact(int32_t n_traces, const DevOut& o, const int32_t* seg_off, c
 // row tables (slot array pre-filled with 0xFF)
 void launch_index_build(const DevGraph& g, const uint32_t* turn_units, uint32_t cmax, int32_t* row_cnt,
                         const IdxRow* rows, uint4* slot, bool write, hipStream_t s);
-// slots of a row of c entries (the index's load factor)
-int64_t index_row_cap(int32_t c);
-void launch_row_sizes(const int32_t* row_cnt, int64_t* row_sizes, int32_t n, hipStream_t s);
+// the route index's table loads (percent): the faster one, and the denser one
+// an index falls back to when the faster does not fit its HBM budget
+int index_load_fast();
+int index_load_dense();
+void launch_row_sizes(const int32_t* row_cnt, int64_t* row_sizes, int32_t n, int pct, hipStream_t s);
 struct BatchStatus {
   int32_t abort, grow;  // grow bit 0: the huge search tier needs (larger) tables; bit 1: the candidate HBM tier
   int64_t ttotal;

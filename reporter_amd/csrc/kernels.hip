@@ -558,11 +558,6 @@ constexpr int CAND_LANE_CAP = OTM_CAND_LANE_CAP;
 #define OTM_CAND_WAVES 8
 #endif
 constexpr int CAND_TB = OTM_CAND_TB;
-// lane tier: whole 64-B record and 32-B emission blocks per point (1), or only
-// the 16-B pieces that hold candidates (0)
-#ifndef OTM_CAND_WHOLE
-#define OTM_CAND_WHOLE 1
-#endif
 #ifndef OTM_CAND_INFL
 #define OTM_CAND_INFL 2
 #endif
@@ -740,18 +735,16 @@ __global__ __launch_bounds__(CAND_TB, OTM_CAND_WAVES) void k_cand_lane(DevGraph 
         E[j * S] = em;
       }
     }
-    // the K chosen, in order, out as whole blocks: the point's 64-B record
-    // block in four 16-B stores, its 32-B emission block in two (unused
-    // slots: edge -1, emission +inf) -- whole lines to write back, not
-    // partially written ones
-    static_assert(CAND_LANE_CAP <= KIN, "the lane tier's candidates fit the inline slots");
+    // the K chosen, in order: the point's inline blocks whole (its 8-B
+    // records in 16-B stores, its emissions in 16-B pieces; unused slots: edge
+    // -1, emission +inf) -- whole lines to write back, not partially written
+    // ones -- and any candidates past KIN one by one into its overflow slots
     int4* eo4 = (int4*)(w.cand_eo + p * KIN);
     float4* em4 = (float4*)(w.cand_em + p * KIN);
     float emv[4];
 #pragma unroll
-    for (int j = 0; j < KIN; j += 2) {
-      // OTM_CAND_WHOLE = 0: only the 16-B pieces holding candidates (the A/B)
-      if (!OTM_CAND_WHOLE && j >= K && !((j & 3) == 2 && j - 2 < K)) break;
+    for (int j = 0; j < (CAND_LANE_CAP > KIN ? CAND_LANE_CAP : KIN); j += 2) {
+      if (j >= KIN && j >= K) break;
       int32_t e2[2];
       float o2[2];
 #pragma unroll
@@ -771,8 +764,17 @@ __global__ __launch_bounds__(CAND_TB, OTM_CAND_WAVES) void k_cand_lane(DevGraph 
         }
         emv[(j + u) & 3] = emj;
       }
-      if (OTM_CAND_WHOLE || j < K) eo4[j >> 1] = make_int4(e2[0], __float_as_int(o2[0]), e2[1], __float_as_int(o2[1]));
-      if ((j & 3) == 2) em4[j >> 2] = make_float4(emv[0], emv[1], emv[2], emv[3]);
+      if (j < KIN) {
+        eo4[j >> 1] = make_int4(e2[0], __float_as_int(o2[0]), e2[1], __float_as_int(o2[1]));
+        if ((j & 3) == 2) em4[j >> 2] = make_float4(emv[0], emv[1], emv[2], emv[3]);
+      } else {
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+          if (j + u < K) {
+            w.cand_xeo[p * KX + (j + u - KIN)] = make_int2(e2[u], __float_as_int(o2[u]));
+            w.cand_xem[p * KX + (j + u - KIN)] = emv[(j + u) & 3];
+          }
+      }
     }
 
     w.ncand[p] = K;
@@ -1347,20 +1349,22 @@ __device__ __forceinline__ uint32_t idx_hash(uint32_t v) {
   return v;
 }
 
-// A row's table: entries x 100 / OTM_IDX_LOAD_PCT slots rounded up to an even
-// count (at least one slot empty, so every probe ends), the hash mapped onto
-// its 2-slot buckets by a multiply-high.  A label's probe starts at its
-// bucket's first slot and goes on linearly; a lookup loads the bucket's two
-// slots (32 aligned bytes, one line) at once, which at this load holds the
-// label or ends the probe for nearly every lookup.  A slot is 16 bytes with
-// the predecessor inside (idx_slot_*): 16 x 100 / 40 = 40 B per entry
-// (round 4: 20 % load, 20-B slots, 100 B per entry).
-#ifndef OTM_IDX_LOAD_PCT
-#define OTM_IDX_LOAD_PCT 40
-#endif
-__host__ __device__ __forceinline__ int64_t idx_row_cap(int32_t c) {
+// A row's table: entries x 100 / pct slots rounded up to an even count (at
+// least one slot empty, so every probe ends), the hash mapped onto its 2-slot
+// buckets by a multiply-high.  A label's probe starts at its bucket's first
+// slot and goes on linearly; a lookup loads the bucket's two slots (32 aligned
+// bytes, one line) at once, which holds the label or ends the probe for most
+// lookups.  A slot is 16 bytes with the predecessor inside (idx_slot_*).  The
+// engine picks pct per index (engine.cpp build_index_at): IDX_LOAD_FAST (30 %,
+// 53 B per entry) when the tables fit the HBM budget, IDX_LOAD_DENSE (40 %,
+// 40 B per entry) when only that fits -- measured on configs 2 / 4 / 3,
+// k_trans_sub at 40 % is 9 / 6 / 7 % slower than at 30 % (more lookups past
+// their bucket), round 4's 20-B slots at 20 % (100 B per entry) 1 / 2 / 1 %
+// faster.
+constexpr int IDX_LOAD_FAST = 30, IDX_LOAD_DENSE = 40;
+__host__ __device__ __forceinline__ int64_t idx_row_cap(int32_t c, int pct) {
   if (c <= 0) return 0;
-  int64_t cap = ((int64_t)c * 100 + OTM_IDX_LOAD_PCT - 1) / OTM_IDX_LOAD_PCT;
+  int64_t cap = ((int64_t)c * 100 + pct - 1) / pct;
   if (cap <= c) cap = (int64_t)c + 1;
   return (cap + 1) & ~(int64_t)1;
 }
@@ -1377,7 +1381,7 @@ __device__ __forceinline__ uint32_t idx_next(uint32_t h, const IdxRow& R) {
 // the row split over the two top bytes (IDX_NO_PRED: the route's first edge).
 constexpr uint32_t IDX_LOW24 = 0xFFFFFFu;
 constexpr uint32_t IDX_NO_PRED = 0xFFFFu;
-static_assert((int64_t)INDEX_BUILD_LIMIT * 100 / OTM_IDX_LOAD_PCT + 2 < (int64_t)IDX_NO_PRED,
+static_assert((int64_t)INDEX_BUILD_LIMIT * 100 / IDX_LOAD_FAST + 2 < (int64_t)IDX_NO_PRED,
               "a row's slots must be numbered in 16 bits");
 __host__ __device__ __forceinline__ uint32_t idx_slot_cost(const uint4& s) { return s.y & IDX_LOW24; }
 __host__ __device__ __forceinline__ uint32_t idx_slot_units(const uint4& s) { return s.w & IDX_LOW24; }
@@ -1490,10 +1494,10 @@ __global__ __launch_bounds__(TB) void k_index_build(DevGraph g, const uint32_t* 
   }
 }
 
-// table capacity of a row (idx_row_cap)
-__global__ void k_row_sizes(const int32_t* row_cnt, int64_t* sizes, int32_t n) {
+// table capacity of a row (idx_row_cap at load pct)
+__global__ void k_row_sizes(const int32_t* row_cnt, int64_t* sizes, int32_t n, int pct) {
   const int32_t u = blockIdx.x * blockDim.x + threadIdx.x;
-  if (u < n) sizes[u] = idx_row_cap(row_cnt[u]);
+  if (u < n) sizes[u] = idx_row_cap(row_cnt[u], pct);
   if (u == n) sizes[n] = 0;
 }
 
@@ -2342,10 +2346,10 @@ __global__ __launch_bounds__(TB, OTM_VIT_WAVES) void k_viterbi(DevBatch b, DevWo
             if (kq > 0) {
               const float4* e4 = (const float4*)(w.cand_em + (a + q) * KIN);
               const float4 x0 = e4[0];
-              const float4 x1 = kq > 4 ? e4[1] : x0;
+              const float4 x1 = KIN > 4 && kq > 4 ? e4[KIN > 4 ? 1 : 0] : x0;
               const float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
 #pragma unroll
-              for (int u = 0; u < 8; ++u)
+              for (int u = 0; u < KIN; ++u)
                 if (u < kq) sEm[eq + u] = v[u];
             }
             for (int j0 = KIN; __ballot(j0 < kq) != 0ull; j0 += 4) {
@@ -2501,10 +2505,12 @@ __global__ __launch_bounds__(TB, G == 8 ? OTM_VG8_WAVES : 3) void k_viterbi_g(De
   // spill snapshot B (see k_viterbi)
   if (OTM_FOLD_BOOKKEEPING && snap && blockIdx.x == 0 && threadIdx.x == 0) fold_snap(w, 1, true);
   if (*w.abort) return;
-  // (group rows padded by one word: the groups' same offsets on different banks;
-  // unpadded, 44 % of the LDS cycles were bank conflicts, config 2)
-  __shared__ float sT[NT][VT + 1];
-  __shared__ float sE[NT][CH * G + 1];  // [point of the chunk][state]
+  // group rows padded by G words: group g's row starts g x G banks on, so the
+  // wave's 64 lanes staging (or reading) the same offset j of their groups'
+  // rows hit 64 different banks (round 4's one-word pad put group g + 1's
+  // j on group g's j + 1: 39 % of the LDS cycles were bank conflicts, config 4)
+  __shared__ float sT[NT][VT + G];
+  __shared__ float sE[NT][CH * G + G];  // [point of the chunk][state]
   // backpointers, a nibble per state (15: dead), two states a byte: [point * G / 2 + state / 2]
   __shared__ uint8_t sBp[NT][VG_PTS * G / 2 + 4];
   __shared__ uint8_t sFl[NT][VG_PTS];  // flags; after the walk: VG_CS | (state + 1) << 3
@@ -4144,10 +4150,11 @@ void launch_index_build(const DevGraph& g, const uint32_t* turn_units, uint32_t 
   else
     hipLaunchKernelGGL(k_index_build<false>, dim3(grid), dim3(TB), 0, s, g, turn_units, cmax, row_cnt, rows, slot);
 }
-int64_t index_row_cap(int32_t c) { return idx_row_cap(c); }
-void launch_row_sizes(const int32_t* row_cnt, int64_t* row_sizes, int32_t n, hipStream_t s) {
+int index_load_fast() { return IDX_LOAD_FAST; }
+int index_load_dense() { return IDX_LOAD_DENSE; }
+void launch_row_sizes(const int32_t* row_cnt, int64_t* row_sizes, int32_t n, int pct, hipStream_t s) {
   hipLaunchKernelGGL(k_row_sizes, dim3(grid_for((int64_t)n + 1, 256, 1 << 30)), dim3(256), 0, s, row_cnt, row_sizes,
-                     n);
+                     n, pct);
 }
 void launch_row_pack(const int32_t* row_cnt, const int64_t* row_off, IdxRow* rows, int32_t n, hipStream_t s) {
   hipLaunchKernelGGL(k_row_pack, dim3(grid_for((int64_t)n, 256, 1 << 30)), dim3(256), 0, s, row_cnt, row_off, rows, n);

@@ -340,6 +340,13 @@ class Engine(object):
             raise OtmError("otm_index_levels failed: %s" % _lib.last_error())
         return [{"radius_m": r[i], "entries": e[i]} for i in range(min(n, 8))]
 
+    def index_tables(self):
+        """The route index's device tables (full + near): {"slots", "bytes",
+        "load_pct"} (otm_index_tables)."""
+        n, b, p = C.c_int64(), C.c_int64(), C.c_int32()
+        _check(lib().otm_index_tables(self.h, C.byref(n), C.byref(b), C.byref(p)))
+        return {"slots": n.value, "bytes": b.value, "load_pct": p.value}
+
     def grid_info(self):
         cd, r, c, n, m = C.c_double(), C.c_int32(), C.c_int32(), C.c_int64(), C.c_int32()
         _check(lib().otm_grid_info(self.h, C.byref(cd), C.byref(r), C.byref(c), C.byref(n), C.byref(m)))

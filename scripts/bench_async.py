@@ -32,11 +32,16 @@ def main():
                                      b["accuracy"][a:e].astype(np.int32)))
     arr = (C.c_char_p * nb)(*bodies)
     lens = (C.c_size_t * nb)(*[len(x) for x in bodies])
+    arena = None
+    if os.environ.get("ARENA", "1") == "1":  # the bodies in a request arena (otm_request_arena_alloc)
+        from reporter_amd import RequestArena
+        arena = RequestArena(bodies)
+        arr, lens = arena.ptrs, arena.lens
     tags = [(C.c_uint64 * nb)(*range(r * nb, (r + 1) * nb)) for r in range(rounds)]
     rdt = np.dtype([("tag", "<u8"), ("code", "<i4"), ("pad", "<i4"), ("body", "<u8"), ("len", "<u8")])
     cap = 1 << 16
     rbuf = (_lib.Result * cap)()
-    out = {"env": {k: os.environ.get(k) for k in ("OTM_ASYNC_WORKERS", "OTM_ASYNC_BATCH", "OTM_HOST_THREADS")}}
+    out = {"env": {k: os.environ.get(k) for k in ("OTM_ASYNC_WORKERS", "OTM_ASYNC_BATCH", "OTM_HOST_THREADS", "ARENA")}}
     with Engine(graph_path=graph) as eng:
         def run():
             parts, got = [], 0

@@ -79,3 +79,36 @@ def test_config4_state_graph(oracle, results_equal):
         assert eng.index_info()["radius_m"] >= 5000.0
         sp = eng.spill_stats()
         assert sp["trans_online"] == 0 and sp["route_online"] == 0, sp
+
+
+@pytest.mark.parametrize("budget", ["dense", "shrunk"])
+def test_config3_shard_index_budget(oracle, results_equal, monkeypatch, budget):
+    """Config 3's shard under an HBM budget the fast route index (30 % load,
+    53 B per entry) does not fit: "dense" leaves room for the 40 % tables (40 B
+    per entry) at the full radius, "shrunk" for neither, so the radius is cut
+    and the columns past it go to the online search tiers.  Bit-identical to
+    the oracle either way."""
+    graph = synth.cached_graph(3)
+    tr = dict(synth.CONFIGS[3]["traces"])
+    ids = synth.shard_vehicle_ids(tr["n_vehicles"] // 8, 0, 8)[:40000]  # 4M points of the shard
+    tr["n_vehicles"] = len(ids)
+    b = synth.make_traces(graph, vehicle_ids=ids, **tr)
+    with Engine(graph_path=graph) as eng:
+        full = dict(eng.index_info(), **eng.index_tables())
+    assert full["load_pct"] == 30
+    # the full index's tables take ~53 B per entry at 30 % load, ~40 B at 40 %
+    per_entry = 46 if budget == "dense" else 20
+    monkeypatch.setenv("OTM_INDEX_BUDGET_MB", str(full["entries"] * per_entry >> 20))
+    with Engine(graph_path=graph) as eng:
+        info = dict(eng.index_info(), **eng.index_tables())
+        assert info["load_pct"] == 40
+        if budget == "dense":
+            assert info["radius_m"] == full["radius_m"] and info["entries"] == full["entries"]
+            assert info["bytes"] < full["bytes"]
+        else:
+            assert 100.0 <= info["radius_m"] < full["radius_m"]
+        res = eng.match(b)
+        sp = eng.spill_stats()
+        if budget == "shrunk":
+            assert sp["trans_online"] > 0 and sp["route_online"] > 0, sp
+        _check_vs_oracle(oracle, results_equal, graph, b, res)

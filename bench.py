@@ -413,8 +413,14 @@ def main():
             if _lib.lib().otm_match_compact(engines[i].h, C.byref(hcb), C.byref(outs[i])) != 0:
                 raise RuntimeError("otm_match_compact: %s" % _lib.last_error())
 
-        hel_c = run_leg(compact_step)
-        hel_s = run_leg(soa_step)
+        # the two legs alternate (soa, compact, soa, compact), each timed
+        # over host_steps, so neither gains from running second
+        runs_s, runs_c = [], []
+        for _ in range(2):
+            runs_s.append(run_leg(soa_step))
+            runs_c.append(run_leg(compact_step))
+        hel_c = sum(runs_c) / len(runs_c)
+        hel_s = sum(runs_s) / len(runs_s)
         for p_ in pinned:
             L.otm_host_free(p_)
         in_c = sum(np.asarray(v).nbytes for v in cb.values()) / P
@@ -422,11 +428,13 @@ def main():
                     "steps": host_steps, "batches_in_flight": inflight,
                     "host_buffers": "pageable" if args.host_pageable else "page-locked (otm_host_alloc)",
                     "input_bytes_per_point": round(in_c, 2),
+                    "ms_per_step_runs": [x * 1e3 / host_steps for x in runs_c],
                     "includes": "otm_match_compact from the host arrays in the Java host's own types (float lat/lon, "
                                 "int32 time delta from a per-trace int64 base, int16 accuracy): H2D of the inputs, "
                                 "their widening on the device, all kernels, result compaction, D2H of traces / "
                                 "segments / reports / way ids into pinned host buffers; JSON not included",
                     "soa": {"value": P * host_steps / hel_s, "ms_per_step": hel_s * 1e3 / host_steps,
+                            "ms_per_step_runs": [x * 1e3 / host_steps for x in runs_s],
                             "input_bytes_per_point": 24.0 + 8.0 * (nt_ + 1) / P,
                             "includes": "the same through otm_match_soa (double time, float accuracy)"}}
         hist.zero_()

@@ -148,13 +148,9 @@ class HostPool {
   size_t nthreads_ = 0;
 };
 
-bool host_pool() {
-  const char* v = std::getenv("OTM_HOST_POOL");
-  return !(v && *v == '0');
-}
 
 // fn(a, e) over [0, n) in contiguous chunks, one per thread (the caller's the
-// first); on the persistent pool unless OTM_HOST_POOL=0 (threads per call)
+// first); on the persistent pool
 template <class F>
 void par_for(size_t n, F fn) {
   const size_t T = host_threads(n);
@@ -162,43 +158,10 @@ void par_for(size_t n, F fn) {
     fn((size_t)0, n);
     return;
   }
-  if (host_pool()) {
-    const std::function<void(size_t, size_t)> f = std::ref(fn);
-    HostPool::get().run(n, T, f);
-    return;
-  }
-  const size_t per = (n + T - 1) / T;
-  std::vector<std::thread> th;
-  std::vector<std::exception_ptr> errs(T);
-  for (size_t i = 1; i < T; ++i) {
-    const size_t a = i * per, e = std::min(n, a + per);
-    if (a >= e) continue;
-    try {
-      // an exception in a worker is carried back to the caller, not terminate()
-      th.emplace_back([&fn, &errs, i, a, e] {
-        try {
-          fn(a, e);
-        } catch (...) {
-          errs[i] = std::current_exception();
-        }
-      });
-    } catch (...) {
-      fn(a, e);  // no thread to be had: this chunk on the caller
-    }
-  }
-  try {
-    fn((size_t)0, std::min(n, per));
-  } catch (...) {
-    errs[0] = std::current_exception();
-  }
-  for (auto& t : th) t.join();
-  for (auto& x : errs)
-    if (x) std::rethrow_exception(x);  // to the entry point's guard
+  const std::function<void(size_t, size_t)> f = std::ref(fn);
+  HostPool::get().run(n, T, f);
 }
 
-#ifndef OTM_JSON_SCRATCH
-#define OTM_JSON_SCRATCH 1
-#endif
 // the Java request bytes read without a DOM (otm::fast_request); OTM_FAST_JSON=0
 // sends every body through the DOM (A/B and the parity tests)
 bool fast_requests() {
@@ -206,10 +169,6 @@ bool fast_requests() {
   return !(v && *v == '0');
 }
 
-bool pack_reuse() {
-  const char* v = std::getenv("OTM_PACK_REUSE");
-  return !(v && *v == '0');
-}
 
 char* dup_out(const std::string& s, size_t* n) {
   char* p = (char*)std::malloc(s.size() + 1);
@@ -258,11 +217,10 @@ bool fill_device_params(otm_engine* E, std::string* err) {
   E->dp.max_search_radius = m.max_search_radius;
   E->dp.gps_accuracy = m.gps_accuracy;
   E->dp.max_candidates = m.max_candidates;
-  // spatial work order per kernel (bit 0 candidates, 1 transitions, 2 route)
-  const char* om = std::getenv("OTM_ORDER_MASK");
-  // default: all three (measured on config 2: candidates 0.60 -> 0.44 ms,
-  // route 0.107 -> 0.089, transitions 0.408 -> 0.388)
-  E->dp.order_mask = om ? (int)std::strtol(om, nullptr, 0) : otm::ORDER_CAND | otm::ORDER_TRANS | otm::ORDER_ROUTE;
+  // the spatial work order in all three kernels that walk it (measured on
+  // config 2: candidates 0.60 -> 0.44 ms, route 0.107 -> 0.089, transitions
+  // 0.408 -> 0.388)
+  E->dp.order_mask = otm::ORDER_CAND | otm::ORDER_TRANS | otm::ORDER_ROUTE;
   E->dp.cand_wave_all = 0;
   // batches under this many points take the small-batch (latency) path
   const char* sp = std::getenv("OTM_SMALL_POINTS");
@@ -369,12 +327,12 @@ void run_requests(otm_engine* E, std::vector<Req>& rq, std::vector<int>& codes, 
   const size_t np = (size_t)off.back();
   // the batch arrays: per calling thread, kept between calls (grown, never
   // shrunk) -- fresh ones cost ~3 ms of page faults to fill and ~2.5 ms to
-  // unmap per 1M points; OTM_PACK_REUSE=0 allocates them per call
+  // unmap per 1M points
   thread_local std::vector<float> keep_lat, keep_lon, keep_acc;
   thread_local std::vector<double> keep_tm;
   std::vector<float> own_lat, own_lon, own_acc;
   std::vector<double> own_tm;
-  const bool reuse = pack_reuse();
+  constexpr bool reuse = true;
   std::vector<float>& lat = reuse ? keep_lat : own_lat;
   std::vector<float>& lon = reuse ? keep_lon : own_lon;
   std::vector<float>& acc = reuse ? keep_acc : own_acc;
@@ -444,17 +402,12 @@ void run_requests(otm_engine* E, std::vector<Req>& rq, std::vector<int>& codes, 
               bodies[(size_t)k] = std::move(out);
             }
           } else {
-#if OTM_JSON_SCRATCH
             // written into a per-thread buffer that keeps its capacity, then
             // copied once at its final size (no growth reallocations per body)
             thread_local std::string scratch;
             scratch.clear();
             codes[(size_t)k] = otm::write_report_response(r, (int32_t)n, &scratch);
             bodies[(size_t)k].assign(scratch);
-#else
-            codes[(size_t)k] = otm::write_report_response(r, (int32_t)n, &out);
-            bodies[(size_t)k] = std::move(out);
-#endif
           }
         }
       });
@@ -1088,15 +1041,6 @@ int async_workers(const otm_engine* E) {
   return e ? std::max(1, std::min(8, std::atoi(e))) : 3;
 }
 
-// The workers' request copies in take order (H2DOrder; OTM_ASYNC_ORDER=0:
-// each as soon as its worker stages it, the A/B)
-bool async_ordered() {
-  static const bool on = [] {
-    const char* v = std::getenv("OTM_ASYNC_ORDER");
-    return !(v && *v == '0');
-  }();
-  return on;
-}
 
 // Worker wi of the async pipeline: take the next batch (in submit order, a
 // ticket each), run it whole on its own context -- parse, GPU, responses --
@@ -1140,7 +1084,7 @@ void worker_loop(otm_engine* E, int wi) {
     const double tw0 = now_ms();
     try {
       report_many(ctx, n, reqs.data(), lens.data(), codes.data(), resps.data(), rl.data(), pin.data(),
-                  async_ordered() ? &E->aorder : nullptr, seq);
+                  &E->aorder, seq);  // (copies in take order, H2DOrder)
     } catch (...) {
       // out of host memory (report_many freed what it made): the batch's
       // requests complete with a null body and code 500
@@ -1413,7 +1357,6 @@ static int otm_engine_create_impl(const char* cfg_path, const int* devices, int 
   }
   const Value* tl = o->get("trans_lanes");
   if (tl && tl->kind == Kind::Int) E->trans_lanes = (int)tl->i;
-  if (const char* v = std::getenv("OTM_TRANS_SUB")) E->trans_lanes = std::atoi(v);  // A/B override
   if (E->trans_lanes != 8 && E->trans_lanes != 16) {
     delete E;
     return fail(OTM_EINVAL, "trans_lanes must be 8 or 16");

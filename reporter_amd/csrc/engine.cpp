@@ -64,12 +64,9 @@ static T* P(otm_engine::Buf& b) {
 // otm_match_device batches (their caller drives the GPU from its own threads:
 // measured 1.27 vs 1.25G points/s on the bench's device leg, while the host
 // leg went 0.57 -> 0.80G and the async JSON path 170 -> 221M with blocking
-// waits).  OTM_BLOCKING_SYNC=0 spins always.
+// waits).
 static hipError_t wait_batch(otm_engine* E, hipStream_t s, int64_t points) {
-  static const int64_t min_pts = [] {
-    const char* v = std::getenv("OTM_BLOCKING_SYNC");
-    return v && *v == '0' ? INT64_MAX : (int64_t)65536;
-  }();
+  constexpr int64_t min_pts = 65536;
   if (points < min_pts || E->spin_waits) return hipStreamSynchronize(s);
   if (!E->sync_ev) {
     const hipError_t e = hipEventCreateWithFlags(&E->sync_ev, hipEventBlockingSync | hipEventDisableTiming);
@@ -309,28 +306,11 @@ int engine_init(otm_engine* E, const char* graph_path, int device, std::string* 
   return build_index(E, err);
 }
 
-// The stream of batch context `slot` (0: the engine, k: its k-th clone).
-// OTM_STREAM_PRIO="hi,lo,..." gives the contexts HIP stream priorities (hi =
-// greatest, lo = least, or an integer), so that batches in flight drift out of
-// phase: the prioritised one finishes its kernels first and copies while the
-// others compute (an A/B knob; default: every stream at normal priority).
+// The stream of batch context `slot` (0: the engine, k: its k-th clone), at
+// normal priority (round 2: a prioritised context made the device leg slower,
+// 0.78 -> 0.90-1.12 ms per step)
 int create_stream(int slot, hipStream_t* s) {
-  const char* v = std::getenv("OTM_STREAM_PRIO");
-  if (v && *v) {
-    std::string list(v);
-    std::string item;
-    for (int k = 0; k <= slot; ++k) {
-      const size_t c = list.find(',');
-      item = list.substr(0, c);
-      list = c == std::string::npos ? std::string() : list.substr(c + 1);
-    }
-    if (!item.empty()) {
-      int least = 0, greatest = 0;
-      if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) return 1;
-      const int pr = item == "hi" ? greatest : item == "lo" ? least : std::atoi(item.c_str());
-      return hipStreamCreateWithPriority(s, hipStreamNonBlocking, pr) != hipSuccess;
-    }
-  }
+  (void)slot;
   return hipStreamCreateWithFlags(s, hipStreamNonBlocking) != hipSuccess;
 }
 
@@ -407,9 +387,9 @@ struct IndexBuilt {
 // One index at radius *r: count, size + scan, insert.  The tables take the
 // faster load (index_load_fast, 30 %) when they fit `budget`, else the denser
 // (index_load_dense, 40 %: 40 B per entry).  With `shrink`, a radius whose
-// dense tables still exceed `budget` is cut (rows shrink as R^2) and counted
-// again, down to 100 m (then no index: *r = 0); without, such an index is
-// left out (*r = 0).
+// dense tables still exceed `budget` is cut (rows shrink as R^2; the tables
+// stay dense) and counted again, down to 100 m (then no index: *r = 0);
+// without, such an index is left out (*r = 0).
 int build_index_at(otm_engine* E, float* r, bool shrink, size_t budget, IndexBuilt& out, std::string* err) {
   out = IndexBuilt{};
   const int32_t N = E->g.n_edges + E->g.n_nodes;  // rows
@@ -435,10 +415,11 @@ int build_index_at(otm_engine* E, float* r, bool shrink, size_t budget, IndexBui
   };
   for (int attempt = 0;; ++attempt) {
     launch_index_build(E->g, E->dp.turn_units, index_cost_bound(*r), row_cnt, nullptr, nullptr, false, s);
-    pct = index_load_fast();
     if (size_rows(pct)) return OTM_EDEVICE;
-    if (((double)total + 1.0) * IDX_SLOT_BYTES > (double)budget) {
-      pct = index_load_dense();  // the same rows, denser tables
+    if (pct != index_load_dense() && ((double)total + 1.0) * IDX_SLOT_BYTES > (double)budget) {
+      // the same rows, denser tables -- and denser from here on: a radius
+      // cut below costs the online tiers far more than the denser probes
+      pct = index_load_dense();
       if (size_rows(pct)) return OTM_EDEVICE;
     }
     const double need = ((double)total + 1.0) * IDX_SLOT_BYTES;
@@ -727,11 +708,10 @@ static int engine_match_once(otm_engine* E, const DevBatch& b, hipStream_t s, st
   w.kq_prev = P<int32_t>(E->kq_prev);
   w.vmeta = P<uint8_t>(E->vmeta);
   {
-    // ordered column records for K4 (OTM_TRANS_COLREC=0: the per-point arrays)
-    static const char* ce = std::getenv("OTM_TRANS_COLREC");
-    const bool on = !ce || std::atoi(ce) != 0;
-    w.colrec = on ? P<int4>(E->colrec) : nullptr;
-    w.colrec_pos = on ? P<int32_t>(E->colrec_pos) : nullptr;
+    // ordered column records for K4 (spatial-order batches; the others read
+    // the per-point arrays)
+    w.colrec = P<int4>(E->colrec);
+    w.colrec_pos = P<int32_t>(E->colrec_pos);
   }
   w.trans_off = P<int64_t>(E->trans_off);
   w.bp = P<uint8_t>(E->bp);

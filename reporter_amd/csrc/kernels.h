@@ -144,7 +144,7 @@ constexpr int INDEX_BUILD_LIMIT = 1536; // labels per row before the row is left
 // cost bound (1/64 m) of a search bounded by B metres (oracle cost_bound)
 __host__ __device__ inline uint32_t index_cost_bound(float B) { return (uint32_t)floor((double)B * 64.0); }
 
-// which kernels walk the spatial work order (env OTM_ORDER_MASK)
+// which kernels walk the spatial work order (DevParams::order_mask: all three)
 constexpr int ORDER_CAND = 1, ORDER_TRANS = 2, ORDER_ROUTE = 4;
 constexpr int TURN_TABLE = 181;                 // turn units per deviation 0..180 degrees
 constexpr uint32_t TURN_UNITS_MAX = 0xFFFFFFu;   // 2^24 - 1: a route's units sum exact in a float

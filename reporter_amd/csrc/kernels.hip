@@ -76,41 +76,10 @@ __device__ __forceinline__ float seg_sqdist(float alat, float alon, float blat, 
   return px * px + py * py;
 }
 
-// seg_sqdist for the lane tier's scan, with a division-free early out: a
-// segment whose whole line lies farther than the radius (cross(a, v)^2 >
-// r2m x |v|^2, r2m = r^2 x 1.001) is a miss, reported as +inf; any other is
-// seg_sqdist's exact value (same operations).  The 0.1 % margin is far above
-// the few-ulp rounding of the cross product and of seg_sqdist itself, so a
-// segment the test drops is one seg_sqdist would have put beyond r^2 too.
-// Measured slower (round 4, bit-identical: k_cand_lane 0.229 vs 0.221 ms on
-// config 2, 1.89 vs 1.85 on config 4; profiles/r04_ab/cand_line/): the
-// branch splits the wave where the division did not; off by default.
-#ifndef OTM_CAND_LINE_TEST
-#define OTM_CAND_LINE_TEST 0
-#endif
-__device__ __forceinline__ float seg_sqdist_r(float alat, float alon, float blat, float blon, float lat, float lon,
-                                              float ls, float r2m) {
-  const float ax = (alon - lon) * ls;
-  const float ay = (alat - lat) * MPD_F;
-  const float bx = (blon - lon) * ls;
-  const float by = (blat - lat) * MPD_F;
-  const float vx = bx - ax;
-  const float vy = by - ay;
-  const float l2 = vx * vx + vy * vy;
-  if (OTM_CAND_LINE_TEST) {
-    const float cr = ax * vy - ay * vx;
-    if (cr * cr > r2m * l2) return INFINITY;
-  }
-  float t = 0.0f;
-  if (l2 > 0.0f) {
-    const float dot = ax * vx + ay * vy;
-    t = -dot / l2;
-    t = t < 0.0f ? 0.0f : (t > 1.0f ? 1.0f : t);
-  }
-  const float px = ax + t * vx;
-  const float py = ay + t * vy;
-  return px * px + py * py;
-}
+// (round 4 A/B, not kept: a division-free early out in the lane tier's scan
+// for segments whose whole line lies beyond the radius measured slower --
+// k_cand_lane 0.229 vs 0.221 ms on config 2, 1.89 vs 1.85 on config 4; the
+// branch splits the wave where the division did not)
 
 __device__ __forceinline__ void project(const DevGraph& g, int32_t e, int32_t k, float lat, float lon, float ls,
                                         float& sqd, float& off_out, bool& at_end) {
@@ -605,7 +574,6 @@ __global__ __launch_bounds__(CAND_TB, OTM_CAND_WAVES) void k_cand_lane(DevGraph 
     const float lat = pr.x, lon = pr.y;
     const float r = probe_radius(P, pr.z);
     const float r2 = r * r;
-    const float r2m = r2 * 1.001f;  // (seg_sqdist_r's early-out margin)
     const float ls = MPD_F * cos_deg(lat);
     const float dlat = r / MPD_F;
     const float dlon = r / ls;
@@ -644,7 +612,7 @@ __global__ __launch_bounds__(CAND_TB, OTM_CAND_WAVES) void k_cand_lane(DevGraph 
             if (q + u < q1) {
               const float4 G = g.ent_geo[q + u];
               en[u] = g.cell_ent[q + u];
-              sq[u] = seg_sqdist_r(G.x, G.y, G.z, G.w, lat, lon, ls, r2m);
+              sq[u] = seg_sqdist(G.x, G.y, G.z, G.w, lat, lon, ls);
             }
           }
 #pragma unroll
@@ -4023,11 +3991,9 @@ void launch_transitions(const DevGraph& g, const DevBatch& b, const DevParams& p
   // many more waves than fit at once (each column is a few dependent
   // round trips): measured 0.78 ms at 16K waves, 0.67 ms at 64K; a grid of
   // one resident round was slowest (0.92 ms, partial rounds at 7 waves/SIMD)
-  static const char* genv = std::getenv("OTM_TRANS_GRID");
   // sub: lanes per column (engine trans_lanes)
   const int per = TB / sub;  // columns per wave step
-  const int grid = genv ? std::max(ORDER_GROUPS, std::atoi(genv) / ORDER_GROUPS * ORDER_GROUPS)
-                        : order_grid((b.n_points + per - 1) / per, 1, TRANS_GRID_CAP);
+  const int grid = order_grid((b.n_points + per - 1) / per, 1, TRANS_GRID_CAP);
   if (sub == 8) {
     // 8 lanes per column over the columns of <= OTM_TRANS_KC8 candidates a
     // side, then 16 lanes over the wide rest (a list filled on the device)
@@ -4045,8 +4011,8 @@ void launch_transitions(const DevGraph& g, const DevBatch& b, const DevParams& p
   mk.end(KN_TRANS_GLOBAL, s);
 }
 void launch_viterbi(const DevBatch& b, DevWork& w, hipStream_t s, const Marks& mk) {
-  // the form: OTM_VIT_FORM (8, 16 or 64) for A/B; by default the grouped
-  // forms from OTM_VIT_G_MIN traces up (default 32768), the wave form below:
+  // the form: OTM_VIT_FORM (8, 16 or 64) for the tests; by default the
+  // grouped forms from 32,768 traces up, the wave form below:
   // a small batch's waves all fit the GPU at once, so its time is one wave's
   // (~100 steps of a latency-bound chain either way), while a large batch's
   // is wave rounds, which 8 traces per wave divide (round-4 A/B,
@@ -4054,9 +4020,8 @@ void launch_viterbi(const DevBatch& b, DevWork& w, hipStream_t s, const Marks& m
   // config 4 1.13 vs 0.73)
   // (read per batch: tests switch them)
   const char* fe = std::getenv("OTM_VIT_FORM");
-  const char* ge = std::getenv("OTM_VIT_G_MIN");
   const int forced = fe ? std::atoi(fe) : 0;
-  const int gmin = ge ? std::atoi(ge) : 32768;
+  constexpr int gmin = 32768;
   const int form = forced ? forced : (b.n_traces >= gmin ? 8 : 64);
   if (form == 64) {
     TIMED(KN_VITERBI, hipLaunchKernelGGL(k_viterbi, dim3(grid_for(b.n_traces, 1, WAVE_GRID_CAP)), dim3(TB), 0, s, b,
@@ -4127,12 +4092,9 @@ void launch_compact(int32_t n_traces, const DevOut& o, const int32_t* seg_off, c
 void launch_report(const DevBatch& b, const DevReportCfg& rc, DevWork& w, DevOut& o, hipStream_t s,
                    const Marks& mk) {
   // thread per trace; the serial segment walk is latency-bound, so small
-  // blocks spread the traces over more waves (env OTM_REPORT_TB)
-  static const int tb = [] {
-    const char* e = std::getenv("OTM_REPORT_TB");
-    const int v = e ? std::atoi(e) : 8;  // 0.053 -> 0.050 ms against 64 on config 2
-    return v == 16 || v == 32 || v == 64 || v == 128 ? v : 16;
-  }();
+  // blocks spread the traces over more waves (0.053 -> 0.050 ms against 64 on
+  // config 2)
+  constexpr int tb = 16;
   if (OTM_REPORT_FORM == 1 || (OTM_REPORT_FORM == 2 && b.n_traces <= REPW_MAX_TRACES))
     TIMED(KN_REPORT, hipLaunchKernelGGL(k_report_wave, dim3(grid_for(b.n_traces, 1, WAVE_GRID_CAP)), dim3(TB), 0, s,
                                         b, rc, w, o, 0));

@@ -19,15 +19,6 @@ done
 for v in default r04 load30; do
   OTM_LIB=$(lib $v) timeout -k 10 400 python -u bench.py --config 3 --steps 5 --warmup 2 $FAST > $O/c3_$v.json 2> $O/c3_$v.err
 done
-# the async pipeline: request copies on the batch stream (default) or a copy
-# stream per context (OTM_ASYNC_STREAMS=2), bodies in a request arena or copied
-timeout -k 10 300 python -u -m pytest tests/test_gpu_report.py -m gpu -x -q --timeout 120 --timeout-method thread \
-  > $O/pytest_report.log 2>&1
-for rep in 1 2; do
-  for st in 1 2; do
-    for ar in 1 0; do
-      OTM_ASYNC_STREAMS=$st ARENA=$ar OTM_JSON_PROFILE=1 timeout -k 10 200 python -u scripts/bench_async.py \
-        > $O/async_s${st}_a${ar}_$rep.json 2> $O/async_s${st}_a${ar}_$rep.err
-    done
-  done
-done
+# (round 5 also ran the async pipeline here with its request copies on the
+# batch stream or on a copy stream per context, bodies in a request arena or
+# copied: no setting won every run, one stream per context kept)

@@ -111,6 +111,8 @@ def parse():
                     help="route index radius in metres (default: the engine sizes it from the graph; 0: no index)")
     ap.add_argument("--inflight", type=int, default=3,
                     help="batches in flight per GPU: engine clones on their own HIP streams, one host thread each")
+    ap.add_argument("--host-inflight", type=int, default=4,
+                    help="batches in flight in the host-inclusive legs (their PCIe copies leave room for a fourth)")
     return ap.parse_args()
 
 
@@ -379,13 +381,15 @@ def main():
         hc = host_buffers(cb)
         hcb = _lib.BatchCompact(nt_, P, hc["trace_off"], hc["time_base"], hc["lat"], hc["lon"], hc["time_delta"],
                                 hc["accuracy"])
-        outs = [_lib.Results() for _ in engines]
+        hinf = max(1, args.host_inflight)
+        hengines = engines[:hinf] + [eng.clone() for _ in range(hinf - len(engines))]
+        outs = [_lib.Results() for _ in hengines]
 
         def run_leg(call):
-            for i in range(inflight):
+            for i in range(hinf):
                 call(i)
             hticket = itertools.count()
-            hgate = threading.Barrier(inflight + 1)
+            hgate = threading.Barrier(hinf + 1)
 
             def hworker(i):
                 hgate.wait()
@@ -394,7 +398,7 @@ def main():
                 while next(hticket) < host_steps:
                     call(i)
 
-            hthreads = [threading.Thread(target=hworker, args=(i,)) for i in range(inflight)]
+            hthreads = [threading.Thread(target=hworker, args=(i,)) for i in range(hinf)]
             for t in hthreads:
                 t.start()
             torch.cuda.synchronize(dev)
@@ -406,11 +410,11 @@ def main():
             return time.perf_counter() - th0
 
         def soa_step(i):
-            if _lib.lib().otm_match_soa(engines[i].h, C.byref(hb), C.byref(outs[i])) != 0:
+            if _lib.lib().otm_match_soa(hengines[i].h, C.byref(hb), C.byref(outs[i])) != 0:
                 raise RuntimeError("otm_match_soa: %s" % _lib.last_error())
 
         def compact_step(i):
-            if _lib.lib().otm_match_compact(engines[i].h, C.byref(hcb), C.byref(outs[i])) != 0:
+            if _lib.lib().otm_match_compact(hengines[i].h, C.byref(hcb), C.byref(outs[i])) != 0:
                 raise RuntimeError("otm_match_compact: %s" % _lib.last_error())
 
         # the two legs alternate (soa, compact, soa, compact), each timed
@@ -423,9 +427,11 @@ def main():
         hel_s = sum(runs_s) / len(runs_s)
         for p_ in pinned:
             L.otm_host_free(p_)
+        for e_ in hengines[len(engines):]:
+            e_.close()
         in_c = sum(np.asarray(v).nbytes for v in cb.values()) / P
         host_leg = {"value": P * host_steps / hel_c, "unit": "points/s", "ms_per_step": hel_c * 1e3 / host_steps,
-                    "steps": host_steps, "batches_in_flight": inflight,
+                    "steps": host_steps, "batches_in_flight": hinf,
                     "host_buffers": "pageable" if args.host_pageable else "page-locked (otm_host_alloc)",
                     "input_bytes_per_point": round(in_c, 2),
                     "ms_per_step_runs": [x * 1e3 / host_steps for x in runs_c],

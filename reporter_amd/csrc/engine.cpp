@@ -575,6 +575,25 @@ void engine_free(otm_engine* E) {
   E->stream = nullptr;
 }
 
+// The growth cap of an on-demand tier (log2 of its table slots): the
+// kernels.h default, or lower by env (a test hook)
+static int max_log2(const char* env, int dflt) {
+  const char* v = std::getenv(env);
+  return v ? std::min(dflt, std::atoi(v)) : dflt;
+}
+
+// The candidate HBM tier's tables (kernels.h CAND_BIG_SLOTS): none until a
+// probe outgrows the LDS tier; k_candidates<true> clears them per probe.
+static int ensure_cand(otm_engine* E, std::string* err) {
+  if (E->cand_log2 <= 0) return OTM_OK;
+  const size_t n = (size_t)CAND_BIG_SLOTS << E->cand_log2;
+  int rc;
+  if ((rc = ensure(E->cbig_key, n * 4, err))) return rc;
+  if ((rc = ensure(E->cbig_val, n * 8, err))) return rc;
+  if ((rc = ensure(E->cbig_skey, n / 2 * 8, err))) return rc;
+  return OTM_OK;
+}
+
 // The huge search tier's tables (kernels.h HUGE_SLOTS): none until a search
 // outgrows the global tier; then 2^huge_log2 slots each, grown 4x and the batch
 // redone whenever a search does not fit (engine_match).
@@ -757,12 +776,8 @@ static int engine_match_once(otm_engine* E, const DevBatch& b, hipStream_t s, st
     mk.begin(KN_ORDER, s);
     mk.end(KN_ORDER, s);
   }
-  if (E->cand_log2 > 0) {  // k_candidates<true> clears its tables per probe
-    const size_t n = (size_t)CAND_BIG_SLOTS << E->cand_log2;
-    if ((rc = ensure(E->cbig_key, n * 4, err))) return rc;
-    if ((rc = ensure(E->cbig_val, n * 8, err))) return rc;
-    if ((rc = ensure(E->cbig_skey, n / 2 * 8, err))) return rc;
-  }
+  if ((rc = ensure_cand(E, err))) return rc;
+  w.cand_final = E->cand_final;
   w.cbig_key = P<uint32_t>(E->cbig_key);
   w.cbig_val = P<unsigned long long>(E->cbig_val);
   w.cbig_skey = P<unsigned long long>(E->cbig_skey);
@@ -795,6 +810,7 @@ static int engine_match_once(otm_engine* E, const DevBatch& b, hipStream_t s, st
   w.huge_ins = P<uint32_t>(E->huge_ins);
   w.huge_prev = P<int32_t>(E->huge_prev);
   w.huge_log2 = E->huge_log2;
+  w.huge_final = E->huge_final;
   launch_transitions(E->g, b, dp, w, s, mk, E->trans_lanes);
   // spill snapshot B: columns per transition tier (Viterbi does not touch
   // the counters; they start over for the route tiers)
@@ -878,23 +894,30 @@ int engine_match(otm_engine* E, const DevBatch& b, hipStream_t s, std::string* e
     }
     if (ttotal > E->trans_cap) E->trans_cap = ttotal + ttotal / 4 + 4096;
     if (st.grow & 1) {
-      // a search outgrew the huge tier's tables (or found none): 4x the slots
+      // a search outgrew the huge tier's tables (or found none): 4x the slots,
+      // or, past the cap or out of HBM, the overflowing traces fail alone
       const int32_t next = E->huge_log2 ? E->huge_log2 + 2 : 19;
-      if (next > 29) {
-        *err = "a route search outgrew 2^29 table slots";
-        return OTM_EDEVICE;
-      }
+      const int32_t prev = E->huge_log2;
       E->huge_log2 = next;
+      if (next > max_log2("OTM_HUGE_MAX_LOG2", HUGE_MAX_LOG2) || ensure_huge(E, err) != OTM_OK) {
+        E->huge_log2 = prev;
+        E->huge_final = 1;
+        E->huge_ready_log2 = 0;  // (a buffer regrown before the failure: cleared again)
+        err->clear();
+      }
     }
     if (st.grow & 2) {
       // a probe had more distinct edges in its radius than the candidate
-      // HBM tier's tables hold (or there were none): 4x the slots
+      // HBM tier's tables hold (or there were none): 4x the slots, or the
+      // overflowing traces fail alone
       const int32_t next = E->cand_log2 ? E->cand_log2 + 2 : 13;
-      if (next > 25) {
-        *err = "a candidate search outgrew 2^25 table slots";
-        return OTM_EDEVICE;
-      }
+      const int32_t prev = E->cand_log2;
       E->cand_log2 = next;
+      if (next > max_log2("OTM_CAND_MAX_LOG2", CAND_MAX_LOG2) || ensure_cand(E, err) != OTM_OK) {
+        E->cand_log2 = prev;
+        E->cand_final = 1;
+        err->clear();
+      }
     }
     if (cnt[2]) E->pool_cap = (int32_t)std::min<size_t>((size_t)cnt[1] * 2 + 1024, (size_t)INT32_MAX / 2);
   }
@@ -1017,16 +1040,18 @@ int engine_match_compact(otm_engine* E, const otm_batch_compact* in, std::string
   int rc;
   const size_t b_off = ((size_t)NT + 1) * 8, b_base = (size_t)NT * 8, b_pt = (size_t)NP * 4,
                b_acc = ((size_t)NP * 2 + 7) & ~(size_t)7;
-  // device: [offsets | time bases | lat | lon | time deltas | accuracies], then
-  // the widened time and accuracy arrays
-  const size_t total = b_off + b_base + 3 * b_pt + b_acc;
+  // device: [offsets | time bases | lat | lon | time deltas | accuracies], each
+  // section 256-B aligned (the runtime's copy kernels take an unaligned
+  // destination on a slower path), then the widened time and accuracy arrays
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  const size_t o_base = al(b_off), o_lat = al(o_base + b_base), o_lon = al(o_lat + b_pt), o_dt = al(o_lon + b_pt),
+               o_acc = al(o_dt + b_pt);
+  const size_t total = o_acc + b_acc;
   if ((rc = ensure(E->in_blob, total, err))) return rc;
   if ((rc = ensure(E->in_time, (size_t)NP * 8 + 8, err))) return rc;
   if ((rc = ensure(E->in_acc, (size_t)NP * 4 + 8, err))) return rc;
   hipStream_t s = E->stream;
   char* d = (char*)E->in_blob.p;
-  const size_t o_base = b_off, o_lat = o_base + b_base, o_lon = o_lat + b_pt, o_dt = o_lon + b_pt,
-               o_acc = o_dt + b_pt;
   if (NP <= (int64_t)1 << 18) {
     // small batches: one host copy into pinned staging, then ONE DMA
     if ((rc = ensure_pinned(E->h_in, total, err))) return rc;

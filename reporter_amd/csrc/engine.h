@@ -105,6 +105,7 @@ struct otm_engine {
   int32_t huge_ready_log2 = 0;  // the layout the huge tables were last cleared for
   Buf cbig_key, cbig_val, cbig_skey;
   int32_t cand_log2 = 0;  // candidate HBM tier: 2^cand_log2 slots per table (0: none yet; grown on demand)
+  int32_t huge_final = 0, cand_final = 0;  // the tier's tables cannot grow: overflows fail their traces
   int32_t last_attempts = 0;  // runs of the last batch (otm_spill_stats::attempts)
   Buf ord_tile, ord_cnt, ord_cursor, ord_grp, ord_item;  // spatial work order
   Buf abort_flag;                                       // capacity overflow of the batch in flight

@@ -47,6 +47,12 @@ constexpr int HUGE_SLOTS = 8;
 // distinct edges within their radius, CAND_BIG_SLOTS at a time, in tables of
 // 2^cand_log2 slots (half of them the sort keys) sized like the huge tier.
 constexpr int CAND_BIG_SLOTS = 64;
+// the largest tables the host grows the two on-demand tiers to (8 x 2^27 huge
+// slots ~ 29 GB, 64 x 2^23 candidate slots ~ 8.6 GB; env OTM_HUGE_MAX_LOG2 /
+// OTM_CAND_MAX_LOG2 lower them, test hooks): past them, or when HBM runs out,
+// a search or probe that does not fit fails its own trace with a 500, not
+// the batch
+constexpr int HUGE_MAX_LOG2 = 27, CAND_MAX_LOG2 = 23;
 __host__ __device__ inline int huge_limit(int log2) { return log2 > 2 ? 3 << (log2 - 2) : 0; }  // 0.75 x slots
 
 struct DevGraph {
@@ -250,11 +256,13 @@ struct DevWork {
   uint32_t* huge_ins;      // [HUGE_SLOTS * huge_limit(huge_log2)]
   int32_t* huge_prev;      // [HUGE_SLOTS]
   int32_t huge_log2;
+  int32_t huge_final;      // the huge tables cannot grow: an overflowing search fails its trace (500)
   // candidate HBM tier ([CAND_BIG_SLOTS << cand_log2] slots; cand_log2 == 0: none yet)
   uint32_t* cbig_key;
   unsigned long long* cbig_val;
   unsigned long long* cbig_skey;  // [CAND_BIG_SLOTS << (cand_log2 - 1)]
   int32_t cand_log2;
+  int32_t cand_final;      // the candidate tables cannot grow: an overflowing probe fails its trace (500)
   int32_t* overflow_list3; // [P] searches the global tier spilled (counts: [21] transitions, [22] route)
   DevCounters* ctr;        // nullptr when counting is off
 };

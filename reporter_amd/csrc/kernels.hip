@@ -801,9 +801,14 @@ __global__ __launch_bounds__(TB) void k_candidates(DevGraph g, DevBatch b, DevPa
   const int lane = threadIdx.x;
   const int64_t nwork = BIG ? w.counters_i32[24] : w.counters_i32[5];
   const int32_t* list = BIG ? w.overflow_list3 : w.overflow_list0;
-  if (BIG && nwork > 0 && w.cand_log2 == 0) {  // no tables yet: the host makes them, redoes the batch
-    for (int64_t it = (int64_t)blockIdx.x * TB + lane; it < nwork; it += (int64_t)gridDim.x * TB) w.ncand[list[it]] = 0;
-    if (blockIdx.x == 0 && lane == 0) {
+  if (BIG && nwork > 0 && w.cand_log2 == 0) {
+    // no tables yet: the host makes them and redoes the batch -- or, when it
+    // cannot (cand_final), these probes' traces answer 500 (OTM_TERR_CAND_OVERFLOW)
+    for (int64_t it = (int64_t)blockIdx.x * TB + lane; it < nwork; it += (int64_t)gridDim.x * TB) {
+      w.ncand[list[it]] = 0;
+      if (w.cand_final) atomicCAS(&w.trace_err[w.pt_trace[list[it]]], 0, OTM_TERR_CAND_OVERFLOW);
+    }
+    if (!w.cand_final && blockIdx.x == 0 && lane == 0) {
       w.counters_i32[25] = 1;
       *w.abort = 1;
     }
@@ -906,6 +911,11 @@ __global__ __launch_bounds__(TB) void k_candidates(DevGraph g, DevBatch b, DevPa
       if (lane == 0) {
         if (!BIG) {
           w.overflow_list3[atomicAdd(&w.counters_i32[24], 1)] = (int32_t)p;  // to the HBM tables
+        } else if (w.cand_final) {
+          // the tables are as large as they get: this probe's trace fails
+          // alone (500, OTM_TERR_CAND_OVERFLOW), the batch goes on
+          w.ncand[p] = 0;
+          atomicCAS(&w.trace_err[w.pt_trace[p]], 0, OTM_TERR_CAND_OVERFLOW);
         } else {
           w.ncand[p] = 0;
           w.counters_i32[25] = 1;  // the tables are too small: grow, redo the batch
@@ -1869,14 +1879,28 @@ __device__ __forceinline__ Table tier_table(const DevWork& w, uint32_t* lkey, un
   return Table{lkey, llab, linq, lfr0, lfr1, 8, LDS_TABLE_LIMIT};
 }
 // the huge tier has work but no tables yet: the host allocates them and
-// redoes the batch (returns true: the launch is done)
-__device__ __forceinline__ bool huge_unready(DevWork& w, int64_t nwork) {
+// redoes the batch -- or, when it cannot (huge_final), the listed columns'
+// traces answer 500 (OTM_TERR_SEARCH_OVERFLOW) (returns true: the launch is done)
+__device__ __forceinline__ bool huge_unready(DevWork& w, int64_t nwork, const int32_t* list) {
   if (nwork <= 0 || w.huge_log2 > 0) return false;
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
+  if (w.huge_final) {
+    for (int64_t it = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; it < nwork; it += (int64_t)gridDim.x * blockDim.x)
+      atomicCAS(&w.trace_err[w.pt_trace[list[it]]], 0, OTM_TERR_SEARCH_OVERFLOW);
+  } else if (blockIdx.x == 0 && threadIdx.x == 0) {
     w.counters_i32[23] = 1;
     *w.abort = 1;
   }
   return true;
+}
+// a huge-tier search that outgrew its table: the host grows the tables and
+// redoes the batch, or (huge_final) the column's trace answers 500
+__device__ __forceinline__ void huge_overflow(DevWork& w, int64_t p) {
+  if (w.huge_final) {
+    atomicCAS(&w.trace_err[w.pt_trace[p]], 0, OTM_TERR_SEARCH_OVERFLOW);
+  } else {
+    w.counters_i32[23] = 1;  // the huge tables are too small: grow, redo
+    *w.abort = 1;
+  }
 }
 
 // TIER 0: LDS tables; 1: global tables (BIG_SLOTS x BIG_TABLE_CAP); 2: the
@@ -1906,7 +1930,7 @@ __global__ __launch_bounds__(TB) void k_transitions(DevGraph g, DevBatch b, DevP
   const int32_t* list = TIER == 2 ? w.overflow_list3 : (BIG ? w.overflow_list2 : w.overflow_list0);
   const int64_t nwork = TIER == 2 ? (int64_t)w.counters_i32[21]
                                   : (BIG ? (int64_t)w.counters_i32[3] : (int64_t)w.counters_i32[4]);
-  if (TIER == 2 && huge_unready(w, nwork)) return;
+  if (TIER == 2 && huge_unready(w, nwork, list)) return;
   __syncthreads();
   for (int64_t it = blockIdx.x; it < nwork; it += gridDim.x) {
     const int64_t p = (int64_t)list[it];
@@ -2007,8 +2031,7 @@ __global__ __launch_bounds__(TB) void k_transitions(DevGraph g, DevBatch b, DevP
       } else if (TIER == 1) {
         w.overflow_list3[atomicAdd(&w.counters_i32[21], 1)] = (int32_t)p;
       } else {
-        w.counters_i32[23] = 1;  // the huge tables are too small: grow, redo
-        *w.abort = 1;
+        huge_overflow(w, p);
       }
     }
     __syncthreads();
@@ -2771,7 +2794,7 @@ __global__ __launch_bounds__(TB) void k_route(DevGraph g, DevBatch b, DevParams 
   const int32_t* list = TIER == 2 ? w.overflow_list3 : (BIG ? w.overflow_list2 : w.overflow_list0);
   const int64_t nwork = TIER == 2 ? (int64_t)w.counters_i32[22]
                                   : (BIG ? (int64_t)w.counters_i32[3] : (int64_t)w.counters_i32[4]);
-  if (TIER == 2 && huge_unready(w, nwork)) return;
+  if (TIER == 2 && huge_unready(w, nwork, list)) return;
   __syncthreads();
   for (int64_t it = blockIdx.x; it < nwork; it += gridDim.x) {
     const int64_t p = (int64_t)list[it];
@@ -2795,8 +2818,7 @@ __global__ __launch_bounds__(TB) void k_route(DevGraph g, DevBatch b, DevParams 
         } else if (TIER == 1) {
           w.overflow_list3[atomicAdd(&w.counters_i32[22], 1)] = (int32_t)p;
         } else {
-          w.counters_i32[23] = 1;  // the huge tables are too small: grow, redo
-          *w.abort = 1;
+          huge_overflow(w, p);
         }
       }
       __syncthreads();
@@ -3809,62 +3831,61 @@ __global__ __launch_bounds__(TB) void k_compact(int32_t n_traces, DevOut o, cons
   }
 }
 
-// One block of 1024 threads: each thread sums a contiguous chunk of the
-// three count arrays, a block scan gives its chunk's bases, then the chunk's
-// exclusive offsets are written; totals at o*[n].
+// One block of 1024 threads: the three count arrays' exclusive scans, totals
+// at o*[n].  (Round 4's form summed a contiguous chunk per thread: strided,
+// uncoalesced loads, ~90 us per 10k traces with other batches in flight.)
 __global__ __launch_bounds__(1024) void k_fetch_scan(int32_t n, const int32_t* c0, const int32_t* c1,
                                                      const int32_t* c2, int32_t* o0, int32_t* o1, int32_t* o2) {
+  // tiles of 1024 consecutive counts (coalesced loads and stores), each tile
+  // scanned in the block and added to the running carry
   __shared__ int32_t ws[3][16];
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  const int per = (n + 1023) / 1024;
-  const int a = min(n, t * per), e = min(n, a + per);
-  int s0 = 0, s1 = 0, s2 = 0;
-  for (int i = a; i < e; ++i) {
-    s0 += c0[i];
-    s1 += c1[i];
-    s2 += c2[i];
-  }
-  // inclusive scans within the wave, then across the 16 waves
-  int i0 = s0, i1 = s1, i2 = s2;
-  for (int o = 1; o < 64; o <<= 1) {
-    const int x0 = __shfl_up(i0, o, 64), x1 = __shfl_up(i1, o, 64), x2 = __shfl_up(i2, o, 64);
-    if (lane >= o) {
-      i0 += x0;
-      i1 += x1;
-      i2 += x2;
+  int carry0 = 0, carry1 = 0, carry2 = 0;
+  for (int base = 0; base < n; base += 1024) {
+    const int i = base + t;
+    const int s0 = i < n ? c0[i] : 0, s1 = i < n ? c1[i] : 0, s2 = i < n ? c2[i] : 0;
+    // inclusive scans within the wave, then across the 16 waves
+    int i0 = s0, i1 = s1, i2 = s2;
+    for (int o = 1; o < 64; o <<= 1) {
+      const int x0 = __shfl_up(i0, o, 64), x1 = __shfl_up(i1, o, 64), x2 = __shfl_up(i2, o, 64);
+      if (lane >= o) {
+        i0 += x0;
+        i1 += x1;
+        i2 += x2;
+      }
     }
-  }
-  if (lane == 63) {
-    ws[0][wv] = i0;
-    ws[1][wv] = i1;
-    ws[2][wv] = i2;
-  }
-  __syncthreads();
-  int b0 = 0, b1 = 0, b2 = 0;
-  for (int k = 0; k < wv; ++k) {
-    b0 += ws[0][k];
-    b1 += ws[1][k];
-    b2 += ws[2][k];
-  }
-  int r0 = b0 + i0 - s0, r1 = b1 + i1 - s1, r2 = b2 + i2 - s2;  // this chunk's exclusive bases
-  for (int i = a; i < e; ++i) {
-    o0[i] = r0;
-    o1[i] = r1;
-    o2[i] = r2;
-    r0 += c0[i];
-    r1 += c1[i];
-    r2 += c2[i];
-  }
-  if (t == 1023) {
-    int z0 = 0, z1 = 0, z2 = 0;
+    if (lane == 63) {
+      ws[0][wv] = i0;
+      ws[1][wv] = i1;
+      ws[2][wv] = i2;
+    }
+    __syncthreads();
+    int b0 = 0, b1 = 0, b2 = 0, z0 = 0, z1 = 0, z2 = 0;
     for (int k = 0; k < 16; ++k) {
-      z0 += ws[0][k];
-      z1 += ws[1][k];
-      z2 += ws[2][k];
+      const int w0 = ws[0][k], w1 = ws[1][k], w2 = ws[2][k];
+      if (k < wv) {
+        b0 += w0;
+        b1 += w1;
+        b2 += w2;
+      }
+      z0 += w0;
+      z1 += w1;
+      z2 += w2;
     }
-    o0[n] = z0;
-    o1[n] = z1;
-    o2[n] = z2;
+    if (i < n) {
+      o0[i] = carry0 + b0 + i0 - s0;
+      o1[i] = carry1 + b1 + i1 - s1;
+      o2[i] = carry2 + b2 + i2 - s2;
+    }
+    carry0 += z0;
+    carry1 += z1;
+    carry2 += z2;
+    __syncthreads();  // (ws is rewritten by the next tile)
+  }
+  if (t == 0) {
+    o0[n] = carry0;
+    o1[n] = carry1;
+    o2[n] = carry2;
   }
 }
 

@@ -186,3 +186,62 @@ def test_gpu_long_gaps_huge_search_tier(dense_grid, oracle, results_equal):
     assert first["trans_huge"] > 0 and first["route_huge"] > 0
     assert first["attempts"] >= 2
     assert second["attempts"] == 1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tier", ["cand", "huge"])
+def test_gpu_tables_that_cannot_grow_fail_their_traces_only(star, dense_grid, oracle, results_equal, monkeypatch,
+                                                           tier):
+    """Past the on-demand tiers' growth cap (kernels.h HUGE_MAX_LOG2 /
+    CAND_MAX_LOG2, lowered to 0 here: no tables at all) or out of HBM, a probe
+    or search that needs the tier fails its own trace with the 500 the
+    reference sends for a matcher exception (error_kind CAND_OVERFLOW /
+    SEARCH_OVERFLOW); every other trace of the batch matches the oracle
+    (round 4 failed the whole batch)."""
+    from reporter_amd import Engine
+    if tier == "cand":
+        monkeypatch.setenv("OTM_CAND_MAX_LOG2", "0")
+        graph, meili = star[0], dict(search_radius=20.0, max_search_radius=20.0)
+        b = star_batch()  # traces 0-2 each hold a probe within 20 m of the hub (400 edges)
+        lat, lon = zip(*[_star_point(5, 85), _star_point(5, 60), _star_point(6, 40)])  # + one that never nears it
+        b = dict(trace_off=np.append(b["trace_off"], len(b["lat"]) + 3),
+                 lat=np.append(b["lat"], np.array(lat, np.float32)), lon=np.append(b["lon"], np.array(lon, np.float32)),
+                 time=np.append(b["time"], 5000.0 + np.arange(3) * 6.0),
+                 accuracy=np.append(b["accuracy"], np.full(3, 5.0, np.float32)))
+        kind, failing = 2, [0, 1, 2]
+    else:
+        monkeypatch.setenv("OTM_HUGE_MAX_LOG2", "0")
+        graph, meili = dense_grid, GRID_MEILI
+        far = grid_batch(dense_grid)  # 600 s gaps: searches past the global tier
+        near = synth.make_traces(dense_grid, 2, 6, interval_s=5.0, noise_sigma_m=5.0, accuracy=5.0, seed=6)
+        b = {k: np.concatenate([far[k], near[k]]) for k in ("lat", "lon", "time", "accuracy")}
+        b["trace_off"] = np.concatenate([far["trace_off"], far["trace_off"][-1] + near["trace_off"][1:]])
+        kind, failing = 3, None
+    with Engine(graph_path=graph, **meili) as eng:
+        res = eng.match(b)
+        sp = eng.spill_stats()
+    orc = oracle.match_batch(oracle.Graph(graph), b, p=oracle.params(**meili), nthreads=4)
+    tr = res.traces
+    bad = [t for t in range(len(tr)) if tr["code"][t] != 200]
+    if failing is not None:
+        assert bad == failing
+    else:
+        assert bad and len(bad) < len(tr) and sp["trans_huge"] + sp["route_huge"] > 0
+    for t in bad:
+        assert tr["code"][t] == 500 and tr["error_kind"][t] == kind
+    ok = [t for t in range(len(tr)) if t not in bad]
+    assert all(orc["traces"]["code"][t] == 200 for t in range(len(tr)))
+    for t in ok:  # every other trace: the oracle's records (way ids by their own offsets)
+        a, n = tr["seg_off"][t], tr["seg_cnt"][t]
+        oa, on = orc["traces"]["seg_off"][t], orc["traces"]["seg_cnt"][t]
+        assert n == on
+        gs, os_ = res.segments[a:a + n], orc["segments"][oa:oa + on]
+        for f in gs.dtype.names:
+            if f != "way_off":
+                assert np.array_equal(gs[f], os_[f]), f
+        for x, y in zip(gs, os_):
+            assert np.array_equal(res.way_ids[x["way_off"]:x["way_off"] + x["way_cnt"]],
+                                  orc["way_ids"][y["way_off"]:y["way_off"] + y["way_cnt"]])
+        ra, rn = tr["rep_off"][t], tr["rep_cnt"][t]
+        ora, orn = orc["traces"]["rep_off"][t], orc["traces"]["rep_cnt"][t]
+        assert res.reports[ra:ra + rn].tobytes() == orc["reports"][ora:ora + orn].tobytes()

@@ -809,13 +809,14 @@ void report_many_device(otm_engine* E, int n, const char* const* reqs, const siz
   std::vector<int> rest;  // left to the host readers
   std::vector<int> inv;   // invalid speeds per GPU-read request (stderr lines)
   std::vector<int> which;
-  double t1 = t0, t2 = t0, t3 = t0;
+  double t1 = t0, t2 = t0, t3 = t0, tl = t0, tm = t0;
   int rc;
   std::string err;
   for (int k = 0; k < n; ++k) resps[k] = nullptr;
   std::atomic<bool> oom{false};
   {
     std::lock_guard<std::mutex> lk(E->mu);
+    tl = now_ms();
     // an async worker's batch (ord): its copies on the batch stream (one
     // stream per context, engine.h); a one-call batch: a copy stream, so each
     // piece's read overlaps the next piece's copy
@@ -880,6 +881,7 @@ void report_many_device(otm_engine* E, int n, const char* const* reqs, const siz
       const otm_trace_result* trs = nullptr;
       int64_t total = 0;
       rc = otm::engine_match_requests(E, n, bytes, true, &ok, &nt, &err);
+      tm = now_ms();
       if (!rc) {
         if (gw) {
           rc = otm::engine_write_responses(E, &boff, &hostw, &trs, &total, &err);
@@ -1004,8 +1006,9 @@ void report_many_device(otm_engine* E, int n, const char* const* reqs, const siz
   }
   if (json_profile())
     std::fprintf(stderr, "[otm json gpu] %d requests (%zu on the host readers): stage %.2f, gpu %.2f, copy out %.2f, "
-                 "host readers %.2f ms\n",
-                 n, rest.size(), t1 - t0, t2 - t1, t3 - t2, now_ms() - t3);
+                 "host readers %.2f ms; at %.2f: lock %.2f, read+sync %.2f, match %.2f, write %.2f ms\n",
+                 n, rest.size(), t1 - t0, t2 - t1, t3 - t2, now_ms() - t3, t0, tl - t0,
+                 E->t_read_done - t1, tm - E->t_read_done, t2 - tm);
 }
 
 // (pinned[k]: the page-locked submission slab body k lies in, or null;

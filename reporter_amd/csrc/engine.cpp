@@ -6,6 +6,7 @@
 #include "engine.h"
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdlib>
 
@@ -948,6 +949,15 @@ int engine_match(otm_engine* E, const DevBatch& b, hipStream_t s, std::string* e
 // batch contexts, hipMemcpyWithStream, and the library's own copy kernel with
 // 16-128 workgroups -- the leg runs at the sum of its PCIe bytes and kernels.
 static hipError_t big_copy(void* dst, const void* src, size_t n, hipMemcpyKind k, hipStream_t s) {
+  static const int wgs = [] {
+    const char* v = std::getenv("OTM_D2H_KERNEL");  // (A/B: workgroups of the library's own D2H copy)
+    return v ? std::atoi(v) : 0;
+  }();
+  if (k == hipMemcpyDeviceToHost && wgs > 0 && n >= ((size_t)1 << 20) && ((uintptr_t)dst & 15) == 0 &&
+      ((uintptr_t)src & 15) == 0) {
+    launch_copy_out(dst, src, n, wgs, s);
+    return hipGetLastError();
+  }
   return hipMemcpyAsync(dst, src, n, k, s);
 }
 
@@ -1255,6 +1265,7 @@ int engine_match_requests(otm_engine* E, int32_t n, size_t bytes, bool pushed, c
   if (n) HIPCHK(hipMemcpyAsync(h + 8, E->req_ok.p, (size_t)n, hipMemcpyDeviceToHost, s));
   HIPCHK(hipGetLastError());
   HIPCHK(wait_batch(E, s, (int64_t)(bytes / 40)));
+  E->t_read_done = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
   int64_t tot;
   std::memcpy(&tot, h, 8);
   b.n_traces = (int32_t)(tot >> 40);
@@ -1343,11 +1354,12 @@ int engine_fetch(otm_engine* E, otm_results* out, std::string* err) {
   if ((rc = ensure_pinned(E->h_reps_dense, ((size_t)NR + 1) * sizeof(otm_report_rec), err))) return rc;
   if ((rc = ensure_pinned(E->h_ways, ((size_t)NW + 1) * 8, err))) return rc;
   const hipMemcpyKind d2h = hipMemcpyDeviceToHost;
-  if (NT) HIPCHK(big_copy(E->h_traces.p, E->f_traces.p, (size_t)NT * sizeof(otm_trace_result), d2h, s));
-  if (NS) HIPCHK(big_copy(E->h_segs.p, E->f_segs.p, (size_t)NS * sizeof(otm_segment), d2h, s));
-  if (NR) HIPCHK(big_copy(E->h_reps_dense.p, E->f_reps.p, (size_t)NR * sizeof(otm_report_rec), d2h, s));
-  if (NW) HIPCHK(big_copy(E->h_ways.p, E->f_ways.p, (size_t)NW * 8, d2h, s));
-  HIPCHK(wait_batch(E, s, E->last_P));
+  hipStream_t c = s;
+  if (NT) HIPCHK(big_copy(E->h_traces.p, E->f_traces.p, (size_t)NT * sizeof(otm_trace_result), d2h, c));
+  if (NS) HIPCHK(big_copy(E->h_segs.p, E->f_segs.p, (size_t)NS * sizeof(otm_segment), d2h, c));
+  if (NR) HIPCHK(big_copy(E->h_reps_dense.p, E->f_reps.p, (size_t)NR * sizeof(otm_report_rec), d2h, c));
+  if (NW) HIPCHK(big_copy(E->h_ways.p, E->f_ways.p, (size_t)NW * 8, d2h, c));
+  HIPCHK(wait_batch(E, c, E->last_P));
   out->n_traces = NT;
   out->n_segments = NS;
   out->n_reports = NR;

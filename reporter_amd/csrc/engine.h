@@ -141,6 +141,7 @@ struct otm_engine {
   Buf req_lat, req_lon, req_time, req_acc;  // the reader's sparse point slots (requests.hip)
   int32_t req_read = 0;                     // requests of the staged batch read so far
   hipStream_t req_copy = nullptr;           // the request pieces' H2D copies (created at first use)
+  double t_read_done = 0.0;                 // (OTM_JSON_PROFILE) when the last request batch's read synced
   // the request pieces' copies on the batch stream instead of req_copy: the
   // async workers' contexts, so that three contexts hold three streams and
   // never share one of the runtime's hardware queues (GPU_MAX_HW_QUEUES, 4),

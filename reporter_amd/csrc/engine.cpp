@@ -947,17 +947,10 @@ int engine_match(otm_engine* E, const DevBatch& b, hipStream_t s, std::string* e
 // Measured and not kept (profiles/r02_hostleg_ab/): a copy
 // engine through hipMemcpyDeviceToDeviceNoCU, copies taking turns across the
 // batch contexts, hipMemcpyWithStream, and the library's own copy kernel with
-// 16-128 workgroups -- the leg runs at the sum of its PCIe bytes and kernels.
+// 16-128 workgroups -- the leg runs at the sum of its PCIe bytes and kernels;
+// round 5: the D2H copies on a stream of their own, and the library's copy
+// kernel (16-64 workgroups) for the D2H copies -- both slower.
 static hipError_t big_copy(void* dst, const void* src, size_t n, hipMemcpyKind k, hipStream_t s) {
-  static const int wgs = [] {
-    const char* v = std::getenv("OTM_D2H_KERNEL");  // (A/B: workgroups of the library's own D2H copy)
-    return v ? std::atoi(v) : 0;
-  }();
-  if (k == hipMemcpyDeviceToHost && wgs > 0 && n >= ((size_t)1 << 20) && ((uintptr_t)dst & 15) == 0 &&
-      ((uintptr_t)src & 15) == 0) {
-    launch_copy_out(dst, src, n, wgs, s);
-    return hipGetLastError();
-  }
   return hipMemcpyAsync(dst, src, n, k, s);
 }
 

@@ -368,8 +368,6 @@ struct BatchStatus {
   int32_t cnt[3], pad2;
 };
 void launch_batch_init(int32_t* counters, int32_t* abort, hipStream_t s);
-// a device -> page-locked host copy by `wgs` workgroups of 512 threads (16-B aligned ends)
-void launch_copy_out(void* dst, const void* src, size_t n, int wgs, hipStream_t s);
 // otm_match_compact's inputs widened on the device (time = base + delta, accuracy as float)
 void launch_expand_compact(const int64_t* trace_off, const int64_t* tbase, const int32_t* dt, const int16_t* acc16,
                            double* time, float* acc, int32_t n_traces, hipStream_t s);

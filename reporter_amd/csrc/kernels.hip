@@ -3978,21 +3978,6 @@ void launch_batch_init(int32_t* counters, int32_t* abort, hipStream_t s) {
 void launch_snap(int32_t* counters, int32_t* snap, bool reset, hipStream_t s) {
   hipLaunchKernelGGL(k_snap, dim3(1), dim3(64), 0, s, counters, snap, reset ? 1 : 0);
 }
-// A device -> page-locked host copy done by a few workgroups of this library
-// (A/B against the runtime's copy, OTM_D2H_KERNEL): 16-byte words, the tail
-// bytes by one thread.  The runtime sends large D2H copies through a blit
-// kernel that takes one workgroup on every CU while it waits on PCIe.
-__global__ __launch_bounds__(512) void k_copy_out(const uint4* __restrict__ src, uint4* dst, size_t n16,
-                                                  const unsigned char* s8, unsigned char* d8, size_t n) {
-  const size_t stride = (size_t)gridDim.x * blockDim.x;
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride) dst[i] = src[i];
-  if (blockIdx.x == 0 && threadIdx.x == 0)
-    for (size_t i = n16 * 16; i < n; ++i) d8[i] = s8[i];
-}
-void launch_copy_out(void* dst, const void* src, size_t n, int wgs, hipStream_t s) {
-  hipLaunchKernelGGL(k_copy_out, dim3(wgs), dim3(512), 0, s, (const uint4*)src, (uint4*)dst, n / 16,
-                     (const unsigned char*)src, (unsigned char*)dst, n);
-}
 // The compact host batch (otm_match_compact) widened on the device: a wave per
 // trace, its points' time = base + delta (whole seconds, exact in a double)
 // and accuracy as float -- the arrays every stage reads.

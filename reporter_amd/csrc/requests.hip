@@ -15,10 +15,11 @@
 // Per request: the header `{"uuid":"` + printable uuid + `","trace":[`, the
 // trailer `]}`, and the points region in between.  The region is walked in
 // 4 KB windows staged in LDS (+ a 256-byte margin: a point that starts in a
-// window ends in its margin, or the body goes to the host); a lane owns the
-// '{' bytes of its 64-byte slice and parses those points from LDS, all lanes
-// in lockstep (parsing inside the byte loop serialised the wave on every
-// distinct offset: 2.4 -> 0.06 ms per pass).  Each point must be followed by
+// window ends in its margin, or the body goes to the host); the '{' bytes are
+// found in the loaded 16-byte words, listed in order in LDS, and lane j parses
+// the window's point j from LDS, all lanes in lockstep (parsing inside a byte
+// loop serialised the wave on every distinct offset: 2.4 -> 0.06 ms per pass;
+// round 5 dropped the per-lane byte scan for the word masks).  Each point must be followed by
 // ",{" or by the end of the region, and it starts with '{', so the checks
 // cover every byte of the region; a '{' can occur nowhere else in a valid
 // region, so the point count is the '{' count.
@@ -107,15 +108,6 @@ __device__ bool parse_point(const unsigned char* L, int j, int lim, int rend, do
   return c.ch(c.i) == ',' && c.ch(c.i + 1) == '{';
 }
 
-__device__ __forceinline__ int wave_scan_incl(int v, int lane) {
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int n = __shfl_up(v, o, 64);
-    if (lane >= o) v += n;
-  }
-  return v;
-}
-
 // The header of request [a, e): the region [t0, t1) between `","trace":[`
 // and the final `]}`, or false.  Lane-parallel search for the uuid's end.
 __device__ bool req_header(const unsigned char* blob, int64_t a, int64_t e, int lane, int64_t* t0, int64_t* t1) {
@@ -152,12 +144,32 @@ __device__ bool req_header(const unsigned char* blob, int64_t a, int64_t e, int 
   return *t1 > *t0;
 }
 
+// The '{' bytes of a 32-bit word: bit 8j+7 set for each byte j equal to '{'
+// (exact, no borrow between bytes)
+__device__ __forceinline__ uint32_t brace_bits(uint32_t x) {
+  const uint32_t y = x ^ 0x7B7B7B7Bu;
+  return ~(((y & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | y | 0x7F7F7F7Fu);
+}
+// the flag bits (8j+7) of bytes j in [a, b) of a 64-bit word (a, b clamped to [0, 8])
+__device__ __forceinline__ uint64_t byte_flags(int a, int b) {
+  a = max(a, 0);
+  b = min(b, 8);
+  if (b <= a) return 0;
+  const uint64_t below_b = b >= 8 ? ~0ull : ((1ull << (8 * b)) - 1ull);
+  const uint64_t from_a = ~((1ull << (8 * a)) - 1ull);
+  return below_b & from_a & 0x8080808080808080ull;
+}
+
 // Walk request r's points region: validate and count, and write each point
 // that parses at out + base + its index (below cap).  Windows of
 // CH bytes (+ MARGIN) are staged in LDS with 16-byte aligned loads, all of a
-// lane's in flight at once; a lane owns the '{' bytes of its 64-byte slice.
-__device__ bool walk_points(const unsigned char* blob, int64_t t0, int64_t t1, int lane, unsigned char* L, int64_t base,
-                            int64_t cap, const DevBatch* out, int* npts) {
+// lane's in flight at once.  The '{' bytes are found in the loaded words
+// themselves (a 16-byte word holds at most one point start: a valid point is
+// >= 39 bytes) and listed in LDS in order, so lane j parses the window's
+// point j (no byte loop over LDS).
+constexpr int PMAX = 128;  // point starts listed per window (a valid window holds <= CH / 39 + 1)
+__device__ bool walk_points(const unsigned char* blob, int64_t t0, int64_t t1, int lane, unsigned char* L,
+                            int16_t* PS, int64_t base, int64_t cap, const DevBatch* out, int* npts) {
   int count = 0;
   bool good = true;
   for (int64_t w0 = t0; w0 < t1; w0 += CH) {
@@ -178,33 +190,46 @@ __device__ bool walk_points(const unsigned char* blob, int64_t t0, int64_t t1, i
       const int k = u * RTB + lane;
       if (k < nld) ((uint4*)L)[k] = v[u];
     }
+    // the point starts of this step (window offsets [0, min(CH, lim))), in
+    // order: word k = u * RTB + lane covers offsets [16k - sh, 16k - sh + 16)
+    const int send = min(CH, lim);
+    int listed = 0;
+#pragma unroll
+    for (int u = 0; u < WLOADS; ++u) {
+      const int k = u * RTB + lane;
+      int at = -1;
+      if (k < nld) {
+        const uint32_t b0 = brace_bits(v[u].x), b1 = brace_bits(v[u].y), b2 = brace_bits(v[u].z),
+                       b3 = brace_bits(v[u].w);
+        const uint64_t lo = (uint64_t)b0 | ((uint64_t)b1 << 32), hi = (uint64_t)b2 | ((uint64_t)b3 << 32);
+        // bytes of the word inside [0, send): o = 16k - sh + j
+        const int o0 = 16 * k - sh;
+        const int j0 = o0 < 0 ? -o0 : 0, j1 = min(16, send - o0);
+        const uint64_t flo = lo & byte_flags(j0, j1), fhi = hi & byte_flags(j0 - 8, j1 - 8);
+        const int nb = __popcll(flo) + __popcll(fhi);
+        if (nb > 1) good = false;  // two point starts within 16 bytes: no valid body has them
+        if (nb >= 1) at = o0 + (flo ? (__ffsll((long long)flo) - 1) >> 3 : 8 + ((__ffsll((long long)fhi) - 1) >> 3));
+      }
+      const unsigned long long m = __ballot(at >= 0);
+      const int pos = listed + __popcll(m & ((1ull << lane) - 1ull));
+      if (at >= 0 && pos < PMAX) PS[pos] = (int16_t)at;
+      listed += __popcll(m);
+    }
+    if (listed > PMAX) good = false;  // more starts than a valid window holds
     __syncthreads();
     const unsigned char* W = L + sh;  // W[0] = byte w0
-    // the points that start in this lane's 64 bytes of the step: a valid
-    // point is >= 39 bytes, so at most two ('{' bytes beyond two: the body is
-    // invalid, and the lane's third '{' fails it below)
-    int mine = 0, k0 = -1, k1 = -1;
-    const int s0 = lane * 64, s1 = min(s0 + 64, min(CH, lim));
-    for (int k = s0; k < s1; ++k) {
-      if (W[k] != '{') continue;
-      if (mine == 0) k0 = k;
-      else if (mine == 1) k1 = k;
-      ++mine;
-    }
-    const int incl = wave_scan_incl(mine, lane);
-    const int idx = count + incl - mine;
     if (w0 == t0 && lane == 0 && W[0] != '{') good = false;  // the region starts with a point
-    if (mine > 2) good = false;
-    // the lanes parse their points in lockstep (first points, then second)
-    for (int m = 0; m < 2; ++m) {
-      const int k = m == 0 ? k0 : k1;
-      if (__ballot(k >= 0) == 0ull) break;
-      if (k < 0) continue;
+    // lane j parses the step's point j (then j + 64)
+    const int np = min(listed, PMAX);
+    for (int j = lane; j - lane < np; j += RTB) {
+      if (j >= np) continue;
+      const int k = PS[j];
       double la, lo, ti, ac;
       const bool ok = parse_point(W, k, lim, (int)(t1 - w0), &la, &lo, &ti, &ac);
       good = good && ok;
-      if (ok && idx + m < cap) {  // (cap: an invalid body's stray '{'s write nothing past its range)
-        const int64_t p = base + idx + m;
+      const int idx = count + j;
+      if (ok && idx < cap) {  // (cap: an invalid body's stray '{'s write nothing past its range)
+        const int64_t p = base + idx;
         // extract_points' conversions (report.cpp)
         ((float*)out->lat)[p] = (float)la;
         ((float*)out->lon)[p] = (float)lo;
@@ -212,7 +237,7 @@ __device__ bool walk_points(const unsigned char* blob, int64_t t0, int64_t t1, i
         ((float*)out->acc)[p] = (float)ac;
       }
     }
-    count += __shfl(incl, 63, 64);
+    count += listed;
     if (!__all(good)) return false;
   }
   *npts = count;
@@ -232,13 +257,14 @@ __device__ __forceinline__ int64_t sparse_base(int32_t r, int64_t a) { return (i
 __global__ __launch_bounds__(RTB) void k_req_read(const unsigned char* blob, const int64_t* off, int32_t r0,
                                                   int32_t r1, int32_t n, int64_t* cnt, uint8_t* ok, DevBatch sp) {
   __shared__ __attribute__((aligned(16))) unsigned char L[WBUF];
+  __shared__ int16_t PS[PMAX];
   const int lane = threadIdx.x;
   for (int32_t r = r0 + blockIdx.x; r < r1; r += gridDim.x) {
     const int64_t a = off[r], e = off[r + 1];
     int64_t t0 = 0, t1 = 0;
     int np = 0;
     bool acc = req_header(blob, a, e, lane, &t0, &t1);
-    acc = acc && walk_points(blob, t0, t1, lane, L, sparse_base(r, a), (e - a) / 39, &sp, &np) && np >= 2;
+    acc = acc && walk_points(blob, t0, t1, lane, L, PS, sparse_base(r, a), (e - a) / 39, &sp, &np) && np >= 2;
     if (lane == 0) {
       cnt[r] = acc ? ((int64_t)1 << 40) | (int64_t)np : 0;
       ok[r] = acc ? 1 : 0;

@@ -459,6 +459,9 @@ int otm_debug_py_round3(double x, double* out);
  * strided share of everyone's, with plain allocations through the same
  * scan).  Returns the arenas left live after (0 expected), -1 on bad args. */
 int otm_debug_arena_stress(int threads, int rounds);
+/* Test hook: the chunks eng's last otm_report_batch was split into (one per
+ * batch context, run concurrently; 1: not split). */
+int otm_debug_last_split(const otm_engine* eng);
 /* Which HIP runtime this library is bound to ("<path> hip_runtime_version=N"):
  * a host that also runs torch must load torch first so both share one. */
 const char* otm_runtime_info(void);

@@ -178,6 +178,7 @@ def _declare(L):
         "otm_debug_py_repr": (C.c_int, [C.c_double, C.c_char_p]),
         "otm_debug_py_round3": (C.c_int, [C.c_double, C.POINTER(C.c_double)]),
         "otm_debug_arena_stress": (C.c_int, [C.c_int, C.c_int]),
+        "otm_debug_last_split": (C.c_int, [vp]),
         "otm_batcher_defaults": (None, [C.POINTER(BatcherCfg)]),
         "otm_batcher_create": (C.c_int, [vp, C.POINTER(BatcherCfg), REPORT_FN, vp, pp]),
         "otm_batcher_destroy": (None, [vp]),

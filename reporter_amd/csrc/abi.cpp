@@ -244,8 +244,15 @@ bool json_profile() {
 }
 thread_local double t_gpu_ms = 0.0, t_pack_ms = 0.0, t_write_ms = 0.0, t_extract_ms = 0.0;
 
-// The reference's stderr line per invalid speed (reporter_service.py)
+// The reference's stderr line per invalid speed (reporter_service.py); a
+// split call's chunk threads (report_many_split) collect the counts in t_lines
+// instead, for the caller to print in chunk order
+thread_local std::vector<int>* t_lines = nullptr;
 void speed_lines(int n) {
+  if (t_lines) {
+    t_lines->push_back(n);
+    return;
+  }
   for (int q = 0; q < n; ++q) std::fputs("Speed exceeds 200kph\n", stderr);
 }
 
@@ -817,10 +824,11 @@ void report_many_device(otm_engine* E, int n, const char* const* reqs, const siz
   {
     std::lock_guard<std::mutex> lk(E->mu);
     tl = now_ms();
-    // an async worker's batch (ord): its copies on the batch stream (one
-    // stream per context, engine.h); a one-call batch: a copy stream, so each
-    // piece's read overlaps the next piece's copy
-    E->req_on_batch_stream = ord != nullptr;
+    // an async worker's batch (ord): its copies on the pipeline's one copy
+    // stream (engine.h req_shared; created by the turn's holder, so by one
+    // thread at a time); a one-call batch: the context's own copy stream
+    if (ord && !ord->copy) (void)hipStreamCreateWithFlags(&ord->copy, hipStreamNonBlocking);
+    E->req_shared = ord ? ord->copy : nullptr;
     size_t bytes = 0;
     for (int k = 0; k < n; ++k) bytes += lens[k];
     int64_t* off = nullptr;
@@ -1113,15 +1121,104 @@ void worker_loop(otm_engine* E, int wi) {
 }
 
 // the pipeline's workers and their contexts, at the first submission (under E->qmu)
-void start_workers(otm_engine* E) {
+void make_contexts(otm_engine* E) {
   const int nw = async_workers(E);
-  for (int i = 1; i < nw; ++i) {
+  while ((int)E->actx.size() < nw - 1) {
     otm_engine* C = nullptr;
-    if (otm_engine_clone(E, &C) != OTM_OK) break;  // fewer workers, same results
+    if (otm_engine_clone(E, &C) != OTM_OK) break;  // fewer contexts, same results
     E->actx.push_back(C);
   }
+}
+
+void start_workers(otm_engine* E) {
+  make_contexts(E);
   for (int i = 0; i <= (int)E->actx.size(); ++i) E->workers.emplace_back(worker_loop, E, i);
   E->worker_started = true;
+}
+
+// One otm_report_batch call over two batch contexts: the bodies cut into two
+// chunks (half the bytes each), each run whole on its context (report_many)
+// in a thread of its own, the chunks' request copies in chunk order on one
+// copy stream (E->split_order), so the first chunk's kernels run while the
+// second crosses PCIe, and its responses come back while the second runs.  Each chunk is a batch of its own: the same per-request results
+// (the matcher's results do not depend on a trace's batch).  The reference's
+// stderr lines are printed after, in chunk order.  Not split: a multi-device
+// engine or a clone (one context), an engine counting or timing its kernels
+// (those figures are per context), or fewer than SPLIT_MIN requests a chunk.
+// Measured (round 5, bench.py json_report on one box, profiles/r05_ab/json_split/):
+// two chunks with the first 50-60 % of the bytes 334-343M points/s, 40 %
+// 315-323M, 25 % 300-305M, one batch 286-292M; three chunks 268M (their
+// kernels share the GPU at once: each small batch's fixed cost is paid three
+// times over).
+constexpr int SPLIT_CHUNKS = 2;
+constexpr int SPLIT_FIRST_PCT = 50;
+constexpr int SPLIT_MIN = 2048;
+void report_many_split(otm_engine* E, int n, const char* const* reqs, const size_t* lens, int* codes, char** resps,
+                       size_t* resp_lens, const void* const* pinned) {
+  std::vector<otm_engine*> ctx{E};
+  if (E->members.empty() && !E->parent && !E->counting && !E->timing && n >= 2 * SPLIT_MIN) {
+    std::lock_guard<std::mutex> lk(E->qmu);
+    if (!E->worker_started) make_contexts(E);  // (fixed once the workers run)
+    ctx.insert(ctx.end(), E->actx.begin(), E->actx.end());
+  }
+  const int chunks = std::min<int>(std::min<int>((int)ctx.size(), SPLIT_CHUNKS), n / SPLIT_MIN);
+  std::vector<int> cut((size_t)std::max(chunks, 1) + 1, n);
+  cut[0] = 0;
+  if (chunks >= 2) {
+    // the first chunk SPLIT_FIRST_PCT % of the bytes (its kernels run while the
+    // rest is copied), the others equal shares of the rest
+    size_t total = 0, acc = 0;
+    for (int k = 0; k < n; ++k) total += lens[k];
+    const size_t first = total * SPLIT_FIRST_PCT / 100;
+    int c = 1;
+    for (int k = 0; k < n && c < chunks; ++k) {
+      acc += lens[k];
+      const size_t want = first + (total - first) * (size_t)(c - 1) / (size_t)(chunks - 1);
+      if (acc >= want) cut[(size_t)c++] = k + 1;
+    }
+  }
+  bool even = chunks >= 2;
+  for (int c = 0; even && c < chunks; ++c) even = cut[(size_t)c + 1] - cut[(size_t)c] >= SPLIT_MIN / 2;
+  if (!even || !gpu_reader(E, n / chunks)) {
+    E->last_split = 1;
+    report_many(E, n, reqs, lens, codes, resps, resp_lens, pinned);
+    return;
+  }
+  E->last_split = chunks;
+  std::lock_guard<std::mutex> sl(E->split_mu);
+  otm::H2DOrder& ord = E->split_order;
+  {
+    std::lock_guard<std::mutex> lk(ord.m);
+    ord.next = 0;
+  }
+  std::vector<std::vector<int>> lines((size_t)chunks);
+  std::vector<std::exception_ptr> errs((size_t)chunks);
+  auto run = [&](int c) {
+    const int a = cut[(size_t)c], m = cut[(size_t)c + 1] - a;
+    t_lines = &lines[(size_t)c];
+    try {
+      report_many(ctx[(size_t)c], m, reqs + a, lens + a, codes + a, resps + a, resp_lens + a,
+                  pinned ? pinned + a : nullptr, &ord, (uint64_t)c);
+    } catch (...) {
+      errs[(size_t)c] = std::current_exception();  // (its turn was passed on: H2DTurn's destructor)
+    }
+    t_lines = nullptr;
+  };
+  std::vector<std::thread> th;
+  for (int c = 1; c < chunks; ++c) th.emplace_back(run, c);
+  run(0);
+  for (auto& t : th) t.join();
+  for (int c = 0; c < chunks; ++c)
+    if (errs[(size_t)c]) {
+      // out of host memory in a chunk (it freed its own): the other chunks' bodies too
+      for (int k = 0; k < n; ++k) {
+        arena::free_body(resps[k]);
+        resps[k] = nullptr;
+      }
+      std::rethrow_exception(errs[(size_t)c]);
+    }
+  for (const auto& l : lines)
+    for (int v : l) speed_lines(v);
 }
 
 }  // namespace
@@ -1164,6 +1261,8 @@ int otm_kmax(void) { return otm::KMAX; }
 // the arenas released (0 when every arena was released once, by its own last
 // body: a body freed into the wrong arena releases one early, and the real
 // arena never).
+int otm_debug_last_split(const otm_engine* E) { return E ? E->last_split : -1; }
+
 int otm_debug_arena_stress(int threads, int rounds) {
   if (threads < 1 || threads > 64 || rounds < 0) return -1;
   constexpr int NB = 16;
@@ -1414,9 +1513,12 @@ void otm_engine_destroy(otm_engine* E) {
     E->qcv.notify_all();
     for (auto& t : E->workers) t.join();  // (queued requests are finished first)
     for (auto& r : E->done) arena::free_body(r.body);
-    for (otm_engine* C : E->actx) otm_engine_destroy(C);
-    for (hipEvent_t ev : E->aorder.ev)
+  }
+  for (otm_engine* C : E->actx) otm_engine_destroy(C);
+  for (otm::H2DOrder* o : {&E->aorder, &E->split_order}) {
+    for (hipEvent_t ev : o->ev)
       if (ev) (void)hipEventDestroy(ev);
+    if (o->copy) (void)hipStreamDestroy(o->copy);
   }
   if (!E->members.empty()) {
     otm::member_pool_free(E);
@@ -1456,7 +1558,7 @@ static int otm_report_batch_impl(otm_engine* E, int n, const char* const* reqs, 
     pin[(size_t)k] = held[(size_t)k].get();
     any = any || pin[(size_t)k];
   }
-  report_many(E, n, reqs, lens, codes, resps, resp_lens, any ? pin.data() : nullptr);
+  report_many_split(E, n, reqs, lens, codes, resps, resp_lens, any ? pin.data() : nullptr);
   return OTM_OK;
 }
 

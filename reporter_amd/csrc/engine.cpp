@@ -1153,39 +1153,29 @@ static void read_requests(otm_engine* E, int32_t n, int32_t upto) {
   E->req_read = upto;
 }
 
-// The pieces go to HBM on a copy stream of their own, each followed by an
-// event that the batch stream waits on before it reads the piece's requests,
-// so one piece's read overlaps the next piece's copy.
-// With E->req_on_batch_stream (the async workers' contexts) the pieces go on
-// the batch stream itself, each read behind its copy: one stream, so one
-// hardware queue, per context (see otm_engine::req_on_batch_stream).
+// The request pieces' copy stream: the async pipeline's shared one, or E's own
+static hipStream_t req_copy_stream(otm_engine* E) {
+  if (E->req_shared) return E->req_shared;
+  if (!E->req_copy && hipStreamCreateWithFlags(&E->req_copy, hipStreamNonBlocking) != hipSuccess) return nullptr;
+  return E->req_copy;
+}
+
+// The pieces go to HBM on a copy stream (E's own, or with E->req_shared the
+// async pipeline's one copy stream), each followed by an event that the batch
+// stream waits on before it reads the piece's requests, so one piece's read
+// overlaps the next piece's copy.
 int engine_push_requests(otm_engine* E, int32_t n, size_t bytes, size_t from, size_t to, const char* src,
                          int32_t upto, std::string* err) {
-  if (E->req_on_batch_stream) {
-    char* d = (char*)E->d_req.p;
-    const char* h = (const char*)E->h_req.p;
-    const size_t hdr = req_hdr_bytes(n);
-    const hipMemcpyKind h2d = hipMemcpyHostToDevice;
-    if (!src) {
-      const size_t a = from ? hdr + from : 0;
-      const size_t b = hdr + (to >= bytes ? bytes + REQ_PAD : to);
-      if (b > a) HIPCHK(big_copy(d + a, h + a, b - a, h2d, E->stream));
-    } else {
-      if (from == 0) HIPCHK(hipMemcpyAsync(d, h, hdr, h2d, E->stream));
-      if (to > from) HIPCHK(big_copy(d + hdr + from, src, to - from, h2d, E->stream));
-      if (to >= bytes) HIPCHK(hipMemsetAsync(d + hdr + bytes, 0, REQ_PAD, E->stream));
-    }
-    read_requests(E, n, upto < n ? upto : n);
-    HIPCHK(hipGetLastError());
-    return OTM_OK;
+  hipStream_t c = req_copy_stream(E);
+  if (!c) {
+    *err = "no request copy stream";
+    return OTM_EDEVICE;
   }
-  if (!E->req_copy) HIPCHK(hipStreamCreateWithFlags(&E->req_copy, hipStreamNonBlocking));
   while (E->req_ev.size() < E->req_piece + 2) {  // [0]: the fence, [1 + p]: piece p
     hipEvent_t ev = nullptr;
     HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     E->req_ev.push_back(ev);
   }
-  hipStream_t c = E->req_copy;
   char* d = (char*)E->d_req.p;
   const char* h = (const char*)E->h_req.p;
   const size_t hdr = req_hdr_bytes(n);
@@ -1213,15 +1203,13 @@ int engine_push_requests(otm_engine* E, int32_t n, size_t bytes, size_t from, si
 }
 
 int engine_push_after(otm_engine* E, hipEvent_t ev) {
-  if (E->req_on_batch_stream) return hipStreamWaitEvent(E->stream, ev, 0) == hipSuccess ? OTM_OK : OTM_EDEVICE;
-  if (!E->req_copy && hipStreamCreateWithFlags(&E->req_copy, hipStreamNonBlocking) != hipSuccess) return OTM_EDEVICE;
-  return hipStreamWaitEvent(E->req_copy, ev, 0) == hipSuccess ? OTM_OK : OTM_EDEVICE;
+  hipStream_t c = req_copy_stream(E);
+  return c && hipStreamWaitEvent(c, ev, 0) == hipSuccess ? OTM_OK : OTM_EDEVICE;
 }
 
 int engine_push_mark(otm_engine* E, hipEvent_t ev) {
-  if (E->req_on_batch_stream) return hipEventRecord(ev, E->stream) == hipSuccess ? OTM_OK : OTM_EDEVICE;
-  if (!E->req_copy && hipStreamCreateWithFlags(&E->req_copy, hipStreamNonBlocking) != hipSuccess) return OTM_EDEVICE;
-  return hipEventRecord(ev, E->req_copy) == hipSuccess ? OTM_OK : OTM_EDEVICE;
+  hipStream_t c = req_copy_stream(E);
+  return c && hipEventRecord(ev, c) == hipSuccess ? OTM_OK : OTM_EDEVICE;
 }
 
 int engine_match_requests(otm_engine* E, int32_t n, size_t bytes, bool pushed, const uint8_t** ok,

@@ -34,6 +34,9 @@ struct H2DOrder {
   std::condition_variable cv;
   uint64_t next = 0;
   hipEvent_t ev[2] = {nullptr, nullptr};
+  // the pipeline's one request-copy stream (created by the first turn's
+  // holder): every context's pieces go there, in ticket order
+  hipStream_t copy = nullptr;
 };
 }  // namespace otm
 
@@ -142,12 +145,12 @@ struct otm_engine {
   int32_t req_read = 0;                     // requests of the staged batch read so far
   hipStream_t req_copy = nullptr;           // the request pieces' H2D copies (created at first use)
   double t_read_done = 0.0;                 // (OTM_JSON_PROFILE) when the last request batch's read synced
-  // the request pieces' copies on the batch stream instead of req_copy: the
-  // async workers' contexts, so that three contexts hold three streams and
-  // never share one of the runtime's hardware queues (GPU_MAX_HW_QUEUES, 4),
-  // where a stream's wait on another batch's copies stalls every stream
-  // queued behind it
-  bool req_on_batch_stream = false;
+  // the async workers' contexts: their request pieces go on the pipeline's
+  // one copy stream (H2DOrder::copy) instead of req_copy, so three batch
+  // streams and one copy stream fit the runtime's four hardware queues
+  // (GPU_MAX_HW_QUEUES), and the copies run on a copy engine, not as blit
+  // kernels on the batch stream beside the batch's kernels
+  hipStream_t req_shared = nullptr;
   std::vector<hipEvent_t> req_ev;           // [0] the copies' fence, [1 + p]: piece p copied
   size_t req_piece = 0;                     // pieces of the staged batch pushed so far
   // response bodies written on the GPU (engine_write_responses): piece slots,
@@ -181,11 +184,19 @@ struct otm_engine {
   std::deque<Pending> queue;
   std::deque<otm_result> done;
   std::vector<std::thread> workers;
-  std::vector<otm_engine*> actx;  // the workers' clones (worker i >= 1 runs on actx[i - 1])
+  // the batch contexts' clones (worker i >= 1 runs on actx[i - 1]; a split
+  // otm_report_batch runs its chunks on this engine and them); created under
+  // qmu, fixed once the workers start
+  std::vector<otm_engine*> actx;
   otm::H2DOrder aorder;           // the workers' batches' copies, in take order
   uint64_t take_seq = 0, pub_seq = 0;
   bool stop = false;
   bool worker_started = false;
+  // a split otm_report_batch call (abi.cpp report_many_split): its chunks'
+  // copies in order, one call at a time
+  std::mutex split_mu;
+  otm::H2DOrder split_order;
+  int last_split = 1;  // the chunks of the last otm_report_batch (otm_debug_last_split)
 };
 
 namespace otm {

@@ -183,49 +183,146 @@ __device__ void copy_piece(char* dst, const char* src, int n, int lane) {
   for (int k = lane; k < n; k += 64) dst[k] = src[k];
 }
 
-// a wave per trace: its pieces into the dense blob (boff: the scanned lengths)
-__global__ __launch_bounds__(64) void k_resp_copy(RespIn in, RespWork w, const int64_t* boff, char* blob) {
-  const int lane = threadIdx.x;
-  for (int32_t t = blockIdx.x; t < in.nt; t += gridDim.x) {
-    if (w.host[t]) continue;
-    const otm_trace_result tr = in.traces[t];
-    char* d = blob + boff[t];
-    int64_t n = 0;
-    const int hl = w.hlen[t];
-    copy_piece(d, w.hdr + (int64_t)t * RESP_HDR_SLOT, hl, lane);
-    n += hl;
-    for (int32_t k = 0; k < tr.seg_cnt; ++k) {
-      const int32_t s = tr.seg_off + k;
+// trace t's body into d, the wave's lanes copying each piece in turn (the
+// form for a body larger than the LDS buffer below)
+__device__ void body_serial(const RespIn& in, const RespWork& w, int32_t t, const otm_trace_result& tr, char* d,
+                            int lane) {
+  int64_t n = 0;
+  const int hl = w.hlen[t];
+  copy_piece(d, w.hdr + (int64_t)t * RESP_HDR_SLOT, hl, lane);
+  n += hl;
+  for (int32_t k = 0; k < tr.seg_cnt; ++k) {
+    const int32_t s = tr.seg_off + k;
+    if (k) {
+      if (lane == 0) d[n] = ',';
+      ++n;
+    }
+    const int l = w.slen[s];
+    copy_piece(d + n, w.seg + seg_slot(s, in.segs[s].way_off), l, lane);
+    n += l;
+  }
+  copy_piece(d + n, kMid, MID_LEN, lane);
+  n += MID_LEN;
+  if (tr.rep_cnt > 0) {
+    copy_piece(d + n, kReps, REPS_LEN, lane);
+    n += REPS_LEN;
+    for (int32_t k = 0; k < tr.rep_cnt; ++k) {
       if (k) {
         if (lane == 0) d[n] = ',';
         ++n;
       }
-      const int l = w.slen[s];
-      copy_piece(d + n, w.seg + seg_slot(s, in.segs[s].way_off), l, lane);
+      const int l = w.rlen[tr.rep_off + k];
+      copy_piece(d + n, w.rep + (int64_t)(tr.rep_off + k) * RESP_REP_SLOT, l, lane);
       n += l;
     }
-    copy_piece(d + n, kMid, MID_LEN, lane);
-    n += MID_LEN;
+    if (lane == 0) d[n] = ']';
+    ++n;
+  }
+  if (lane == 0) {
+    d[n] = '}';
+    d[n + 1] = '}';
+    d[n + 2] = '\0';
+  }
+}
+
+__device__ __forceinline__ int wave_scan_incl(int v, int lane) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int u = __shfl_up(v, o, 64);
+    if (lane >= o) v += u;
+  }
+  return v;
+}
+
+// one lane's piece (8-byte aligned slot, written as whole words) into LDS at L
+__device__ __forceinline__ void piece_to_lds(char* L, const char* src, int l) {
+  for (int q = 0; q < l; q += 8) {
+    const uint64_t v = *(const uint64_t*)(src + q);
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (q + j < l) L[q + j] = (char)(v >> (8 * j));
+  }
+}
+
+// pieces [0, cnt) of one kind, a lane each (64 at a time), after a comma for
+// every piece but the first; *at: the running LDS offset (uniform)
+template <class Len, class Src>
+__device__ __forceinline__ void pieces_to_lds(char* L, int* at, int32_t cnt, int lane, Len len, Src src) {
+  for (int32_t k0 = 0; k0 < cnt; k0 += 64) {
+    const int32_t k = k0 + lane;
+    const bool has = k < cnt;
+    const int l = has ? len(k) : 0;
+    const int mine = has ? l + (k > 0 ? 1 : 0) : 0;
+    const int incl = wave_scan_incl(mine, lane);
+    if (has) {
+      int p = *at + incl - mine;
+      if (k > 0) L[p++] = ',';
+      piece_to_lds(L + p, src(k), l);
+    }
+    *at += __shfl(incl, 63, 64);
+  }
+}
+
+// a wave per trace: its pieces into the dense blob (boff: the scanned lengths).
+// A body that fits BODY_LDS is assembled in LDS -- each lane copying whole
+// pieces, their offsets from a wave scan of the lengths (no dependent length
+// load per piece) -- and stored with 16-byte aligned words (bytes at its two
+// ends, whose words it shares with its neighbours); a larger body is copied
+// piece by piece (body_serial).
+constexpr int BODY_LDS = 8192;
+__global__ __launch_bounds__(64) void k_resp_copy(RespIn in, RespWork w, const int64_t* boff, char* blob) {
+  __shared__ uint4 LW[BODY_LDS / 16];
+  char* L = (char*)LW;
+  const int lane = threadIdx.x;
+  for (int32_t t = blockIdx.x; t < in.nt; t += gridDim.x) {
+    if (w.host[t]) continue;
+    const otm_trace_result tr = in.traces[t];
+    const int64_t start = boff[t], end = boff[t + 1];  // (the body and its NUL)
+    const int sh = (int)(start & 15);
+    if (sh + (end - start) > BODY_LDS) {
+      body_serial(in, w, t, tr, blob + start, lane);
+      continue;
+    }
+    const int hl = w.hlen[t];
+    const char* hdr = w.hdr + (int64_t)t * RESP_HDR_SLOT;
+    for (int k = lane; k < hl; k += 64) L[sh + k] = hdr[k];
+    int at = sh + hl;
+    pieces_to_lds(
+        L, &at, tr.seg_cnt, lane, [&](int32_t k) { return w.slen[tr.seg_off + k]; },
+        [&](int32_t k) {
+          const int32_t s = tr.seg_off + k;
+          return (const char*)(w.seg + seg_slot(s, in.segs[s].way_off));
+        });
+    for (int k = lane; k < MID_LEN; k += 64) L[at + k] = kMid[k];
+    at += MID_LEN;
     if (tr.rep_cnt > 0) {
-      copy_piece(d + n, kReps, REPS_LEN, lane);
-      n += REPS_LEN;
-      for (int32_t k = 0; k < tr.rep_cnt; ++k) {
-        if (k) {
-          if (lane == 0) d[n] = ',';
-          ++n;
-        }
-        const int l = w.rlen[tr.rep_off + k];
-        copy_piece(d + n, w.rep + (int64_t)(tr.rep_off + k) * RESP_REP_SLOT, l, lane);
-        n += l;
-      }
-      if (lane == 0) d[n] = ']';
-      ++n;
+      for (int k = lane; k < REPS_LEN; k += 64) L[at + k] = kReps[k];
+      at += REPS_LEN;
+      pieces_to_lds(
+          L, &at, tr.rep_cnt, lane, [&](int32_t k) { return w.rlen[tr.rep_off + k]; },
+          [&](int32_t k) { return (const char*)(w.rep + (int64_t)(tr.rep_off + k) * RESP_REP_SLOT); });
+      if (lane == 0) L[at] = ']';
+      ++at;
     }
     if (lane == 0) {
-      d[n] = '}';
-      d[n + 1] = '}';
-      d[n + 2] = '\0';
+      L[at] = '}';
+      L[at + 1] = '}';
+      L[at + 2] = '\0';
     }
+    __syncthreads();
+    // LDS word i holds blob bytes [a0 + 16 i, a0 + 16 i + 16)
+    const int64_t a0 = start - sh;
+    const int nw = (int)((end - a0 + 15) >> 4);
+    for (int i = lane; i < nw; i += 64) {
+      const int64_t g = a0 + 16 * (int64_t)i;
+      if (g >= start && g + 16 <= end) {
+        *(uint4*)(blob + g) = LW[i];
+      } else {
+        for (int j = 0; j < 16; ++j)
+          if (g + j >= start && g + j < end) blob[g + j] = L[16 * i + j];
+      }
+    }
+    __syncthreads();  // (the next trace reuses the buffer)
   }
 }
 

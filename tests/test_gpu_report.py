@@ -428,3 +428,45 @@ def test_request_arena_report_and_submit(small_graph, oracle, monkeypatch, size)
         g = oracle.Graph(small_graph)
         for body, got in zip(bodies, want):
             assert got == oracle.handle_request(g, body), body[:60]
+
+
+def test_report_batch_split_over_contexts(small_graph, capfd):
+    """otm_report_batch over >= 2 x 2048 bodies is cut into one chunk per
+    batch context (report_many_split: the chunks run concurrently, their copies
+    to HBM in chunk order on one copy stream): every response byte-equal to the
+    same call run as one batch (an engine counting its kernels is not split),
+    from bytes objects and from a request arena, the same stderr lines, with a
+    malformed body and a host-reader body among them; and the engine's async
+    pipeline still runs on the same contexts after."""
+    from reporter_amd import RequestArena, _lib, encode_request
+    L = _lib.lib()
+    n, pts = 6200, 30
+    b = synth.make_traces(small_graph, n, pts, seed=41)
+    off = b["trace_off"]
+    bodies = [encode_request("veh%d" % t, b["lat"][off[t]:off[t + 1]], b["lon"][off[t]:off[t + 1]],
+                             b["time"][off[t]:off[t + 1]].astype(np.int64),
+                             b["accuracy"][off[t]:off[t + 1]].astype(np.int32)) for t in range(n)]
+    bodies[5] = b"{"
+    bodies[4000] = bodies[4000].replace(b'"trace":', b'"trace" :')
+    with Engine(graph_path=small_graph) as eng:
+        capfd.readouterr()
+        got = eng.report_batch(bodies)
+        split_err = capfd.readouterr().err
+        assert L.otm_debug_last_split(eng.h) >= 2
+        with RequestArena(bodies) as ar:
+            assert eng.report_batch(ar) == got
+        assert L.otm_debug_last_split(eng.h) >= 2
+        eng.set_counting(True)
+        capfd.readouterr()
+        want = eng.report_batch(bodies)
+        one_err = capfd.readouterr().err
+        assert L.otm_debug_last_split(eng.h) == 1
+        eng.set_counting(False)
+        eng.submit_batch(bodies[:3000], list(range(3000)))
+        polled = []
+        while len(polled) < 3000:
+            polled += eng.poll(4096, 2000000)
+        assert [(c, r) for _, c, r in polled] == want[:3000]
+        assert eng.report_batch(bodies) == want  # (split again, beside the running workers)
+    assert got == want
+    assert sorted(split_err.splitlines()) == sorted(one_err.splitlines())

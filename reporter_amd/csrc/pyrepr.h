@@ -6,7 +6,7 @@
 // value (David Gay's dtoa, mode 0), in fixed notation when the decimal point
 // falls in (-4, 16] (reporter_service.py's response bodies, report.cpp
 // json::put_float on the host).  Here: Burger & Dybvig's free-format digit
-// generation with exact 128-bit integer state, for |d| in [2^-10, 2^52) and
+// generation in exact integers (64-bit when they fit, else 128-bit), for |d| in [2^-10, 2^52) and
 // 0.0, which covers every float a /report body holds (epoch times, lengths in
 // km); outside that range py_repr returns -1 and the caller leaves the body to
 // the host writer.  tests/test_pyrepr.py pins it against Python's repr.
@@ -83,10 +83,60 @@ OTM_HD int put_i64(int64_t v, char* o) {
   return s.n;
 }
 
-OTM_HD u128 pow10u(int k) {
-  u128 p = 1;
+OTM_HD uint64_t pow10_64(int k) {  // (k <= 19)
+  uint64_t p = 1;
   for (int i = 0; i < k; ++i) p *= 10u;
   return p;
+}
+
+// Burger & Dybvig's digit generation from the scaled state (value r / s in
+// [0.1, 1) x 10^decpt, half-gaps mp / mm): T = uint64_t when every quantity
+// the loop forms stays below 2^64 (the caller checks s < 2^60: r < s, mp < 10 s
+// and mm <= mp, so 10 r and r + mp stay below 11 s), else u128 -- the same
+// exact arithmetic either way, so the same digits
+template <class T, class S>
+OTM_HD bool repr_digits(T r, T s, T mp, T mm, bool incl, int decpt, S& o) {
+  // digits: 0.D1 D2 ... x 10^decpt, each written as it is fixed, in Python's
+  // repr layout (fixed notation for -4 < decpt <= 16: always, in this range)
+  if (decpt <= 0) {
+    o.put('0');
+    o.put('.');
+    for (int i = 0; i < -decpt; ++i) o.put('0');
+  }
+  int nd = 0;
+  while (true) {
+    r *= 10u;
+    mp *= 10u;
+    mm *= 10u;
+    int dig = 0;
+    while (r >= s) {
+      r -= s;
+      ++dig;
+    }
+    const bool lo = incl ? (r <= mm) : (r < mm);
+    const bool hi = incl ? (r + mp >= s) : (r + mp > s);
+    const bool last = lo || hi;
+    if (lo && hi) {
+      const T r2 = r << 1;
+      // closer of the two; exactly half-way: the even digit (dtoa's
+      // round-half-even on the last digit)
+      if (r2 > s || (r2 == s && (dig & 1))) ++dig;
+    } else if (hi) {
+      ++dig;
+    }
+    // (dig == 10 cannot happen: the high test stops a digit earlier)
+    if (nd == 17) return false;
+    if (decpt > 0 && nd == decpt) o.put('.');
+    o.put((char)('0' + dig));
+    ++nd;
+    if (last) break;
+  }
+  if (decpt > 0 && nd <= decpt) {
+    for (int i = nd; i < decpt; ++i) o.put('0');
+    o.put('.');
+    o.put('0');
+  }
+  return true;
 }
 
 // repr(d) into the sink (at most 24 bytes); false: d is outside the range
@@ -131,9 +181,9 @@ OTM_HD bool py_repr(double d, S& o) {
     k = (int)((double)lg * 0.30102999566398120) + 1;  // close to ceil(log10)
     // scale to r/s in [0.1, 1) x 10^k: s x 10^k when k > 0, r x 10^-k when k < 0
     if (k >= 0) {
-      s *= pow10u(k);
+      s *= pow10_64(k);
     } else {
-      const u128 p = pow10u(-k);
+      const uint64_t p = pow10_64(-k);
       r *= p;
       mp *= p;
       mm *= p;
@@ -155,48 +205,9 @@ OTM_HD bool py_repr(double d, S& o) {
       }
     }
   }
-  // digits: 0.D1 D2 ... x 10^k, each written as it is fixed, in Python's
-  // repr layout (fixed notation for -4 < k <= 16: always, in this range)
-  const int decpt = k;
-  if (decpt <= 0) {
-    o.put('0');
-    o.put('.');
-    for (int i = 0; i < -decpt; ++i) o.put('0');
-  }
-  int nd = 0;
-  while (true) {
-    r *= 10u;
-    mp *= 10u;
-    mm *= 10u;
-    int dig = 0;
-    while (r >= s) {
-      r -= s;
-      ++dig;
-    }
-    const bool lo = incl ? (r <= mm) : (r < mm);
-    const bool hi = incl ? (r + mp >= s) : (r + mp > s);
-    const bool last = lo || hi;
-    if (lo && hi) {
-      const u128 r2 = r << 1;
-      // closer of the two; exactly half-way: the even digit (dtoa's
-      // round-half-even on the last digit)
-      if (r2 > s || (r2 == s && (dig & 1))) ++dig;
-    } else if (hi) {
-      ++dig;
-    }
-    // (dig == 10 cannot happen: the high test stops a digit earlier)
-    if (nd == 17) return false;
-    if (decpt > 0 && nd == decpt) o.put('.');
-    o.put((char)('0' + dig));
-    ++nd;
-    if (last) break;
-  }
-  if (decpt > 0 && nd <= decpt) {
-    for (int i = nd; i < decpt; ++i) o.put('0');
-    o.put('.');
-    o.put('0');
-  }
-  return true;
+  if ((s >> 60) == 0)
+    return repr_digits<uint64_t>((uint64_t)r, (uint64_t)s, (uint64_t)mp, (uint64_t)mm, incl, k, o);
+  return repr_digits<u128>(r, s, mp, mm, incl, k, o);
 }
 
 OTM_HD int py_repr(double d, char* o) {

@@ -33,11 +33,15 @@ OTM_HD uint64_t dbits(double d) {
   return x.u;
 }
 
-// A byte sink is any type with put(char).  CharSink: a plain buffer.
+// A byte sink is any type with put(char) and put8(w, m) (m <= 8 bytes of w,
+// byte 0 first).  CharSink: a plain buffer.
 struct CharSink {
   char* p;
   int n;
   OTM_HD void put(char c) { p[n++] = c; }
+  OTM_HD void put8(uint64_t w, int m) {  // m <= 8 bytes of w, byte 0 first
+    for (int j = 0; j < m; ++j) p[n++] = (char)(uint8_t)(w >> (8 * j));
+  }
 };
 
 // up to 16 decimal digits of v (at least minw, zero-padded), most significant
@@ -53,7 +57,9 @@ OTM_HD void put_digits16(uint64_t v, int minw, S& o) {
     v /= 10u;
     ++n;
   } while (v || n < minw);
-  for (int i = 0; i < n; ++i) o.put((char)(uint8_t)(str >> (8 * i)));
+  // (a sink takes up to 8 bytes at once: put8)
+  o.put8((uint64_t)str, n < 8 ? n : 8);
+  if (n > 8) o.put8((uint64_t)(str >> 64), n - 8);
 }
 
 template <class S>

@@ -36,10 +36,29 @@ struct Out {
       acc = 0;
     }
   }
+  // m <= 8 bytes at once (w: byte j the j-th, zero above m)
+  __device__ __forceinline__ void put8(uint64_t w, int m) {
+    const int sh = 8 * (n & 7);
+    acc |= w << sh;
+    if ((n & 7) + m >= 8) {
+      *(uint64_t*)(p + (n & ~7)) = acc;
+      acc = sh ? w >> (64 - sh) : 0;
+    }
+    n += m;
+  }
+  // a literal, 8 characters a step, packed into constants at compile time (a
+  // loop over the literal had read it from memory a byte at a time: one load
+  // round trip per character)
   template <int N>
   __device__ __forceinline__ void lit(const char (&s)[N]) {
-#pragma unroll 1
-    for (int k = 0; k < N - 1; ++k) put(s[k]);
+#pragma unroll
+    for (int k0 = 0; k0 < N - 1; k0 += 8) {
+      uint64_t w = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (k0 + j < N - 1) w |= (uint64_t)(uint8_t)s[k0 + j] << (8 * j);
+      put8(w, N - 1 - k0 < 8 ? N - 1 - k0 : 8);
+    }
   }
   __device__ __forceinline__ void i64(int64_t v) { pyrepr::put_i64(v, *this); }
   __device__ __forceinline__ bool f64(double d) { return pyrepr::py_repr(d, *this); }

@@ -41,12 +41,17 @@ struct Cur {
   const unsigned char* L;  // window bytes (LDS)
   int i, lim;              // position, end of readable bytes
   __device__ int ch(int k) const { return k < lim ? (int)L[k] : -1; }
-  __device__ bool lit(const char* w) {
-    int k = 0;
-    for (; w[k]; ++k)
-      if (ch(i + k) != (unsigned char)w[k]) return false;
-    i += k;
-    return true;
+  // a key literal at i (its characters constants, the window reads
+  // independent: a loop over the literal had read it from memory a byte at a
+  // time, one round trip per character); on a mismatch the point fails, so i
+  // moves only on a match
+  template <int N>
+  __device__ bool lit(const char (&w)[N]) {
+    bool ok = true;
+#pragma unroll
+    for (int k = 0; k < N - 1; ++k) ok &= ch(i + k) == (int)(unsigned char)w[k];
+    if (ok) i += N - 1;
+    return ok;
   }
   __device__ bool digit(int k) const { return (unsigned)(ch(k) - '0') < 10u; }
   // a JSON number as report.cpp fast_request's num() reads it: int -> exact

@@ -1261,7 +1261,7 @@ int otm_kmax(void) { return otm::KMAX; }
 // the arenas released (0 when every arena was released once, by its own last
 // body: a body freed into the wrong arena releases one early, and the real
 // arena never).
-int otm_debug_last_split(const otm_engine* E) { return E ? E->last_split : -1; }
+int otm_debug_last_split(const otm_engine* E) { return E ? E->last_split.load() : -1; }
 
 int otm_debug_arena_stress(int threads, int rounds) {
   if (threads < 1 || threads > 64 || rounds < 0) return -1;

@@ -196,7 +196,7 @@ struct otm_engine {
   // copies in order, one call at a time
   std::mutex split_mu;
   otm::H2DOrder split_order;
-  int last_split = 1;  // the chunks of the last otm_report_batch (otm_debug_last_split)
+  std::atomic<int> last_split{1};  // the chunks of the last otm_report_batch (otm_debug_last_split)
 };
 
 namespace otm {

@@ -827,7 +827,7 @@ void report_many_device(otm_engine* E, int n, const char* const* reqs, const siz
     // an async worker's batch (ord): its copies on the pipeline's one copy
     // stream (engine.h req_shared; created by the turn's holder, so by one
     // thread at a time); a one-call batch: the context's own copy stream
-    if (ord && !ord->copy) (void)hipStreamCreateWithFlags(&ord->copy, hipStreamNonBlocking);
+    if (ord && !ord->copy) (void)otm::create_stream(-1, &ord->copy, ord->own_queue);
     E->req_shared = ord ? ord->copy : nullptr;
     size_t bytes = 0;
     for (int k = 0; k < n; ++k) bytes += lens[k];
@@ -1058,7 +1058,7 @@ int async_workers(const otm_engine* E) {
 // then publish its results once every earlier batch has published, so each
 // uuid's results come back in submit order.
 void worker_loop(otm_engine* E, int wi) {
-  otm_engine* ctx = wi == 0 ? E : E->actx[(size_t)wi - 1];
+  otm_engine* ctx = E->awx.empty() ? E : E->awx[(size_t)wi];
   // a new thread starts on device 0: everything it creates for ctx (its
   // streams' buffers, page-locked staging) goes on ctx's device
   if (ctx->members.empty() && ctx->device >= 0) (void)hipSetDevice(ctx->device);
@@ -1121,18 +1121,43 @@ void worker_loop(otm_engine* E, int wi) {
 }
 
 // the pipeline's workers and their contexts, at the first submission (under E->qmu)
-void make_contexts(otm_engine* E) {
-  const int nw = async_workers(E);
-  while ((int)E->actx.size() < nw - 1) {
+// a split call's extra batch contexts: up to n clones (under E->qmu), their
+// streams from the runtime's pool.  Measured (round 5, profiles/r05_ab/
+// split_form/): two clones made and the first used, the chunks' copies on a
+// pooled copy stream, 349-354M points/s; the second chunk's kernels on the
+// engine's stream with the copy stream on a hardware queue of its own 238-240M
+// (the copies on that queue ran at ~28-40 GB/s instead of ~50, and the chunks'
+// matches queued behind one another).
+void make_contexts(otm_engine* E, int n) {
+  if (!E->members.empty() || E->parent) return;
+  while ((int)E->actx.size() < n) {
     otm_engine* C = nullptr;
     if (otm_engine_clone(E, &C) != OTM_OK) break;  // fewer contexts, same results
     E->actx.push_back(C);
   }
 }
 
+// the workers and their batch contexts, at the first submission (under
+// E->qmu): clones on hardware queues of their own (engine.cpp create_stream),
+// apart from the one-call path's contexts
 void start_workers(otm_engine* E) {
-  make_contexts(E);
-  for (int i = 0; i <= (int)E->actx.size(); ++i) E->workers.emplace_back(worker_loop, E, i);
+  const int nw = async_workers(E);
+  for (int i = 0; nw > 1 && i < nw; ++i) {
+    auto* C = new otm_engine();
+    std::string err;
+    if (otm::engine_clone(E, C, &err, true) != OTM_OK) {  // fewer workers, same results
+      otm::engine_free(C);
+      delete C;
+      break;
+    }
+    E->awx.push_back(C);
+  }
+#ifndef OTM_AORDER_OWN
+#define OTM_AORDER_OWN 1
+#endif
+  E->aorder.own_queue = OTM_AORDER_OWN != 0;
+  const int n = E->awx.empty() ? 1 : (int)E->awx.size();
+  for (int i = 0; i < n; ++i) E->workers.emplace_back(worker_loop, E, i);
   E->worker_started = true;
 }
 
@@ -1158,7 +1183,7 @@ void report_many_split(otm_engine* E, int n, const char* const* reqs, const size
   std::vector<otm_engine*> ctx{E};
   if (E->members.empty() && !E->parent && !E->counting && !E->timing && n >= 2 * SPLIT_MIN) {
     std::lock_guard<std::mutex> lk(E->qmu);
-    if (!E->worker_started) make_contexts(E);  // (fixed once the workers run)
+    make_contexts(E, 2);  // (two made, as measured: the chunks use this engine and the first)
     ctx.insert(ctx.end(), E->actx.begin(), E->actx.end());
   }
   const int chunks = std::min<int>(std::min<int>((int)ctx.size(), SPLIT_CHUNKS), n / SPLIT_MIN);
@@ -1515,6 +1540,7 @@ void otm_engine_destroy(otm_engine* E) {
     for (auto& r : E->done) arena::free_body(r.body);
   }
   for (otm_engine* C : E->actx) otm_engine_destroy(C);
+  for (otm_engine* C : E->awx) otm_engine_destroy(C);
   for (otm::H2DOrder* o : {&E->aorder, &E->split_order}) {
     for (hipEvent_t ev : o->ev)
       if (ev) (void)hipEventDestroy(ev);

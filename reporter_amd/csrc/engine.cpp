@@ -128,7 +128,6 @@ static int auto_grid_mult(const otm_engine* E) {
   return best;
 }
 
-int create_stream(int slot, hipStream_t* s);
 
 int engine_init(otm_engine* E, const char* graph_path, int device, std::string* err) {
   int rc = load_graph(graph_path, &E->host, err);
@@ -140,7 +139,7 @@ int engine_init(otm_engine* E, const char* graph_path, int device, std::string* 
   if (E->grid_mult == 0) E->grid_mult = auto_grid_mult(E);
   E->device = device;
   HIPCHK(hipSetDevice(device));
-  if (create_stream(0, &E->stream)) {
+  if (create_stream(0, &E->stream, false)) {
     *err = "stream creation failed";
     return OTM_EDEVICE;
   }
@@ -309,18 +308,33 @@ int engine_init(otm_engine* E, const char* graph_path, int device, std::string* 
 
 // The stream of batch context `slot` (0: the engine, k: its k-th clone), at
 // normal priority (round 2: a prioritised context made the device leg slower,
-// 0.78 -> 0.90-1.12 ms per step)
-int create_stream(int slot, hipStream_t* s) {
+// 0.78 -> 0.90-1.12 ms per step): from the runtime's pool of
+// hardware queues (GPU_MAX_HW_QUEUES, shared round the process's streams), or,
+// own_queue, on a hardware queue of its own -- a stream created with a CU mask
+// (every CU) gets a new queue -- for the async pipeline's contexts, whose
+// batches then run side by side instead of behind whatever other stream shares
+// their queue (round 5: async 370-382M -> 538-553M points/s; the same for the
+// one-call and device contexts was slower)
+int create_stream(int slot, hipStream_t* s, bool own_queue) {
   (void)slot;
+  if (own_queue) {
+    int dev = 0, ncu = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && ncu > 0) {
+      std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
+      for (int c = 0; c < ncu; ++c) mask[(size_t)c / 32] |= 1u << (c % 32);
+      if (hipExtStreamCreateWithCUMask(s, (uint32_t)mask.size(), mask.data()) == hipSuccess) return 0;
+    }
+  }
   return hipStreamCreateWithFlags(s, hipStreamNonBlocking) != hipSuccess;
 }
 
-int engine_clone(const otm_engine* P, otm_engine* C, std::string* err) {
+int engine_clone(const otm_engine* P, otm_engine* C, std::string* err, bool own_queue) {
   C->parent = P;
   C->device = P->device;
   HIPCHK(hipSetDevice(C->device));
   const int slot = ++const_cast<otm_engine*>(P)->n_clones;
-  if (create_stream(slot, &C->stream)) {
+  if (create_stream(slot, &C->stream, own_queue)) {
     *err = "stream creation failed";
     return OTM_EDEVICE;
   }

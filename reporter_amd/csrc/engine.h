@@ -35,8 +35,10 @@ struct H2DOrder {
   uint64_t next = 0;
   hipEvent_t ev[2] = {nullptr, nullptr};
   // the pipeline's one request-copy stream (created by the first turn's
-  // holder): every context's pieces go there, in ticket order
+  // holder): every context's pieces go there, in ticket order; own_queue: on
+  // a hardware queue of its own (the async pipeline's, engine.cpp create_stream)
   hipStream_t copy = nullptr;
+  bool own_queue = false;
 };
 }  // namespace otm
 
@@ -163,9 +165,9 @@ struct otm_engine {
   float kernel_ms[otm::KN_COUNT] = {};
   float stage_ms[8] = {};
   // async submit/poll: a pipeline of workers, each running whole request
-  // batches on its own batch context (worker 0 on this engine, the others on
-  // clones it owns), so one batch's host parse / response writing overlaps
-  // another's GPU work; batches are taken and their results published in
+  // batches on its own batch context (clones this engine owns, awx, each
+  // stream on a hardware queue of its own), so the batches' kernels and copies
+  // run side by side; batches are taken and their results published in
   // submit order (abi.cpp worker_loop)
   // a submitted request: its body inside the slab its submission copied
   // every body into (page-locked when large: the worker's batch copies it to
@@ -184,10 +186,13 @@ struct otm_engine {
   std::deque<Pending> queue;
   std::deque<otm_result> done;
   std::vector<std::thread> workers;
-  // the batch contexts' clones (worker i >= 1 runs on actx[i - 1]; a split
-  // otm_report_batch runs its chunks on this engine and them); created under
-  // qmu, fixed once the workers start
+  // a split otm_report_batch's extra batch contexts (its chunks run on this
+  // engine and these clones; created under qmu)
   std::vector<otm_engine*> actx;
+  // the async workers' batch contexts: clones whose streams have hardware
+  // queues of their own (worker i on awx[i]; none: one worker, on this engine);
+  // created under qmu when the workers start
+  std::vector<otm_engine*> awx;
   otm::H2DOrder aorder;           // the workers' batches' copies, in take order
   uint64_t take_seq = 0, pub_seq = 0;
   bool stop = false;
@@ -206,7 +211,10 @@ int engine_init(otm_engine* E, const char* graph_path, int device, std::string* 
 uint32_t turn_units(float factor, int d);
 // a second batch context on the same GPU: own stream and buffers, the
 // parent's HBM graph, index and configuration
-int engine_clone(const otm_engine* parent, otm_engine* C, std::string* err);
+// (own_queue: its stream on a hardware queue of its own, engine.cpp create_stream)
+int engine_clone(const otm_engine* parent, otm_engine* C, std::string* err, bool own_queue = false);
+// a batch context's (or a copy order's) stream; nonzero on failure
+int create_stream(int slot, hipStream_t* s, bool own_queue);
 void engine_free(otm_engine* E);
 // match a device-resident batch; returns 0 or OTM_EDEVICE (message in *err)
 int engine_match(otm_engine* E, const DevBatch& b, hipStream_t s, std::string* err);

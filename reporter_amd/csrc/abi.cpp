@@ -1152,10 +1152,7 @@ void start_workers(otm_engine* E) {
     }
     E->awx.push_back(C);
   }
-#ifndef OTM_AORDER_OWN
-#define OTM_AORDER_OWN 1
-#endif
-  E->aorder.own_queue = OTM_AORDER_OWN != 0;
+  E->aorder.own_queue = true;  // (pooled: async 470-480M against 549-554M)
   const int n = E->awx.empty() ? 1 : (int)E->awx.size();
   for (int i = 0; i < n; ++i) E->workers.emplace_back(worker_loop, E, i);
   E->worker_started = true;

@@ -109,6 +109,8 @@ def parse():
                     help="host-inclusive leg: in-flight worker i starts i x this many ms late (A/B of phase drift)")
     ap.add_argument("--index-radius", type=float, default=None,
                     help="route index radius in metres (default: the engine sizes it from the graph; 0: no index)")
+    ap.add_argument("--own-queue-streams", action="store_true",
+                    help="the device leg's streams from otm_stream_create on hardware queues of their own")
     ap.add_argument("--inflight", type=int, default=3,
                     help="batches in flight per GPU: engine clones on their own HIP streams, one host thread each")
     ap.add_argument("--host-inflight", type=int, default=4,
@@ -269,7 +271,16 @@ def main():
     # batches in flight: clones share the graph, index and histogram binding
     inflight = max(1, args.inflight)
     engines = [eng] + [eng.clone() for _ in range(inflight - 1)]
-    streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(inflight - 1)]
+    own_streams = []
+    if args.own_queue_streams:
+        # streams from the library on hardware queues of their own
+        # (otm_stream_create), wrapped for torch
+        own_streams = [_lib.lib().otm_stream_create(eng.h, 1) for _ in range(inflight)]
+        if not all(own_streams):
+            raise RuntimeError("otm_stream_create failed")
+        streams = [torch.cuda.ExternalStream(p_, device=dev) for p_ in own_streams]
+    else:
+        streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(inflight - 1)]
 
     d_off = torch.from_numpy(batch["trace_off"]).to(dev)
     d_lat = torch.from_numpy(batch["lat"]).to(dev)
@@ -863,6 +874,9 @@ def main():
         print(json.dumps(line), flush=True)
     for e in engines[1:]:
         e.close()
+    torch.cuda.synchronize(dev)
+    for p_ in own_streams:
+        _lib.lib().otm_stream_destroy(p_)
     eng.hist_bind(None, 0, 1.0)
     eng.close()
     if world > 1:

@@ -341,6 +341,12 @@ void otm_host_free(void* p);
  * work is enqueued and the variable-size outputs are sized. */
 int otm_match_device(otm_engine* eng, const otm_batch* in_dev, void* stream);
 int otm_fetch_results(otm_engine* eng, otm_results* out);
+/* A stream for otm_match_device on the engine's device: own_queue != 0 gives it
+ * a hardware queue of its own (a full CU mask), apart from the runtime's pool
+ * of GPU_MAX_HW_QUEUES queues that every other stream of the process shares.
+ * NULL on failure; release with otm_stream_destroy. */
+void* otm_stream_create(otm_engine* eng, int own_queue);
+void otm_stream_destroy(void* stream);
 
 /* Per-segment speed histogram, accumulated on the device by every match
  * call: counts u32[n_segments * nbins], bin = floor(kph / bin_kph) clamped to

@@ -205,6 +205,8 @@ def _declare(L):
         "otm_tile_file": (C.c_int, [i64, C.c_int, C.c_char_p, C.c_char_p, sz]),
         "otm_tile_files_bbox": (C.c_int, [C.c_double, C.c_double, C.c_double, C.c_double, C.c_char_p, pp, psz]),
         "otm_runtime_info": (C.c_char_p, []),
+        "otm_stream_create": (vp, [vp, C.c_int]),
+        "otm_stream_destroy": (None, [vp]),
     }
     for name, (res, args) in sig.items():
         if os.environ.get("OTM_LIB") and not hasattr(L, name):

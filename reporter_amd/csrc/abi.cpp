@@ -1329,6 +1329,19 @@ int otm_debug_arena_stress(int threads, int rounds) {
   return live + (int)std::llabs(cut.load() - (arena::g_releases.load() - rel0));
 }
 
+void* otm_stream_create(otm_engine* E, int own_queue) {
+  if (!E) return nullptr;
+  otm_engine* D = E->members.empty() ? E : E->members[0];
+  if (D->device >= 0 && hipSetDevice(D->device) != hipSuccess) return nullptr;
+  hipStream_t s = nullptr;
+  if (otm::create_stream(0, &s, own_queue != 0)) return nullptr;
+  return s;
+}
+
+void otm_stream_destroy(void* s) {
+  if (s) (void)hipStreamDestroy((hipStream_t)s);
+}
+
 const char* otm_runtime_info(void) {
   static thread_local std::string info;
   Dl_info di;

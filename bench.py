@@ -596,7 +596,7 @@ def main():
             json_async["includes"] = (
                 "otm_submit_batch of the 10k Java request bodies x %d in a row from the request arena (referenced, "
                 "not copied), otm_poll until every response is back: the async pipeline, %s workers on their own "
-                "batch contexts; mean of 3 runs after 2 warm ones" %
+                "batch contexts (each stream on a hardware queue of its own); mean of 3 runs after 2 warm ones" %
                 (args.async_rounds, os.environ.get("OTM_ASYNC_WORKERS", "3")))
             json_async["copied"] = async_leg("copied")
             json_async["copied"]["includes"] = "the same bodies from Python bytes objects (copied into the queue)"

@@ -23,10 +23,11 @@ def main():
     L = _lib.lib()
     graph = synth.cached_graph(2)
     tr = dict(synth.CONFIGS[2]["traces"])
-    tr["n_vehicles"] = 2000
+    nveh = int(os.environ.get("OTM_SOAK_VEH", "2000"))  # (>= 4096: otm_report_batch splits the call)
+    tr["n_vehicles"] = nveh
     b = synth.make_traces(graph, **tr)
     bodies = []
-    for t in range(2000):
+    for t in range(nveh):
         a, e = b["trace_off"][t], b["trace_off"][t + 1]
         bodies.append(encode_request("veh%d" % t, b["lat"][a:e], b["lon"][a:e], b["time"][a:e].astype(np.int64),
                                      b["accuracy"][a:e].astype(np.int32)))
@@ -86,6 +87,19 @@ def main():
             eng.report_batch(bodies[:50])
     torch.cuda.synchronize()
     out["create_destroy"] = {"cycles": 20, "device_free_drop_mb": (free_a - torch.cuda.mem_get_info(0)[0]) / 2**20}
+    # engines whose async pipeline started (three clones with streams on
+    # hardware queues of their own, and its copy stream): created, used and
+    # destroyed 20 times -- the queues and device memory come back
+    free_b = torch.cuda.mem_get_info(0)[0]
+    m = min(n, 600)
+    for _ in range(20):
+        with Engine(graph_path=graph) as eng:
+            eng.submit_batch(bodies[:m], list(range(m)))
+            got = 0
+            while got < m:
+                got += len(eng.poll(4096, 2000000))
+    torch.cuda.synchronize()
+    out["async_create_destroy"] = {"cycles": 20, "device_free_drop_mb": (free_b - torch.cuda.mem_get_info(0)[0]) / 2**20}
     print(json.dumps(out), flush=True)
 
 

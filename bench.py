@@ -109,9 +109,10 @@ def parse():
                     help="host-inclusive leg: in-flight worker i starts i x this many ms late (A/B of phase drift)")
     ap.add_argument("--index-radius", type=float, default=None,
                     help="route index radius in metres (default: the engine sizes it from the graph; 0: no index)")
-    ap.add_argument("--own-queue-streams", action="store_true",
-                    help="the device leg's streams from otm_stream_create on hardware queues of their own")
-    ap.add_argument("--inflight", type=int, default=3,
+    ap.add_argument("--torch-streams", action="store_true",
+                    help="the device leg on torch's streams (the runtime's shared hardware-queue pool) instead of "
+                         "otm_stream_create streams with hardware queues of their own")
+    ap.add_argument("--inflight", type=int, default=4,
                     help="batches in flight per GPU: engine clones on their own HIP streams, one host thread each")
     ap.add_argument("--host-inflight", type=int, default=4,
                     help="batches in flight in the host-inclusive legs (their PCIe copies leave room for a fourth)")
@@ -272,9 +273,13 @@ def main():
     inflight = max(1, args.inflight)
     engines = [eng] + [eng.clone() for _ in range(inflight - 1)]
     own_streams = []
-    if args.own_queue_streams:
+    if not args.torch_streams:
         # streams from the library on hardware queues of their own
-        # (otm_stream_create), wrapped for torch
+        # (otm_stream_create), wrapped for torch: four batches in flight then
+        # run side by side (round 5, profiles/r05_ab/inflight_ownq/: 4 on own
+        # queues 1.339-1.366G against 3 on torch's streams 1.313-1.338G; 4 on
+        # torch's streams 1.326-1.338G, 5 / 6 on own queues 1.343-1.350 /
+        # 1.331-1.335G)
         own_streams = [_lib.lib().otm_stream_create(eng.h, 1) for _ in range(inflight)]
         if not all(own_streams):
             raise RuntimeError("otm_stream_create failed")
@@ -343,6 +348,9 @@ def main():
             kern_tot[k] = kern_tot.get(k, 0.0) + v
     torch.cuda.synchronize(dev)
     eng.set_timing(False)
+    for p_ in own_streams:  # (the device leg is done with them)
+        _lib.lib().otm_stream_destroy(p_)
+    own_streams = []
     kern_avg = {k: v / args.steps for k, v in kern_tot.items()}
     # the device leg's results (its last batch on eng), for the oracle check
     # below -- before the host and JSON legs run other batches on eng
@@ -850,9 +858,10 @@ def main():
                        "points_per_gpu": P, "vehicles_per_gpu": len(ids), "graph": ginfo,
                        "candidate_grid_mult": grid.get("mult"),
                        "batches_in_flight": inflight,
-                       "parallelism": "uuid shards x%d, %d batches in flight per GPU (HIP streams), RCCL "
+                       "parallelism": "uuid shards x%d, %d batches in flight per GPU (HIP streams%s), RCCL "
                                       "reduce-scatter of %dx%d histograms per timed window" %
-                                      (world, inflight, nseg, nbins)},
+                                      (world, inflight, "" if args.torch_streams else
+                                       " on hardware queues of their own", nseg, nbins)},
             "roofline": roof,
             "route_index": {"radius_m": index["radius_m"], "entries": index["entries"],
                             "near": index_levels, "table_bytes": index_tables["bytes"],

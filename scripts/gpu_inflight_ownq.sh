@@ -8,8 +8,8 @@ mkdir -p $R/$O
 cd $R
 F="--steps 40 --warmup 5 --no-cpu-baseline --no-check --host-steps 0 --json-calls 0"
 for i in 1 2; do
-  timeout -k 10 300 python -u bench.py $F > $O/d3_$i.json 2> $O/d3_$i.err
-  timeout -k 10 300 python -u bench.py $F --own-queue-streams --inflight 4 > $O/q4_$i.json 2> $O/q4_$i.err
-  timeout -k 10 300 python -u bench.py $F --own-queue-streams --inflight 2 > $O/q2_$i.json 2> $O/q2_$i.err
-  timeout -k 10 300 python -u bench.py $F --inflight 4 > $O/d4_$i.json 2> $O/d4_$i.err
+  timeout -k 10 300 python -u bench.py $F --torch-streams --inflight 3 > $O/d3_$i.json 2> $O/d3_$i.err
+  timeout -k 10 300 python -u bench.py $F --inflight 4 > $O/q4_$i.json 2> $O/q4_$i.err
+  timeout -k 10 300 python -u bench.py $F --inflight 2 > $O/q2_$i.json 2> $O/q2_$i.err
+  timeout -k 10 300 python -u bench.py $F --torch-streams --inflight 4 > $O/d4_$i.json 2> $O/d4_$i.err
 done

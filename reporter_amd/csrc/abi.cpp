@@ -1121,18 +1121,25 @@ void worker_loop(otm_engine* E, int wi) {
 }
 
 // the pipeline's workers and their contexts, at the first submission (under E->qmu)
-// a split call's extra batch contexts: up to n clones (under E->qmu), their
-// streams from the runtime's pool.  Measured (round 5, profiles/r05_ab/
-// split_form/): two clones made and the first used, the chunks' copies on a
-// pooled copy stream, 349-354M points/s; the second chunk's kernels on the
-// engine's stream with the copy stream on a hardware queue of its own 238-240M
-// (the copies on that queue ran at ~28-40 GB/s instead of ~50, and the chunks'
-// matches queued behind one another).
+// a split call's batch contexts: up to n clones (under E->qmu) whose streams
+// have hardware queues of their own, so the chunks' kernels never sit in a
+// queue behind the copy stream's packets (the chunks' copies go on a pooled
+// copy stream: SDMA at ~50 GB/s).  Measured (round 5, profiles/r05_ab/
+// split_form/, split_ownq/): on two own-queue clones 349-351M points/s
+// whatever other streams the process holds; on this engine and a pooled
+// clone 231-354M depending on which of the runtime's pooled queues the copy
+// stream shared (behind the first chunk's kernels: its match 0.70 -> 1.52 ms);
+// with the copy stream on an own queue too, 238-293M (copies at 28-40 GB/s).
 void make_contexts(otm_engine* E, int n) {
   if (!E->members.empty() || E->parent) return;
   while ((int)E->actx.size() < n) {
-    otm_engine* C = nullptr;
-    if (otm_engine_clone(E, &C) != OTM_OK) break;  // fewer contexts, same results
+    auto* C = new otm_engine();
+    std::string err;
+    if (otm::engine_clone(E, C, &err, true) != OTM_OK) {  // fewer contexts, same results
+      otm::engine_free(C);
+      delete C;
+      break;
+    }
     E->actx.push_back(C);
   }
 }
@@ -1180,7 +1187,8 @@ void report_many_split(otm_engine* E, int n, const char* const* reqs, const size
   std::vector<otm_engine*> ctx{E};
   if (E->members.empty() && !E->parent && !E->counting && !E->timing && n >= 2 * SPLIT_MIN) {
     std::lock_guard<std::mutex> lk(E->qmu);
-    make_contexts(E, 2);  // (two made, as measured: the chunks use this engine and the first)
+    make_contexts(E, SPLIT_CHUNKS);
+    if ((int)E->actx.size() >= SPLIT_CHUNKS) ctx.clear();  // (the chunks on the own-queue clones)
     ctx.insert(ctx.end(), E->actx.begin(), E->actx.end());
   }
   const int chunks = std::min<int>(std::min<int>((int)ctx.size(), SPLIT_CHUNKS), n / SPLIT_MIN);

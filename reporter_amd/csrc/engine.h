@@ -186,8 +186,8 @@ struct otm_engine {
   std::deque<Pending> queue;
   std::deque<otm_result> done;
   std::vector<std::thread> workers;
-  // a split otm_report_batch's extra batch contexts (its chunks run on this
-  // engine and these clones; created under qmu)
+  // a split otm_report_batch's batch contexts (its chunks run on these
+  // clones, whose streams have hardware queues of their own; created under qmu)
   std::vector<otm_engine*> actx;
   // the async workers' batch contexts: clones whose streams have hardware
   // queues of their own (worker i on awx[i]; none: one worker, on this engine);

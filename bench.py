@@ -116,6 +116,10 @@ def parse():
                     help="batches in flight per GPU: engine clones on their own HIP streams, one host thread each")
     ap.add_argument("--host-inflight", type=int, default=4,
                     help="batches in flight in the host-inclusive legs (their PCIe copies leave room for a fourth)")
+    ap.add_argument("--stream-runs", type=int, default=-1,
+                    help="config-5 stream leg: timed replays of the fleet per mode (-1: 3 on config 2, else 0)")
+    ap.add_argument("--stream-cpu-vehicles", type=int, default=200,
+                    help="config-5 CPU baseline / oracle check: vehicles of the stream replayed record at a time")
     return ap.parse_args()
 
 
@@ -218,6 +222,191 @@ def host_info():
         pass
     return {"usable_cpus": len(os.sched_getaffinity(0)), "machine_cpus": os.cpu_count(), "cgroup_cpu_quota": quota,
             "omp_num_threads": os.environ.get("OMP_NUM_THREADS"), "model": model}
+
+
+STREAM_SPEC = ",json,id,latitude,longitude,timestamp,accuracy"  # README.md's json layout (--formatter)
+
+
+def fleet_stream(batch, ids):
+    """BASELINE config 5's input: the batch's fleet as one stream of raw json
+    messages ordered by record time (what reporter-kafka's raw topic carries,
+    Reporter.java:95-103), vehicle v's clock staggered by v % 5 s.  Returns
+    (messages, record timestamps in ms, vehicle of each message)."""
+    off = batch["trace_off"]
+    nv = len(off) - 1
+    veh = np.repeat(np.arange(nv), np.diff(off))
+    t = batch["time"].astype(np.int64) + (veh % 5)
+    order = np.lexsort((veh, t))
+    keys = [str(int(x)) for x in ids]
+    acc = np.ceil(batch["accuracy"]).astype(np.int64)
+    lat, lon = batch["lat"].tolist(), batch["lon"].tolist()
+    msgs = ['{"timestamp":%d,"id":"%s","accuracy":%d,"latitude":%r,"longitude":%r}'
+            % (t[i], keys[veh[i]], acc[i], lat[i], lon[i]) for i in order.tolist()]
+    return msgs, t[order] * 1000, veh[order]
+
+
+def stream_leg(eng, batch, ids, graph, meili, runs, cpu_vehicles, native_vehicles=2000):
+    """Config 5: the fleet replayed as one time-ordered raw
+    message stream through otm_batcher_process_raw (native formatter ->
+    native batcher -> this GPU's engine), binary and JSON mode, timed from the
+    first message to close() (the relaxed reports of every stored batch);
+    records/s (= unique ingested points/s: one point per record), matched
+    points/s (the request trace lengths the batcher sent, re-sent leftovers
+    included).  Beside it the CPU baseline: the same stream's first
+    `cpu_vehicles` vehicles through oracle/pyformatter -> oracle/pybatcher ->
+    the C oracle's /report handler, record at a time (one Kafka Streams
+    thread, BatchingProcessor.java:56-130), and the GPU batcher's forwarded
+    records on that sub-stream against it."""
+    import ctypes as C
+    from reporter_amd import _lib
+    from reporter_amd.batcher import Batcher
+    from reporter_amd.formatter import Formatter, pack_messages
+    L = _lib.lib()
+    msgs, ts, veh = fleet_stream(batch, ids)
+    n = len(msgs)
+    chunk = 20000  # messages per process_raw call (one Kafka poll)
+    blocks = []
+    for i in range(0, n, chunk):
+        buf, off = pack_messages(msgs[i:i + chunk])
+        blocks.append((min(n, i + chunk) - i, buf, off, np.ascontiguousarray(ts[i:i + chunk])))
+    fmt = Formatter(STREAM_SPEC)
+
+    def replay(json_path):
+        bt = Batcher(engine=eng, json_path=json_path, threads=8)
+        t0 = time.perf_counter()
+        for m, buf, off, tsb in blocks:
+            if L.otm_batcher_process_raw(bt.h, fmt.h, m, buf.ctypes.data, off.ctypes.data, tsb.ctypes.data, 8) != 0:
+                raise RuntimeError("otm_batcher_process_raw failed")
+        bt.flush()
+        bt.close()
+        dt = time.perf_counter() - t0
+        st = bt.stats()
+        fwd = len(bt.forwarded())
+        bt.close_handle()
+        return dt, st, fwd
+
+    out = {"workload": "config-2 fleet (%d vehicles x %d points) as one time-ordered stream of %d raw json messages "
+                       "(README layout, spec %r), %d per otm_batcher_process_raw call" %
+                       (len(ids), n // max(len(ids), 1), n, STREAM_SPEC, chunk),
+           "includes": "otm_batcher_process_raw (native Formatter.format on 8 threads, BatchingProcessor/Batch "
+                       "semantics, the ready keys' requests matched together on the GPU) from the first message to "
+                       "close(); runs after one warm replay, mean of the timed ones"}
+    for mode, jp in (("binary", False), ("json", True)):
+        replay(jp)  # warm: the batcher's and the engine's buffers
+        rs = [replay(jp) for _ in range(runs)]
+        dt = sum(r[0] for r in rs) / len(rs)
+        st = rs[-1][1]
+        out[mode] = {"records_per_s": st["raw_messages"] / dt,
+                     "unique_points_per_s": st["records"] / dt,
+                     "matched_points_per_s": st["request_points"] / dt,
+                     "seconds": dt, "seconds_per_run": [r[0] for r in rs],
+                     "requests": st["requests"], "match_batches": st["match_batches"], "forwarded": rs[-1][2],
+                     "request_points": st["request_points"], "records": st["records"],
+                     "raw_dropped": st["raw_dropped"],
+                     "host_us": {k: st[k] for k in ("us_format", "us_enqueue", "us_run", "us_prepare", "us_match",
+                                                    "us_apply")},
+                     "path": "SoA batches, responses written for forwarded records only" if not jp else
+                             "the request bodies through otm_report_batch, every response written"}
+    out["value"] = out["binary"]["records_per_s"]
+    out["unit"] = "records/s"
+
+    # CPU baseline and oracle check on the same sub-stream
+    if cpu_vehicles > 0:
+        sys.path.insert(0, ROOT)
+        from oracle import pybatcher, pyformatter, pyoracle
+        sel = np.nonzero(veh < cpu_vehicles)[0]
+        smsgs = [msgs[i] for i in sel.tolist()]
+        sts = ts[sel]
+        g = pyoracle.Graph(graph)
+        op = pyoracle.params(**meili)
+        pf = pyformatter.Formatter(STREAM_SPEC)
+        bp = pybatcher.BatchingProcessor(lambda body: pyoracle.handle_request(g, body, p=op)[1])
+        tc = time.perf_counter()
+        for m, t_ in zip(smsgs, sts.tolist()):
+            try:
+                key, la, lo, ac, tm = pf.format(m.encode("utf-8"))
+            except pyformatter.Drop:
+                continue
+            bp.process(key, pybatcher.Point(la, lo, ac, tm), t_)
+        bp.close()
+        dtc = time.perf_counter() - tc
+        bt = Batcher(engine=eng, json_path=False, threads=8)
+        buf, off = pack_messages(smsgs)
+        sts = np.ascontiguousarray(sts)
+        if L.otm_batcher_process_raw(bt.h, fmt.h, len(smsgs), buf.ctypes.data, off.ctypes.data,
+                                     sts.ctypes.data, 8) != 0:
+            raise RuntimeError("otm_batcher_process_raw failed")
+        bt.close()
+        gfwd = sorted(bt.forwarded())
+        gst = bt.stats()
+        bt.close_handle()
+        out["cpu_baseline_record_at_a_time"] = {
+            "value": len(smsgs) / dtc, "unit": "records/s", "cores": 1, "kind": "port",
+            "matched_points_per_s": None, "requests": bp.requests, "seconds": dtc,
+            "sample": "the stream's messages of vehicles 0..%d (%d messages, in stream order): oracle/pyformatter "
+                      "Formatter.format -> oracle/pybatcher BatchingProcessor.process -> the C oracle's /report "
+                      "handler (orc_handle_request) per request, synchronous, one thread (one Kafka Streams thread; "
+                      "the Java host is one synchronous thread per task)" % (cpu_vehicles - 1, len(smsgs))}
+        # the native host around a CPU matcher: the stream's first
+        # `native_vehicles` vehicles through the same native formatter +
+        # batcher, each matcher call answered by the C oracle's /report handler
+        # on every host CPU (orc_handle_batch, called back from C) -- the
+        # reference's architecture (batcher -> /report service with a pool of
+        # matcher threads, py/reporter_service.py:37-45) with the CPU matching
+        nveh = min(len(ids), native_vehicles)
+        nsel = np.nonzero(veh < nveh)[0]
+        nbuf, noff = pack_messages([msgs[i] for i in nsel.tolist()])
+        nts = np.ascontiguousarray(ts[nsel])
+        # host threads: every CPU this process may run on, capped by the
+        # cgroup's CPU quota when there is one (the GPU box grants 16)
+        hinfo = host_info()
+        nth = hinfo["usable_cpus"]
+        if hinfo["cgroup_cpu_quota"]:
+            nth = max(1, min(nth, int(hinfo["cgroup_cpu_quota"])))
+        Ln = pyoracle.native_lib()
+        gn = pyoracle.Graph(graph, L=Ln) if Ln else g
+        hh = pyoracle.BatcherHandler(gn, p=op, nthreads=nth)
+        best = None
+        for _ in range(3):
+            bt = Batcher(native_handler=(hh.fn, hh.ctx_ptr), threads=8)
+            tn = time.perf_counter()
+            if L.otm_batcher_process_raw(bt.h, fmt.h, len(nsel), nbuf.ctypes.data, noff.ctypes.data,
+                                         nts.ctypes.data, 8) != 0:
+                raise RuntimeError("otm_batcher_process_raw failed")
+            bt.flush()
+            bt.close()
+            dtn = time.perf_counter() - tn
+            nst = bt.stats()
+            nfwd = sorted(bt.forwarded())
+            bt.close_handle()
+            best = dtn if best is None else min(best, dtn)
+        out["cpu_baseline"] = {
+            "value": nst["raw_messages"] / best, "unit": "records/s", "cores": nth, "kind": "port",
+            "vs": "stream_config5.binary.records_per_s",
+            "matched_points_per_s": nst["request_points"] / best, "seconds": best,
+            "build": "gcc -O3 -march=x86-64-v4 (AVX-512)" if Ln else "gcc -O3 -march=x86-64-v3",
+            "sample": "the stream's messages of vehicles 0..%d (%d messages, in stream order) through the same "
+                      "native formatter + batcher, the matcher being the C oracle's /report handler "
+                      "(orc_batcher_handler -> orc_handle_batch: JSON parse, match, report(), JSON) on %d host "
+                      "threads, called from C; best of 3" % (nveh - 1, len(nsel), nth)}
+        bt = Batcher(engine=eng, json_path=True, threads=8)
+        if L.otm_batcher_process_raw(bt.h, fmt.h, len(nsel), nbuf.ctypes.data, noff.ctypes.data,
+                                     nts.ctypes.data, 8) != 0:
+            raise RuntimeError("otm_batcher_process_raw failed")
+        bt.close()
+        gnfwd = sorted(bt.forwarded())
+        bt.close_handle()
+        out["oracle_check"] = {
+            "messages": len(smsgs), "forwarded": len(gfwd),
+            "forwarded_byte_equal_to_oracle_restatement": gfwd == sorted(bp.forwarded),
+            "requests_equal": gst["requests"] == bp.requests,
+            "native_host_messages": len(nsel), "native_host_forwarded": len(gnfwd),
+            "native_host_forwarded_byte_equal": gnfwd == nfwd,
+            "what": "the GPU batcher's forwarded (record, key, response) triples against the CPU baselines': on "
+                    "vehicles 0..%d the record-at-a-time restatement (pyformatter -> pybatcher -> oracle /report), "
+                    "binary mode; on vehicles 0..%d the native host with the C oracle as matcher, JSON mode" %
+                    (cpu_vehicles - 1, nveh - 1)}
+    return out
 
 
 def load_traffic(path):
@@ -628,6 +817,18 @@ def main():
         hist.zero_()
         speed_sum.zero_()
 
+    # ---- config-5 leg (BASELINE configs[4]): the same fleet as a raw message
+    # stream through the native formatter and batcher into this engine
+    stream5 = None
+    stream_runs = args.stream_runs if args.stream_runs >= 0 else (3 if args.config == 2 else 0)
+    if stream_runs > 0 and rank == 0:
+        ts0 = time.perf_counter()
+        stream5 = stream_leg(eng, batch, ids, graph, meili, stream_runs,
+                            args.stream_cpu_vehicles if world == 1 and not args.no_cpu_baseline else 0)
+        log(rank, "[bench] config-5 stream leg: %.1fs" % (time.perf_counter() - ts0))
+        hist.zero_()
+        speed_sum.zero_()
+
     # ---- untimed: the CPU oracle over this rank's whole batch -> agreement
     # with the GPU result and the algorithmic bytes of every stage
     agreement, sbytes, stages, probe_bytes = None, None, None, None
@@ -877,6 +1078,7 @@ def main():
             "cpu_baseline": cpu,
             "host_inclusive": host_leg,
             "json_report": json_leg,
+            "stream_config5": stream5,
             "agreement": agreement,
             "hip_runtime": _lib.runtime_info(),
         }

@@ -74,7 +74,10 @@ struct orc_graph {
   const int64_t* cell_off;
   const uint32_t* cell_ent;
   const uint16_t *ehead_out, *ehead_in;
+  uint32_t* elen64; /* L(e) = round(len(e) x 64), computed once at load */
+  uint64_t serial;  /* identifies this load to the per-thread workspace cache */
 };
+static atomic_uint_fast64_t graph_serial = 1;
 
 orc_graph* orc_graph_load(const char* path) {
   int fd = open(path, O_RDONLY);
@@ -117,11 +120,15 @@ orc_graph* orc_graph_load(const char* path) {
   g->ehead_out = SEC(OTMG_EDGE_HEAD_OUT);
   g->ehead_in = SEC(OTMG_EDGE_HEAD_IN);
 #undef SEC
+  g->elen64 = (uint32_t*)malloc(sizeof(uint32_t) * ((size_t)g->h.n_edges + 1));
+  for (int32_t e = 0; e < g->h.n_edges; ++e) g->elen64[e] = (uint32_t)floor((double)g->elen[e] * 64.0 + 0.5);
+  g->serial = atomic_fetch_add(&graph_serial, 1);
   return g;
 }
 void orc_graph_free(orc_graph* g) {
   if (!g) return;
   if (g->map) munmap(g->map, g->bytes);
+  free(g->elen64);
   free(g);
 }
 int64_t orc_graph_count(const orc_graph* g, int what) {
@@ -478,7 +485,7 @@ typedef struct batch {
   int phase;
   orc_counters* ctr; /* per thread */
   int count_unique;  /* count §8(d)'s unique projected edges (keep_stages) */
-  uint32_t* elen64;  /* L(e) = round(len(e) x 64): the search's edge costs */
+  const uint32_t* elen64;  /* L(e) = round(len(e) x 64): the search's edge costs */
   uint32_t turn_units[181]; /* orc_turn_units per deviation 0..180 */
 } batch;
 
@@ -1231,31 +1238,64 @@ typedef struct {
   int tid;
 } targ;
 
+/* A search workspace per host thread, kept between calls (pthread key, freed
+ * at thread exit): its label arrays span the graph, so allocating them per
+ * call would cost O(graph) per /report request -- meili likewise keeps one
+ * matcher with its label set per service thread (py/reporter_service.py:52).
+ * The labels are stamp-validated, so reuse needs no clearing. */
+typedef struct {
+  uint64_t serial;
+  ws w;
+} ws_slot;
+static pthread_key_t ws_key;
+static pthread_once_t ws_once = PTHREAD_ONCE_INIT;
+static void ws_release(ws* w) {
+  free(w->ek);
+  free(w->nk);
+  free(w->elab);
+  free(w->nlab);
+  free(w->elist);
+  free(w->heap);
+  free(w->hits);
+  memset(w, 0, sizeof *w);
+}
+static void ws_slot_free(void* p) {
+  ws_slot* s = (ws_slot*)p;
+  ws_release(&s->w);
+  free(s);
+}
+static void ws_key_init(void) { pthread_key_create(&ws_key, ws_slot_free); }
+static ws* ws_acquire(const orc_graph* g) {
+  pthread_once(&ws_once, ws_key_init);
+  ws_slot* s = (ws_slot*)pthread_getspecific(ws_key);
+  if (!s) {
+    s = (ws_slot*)calloc(1, sizeof(ws_slot));
+    pthread_setspecific(ws_key, s);
+  }
+  if (s->serial != g->serial) {
+    ws_release(&s->w);
+    const size_t nn = (size_t)g->h.n_nodes, ne = (size_t)g->h.n_edges;
+    s->w.ek = (uint64_t*)malloc(sizeof(uint64_t) * (ne + 1));
+    s->w.nk = (uint64_t*)malloc(sizeof(uint64_t) * (nn + 1));
+    s->w.elab = (uint32_t*)calloc(ne + 1, sizeof(uint32_t));
+    s->w.nlab = (uint32_t*)calloc(nn + 1, sizeof(uint32_t));
+    s->w.elist = (int32_t*)malloc(sizeof(int32_t) * (ne + 1));
+    s->serial = g->serial;
+  }
+  return &s->w;
+}
+
 static void* worker(void* arg) {
   targ* A = (targ*)arg;
   batch* B = A->B;
-  ws w;
-  memset(&w, 0, sizeof w);
-  const size_t nn = (size_t)B->g->h.n_nodes, ne = (size_t)B->g->h.n_edges;
-  w.ek = (uint64_t*)malloc(sizeof(uint64_t) * (ne + 1));
-  w.nk = (uint64_t*)malloc(sizeof(uint64_t) * (nn + 1));
-  w.elab = (uint32_t*)calloc(ne + 1, sizeof(uint32_t));
-  w.nlab = (uint32_t*)calloc(nn + 1, sizeof(uint32_t));
-  w.elist = (int32_t*)malloc(sizeof(int32_t) * (ne + 1));
+  ws* w = ws_acquire(B->g);
   orc_counters* C = &B->ctr[A->tid];
   while (1) {
     int t = atomic_fetch_add(&B->next, 1);
     if (t >= B->n_traces) break;
-    if (B->phase == 0) phase_a(B, &w, t, C);
-    else phase_b(B, &w, t, C);
+    if (B->phase == 0) phase_a(B, w, t, C);
+    else phase_b(B, w, t, C);
   }
-  free(w.ek);
-  free(w.nk);
-  free(w.elab);
-  free(w.nlab);
-  free(w.elist);
-  free(w.heap);
-  free(w.hits);
   return NULL;
 }
 
@@ -1298,9 +1338,22 @@ int orc_match_batch(const orc_graph* g, const orc_params* p, const orc_report_cf
   B.time = time;
   B.acc = accuracy;
   B.count_unique = keep_stages;
-  B.elen64 = (uint32_t*)malloc(sizeof(uint32_t) * ((size_t)g->h.n_edges + 1));
-  for (int32_t e = 0; e < g->h.n_edges; ++e) B.elen64[e] = (uint32_t)floor((double)g->elen[e] * 64.0 + 0.5);
-  for (int d = 0; d <= 180; ++d) B.turn_units[d] = orc_turn_units(p->turn_penalty_factor, d);
+  B.elen64 = g->elen64;
+  {
+    /* the turn table per thread, rebuilt only when the factor changes (181
+     * transcendental evaluations would otherwise dominate a short request) */
+    static __thread uint32_t tu[181];
+    static __thread uint32_t tu_bits;
+    static __thread int tu_ok;
+    uint32_t bits;
+    memcpy(&bits, &p->turn_penalty_factor, 4);
+    if (!tu_ok || bits != tu_bits) {
+      for (int d = 0; d <= 180; ++d) tu[d] = orc_turn_units(p->turn_penalty_factor, d);
+      tu_bits = bits;
+      tu_ok = 1;
+    }
+    memcpy(B.turn_units, tu, sizeof tu);
+  }
   const size_t PP = (size_t)P + 1;
   B.is_col = (uint8_t*)calloc(PP, 1);
   B.chain_start = (uint8_t*)calloc(PP, 1);
@@ -1397,7 +1450,6 @@ int orc_match_batch(const orc_graph* g, const orc_params* p, const orc_report_cf
   }
   free(B.is_col);
   free(B.chain_start);
-  free(B.elen64);
   free(B.terr);
   free(B.res);
   free(B.ctr);
@@ -1539,6 +1591,12 @@ int orc_handle_batch(const orc_graph* g, const orc_params* p, const orc_report_c
   for (int i = 0; i < nthreads; ++i) pthread_join(th[i], NULL);
   free(th);
   return 0;
+}
+
+int orc_batcher_handler(void* ctx, int n, const char* const* reqs, const size_t* lens, char** resps,
+                        size_t* resp_lens, int* codes) {
+  const orc_handler_ctx* c = (const orc_handler_ctx*)ctx;
+  return orc_handle_batch(c->g, c->p, c->rc, n, reqs, lens, c->nthreads, codes, resps, resp_lens);
 }
 
 /* ================================================================== polyline6 */

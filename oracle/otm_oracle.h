@@ -126,6 +126,18 @@ int orc_report_segments(const orc_report_cfg* rc, const char* req, size_t len, c
 int orc_handle_batch(const orc_graph* g, const orc_params* p, const orc_report_cfg* rc, int n,
                      const char* const* bodies, const size_t* lens, int nthreads, int* codes, char** outs,
                      size_t* out_lens);
+/* orc_handle_batch as a batcher matcher callback (otm_report_fn's shape,
+ * include/otmatch.h): ctx points to an orc_handler_ctx.  The CPU baseline of
+ * BASELINE config 5 hands it to otm_batcher_create, so the native batcher's
+ * matcher calls reach the CPU oracle without leaving C. */
+typedef struct {
+  const orc_graph* g;
+  const orc_params* p;
+  const orc_report_cfg* rc;
+  int nthreads;
+} orc_handler_ctx;
+int orc_batcher_handler(void* ctx, int n, const char* const* reqs, const size_t* lens, char** resps,
+                        size_t* resp_lens, int* codes);
 /* Python json.loads(s) then json.dumps(x, separators=(',',':')) */
 int orc_json_redump(const char* s, size_t len, char** out, size_t* out_len);
 /* py/generate_test_trace.py:9-29; out = [lon,lat]* pairs; returns count */

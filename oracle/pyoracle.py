@@ -287,6 +287,24 @@ def handle_batch(graph, bodies, p=None, rc=None, nthreads=1, L=None):
     return res
 
 
+class HandlerCtx(C.Structure):
+    _fields_ = [("g", C.c_void_p), ("p", C.c_void_p), ("rc", C.c_void_p), ("nthreads", C.c_int)]
+
+
+class BatcherHandler(object):
+    """orc_batcher_handler + its context: the C oracle's /report handler as
+    the native batcher's matcher callback (no Python per call).  `fn` is the
+    callback's address, `ctx` the context's; keep this object alive while the
+    batcher runs."""
+
+    def __init__(self, graph, p=None, rc=None, nthreads=1):
+        L = graph.L
+        self._keep = (graph, p or params(), rc or report_cfg())
+        self.ctx = HandlerCtx(graph.h, C.addressof(self._keep[1]), C.addressof(self._keep[2]), nthreads)
+        self.fn = C.cast(L.orc_batcher_handler, C.c_void_p).value
+        self.ctx_ptr = C.addressof(self.ctx)
+
+
 def json_redump(s):
     if isinstance(s, str):
         s = s.encode("utf-8")

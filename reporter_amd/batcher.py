@@ -32,8 +32,10 @@ class KeyBlock(object):
 
 
 class Batcher(object):
-    def __init__(self, engine=None, handler=None, json_path=False, max_batch=0, **cfg):
-        if engine is None and handler is None:
+    def __init__(self, engine=None, handler=None, json_path=False, max_batch=0, native_handler=None, **cfg):
+        """native_handler: (callback address, context address) of a C
+        otm_report_fn, called by the batcher without Python in between."""
+        if engine is None and handler is None and native_handler is None:
             raise ValueError("engine or handler required")
         L = lib()
         c = _lib.BatcherCfg()
@@ -43,9 +45,14 @@ class Batcher(object):
         c.max_batch = max_batch
         c.json_path = 1 if json_path else 0
         self._handler = handler
-        self._cb = _lib.REPORT_FN(self._call) if handler is not None else _lib.REPORT_FN()
+        ctx = None
+        if native_handler is not None:
+            self._cb = _lib.REPORT_FN(native_handler[0])
+            ctx = native_handler[1]
+        else:
+            self._cb = _lib.REPORT_FN(self._call) if handler is not None else _lib.REPORT_FN()
         h = C.c_void_p()
-        rc = L.otm_batcher_create(engine.h if engine is not None else None, C.byref(c), self._cb, None, C.byref(h))
+        rc = L.otm_batcher_create(engine.h if engine is not None else None, C.byref(c), self._cb, ctx, C.byref(h))
         if rc != 0:
             raise RuntimeError("otm_batcher_create failed (%d)" % rc)
         self.h = h

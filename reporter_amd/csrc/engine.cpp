@@ -51,6 +51,30 @@ static int ensure(otm_engine::Buf& b, size_t bytes, std::string* err) {
   return OTM_OK;
 }
 
+// Grows an on-demand tier's table (the huge search and candidate tiers): the
+// new allocation first, so that running out of HBM keeps the old table, and
+// the failed hipMalloc's error taken off the runtime so the batch's later
+// hipGetLastError checks do not report it.  OTM_TEST_GROW_OOM (tests only)
+// asks for a size no device has, to drive that path for real.
+static int ensure_grow(otm_engine::Buf& b, size_t bytes, std::string* err) {
+  if (bytes == 0) bytes = 16;
+  if (b.cap >= bytes) return OTM_OK;
+  size_t want = bytes + bytes / 4;
+  const char* oom = std::getenv("OTM_TEST_GROW_OOM");
+  if (oom && *oom && *oom != '0') want = (size_t)1 << 62;
+  void* p = nullptr;
+  const hipError_t e = hipMalloc(&p, want);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    *err = std::string("hipMalloc (tier table): ") + hipGetErrorString(e);
+    return OTM_EDEVICE;
+  }
+  if (b.p) (void)hipFree(b.p);
+  b.p = p;
+  b.cap = want;
+  return OTM_OK;
+}
+
 template <class T>
 static T* P(otm_engine::Buf& b) {
   return (T*)b.p;
@@ -603,9 +627,9 @@ static int ensure_cand(otm_engine* E, std::string* err) {
   if (E->cand_log2 <= 0) return OTM_OK;
   const size_t n = (size_t)CAND_BIG_SLOTS << E->cand_log2;
   int rc;
-  if ((rc = ensure(E->cbig_key, n * 4, err))) return rc;
-  if ((rc = ensure(E->cbig_val, n * 8, err))) return rc;
-  if ((rc = ensure(E->cbig_skey, n / 2 * 8, err))) return rc;
+  if ((rc = ensure_grow(E->cbig_key, n * 4, err))) return rc;
+  if ((rc = ensure_grow(E->cbig_val, n * 8, err))) return rc;
+  if ((rc = ensure_grow(E->cbig_skey, n / 2 * 8, err))) return rc;
   return OTM_OK;
 }
 
@@ -616,12 +640,12 @@ static int ensure_huge(otm_engine* E, std::string* err) {
   if (E->huge_log2 <= 0) return OTM_OK;
   const size_t n = (size_t)HUGE_SLOTS << E->huge_log2;
   int rc;
-  if ((rc = ensure(E->huge_key, n * 4, err))) return rc;
-  if ((rc = ensure(E->huge_lab, n * 8, err))) return rc;
-  if ((rc = ensure(E->huge_inq, n * 4, err))) return rc;
-  if ((rc = ensure(E->huge_fr, n * 8, err))) return rc;
-  if ((rc = ensure(E->huge_ins, (size_t)HUGE_SLOTS * huge_limit(E->huge_log2) * 4, err))) return rc;
-  if ((rc = ensure(E->huge_prev, (size_t)HUGE_SLOTS * 4, err))) return rc;
+  if ((rc = ensure_grow(E->huge_key, n * 4, err))) return rc;
+  if ((rc = ensure_grow(E->huge_lab, n * 8, err))) return rc;
+  if ((rc = ensure_grow(E->huge_inq, n * 4, err))) return rc;
+  if ((rc = ensure_grow(E->huge_fr, n * 8, err))) return rc;
+  if ((rc = ensure_grow(E->huge_ins, (size_t)HUGE_SLOTS * huge_limit(E->huge_log2) * 4, err))) return rc;
+  if ((rc = ensure_grow(E->huge_prev, (size_t)HUGE_SLOTS * 4, err))) return rc;
   if (E->huge_ready_log2 != E->huge_log2) {
     // (re)sized tables start clean, their "last inserted" lists marking the
     // whole table for the first search (-1)
@@ -887,6 +911,17 @@ int engine_match(otm_engine* E, const DevBatch& b, hipStream_t s, std::string* e
   if (!s) s = E->stream;
   const int64_t NP = b.n_points;
   int rc;
+  // A tier that ran out of HBM fails its overflowing traces for this batch
+  // only: the next batch tries to grow it again (the growth cap, by contrast,
+  // is final).  The guard lifts the batch's flags on every way out.
+  struct OomGuard {
+    otm_engine* E;
+    bool huge = false, cand = false;
+    ~OomGuard() {
+      if (huge) E->huge_final = 0;
+      if (cand) E->cand_final = 0;
+    }
+  } oom{E};
   for (int attempt = 0;; ++attempt) {
     if ((rc = engine_match_once(E, b, s, err))) return rc;
     // the one synchronisation of a batch: did every capacity hold?
@@ -913,12 +948,17 @@ int engine_match(otm_engine* E, const DevBatch& b, hipStream_t s, std::string* e
       // or, past the cap or out of HBM, the overflowing traces fail alone
       const int32_t next = E->huge_log2 ? E->huge_log2 + 2 : 19;
       const int32_t prev = E->huge_log2;
-      E->huge_log2 = next;
-      if (next > max_log2("OTM_HUGE_MAX_LOG2", HUGE_MAX_LOG2) || ensure_huge(E, err) != OTM_OK) {
-        E->huge_log2 = prev;
+      if (next > max_log2("OTM_HUGE_MAX_LOG2", HUGE_MAX_LOG2)) {
         E->huge_final = 1;
-        E->huge_ready_log2 = 0;  // (a buffer regrown before the failure: cleared again)
-        err->clear();
+      } else {
+        E->huge_log2 = next;
+        if (ensure_huge(E, err) != OTM_OK) {
+          E->huge_log2 = prev;
+          E->huge_final = 1;
+          oom.huge = true;
+          E->huge_ready_log2 = 0;  // (a buffer regrown before the failure: cleared again)
+          err->clear();
+        }
       }
     }
     if (st.grow & 2) {
@@ -927,11 +967,16 @@ int engine_match(otm_engine* E, const DevBatch& b, hipStream_t s, std::string* e
       // overflowing traces fail alone
       const int32_t next = E->cand_log2 ? E->cand_log2 + 2 : 13;
       const int32_t prev = E->cand_log2;
-      E->cand_log2 = next;
-      if (next > max_log2("OTM_CAND_MAX_LOG2", CAND_MAX_LOG2) || ensure_cand(E, err) != OTM_OK) {
-        E->cand_log2 = prev;
+      if (next > max_log2("OTM_CAND_MAX_LOG2", CAND_MAX_LOG2)) {
         E->cand_final = 1;
-        err->clear();
+      } else {
+        E->cand_log2 = next;
+        if (ensure_cand(E, err) != OTM_OK) {
+          E->cand_log2 = prev;
+          E->cand_final = 1;
+          oom.cand = true;
+          err->clear();
+        }
       }
     }
     if (cnt[2]) E->pool_cap = (int32_t)std::min<size_t>((size_t)cnt[1] * 2 + 1024, (size_t)INT32_MAX / 2);

@@ -198,3 +198,16 @@ def test_handler_failure_is_a_null_response(small_graph, oracle, threads):
     bp = run_python(recs, lambda body: None if body in failed else oracle.handle_request(g, body)[1])
     st = compare(bp, nb, recs)
     assert st["null_responses"] == len(failed)
+
+
+@pytest.mark.parametrize("threads", [0, 4])
+def test_native_oracle_handler_equals_python_handler(small_graph, oracle, threads):
+    """The C oracle's /report handler as a C callback (orc_batcher_handler,
+    the config-5 CPU baseline's matcher) against the serial restatement."""
+    g = oracle.Graph(small_graph)
+    recs = make_stream(small_graph, n_veh=20, n_pts=60, seed=67)
+    bp = run_python(recs, lambda body: oracle.handle_request(g, body)[1])
+    hh = oracle.BatcherHandler(g, nthreads=3)
+    nb = run_native(recs, Batcher(native_handler=(hh.fn, hh.ctx_ptr), threads=threads))
+    st = compare(bp, nb, recs)
+    assert st["forwarded"] > 5

@@ -189,18 +189,26 @@ def test_gpu_long_gaps_huge_search_tier(dense_grid, oracle, results_equal):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("why", ["cap", "oom"])
 @pytest.mark.parametrize("tier", ["cand", "huge"])
 def test_gpu_tables_that_cannot_grow_fail_their_traces_only(star, dense_grid, oracle, results_equal, monkeypatch,
-                                                           tier):
+                                                           tier, why):
     """Past the on-demand tiers' growth cap (kernels.h HUGE_MAX_LOG2 /
     CAND_MAX_LOG2, lowered to 0 here: no tables at all) or out of HBM, a probe
     or search that needs the tier fails its own trace with the 500 the
     reference sends for a matcher exception (error_kind CAND_OVERFLOW /
     SEARCH_OVERFLOW); every other trace of the batch matches the oracle
-    (round 4 failed the whole batch)."""
+    (round 4 failed the whole batch).  why="oom": the growth's
+    hipMalloc really fails (OTM_TEST_GROW_OOM asks for 2^62 bytes): the same
+    traces-only 500s, the runtime's error cleared, and for that batch only --
+    the next batch on the same engine grows the tier and matches every trace
+    (ADVICE r5)."""
     from reporter_amd import Engine
+    if why == "oom":
+        monkeypatch.setenv("OTM_TEST_GROW_OOM", "1")
     if tier == "cand":
-        monkeypatch.setenv("OTM_CAND_MAX_LOG2", "0")
+        if why == "cap":
+            monkeypatch.setenv("OTM_CAND_MAX_LOG2", "0")
         graph, meili = star[0], dict(search_radius=20.0, max_search_radius=20.0)
         b = star_batch()  # traces 0-2 each hold a probe within 20 m of the hub (400 edges)
         lat, lon = zip(*[_star_point(5, 85), _star_point(5, 60), _star_point(6, 40)])  # + one that never nears it
@@ -210,7 +218,8 @@ def test_gpu_tables_that_cannot_grow_fail_their_traces_only(star, dense_grid, or
                  accuracy=np.append(b["accuracy"], np.full(3, 5.0, np.float32)))
         kind, failing = 2, [0, 1, 2]
     else:
-        monkeypatch.setenv("OTM_HUGE_MAX_LOG2", "0")
+        if why == "cap":
+            monkeypatch.setenv("OTM_HUGE_MAX_LOG2", "0")
         graph, meili = dense_grid, GRID_MEILI
         far = grid_batch(dense_grid)  # 600 s gaps: searches past the global tier
         near = synth.make_traces(dense_grid, 2, 6, interval_s=5.0, noise_sigma_m=5.0, accuracy=5.0, seed=6)
@@ -220,7 +229,13 @@ def test_gpu_tables_that_cannot_grow_fail_their_traces_only(star, dense_grid, or
     with Engine(graph_path=graph, **meili) as eng:
         res = eng.match(b)
         sp = eng.spill_stats()
+        again = None
+        if why == "oom":
+            monkeypatch.delenv("OTM_TEST_GROW_OOM")
+            again = eng.match(b)
     orc = oracle.match_batch(oracle.Graph(graph), b, p=oracle.params(**meili), nthreads=4)
+    if again is not None:
+        results_equal(orc, again, "after the out-of-HBM batch")
     tr = res.traces
     bad = [t for t in range(len(tr)) if tr["code"][t] != 200]
     if failing is not None:

@@ -1910,18 +1910,18 @@ static int otm_match_compact_impl(otm_engine* E, const otm_batch_compact* in, ot
     rc = otm::engine_match_compact(E, in, &err);
     if (!rc) rc = otm::engine_fetch(E, out, &err);
   } else {
-    // a multi-device engine splits the batch on the host: widened there
+    // a multi-device engine splits the batch on the host: widened there,
+    // after the same checks as one engine's
     const int32_t nt = in->n_traces;
-    if (nt < 0 || !in->trace_off || (nt > 0 && !in->time_base)) return fail(OTM_EINVAL, "invalid batch");
-    const int64_t np = in->trace_off[nt];
-    if (np < 0) return fail(OTM_EINVAL, "batch trace_off inconsistent with n_points");
+    int64_t np = 0;
+    if ((rc = otm::validate_compact(in, &np, &err))) return fail(rc, err);
     std::vector<double> tm((size_t)np);
     std::vector<float> acc((size_t)np);
     for (int32_t t = 0; t < nt; ++t)
-      for (int64_t i = in->trace_off[t]; i < in->trace_off[t + 1] && i >= 0 && i < np; ++i)
+      for (int64_t i = in->trace_off[t]; i < in->trace_off[t + 1]; ++i)
         tm[(size_t)i] = (double)(in->time_base[t] + (int64_t)in->time_delta[i]);
     for (int64_t i = 0; i < np; ++i) acc[(size_t)i] = (float)in->accuracy[i];
-    const otm_batch b{nt, in->n_points, in->trace_off, in->lat, in->lon, tm.data(), acc.data()};
+    const otm_batch b{nt, np, in->trace_off, in->lat, in->lon, tm.data(), acc.data()};
     rc = otm::match_host_fetch(E, &b, nullptr, out, &err);
   }
   return rc ? fail(rc, err) : OTM_OK;

@@ -225,6 +225,48 @@ int engine_init(otm_engine* E, const char* graph_path, int device, std::string* 
     g.e_len64 = (const uint32_t*)d;
   }
   {
+    // K7's edge record: what the segment pass reads per traversal -- length,
+    // OSMLR segment, position in it, flags, way -- in one 16-byte word, so a
+    // traversal's gather touches one line instead of five.
+    // Ways are numbered through a table of the graph's distinct way ids (two
+    // edges have the same way exactly when their numbers are equal).
+    const float* len = (const float*)E->host.section(OTMG_EDGE_LEN);
+    const int32_t* seg = (const int32_t*)E->host.section(OTMG_EDGE_SEG);
+    const int32_t* pos = (const int32_t*)E->host.section(OTMG_EDGE_SEG_POS);
+    const uint8_t* fl = (const uint8_t*)E->host.section(OTMG_EDGE_FLAGS);
+    const int64_t* way = (const int64_t*)E->host.section(OTMG_EDGE_WAY);
+    std::vector<int64_t> ways(way, way + h.n_edges);
+    std::sort(ways.begin(), ways.end());
+    ways.erase(std::unique(ways.begin(), ways.end()), ways.end());
+    if (ways.size() >= (size_t)INT32_MAX) {
+      *err = "graph: more than 2^31 distinct way ids";
+      return OTM_EINVAL;
+    }
+    std::vector<uint32_t> rec((size_t)h.n_edges * 4 + 4, 0u);
+    for (int32_t e = 0; e < h.n_edges; ++e) {
+      if (seg[e] >= 0 && (pos[e] < 0 || pos[e] >= (1 << 24))) {
+        *err = "graph: an edge's position in its OSMLR segment exceeds 2^24";
+        return OTM_EINVAL;
+      }
+      uint32_t* r = &rec[(size_t)e * 4];
+      std::memcpy(&r[0], &len[e], 4);
+      r[1] = (uint32_t)seg[e];
+      r[2] = ((uint32_t)(seg[e] >= 0 ? pos[e] : 0) & 0xFFFFFFu) | ((uint32_t)fl[e] << 24);
+      r[3] = (uint32_t)(std::lower_bound(ways.begin(), ways.end(), way[e]) - ways.begin());
+    }
+    if (ways.empty()) ways.push_back(0);
+    void* d = nullptr;
+    HIPCHK(hipMalloc(&d, rec.size() * 4));
+    HIPCHK(hipMemcpy(d, rec.data(), rec.size() * 4, hipMemcpyHostToDevice));
+    E->graph_allocs.push_back(d);
+    g.e_rec = (const uint4*)d;
+    d = nullptr;
+    HIPCHK(hipMalloc(&d, ways.size() * 8));
+    HIPCHK(hipMemcpy(d, ways.data(), ways.size() * 8, hipMemcpyHostToDevice));
+    E->graph_allocs.push_back(d);
+    g.way_tab = (const int64_t*)d;
+  }
+  {
     // The grid index of the candidate search.  The file's cells (meili's
     // 500 per 0.25 deg tile, ~55 m) may be merged m x m into coarser ones
     // (OTM_GRID_MULT, or grid_mult in the config): a probe's radius box then
@@ -867,7 +909,7 @@ static int engine_match_once(otm_engine* E, const DevBatch& b, hipStream_t s, st
     *err = "batch too large for one launch (segment regions exceed 2^31)";
     return OTM_EINVAL;
   }
-  ENS(seg_ub, Pn * 8 + 8);
+  ENS(seg_ub, ((size_t)NT + 1) * 8);
   ENS(o_segments, cap * sizeof(otm_segment));
   ENS(o_seg_gidx, cap * 4);
   ENS(o_reports, cap * sizeof(otm_report_rec));
@@ -892,9 +934,10 @@ static int engine_match_once(otm_engine* E, const DevBatch& b, hipStream_t s, st
     o.nbins = H->nbins;
     o.bin_kph = H->bin_kph;
   }
+  HIPCHK(hipMemsetAsync(E->seg_ub.p, 0, ((size_t)NT + 1) * 8, s));
   launch_seg_bound(E->g, b, dp, w, P<int64_t>(E->seg_ub), s, mk);
   mk.begin(KN_SEG_SCAN, s);
-  scan_i64(P<int64_t>(E->seg_ub), NP, E->scan_tmp.p, E->scan_tmp.cap, s);
+  scan_i64(P<int64_t>(E->seg_ub), NT, E->scan_tmp.p, E->scan_tmp.cap, s);
   mk.end(KN_SEG_SCAN, s);
   launch_segments(E->g, b, w, o, true, s, mk);
   launch_report(b, E->drc, w, o, s, mk);
@@ -1083,7 +1126,9 @@ int engine_match_host(otm_engine* E, const otm_batch* in, std::string* err) {
 // HBM, then widened on the device (k_expand_compact) into the arrays every
 // stage reads.  Same results as engine_match_host on the widened batch;
 // 10 B per point less over PCIe.
-int engine_match_compact(otm_engine* E, const otm_batch_compact* in, std::string* err) {
+// The checks of a compact batch, for one engine and a multi-device engine
+// alike (n_points 0: derived from trace_off); *np = the batch's point count.
+int validate_compact(const otm_batch_compact* in, int64_t* np, std::string* err) {
   const int32_t NT = in->n_traces;
   if (NT < 0 || !in->trace_off || (NT > 0 && !in->time_base)) {
     *err = "invalid batch";
@@ -1099,7 +1144,19 @@ int engine_match_compact(otm_engine* E, const otm_batch_compact* in, std::string
       *err = "batch trace_off not monotonic";
       return OTM_EINVAL;
     }
+  if (NP > 0 && (!in->lat || !in->lon || !in->time_delta || !in->accuracy)) {
+    *err = "invalid batch";
+    return OTM_EINVAL;
+  }
+  *np = NP;
+  return OTM_OK;
+}
+
+int engine_match_compact(otm_engine* E, const otm_batch_compact* in, std::string* err) {
+  const int32_t NT = in->n_traces;
+  int64_t NP = 0;
   int rc;
+  if ((rc = validate_compact(in, &NP, err))) return rc;
   const size_t b_off = ((size_t)NT + 1) * 8, b_base = (size_t)NT * 8, b_pt = (size_t)NP * 4,
                b_acc = ((size_t)NP * 2 + 7) & ~(size_t)7;
   // device: [offsets | time bases | lat | lon | time deltas | accuracies], each
@@ -1481,8 +1538,7 @@ int engine_copy_responses(otm_engine* E, char* dst, int64_t total, const char** 
 
 // report() on the GPU over caller-supplied segments: the k_report kernel
 // alone, with the per-trace segment regions laid out as the matcher's
-// pipeline leaves them (DevOut: trace t's segments start at
-// seg_base[trace_off[t]]).
+// pipeline leaves them (DevOut: trace t's segments start at seg_base[t]).
 int engine_report_segments(otm_engine* E, int32_t T, const int64_t* trace_off, const double* time,
                            const int32_t* seg_off, const otm_segment* segs, otm_trace_result* traces,
                            otm_report_rec* reports, std::string* err) {
@@ -1494,9 +1550,9 @@ int engine_report_segments(otm_engine* E, int32_t T, const int64_t* trace_off, c
       return OTM_EINVAL;
     }
   int rc;
-  // one device blob: trace_off, seg_base (per point), time, segments,
+  // one device blob: trace_off, seg_base (per trace), time, segments,
   // seg_cnt, seg_gidx, trace_err, abort; outputs: traces, reports, rep_cnt
-  const size_t b_off = ((size_t)T + 1) * 8, b_sb = ((size_t)NP + 1) * 8, b_tm = (size_t)NP * 8;
+  const size_t b_off = ((size_t)T + 1) * 8, b_sb = ((size_t)T + 1) * 8, b_tm = (size_t)NP * 8;
   const size_t b_seg = ((size_t)NS + 1) * sizeof(otm_segment), b_cnt = ((size_t)T + 1) * 4;
   const size_t b_gidx = ((size_t)NS + 1) * 4, b_err = b_cnt, b_ab = 16;
   const size_t b_tr = ((size_t)T + 1) * sizeof(otm_trace_result), b_rep = ((size_t)NS + 1) * sizeof(otm_report_rec);
@@ -1514,7 +1570,7 @@ int engine_report_segments(otm_engine* E, int32_t T, const int64_t* trace_off, c
   int64_t* sb = (int64_t*)(h.data() + off[1]);
   int32_t* cnt = (int32_t*)(h.data() + off[4]);
   for (int32_t t = 0; t < T; ++t) {
-    sb[trace_off[t]] = seg_off[t];
+    sb[t] = seg_off[t];
     cnt[t] = seg_off[t + 1] - seg_off[t];
   }
   if (NP) std::memcpy(h.data() + off[2], time, b_tm);

@@ -220,6 +220,8 @@ void engine_free(otm_engine* E);
 int engine_match(otm_engine* E, const DevBatch& b, hipStream_t s, std::string* err);
 // stage a host batch to the device and match it
 int engine_match_host(otm_engine* E, const otm_batch* in, std::string* err);
+// checks of a compact batch (both engine kinds); *np = its point count
+int validate_compact(const otm_batch_compact* in, int64_t* np, std::string* err);
 int engine_match_compact(otm_engine* E, const otm_batch_compact* in, std::string* err);
 // The /report request bodies read on the GPU: engine_stage_requests returns a
 // pinned host staging buffer for n requests of `bytes` body bytes in all:

@@ -43,6 +43,14 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 DEFAULT_TRAFFIC = os.path.join(ROOT, "profiles", "pmc_traffic_latest.json")
 # committed PMC summaries per config (scripts/pmc.sh); --traffic-json overrides
 CONFIG_TRAFFIC = {2: DEFAULT_TRAFFIC, 4: os.path.join(ROOT, "profiles", "pmc_traffic_config4_latest.json")}
+# committed rocprofv3 --kernel-trace --stats summaries per config: they name the
+# dominant kernel of the roofline line (the live HIP events only time it), so
+# two kernels within a few % of each other cannot swap the line's kernel -- and
+# its frac -- from run to run
+CONFIG_ROCPROF = {2: os.path.join(ROOT, "profiles", "rocprof_config2_latest.csv"),
+                  4: os.path.join(ROOT, "profiles", "rocprof_config4_latest.csv")}
+# the two stages whose roofline the line always carries, by their main kernel
+ROOF_STAGES = {"candidates": "k_cand_lane", "transitions": "k_trans_sub"}
 
 # config -> (graph, workload); config 2 is the headline line, config 4 a
 # secondary one (BASELINE.json configs[3]: wide radius, long transitions)
@@ -407,6 +415,44 @@ def stream_leg(eng, batch, ids, graph, meili, runs, cpu_vehicles, native_vehicle
                     "binary mode; on vehicles 0..%d the native host with the C oracle as matcher, JSON mode" %
                     (cpu_vehicles - 1, nveh - 1)}
     return out
+
+
+def rocprof_dominant(path, names):
+    """The kernel of `names` with the longest mean launch in a rocprof kernel
+    stats summary (name, file), or (None, None)."""
+    import csv
+    import re
+    if not path or not os.path.exists(path):
+        return None, None
+    avg = {}
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            m = re.search(r"::(k_[a-z_]+)[<(]", r["Name"])
+            if m and m.group(1) in names:
+                avg[m.group(1)] = max(avg.get(m.group(1), 0.0), float(r["AverageNs"]))
+    if not avg:
+        return None, None
+    return max(avg, key=avg.get), os.path.relpath(path, ROOT)
+
+
+def step_dram(tj, ms_per_step):
+    """Sum of the PMC summary's per-launch DRAM bytes over the step's own
+    kernels (one launch each per batch; the runtime's copies and fills and
+    torch's kernels left out), over the bench's time per batch."""
+    if not tj:
+        return None
+    tot, n = 0.0, 0
+    for name, d in tj.get("kernels", {}).items():
+        if name.startswith("__amd_rocclr") or name.startswith("at::") or "k_index_build" in name \
+                or "k_row_" in name or "k_compact" in name or "k_fetch_scan" in name \
+                or "hbm_bytes_per_launch" not in d:
+            continue
+        tot += d["hbm_bytes_per_launch"]
+        n += 1
+    return {"bytes_per_step": tot, "kernels": n, "GB_per_s": tot / (ms_per_step * 1e-3) / 1e9,
+            "frac": tot / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "basis": "sum of the PMC summary's DRAM bytes per launch over the batch's kernels, divided by "
+                     "ms_per_step (a batch's share of the timed window with the batches in flight)"}
 
 
 def load_traffic(path):
@@ -910,7 +956,10 @@ def main():
     # probe's bytes where the index replaces the oracle's bounded searches
     # (transitions); the §8(d) bytes of those searches are reported beside it
     # as an equivalent-work rate, never as `frac`
-    dom = max(kern_avg, key=lambda k: kern_avg[k])
+    dom_live = max(kern_avg, key=lambda k: kern_avg[k])
+    dom, dom_src = rocprof_dominant(CONFIG_ROCPROF.get(args.config), set(kern_avg))
+    if dom is None:
+        dom, dom_src = dom_live, None
     roof = None
     if sbytes is not None:
         st = KERNEL_STAGE[dom]
@@ -936,7 +985,25 @@ def main():
                 "unit": "GB/s", "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
                 "algorithmic_bytes_per_launch": own, "launch_ms": kern_avg[dom],
                 "algorithmic_bytes_basis": basis,
+                "dominant_by": ("the committed rocprof summary %s (longest mean launch); this run's HIP events: "
+                                "%s" % (dom_src, dom_live)) if dom_src else "this run's HIP events",
                 "traffic_source": os.path.relpath(tpath, ROOT) if traffic is not None else None}
+        # both heavy stages, each over its own main kernel's live launch time
+        roof["stage_fracs"] = {}
+        for rst, rk in ROOF_STAGES.items():
+            if rk not in kern_avg:
+                continue
+            rb = probe_bytes if rst == "transitions" else sbytes.get(rst)
+            rsec = kern_avg[rk] * 1e-3
+            ent = {"kernel": rk, "launch_ms": kern_avg[rk], "algorithmic_bytes_per_launch": rb,
+                   "achieved": rb / rsec / 1e9 if rb else None,
+                   "frac": rb / rsec / 1e9 / HBM_PEAK_GBS if rb else None}
+            if tj and rk in tj.get("kernels", {}):
+                tb_ = tj["kernels"][rk].get("hbm_bytes_per_launch")
+                ent["traffic"] = tb_
+                ent["frac_counter"] = tb_ / rsec / 1e9 / HBM_PEAK_GBS if tb_ else None
+            roof["stage_fracs"][rst] = ent
+        roof["step_dram"] = step_dram(tj, ms_per_step)
         if equiv:
             roof["equivalent_bytes_per_launch"] = equiv
             roof["equivalent_GB_per_s"] = equiv / sec / 1e9

@@ -72,6 +72,10 @@ struct DevGraph {
   const float4* ent_geo;  // per cell entry: shape segment endpoints (lat_a, lon_a, lat_b, lon_b)
   const uint16_t *e_head_out, *e_head_in;  // edge bearing at start / end, whole degrees (turn costs)
   const uint32_t* e_len64;                 // L(e) = round(len(e) x 64): the route searches' edge costs (1/64 m)
+  // K7's per-edge record {len bits, seg, seg_pos | flags << 24, way number}
+  // and the way numbers' ids (engine.cpp)
+  const uint4* e_rec;
+  const int64_t* way_tab;
   int32_t n_nodes, n_edges, n_segments, grid_rows, grid_cols;
   double lat0, lon0, cell;
   // spatial work order tiles: the node bbox cut into ORDER_SIDE^2 tiles
@@ -269,15 +273,16 @@ struct DevWork {
 
 // Outputs of one batch.  Segments, way ids and reports are written in one
 // pass into per-trace regions sized by an upper bound (2 traversals per
-// matched point + its route's path edges, scanned over points: trace t's
-// region starts at seg_base[trace_off[t]]); otm_fetch_results compacts them.
+// matched point + its route's path edges, summed per trace and scanned over
+// traces: trace t's region starts at seg_base[t]); otm_fetch_results compacts
+// them.
 struct DevOut {
   // per trace
   void* traces;          // otm_trace_result[T] (seg_off / rep_off = region start)
   int32_t* seg_cnt;      // [T+1] segments per trace
   int32_t* way_cnt;      // [T+1] way ids per trace
   int32_t* rep_cnt;      // [T+1] reports per trace
-  const int64_t* seg_base;  // [P+1] exclusive scan of the per-point bound
+  const int64_t* seg_base;  // [T+1] exclusive scan of the per-trace bound
   // regions (capacity = bound total)
   void* segments;        // otm_segment[]
   int32_t* seg_gidx;     // [] segment index in graph (-1 none)
@@ -344,9 +349,9 @@ void launch_segments(const DevGraph& g, const DevBatch& b, DevWork& w, DevOut& o
 void launch_report(const DevBatch& b, const DevReportCfg& rc, DevWork& w, DevOut& o, hipStream_t s, const Marks& mk);
 // spatial work order: tile counts, plan (group cuts), scatter of the columns
 void launch_order(const DevBatch& b, DevWork& w, hipStream_t s, const Marks& mk);
-// per-point bound of the segments / way ids a matched point can emit (scanned
-// into DevOut::seg_base)
-void launch_seg_bound(const DevGraph& g, const DevBatch& b, const DevParams& p, DevWork& w, int64_t* ub, hipStream_t s,
+// per-trace bound of the segments / way ids its matched points can emit, added
+// into tb[T] (zeroed by the caller; scanned into DevOut::seg_base)
+void launch_seg_bound(const DevGraph& g, const DevBatch& b, const DevParams& p, DevWork& w, int64_t* tb, hipStream_t s,
                       const Marks& mk);
 // fetch-time compaction of the per-trace regions into dense arrays; offsets
 // are the exclusive scans of seg_cnt / way_cnt / rep_cnt

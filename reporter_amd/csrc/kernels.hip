@@ -2876,13 +2876,21 @@ struct EAttr {
   float glen;
 };
 
+// the edge's K7 record (one 16-byte load): {len bits, seg, seg_pos | flags << 24, way number}
+__device__ __forceinline__ uint4 edge_rec(const DevGraph& g, int32_t e) { return g.e_rec[e]; }
+__device__ __forceinline__ float rec_len(const uint4& r) { return __uint_as_float(r.x); }
+__device__ __forceinline__ int32_t rec_seg(const uint4& r) { return (int32_t)r.y; }
+__device__ __forceinline__ int32_t rec_pos(const uint4& r) { return (int32_t)(r.z & 0xFFFFFFu); }
+__device__ __forceinline__ uint32_t rec_flags(const uint4& r) { return r.z >> 24; }
+
 __device__ __forceinline__ EAttr edge_attr(const DevGraph& g, int32_t e) {
+  const uint4 r = edge_rec(g, e);
   EAttr a;
-  a.len = g.e_len[e];
-  a.seg = g.e_seg[e];
-  a.seg_pos = g.e_seg_pos[e];
-  a.flags = g.e_flags[e];
-  a.way = g.e_way[e];
+  a.len = rec_len(r);
+  a.seg = rec_seg(r);
+  a.seg_pos = a.seg >= 0 ? rec_pos(r) : 0;
+  a.flags = rec_flags(r);
+  a.way = g.way_tab[r.w];
   a.gid = a.seg >= 0 ? g.g_id[a.seg] : 0ull;
   a.glen = a.seg >= 0 ? g.g_len[a.seg] : 0.0f;
   return a;
@@ -3187,45 +3195,64 @@ __device__ __forceinline__ int wave_incl_max(int v, int lane) {
   return v;
 }
 
-// what a state contributes (recomputed in the two passes that need it)
+// what a state contributes (recomputed in the two passes that need it).
+// Every global load of a state is issued at once, unconditionally -- none
+// depends on another (the neighbours' points come from LDS) -- so a pass
+// costs one round trip for them, not three (round 6; the values and the
+// arithmetic on them are the same as before).
 struct StateStep {
-  int pl, lp;      // point, previous state's point
-  bool cs, last;   // chain start, last state of its chain
-  bool step, same; // a step from lp; stays on the open edge
+  int32_t pts;     // point (low 16 bits) | previous state's point << 16
+  uint32_t f;      // 1 chain start, 2 last state of its chain, 4 a step from lp, 8 stays on the open edge
   int32_t ei, ej;  // previous state's edge (== the open traversal's), own edge
   float oi, oj;
   int32_t plen, poff;
+  double ta, tb;   // times of lp and pl
+  float rd;        // the step's route distance
+  __device__ int pl() const { return pts & 0xFFFF; }
+  __device__ int lp() const { return pts >> 16; }
+  __device__ bool cs() const { return f & 1u; }
+  __device__ bool last() const { return f & 2u; }
+  __device__ bool step() const { return f & 4u; }
+  __device__ bool same() const { return f & 8u; }
 };
 template <class SP>
-__device__ __forceinline__ StateStep state_step(const DevWork& w, int64_t a, const SP& S, int k, int ns) {
+__device__ __forceinline__ StateStep state_step(const DevWork& w, const DevBatch& b, int64_t a, const SP& S, int k,
+                                                int ns) {
   StateStep r;
-  r.pl = S.sidx[k];
-  const int64_t p = a + r.pl;
-  r.cs = w.chain_start[p] != 0;
-  r.last = k == ns - 1 || w.chain_start[a + S.sidx[k + 1]] != 0;
-  r.step = !r.cs && k > 0;
-  r.lp = r.step ? S.sidx[k - 1] : r.pl;
+  const int pl = S.sidx[k];
+  const int nx = k + 1 < ns ? S.sidx[k + 1] : pl;
+  const int pv = k > 0 ? S.sidx[k - 1] : pl;
+  const int64_t p = a + pl;
+  const bool csp = w.chain_start[p] != 0;
+  const bool csn = w.chain_start[a + nx] != 0;
   const int2 cj = w.chosen[p];
+  const int2 cv = w.chosen[a + pv];
+  const int32_t pln = w.path_len[p], pof = w.path_off[p];
+  const double tp = b.time[p], tv = b.time[a + pv];
+  r.rd = w.route_dist[p];
+  const bool last = k == ns - 1 || csn;
+  const bool step = !csp && k > 0;
+  const int lp = step ? pv : pl;
+  r.pts = pl | (lp << 16);
   r.ej = cj.x;
   r.oj = __int_as_float(cj.y);
-  const int64_t q = a + r.lp;
-  const int2 ci = w.chosen[q];
+  const int2 ci = step ? cv : cj;
   r.ei = ci.x;
   r.oi = __int_as_float(ci.y);
-  r.same = r.step && same_edge_step(r.ei, r.oi, r.ej, r.oj);
-  r.plen = 0;
-  r.poff = 0;
-  if (r.step && !r.same) {
-    r.plen = w.path_len[p] > 0 ? w.path_len[p] : 0;
-    r.poff = w.path_off[p];
-  }
+  const bool same = step && same_edge_step(r.ei, r.oi, r.ej, r.oj);
+  r.f = (csp ? 1u : 0u) | (last ? 2u : 0u) | (step ? 4u : 0u) | (same ? 8u : 0u);
+  const bool leaves = step && !same;
+  r.plen = leaves ? (pln > 0 ? pln : 0) : 0;
+  r.poff = leaves ? pof : 0;
+  r.tb = tp;
+  r.ta = step ? tv : tp;
   return r;
 }
 
 // list / list_n: the traces to walk (null: all); spill / spill_n: where a
 // trace beyond this plan goes (null: the serial walk)
 template <int PT, int TR>
-__global__ __launch_bounds__(TB) void k_segments(DevGraph g, DevBatch b, DevWork w, DevOut o, const int32_t* list,
+__global__ __launch_bounds__(TB, (PT <= 128 ? 4 : 2)) void k_segments(DevGraph g, DevBatch b, DevWork w, DevOut o, const int32_t* list,
                                                  const int32_t* list_n, int32_t* spill, int32_t* spill_n) {
   if (*w.abort) return;  // a capacity was exceeded: the host redoes the batch
   __shared__ SegParT<PT, TR> S;
@@ -3236,7 +3263,7 @@ __global__ __launch_bounds__(TB) void k_segments(DevGraph g, DevBatch b, DevWork
     const int32_t t = list ? list[it] : it;
     const int64_t a = b.trace_off[t];
     const int n = (int)(b.trace_off[t + 1] - a);
-    const int32_t base = (int32_t)o.seg_base[a];
+    const int32_t base = (int32_t)o.seg_base[t];
     if (w.trace_err[t] != 0) {
       if (lane == 0) {
         o.seg_cnt[t] = 0;
@@ -3251,41 +3278,55 @@ __global__ __launch_bounds__(TB) void k_segments(DevGraph g, DevBatch b, DevWork
       }
       continue;
     }
-    // ---- states in point order
+    // ---- states in point order (n <= PT here: every chunk's loads at once)
+    constexpr int NCH = (PT + TB - 1) / TB;
+    bool stv[NCH];
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int pl = c * TB + lane;
+      const bool in = pl < n;
+      const uint8_t ic = in ? w.is_col[a + pl] : (uint8_t)0;
+      const int32_t sv = in ? w.state[a + pl] : -1;
+      stv[c] = ic && sv >= 0;
+    }
     int ns = 0;
-    for (int c0 = 0; c0 < n; c0 += TB) {
-      const int pl = c0 + lane;
-      const bool st = pl < n && w.is_col[a + pl] && w.state[a + pl] >= 0;
-      const unsigned long long m = __ballot(st);
-      if (st) S.sidx[ns + __popcll(m & lt)] = (int16_t)pl;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const unsigned long long m = __ballot(stv[c]);
+      if (stv[c]) S.sidx[ns + __popcll(m & lt)] = (int16_t)(c * TB + lane);
       ns += __popcll(m);
     }
     __syncthreads();
+    // every state's loads at once, kept in registers for both passes below
+    StateStep rs[NCH];
+#pragma unroll
+    for (int c = 0; c < NCH; ++c)
+      if (c * TB + lane < ns) rs[c] = state_step(w, b, a, S, c * TB + lane, ns);
     // ---- per state: opener fields, chain index, latest opener, slot counts
     int c_chain = 0, c_open = -1, c_base = 0;
-    for (int k0 = 0; k0 < ns; k0 += TB) {
-      const int k = k0 + lane;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      if (c * TB >= ns) break;
+      const int k = c * TB + lane;
       const bool valid = k < ns;
       int cs = 0, opener = -1, nem = 0;
       if (valid) {
-        const StateStep r = state_step(w, a, S, k, ns);
-        cs = r.cs ? 1 : 0;
-        if (r.cs || !r.same) {
+        const StateStep& r = rs[c];
+        cs = r.cs() ? 1 : 0;
+        if (r.cs() || !r.same()) {
           opener = k;
-          if (r.cs) {
-            S.o_t0[k] = b.time[a + r.pl];
+          if (r.cs()) {
+            S.o_t0[k] = r.tb;
             S.o_off0[k] = r.oj;
-            S.o_sh0[k] = (int16_t)r.pl;
+            S.o_sh0[k] = (int16_t)r.pl();
           } else {
-            const float Rd = w.route_dist[a + r.pl];
-            const double ta = b.time[a + r.lp], tb = b.time[a + r.pl];
-            const float start = src_start(g, r.ei, r.oi);
+            const float start = cand_node(r.oi) ? 0.0f : rec_len(edge_rec(g, r.ei)) - r.oi;  // src_start
             float dd = 0.0f;
-            for (int i = 0; i < r.plen; ++i) dd = dd + g.e_len[w.path_pool[r.poff + i]];
+            for (int i = 0; i < r.plen; ++i) dd = dd + rec_len(edge_rec(g, w.path_pool[r.poff + i]));
             const float x = start + dd;
             double t0;
             int sh;
-            step_bound(b, w, a, r.lp, r.pl, Rd, ta, tb, x, t0, sh);
+            step_bound(b, w, a, r.lp(), r.pl(), r.rd, r.ta, r.tb, x, t0, sh);
             S.o_t0[k] = t0;
             S.o_off0[k] = 0.0f;
             S.o_sh0[k] = (int16_t)sh;
@@ -3293,8 +3334,8 @@ __global__ __launch_bounds__(TB) void k_segments(DevGraph g, DevBatch b, DevWork
         }
         // the close of the open traversal (none from a node candidate), the
         // route's edges, the chain's final close (none at a node candidate)
-        nem = (r.step && !r.same ? (cand_node(r.oi) ? 0 : 1) + r.plen : 0) +
-              (r.last && !r.cs && !cand_node(r.oj) ? 1 : 0);
+        nem = (r.step() && !r.same() ? (cand_node(r.oi) ? 0 : 1) + r.plen : 0) +
+              (r.last() && !r.cs() && !cand_node(r.oj) ? 1 : 0);
       }
       const int ch = c_chain + wave_incl_scan(cs, lane);
       int lo = wave_incl_max(opener, lane);
@@ -3320,17 +3361,18 @@ __global__ __launch_bounds__(TB) void k_segments(DevGraph g, DevBatch b, DevWork
       continue;
     }
     // ---- traversals, each state writing its own
-    for (int k0 = 0; k0 < ns; k0 += TB) {
-      const int k = k0 + lane;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int k = c * TB + lane;
       if (k >= ns) continue;
-      const StateStep r = state_step(w, a, S, k, ns);
+      const StateStep& r = rs[c];
       int slot = S.tbase[k];
       const int16_t chk = S.chain[k];
-      if (r.step && !r.same) {
-        const float Rd = w.route_dist[a + r.pl];
-        const double ta = b.time[a + r.lp], tb = b.time[a + r.pl];
-        const float elen = g.e_len[r.ei];
-        const float start = src_start(g, r.ei, r.oi);
+      if (r.step() && !r.same()) {
+        const float Rd = r.rd;
+        const double ta = r.ta, tb = r.tb;
+        const float elen = rec_len(edge_rec(g, r.ei));
+        const float start = cand_node(r.oi) ? 0.0f : elen - r.oi;  // src_start
         if (!cand_node(r.oi)) {
           const int jo = S.lopen[k - 1];
           S.t_edge[slot] = r.ei;
@@ -3340,7 +3382,7 @@ __global__ __launch_bounds__(TB) void k_segments(DevGraph g, DevBatch b, DevWork
           S.t_off1[slot] = elen;
           double t1;
           int sh;
-          step_bound(b, w, a, r.lp, r.pl, Rd, ta, tb, start, t1, sh);
+          step_bound(b, w, a, r.lp(), r.pl(), Rd, ta, tb, start, t1, sh);
           S.t_t1[slot] = t1;
           S.t_sh1[slot] = (int16_t)sh;
           S.t_chain[slot] = chk;
@@ -3349,7 +3391,7 @@ __global__ __launch_bounds__(TB) void k_segments(DevGraph g, DevBatch b, DevWork
         float dd = 0.0f;
         for (int i = 0; i < r.plen; ++i) {
           const int32_t pe = w.path_pool[r.poff + i];
-          const float len = g.e_len[pe];
+          const float len = rec_len(edge_rec(g, pe));
           const float xb = start + dd;
           dd = dd + len;
           const float xe = start + dd;
@@ -3358,17 +3400,17 @@ __global__ __launch_bounds__(TB) void k_segments(DevGraph g, DevBatch b, DevWork
           S.t_off1[slot] = len;
           double tt;
           int sh;
-          step_bound(b, w, a, r.lp, r.pl, Rd, ta, tb, xb, tt, sh);
+          step_bound(b, w, a, r.lp(), r.pl(), Rd, ta, tb, xb, tt, sh);
           S.t_t0[slot] = tt;
           S.t_sh0[slot] = (int16_t)sh;
-          step_bound(b, w, a, r.lp, r.pl, Rd, ta, tb, xe, tt, sh);
+          step_bound(b, w, a, r.lp(), r.pl(), Rd, ta, tb, xe, tt, sh);
           S.t_t1[slot] = tt;
           S.t_sh1[slot] = (int16_t)sh;
           S.t_chain[slot] = chk;
           ++slot;
         }
       }
-      if (r.last && !r.cs && !cand_node(r.oj)) {
+      if (r.last() && !r.cs() && !cand_node(r.oj)) {
         const int jo = S.lopen[k];
         // the traversal ends at the largest offset of its states (the opener
         // jo's and every stay after it: rule 4)
@@ -3382,34 +3424,34 @@ __global__ __launch_bounds__(TB) void k_segments(DevGraph g, DevBatch b, DevWork
         S.t_t0[slot] = S.o_t0[jo];
         S.t_sh0[slot] = S.o_sh0[jo];
         S.t_off1[slot] = omax;
-        S.t_t1[slot] = b.time[a + r.pl];
-        S.t_sh1[slot] = (int16_t)r.pl;
+        S.t_t1[slot] = r.tb;
+        S.t_sh1[slot] = (int16_t)r.pl();
         S.t_chain[slot] = chk;
       }
     }
     __syncthreads();
     // ---- groups (OSMLR segments) and way ids
+    // (one 16-byte edge record per traversal; ways compared by number, the id
+    // looked up only for the way ids written)
     int c_seg = 0, c_way = 0;
-    int32_t p_seg = 0, p_pos = 0, p_ch = -1;
+    int32_t p_seg = 0, p_pos = 0, p_ch = -1, p_way = -1;
     uint32_t p_fl = 0;
-    int64_t p_way = 0;
     for (int k0 = 0; k0 < nt; k0 += TB) {
       const int k = k0 + lane;
       const bool valid = k < nt;
-      int32_t seg = -1, pos = 0, ch = -2;
+      int32_t seg = -1, pos = 0, ch = -2, way = -1;
       uint32_t fl = 0;
-      int64_t way = 0;
       if (valid) {
-        const int32_t e = S.t_edge[k];
-        seg = g.e_seg[e];
-        pos = g.e_seg_pos[e];
-        fl = g.e_flags[e];
-        way = g.e_way[e];
+        const uint4 er = edge_rec(g, S.t_edge[k]);
+        seg = rec_seg(er);
+        pos = rec_pos(er);
+        fl = rec_flags(er);
+        way = (int32_t)er.w;
         ch = S.t_chain[k];
       }
       int32_t qs = __shfl_up(seg, 1, 64), qp = __shfl_up(pos, 1, 64), qc = __shfl_up(ch, 1, 64);
       uint32_t qf = __shfl_up(fl, 1, 64);
-      int64_t qw = __shfl_up(way, 1, 64);
+      int32_t qw = __shfl_up(way, 1, 64);
       if (lane == 0) {
         qs = p_seg;
         qp = p_pos;
@@ -3427,7 +3469,7 @@ __global__ __launch_bounds__(TB) void k_segments(DevGraph g, DevBatch b, DevWork
       const unsigned long long ms = __ballot(start), mw = __ballot(wemit);
       const int gi = c_seg + __popcll(ms & lt) + (start ? 0 : -1);  // this traversal's group
       const int wi = c_way + __popcll(mw & lt);
-      if (wemit) o.way_ids[base + wi] = way;
+      if (wemit) o.way_ids[base + wi] = g.way_tab[way];
       if (start) {
         S.g_first[gi] = (int16_t)k;
         S.g_w0[gi] = (int16_t)wi;
@@ -3451,10 +3493,15 @@ __global__ __launch_bounds__(TB) void k_segments(DevGraph g, DevBatch b, DevWork
       const int si = s0 + lane;
       if (si >= c_seg) continue;
       const int kf = S.g_first[si], kl = S.g_last[si];
-      const EAttr fa = edge_attr(g, S.t_edge[kf]);
-      const int32_t el = S.t_edge[kl];
-      const float llen = g.e_len[el];
-      const uint32_t lfl = g.e_flags[el];
+      const uint4 fr = edge_rec(g, S.t_edge[kf]);
+      EAttr fa;
+      fa.seg = rec_seg(fr);
+      fa.flags = rec_flags(fr);
+      fa.gid = fa.seg >= 0 ? g.g_id[fa.seg] : 0ull;
+      fa.glen = fa.seg >= 0 ? g.g_len[fa.seg] : 0.0f;
+      const uint4 lr = edge_rec(g, S.t_edge[kl]);
+      const float llen = rec_len(lr);
+      const uint32_t lfl = rec_flags(lr);
       otm_segment sr;
       const int32_t sg = fa.seg;
       bool sv, ev;
@@ -3646,7 +3693,7 @@ __global__ __launch_bounds__(256, OTM_REPORT_WAVES) void k_report(DevBatch b, De
   if (t >= b.n_traces) return;
   otm_trace_result r;
   r.error_kind = w.trace_err[t];
-  r.seg_off = (int32_t)o.seg_base[b.trace_off[t]];
+  r.seg_off = (int32_t)o.seg_base[t];
   r.seg_cnt = o.seg_cnt[t];
   r.rep_off = r.seg_off;
   otm_report_rec* REP = (otm_report_rec*)o.reports + r.rep_off;
@@ -3677,7 +3724,7 @@ __global__ __launch_bounds__(TB) void k_report_wave(DevBatch b, DevReportCfg rc,
   for (int32_t t = blockIdx.x; t < b.n_traces; t += gridDim.x) {
     otm_trace_result r;
     r.error_kind = w.trace_err[t];
-    r.seg_off = (int32_t)o.seg_base[b.trace_off[t]];
+    r.seg_off = (int32_t)o.seg_base[t];
     r.seg_cnt = o.seg_cnt[t];
     r.rep_off = r.seg_off;
     const otm_segment* G = (const otm_segment*)o.segments + r.seg_off;
@@ -3771,15 +3818,22 @@ __device__ float interp_pos(const DevGraph& g, const DevBatch& b, const DevParam
 
 // Traversals a matched point can add: the close of the open traversal, its
 // route's path edges, the re-open (+ the chain's final close): <= 2 + path.
-// An interpolated point's thread places it instead (K7a).
-__global__ __launch_bounds__(256) void k_seg_bound(DevGraph g, DevBatch b, DevParams P, DevWork w, int64_t* ub) {
+// Summed per trace into tb[t] (zeroed by the host; its exclusive scan is each
+// trace's segment region, DevOut::seg_base): a wave's points are runs of
+// whole traces, so a segmented suffix sum over the wave leaves each run's
+// total on its first lane, which adds it with one atomic -- no per-point
+// bound array, no point-length scan.  An interpolated point's thread places
+// it instead (K7a).
+__global__ __launch_bounds__(256) void k_seg_bound(DevGraph g, DevBatch b, DevParams P, DevWork w, int64_t* tb) {
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   // spill snapshot C: steps per route tier (kept for the status read)
   if (OTM_FOLD_BOOKKEEPING && k == b.n_points) fold_snap(w, 2, false);
   if (*w.abort) return;  // a capacity was exceeded: the host redoes the batch
-  if (k > b.n_points) return;
+  const int lane = threadIdx.x & 63;
   int64_t v = 0;
+  int32_t t = -1;
   if (k < b.n_points) {
+    t = w.pt_trace[k];
     if (w.is_col[k]) {
       if (w.state[k] >= 0) {
         const int32_t pl = w.path_len[k];
@@ -3790,14 +3844,23 @@ __global__ __launch_bounds__(256) void k_seg_bound(DevGraph g, DevBatch b, DevPa
       const int32_t q = w.prevc[k];
       const int32_t p = q >= 0 ? w.nextc[q] : -1;
       if (p >= 0 && w.col_prev[p] == q && !w.chain_start[p] && w.state[p] >= 0 && w.path_len[p] >= 0 &&
-          w.trace_err[w.pt_trace[k]] == 0) {
+          w.trace_err[t] == 0) {
         const int2 ci = w.chosen[q], cj = w.chosen[p];
         if (!same_edge_step(ci.x, __int_as_float(ci.y), cj.x, __int_as_float(cj.y)))
           w.ipos[k] = interp_pos(g, b, P, w, q, p, k);
       }
     }
   }
-  ub[k] = v;
+  // segmented suffix sum over the wave's runs of equal t (lanes past the
+  // batch's end have t = -1, a run of their own)
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int64_t vn = __shfl_down(v, d, 64);
+    const int32_t tn = __shfl_down(t, d, 64);
+    if (lane + d < 64 && tn == t) v += vn;
+  }
+  const int32_t tp = __shfl_up(t, 1, 64);
+  if (t >= 0 && (lane == 0 || tp != t) && v != 0) atomicAdd((unsigned long long*)&tb[t], (unsigned long long)v);
 }
 
 // One wavefront per trace: copy its segments (way offsets rebased), way ids
@@ -4098,10 +4161,10 @@ void launch_segments(const DevGraph& g, const DevBatch& b, DevWork& w, DevOut& o
                      o, (const int32_t*)lst, (const int32_t*)cnt, (int32_t*)nullptr, (int32_t*)nullptr);
   mk.end(KN_SEG_WRITE, s);
 }
-void launch_seg_bound(const DevGraph& g, const DevBatch& b, const DevParams& p, DevWork& w, int64_t* ub, hipStream_t s,
+void launch_seg_bound(const DevGraph& g, const DevBatch& b, const DevParams& p, DevWork& w, int64_t* tb, hipStream_t s,
                       const Marks& mk) {
   TIMED(KN_SEG_BOUND, hipLaunchKernelGGL(k_seg_bound, dim3(grid_for(b.n_points + 1, 256, 1 << 30)), dim3(256), 0, s,
-                                         g, b, p, w, ub));
+                                         g, b, p, w, tb));
 }
 void launch_compact(int32_t n_traces, const DevOut& o, const int32_t* seg_off, const int32_t* way_off,
                     const int32_t* rep_off, void* segs_out, int64_t* ways_out, void* reps_out, void* traces_out,

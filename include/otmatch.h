@@ -441,6 +441,9 @@ typedef struct otm_spill_stats {
    * label limit (trans_huge / route_huge), and how many times the batch was
    * run to size its buffers and tables (attempts, 1 = no redo) */
   int32_t cand_big, trans_huge, route_huge, attempts;
+  /* round 6: of those runs, how many resumed from the tier whose tables grew
+   * (the stages before it kept their results) instead of redoing the batch */
+  int32_t resumed;
 } otm_spill_stats;
 int otm_get_spill_stats(otm_engine* eng, otm_spill_stats* out);
 

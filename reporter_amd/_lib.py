@@ -53,7 +53,7 @@ class WorkCounters(C.Structure):
 class SpillStats(C.Structure):
     _fields_ = [(n, C.c_int32) for n in ("cand_wave", "trans_online", "trans_wave", "trans_global", "route_online",
                                          "route_wave", "route_global", "cand_big", "trans_huge", "route_huge",
-                                         "attempts")]
+                                         "attempts", "resumed")]
 
 
 class BatcherCfg(C.Structure):

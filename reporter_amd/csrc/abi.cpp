@@ -221,6 +221,7 @@ bool fill_device_params(otm_engine* E, std::string* err) {
   // config 2: candidates 0.60 -> 0.44 ms, route 0.107 -> 0.089, transitions
   // 0.408 -> 0.388)
   E->dp.order_mask = otm::ORDER_CAND | otm::ORDER_TRANS | otm::ORDER_ROUTE;
+  if (const char* om = std::getenv("OTM_ORDER_MASK")) E->dp.order_mask = std::atoi(om) & 7;  // A/B knob
   E->dp.cand_wave_all = 0;
   // batches under this many points take the small-batch (latency) path
   const char* sp = std::getenv("OTM_SMALL_POINTS");

@@ -724,8 +724,10 @@ static int ensure_big(otm_engine* E, std::string* err) {
 // One attempt at a batch, enqueued with no host synchronisation: buffers are
 // sized from capacities (transition matrices, path pool) that the kernels
 // check; an overflow sets w.abort, every later kernel returns at once, and
-// engine_match grows the capacity and runs the batch again.
-static int engine_match_once(otm_engine* E, const DevBatch& b, hipStream_t s, std::string* err) {
+// engine_match grows the capacity and runs the batch again -- whole
+// (from = RESUME_ALL), or from the on-demand tier that overflowed (Resume).
+static int engine_match_once(otm_engine* E, const DevBatch& b, hipStream_t s, std::string* err,
+                             int from = RESUME_ALL) {
   const int64_t NP = b.n_points;
   const int32_t NT = b.n_traces;
   const size_t Pn = (size_t)NP + 1;
@@ -833,7 +835,7 @@ static int engine_match_once(otm_engine* E, const DevBatch& b, hipStream_t s, st
   w.counters_i32 = P<int32_t>(E->counters_i32);
   w.snap = P<int32_t>(E->snap);
   w.ctr = E->counting ? E->ctr : nullptr;
-  if (E->counting) HIPCHK(hipMemsetAsync(E->ctr, 0, sizeof(DevCounters), s));
+  if (E->counting && from == RESUME_ALL) HIPCHK(hipMemsetAsync(E->ctr, 0, sizeof(DevCounters), s));
   w.abort = P<int32_t>(E->abort_flag);
   // the counters' and abort flag's reset, the spill snapshots and the
   // transition capacity check ride in K1, K3, K4, K5 and K7 (OTM_FOLD_BOOKKEEPING)
@@ -850,12 +852,14 @@ static int engine_match_once(otm_engine* E, const DevBatch& b, hipStream_t s, st
   w.ord.tile = P<uint16_t>(E->ord_tile);
   w.ord.tile_cnt = dp.order_mask ? P<int32_t>(E->ord_cnt) : nullptr;
   w.ord.cursor = P<int32_t>(E->ord_cursor);
-  launch_columns(E->g, b, dp, w, s, mk);
-  if (dp.order_mask) {
-    launch_order(b, w, s, mk);
-  } else if (E->timing) {
-    mk.begin(KN_ORDER, s);
-    mk.end(KN_ORDER, s);
+  if (from == RESUME_ALL) {
+    launch_columns(E->g, b, dp, w, s, mk);
+    if (dp.order_mask) {
+      launch_order(b, w, s, mk);
+    } else if (E->timing) {
+      mk.begin(KN_ORDER, s);
+      mk.end(KN_ORDER, s);
+    }
   }
   if ((rc = ensure_cand(E, err))) return rc;
   w.cand_final = E->cand_final;
@@ -863,15 +867,17 @@ static int engine_match_once(otm_engine* E, const DevBatch& b, hipStream_t s, st
   w.cbig_val = P<unsigned long long>(E->cbig_val);
   w.cbig_skey = P<unsigned long long>(E->cbig_skey);
   w.cand_log2 = E->cand_log2;
-  launch_candidates(E->g, b, dp, w, s, mk);
+  if (from <= RESUME_CAND_BIG) launch_candidates(E->g, b, dp, w, s, mk, from);
   // spill snapshot A: candidate probes the lane tier handed to the wave tier;
   // the counters start over for the transition tiers (links, scan and the
   // capacity check do not touch them)
   if (!fold_bookkeeping()) launch_snap(w.counters_i32, P<int32_t>(E->snap), true, s);
-  launch_links(b, dp, w, s, mk);
-  mk.begin(KN_SCAN_TRANS, s);
-  scan_i64(w.trans_off, NP, E->scan_tmp.p, E->scan_tmp.cap, s);
-  mk.end(KN_SCAN_TRANS, s);
+  if (from <= RESUME_CAND_BIG) {
+    launch_links(b, dp, w, s, mk);
+    mk.begin(KN_SCAN_TRANS, s);
+    scan_i64(w.trans_off, NP, E->scan_tmp.p, E->scan_tmp.cap, s);
+    mk.end(KN_SCAN_TRANS, s);
+  }
   ENS(trans, ((size_t)E->trans_cap + 1) * 4);
   w.trans = P<float>(E->trans);
   w.trans_cap = E->trans_cap;
@@ -892,12 +898,12 @@ static int engine_match_once(otm_engine* E, const DevBatch& b, hipStream_t s, st
   w.huge_prev = P<int32_t>(E->huge_prev);
   w.huge_log2 = E->huge_log2;
   w.huge_final = E->huge_final;
-  launch_transitions(E->g, b, dp, w, s, mk, E->trans_lanes);
+  if (from <= RESUME_TRANS_HUGE) launch_transitions(E->g, b, dp, w, s, mk, E->trans_lanes, from);
   // spill snapshot B: columns per transition tier (Viterbi does not touch
   // the counters; they start over for the route tiers)
   if (!fold_bookkeeping()) launch_snap(w.counters_i32, P<int32_t>(E->snap) + 16, true, s);
-  launch_viterbi(b, w, s, mk);
-  launch_route(E->g, b, dp, w, s, mk);
+  if (from <= RESUME_TRANS_HUGE) launch_viterbi(b, w, s, mk);
+  launch_route(E->g, b, dp, w, s, mk, from);
   // spill snapshot C: steps per route tier
   if (!fold_bookkeeping()) launch_snap(w.counters_i32, P<int32_t>(E->snap) + 32, false, s);
 
@@ -965,8 +971,10 @@ int engine_match(otm_engine* E, const DevBatch& b, hipStream_t s, std::string* e
       if (cand) E->cand_final = 0;
     }
   } oom{E};
+  int from = RESUME_ALL;
+  E->last_resumes = 0;
   for (int attempt = 0;; ++attempt) {
-    if ((rc = engine_match_once(E, b, s, err))) return rc;
+    if ((rc = engine_match_once(E, b, s, err, from))) return rc;
     // the one synchronisation of a batch: did every capacity hold?
     // (gathered on the device, one copy into pinned memory)
     if ((rc = ensure_pinned(E->h_status, sizeof(BatchStatus), err))) return rc;
@@ -1023,6 +1031,28 @@ int engine_match(otm_engine* E, const DevBatch& b, hipStream_t s, std::string* e
       }
     }
     if (cnt[2]) E->pool_cap = (int32_t)std::min<size_t>((size_t)cnt[1] * 2 + 1024, (size_t)INT32_MAX / 2);
+    // Where to resume: a matrix or path-pool overflow redoes
+    // the whole batch (those buffers are reallocated); a tier whose tables
+    // grew -- candidate HBM tier, or the huge search tier of the transition
+    // or route stage -- runs again from itself: every earlier stage finished
+    // and kept its results, every later one returned at once on the abort.
+    // The spill counters go back to the snapshot the aborted attempt took at
+    // that stage's boundary (A after the candidates, B after the transitions,
+    // C after the routes), so the resumed kernels retake the same snapshots.
+    const char* nr = std::getenv("OTM_NO_RESUME");  // A/B knob: every redo whole (rounds 1-5)
+    const bool whole = !fold_bookkeeping() || ttotal > E->trans_cap || cnt[2] || !(st.grow & 3) ||
+                       (nr && *nr && *nr != '0');
+    from = whole ? RESUME_ALL
+                 : (st.grow & 2) ? RESUME_CAND_BIG : (st.route_huge ? RESUME_ROUTE_HUGE : RESUME_TRANS_HUGE);
+    if (from != RESUME_ALL) {
+      const int snap = from == RESUME_CAND_BIG ? 0 : (from == RESUME_TRANS_HUGE ? 16 : 32);
+      int32_t* ctr = P<int32_t>(E->counters_i32);
+      HIPCHK(hipMemcpyAsync(ctr, P<int32_t>(E->snap) + snap, 16 * 4, hipMemcpyDeviceToDevice, s));
+      HIPCHK(hipMemsetAsync(ctr + 23, 0, 4, s));  // the grow flags
+      HIPCHK(hipMemsetAsync(ctr + 25, 0, 4, s));
+      HIPCHK(hipMemsetAsync(E->abort_flag.p, 0, 4, s));
+      E->last_resumes += 1;
+    }
   }
   if (E->timing) {
     // kernel-only spans on the launch stream (the final attempt).  Stages are sums of their
@@ -1593,7 +1623,7 @@ int engine_report_segments(otm_engine* E, int32_t T, const int64_t* trace_off, c
   o.traces = d + off[8];
   o.seg_cnt = (int32_t*)(d + off[4]);
   o.rep_cnt = (int32_t*)(d + off[10]);
-  o.seg_base = (const int64_t*)(d + off[1]);
+  o.seg_base = (int64_t*)(d + off[1]);
   o.segments = d + off[3];
   o.seg_gidx = (int32_t*)(d + off[5]);
   o.reports = d + off[9];
@@ -1687,6 +1717,7 @@ int engine_spill_stats(otm_engine* E, otm_spill_stats* out) {
   out->trans_huge = c[21];
   out->route_huge = c[22];
   out->attempts = E->last_attempts;
+  out->resumed = E->last_resumes;
   return OTM_OK;
 }
 

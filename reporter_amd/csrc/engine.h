@@ -112,6 +112,7 @@ struct otm_engine {
   int32_t cand_log2 = 0;  // candidate HBM tier: 2^cand_log2 slots per table (0: none yet; grown on demand)
   int32_t huge_final = 0, cand_final = 0;  // the tier's tables cannot grow: overflows fail their traces
   int32_t last_attempts = 0;  // runs of the last batch (otm_spill_stats::attempts)
+  int32_t last_resumes = 0;   // ... of them resumed from a grown tier (otm_spill_stats::resumed)
   Buf ord_tile, ord_cnt, ord_cursor, ord_grp, ord_item;  // spatial work order
   Buf abort_flag;                                       // capacity overflow of the batch in flight
   Buf rs_blob;                                          // otm_report_segments_device in/out

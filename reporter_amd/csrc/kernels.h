@@ -282,7 +282,7 @@ struct DevOut {
   int32_t* seg_cnt;      // [T+1] segments per trace
   int32_t* way_cnt;      // [T+1] way ids per trace
   int32_t* rep_cnt;      // [T+1] reports per trace
-  const int64_t* seg_base;  // [T+1] exclusive scan of the per-trace bound
+  int64_t* seg_base;     // [T+1] exclusive scan of the per-trace bound
   // regions (capacity = bound total)
   void* segments;        // otm_segment[]
   int32_t* seg_gidx;     // [] segment index in graph (-1 none)
@@ -332,25 +332,29 @@ struct Marks {
 // ---- launch wrappers (kernels.hip)
 void launch_columns(const DevGraph& g, const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s,
                     const Marks& mk);
+// Where a batch resumes after a tier's tables grew (engine_match): the stages
+// before the tier that overflowed kept their results, so only that tier and
+// what follows it run again (RESUME_ALL: the whole batch).
+enum Resume { RESUME_ALL = 0, RESUME_CAND_BIG = 1, RESUME_TRANS_HUGE = 2, RESUME_ROUTE_HUGE = 3 };
 void launch_candidates(const DevGraph& g, const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s,
-                       const Marks& mk);
+                       const Marks& mk, int from = RESUME_ALL);
 void launch_links(const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s, const Marks& mk);
 // sets *w.abort when the scanned transition total exceeds w.trans_cap
 void launch_cap_check(const DevBatch& b, DevWork& w, hipStream_t s);
 // index tier -> LDS search tier -> global tier, spill lists on the device
 // (counters_i32[3] / [4] / [6] must be zero on entry)
 void launch_transitions(const DevGraph& g, const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s,
-                        const Marks& mk, int sub);
+                        const Marks& mk, int sub, int from = RESUME_ALL);
 void launch_viterbi(const DevBatch& b, DevWork& w, hipStream_t s, const Marks& mk);
 void launch_route(const DevGraph& g, const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s,
-                  const Marks& mk);
+                  const Marks& mk, int from = RESUME_ALL);
 void launch_segments(const DevGraph& g, const DevBatch& b, DevWork& w, DevOut& o, bool write, hipStream_t s,
                      const Marks& mk);
 void launch_report(const DevBatch& b, const DevReportCfg& rc, DevWork& w, DevOut& o, hipStream_t s, const Marks& mk);
 // spatial work order: tile counts, plan (group cuts), scatter of the columns
 void launch_order(const DevBatch& b, DevWork& w, hipStream_t s, const Marks& mk);
-// per-trace bound of the segments / way ids its matched points can emit, added
-// into tb[T] (zeroed by the caller; scanned into DevOut::seg_base)
+// K7a: each trace's segment bound added into tb[T] (zeroed by the caller;
+// scanned into DevOut::seg_base) and the interpolated points placed
 void launch_seg_bound(const DevGraph& g, const DevBatch& b, const DevParams& p, DevWork& w, int64_t* tb, hipStream_t s,
                       const Marks& mk);
 // fetch-time compaction of the per-trace regions into dense arrays; offsets
@@ -370,7 +374,8 @@ void launch_row_sizes(const int32_t* row_cnt, int64_t* row_sizes, int32_t n, int
 struct BatchStatus {
   int32_t abort, grow;  // grow bit 0: the huge search tier needs (larger) tables; bit 1: the candidate HBM tier
   int64_t ttotal;
-  int32_t cnt[3], pad2;
+  int32_t cnt[3];
+  int32_t route_huge;   // counters_i32[22]: the route stage reached its huge tier (else the transition stage did)
 };
 void launch_batch_init(int32_t* counters, int32_t* abort, hipStream_t s);
 // otm_match_compact's inputs widened on the device (time = base + delta, accuracy as float)

@@ -1090,6 +1090,7 @@ __global__ void k_status(const int32_t* abort, const int64_t* ttotal, const int3
     out->cnt[0] = counters[0];
     out->cnt[1] = counters[1];
     out->cnt[2] = counters[2];
+    out->route_huge = counters[22];
   }
 }
 
@@ -3818,12 +3819,15 @@ __device__ float interp_pos(const DevGraph& g, const DevBatch& b, const DevParam
 
 // Traversals a matched point can add: the close of the open traversal, its
 // route's path edges, the re-open (+ the chain's final close): <= 2 + path.
-// Summed per trace into tb[t] (zeroed by the host; its exclusive scan is each
-// trace's segment region, DevOut::seg_base): a wave's points are runs of
-// whole traces, so a segmented suffix sum over the wave leaves each run's
-// total on its first lane, which adds it with one atomic -- no per-point
-// bound array, no point-length scan.  An interpolated point's thread places
-// it instead (K7a).
+// Summed per trace into tb[t] (scanned over traces into DevOut::seg_base): a
+// wave's points are runs of whole traces, so a segmented suffix sum over the
+// wave leaves each run's total on its first lane, which adds it with one
+// atomic -- no per-point bound array, no point-length scan (round 6).  An
+// interpolated point's thread places it instead (K7a).  Measured against a
+// wave per trace (coalesced runs, no atomics): 0.027 vs 0.032 ms on config 2,
+// 0.067 vs 0.064 on config 4; and against each trace's region taken from one
+// cursor by k_segments (no bound pass at all): k_segments 0.047 -> 0.142 ms on
+// config 2, the one address's atomics serialised (profiles/r06/k7/).
 __global__ __launch_bounds__(256) void k_seg_bound(DevGraph g, DevBatch b, DevParams P, DevWork w, int64_t* tb) {
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   // spill snapshot C: steps per route tier (kept for the status read)
@@ -4017,17 +4021,19 @@ void launch_order(const DevBatch& b, DevWork& w, hipStream_t s, const Marks& mk)
 }
 
 void launch_candidates(const DevGraph& g, const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s,
-                       const Marks& mk) {
+                       const Marks& mk, int from) {
   // (the work counters in their own instance: their registers cost the
   // uncounted one entries in flight)
-  if (w.ctr)
-    TIMED(KN_CAND_LANE, hipLaunchKernelGGL(k_cand_lane<true>, dim3(order_grid(b.n_points, CAND_TB, 1 << 30)),
-                                           dim3(CAND_TB), 0, s, g, b, p, w));
-  else
-    TIMED(KN_CAND_LANE, hipLaunchKernelGGL(k_cand_lane<false>, dim3(order_grid(b.n_points, CAND_TB, 1 << 30)),
-                                           dim3(CAND_TB), 0, s, g, b, p, w));
+  if (from < RESUME_CAND_BIG) {
+    if (w.ctr)
+      TIMED(KN_CAND_LANE, hipLaunchKernelGGL(k_cand_lane<true>, dim3(order_grid(b.n_points, CAND_TB, 1 << 30)),
+                                             dim3(CAND_TB), 0, s, g, b, p, w));
+    else
+      TIMED(KN_CAND_LANE, hipLaunchKernelGGL(k_cand_lane<false>, dim3(order_grid(b.n_points, CAND_TB, 1 << 30)),
+                                             dim3(CAND_TB), 0, s, g, b, p, w));
+  }
   mk.begin(KN_CAND_WAVE, s);
-  hipLaunchKernelGGL(k_candidates<false>, dim3(4096), dim3(TB), 0, s, g, b, p, w);
+  if (from < RESUME_CAND_BIG) hipLaunchKernelGGL(k_candidates<false>, dim3(4096), dim3(TB), 0, s, g, b, p, w);
   hipLaunchKernelGGL(k_candidates<true>, dim3(CAND_BIG_SLOTS), dim3(TB), 0, s, g, b, p, w);
   mk.end(KN_CAND_WAVE, s);
 }
@@ -4071,7 +4077,14 @@ void launch_cap_check(const DevBatch& b, DevWork& w, hipStream_t s) {
   hipLaunchKernelGGL(k_cap_check, dim3(1), dim3(1), 0, s, b, w);
 }
 void launch_transitions(const DevGraph& g, const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s,
-                        const Marks& mk, int sub) {
+                        const Marks& mk, int sub, int from) {
+  if (from >= RESUME_TRANS_HUGE) {
+    // the tiers below the huge one kept their matrices: the huge tier alone
+    mk.begin(KN_TRANS_GLOBAL, s);
+    hipLaunchKernelGGL(k_transitions<2>, dim3(HUGE_SLOTS), dim3(TB), 0, s, g, b, p, w);
+    mk.end(KN_TRANS_GLOBAL, s);
+    return;
+  }
   // many more waves than fit at once (each column is a few dependent
   // round trips): measured 0.78 ms at 16K waves, 0.67 ms at 64K; a grid of
   // one resident round was slowest (0.92 ms, partial rounds at 7 waves/SIMD)
@@ -4137,7 +4150,13 @@ void launch_viterbi(const DevBatch& b, DevWork& w, hipStream_t s, const Marks& m
   mk.end(KN_VITERBI, s);
 }
 void launch_route(const DevGraph& g, const DevBatch& b, const DevParams& p, DevWork& w, hipStream_t s,
-                  const Marks& mk) {
+                  const Marks& mk, int from) {
+  if (from >= RESUME_ROUTE_HUGE) {
+    mk.begin(KN_ROUTE_GLOBAL, s);
+    hipLaunchKernelGGL(k_route<2>, dim3(HUGE_SLOTS), dim3(TB), 0, s, g, b, p, w);
+    mk.end(KN_ROUTE_GLOBAL, s);
+    return;
+  }
   TIMED(KN_ROUTE_INDEX, hipLaunchKernelGGL(k_route_index, dim3(order_grid(b.n_points, 256, 1 << 30)), dim3(256), 0,
                                            s, g, b, p, w));
   TIMED(KN_ROUTE_WAVE, hipLaunchKernelGGL(k_route<0>, dim3(SPILL_GRID), dim3(TB), 0, s, g, b, p, w));

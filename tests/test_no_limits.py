@@ -178,6 +178,10 @@ def test_gpu_star_candidate_hbm_tier(star, oracle, results_equal, monkeypatch, p
     assert first["cand_big"] == len(star_batch()["lat"])  # every probe: 400 edges
     assert first["attempts"] >= 2  # the tables were made on demand ...
     assert second["attempts"] == 1 and second["cand_big"] == first["cand_big"]  # ... and kept
+    # the runs for the tier's growth resumed at the candidate HBM tier (round
+    # 6); a transition-matrix overflow in the same batch still redoes it whole
+    assert first["resumed"] >= 1 and second["resumed"] == 0
+    assert second["cand_wave"] == first["cand_wave"]  # the spill snapshots survive the resume
 
 
 @pytest.mark.gpu
@@ -186,6 +190,12 @@ def test_gpu_long_gaps_huge_search_tier(dense_grid, oracle, results_equal):
     assert first["trans_huge"] > 0 and first["route_huge"] > 0
     assert first["attempts"] >= 2
     assert second["attempts"] == 1
+    # the runs after the first resumed at the huge tier of the transition or
+    # route stage (round 6); the spill snapshots equal the clean run's
+    assert first["resumed"] >= 1 and second["resumed"] == 0
+    for k in ("cand_wave", "trans_online", "trans_global", "route_online", "route_global", "trans_huge",
+              "route_huge"):
+        assert first[k] == second[k], k
 
 
 @pytest.mark.gpu
@@ -260,3 +270,32 @@ def test_gpu_tables_that_cannot_grow_fail_their_traces_only(star, dense_grid, or
         ra, rn = tr["rep_off"][t], tr["rep_cnt"][t]
         ora, orn = orc["traces"]["rep_off"][t], orc["traces"]["rep_cnt"][t]
         assert res.reports[ra:ra + rn].tobytes() == orc["reports"][ora:ora + orn].tobytes()
+
+
+@pytest.mark.gpu
+def test_gpu_resume_equals_whole_redo(dense_grid, oracle, results_equal, monkeypatch):
+    """A batch of ordinary traces with one whose 600 s gaps need the huge
+    search tier: on a fresh engine the tier's tables are made on demand and
+    the batch resumes at that tier (round 6) -- its results equal a whole
+    redo's (OTM_NO_RESUME, rounds 1-5), a clean run's on tables already
+    grown, and the oracle's."""
+    from reporter_amd import Engine
+    normal = synth.make_traces(dense_grid, 300, 30, interval_s=5.0, noise_sigma_m=5.0, accuracy=5.0, seed=11)
+    far = grid_batch(dense_grid)
+    b = {k: np.concatenate([normal[k], far[k]]) for k in ("lat", "lon", "time", "accuracy")}
+    b["trace_off"] = np.concatenate([normal["trace_off"], normal["trace_off"][-1] + far["trace_off"][1:]])
+    with Engine(graph_path=dense_grid, **GRID_MEILI) as eng:
+        first = eng.match(b)
+        st1 = eng.spill_stats()
+        clean = eng.match(b)
+        st2 = eng.spill_stats()
+    monkeypatch.setenv("OTM_NO_RESUME", "1")
+    with Engine(graph_path=dense_grid, **GRID_MEILI) as eng:
+        whole = eng.match(b)
+        st3 = eng.spill_stats()
+    assert st1["attempts"] >= 2 and st1["resumed"] >= 1
+    assert st2["attempts"] == 1 and st3["resumed"] == 0 and st3["attempts"] >= 2
+    orc = oracle.match_batch(oracle.Graph(dense_grid), b, p=oracle.params(**GRID_MEILI), nthreads=4)
+    results_equal(orc, first, "resumed")
+    results_equal(orc, clean, "clean")
+    results_equal(orc, whole, "whole redo")

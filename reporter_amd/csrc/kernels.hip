@@ -621,14 +621,16 @@ __global__ __launch_bounds__(CAND_TB, OTM_CAND_WAVES) void k_cand_lane(DevGraph 
             if (spill || !(sqd <= r2)) continue;
             const uint32_t ent = en[u];
             const uint32_t e = ent >> 4;
-            int f = -1;
-            // every slot's edge read at once (independent LDS reads, no
-            // early exit): one LDS round trip per hit instead of up to 8
+            // every slot's edge read at once and unconditionally -- slots past
+            // n hold stale words, masked by the select -- so the compiler
+            // emits eight LDS reads and selects, not eight guarded branches
+            // (one LDS round trip per hit instead of up to 8)
+            uint32_t ev[CAND_LANE_CAP];
 #pragma unroll
-            for (int m = 0; m < CAND_LANE_CAP; ++m) {
-              const uint32_t em = E[m * S];
-              if (m < n && (em >> 4) == e) f = m;
-            }
+            for (int m = 0; m < CAND_LANE_CAP; ++m) ev[m] = E[m * S];
+            int f = -1;
+#pragma unroll
+            for (int m = 0; m < CAND_LANE_CAP; ++m) f = (m < n && (ev[m] >> 4) == e) ? m : f;
             if (f < 0) {
               if (n == CAND_LANE_CAP) {
                 spill = true;

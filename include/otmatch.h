@@ -445,6 +445,12 @@ typedef struct otm_spill_stats {
    * (the stages before it kept their results) instead of redoing the batch */
   int32_t resumed;
 } otm_spill_stats;
+/* The stats (like otm_get_stage_ms / otm_get_kernel_ms / otm_get_counters)
+ * describe the last batch run on this handle's own batch context.  An
+ * otm_report_batch of 4,096 requests or more runs its two halves on the
+ * engine's clones, and otm_submit / otm_submit_batch run on the async
+ * pipeline's clones: those batches do not update the handle's figures (each
+ * clone keeps its own, and grows its own on-demand tier tables). */
 int otm_get_spill_stats(otm_engine* eng, otm_spill_stats* out);
 
 /* Stage outputs of the last batch, for parity tests (device -> host copy).

@@ -11,7 +11,7 @@ TAG=${1:-final}
 O=gpurun_out/$TAG
 mkdir -p $R/$O
 cd $R
-FAST="--no-cpu-baseline --no-check --host-steps 0 --json-calls 0 --inflight 1"
+FAST="--no-cpu-baseline --no-check --host-steps 0 --json-calls 0 --stream-runs 0 --inflight 1"
 if [ "${PART:-1}" = "1" ]; then
   timeout -k 10 700 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1
   (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$O/prof1 -o run -- python3 $R/bench.py --steps 10 --warmup 3 $FAST > $R/$O/prof1.log 2>&1)

@@ -12,7 +12,7 @@ OUT=$R/${1:-gpurun_out/pmc}
 TAG=${2:-latest}
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
-BENCH="python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-check --host-steps 0 --json-calls 0 --traffic-json none --inflight 1 ${PMC_BENCH_ARGS:-}"
+BENCH="python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-check --host-steps 0 --json-calls 0 --stream-runs 0 --traffic-json none --inflight 1 ${PMC_BENCH_ARGS:-}"
 pass() {
   local name=$1; shift
   timeout -s KILL 120 rocprofv3 --pmc "$@" --output-format csv -d $OUT/$name -o $name -- $BENCH > $OUT/$name.log 2>&1

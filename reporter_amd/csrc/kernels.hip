@@ -65,12 +65,12 @@ __device__ __forceinline__ float seg_sqdist(float alat, float alon, float blat, 
   const float vx = bx - ax;
   const float vy = by - ay;
   const float l2 = vx * vx + vy * vy;
-  float t = 0.0f;
-  if (l2 > 0.0f) {
-    const float dot = ax * vx + ay * vy;
-    t = -dot / l2;
-    t = t < 0.0f ? 0.0f : (t > 1.0f ? 1.0f : t);
-  }
+  // branch-free: the quotient of a zero-length segment (inf / nan) is
+  // selected away, so the lanes of the scan never split here
+  const float dot = ax * vx + ay * vy;
+  float t = -dot / l2;
+  t = t < 0.0f ? 0.0f : (t > 1.0f ? 1.0f : t);
+  t = l2 > 0.0f ? t : 0.0f;
   const float px = ax + t * vx;
   const float py = ay + t * vy;
   return px * px + py * py;
@@ -3305,7 +3305,12 @@ __global__ __launch_bounds__(TB, (PT <= 128 ? 4 : 2)) void k_segments(DevGraph g
 #pragma unroll
     for (int c = 0; c < NCH; ++c)
       if (c * TB + lane < ns) rs[c] = state_step(w, b, a, S, c * TB + lane, ns);
-    // ---- per state: opener fields, chain index, latest opener, slot counts
+    // ---- per state: chain index, latest opener, slot counts (registers only);
+    // the open edge's length of a state that leaves it is loaded here, so its
+    // round trip overlaps the scans and the route-edge fetch below
+    float elen[NCH];
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) elen[c] = 0.0f;
     int c_chain = 0, c_open = -1, c_base = 0;
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
@@ -3316,25 +3321,8 @@ __global__ __launch_bounds__(TB, (PT <= 128 ? 4 : 2)) void k_segments(DevGraph g
       if (valid) {
         const StateStep& r = rs[c];
         cs = r.cs() ? 1 : 0;
-        if (r.cs() || !r.same()) {
-          opener = k;
-          if (r.cs()) {
-            S.o_t0[k] = r.tb;
-            S.o_off0[k] = r.oj;
-            S.o_sh0[k] = (int16_t)r.pl();
-          } else {
-            const float start = cand_node(r.oi) ? 0.0f : rec_len(edge_rec(g, r.ei)) - r.oi;  // src_start
-            float dd = 0.0f;
-            for (int i = 0; i < r.plen; ++i) dd = dd + rec_len(edge_rec(g, w.path_pool[r.poff + i]));
-            const float x = start + dd;
-            double t0;
-            int sh;
-            step_bound(b, w, a, r.lp(), r.pl(), r.rd, r.ta, r.tb, x, t0, sh);
-            S.o_t0[k] = t0;
-            S.o_off0[k] = 0.0f;
-            S.o_sh0[k] = (int16_t)sh;
-          }
-        }
+        if (r.cs() || !r.same()) opener = k;
+        if (!r.cs() && !r.same()) elen[c] = rec_len(edge_rec(g, r.ei));
         // the close of the open traversal (none from a node candidate), the
         // route's edges, the chain's final close (none at a node candidate)
         nem = (r.step() && !r.same() ? (cand_node(r.oi) ? 0 : 1) + r.plen : 0) +
@@ -3363,6 +3351,68 @@ __global__ __launch_bounds__(TB, (PT <= 128 ? 4 : 2)) void k_segments(DevGraph g
       __syncthreads();
       continue;
     }
+    // ---- the route edges: each state marks its route edges' slots with their
+    // pool positions (every other slot -1), then the wave fetches every slot's
+    // edge and length at once, a lane a slot -- one round trip for the
+    // trace's path edges instead of two per edge along each state's path
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int k = c * TB + lane;
+      if (k >= ns) continue;
+      const StateStep& r = rs[c];
+      int slot = S.tbase[k];
+      if (r.step() && !r.same()) {
+        if (!cand_node(r.oi)) S.t_edge[slot++] = -1;
+        for (int i = 0; i < r.plen; ++i) S.t_edge[slot++] = -2 - (r.poff + i);
+      }
+      if (r.last() && !r.cs() && !cand_node(r.oj)) S.t_edge[slot] = -1;
+    }
+    __syncthreads();
+    {
+      constexpr int NTC = (TR + TB - 1) / TB;
+      int32_t pe[NTC];
+#pragma unroll
+      for (int c = 0; c < NTC; ++c) {
+        const int s = c * TB + lane;
+        const int32_t v = s < nt ? S.t_edge[s] : -1;
+        pe[c] = v <= -2 ? w.path_pool[-2 - v] : -1;
+      }
+#pragma unroll
+      for (int c = 0; c < NTC; ++c) {
+        const int s = c * TB + lane;
+        if (pe[c] >= 0) {
+          S.t_edge[s] = pe[c];
+          S.t_off1[s] = rec_len(edge_rec(g, pe[c]));
+        }
+      }
+    }
+    __syncthreads();
+    // ---- opener fields: a chain start's own, or the re-open on the new edge
+    // at the end of the step's route (its length summed in route order)
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int k = c * TB + lane;
+      if (k >= ns) continue;
+      const StateStep& r = rs[c];
+      if (r.cs()) {
+        S.o_t0[k] = r.tb;
+        S.o_off0[k] = r.oj;
+        S.o_sh0[k] = (int16_t)r.pl();
+      } else if (!r.same()) {
+        const float start = cand_node(r.oi) ? 0.0f : elen[c] - r.oi;  // src_start
+        const int s0 = S.tbase[k] + (cand_node(r.oi) ? 0 : 1);
+        float dd = 0.0f;
+        for (int i = 0; i < r.plen; ++i) dd = dd + S.t_off1[s0 + i];
+        const float x = start + dd;
+        double t0;
+        int sh;
+        step_bound(b, w, a, r.lp(), r.pl(), r.rd, r.ta, r.tb, x, t0, sh);
+        S.o_t0[k] = t0;
+        S.o_off0[k] = 0.0f;
+        S.o_sh0[k] = (int16_t)sh;
+      }
+    }
+    __syncthreads();
     // ---- traversals, each state writing its own
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
@@ -3374,15 +3424,15 @@ __global__ __launch_bounds__(TB, (PT <= 128 ? 4 : 2)) void k_segments(DevGraph g
       if (r.step() && !r.same()) {
         const float Rd = r.rd;
         const double ta = r.ta, tb = r.tb;
-        const float elen = rec_len(edge_rec(g, r.ei));
-        const float start = cand_node(r.oi) ? 0.0f : elen - r.oi;  // src_start
+        const float el = elen[c];
+        const float start = cand_node(r.oi) ? 0.0f : el - r.oi;  // src_start
         if (!cand_node(r.oi)) {
           const int jo = S.lopen[k - 1];
           S.t_edge[slot] = r.ei;
           S.t_off0[slot] = S.o_off0[jo];
           S.t_t0[slot] = S.o_t0[jo];
           S.t_sh0[slot] = S.o_sh0[jo];
-          S.t_off1[slot] = elen;
+          S.t_off1[slot] = el;
           double t1;
           int sh;
           step_bound(b, w, a, r.lp(), r.pl(), Rd, ta, tb, start, t1, sh);
@@ -3393,14 +3443,11 @@ __global__ __launch_bounds__(TB, (PT <= 128 ? 4 : 2)) void k_segments(DevGraph g
         }
         float dd = 0.0f;
         for (int i = 0; i < r.plen; ++i) {
-          const int32_t pe = w.path_pool[r.poff + i];
-          const float len = rec_len(edge_rec(g, pe));
+          const float len = S.t_off1[slot];  // (edge and length fetched above)
           const float xb = start + dd;
           dd = dd + len;
           const float xe = start + dd;
-          S.t_edge[slot] = pe;
           S.t_off0[slot] = 0.0f;
-          S.t_off1[slot] = len;
           double tt;
           int sh;
           step_bound(b, w, a, r.lp(), r.pl(), Rd, ta, tb, xb, tt, sh);

@@ -32,6 +32,15 @@ namespace {
 constexpr uint32_t EMPTY = 0xFFFFFFFFu;
 constexpr unsigned long long LAB_NONE = ~0ull;
 constexpr int TB = 64;  // one wavefront per workgroup for the wave kernels
+// A one-wavefront block's LDS operations execute in issue order, so its
+// cross-lane LDS hand-offs need only the compiler kept from moving memory
+// accesses across this point.  __syncthreads() would also wait for every
+// global load and store in flight (s_waitcnt vmcnt(0)): the next chunks'
+// prefetches, or the last item's result stores before the next item starts.
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+}
 
 __device__ __forceinline__ float cos_deg(float deg) {
   const float x = deg * 0.017453292519943295f;
@@ -1623,7 +1632,7 @@ __global__ __launch_bounds__(TB, OTM_TRANS_WAVES) void k_trans_sub(DevGraph g, D
       w.overflow_list0[slot] = (int32_t)p;
     }
     act = act && !spill;
-    __syncthreads();
+    wave_sync();
     if (act) {
       float* Tm = w.trans + toff;
       unsigned long long ntr = 0;
@@ -1725,7 +1734,7 @@ __global__ __launch_bounds__(TB, OTM_TRANS_WAVES) void k_trans_sub(DevGraph g, D
         c_trans += ntr;
       }
     }
-    __syncthreads();
+    wave_sync();
   }
   if (w.ctr) {
     for (int sh = 32; sh > 0; sh >>= 1) {
@@ -2454,14 +2463,9 @@ __global__ __launch_bounds__(TB, OTM_VIT_WAVES) void k_viterbi(DevBatch b, DevWo
 // VG_PTS points, goes to the next form's list (G = 8 -> G = 16 -> the wave
 // form).  Same recurrence (min over i in order, strict <), tie rules and chain
 // breaks as viterbi_trace_global: bit-identical to the oracle.
-// The block is one wavefront (TB = 64): its LDS operations execute in issue
-// order, so a chunk's staging only needs the compiler kept from moving LDS
-// accesses across this point.  __syncthreads() would also wait for every
-// global load in flight -- the next chunks' prefetches.
-__device__ __forceinline__ void wave_sync() {
-  __builtin_amdgcn_wave_barrier();
-  asm volatile("" ::: "memory");
-}
+// The block is one wavefront (TB = 64): a chunk's staging needs only
+// wave_sync(), not __syncthreads(), which would wait for the next chunks'
+// prefetches.
 __device__ __forceinline__ int wave_max_i(int v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -3164,6 +3168,38 @@ __device__ void segments_trace(const DevGraph& g, const DevWork& w, DevOut& o, i
 // traversals: 13.6 KB, 3 waves per SIMD); one that does not fit goes to a
 // list for the large one (256 / 512: 26.6 KB); beyond that, the serial walk.
 // Measured on config 2: 0.131 -> 0.111 ms against the large plan alone.
+// Diagnostic phase timing of k_segments (a build with -DOTM_SEG_PROF only):
+// per wave the clock between the phase boundaries, summed over the launch and
+// printed by the launch's last wave for a launch over >= 50k traces.
+#ifdef OTM_SEG_PROF
+__device__ unsigned long long g_segp[10];
+__device__ unsigned int g_segp_done, g_segp_prints;
+#define SEGP_DECL unsigned long long segp_acc[9] = {}; long long segp_t = 0; unsigned long long segp_n = 0;
+#define SEGP_START { segp_t = clock64(); ++segp_n; }
+#define SEGP_MARK(i) { const long long _n = clock64(); segp_acc[i] += (unsigned long long)(_n - segp_t); segp_t = _n; }
+#define SEGP_END                                                                                          \
+  if (threadIdx.x == 0) {                                                                                 \
+    for (int _i = 1; _i <= 8; ++_i) atomicAdd(&g_segp[_i], segp_acc[_i]);                                 \
+    atomicAdd(&g_segp[9], segp_n);                                                                        \
+    __threadfence();                                                                                      \
+    if (atomicAdd(&g_segp_done, 1u) == gridDim.x - 1) {                                                   \
+      unsigned long long v[10];                                                                           \
+      for (int _i = 1; _i <= 9; ++_i) v[_i] = atomicAdd(&g_segp[_i], 0ull);                               \
+      if (nwork >= 5000 && atomicAdd(&g_segp_prints, 1u) < 4)                                            \
+        printf("SEGP traces %llu cycles/trace: states %llu scan %llu mark %llu fetch %llu opener %llu "  \
+               "trav %llu group %llu record %llu\n", v[9], v[1] / v[9], v[2] / v[9], v[3] / v[9],      \
+               v[4] / v[9], v[5] / v[9], v[6] / v[9], v[7] / v[9], v[8] / v[9]);                         \
+      for (int _i = 0; _i <= 9; ++_i) atomicExch(&g_segp[_i], 0ull);                                     \
+      atomicExch(&g_segp_done, 0u);                                                                       \
+    }                                                                                                     \
+  }
+#else
+#define SEGP_DECL
+#define SEGP_START
+#define SEGP_MARK(i)
+#define SEGP_END
+#endif
+
 template <int PT, int TR>
 struct SegParT {
   double o_t0[PT];  // per state: start time of the traversal it opens
@@ -3262,7 +3298,9 @@ __global__ __launch_bounds__(TB, (PT <= 128 ? 4 : 2)) void k_segments(DevGraph g
   const int lane = threadIdx.x;
   const unsigned long long lt = (1ull << lane) - 1ull;
   const int32_t nwork = list ? *list_n : b.n_traces;
+  SEGP_DECL
   for (int32_t it = blockIdx.x; it < nwork; it += gridDim.x) {
+    SEGP_START
     const int32_t t = list ? list[it] : it;
     const int64_t a = b.trace_off[t];
     const int n = (int)(b.trace_off[t + 1] - a);
@@ -3299,7 +3337,8 @@ __global__ __launch_bounds__(TB, (PT <= 128 ? 4 : 2)) void k_segments(DevGraph g
       if (stv[c]) S.sidx[ns + __popcll(m & lt)] = (int16_t)(c * TB + lane);
       ns += __popcll(m);
     }
-    __syncthreads();
+    wave_sync();
+    SEGP_MARK(1)
     // every state's loads at once, kept in registers for both passes below
     StateStep rs[NCH];
 #pragma unroll
@@ -3342,13 +3381,14 @@ __global__ __launch_bounds__(TB, (PT <= 128 ? 4 : 2)) void k_segments(DevGraph g
       c_base += __shfl(inc, 63, 64);
     }
     const int nt = c_base;
-    __syncthreads();
+    wave_sync();
+    SEGP_MARK(2)
     if (nt > TR) {
       if (lane == 0) {
         if (spill) spill[atomicAdd(spill_n, 1)] = t;
         else segments_trace<true>(g, w, o, t, n, base, SegSrcGlobal{&g, &b, &w, a});
       }
-      __syncthreads();
+      wave_sync();
       continue;
     }
     // ---- the route edges: each state marks its route edges' slots with their
@@ -3367,7 +3407,8 @@ __global__ __launch_bounds__(TB, (PT <= 128 ? 4 : 2)) void k_segments(DevGraph g
       }
       if (r.last() && !r.cs() && !cand_node(r.oj)) S.t_edge[slot] = -1;
     }
-    __syncthreads();
+    wave_sync();
+    SEGP_MARK(3)
     {
       constexpr int NTC = (TR + TB - 1) / TB;
       int32_t pe[NTC];
@@ -3386,7 +3427,8 @@ __global__ __launch_bounds__(TB, (PT <= 128 ? 4 : 2)) void k_segments(DevGraph g
         }
       }
     }
-    __syncthreads();
+    wave_sync();
+    SEGP_MARK(4)
     // ---- opener fields: a chain start's own, or the re-open on the new edge
     // at the end of the step's route (its length summed in route order)
 #pragma unroll
@@ -3412,7 +3454,8 @@ __global__ __launch_bounds__(TB, (PT <= 128 ? 4 : 2)) void k_segments(DevGraph g
         S.o_sh0[k] = (int16_t)sh;
       }
     }
-    __syncthreads();
+    wave_sync();
+    SEGP_MARK(5)
     // ---- traversals, each state writing its own
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
@@ -3479,7 +3522,8 @@ __global__ __launch_bounds__(TB, (PT <= 128 ? 4 : 2)) void k_segments(DevGraph g
         S.t_chain[slot] = chk;
       }
     }
-    __syncthreads();
+    wave_sync();
+    SEGP_MARK(6)
     // ---- groups (OSMLR segments) and way ids
     // (one 16-byte edge record per traversal; ways compared by number, the id
     // looked up only for the way ids written)
@@ -3537,7 +3581,8 @@ __global__ __launch_bounds__(TB, (PT <= 128 ? 4 : 2)) void k_segments(DevGraph g
       S.g_last[c_seg - 1] = (int16_t)(nt - 1);
       S.g_w0[c_seg] = (int16_t)c_way;
     }
-    __syncthreads();
+    wave_sync();
+    SEGP_MARK(7)
     // ---- one record per group (SegEmitter::flush)
     for (int s0 = 0; s0 < c_seg; s0 += TB) {
       const int si = s0 + lane;
@@ -3591,8 +3636,10 @@ __global__ __launch_bounds__(TB, (PT <= 128 ? 4 : 2)) void k_segments(DevGraph g
       o.seg_cnt[t] = c_seg;
       o.way_cnt[t] = c_way;
     }
-    __syncthreads();
+    wave_sync();
+    SEGP_MARK(8)
   }
+  SEGP_END
 }
 
 // ============================================================== K8 report

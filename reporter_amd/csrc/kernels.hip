@@ -2379,20 +2379,25 @@ __global__ __launch_bounds__(TB, OTM_VIT_WAVES) void k_viterbi(DevBatch b, DevWo
           const int pbits = __float_as_int(prev);
           int i = 0;
           for (; i + 4 <= Kq; i += 4) {
-            // four independent LDS reads in flight; visited in i order
+            // four independent LDS reads in flight.  The four in i order with
+            // strict < are: the chunk's minimum, if below best, at the first
+            // u that reaches it -- a min tree and three selects instead of
+            // four compare-and-select pairs (sums of costs >= +0: no NaN, no
+            // -0, so min and == see exactly what < saw)
             float tv[4], pv[4];
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
               tv[u] = Tm[(i + u) * Kp];
               pv[u] = __int_as_float(__builtin_amdgcn_readlane(pbits, i + u));
             }
+            float v[4];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-              const float v = pv[u] + tv[u];
-              if (v < best) {
-                best = v;
-                bi = i + u;
-              }
+            for (int u = 0; u < 4; ++u) v[u] = pv[u] + tv[u];
+            const float m = fminf(fminf(v[0], v[1]), fminf(v[2], v[3]));
+            const int fu = v[0] == m ? 0 : (v[1] == m ? 1 : (v[2] == m ? 2 : 3));
+            if (m < best) {
+              best = m;
+              bi = i + fu;
             }
           }
           for (; i < Kq; ++i) {

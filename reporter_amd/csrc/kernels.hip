@@ -2675,13 +2675,18 @@ __global__ __launch_bounds__(TB, G == 8 ? OTM_VG8_WAVES : 3) void k_viterbi_g(De
               tv[u] = link && i < lastK ? Tm[i * Kp] : INFINITY;
               pv[u] = __shfl(prev, gb + (i < G ? i : 0), TB);
             }
+            // (an i past lastK, or a lane of an unlinked group, reads +inf:
+            // its sum is +inf and never below best.)  In i order with strict
+            // <, the four are the chunk's minimum, if below best, at the first
+            // u that reaches it (k_viterbi's form; costs >= +0: no NaN or -0)
+            float v[4];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-              const float v = pv[u] + tv[u];
-              if (link && i0 + u < lastK && v < best) {
-                best = v;
-                bi = i0 + u;
-              }
+            for (int u = 0; u < 4; ++u) v[u] = pv[u] + tv[u];
+            const float m = fminf(fminf(v[0], v[1]), fminf(v[2], v[3]));
+            const int fu = v[0] == m ? 0 : (v[1] == m ? 1 : (v[2] == m ? 2 : 3));
+            if (m < best) {
+              best = m;
+              bi = i0 + fu;
             }
           }
           const bool alive = link && j < Kp && bi >= 0;

@@ -20,9 +20,8 @@ def main():
         km = line.get("kernel_ms", {})
         print(os.path.basename(f), "%.4fG" % (line["value"] / 1e9),
               " ".join("%s=%.4f" % (k, km[k]) for k in KERNELS if k in km))
-    log = os.path.join(d, "pytest_parity.log")
-    if os.path.exists(log):
-        print(open(log).read().strip().splitlines()[-1])
+    for log in sorted(glob.glob(os.path.join(d, "pytest*.log"))):
+        print(os.path.basename(log), open(log).read().strip().splitlines()[-1])
 
 
 if __name__ == "__main__":

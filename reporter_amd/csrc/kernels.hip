@@ -2517,6 +2517,9 @@ __global__ __launch_bounds__(TB, G == 8 ? OTM_VG8_WAVES : 3) void k_viterbi_g(De
   // backpointers, a nibble per state (15: dead), two states a byte: [point * G / 2 + state / 2]
   __shared__ uint8_t sBp[NT][VG_PTS * G / 2 + 4];
   __shared__ uint8_t sFl[NT][VG_PTS];  // flags; after the walk: VG_CS | (state + 1) << 3
+  // each group's previous-column scores, so a step reads four of them with one
+  // 16-byte broadcast read instead of four cross-lane shuffles
+  __shared__ __attribute__((aligned(16))) float sP[NT][G];
   const int lane = threadIdx.x;
   const int g = lane / G, j = lane % G, gb = g * G;
   const unsigned long long gmask = (1ull << G) - 1ull;
@@ -2603,6 +2606,7 @@ __global__ __launch_bounds__(TB, G == 8 ? OTM_VG8_WAVES : 3) void k_viterbi_g(De
     ld_data(1, m1, (int)(lo1 - t0), (int)(hi1 - t0), pTb, pEb);
     // ---- forward pass (wave-uniform step count; groups predicated)
     float prev = INFINITY;
+    sP[g][j] = INFINITY;
     bool open = false;
     int last = -1, lastK = 0;
     int acc = 0;  // the trace's transition floats before this column (K3's Kq x Kp counts, summed in order)
@@ -2669,11 +2673,15 @@ __global__ __launch_bounds__(TB, G == 8 ? OTM_VG8_WAVES : 3) void k_viterbi_g(De
           const float* Tm = &sT[g][tb + jj];
           for (int i0 = 0; __ballot(link && i0 < lastK) != 0ull; i0 += 4) {
             float tv[4], pv[4];
+            const float4 p4 = *(const float4*)&sP[g][i0 < G ? i0 : 0];
+            pv[0] = p4.x;
+            pv[1] = p4.y;
+            pv[2] = p4.z;
+            pv[3] = p4.w;
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
               const int i = i0 + u;
               tv[u] = link && i < lastK ? Tm[i * Kp] : INFINITY;
-              pv[u] = __shfl(prev, gb + (i < G ? i : 0), TB);
             }
             // (an i past lastK, or a lane of an unlinked group, reads +inf:
             // its sum is +inf and never below best.)  In i order with strict
@@ -2708,6 +2716,7 @@ __global__ __launch_bounds__(TB, G == 8 ? OTM_VG8_WAVES : 3) void k_viterbi_g(De
             sFl[g][pl] = VG_COL;
           }
           prev = cur;
+          sP[g][j] = cur;
           open = true;
           last = pl;
           lastK = Kp;

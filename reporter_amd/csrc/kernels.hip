@@ -90,13 +90,33 @@ __device__ __forceinline__ float seg_sqdist(float alat, float alon, float blat, 
 // k_cand_lane 0.229 vs 0.221 ms on config 2, 1.89 vs 1.85 on config 4; the
 // branch splits the wave where the division did not)
 
-__device__ __forceinline__ void project(const DevGraph& g, int32_t e, int32_t k, float lat, float lon, float ls,
-                                        float& sqd, float& off_out, bool& at_end) {
+// A projection's inputs (the shape segment's two points and cumulative
+// metres, the edge length and its last shape point), loaded apart from the
+// arithmetic so a caller can issue several projections' loads at once.
+struct ProjIn {
+  float alon, alat, blon, blat, ca, cb, len;
+  int32_t b, last;
+};
+__device__ __forceinline__ ProjIn proj_load(const DevGraph& g, int32_t e, int32_t k) {
+  ProjIn in;
   const int32_t a = g.e_shape_off[e] + k, b = a + 1;
-  const float ax = (g.s_lon[a] - lon) * ls;
-  const float ay = (g.s_lat[a] - lat) * MPD_F;
-  const float bx = (g.s_lon[b] - lon) * ls;
-  const float by = (g.s_lat[b] - lat) * MPD_F;
+  in.last = g.e_shape_off[e + 1] - 1;
+  in.alon = g.s_lon[a];
+  in.alat = g.s_lat[a];
+  in.blon = g.s_lon[b];
+  in.blat = g.s_lat[b];
+  in.ca = g.s_cum[a];
+  in.cb = g.s_cum[b];
+  in.len = g.e_len[e];
+  in.b = b;
+  return in;
+}
+__device__ __forceinline__ void proj_calc(const ProjIn& in, float lat, float lon, float ls, float& sqd,
+                                          float& off_out, bool& at_end) {
+  const float ax = (in.alon - lon) * ls;
+  const float ay = (in.alat - lat) * MPD_F;
+  const float bx = (in.blon - lon) * ls;
+  const float by = (in.blat - lat) * MPD_F;
   const float vx = bx - ax;
   const float vy = by - ay;
   const float l2 = vx * vx + vy * vy;
@@ -109,11 +129,14 @@ __device__ __forceinline__ void project(const DevGraph& g, int32_t e, int32_t k,
   const float px = ax + t * vx;
   const float py = ay + t * vy;
   sqd = px * px + py * py;
-  float off = g.s_cum[a] + t * (g.s_cum[b] - g.s_cum[a]);
-  const float len = g.e_len[e];
-  off_out = off > len ? len : off;
+  float off = in.ca + t * (in.cb - in.ca);
+  off_out = off > in.len ? in.len : off;
   // clamped to the edge's last shape point: the projection is its end node
-  at_end = t == 1.0f && b == g.e_shape_off[e + 1] - 1;
+  at_end = t == 1.0f && in.b == in.last;
+}
+__device__ __forceinline__ void project(const DevGraph& g, int32_t e, int32_t k, float lat, float lon, float ls,
+                                        float& sqd, float& off_out, bool& at_end) {
+  proj_calc(proj_load(g, e, k), lat, lon, ls, sqd, off_out, at_end);
 }
 __device__ __forceinline__ void project(const DevGraph& g, int32_t e, int32_t k, float lat, float lon, float ls,
                                         float& sqd, float& off_out) {
@@ -540,6 +563,12 @@ constexpr int CAND_TB = OTM_CAND_TB;
 #define OTM_CAND_INFL 2
 #endif
 constexpr int CAND_INFL = OTM_CAND_INFL;
+// lane tier node snap: entries whose projection loads are issued together
+// (more would spill under the 64-VGPR cap)
+#ifndef OTM_SNAP_B
+#define OTM_SNAP_B 2
+#endif
+constexpr int SNAP_B = OTM_SNAP_B;
 // transition index tier: pairs per lane whose first slot loads are issued
 // together.  Round 2 measured 2 best (0.337 -> 0.302 ms on config 2, 1.956 ->
 // 1.888 ms on config 4; 3 and 4 slower: registers, spills); on round 4's
@@ -666,16 +695,45 @@ __global__ __launch_bounds__(CAND_TB, OTM_CAND_WAVES) void k_cand_lane(DevGraph 
     }
     // node snap: an entry whose projection snaps to a node becomes that
     // node's candidate (NODE_ENT | first outgoing edge << 4), one per node
-    // at the smallest distance
+    // at the smallest distance.  First every entry's snap, SNAP_B entries'
+    // loads issued together (a pure function of the entry: round 6 -- the
+    // entry-by-entry walk waited on 3-4 dependent loads per entry); then the
+    // merge in entry order, out of LDS.
+    for (int m0 = 0; m0 < n; m0 += SNAP_B) {
+      uint32_t em[SNAP_B];
+      ProjIn pin[SNAP_B];
+#pragma unroll
+      for (int u = 0; u < SNAP_B; ++u) {
+        em[u] = m0 + u < n ? E[(m0 + u) * S] : 0u;
+        if (m0 + u < n) pin[u] = proj_load(g, (int32_t)(em[u] >> 4), (int32_t)(em[u] & 15u));
+      }
+      int32_t vx[SNAP_B];
+      bool node0[SNAP_B], at_end[SNAP_B];
+#pragma unroll
+      for (int u = 0; u < SNAP_B; ++u) {
+        vx[u] = 0;
+        node0[u] = at_end[u] = false;
+        if (m0 + u < n) {
+          float sqd, off;
+          proj_calc(pin[u], lat, lon, ls, sqd, off, at_end[u]);
+          node0[u] = off == 0.0f;
+          const int32_t e = (int32_t)(em[u] >> 4);
+          if (node0[u] || at_end[u]) vx[u] = node0[u] ? g.e_from[e] : g.e_to[e];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < SNAP_B; ++u) {
+        // snap_node's rule: the start node at offset 0; the end node when
+        // clamped there and it has an outgoing edge
+        if (node0[u] || at_end[u]) {
+          const int32_t o0 = g.out_off[vx[u]], o1 = g.out_off[vx[u] + 1];
+          if (node0[u] || o1 > o0) E[(m0 + u) * S] = NODE_ENT | ((uint32_t)o0 << 4);
+        }
+      }
+    }
     for (int m = 0; m < n; ++m) {
-      const uint32_t em = E[m * S];
-      const int32_t e = (int32_t)(em >> 4);
-      float sqd, off;
-      bool at_end;
-      project(g, e, (int32_t)(em & 15u), lat, lon, ls, sqd, off, at_end);
-      const int32_t v = snap_node(g, e, off, at_end);
-      if (v < 0) continue;
-      const uint32_t key = NODE_ENT | ((uint32_t)g.out_off[v] << 4);
+      const uint32_t key = E[m * S];
+      if (!(key & NODE_ENT)) continue;
       int f = -1;
       for (int t = 0; t < m; ++t)
         if (E[t * S] == key) f = t;
@@ -686,9 +744,7 @@ __global__ __launch_bounds__(CAND_TB, OTM_CAND_WAVES) void k_cand_lane(DevGraph 
         E[m * S] = E[n * S];
         Q[m * S] = Q[n * S];
         --m;
-        continue;
       }
-      E[m * S] = key;
     }
     const int K = n < P.max_candidates ? n : P.max_candidates;
     const float ds = (2.0f * P.sigma_z) * P.sigma_z;

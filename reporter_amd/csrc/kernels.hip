@@ -649,10 +649,14 @@ __global__ __launch_bounds__(CAND_TB, OTM_CAND_WAVES) void k_cand_lane(DevGraph 
             en[u] = 0;
             if (q + u < q1) {
               const float4 G = g.ent_geo[q + u];
-              en[u] = g.cell_ent[q + u];
               sq[u] = seg_sqdist(G.x, G.y, G.z, G.w, lat, lon, ls);
             }
           }
+          // the entry's id only for a hit (~1 in 7 entries): the scattered
+          // load is issued by the lanes that need it, not by every lane
+#pragma unroll
+          for (int u = 0; u < CAND_INFL; ++u)
+            if (sq[u] <= r2) en[u] = g.cell_ent[q + u];
 #pragma unroll
           for (int u = 0; u < CAND_INFL; ++u) {
             const float sqd = sq[u];

@@ -1678,7 +1678,9 @@ __global__ __launch_bounds__(TB, OTM_TRANS_WAVES) void k_trans_sub(DevGraph g, D
         const int2 c = crec(w, q, k);
         const int32_t e = c.x;
         const float o = __int_as_float(c.y);
-        sr[sg][k ^ swz] = make_int4(e, __float_as_int(o), __float_as_int(src_start(g, e, o)), (int)src_head(g, e, o));
+        // (the heading only for the work counters: no load otherwise)
+        sr[sg][k ^ swz] = make_int4(e, __float_as_int(o), __float_as_int(src_start(g, e, o)),
+                                    w.ctr ? (int)src_head(g, e, o) : 0);
         if (idx_ok) {
           const IdxRow R = xrow[src_row(g, e, o)];
           rq[sg][k ^ swz] = R;

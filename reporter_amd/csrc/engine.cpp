@@ -265,6 +265,20 @@ int engine_init(otm_engine* E, const char* graph_path, int device, std::string* 
     HIPCHK(hipMemcpy(d, ways.data(), ways.size() * 8, hipMemcpyHostToDevice));
     E->graph_allocs.push_back(d);
     g.way_tab = (const int64_t*)d;
+    // {from, length bits} per edge: K4 stages a source candidate's index row
+    // (from, for a node candidate) and start (length, for an edge candidate)
+    // with one 8-byte load instead of two masked 4-byte ones
+    const int32_t* from = (const int32_t*)E->host.section(OTMG_EDGE_FROM);
+    std::vector<int32_t> fl2((size_t)h.n_edges * 2 + 2, 0);
+    for (int32_t e = 0; e < h.n_edges; ++e) {
+      fl2[(size_t)e * 2] = from[e];
+      std::memcpy(&fl2[(size_t)e * 2 + 1], &len[e], 4);
+    }
+    d = nullptr;
+    HIPCHK(hipMalloc(&d, fl2.size() * 4));
+    HIPCHK(hipMemcpy(d, fl2.data(), fl2.size() * 4, hipMemcpyHostToDevice));
+    E->graph_allocs.push_back(d);
+    g.e_fl = (const int2*)d;
   }
   {
     // The grid index of the candidate search.  The file's cells (meili's

@@ -75,6 +75,7 @@ struct DevGraph {
   // K7's per-edge record {len bits, seg, seg_pos | flags << 24, way number}
   // and the way numbers' ids (engine.cpp)
   const uint4* e_rec;
+  const int2* e_fl;  // {from node, length bits} per edge: a transition source's row and start in one load
   const int64_t* way_tab;
   int32_t n_nodes, n_edges, n_segments, grid_rows, grid_cols;
   double lat0, lon0, cell;

@@ -1678,11 +1678,13 @@ __global__ __launch_bounds__(TB, OTM_TRANS_WAVES) void k_trans_sub(DevGraph g, D
         const int2 c = crec(w, q, k);
         const int32_t e = c.x;
         const float o = __int_as_float(c.y);
-        // (the heading only for the work counters: no load otherwise)
-        sr[sg][k ^ swz] = make_int4(e, __float_as_int(o), __float_as_int(src_start(g, e, o)),
-                                    w.ctr ? (int)src_head(g, e, o) : 0);
+        // src_start and src_row from the edge's {from, length} pair (one
+        // load); the heading only for the work counters (no load otherwise)
+        const int2 fl = g.e_fl[e];
+        const float start = cand_node(o) ? 0.0f : __int_as_float(fl.y) - o;
+        sr[sg][k ^ swz] = make_int4(e, __float_as_int(o), __float_as_int(start), w.ctr ? (int)src_head(g, e, o) : 0);
         if (idx_ok) {
-          const IdxRow R = xrow[src_row(g, e, o)];
+          const IdxRow R = xrow[cand_node(o) ? (int64_t)g.n_edges + fl.x : (int64_t)e];
           rq[sg][k ^ swz] = R;
           bad = bad || R.cnt < 0;
         }

@@ -1872,8 +1872,10 @@ __global__ __launch_bounds__(256, OTM_ROUTE_WAVES) void k_route_index(DevGraph g
     for (int l = NEAR_LEVELS - 1; l >= 0; --l)
       if (w.idxn[l].rmax > 0.0f && cq <= w.idxn[l].cmax) lvl = l;
     const DevIndex& Xc = lvl >= 0 ? w.idxn[lvl] : X;
+    // the source's row and start from its edge's {from, length} pair (one load)
+    const int2 fli = g.e_fl[ei];
     if (X.rmax > 0.0f && cq <= X.cmax) {
-      Rw = Xc.row[src_row(g, ei, oi)];
+      Rw = Xc.row[cand_node(oi) ? (int64_t)g.n_edges + fli.x : (int64_t)ei];
       sv = idx_find(Xc.slot, Rw, dst_key(g, ej, oj), lab);
     }
     if (sv < 0 || idx_slot_cost(lab) > cq) {
@@ -1900,7 +1902,7 @@ __global__ __launch_bounds__(256, OTM_ROUTE_WAVES) void k_route_index(DevGraph g
       w.path_off[p] = off;
       w.path_len[p] = len;
     }
-    const float start = src_start(g, ei, oi);
+    const float start = cand_node(oi) ? 0.0f : __int_as_float(fli.y) - oi;  // src_start
     const float sd = start + bitsf(lab.z);
     w.route_dist[p] = sd + oj;
     if (w.ctr) {

@@ -3620,8 +3620,10 @@ __global__ __launch_bounds__(TB, (PT <= 128 ? 4 : 2)) void k_segments(DevGraph g
       const bool valid = k < nt;
       int32_t seg = -1, pos = 0, ch = -2, way = -1;
       uint32_t fl = 0;
+      float elk = 0.0f;
       if (valid) {
         const uint4 er = edge_rec(g, S.t_edge[k]);
+        elk = rec_len(er);
         seg = rec_seg(er);
         pos = rec_pos(er);
         fl = rec_flags(er);
@@ -3648,6 +3650,14 @@ __global__ __launch_bounds__(TB, (PT <= 128 ? 4 : 2)) void k_segments(DevGraph g
       const unsigned long long ms = __ballot(start), mw = __ballot(wemit);
       const int gi = c_seg + __popcll(ms & lt) + (start ? 0 : -1);  // this traversal's group
       const int wi = c_way + __popcll(mw & lt);
+      if (valid) {
+        // what the record pass needs of this traversal's edge, kept in the two
+        // slots it no longer reads (its edge and chain): the segment index, and
+        // the flags with whether the traversal ends at the edge's end -- no
+        // second and third gather of the edge record there
+        S.t_edge[k] = seg;
+        S.t_chain[k] = (int16_t)(fl | (S.t_off1[k] == elk ? 0x100u : 0u));
+      }
       if (wemit) o.way_ids[base + wi] = g.way_tab[way];
       if (start) {
         S.g_first[gi] = (int16_t)k;
@@ -3673,27 +3683,25 @@ __global__ __launch_bounds__(TB, (PT <= 128 ? 4 : 2)) void k_segments(DevGraph g
       const int si = s0 + lane;
       if (si >= c_seg) continue;
       const int kf = S.g_first[si], kl = S.g_last[si];
-      const uint4 fr = edge_rec(g, S.t_edge[kf]);
       EAttr fa;
-      fa.seg = rec_seg(fr);
-      fa.flags = rec_flags(fr);
+      fa.seg = S.t_edge[kf];
+      fa.flags = (uint32_t)S.t_chain[kf] & 0xFFu;
       fa.gid = fa.seg >= 0 ? g.g_id[fa.seg] : 0ull;
       fa.glen = fa.seg >= 0 ? g.g_len[fa.seg] : 0.0f;
-      const uint4 lr = edge_rec(g, S.t_edge[kl]);
-      const float llen = rec_len(lr);
-      const uint32_t lfl = rec_flags(lr);
+      const uint32_t lfl = (uint32_t)S.t_chain[kl] & 0xFFu;
+      const bool lfull = ((uint32_t)S.t_chain[kl] & 0x100u) != 0u;  // t_off1[kl] == the edge's length
       otm_segment sr;
       const int32_t sg = fa.seg;
       bool sv, ev;
       sr.flags = 0u;
       if (sg >= 0) {
         sv = S.t_off0[kf] == 0.0f && (fa.flags & SegEmitter<true>::OTM_EDGE_SEG_BEGIN_D);
-        ev = S.t_off1[kl] == llen && (lfl & SegEmitter<true>::OTM_EDGE_SEG_END_D);
+        ev = lfull && (lfl & SegEmitter<true>::OTM_EDGE_SEG_END_D);
         sr.segment_id = (int64_t)fa.gid;
         sr.length = (sv && ev) ? (int32_t)floor((double)fa.glen + 0.5) : -1;
       } else {
         sv = S.t_off0[kf] == 0.0f;
-        ev = S.t_off1[kl] == llen;
+        ev = lfull;
         sr.segment_id = -1;
         sr.length = -1;
         if (fa.flags & SegEmitter<true>::OTM_EDGE_INTERNAL_D) sr.flags |= OTM_SEG_INTERNAL;

@@ -126,6 +126,9 @@ def parse():
                     help="batches in flight in the host-inclusive legs (their PCIe copies leave room for a fourth)")
     ap.add_argument("--stream-runs", type=int, default=-1,
                     help="config-5 stream leg: timed replays of the fleet per mode (-1: 3 on config 2, else 0)")
+    ap.add_argument("--stream-threads", type=int, default=0,
+                    help="config-5 stream leg: formatter and batcher host threads (0: the CPU quota, at most 16; "
+                         "16 measured 5.5-6.0M records/s against 4.7-4.8M at 8, profiles/r06/sthr/)")
     ap.add_argument("--stream-cpu-vehicles", type=int, default=200,
                     help="config-5 CPU baseline / oracle check: vehicles of the stream replayed record at a time")
     return ap.parse_args()
@@ -253,7 +256,7 @@ def fleet_stream(batch, ids):
     return msgs, t[order] * 1000, veh[order]
 
 
-def stream_leg(eng, batch, ids, graph, meili, runs, cpu_vehicles, native_vehicles=2000):
+def stream_leg(eng, batch, ids, graph, meili, runs, cpu_vehicles, native_vehicles=2000, threads=8):
     """Config 5: the fleet replayed as one time-ordered raw
     message stream through otm_batcher_process_raw (native formatter ->
     native batcher -> this GPU's engine), binary and JSON mode, timed from the
@@ -280,10 +283,10 @@ def stream_leg(eng, batch, ids, graph, meili, runs, cpu_vehicles, native_vehicle
     fmt = Formatter(STREAM_SPEC)
 
     def replay(json_path):
-        bt = Batcher(engine=eng, json_path=json_path, threads=8)
+        bt = Batcher(engine=eng, json_path=json_path, threads=threads)
         t0 = time.perf_counter()
         for m, buf, off, tsb in blocks:
-            if L.otm_batcher_process_raw(bt.h, fmt.h, m, buf.ctypes.data, off.ctypes.data, tsb.ctypes.data, 8) != 0:
+            if L.otm_batcher_process_raw(bt.h, fmt.h, m, buf.ctypes.data, off.ctypes.data, tsb.ctypes.data, threads) != 0:
                 raise RuntimeError("otm_batcher_process_raw failed")
         bt.flush()
         bt.close()
@@ -296,9 +299,9 @@ def stream_leg(eng, batch, ids, graph, meili, runs, cpu_vehicles, native_vehicle
     out = {"workload": "config-2 fleet (%d vehicles x %d points) as one time-ordered stream of %d raw json messages "
                        "(README layout, spec %r), %d per otm_batcher_process_raw call" %
                        (len(ids), n // max(len(ids), 1), n, STREAM_SPEC, chunk),
-           "includes": "otm_batcher_process_raw (native Formatter.format on 8 threads, BatchingProcessor/Batch "
+           "includes": "otm_batcher_process_raw (native Formatter.format on %d threads, BatchingProcessor/Batch "
                        "semantics, the ready keys' requests matched together on the GPU) from the first message to "
-                       "close(); runs after one warm replay, mean of the timed ones"}
+                       "close(); runs after one warm replay, mean of the timed ones" % threads}
     for mode, jp in (("binary", False), ("json", True)):
         replay(jp)  # warm: the batcher's and the engine's buffers
         rs = [replay(jp) for _ in range(runs)]
@@ -869,8 +872,13 @@ def main():
     stream_runs = args.stream_runs if args.stream_runs >= 0 else (3 if args.config == 2 else 0)
     if stream_runs > 0 and rank == 0:
         ts0 = time.perf_counter()
+        sthr = args.stream_threads
+        if sthr <= 0:
+            hi = host_info()
+            sthr = min(16, hi["usable_cpus"], int(hi["cgroup_cpu_quota"] or 16))
         stream5 = stream_leg(eng, batch, ids, graph, meili, stream_runs,
-                            args.stream_cpu_vehicles if world == 1 and not args.no_cpu_baseline else 0)
+                            args.stream_cpu_vehicles if world == 1 and not args.no_cpu_baseline else 0,
+                            threads=max(1, sthr))
         log(rank, "[bench] config-5 stream leg: %.1fs" % (time.perf_counter() - ts0))
         hist.zero_()
         speed_sum.zero_()

@@ -435,8 +435,6 @@ __global__ __launch_bounds__(TB) void k_columns(DevGraph g, DevBatch b, DevParam
         w.route_dist[p] = 0.0f;
         w.ipos[p] = -1.0f;
         w.nextc[p] = -1;
-        w.path_len[p] = 0;
-        w.path_off[p] = 0;
       }
     } else {
       for (int pl = lane; pl < n; pl += TB) {
@@ -491,8 +489,8 @@ __global__ __launch_bounds__(TB) void k_columns(DevGraph g, DevBatch b, DevParam
           w.route_dist[p] = 0.0f;
           w.ipos[p] = -1.0f;
           w.nextc[p] = -1;
-          w.path_len[p] = 0;
-          w.path_off[p] = 0;
+          // (path_len / path_off: K6 writes them for every column, and only
+          // columns' are read)
         }
         if (w.ord.tile_cnt) {  // spatial order: this column's tile, counted per wave
           const int tl = col ? tile_of(g, sLat[pl], sLon[pl]) : 0;

@@ -2765,7 +2765,9 @@ __global__ __launch_bounds__(TB, G == 8 ? OTM_VG8_WAVES : 3) void k_viterbi_g(De
           if (link) {
             cur = alive ? best + em : INFINITY;
             const int nib = alive ? bi : 15;
-            const int pair = __shfl_xor(nib, 1, G);  // (every lane of a linked group is here)
+            // the neighbour lane's nibble by a DPP quad permute [1,0,3,2] (one VALU op, no
+            // LDS-pipe shuffle); every lane of a linked group is here
+            const int pair = __builtin_amdgcn_mov_dpp(nib, 0xB1, 0xF, 0xF, false);
             if (!(j & 1)) sBp[g][pl * (G / 2) + (j >> 1)] = (uint8_t)(nib | (pair << 4));
             if (((__ballot(alive) >> gb) & (unsigned long long)gmask) != 0ull) started = true;
             else end_chain();
